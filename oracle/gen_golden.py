@@ -1,0 +1,240 @@
+"""Generate golden fixtures by importing the REFERENCE (read-only, /root/reference) — build container only.
+
+Run:  python oracle/gen_golden.py            (refuses to run if /root/reference is missing)
+
+The reference is imported with the stand-ins under oracle/stubs/ for packages absent from the image
+(cv2, torchvision, timm, efficientnet_pytorch, mmcv). Two of those stand-ins carry arithmetic that the
+reference calls on the hot path — torchvision.ops.nms and mmcv.ops.ModulatedDeformConv2d — and are restated
+from their published algorithms (see the stub docstrings); fixtures that pass through them are marked
+`unpinned_3rdparty` in tests/golden/MANIFEST.json.
+
+Outputs (tests/golden/*.npz, small): per-module input/output/grad tuples at real channel counts, whole-net
+eval outputs at 320^2 and 640^2 (bs 1), a train-mode step at 320^2 bs 2 (head outputs, loss, loss items,
+per-parameter gradient norms), NMS outputs on synthetic predictions, and the state_dict manifests.
+Weights come from oracle/recipe.py, so fixtures never store parameters.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import torch
+
+REF = Path("/root/reference")
+REPO = Path(__file__).resolve().parents[1]
+OUT = REPO / "tests" / "golden"
+sys.path.insert(0, str(REPO / "oracle"))
+from recipe import (recipe_state_dict, seeded_randn, synthetic_images,  # noqa: E402
+                    synthetic_labels, synthetic_predictions)
+
+
+def _import_reference():
+    if not REF.is_dir():
+        raise SystemExit("gen_golden: /root/reference is not present — fixtures are generated in the build container")
+    os.environ.setdefault("PYTHONDONTWRITEBYTECODE", "1")
+    sys.dont_write_bytecode = True
+    os.environ.setdefault("YOLO_CONFIG_DIR", "/tmp/adr_yolo_cfg")
+    sys.path.insert(0, str(REPO / "oracle" / "stubs"))
+    sys.path.insert(1, str(REF))
+    import ultralytics  # noqa: F401
+    from ultralytics.nn import tasks
+    from ultralytics.nn.modules import block, conv, head
+    from ultralytics.utils import loss as uloss
+    from ultralytics.utils import ops as uops
+    return tasks, block, conv, head, uloss, uops
+
+
+def _np(t):
+    return t.detach().cpu().numpy()
+
+
+def load_recipe(module):
+    sd = module.state_dict()
+    rec = recipe_state_dict([(k, v.shape) for k, v in sd.items()])
+    module.load_state_dict(rec, strict=True)
+    return rec
+
+
+def module_fixture(name, mod, specs, seed, extra=None):
+    """Run mod(*inputs) in train mode, backprop a seeded random upstream gradient, save in/out/grads."""
+    torch.manual_seed(seed)
+    load_recipe(mod)
+    mod.train()
+    specs = [sp if isinstance(sp, tuple) and isinstance(sp[0], tuple) else (tuple(sp), 11) for sp in specs]
+    inputs = [seeded_randn(*shp, seed=sd) for shp, sd in specs]
+    ins = [x.clone().requires_grad_(True) for x in inputs]
+    out = mod(ins) if getattr(mod, "_list_input", False) else mod(ins[0])
+    outs = out if isinstance(out, (list, tuple)) else [out]
+    g = torch.Generator().manual_seed(seed + 1)
+    gouts = [torch.randn(o.shape, generator=g) for o in outs]
+    torch.autograd.backward(list(outs), gouts)
+    d = {f"in{i}_shape": np.array(x.shape) for i, x in enumerate(inputs)}
+    d.update({f"in{i}_seed": np.array(sd) for i, (_, sd) in enumerate(specs)})
+    d.update({f"out{i}": _np(o) for i, o in enumerate(outs)})
+    d.update({f"gin{i}": _np(x.grad) for i, x in enumerate(ins)})
+    gn = {k: float(p.grad.norm()) for k, p in mod.named_parameters() if p.grad is not None}
+    d["param_grad_norms_keys"] = np.array(list(gn.keys()))
+    d["param_grad_norms"] = np.array(list(gn.values()), dtype=np.float64)
+    if extra:
+        d.update(extra)
+    np.savez_compressed(OUT / f"mod_{name}.npz", **d)
+    return d
+
+
+def main():
+    tasks, block, conv, head, uloss, uops = _import_reference()
+    OUT.mkdir(parents=True, exist_ok=True)
+    torch.set_num_threads(8)
+    manifest = {"generator": "oracle/gen_golden.py", "reference": "wcq99681-svg/YOLO-AD-Refine @ 2025-12-26",
+                "torch": torch.__version__, "fixtures": {}}
+
+    def note(name, what, cites, unpinned=False):
+        manifest["fixtures"][name] = {"what": what, "reference": cites, "unpinned_3rdparty": unpinned}
+
+    # ---------------- per-module fixtures (train mode, bs 2, real channel counts, small spatial) ---------------
+    m = conv.Conv(16, 32, 3, 2)
+    for mm in m.modules():
+        if isinstance(mm, torch.nn.BatchNorm2d):
+            mm.eps, mm.momentum = 1e-3, 0.03
+    module_fixture("conv_k3s2", m, [((2, 16, 24, 24), 11)], 21)
+    note("mod_conv_k3s2", "Conv(16,32,3,2) train fwd/bwd", "nn/modules/conv.py:36-54")
+
+    def bnfix(mod):
+        for mm in mod.modules():
+            if isinstance(mm, torch.nn.BatchNorm2d):
+                mm.eps, mm.momentum = 1e-3, 0.03
+        return mod
+
+    module_fixture("c3k2", bnfix(block.C3k2(32, 64, 1, False, 0.25)), [((2, 32, 20, 20), 11)], 22)
+    note("mod_c3k2", "C3k2(32,64,1,False,0.25)", "block.py:731-739,232-247,341-354")
+    module_fixture("c3k2_mlca_c3k", bnfix(block.C3k2_MLCA(128, 128, 1, True)), [((2, 128, 20, 20), 11)], 23)
+    note("mod_c3k2_mlca_c3k", "C3k2_MLCA(128,128,1,True)", "block.py:1540-1605")
+    module_fixture("c3k2_mlca", bnfix(block.C3k2_MLCA(128, 128, 1, False)), [((2, 128, 20, 20), 12)], 24)
+    note("mod_c3k2_mlca", "C3k2_MLCA(128,128,1,False) @20x20", "block.py:1540-1605")
+    module_fixture("sppf", bnfix(block.SPPF(256, 256, 5)), [((2, 256, 10, 10), 11)], 25)
+    note("mod_sppf", "SPPF(256,256,5)", "block.py:177-196")
+    module_fixture("ela", block.ELA_HSFPN(128), [((2, 128, 20, 20), 11)], 26)
+    note("mod_ela", "ELA_HSFPN(128, flag=True)", "block.py:1408-1424")
+    module_fixture("ela_noflag", block.ELA_HSFPN(128, False), [((2, 128, 20, 20), 11)], 27)
+    note("mod_ela_noflag", "ELA_HSFPN(128, flag=False)", "block.py:1408-1424")
+    module_fixture("convT", torch.nn.ConvTranspose2d(128, 128, 3, 2, 1, 1), [((2, 128, 10, 10), 11)], 28)
+    note("mod_convT", "nn.ConvTranspose2d(128,128,3,2,1,1)", "tasks.py:1005 (yaml L13/L20)")
+    fu = block.Fusion([128, 128], "bifpn")
+    fu._list_input = True
+    module_fixture("fusion", fu, [((2, 128, 10, 10), 1), ((2, 128, 10, 10), 2)], 29)
+    note("mod_fusion", "Fusion([128,128],'bifpn')", "block.py:1500-1537")
+    module_fixture("c2ptssa", bnfix(block.C2PTSSA(256, 256, 1)), [((2, 256, 20, 20), 11)], 30)
+    note("mod_c2ptssa", "C2PTSSA(256,256,1) @20x20 (MHA over 1200 tokens, EDFFN patch FFT)", "block.py:2376-2710")
+    mona_m = bnfix(block.C2TSSA_DYT_Mona_EDFFN(256, 256, 1))
+    for mm in mona_m.modules():
+        if isinstance(mm, torch.nn.Dropout):
+            mm.p = 0.0
+    module_fixture("c2tssa_mona", mona_m, [((2, 256, 20, 20), 11)], 31)
+    note("mod_c2tssa_mona", "C2TSSA_DYT_Mona_EDFFN(256,256,1) (dropout p=0)", "block.py:1624-1709, mona.py")
+    hd = head.AYHead(80, [128, 128, 128])
+    hd.stride = torch.tensor([8.0, 16.0, 32.0])
+    for mm in hd.modules():
+        if isinstance(mm, torch.nn.BatchNorm2d):
+            mm.eps, mm.momentum = 1e-3, 0.03
+    hd._list_input = True
+    module_fixture("ayhead", hd, [((2, 128, 16, 16), 3), ((2, 128, 8, 8), 4), ((2, 128, 4, 4), 5)], 32)
+    note("mod_ayhead", "AYHead(80,[128]*3) train fwd/bwd incl. DCNv2 (mmcv restated)", "head.py:1049-1252", True)
+
+    # ---------------- whole network -----------------------------------------------------------------------------
+    for tag, yaml_name in (("701", "yolo11-701-YOLO-AD-Refine.yaml"), ("697", "yolo11-697-newfpn+mona+AYHead+mlca3.yaml")):
+        model = tasks.DetectionModel(str(REF / "z-yaml" / yaml_name), verbose=False)
+        for mm in model.modules():
+            if isinstance(mm, torch.nn.Dropout):
+                mm.p = 0.0
+        sd = model.state_dict()
+        manifest[f"state_dict_{tag}"] = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()]
+        rec = load_recipe(model)
+        model.args = type("H", (), {"box": 7.5, "cls": 0.5, "dfl": 1.5})()
+        # eval outputs
+        model.eval()
+        sizes = (320, 640) if tag == "701" else (320,)
+        for S in sizes:
+            x = synthetic_images(1, S, seed=0)
+            with torch.no_grad():
+                y, outs = model(x)
+            np.savez_compressed(OUT / f"net{tag}_eval_{S}.npz", img_seed=np.array(0), y=_np(y))
+            note(f"net{tag}_eval_{S}", f"{yaml_name} eval forward bs1 {S}^2 (recipe weights)",
+                 "nn/tasks.py:141-168, head.py:1181-1204", True)
+        # train step at 320, bs 2
+        model.load_state_dict(rec, strict=True)
+        model.train()
+        x = synthetic_images(2, 320, seed=0)
+        batch = synthetic_labels(2, 80, seed=1)
+        preds = model(x)
+        crit = uloss.v8DetectionLoss(model)
+        loss, items = crit(preds, batch)
+        for p in preds:
+            p.retain_grad()
+        loss.backward()
+        gn = {k: float(p.grad.norm()) if p.grad is not None else 0.0 for k, p in model.named_parameters()}
+        bn_rm = {k: _np(v) for k, v in model.state_dict().items() if k in
+                 ("model.0.bn.running_mean", "model.0.bn.running_var", "model.33.coord_attention_reg.bn1.running_var")}
+        d = {"img_seed": np.array(0), "batch_idx": _np(batch["batch_idx"]), "cls": _np(batch["cls"]), "bboxes": _np(batch["bboxes"]),
+             "loss": _np(loss), "items": _np(items), "gn_keys": np.array(list(gn.keys())),
+             "gn": np.array(list(gn.values()), dtype=np.float64)}
+        for i, p in enumerate(preds):
+            d[f"pred{i}"] = _np(p)
+            d[f"gpred{i}_norm"] = np.array(float(p.grad.norm()))
+            d[f"gpred{i}_sum"] = np.array(float(p.grad.sum()))
+        for k, v in bn_rm.items():
+            d["post_" + k] = v
+        np.savez_compressed(OUT / f"net{tag}_train_320.npz", **d)
+        note(f"net{tag}_train_320", f"{yaml_name} train fwd + v8DetectionLoss + bwd, bs2 320^2",
+             "engine/trainer.py:383-393, utils/loss.py:419-520, utils/tal.py:39-265", True)
+
+    # ---------------- loss on fixed head outputs (independent of the network) ----------------------------------
+    hd2 = head.AYHead(80, [128, 128, 128])
+    hd2.stride = torch.tensor([8.0, 16.0, 32.0])
+
+    class _M(torch.nn.Module):
+        def __init__(s):
+            super().__init__()
+            s.model = torch.nn.ModuleList([hd2])
+            s.args = type("H", (), {"box": 7.5, "cls": 0.5, "dfl": 1.5})()
+
+    crit = uloss.v8DetectionLoss(_M())
+    for S, bs, seed in ((640, 4, 41), (320, 4, 42)):
+        g = torch.Generator().manual_seed(seed)
+        feats = [torch.randn(bs, 144, S // s, S // s, generator=g) for s in (8, 16, 32)]
+        for f in feats:
+            f[:, :64] *= 2.0
+            f.requires_grad_(True)
+        batch = synthetic_labels(bs, 80, seed=seed + 1)
+        loss, items = crit(feats, batch)
+        loss.backward()
+        d = {"batch_idx": _np(batch["batch_idx"]), "cls": _np(batch["cls"]), "bboxes": _np(batch["bboxes"]),
+             "loss": _np(loss), "items": _np(items)}
+        for i, f in enumerate(feats):
+            d[f"feat{i}_seed"] = np.array([seed, i])
+            d[f"gfeat{i}"] = _np(f.grad).astype(np.float32) if S == 320 else np.zeros(0, np.float32)
+            d[f"gfeat{i}_norm"] = np.array(float(f.grad.norm()))
+        np.savez_compressed(OUT / f"loss_{S}_bs{bs}.npz", **d)
+        note(f"loss_{S}_bs{bs}", "v8DetectionLoss on seeded randn head outputs (x2 on box channels)",
+             "utils/loss.py:419-520, tal.py:39-265, metrics.py:74-125,539-564")
+
+    # ---------------- NMS -----------------------------------------------------------------------------------------
+    pred = synthetic_predictions(2, 8400, 80, 640, seed=7)
+    for name, conf, iou, ml in (("predict", 0.25, 0.7, False), ("val", 0.001, 0.7, True), ("tight", 0.25, 0.45, False)):
+        # max_time_img raised so the reference's wall-clock cut-off (ops.py:234, 308-310) cannot truncate the
+        # fixture when it runs over the slow Python NMS stand-in
+        out = uops.non_max_suppression(pred.clone(), conf, iou, multi_label=ml, max_det=300, max_time_img=1e4)
+        d = {f"out{i}": _np(o) for i, o in enumerate(out)}
+        d["conf"], d["iou"], d["multi_label"] = np.array(conf), np.array(iou), np.array(ml)
+        np.savez_compressed(OUT / f"nms_{name}.npz", **d)
+        note(f"nms_{name}", f"non_max_suppression(conf={conf}, iou={iou}, multi_label={ml}) on seed-7 predictions",
+             "utils/ops.py:163-312 -> torchvision.ops.nms (restated)", True)
+
+    (OUT / "MANIFEST.json").write_text(json.dumps(manifest, indent=1))
+    print("wrote", len(list(OUT.glob("*.npz"))), "fixtures to", OUT)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,102 @@
+"""Seeded, reference-free recipes for parity inputs — TEST INFRASTRUCTURE ONLY.
+
+The same recipe is used (a) by oracle/gen_golden.py to load weights into the imported reference and
+(b) by tests / smoke / bench to load the identical weights into the HIP build and the CPU oracle, so golden
+fixtures never need to carry the 4.1 M parameters themselves.
+
+Weights (one generator per state_dict key, seed 1000 + key index, keys in reference order):
+  * running_mean -> 0.1 N;  running_var -> 1 + 0.1 |N|;  num_batches_tracked -> 0
+  * dfl.conv.weight -> arange(16) (frozen in the reference, block.py:63-81)
+  * named scalars/vectors (SPECIAL below) -> default + 0.1 N
+  * tensors with >= 2 dims -> N * fan_in^-1/2 (fan_in = prod(shape[1:]))
+  * '...bias' -> 0.1 N;  other 1-D 'weight' (BN / GN / LN / DyT affine) -> 1 + 0.1 N
+Images: torch.rand(B, 3, S, S) with generator seed `seed` (default 0).
+Labels ("COCO-shape"): per image n ~ Poisson(7.3) clipped [1, 93]; cls ~ U{0..nc-1};
+centres ~ U(0.05, 0.95); w, h = exp(U(ln 0.02, ln 0.6)) clipped to the image; packed as the reference's
+collate_fn (data/dataset.py:230-246): batch_idx (N,), cls (N, 1), bboxes (N, 4) normalised xywh.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+SPECIAL = {
+    "fusion_weight": 1.0, "fft": 1.0, "scale": 1.0, "scale_weights": 1.0 / 3, "stage_attention": 1.0 / 3,
+    "residual_weight1": 0.1, "residual_weight2": 0.1, "temps": 1.0, "temp": 1.0, "alpha": 0.5,
+    "gamma": 1e-6, "gammax": 1.0,
+}
+
+
+def recipe_tensor(idx: int, key: str, shape, dtype=torch.float32) -> torch.Tensor:
+    g = torch.Generator().manual_seed(1000 + idx)
+    leaf = key.rsplit(".", 1)[-1]
+    shape = tuple(shape)
+    if leaf == "num_batches_tracked":
+        return torch.zeros(shape, dtype=torch.int64)
+    n = torch.randn(shape, generator=g, dtype=torch.float32)
+    if leaf == "running_mean":
+        t = 0.1 * n
+    elif leaf == "running_var":
+        t = 1 + 0.1 * n.abs()
+    elif key.endswith("dfl.conv.weight"):
+        t = torch.arange(shape[1], dtype=torch.float32).view(shape)
+    elif leaf == "alphas":
+        t = torch.linspace(0.3, 1.0, shape[1]).view(shape) + 0.1 * n
+    elif leaf in SPECIAL:
+        t = SPECIAL[leaf] + 0.1 * n
+    elif len(shape) >= 2:
+        fan_in = max(1, math.prod(shape[1:]))
+        t = n * fan_in ** -0.5
+    elif "bias" in leaf:
+        t = 0.1 * n
+    else:
+        t = 1 + 0.1 * n
+    return t.to(dtype)
+
+
+def recipe_state_dict(keys_shapes) -> dict:
+    """keys_shapes: ordered iterable of (key, shape[, dtype]). Returns an ordered dict of tensors."""
+    out = {}
+    for idx, item in enumerate(keys_shapes):
+        key, shape = item[0], item[1]
+        out[key] = recipe_tensor(idx, key, shape)
+    return out
+
+
+def seeded_randn(*shape, seed: int = 11) -> torch.Tensor:
+    """Module-fixture inputs: torch.randn(shape) from a fresh generator seeded `seed`."""
+    return torch.randn(*shape, generator=torch.Generator().manual_seed(seed))
+
+
+def synthetic_images(bs: int, size: int, seed: int = 0) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(bs, 3, size, size, generator=g)
+
+
+def synthetic_labels(bs: int, nc: int = 80, seed: int = 1, mean_n: float = 7.3, max_n: int = 93):
+    g = torch.Generator().manual_seed(seed)
+    rates = torch.full((bs,), mean_n)
+    counts = torch.poisson(rates, generator=g).clamp(1, max_n).long()
+    bi, cl, bx = [], [], []
+    for j in range(bs):
+        n = int(counts[j])
+        c = torch.randint(0, nc, (n,), generator=g)
+        ctr = 0.05 + 0.9 * torch.rand(n, 2, generator=g)
+        lo, hi = math.log(0.02), math.log(0.6)
+        wh = torch.exp(lo + (hi - lo) * torch.rand(n, 2, generator=g))
+        wh = torch.minimum(wh, 2 * torch.minimum(ctr, 1 - ctr))  # keep the box inside the image
+        bi.append(torch.full((n,), float(j)))
+        cl.append(c.float().view(-1, 1))
+        bx.append(torch.cat((ctr, wh), 1))
+    return {"batch_idx": torch.cat(bi), "cls": torch.cat(cl), "bboxes": torch.cat(bx)}
+
+
+def synthetic_predictions(bs: int, na: int, nc: int = 80, img: int = 640, seed: int = 7):
+    """Eval-head-shaped predictions (bs, 4+nc, na) for NMS parity: xywh boxes in pixels + sigmoid scores
+    drawn so that conf 0.001 / 0.25 leave thousands / hundreds of candidates with heavy overlap."""
+    g = torch.Generator().manual_seed(seed)
+    xy = torch.rand(bs, 2, na, generator=g) * img
+    wh = torch.exp(math.log(4) + (math.log(300) - math.log(4)) * torch.rand(bs, 2, na, generator=g))
+    logits = torch.randn(bs, nc, na, generator=g) * 2.0 - 5.0
+    return torch.cat((xy, wh, torch.sigmoid(logits)), 1)
