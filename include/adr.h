@@ -1,0 +1,113 @@
+/* libadr_hip — C ABI of the MI355X-native YOLO-AD-Refine hot path (gfx950 / CDNA4).
+ *
+ * Conventions (all entry points):
+ *   - Return ADR_OK (0) on success, a non-zero adr_status otherwise; adr_last_error() (thread-local) has text.
+ *     The Python shim raises RuntimeError, as the reference's native ops do (AT_ASSERTM -> RuntimeError,
+ *     reference ultralytics/nn/modules/ops_dscn/src/cuda/dscn_cuda.cu).
+ *   - The caller owns every buffer (outputs and workspaces included); the library never allocates device
+ *     memory and keeps no mutable global state. Every launch is ordered on the `stream` argument
+ *     (a hipStream_t passed as void*), normally PyTorch's current stream.
+ *   - Activations are NHWC ("channels_last"): pixel-major, channels contiguous, with a per-pixel channel
+ *     stride and a channel offset so channel slices of concat buffers are zero-copy views.
+ *   - Weights of dense convolutions are KRSC (a PyTorch (K, C, R, S) parameter in channels_last memory).
+ *   - dtype: ADR_F32 (exact-fp32 parity mode, MFMA 16x16x4 f32) or ADR_BF16 (bf16 storage, fp32 accumulate).
+ * Each declaration names the reference interface it replaces (file:line, paths relative to the reference).
+ */
+#ifndef ADR_H_
+#define ADR_H_
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ADR_ABI_VERSION 1
+
+enum adr_status { ADR_OK = 0, ADR_ERR_BAD_ARG = 1, ADR_ERR_UNSUPPORTED = 2, ADR_ERR_LAUNCH = 3 };
+enum adr_dtype { ADR_F32 = 0, ADR_BF16 = 1 };
+enum adr_act { ADR_ACT_NONE = 0, ADR_ACT_SILU = 1, ADR_ACT_GELU = 2, ADR_ACT_RELU = 3, ADR_ACT_SIGMOID = 4,
+               ADR_ACT_HSWISH = 5 };
+
+int adr_abi_version(void);
+const char* adr_last_error(void);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Dense convolution as implicit GEMM on MFMA.
+ * Replaces: nn.Conv2d inside Conv (nn/modules/conv.py:44-50), Conv_GN (nn/modules/head.py:607-620),
+ * nn.Conv2d / nn.ConvTranspose2d yaml rows (nn/tasks.py:1005-1016), nn.Linear in CrossScaleAttentionTSSA
+ * (nn/modules/block.py:2426-2446) and the ELA Conv1d (block.py:1413). */
+typedef struct adr_conv_desc {
+  int n, h, w, c;           /* input batch, height, width, channels */
+  int x_cstride, x_coff;    /* input view: elements between pixels, first channel */
+  int k, r, s;              /* output channels, kernel height, kernel width */
+  int stride_h, stride_w, pad_h, pad_w;
+  int ho, wo;               /* output height/width (validated) */
+  int y_cstride, y_coff;    /* output view */
+  int dtype;                /* adr_dtype */
+} adr_conv_desc;
+
+/* y = conv(x, w) (+ bias[k]) (+ y if accumulate). If stats != NULL it receives per-row-tile partial
+ * [tiles][2][k] (sum, sum of squares) of the stored outputs, tiles = adr_conv2d_fwd_stat_tiles(d). */
+int adr_conv2d_fwd(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                   float* stats, int accumulate, void* stream);
+int adr_conv2d_fwd_stat_tiles(const adr_conv_desc* d);
+/* dx = conv_transpose(dy, w) (+ bias[c]) (+ dx if accumulate).  Also ConvTranspose2d forward
+ * (nn.ConvTranspose2d weight (Cin_T, Cout_T, R, S) channels_last == KRSC of the equivalent conv). */
+int adr_conv2d_dgrad(const adr_conv_desc* d, const void* dy, const void* w, const float* bias, void* dx,
+                     int accumulate, void* stream);
+/* dw[k][r][s][c] (fp32, += if accumulate) = sum over output pixels dy * im2col(x); split-K workspace. */
+size_t adr_conv2d_wgrad_workspace(const adr_conv_desc* d);
+int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const void* dy, float* dw, int accumulate,
+                     void* ws, size_t ws_bytes, void* stream);
+
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Normalisation + activation (NHWC). Replaces nn.BatchNorm2d+SiLU in Conv (nn/modules/conv.py:44-50),
+ * nn.GroupNorm(16)+SiLU in Conv_GN / TaskDecomposition / DyDCNv2 (nn/modules/head.py:607-669, 751-782),
+ * GroupNorm+Sigmoid in ELA_HSFPN (nn/modules/block.py:1413-1416), BN+GELU in ProgressiveFeatureFusion
+ * (block.py:2589-2593), BN+Hardswish in CoordAtt (head.py:684-686).
+ * Partial-statistics rows are [P][2][C] floats (sum, sum of squares — or sum g, sum g*x in backward). */
+int adr_nc_reduce_chunks(int HW, int rows_per_chunk);
+/* mode 0: stats of x;  mode 1: g = dz * act'(x*scale+shift) -> (sum g, sum g*x).  Output [N*chunks][2][C]. */
+int adr_nc_reduce(int dtype, int mode, const void* x, int xcs, int xco, const void* dz, int dcs, int dco,
+                  const float* scale, const float* shift, int per_sample, int act, int N, int HW, int C,
+                  int rows_per_chunk, float* partial, void* stream);
+int adr_bn_finalize(const float* partial, int P, int C, double count, const float* gamma, const float* beta,
+                    float* running_mean, float* running_var, float momentum, float eps, int training,
+                    float* scale, float* shift, float* mean, float* rstd, void* stream);
+int adr_bn_bwd_finalize(const float* partial, int P, int C, double count, const float* mean, const float* rstd,
+                        const float* gamma, float* dgamma, float* dbeta, float* A, float* B, float* Cc,
+                        int training, void* stream);
+int adr_gn_finalize(const float* partial, int N, int chunks, int C, int G, double count, const float* gamma,
+                    const float* beta, float eps, float* scale, float* shift, float* mean, float* rstd,
+                    void* stream);
+int adr_gn_bwd_finalize(const float* partial, int N, int chunks, int C, int G, double count, const float* mean,
+                        const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* A, float* B,
+                        float* Cc, void* stream);
+/* z = act(x * scale + shift), scale/shift per channel or (per_sample) per (image, channel). */
+int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco, const float* scale,
+                   const float* shift, int per_sample, int act, int N, int HW, int C, void* stream);
+/* dx (+)= A*g + B*x + C, g = dz * act'(x*scale+shift). */
+int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, const void* dz, int dcs, int dco, void* dx,
+                       int ocs, int oco, const float* scale, const float* shift, const float* A, const float* B,
+                       const float* Cc, int per_sample, int coef_per_sample, int act, int N, int HW, int C,
+                       int accumulate, void* stream);
+/* out[c] (+)= sum_p partial[p][which][c] */
+int adr_partial_sum(const float* partial, int P, int C, int which, float* out, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Parameter plumbing: (K, C, R*S) fp32 <-> KRSC operand (compute dtype); transpose_kc=1 reads a
+ * ConvTranspose2d weight (C_in_T=K, C_out_T=C, R, S) as the equivalent conv's KRSC weight. */
+int adr_pack_weight(int dtype, const float* src, void* dst, int K, int C, int Cp, int RS, int transpose_kc,
+                    void* stream);
+int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, int RS, int transpose_kc,
+                           int accumulate, void* stream);
+/* NCHW fp32 images (detect/train.py:57-59 preprocess output) -> NHWC compute dtype, channels padded to Cp. */
+int adr_image_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cp, void* stream);
+int adr_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long n, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ADR_H_ */

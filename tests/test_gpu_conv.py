@@ -1,0 +1,103 @@
+"""GPU parity: dense conv family (Conv-BN-SiLU, nn.Conv2d+bias, ConvTranspose2d) vs the CPU oracle."""
+import pytest
+import torch
+
+import adr_oracle as O
+from conftest import golden
+from gpu_util import TOL, assert_close, load_recipe_into, param_dict_requires_grad, to_dev
+from recipe import recipe_state_dict, seeded_randn
+
+pytestmark = pytest.mark.gpu
+
+
+def _prefixed(P, pre="m"):
+    return {pre + "." + k: v for k, v in P.items()}
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("c1,c2,k,s,hw", [(16, 32, 3, 2, 24), (32, 64, 1, 1, 20), (64, 128, 3, 1, 13),
+                                           (128, 256, 3, 2, 20), (48, 16, 1, 1, 9), (8, 16, 3, 1, 7)])
+def test_conv_bn_silu(dtype, c1, c2, k, s, hw):
+    from adrefine.nn.modules import Conv
+    m = Conv(c1, c2, k, s)
+    rec = load_recipe_into(m)
+    m = m.cuda().train()
+    x = seeded_randn(2, c1, hw, hw, seed=5)
+    xd = to_dev(x, dtype)
+    y = m(xd)
+    g = seeded_randn(*y.shape, seed=6)
+    y.backward(g.to("cuda", dtype))
+    P = param_dict_requires_grad({k2: v.clone() for k2, v in rec.items()})
+    xr = x.clone().requires_grad_(True)
+    yr = O.conv_bn_act(_prefixed(P), "m", xr, k, s)
+    yr.backward(g)
+    tol = TOL[dtype]
+    assert_close(y.float(), yr, **tol, what="y")
+    assert_close(xd.grad.float(), xr.grad, **tol, what="dx")
+    assert_close(m.conv.weight.grad, P["conv.weight"].grad, **tol, what="dw")
+    assert_close(m.bn.weight.grad, P["bn.weight"].grad, **tol, what="dgamma")
+    assert_close(m.bn.bias.grad, P["bn.bias"].grad, **tol, what="dbeta")
+    assert_close(m.bn.running_mean, P["bn.running_mean"], rtol=1e-4, atol=1e-4 if dtype == torch.float32 else 2e-2,
+                 what="running_mean")
+    assert_close(m.bn.running_var, P["bn.running_var"], rtol=1e-4, atol=1e-4 if dtype == torch.float32 else 2e-2,
+                 what="running_var")
+
+
+def test_conv_golden_fixture():
+    """Same module against the reference-generated fixture directly (fp32)."""
+    from adrefine.nn.modules import Conv
+    g = golden("mod_conv_k3s2")
+    m = Conv(16, 32, 3, 2)
+    load_recipe_into(m)
+    m = m.cuda().train()
+    x = seeded_randn(*[int(v) for v in g["in0_shape"]], seed=int(g["in0_seed"]))
+    xd = to_dev(x, torch.float32)
+    y = m(xd)
+    gen = torch.Generator().manual_seed(22)
+    gout = torch.randn(y.shape, generator=gen)
+    y.backward(gout.cuda())
+    assert_close(y, g["out0"], rtol=1e-4, atol=1e-4, what="y")
+    assert_close(xd.grad, g["gin0"], rtol=1e-4, atol=1e-4, what="dx")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv2d_bias(dtype):
+    from adrefine.nn.modules import Conv2d
+    m = Conv2d(256, 128, 1)
+    rec = load_recipe_into(m)
+    m = m.cuda()
+    x = seeded_randn(2, 256, 10, 10, seed=8)
+    xd = to_dev(x, dtype)
+    y = m(xd)
+    gy = seeded_randn(*y.shape, seed=9)
+    y.backward(gy.to("cuda", dtype))
+    P = param_dict_requires_grad({k: v.clone() for k, v in rec.items()})
+    xr = x.clone().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, P["weight"], P["bias"])
+    yr.backward(gy)
+    tol = TOL[dtype]
+    assert_close(y.float(), yr, **tol, what="y")
+    assert_close(xd.grad.float(), xr.grad, **tol, what="dx")
+    assert_close(m.weight.grad, P["weight"].grad, **tol, what="dw")
+    assert_close(m.bias.grad, P["bias"].grad, **tol, what="db")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_conv_transpose_fixture(dtype):
+    from adrefine.nn.modules import ConvTranspose2d
+    g = golden("mod_convT")
+    m = ConvTranspose2d(128, 128, 3, 2, 1, 1)
+    load_recipe_into(m)
+    m = m.cuda()
+    x = seeded_randn(*[int(v) for v in g["in0_shape"]], seed=int(g["in0_seed"]))
+    xd = to_dev(x, dtype)
+    y = m(xd)
+    gen = torch.Generator().manual_seed(29)
+    gout = torch.randn(y.shape, generator=gen)
+    y.backward(gout.to("cuda", dtype))
+    tol = TOL[dtype]
+    assert_close(y.float(), g["out0"], **tol, what="y")
+    assert_close(xd.grad.float(), g["gin0"], **tol, what="dx")
+    ref = dict(zip([str(k) for k in g["param_grad_norms_keys"]], g["param_grad_norms"]))
+    assert abs(float(m.weight.grad.norm()) - ref["weight"]) <= tol["rtol"] * ref["weight"]
+    assert abs(float(m.bias.grad.norm()) - ref["bias"]) <= tol["rtol"] * ref["bias"]

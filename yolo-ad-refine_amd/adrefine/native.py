@@ -1,0 +1,88 @@
+"""ctypes binding of libadr_hip.so. Prototypes are parsed from include/adr.h so the Python view of the ABI
+cannot drift from the header. Every call checks the status and raises RuntimeError(adr_last_error())."""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = _HERE / "lib" / "libadr_hip.so"
+HEADER = _HERE.parents[1] / "include" / "adr.h"
+if not HEADER.exists():  # installed layout: header shipped next to the library
+    HEADER = _HERE / "lib" / "adr.h"
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_int) for n in (
+        "n", "h", "w", "c", "x_cstride", "x_coff", "k", "r", "s", "stride_h", "stride_w", "pad_h", "pad_w",
+        "ho", "wo", "y_cstride", "y_coff", "dtype")]
+
+
+_STRUCTS = {"adr_conv_desc": ConvDesc}
+
+
+def _ctype(t: str):
+    t = t.replace("const", "").strip()
+    ptr = t.endswith("*")
+    base = t.rstrip("*").strip()
+    if ptr:
+        if base in _STRUCTS:
+            return ctypes.POINTER(_STRUCTS[base])
+        if base == "char":
+            return ctypes.c_char_p
+        return ctypes.c_void_p
+    return {"int": ctypes.c_int, "double": ctypes.c_double, "float": ctypes.c_float, "size_t": ctypes.c_size_t,
+            "long": ctypes.c_long, "int64_t": ctypes.c_int64, "void": None}[base]
+
+
+def parse_header(path=HEADER):
+    src = path.read_text()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"^\s*((?:const\s+)?[a-z_0-9]+\s*\**)\s*(adr_[a-z0-9_]+)\s*\(([^)]*)\)\s*;", src, re.M):
+        ret, name, args = m.group(1), m.group(2), m.group(3)
+        argt = []
+        for a in args.split(","):
+            a = a.strip()
+            if not a or a == "void":
+                continue
+            a = re.sub(r"\b[a-zA-Z_][a-zA-Z_0-9]*$", "", a).strip()  # drop parameter name
+            argt.append(_ctype(a))
+        protos[name] = (_ctype(ret), argt)
+    return protos
+
+
+class _Lib:
+    def __init__(self):
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"libadr_hip.so not built at {LIB_PATH}; run __graft_entry__.build() "
+                               "(make -C yolo-ad-refine_amd)")
+        self.lib = ctypes.CDLL(str(LIB_PATH), mode=ctypes.RTLD_GLOBAL)
+        self.protos = parse_header()
+        self.lib.adr_last_error.restype = ctypes.c_char_p
+        for name, (ret, args) in self.protos.items():
+            fn = getattr(self.lib, name)  # AttributeError == missing export
+            fn.restype = ret
+            fn.argtypes = args
+
+    def __getattr__(self, name):
+        fn = getattr(self.lib, name)
+        ret = self.protos[name][0]
+        if ret is ctypes.c_int and name not in _NONSTATUS:
+            def call(*a):
+                rc = fn(*a)
+                if rc != 0:
+                    raise RuntimeError(f"{name}: {self.lib.adr_last_error().decode()}")
+                return rc
+            setattr(self, name, call)
+            return call
+        setattr(self, name, fn)
+        return fn
+
+
+_NONSTATUS = {"adr_abi_version", "adr_conv2d_fwd_stat_tiles", "adr_nc_reduce_chunks"}
+
+lib = _Lib()
+assert lib.lib.adr_abi_version() == 1, "ABI version mismatch"

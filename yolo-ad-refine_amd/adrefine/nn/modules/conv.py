@@ -1,0 +1,77 @@
+"""Convolution modules — HIP-backed drop-ins for the reference's ultralytics/nn/modules/conv.py.
+
+Class names, constructor signatures and parameter names match the reference so yaml configs and
+state_dicts load unchanged; forward passes run libadr_hip kernels on NHWC (channels_last) activations.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from ... import kernels as K
+
+__all__ = ("Conv", "Conv2d", "ConvTranspose2d", "autopad")
+
+
+def autopad(k, p=None, d=1):
+    """Pad to 'same' output (reference conv.py:27-33)."""
+    if d > 1:
+        k = d * (k - 1) + 1 if isinstance(k, int) else [d * (x - 1) + 1 for x in k]
+    if p is None:
+        p = k // 2 if isinstance(k, int) else [x // 2 for x in k]
+    return p
+
+
+def _act_name(act):
+    if act is True:
+        return Conv.default_act
+    if act is False or act is None:
+        return "none"
+    if isinstance(act, str):
+        return act
+    name = type(act).__name__.lower()
+    return {"silu": "silu", "gelu": "gelu", "relu": "relu", "sigmoid": "sigmoid", "hardswish": "hswish",
+            "identity": "none"}[name]
+
+
+def _in_pad(x, w):
+    """The stem receives images padded to 8 channels (kernels.image_to_nhwc); pad the weight to match."""
+    return x.shape[1] if x.shape[1] != w.shape[1] and w.shape[1] < 8 else 0
+
+
+class Conv2d(nn.Conv2d):
+    """nn.Conv2d drop-in (dense, dilation 1). Used for the yaml `nn.Conv2d` rows (tasks.py:1016)."""
+
+    def forward(self, x):
+        if self.groups != 1 or self.dilation != (1, 1) or self.stride[0] != self.stride[1] or \
+                self.padding[0] != self.padding[1]:
+            raise NotImplementedError("adrefine Conv2d: grouped / dilated / anisotropic convs use DWConv kernels")
+        y, _ = K.conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], False, _in_pad(x, self.weight))
+        return y
+
+
+class ConvTranspose2d(nn.ConvTranspose2d):
+    """nn.ConvTranspose2d drop-in (yaml L13/L20: 128->128, k3 s2 p1 op1)."""
+
+    def forward(self, x, output_size=None):
+        if self.groups != 1 or self.dilation != (1, 1):
+            raise NotImplementedError("adrefine ConvTranspose2d: groups/dilation unsupported")
+        return K.conv_transpose2d(x, self.weight, self.bias, self.stride[0], self.padding[0], self.output_padding[0])
+
+
+class Conv(nn.Module):
+    """Conv2d(no bias) -> BatchNorm2d -> SiLU (reference conv.py:36-54), fused on the GPU:
+    implicit-GEMM conv with BN partial statistics in the epilogue, then normalise + activation."""
+
+    default_act = "silu"
+
+    def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
+        super().__init__()
+        self.conv = Conv2d(c1, c2, k, s, autopad(k, p, d), groups=g, dilation=d, bias=False)
+        self.bn = nn.BatchNorm2d(c2, eps=1e-3, momentum=0.03)  # initialize_weights (torch_utils.py:430-432)
+        self.act_name = _act_name(act)
+
+    def forward(self, x):
+        cv = self.conv
+        y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight))
+        return K.bn_act(y, st, self.bn, self.act_name, self.training)

@@ -1,0 +1,87 @@
+// Shared device/host helpers for libadr_hip (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+#include <stddef.h>
+#include "../../include/adr.h"
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+namespace adr {
+
+// ---- error plumbing (thread-local, C-ABI visible through adr_last_error) ----
+void set_error(const char* fmt, ...);
+int check_launch(const char* what);
+
+#define ADR_REQUIRE(cond, ...)                 \
+  do {                                         \
+    if (!(cond)) {                             \
+      ::adr::set_error(__VA_ARGS__);           \
+      return ADR_ERR_BAD_ARG;                  \
+    }                                          \
+  } while (0)
+
+// ---- scalar conversions ----
+__device__ __forceinline__ float to_f(float v) { return v; }
+__device__ __forceinline__ float to_f(__bf16 v) { return (float)v; }
+template <typename T> __device__ __forceinline__ T from_f(float v);
+template <> __device__ __forceinline__ float from_f<float>(float v) { return v; }
+template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return (__bf16)v; }
+
+// 16-byte vector of T (8 bf16 or 4 f32)
+template <typename T> struct Vec16 { static constexpr int N = 16 / sizeof(T); };
+
+__device__ __forceinline__ u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
+__device__ __forceinline__ void st16(void* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
+
+// ---- activations (shared by norm epilogues and elementwise kernels) ----
+enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_RELU = 3, ACT_SIGMOID = 4, ACT_HSWISH = 5 };
+
+__device__ __forceinline__ float act_fwd(int act, float v) {
+  switch (act) {
+    case ACT_SILU: return v / (1.f + __expf(-v));
+    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+    case ACT_RELU: return v > 0.f ? v : 0.f;
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
+    case ACT_HSWISH: return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    default: return v;
+  }
+}
+// derivative d act(v) / dv
+__device__ __forceinline__ float act_bwd(int act, float v) {
+  switch (act) {
+    case ACT_SILU: {
+      float s = 1.f / (1.f + __expf(-v));
+      return s * (1.f + v * (1.f - s));
+    }
+    case ACT_GELU: {
+      float cdf = 0.5f * (1.f + erff(v * 0.70710678118654752f));
+      float pdf = 0.39894228040143268f * __expf(-0.5f * v * v);
+      return cdf + v * pdf;
+    }
+    case ACT_RELU: return v > 0.f ? 1.f : 0.f;
+    case ACT_SIGMOID: {
+      float s = 1.f / (1.f + __expf(-v));
+      return s * (1.f - s);
+    }
+    case ACT_HSWISH: return v < -3.f ? 0.f : (v > 3.f ? 1.f : (2.f * v + 3.f) * (1.f / 6.f));
+    default: return 1.f;
+  }
+}
+
+inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
+
+// wave-level sum (64 lanes)
+__device__ __forceinline__ float wave_sum(float v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace adr

@@ -1,0 +1,501 @@
+// Implicit-GEMM convolution engine for NHWC activations on CDNA4 MFMA.
+//
+// One kernel template serves the three contractions of a dense 2-D convolution (and everything that is
+// one: 1x1 projections / nn.Linear, the ELA 7x1 Conv1d, ConvTranspose2d which is the dgrad of a conv):
+//   FWD   y [m=(n,oh,ow)][k]          = sum_{tap,c}  x[n, oh*s-p+kh, ow*s-p+kw, c] * w[k][tap][c]
+//   DGRAD dx[m=(n,ih,iw)][c]          = sum_{tap,k}  dy[n, (ih+p-kh)/s, (iw+p-kw)/s, k] * w[k][tap][c]
+//   WGRAD dw[k][tap][c] (split-K)     = sum_{m}      dy[m][k] * x[n, oh*s-p+kh, ow*s-p+kw, c]
+// Weights are KRSC (= a PyTorch (K,C,R,S) parameter stored channels_last), activations NHWC with an
+// arbitrary per-pixel channel stride + channel offset, so channel slices (C2f chunk/cat) are free views.
+//
+// Tiling: 256 threads (4 waves), BM = 128 rows x BN (16..128) cols x BK (32 bf16 / 16 f32) per K-step.
+// Operands are staged global -> registers (16-byte loads) -> LDS images [row][k] (k contiguous, rows padded
+// to 80 B so the 16-lane ds_read_b128 groups are conflict-free), then read as MFMA fragments:
+//   bf16: v_mfma_f32_16x16x32_bf16  (lane l: A[l&15][8(l>>4)+j], B[8(l>>4)+j][l&15], j<8)
+//   f32 : v_mfma_f32_16x16x4_f32    (lane l: A[l&15][l>>4],      B[l>>4][l&15])  -- exact fp32 parity mode
+// The next K-tile's global loads are issued before the current tile's MFMAs (register double buffer).
+// FWD epilogue optionally adds a bias and emits per-(row-tile, channel) partial sum / sum-of-squares of the
+// stored values for a following train-mode BatchNorm (deterministic: fixed-order reduction later).
+#include "adr_common.h"
+
+namespace adr {
+
+enum GemmMode { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+
+struct GemmArgs {
+  const void* x;    // conv input  (FWD, WGRAD)
+  const void* w;    // weights KRSC (FWD, DGRAD)
+  const void* dy;   // conv output gradient (DGRAD, WGRAD)
+  void* out;        // FWD: y ; DGRAD: dx ; WGRAD: fp32 partials [split][K][R*S*C]
+  const float* bias;
+  float* stats;     // FWD: [mtiles][2][N] partial sums (may be null)
+  int n, h, w_, c, xcs, xco;          // conv input geometry and view
+  int k, r, s, sh, sw, ph, pw, ho, wo;  // conv output channels, kernel, stride, pad, output size
+  int ycs, yco;                        // conv output (y or dy) view: channel stride / offset
+  int M, N;                            // GEMM rows / cols
+  int cblocks;                         // reduction-channel blocks per tap
+  int ktiles;                          // K-steps per block
+  int ntiles;                          // column tiles
+  int accumulate;                      // out += result
+  int red_per_split;                   // WGRAD: reduction rows per split (multiple of BK)
+  long red_total;                      // WGRAD: total reduction rows (n*ho*wo)
+};
+
+template <typename T> struct Cfg;
+template <> struct Cfg<__bf16> { static constexpr int BK = 32, VEC = 8, LDA = 40; };
+template <> struct Cfg<float> { static constexpr int BK = 16, VEC = 4, LDA = 20; };
+
+template <typename T, int BN, int MODE>
+__global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
+  constexpr int BM = 128, BK = Cfg<T>::BK, VEC = Cfg<T>::VEC, LDA = Cfg<T>::LDA;
+  constexpr int WAVES_N = (BN >= 128) ? 2 : 1;
+  constexpr int WAVES_M = 4 / WAVES_N;
+  constexpr int WROWS = BM / WAVES_M, WCOLS = BN / WAVES_N;
+  constexpr int TM = WROWS / 16, TN = WCOLS / 16;
+  constexpr int KCH = BK / VEC;  // 16-byte chunks per LDS row (=4)
+  // chunks each thread moves per K-step
+  constexpr int A_CH = (MODE == MODE_WGRAD) ? (BK * (BM / VEC)) / 256 : (BM * KCH) / 256;
+  constexpr int B_TOT = (MODE == MODE_FWD) ? BN * KCH : BK * (BN / VEC);
+  constexpr int B_CH = (B_TOT + 255) / 256;
+
+  __shared__ __attribute__((aligned(16))) T As[BM * LDA];
+  __shared__ __attribute__((aligned(16))) T Bs[BN * LDA];
+  __shared__ float red[2][WAVES_M][BN];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  int bid = blockIdx.x;
+  const int mt = bid / a.ntiles, nt = bid % a.ntiles;
+  const int split = blockIdx.y;
+  const int m0 = mt * BM;
+  const int RS = a.r * a.s;
+
+  // ---- per-thread row decode for the A operand (FWD / DGRAD: output pixels) ----
+  int a_img[A_CH], a_y[A_CH], a_x[A_CH];
+  bool a_ok[A_CH];
+  if constexpr (MODE != MODE_WGRAD) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      int row = (tid + 256 * i) / KCH;
+      long m = (long)m0 + row;
+      a_ok[i] = m < a.M;
+      int hw = (MODE == MODE_FWD) ? a.ho * a.wo : a.h * a.w_;
+      int ww = (MODE == MODE_FWD) ? a.wo : a.w_;
+      long mm = a_ok[i] ? m : 0;
+      a_img[i] = (int)(mm / hw);
+      int rem = (int)(mm % hw);
+      a_y[i] = rem / ww;
+      a_x[i] = rem % ww;
+    }
+  }
+  // column tile -> tap / channel block for WGRAD
+  int wg_tap = 0, wg_c0 = 0;
+  const int n0 = nt * BN;
+  if constexpr (MODE == MODE_WGRAD) {
+    int cbn = (a.c + BN - 1) / BN;
+    wg_tap = nt / cbn;
+    wg_c0 = (nt % cbn) * BN;
+  }
+  const long red_begin = (MODE == MODE_WGRAD) ? (long)split * a.red_per_split : 0;
+
+  u32x4 ra[A_CH], rb[B_CH > 0 ? B_CH : 1];
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+
+  auto load_tile = [&](int t) {
+    if constexpr (MODE == MODE_FWD) {
+      const int tap = t / a.cblocks, cb = t % a.cblocks;
+      const int kh = tap / a.s, kw = tap % a.s;
+      const int kc = tid % KCH;
+      const int c = cb * BK + kc * VEC;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        int ih = a_y[i] * a.sh - a.ph + kh, iw = a_x[i] * a.sw - a.pw + kw;
+        bool ok = a_ok[i] && c < a.c && ih >= 0 && ih < a.h && iw >= 0 && iw < a.w_;
+        const T* p = (const T*)a.x + ((long)(a_img[i] * a.h + ih) * a.w_ + iw) * a.xcs + a.xco + c;
+        ra[i] = ok ? ld16(p) : zero;
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        int q = tid + 256 * i;
+        int row = q / KCH, kcb = q % KCH;
+        int n = n0 + row;
+        int cc = cb * BK + kcb * VEC;
+        bool ok = (q < B_TOT) && n < a.N && cc < a.c;
+        const T* p = (const T*)a.w + ((long)n * RS + tap) * a.c + cc;
+        rb[i] = ok ? ld16(p) : zero;
+      }
+    } else if constexpr (MODE == MODE_DGRAD) {
+      const int tap = t / a.cblocks, cb = t % a.cblocks;
+      const int kh = tap / a.s, kw = tap % a.s;
+      const int kc = tid % KCH;
+      const int co = cb * BK + kc * VEC;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        int ny = a_y[i] + a.ph - kh, nx = a_x[i] + a.pw - kw;
+        bool ok = a_ok[i] && co < a.k && ny >= 0 && nx >= 0;
+        int oy = ny / a.sh, ox = nx / a.sw;
+        ok = ok && (oy * a.sh == ny) && (ox * a.sw == nx) && oy < a.ho && ox < a.wo;
+        const T* p = (const T*)a.dy + ((long)(a_img[i] * a.ho + oy) * a.wo + ox) * a.ycs + a.yco + co;
+        ra[i] = ok ? ld16(p) : zero;
+      }
+      // B image Bs[ci][co] from w[co][tap][ci]: chunk = (co_local, ci chunk)
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        int q = tid + 256 * i;
+        int col = q / (BN / VEC), cch = q % (BN / VEC);
+        int coo = cb * BK + col;
+        int ci = n0 + cch * VEC;
+        bool ok = (q < B_TOT) && coo < a.k && ci < a.c;
+        const T* p = (const T*)a.w + ((long)coo * RS + tap) * a.c + ci;
+        rb[i] = ok ? ld16(p) : zero;
+      }
+    } else {  // WGRAD
+      const long p0 = red_begin + (long)t * BK;
+      // A image As[co][p] from dy[p][co]: chunk = (p_local, co chunk)
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        int q = tid + 256 * i;
+        int pl = q / (BM / VEC), cch = q % (BM / VEC);
+        long p = p0 + pl;
+        int co = m0 + cch * VEC;
+        bool ok = p < a.red_total && p < red_begin + a.red_per_split && co < a.k;
+        const T* ptr = (const T*)a.dy + p * a.ycs + a.yco + co;
+        ra[i] = ok ? ld16(ptr) : zero;
+      }
+      const int kh = wg_tap / a.s, kw = wg_tap % a.s;
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        int q = tid + 256 * i;
+        int pl = q / (BN / VEC), cch = q % (BN / VEC);
+        long p = p0 + pl;
+        int ci = wg_c0 + cch * VEC;
+        bool ok = (q < B_TOT) && p < a.red_total && p < red_begin + a.red_per_split && ci < a.c;
+        long pp = ok ? p : 0;
+        int hw = a.ho * a.wo;
+        int img = (int)(pp / hw), rem = (int)(pp % hw);
+        int oy = rem / a.wo, ox = rem % a.wo;
+        int iy = oy * a.sh - a.ph + kh, ix = ox * a.sw - a.pw + kw;
+        ok = ok && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w_;
+        const T* ptr = (const T*)a.x + ((long)(img * a.h + iy) * a.w_ + ix) * a.xcs + a.xco + ci;
+        rb[i] = ok ? ld16(ptr) : zero;
+      }
+    }
+  };
+
+  auto store_tile = [&]() {
+    if constexpr (MODE == MODE_WGRAD) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        int q = tid + 256 * i;
+        int pl = q / (BM / VEC), cch = q % (BM / VEC);
+        const T* v = reinterpret_cast<const T*>(&ra[i]);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) As[(cch * VEC + e) * LDA + pl] = v[e];
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        int q = tid + 256 * i;
+        int row = q / KCH, kc = q % KCH;
+        st16(&As[row * LDA + kc * VEC], ra[i]);
+      }
+    }
+    if constexpr (MODE == MODE_FWD) {
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        int q = tid + 256 * i;
+        if (q < B_TOT) {
+          int row = q / KCH, kc = q % KCH;
+          st16(&Bs[row * LDA + kc * VEC], rb[i]);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        int q = tid + 256 * i;
+        if (q < B_TOT) {
+          int kl = q / (BN / VEC), cch = q % (BN / VEC);
+          const T* v = reinterpret_cast<const T*>(&rb[i]);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) Bs[(cch * VEC + e) * LDA + kl] = v[e];
+        }
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
+  const int ktiles = a.ktiles;
+  if (ktiles > 0) {
+    load_tile(0);
+    store_tile();
+    __syncthreads();
+  }
+  for (int t = 0; t < ktiles; ++t) {
+    if (t + 1 < ktiles) load_tile(t + 1);
+    if constexpr (sizeof(T) == 2) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(&As[(wr0 + i * 16 + (lane & 15)) * LDA + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[(wc0 + j * 16 + (lane & 15)) * LDA + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int sub = 0; sub < BK / 4; ++sub) {
+        float fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i] = (float)As[(wr0 + i * 16 + (lane & 15)) * LDA + 4 * sub + (lane >> 4)];
+#pragma unroll
+        for (int j = 0; j < TN; ++j) fb[j] = (float)Bs[(wc0 + j * 16 + (lane & 15)) * LDA + 4 * sub + (lane >> 4)];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+    if (t + 1 < ktiles) {
+      store_tile();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue ----
+  if constexpr (MODE == MODE_WGRAD) {
+    float* part = (float*)a.out + (long)split * a.k * ((long)RS * a.c);
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int ci = wg_c0 + wc0 + j * 16 + (lane & 15);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          int co = m0 + wr0 + i * 16 + 4 * (lane >> 4) + e;
+          if (co < a.k && ci < a.c) part[((long)co * RS + wg_tap) * a.c + ci] = acc[i][j][e];
+        }
+      }
+  } else {
+    T* out = (T*)a.out;
+    const int ocs = (MODE == MODE_FWD) ? a.ycs : a.xcs, oco = (MODE == MODE_FWD) ? a.yco : a.xco;
+    float csum[TN], csq[TN];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) { csum[j] = 0.f; csq[j] = 0.f; }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        int n = n0 + wc0 + j * 16 + (lane & 15);
+        float b = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          long m = (long)m0 + wr0 + i * 16 + 4 * (lane >> 4) + e;
+          if (m < a.M && n < a.N) {
+            T* p = out + m * ocs + oco + n;
+            float v = acc[i][j][e] + b;
+            if (a.accumulate) v += to_f(*p);
+            T tv = from_f<T>(v);
+            *p = tv;
+            float vr = to_f(tv);
+            csum[j] += vr;
+            csq[j] += vr * vr;
+          }
+        }
+      }
+    if (a.stats) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        float s = csum[j], q = csq[j];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        q += __shfl_xor(q, 16, 64);
+        q += __shfl_xor(q, 32, 64);
+        if (lane < 16) {
+          red[0][wm][wc0 + j * 16 + lane] = s;
+          red[1][wm][wc0 + j * 16 + lane] = q;
+        }
+      }
+      __syncthreads();
+      if (tid < BN) {
+        int n = n0 + tid;
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int w = 0; w < WAVES_M; ++w) { s += red[0][w][tid]; q += red[1][w][tid]; }
+        if (n < a.N) {
+          a.stats[(long)mt * 2 * a.N + n] = s;
+          a.stats[(long)mt * 2 * a.N + a.N + n] = q;
+        }
+      }
+    }
+  }
+}
+
+// deterministic reduction of WGRAD split partials: dw[i] (+)= sum_s part[s][i]
+__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw, long n, int splits,
+                                    int accumulate) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += part[(long)k * n + i];
+  dw[i] = accumulate ? dw[i] + s : s;
+}
+
+// ------------------------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------------------------
+
+static int pick_bn(int n) {
+  if (n <= 16) return 16;
+  if (n <= 32) return 32;
+  if (n <= 64) return 64;
+  return 128;
+}
+
+template <typename T, int MODE>
+static void launch_bn(int bn, dim3 grid, const GemmArgs& g, hipStream_t st) {
+  switch (bn) {
+    case 16: hipLaunchKernelGGL((gemm_kernel<T, 16, MODE>), grid, dim3(256), 0, st, g); break;
+    case 32: hipLaunchKernelGGL((gemm_kernel<T, 32, MODE>), grid, dim3(256), 0, st, g); break;
+    case 64: hipLaunchKernelGGL((gemm_kernel<T, 64, MODE>), grid, dim3(256), 0, st, g); break;
+    default: hipLaunchKernelGGL((gemm_kernel<T, 128, MODE>), grid, dim3(256), 0, st, g); break;
+  }
+}
+
+static int fill_common(const adr_conv_desc* d, GemmArgs& g) {
+  ADR_REQUIRE(d && d->n > 0 && d->h > 0 && d->w > 0 && d->c > 0 && d->k > 0 && d->r > 0 && d->s > 0,
+              "conv: bad geometry");
+  ADR_REQUIRE(d->dtype == ADR_F32 || d->dtype == ADR_BF16, "conv: unsupported dtype %d", d->dtype);
+  int vec = d->dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(d->c % vec == 0 && d->k % vec == 0, "conv: C (%d) and K (%d) must be multiples of %d", d->c, d->k, vec);
+  ADR_REQUIRE(d->x_cstride % vec == 0 && d->x_coff % vec == 0 && d->y_cstride % vec == 0 && d->y_coff % vec == 0,
+              "conv: channel views must be 16-byte aligned");
+  ADR_REQUIRE(d->x_cstride >= d->x_coff + d->c && d->y_cstride >= d->y_coff + d->k, "conv: view exceeds stride");
+  int ho = (d->h + 2 * d->pad_h - d->r) / d->stride_h + 1;
+  int wo = (d->w + 2 * d->pad_w - d->s) / d->stride_w + 1;
+  ADR_REQUIRE(ho == d->ho && wo == d->wo, "conv: output size mismatch (%dx%d vs %dx%d)", d->ho, d->wo, ho, wo);
+  g.n = d->n; g.h = d->h; g.w_ = d->w; g.c = d->c; g.xcs = d->x_cstride; g.xco = d->x_coff;
+  g.k = d->k; g.r = d->r; g.s = d->s; g.sh = d->stride_h; g.sw = d->stride_w; g.ph = d->pad_h; g.pw = d->pad_w;
+  g.ho = d->ho; g.wo = d->wo; g.ycs = d->y_cstride; g.yco = d->y_coff;
+  return ADR_OK;
+}
+
+static int bk_of(int dtype) { return dtype == ADR_BF16 ? 32 : 16; }
+
+}  // namespace adr
+
+using namespace adr;
+
+extern "C" int adr_conv2d_fwd(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                              float* stats, int accumulate, void* stream) {
+  GemmArgs g{};
+  int rc = fill_common(d, g);
+  if (rc) return rc;
+  g.x = x; g.w = w; g.out = y; g.bias = bias; g.stats = stats; g.accumulate = accumulate;
+  g.M = d->n * d->ho * d->wo;
+  g.N = d->k;
+  int BK = bk_of(d->dtype);
+  g.cblocks = cdiv(d->c, BK);
+  g.ktiles = d->r * d->s * g.cblocks;
+  int bn = pick_bn(g.N);
+  g.ntiles = cdiv(g.N, bn);
+  int mtiles = cdiv(g.M, 128);
+  dim3 grid(mtiles * g.ntiles, 1);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == ADR_BF16) launch_bn<__bf16, MODE_FWD>(bn, grid, g, st);
+  else launch_bn<float, MODE_FWD>(bn, grid, g, st);
+  return check_launch("adr_conv2d_fwd");
+}
+
+extern "C" int adr_conv2d_fwd_stat_tiles(const adr_conv_desc* d) { return cdiv((long)d->n * d->ho * d->wo, 128); }
+
+extern "C" int adr_conv2d_dgrad(const adr_conv_desc* d, const void* dy, const void* w, const float* bias, void* dx,
+                                int accumulate, void* stream) {
+  GemmArgs g{};
+  int rc = fill_common(d, g);
+  if (rc) return rc;
+  // reads dy through the y view (y_cstride, y_coff); writes dx through the x view (x_cstride, x_coff)
+  g.dy = dy; g.w = w; g.out = dx; g.bias = bias; g.accumulate = accumulate;
+  g.M = d->n * d->h * d->w;
+  g.N = d->c;
+  int BK = bk_of(d->dtype);
+  g.cblocks = cdiv(d->k, BK);
+  g.ktiles = d->r * d->s * g.cblocks;
+  int bn = pick_bn(g.N);
+  g.ntiles = cdiv(g.N, bn);
+  dim3 grid(cdiv(g.M, 128) * g.ntiles, 1);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->dtype == ADR_BF16) launch_bn<__bf16, MODE_DGRAD>(bn, grid, g, st);
+  else launch_bn<float, MODE_DGRAD>(bn, grid, g, st);
+  return check_launch("adr_conv2d_dgrad");
+}
+
+static int wgrad_splits(const adr_conv_desc* d, int* bn_out, int* ntiles_out) {
+  long red = (long)d->n * d->ho * d->wo;
+  int BK = bk_of(d->dtype);
+  int bn = pick_bn(d->c);
+  int ntiles = d->r * d->s * cdiv(d->c, bn);
+  int mtiles = cdiv(d->k, 128);
+  long tiles = (long)ntiles * mtiles;
+  long want = (2048 + tiles - 1) / tiles;
+  long maxs = (red + BK * 8 - 1) / (BK * 8);  // at least 8 K-steps per split
+  long s = want < maxs ? want : maxs;
+  if (s < 1) s = 1;
+  if (s > 65535) s = 65535;
+  *bn_out = bn;
+  *ntiles_out = ntiles;
+  return (int)s;
+}
+
+extern "C" size_t adr_conv2d_wgrad_workspace(const adr_conv_desc* d) {
+  int bn, nt;
+  int splits = wgrad_splits(d, &bn, &nt);
+  return (size_t)splits * d->k * d->r * d->s * d->c * sizeof(float);
+}
+
+extern "C" int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const void* dy, float* dw, int accumulate,
+                                void* ws, size_t ws_bytes, void* stream) {
+  GemmArgs g{};
+  int rc = fill_common(d, g);
+  if (rc) return rc;
+  int bn, ntiles;
+  int splits = wgrad_splits(d, &bn, &ntiles);
+  size_t need = (size_t)splits * d->k * d->r * d->s * d->c * sizeof(float);
+  ADR_REQUIRE(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+  int BK = bk_of(d->dtype);
+  long red = (long)d->n * d->ho * d->wo;
+  long per = (red + splits - 1) / splits;
+  per = (per + BK - 1) / BK * BK;
+  g.x = x; g.dy = dy; g.out = ws;
+  g.M = d->k; g.N = d->r * d->s * d->c;
+  g.red_total = red;
+  g.red_per_split = (int)per;
+  g.ktiles = (int)(per / BK);
+  g.ntiles = ntiles;
+  dim3 grid(cdiv(d->k, 128) * ntiles, splits);
+  hipStream_t st = (hipStream_t)stream;
+  if (splits > 1 || accumulate) {
+    // every (co, tap, ci) inside [K x RSC] is written by exactly one block per split
+    if (d->dtype == ADR_BF16) launch_bn<__bf16, MODE_WGRAD>(bn, grid, g, st);
+    else launch_bn<float, MODE_WGRAD>(bn, grid, g, st);
+    rc = check_launch("adr_conv2d_wgrad");
+    if (rc) return rc;
+    long n = (long)d->k * d->r * d->s * d->c;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, (const float*)ws, dw, n, splits,
+                       accumulate);
+  } else {
+    g.out = dw;
+    if (d->dtype == ADR_BF16) launch_bn<__bf16, MODE_WGRAD>(bn, grid, g, st);
+    else launch_bn<float, MODE_WGRAD>(bn, grid, g, st);
+  }
+  return check_launch("adr_conv2d_wgrad");
+}

@@ -1,0 +1,471 @@
+// Normalisation (BatchNorm2d train/eval, GroupNorm) + fused activation, forward and backward, NHWC.
+//
+// Forward:  partial stats (from the conv epilogue or adr_nc_reduce) -> *_finalize -> scale/shift per channel
+//           (BN) or per (image, channel) (GN) -> adr_affine_act:  z = act(x * scale + shift).
+// Backward: adr_nc_reduce(MODE_BWD) gives per-(image, channel) partials of g = dz * act'(x*scale+shift) and of
+//           g*x; *_bwd_finalize turns them into dgamma/dbeta and per-(image, channel) coefficients (A, B, C)
+//           with dx = A*g + B*x + C, applied by adr_affine_act_bwd (g recomputed on the fly).
+// All cross-block reductions are fixed-order (no atomics), so results are deterministic run to run.
+// Reference semantics: nn.BatchNorm2d with eps 1e-3 / momentum 0.03 (utils/torch_utils.py:426-436),
+// unbiased running_var update; GroupNorm(16, C) eps 1e-5 (nn/modules/head.py:613).
+#include "adr_common.h"
+
+namespace adr {
+
+enum RedMode { RED_STATS = 0, RED_BWD = 1, RED_SUM = 2 };
+
+// partial[(n * chunks + chunk)][2][C]
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) nc_reduce_kernel(const T* __restrict__ x, int xcs, int xco,
+                                                        const T* __restrict__ dz, int dcs, int dco,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, int per_sample, int act,
+                                                        int HW, int C, int rows_per_chunk, int chunks,
+                                                        float* __restrict__ partial) {
+  constexpr int VEC = 16 / sizeof(T);
+  __shared__ float sh[2][256 * VEC];
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int G = C / VEC;
+  const int rpp = 256 / G;  // rows per pass
+  const int t = threadIdx.x;
+  const int cg = t % G, r0 = t / G;
+  float s1[VEC], s2[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const int rbeg = chunk * rows_per_chunk;
+  const int rend = min(HW, rbeg + rows_per_chunk);
+  const int c0 = cg * VEC;
+  float sc[VEC], sf[VEC];
+  if (MODE == RED_BWD) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      int ci = per_sample ? n * C + c0 + e : c0 + e;
+      sc[e] = scale[ci];
+      sf[e] = shift[ci];
+    }
+  }
+  if (r0 < rpp) {
+    for (int r = rbeg + r0; r < rend; r += rpp) {
+      long pix = (long)n * HW + r;
+      u32x4 xv = ld16(x + pix * xcs + xco + c0);
+      const T* xe = reinterpret_cast<const T*>(&xv);
+      if (MODE == RED_BWD) {
+        u32x4 dv = ld16(dz + pix * dcs + dco + c0);
+        const T* de = reinterpret_cast<const T*>(&dv);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          float xf = to_f(xe[e]);
+          float g = to_f(de[e]) * act_bwd(act, xf * sc[e] + sf[e]);
+          s1[e] += g;
+          s2[e] += g * xf;
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          float xf = to_f(xe[e]);
+          s1[e] += xf;
+          s2[e] += xf * xf;
+        }
+      }
+    }
+  }
+  // combine rows: threads with the same cg (t = cg + G * r0)
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    sh[0][t * VEC + e] = s1[e];
+    sh[1][t * VEC + e] = s2[e];
+  }
+  __syncthreads();
+  float* out = partial + ((long)n * chunks + chunk) * 2 * C;
+  for (int c = t; c < C; c += 256) {
+    int g = c / VEC, e = c % VEC;
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rpp; ++r) {
+      a += sh[0][(g + r * G) * VEC + e];
+      b += sh[1][(g + r * G) * VEC + e];
+    }
+    out[c] = a;
+    out[C + c] = b;
+  }
+}
+
+// block per channel: deterministic tree over P partial rows in double
+__device__ __forceinline__ void block_sum2(double& a, double& b) {
+  __shared__ double sa[256], sb[256];
+  int t = threadIdx.x;
+  sa[t] = a;
+  sb[t] = b;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (t < o) {
+      sa[t] += sa[t + o];
+      sb[t] += sb[t + o];
+    }
+    __syncthreads();
+  }
+  a = sa[0];
+  b = sb[0];
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ partial, int P, int C, double count,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* running_mean,
+                                                          float* running_var, float momentum, float eps,
+                                                          int training, float* scale, float* shift, float* mean_out,
+                                                          float* rstd_out) {
+  int c = blockIdx.x;
+  double mean, var;
+  if (training) {
+    double a = 0.0, b = 0.0;
+    for (int p = threadIdx.x; p < P; p += 256) {
+      a += partial[(long)p * 2 * C + c];
+      b += partial[(long)p * 2 * C + C + c];
+    }
+    block_sum2(a, b);
+    mean = a / count;
+    var = b / count - mean * mean;
+    if (var < 0) var = 0;
+  } else {
+    mean = running_mean[c];
+    var = running_var[c];
+  }
+  if (threadIdx.x == 0) {
+    double rstd = 1.0 / sqrt(var + (double)eps);
+    double g = gamma ? gamma[c] : 1.0, bb = beta ? beta[c] : 0.0;
+    scale[c] = (float)(g * rstd);
+    shift[c] = (float)(bb - mean * g * rstd);
+    if (mean_out) mean_out[c] = (float)mean;
+    if (rstd_out) rstd_out[c] = (float)rstd;
+    if (training && running_mean) {
+      double unb = count > 1 ? var * count / (count - 1) : var;
+      running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+      running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+    }
+  }
+}
+
+// dgamma/dbeta and coefficients for BN backward. partial holds (sum g, sum g*x) per row.
+__global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __restrict__ partial, int P, int C,
+                                                              double count, const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd,
+                                                              const float* __restrict__ gamma, float* dgamma,
+                                                              float* dbeta, float* A, float* B, float* Cc,
+                                                              int training) {
+  int c = blockIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int p = threadIdx.x; p < P; p += 256) {
+    a += partial[(long)p * 2 * C + c];
+    b += partial[(long)p * 2 * C + C + c];
+  }
+  block_sum2(a, b);
+  if (threadIdx.x == 0) {
+    double mu = mean[c], rs = rstd[c], g = gamma ? gamma[c] : 1.0;
+    double sg = a;                   // sum g
+    double sgx = (b - mu * a) * rs;  // sum g * xhat
+    if (dgamma) dgamma[c] = (float)sgx;
+    if (dbeta) dbeta[c] = (float)sg;
+    double Ak = g * rs;
+    if (training) {
+      double Bk = -Ak * rs * sgx / count;
+      double Ck = -Ak * sg / count - Bk * mu;
+      A[c] = (float)Ak;
+      B[c] = (float)Bk;
+      Cc[c] = (float)Ck;
+    } else {
+      A[c] = (float)Ak;
+      B[c] = 0.f;
+      Cc[c] = 0.f;
+    }
+  }
+}
+
+// GroupNorm forward finalize: block per image; partial [n][chunks][2][C]
+__global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restrict__ partial, int chunks, int C, int G,
+                                                          double count, const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float eps, float* scale,
+                                                          float* shift, float* mean_out, float* rstd_out) {
+  int n = blockIdx.x;
+  __shared__ double gm[64], gr[64];
+  int cpg = C / G;
+  for (int g = threadIdx.x; g < G; g += 256) {
+    double a = 0.0, b = 0.0;
+    for (int ch = 0; ch < chunks; ++ch) {
+      const float* p = partial + ((long)n * chunks + ch) * 2 * C;
+      for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+        a += p[c];
+        b += p[C + c];
+      }
+    }
+    double mu = a / count, var = b / count - mu * mu;
+    if (var < 0) var = 0;
+    gm[g] = mu;
+    gr[g] = 1.0 / sqrt(var + (double)eps);
+    mean_out[n * G + g] = (float)mu;
+    rstd_out[n * G + g] = (float)gr[g];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    int g = c / cpg;
+    double gg = gamma ? gamma[c] : 1.0, bb = beta ? beta[c] : 0.0;
+    scale[n * C + c] = (float)(gg * gr[g]);
+    shift[n * C + c] = (float)(bb - gm[g] * gg * gr[g]);
+  }
+}
+
+// GroupNorm backward finalize: one block; loops over images for dgamma/dbeta.
+__global__ void __launch_bounds__(256) gn_bwd_finalize_kernel(const float* __restrict__ partial, int N, int chunks,
+                                                              int C, int G, double count,
+                                                              const float* __restrict__ mean,
+                                                              const float* __restrict__ rstd,
+                                                              const float* __restrict__ gamma, float* dgamma,
+                                                              float* dbeta, float* A, float* B, float* Cc) {
+  int cpg = C / G;
+  __shared__ double s1[64], s2[64];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    if (dgamma) dgamma[c] = 0.f;
+    if (dbeta) dbeta[c] = 0.f;
+  }
+  __syncthreads();
+  for (int n = 0; n < N; ++n) {
+    // per-channel sums for image n
+    for (int g = threadIdx.x; g < G; g += 256) {
+      double mu = mean[n * G + g], rs = rstd[n * G + g];
+      double S1 = 0.0, S2 = 0.0;
+      for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+        double a = 0.0, b = 0.0;
+        for (int ch = 0; ch < chunks; ++ch) {
+          const float* p = partial + ((long)n * chunks + ch) * 2 * C;
+          a += p[c];
+          b += p[C + c];
+        }
+        double gm = gamma ? gamma[c] : 1.0;
+        double sgx = (b - mu * a) * rs;  // sum g * xhat for channel c
+        if (dgamma) dgamma[c] += (float)sgx;
+        if (dbeta) dbeta[c] += (float)a;
+        S1 += gm * a;    // sum dxhat
+        S2 += gm * sgx;  // sum dxhat * xhat
+      }
+      s1[g] = S1;
+      s2[g] = S2;
+    }
+    __syncthreads();
+    for (int c = threadIdx.x; c < C; c += 256) {
+      int g = c / cpg;
+      double mu = mean[n * G + g], rs = rstd[n * G + g];
+      double gm = gamma ? gamma[c] : 1.0;
+      double Ak = rs * gm;
+      double Bk = -rs * rs * s2[g] / count;
+      double Ck = -rs * s1[g] / count - Bk * mu;
+      A[n * C + c] = (float)Ak;
+      B[n * C + c] = (float)Bk;
+      Cc[n * C + c] = (float)Ck;
+    }
+    __syncthreads();
+  }
+}
+
+// z = act(x * scale + shift) ; NHWC; scale/shift per channel or per (n, channel)
+template <typename T>
+__global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x, int xcs, int xco, T* __restrict__ z,
+                                                         int zcs, int zco, const float* __restrict__ scale,
+                                                         const float* __restrict__ shift, int per_sample, int act,
+                                                         long npix, int HW, int C) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int G = C / VEC;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = npix * G;
+  for (; i < total; i += (long)gridDim.x * blockDim.x) {
+    long pix = i / G;
+    int c0 = (int)(i % G) * VEC;
+    int n = (int)(pix / HW);
+    u32x4 v = ld16(x + pix * xcs + xco + c0);
+    const T* e = reinterpret_cast<const T*>(&v);
+    u32x4 o;
+    T* oe = reinterpret_cast<T*>(&o);
+    int base = per_sample ? n * C + c0 : c0;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(act_fwd(act, to_f(e[k]) * scale[base + k] + shift[base + k]));
+    st16(z + pix * zcs + zco + c0, o);
+  }
+}
+
+// dx = A*g + B*x + C with g = dz * act'(x*scale+shift) ; optional accumulate into dx
+template <typename T>
+__global__ void __launch_bounds__(256) affine_act_bwd_kernel(const T* __restrict__ x, int xcs, int xco,
+                                                             const T* __restrict__ dz, int dcs, int dco,
+                                                             T* __restrict__ dx, int ocs, int oco,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ A,
+                                                             const float* __restrict__ B,
+                                                             const float* __restrict__ Cc, int per_sample,
+                                                             int coef_per_sample, int act, long npix, int HW, int C,
+                                                             int accumulate) {
+  constexpr int VEC = 16 / sizeof(T);
+  const int G = C / VEC;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = npix * G;
+  for (; i < total; i += (long)gridDim.x * blockDim.x) {
+    long pix = i / G;
+    int c0 = (int)(i % G) * VEC;
+    int n = (int)(pix / HW);
+    u32x4 xv = ld16(x + pix * xcs + xco + c0);
+    u32x4 dv = ld16(dz + pix * dcs + dco + c0);
+    const T* xe = reinterpret_cast<const T*>(&xv);
+    const T* de = reinterpret_cast<const T*>(&dv);
+    u32x4 o;
+    T* oe = reinterpret_cast<T*>(&o);
+    u32x4 prev;
+    if (accumulate) prev = ld16(dx + pix * ocs + oco + c0);
+    const T* pe = reinterpret_cast<const T*>(&prev);
+    int sb = per_sample ? n * C + c0 : c0;
+    int cb = coef_per_sample ? n * C + c0 : c0;
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      float xf = to_f(xe[k]);
+      float g = to_f(de[k]) * act_bwd(act, xf * scale[sb + k] + shift[sb + k]);
+      float r = A[cb + k] * g + B[cb + k] * xf + Cc[cb + k];
+      if (accumulate) r += to_f(pe[k]);
+      oe[k] = from_f<T>(r);
+    }
+    st16(dx + pix * ocs + oco + c0, o);
+  }
+}
+
+// out[c] (+)= sum_p partial[p][which][c]
+__global__ void __launch_bounds__(256) partial_sum_kernel(const float* __restrict__ partial, int P, int C, int which,
+                                                          float* out, int accumulate) {
+  int c = blockIdx.x;
+  double a = 0.0, b = 0.0;
+  for (int p = threadIdx.x; p < P; p += 256) a += partial[(long)p * 2 * C + which * C + c];
+  block_sum2(a, b);
+  if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)a : (float)a;
+}
+
+static int grid_for(long work) {
+  long b = (work + 255) / 256;
+  if (b > 65536) b = 65536;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace adr
+
+using namespace adr;
+
+extern "C" int adr_nc_reduce_chunks(int HW, int rows_per_chunk) { return cdiv(HW, rows_per_chunk); }
+
+extern "C" int adr_nc_reduce(int dtype, int mode, const void* x, int xcs, int xco, const void* dz, int dcs, int dco,
+                             const float* scale, const float* shift, int per_sample, int act, int N, int HW, int C,
+                             int rows_per_chunk, float* partial, void* stream) {
+  int vec = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % vec == 0 && C / vec <= 256, "nc_reduce: C=%d unsupported", C);
+  ADR_REQUIRE(xcs % vec == 0 && xco % vec == 0 && dcs % vec == 0 && dco % vec == 0, "nc_reduce: misaligned view");
+  ADR_REQUIRE(mode == RED_STATS || mode == RED_BWD || mode == RED_SUM, "nc_reduce: mode");
+  int chunks = cdiv(HW, rows_per_chunk);
+  dim3 grid(chunks, N);
+  hipStream_t st = (hipStream_t)stream;
+  if (mode == RED_BWD) {
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL((nc_reduce_kernel<__bf16, RED_BWD>), grid, dim3(256), 0, st, (const __bf16*)x, xcs, xco,
+                         (const __bf16*)dz, dcs, dco, scale, shift, per_sample, act, HW, C, rows_per_chunk, chunks,
+                         partial);
+    else
+      hipLaunchKernelGGL((nc_reduce_kernel<float, RED_BWD>), grid, dim3(256), 0, st, (const float*)x, xcs, xco,
+                         (const float*)dz, dcs, dco, scale, shift, per_sample, act, HW, C, rows_per_chunk, chunks,
+                         partial);
+  } else {
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL((nc_reduce_kernel<__bf16, RED_STATS>), grid, dim3(256), 0, st, (const __bf16*)x, xcs, xco,
+                         (const __bf16*)nullptr, 0, 0, scale, shift, per_sample, act, HW, C, rows_per_chunk, chunks,
+                         partial);
+    else
+      hipLaunchKernelGGL((nc_reduce_kernel<float, RED_STATS>), grid, dim3(256), 0, st, (const float*)x, xcs, xco,
+                         (const float*)nullptr, 0, 0, scale, shift, per_sample, act, HW, C, rows_per_chunk, chunks,
+                         partial);
+  }
+  return check_launch("adr_nc_reduce");
+}
+
+extern "C" int adr_bn_finalize(const float* partial, int P, int C, double count, const float* gamma, const float* beta,
+                               float* running_mean, float* running_var, float momentum, float eps, int training,
+                               float* scale, float* shift, float* mean, float* rstd, void* stream) {
+  ADR_REQUIRE(C > 0, "bn_finalize: C");
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, P, C, count, gamma, beta,
+                     running_mean, running_var, momentum, eps, training, scale, shift, mean, rstd);
+  return check_launch("adr_bn_finalize");
+}
+
+extern "C" int adr_bn_bwd_finalize(const float* partial, int P, int C, double count, const float* mean,
+                                   const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* A,
+                                   float* B, float* Cc, int training, void* stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, P, C, count, mean,
+                     rstd, gamma, dgamma, dbeta, A, B, Cc, training);
+  return check_launch("adr_bn_bwd_finalize");
+}
+
+extern "C" int adr_gn_finalize(const float* partial, int N, int chunks, int C, int G, double count, const float* gamma,
+                               const float* beta, float eps, float* scale, float* shift, float* mean, float* rstd,
+                               void* stream) {
+  ADR_REQUIRE(G <= 64 && C % G == 0, "gn_finalize: G=%d C=%d", G, C);
+  hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, partial, chunks, C, G, count,
+                     gamma, beta, eps, scale, shift, mean, rstd);
+  return check_launch("adr_gn_finalize");
+}
+
+extern "C" int adr_gn_bwd_finalize(const float* partial, int N, int chunks, int C, int G, double count,
+                                   const float* mean, const float* rstd, const float* gamma, float* dgamma,
+                                   float* dbeta, float* A, float* B, float* Cc, void* stream) {
+  ADR_REQUIRE(G <= 64 && C % G == 0, "gn_bwd_finalize: G=%d C=%d", G, C);
+  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partial, N, chunks, C, G,
+                     count, mean, rstd, gamma, dgamma, dbeta, A, B, Cc);
+  return check_launch("adr_gn_bwd_finalize");
+}
+
+extern "C" int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco,
+                              const float* scale, const float* shift, int per_sample, int act, int N, int HW, int C,
+                              void* stream) {
+  int vec = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % vec == 0 && xcs % vec == 0 && xco % vec == 0 && zcs % vec == 0 && zco % vec == 0,
+              "affine_act: misaligned view (C=%d)", C);
+  long npix = (long)N * HW;
+  int grid = grid_for(npix * (C / vec));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(affine_act_kernel<__bf16>, dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, xco,
+                       (__bf16*)z, zcs, zco, scale, shift, per_sample, act, npix, HW, C);
+  else
+    hipLaunchKernelGGL(affine_act_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, xcs, xco, (float*)z,
+                       zcs, zco, scale, shift, per_sample, act, npix, HW, C);
+  return check_launch("adr_affine_act");
+}
+
+extern "C" int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, const void* dz, int dcs, int dco,
+                                  void* dx, int ocs, int oco, const float* scale, const float* shift, const float* A,
+                                  const float* B, const float* Cc, int per_sample, int coef_per_sample, int act,
+                                  int N, int HW, int C, int accumulate, void* stream) {
+  int vec = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % vec == 0 && xcs % vec == 0 && xco % vec == 0 && dcs % vec == 0 && dco % vec == 0 &&
+                  ocs % vec == 0 && oco % vec == 0,
+              "affine_act_bwd: misaligned view");
+  long npix = (long)N * HW;
+  int grid = grid_for(npix * (C / vec));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(affine_act_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, xco,
+                       (const __bf16*)dz, dcs, dco, (__bf16*)dx, ocs, oco, scale, shift, A, B, Cc, per_sample,
+                       coef_per_sample, act, npix, HW, C, accumulate);
+  else
+    hipLaunchKernelGGL(affine_act_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, xcs, xco,
+                       (const float*)dz, dcs, dco, (float*)dx, ocs, oco, scale, shift, A, B, Cc, per_sample,
+                       coef_per_sample, act, npix, HW, C, accumulate);
+  return check_launch("adr_affine_act_bwd");
+}
+
+extern "C" int adr_partial_sum(const float* partial, int P, int C, int which, float* out, int accumulate,
+                               void* stream) {
+  hipLaunchKernelGGL(partial_sum_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, P, C, which, out,
+                     accumulate);
+  return check_launch("adr_partial_sum");
+}

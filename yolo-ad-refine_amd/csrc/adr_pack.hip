@@ -1,0 +1,117 @@
+// Parameter plumbing kernels: pack fp32 PyTorch-layout weights into the kernels' KRSC operand layout
+// (with the cast to the compute dtype), and unpack KRSC fp32 weight gradients back to (K, C, R, S).
+#include "adr_common.h"
+
+namespace adr {
+
+template <typename T>
+__global__ void pack_weight_kernel(const float* __restrict__ src, T* __restrict__ dst, int K, int C, int Cp, int RS,
+                                   int transpose_kc) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long n = (long)K * Cp * RS;
+  if (i >= n) return;
+  // destination index i = (k * RS + t) * Cp + c ; channels c >= C are zero padding
+  int c = (int)(i % Cp);
+  long r = i / Cp;
+  int t = (int)(r % RS);
+  int k = (int)(r / RS);
+  // source (K, C, RS) or, for ConvTranspose2d weights viewed as the equivalent conv, (C, K, RS)
+  if (c >= C) {
+    dst[i] = from_f<T>(0.f);
+    return;
+  }
+  long s = transpose_kc ? ((long)c * K + k) * RS + t : ((long)k * C + c) * RS + t;
+  dst[i] = from_f<T>(src[s]);
+}
+
+__global__ void unpack_weight_grad_kernel(const float* __restrict__ src, float* __restrict__ dst, int K, int C,
+                                          int Cp, int RS, int transpose_kc, int accumulate) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long n = (long)K * Cp * RS;
+  if (i >= n) return;
+  int c = (int)(i % Cp);
+  long r = i / Cp;
+  int t = (int)(r % RS);
+  int k = (int)(r / RS);
+  if (c >= C) return;
+  long s = transpose_kc ? ((long)c * K + k) * RS + t : ((long)k * C + c) * RS + t;
+  dst[s] = accumulate ? dst[s] + src[i] : src[i];
+}
+
+template <typename A, typename B>
+__global__ void cast_kernel(const A* __restrict__ src, B* __restrict__ dst, long n) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = from_f<B>(to_f(src[i]));
+}
+
+}  // namespace adr
+
+using namespace adr;
+
+extern "C" int adr_pack_weight(int dtype, const float* src, void* dst, int K, int C, int Cp, int RS,
+                               int transpose_kc, void* stream) {
+  ADR_REQUIRE(Cp >= C, "pack_weight: Cp < C");
+  long n = (long)K * Cp * RS;
+  ADR_REQUIRE(n > 0, "pack_weight: empty");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<__bf16>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (__bf16*)dst, K, C, Cp,
+                       RS, transpose_kc);
+  else
+    hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (float*)dst, K, C, Cp,
+                       RS, transpose_kc);
+  return check_launch("adr_pack_weight");
+}
+
+extern "C" int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, int RS,
+                                      int transpose_kc, int accumulate, void* stream) {
+  long n = (long)K * Cp * RS;
+  hipLaunchKernelGGL(unpack_weight_grad_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, src, dst, K, C,
+                     Cp, RS, transpose_kc, accumulate);
+  return check_launch("adr_unpack_weight_grad");
+}
+
+extern "C" int adr_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long n, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g(cdiv(n, 256));
+  if (src_dtype == ADR_F32 && dst_dtype == ADR_BF16)
+    hipLaunchKernelGGL((cast_kernel<float, __bf16>), g, dim3(256), 0, st, (const float*)src, (__bf16*)dst, n);
+  else if (src_dtype == ADR_BF16 && dst_dtype == ADR_F32)
+    hipLaunchKernelGGL((cast_kernel<__bf16, float>), g, dim3(256), 0, st, (const __bf16*)src, (float*)dst, n);
+  else if (src_dtype == ADR_F32 && dst_dtype == ADR_F32)
+    hipLaunchKernelGGL((cast_kernel<float, float>), g, dim3(256), 0, st, (const float*)src, (float*)dst, n);
+  else
+    hipLaunchKernelGGL((cast_kernel<__bf16, __bf16>), g, dim3(256), 0, st, (const __bf16*)src, (__bf16*)dst, n);
+  return check_launch("adr_cast");
+}
+
+// NCHW fp32 image batch -> NHWC compute dtype with channels zero-padded to Cp (detect/train.py:57-59 hands the
+// model float images in [0,1]; the first conv's C=3 is padded so every conv input is 16-byte vectorisable).
+template <typename T>
+__global__ void image_to_nhwc_kernel(const float* __restrict__ src, T* __restrict__ dst, int N, int C, int H, int W,
+                                     int Cp) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long n = (long)N * H * W * Cp;
+  if (i >= n) return;
+  int c = (int)(i % Cp);
+  long pix = i / Cp;
+  int w = (int)(pix % W);
+  long r = pix / W;
+  int h = (int)(r % H);
+  int b = (int)(r / H);
+  float v = c < C ? src[(((long)b * C + c) * H + h) * W + w] : 0.f;
+  dst[i] = from_f<T>(v);
+}
+
+extern "C" int adr_image_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cp,
+                                 void* stream) {
+  long n = (long)N * H * W * Cp;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(image_to_nhwc_kernel<__bf16>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (__bf16*)dst, N, C, H,
+                       W, Cp);
+  else
+    hipLaunchKernelGGL(image_to_nhwc_kernel<float>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (float*)dst, N, C, H, W,
+                       Cp);
+  return check_launch("adr_image_to_nhwc");
+}
