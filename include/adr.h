@@ -31,6 +31,8 @@ enum adr_act { ADR_ACT_NONE = 0, ADR_ACT_SILU = 1, ADR_ACT_GELU = 2, ADR_ACT_REL
 
 int adr_abi_version(void);
 const char* adr_last_error(void);
+/* hipMemsetAsync(ptr, 0, bytes) on `stream` (zero-initialised gradient / accumulation buffers). */
+int adr_memset_zero(void* ptr, size_t bytes, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Dense convolution as implicit GEMM on MFMA.
@@ -106,6 +108,66 @@ int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, i
 /* NCHW fp32 images (detect/train.py:57-59 preprocess output) -> NHWC compute dtype, channels padded to Cp. */
 int adr_image_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cp, void* stream);
 int adr_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long n, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Elementwise glue on NHWC views (npix pixels x C channels, per-pixel channel strides).
+ * op: 0 copy (torch.cat pieces, block.py:244-247) | 1 o = ca*a + cb*b (Fusion bifpn block.py:1532-1535,
+ * residual adds block.py:353, Add :1448-1453) | 2 o = a*b (Multiply :1442-1447) | 3 o = a + b*c
+ * (CrossTaskInteraction head.py:744-745) | 4 o = act(a) | 5 o = b*act'(a) | 6 o = a+b+c.
+ * ca / cb are device scalars (null = 1). accumulate: o += result. */
+int adr_ew(int dtype, int op, int act, const void* a, int acs, const void* b, int bcs, const void* c, int ccs,
+           void* o, int ocs, long npix, int C, const float* ca, const float* cb, int accumulate, void* stream);
+/* o (+)= x * g[n*gns + c*gcs] (+ res): per-image / per-channel broadcast scale (TaskDecomposition
+ * head.py:657-664, Scale head.py:797, residual_weight block.py:2680). */
+int adr_bcast_mul(int dtype, const void* x, int xcs, const float* g, int gns, int gcs, const void* res, int rcs,
+                  void* o, int ocs, int N, int HW, int C, int accumulate, void* stream);
+/* partial[n][chunk][0][c] = sum x*dz, [1][c] = sum dz (x may be NULL); then collapse over chunks (+n, +c). */
+int adr_dot_reduce(int dtype, const void* x, int xcs, const void* dz, int dcs, int N, int HW, int C,
+                   int rows_per_chunk, float* partial, void* stream);
+int adr_nc_collapse(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n, int sum_c,
+                    int accumulate, void* stream);
+/* BiFPN weights w = relu(fw)/(sum relu(fw)+eps) and backward (block.py:1532-1535). */
+int adr_fusion_weights(const float* fw, int n, float eps, float* w, void* stream);
+int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Pooling / resampling (NHWC). Max pool k x k stride 1 pad k/2 with uint8 argmax (SPPF block.py:177-196);
+ * axis means + separable gate (ELA_HSFPN block.py:1408-1424, CoordAtt head.py:671-707); adaptive average
+ * pooling (block.py:1558-1581, 2455); bilinear resize align_corners=False (block.py:2459-2462).
+ * Axis-mean outputs / gate inputs are [n][l][c] planes addressed as base + n*stride_n + l*C + c. */
+int adr_maxpool(int dtype, const void* x, int xcs, void* y, int ycs, uint8_t* arg, int N, int H, int W, int C, int k,
+                void* stream);
+int adr_maxpool_bwd(int dtype, const void* dy, int dcs, const uint8_t* arg, void* dx, int ocs, int N, int H, int W,
+                    int C, int k, int accumulate, void* stream);
+int adr_axis_mean(int dtype, const void* x, int xcs, int N, int H, int W, int C, void* oh, long ohn, void* ow,
+                  long own, void* stream);
+int adr_axis_mean_bwd(int dtype, const void* dh, long dhn, const void* dw, long dwn, void* dx, int ocs, int N, int H,
+                      int W, int C, int accumulate, void* stream);
+int adr_gate(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw, long awn, void* o, int ocs,
+             int N, int H, int W, int C, void* stream);
+int adr_gate_bwd(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw, long awn,
+                 const void* dout, int dcs, void* dx, int ocs, void* dah, long dahn, void* daw, long dawn, int N,
+                 int H, int W, int C, int accumulate, void* stream);
+int adr_adapool(int dtype, const void* x, int xcs, int N, int H, int W, int C, void* y, int ycs, int OH, int OW,
+                void* stream);
+int adr_adapool_bwd(int dtype, const void* dy, int dcs, int N, int H, int W, int C, void* dx, int ocs, int OH, int OW,
+                    int accumulate, void* stream);
+int adr_bilinear(int dtype, const void* x, int xcs, int N, int H, int W, int C, void* y, int ycs, int OH, int OW,
+                 void* stream);
+int adr_bilinear_bwd(int dtype, const void* dy, int dcs, int N, int H, int W, int C, void* dx, int ocs, int OH,
+                     int OW, int accumulate, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * MLCA (block.py:1540-1584) fused: out = res + y * up(att(y)).  Saved tensors (fp32, caller-owned):
+ * local [N][25][C], att [N][25][C], sig_l [N][25*C], sig_g [N][C]. */
+int adr_mlca_fwd(int dtype, const void* y, int ycs, const void* res, int rcs, void* out, int ocs, int N, int H, int W,
+                 int C, const float* wl, const float* wg, int k, float local_weight, float* local, float* att,
+                 float* sig_l, float* sig_g, void* stream);
+size_t adr_mlca_bwd_workspace(int N, int C, int k);
+int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout, int dcs, void* dy, int ocs, int N, int H, int W,
+                 int C, const float* wl, const float* wg, int k, float local_weight, const float* local,
+                 const float* att, const float* sig_l, const float* sig_g, float* dwl, float* dwg, float* ws,
+                 size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

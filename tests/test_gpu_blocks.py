@@ -1,0 +1,94 @@
+"""GPU parity: backbone / neck blocks against the reference-generated module fixtures (and the oracle)."""
+import pytest
+import torch
+
+from conftest import golden
+from gpu_util import TOL, assert_close, load_recipe_into, to_dev
+from recipe import seeded_randn
+
+pytestmark = pytest.mark.gpu
+
+SEEDS = {"conv_k3s2": 21, "c3k2": 22, "c3k2_mlca_c3k": 23, "c3k2_mlca": 24, "sppf": 25, "ela": 26,
+         "ela_noflag": 27, "convT": 28, "fusion": 29, "c2ptssa": 30, "c2tssa_mona": 31, "ayhead": 32}
+
+
+def run_fixture(name, module, dtype, list_input=False, tol=None):
+    g = golden(f"mod_{name}")
+    load_recipe_into(module)
+    module = module.cuda().train()
+    ins, i = [], 0
+    while f"in{i}_shape" in g:
+        x = seeded_randn(*[int(v) for v in g[f"in{i}_shape"]], seed=int(g[f"in{i}_seed"]))
+        ins.append(to_dev(x, dtype))
+        i += 1
+    out = module(ins) if list_input else module(ins[0])
+    outs = out if isinstance(out, (list, tuple)) else [out]
+    gen = torch.Generator().manual_seed(SEEDS[name] + 1)
+    gouts = [torch.randn(o.shape, generator=gen) for o in outs]
+    torch.autograd.backward(list(outs), [gg.to("cuda", dtype).contiguous(memory_format=torch.channels_last)
+                                         if gg.dim() == 4 else gg.to("cuda", dtype) for gg in gouts])
+    tol = tol or TOL[dtype]
+    for j, o in enumerate(outs):
+        assert_close(o.float(), g[f"out{j}"], **tol, what=f"{name} out{j}")
+    for j, x in enumerate(ins):
+        if name == "sppf" and dtype == torch.bfloat16:
+            # bf16 rounding creates max-pool ties the fp32 reference does not have, so gradients route to a
+            # different (equal-valued) element; compare in relative L2 instead of elementwise
+            d = (x.grad.float().cpu() - torch.as_tensor(g[f"gin{j}"])).norm() / torch.as_tensor(g[f"gin{j}"]).norm()
+            assert float(d) < 0.15, float(d)
+            continue
+        assert_close(x.grad.float(), g[f"gin{j}"], **tol, what=f"{name} gin{j}")
+    ref = dict(zip([str(k) for k in g["param_grad_norms_keys"]], g["param_grad_norms"]))
+    params = dict(module.named_parameters())
+    bad = []
+    for k, v in ref.items():
+        mine = float(params[k].grad.norm()) if params[k].grad is not None else 0.0
+        if abs(mine - v) > tol["rtol"] * 4 * max(v, 1e-3):
+            bad.append((k, mine, v))
+    assert not bad, bad[:8]
+    return module
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c3k2(dtype):
+    from adrefine.nn.modules.block import C3k2
+    run_fixture("c3k2", C3k2(32, 64, 1, False, 0.25), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c3k2_mlca(dtype):
+    from adrefine.nn.modules.block import C3k2_MLCA
+    run_fixture("c3k2_mlca", C3k2_MLCA(128, 128, 1, False), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c3k2_mlca_c3k(dtype):
+    from adrefine.nn.modules.block import C3k2_MLCA
+    run_fixture("c3k2_mlca_c3k", C3k2_MLCA(128, 128, 1, True), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sppf(dtype):
+    from adrefine.nn.modules.block import SPPF
+    run_fixture("sppf", SPPF(256, 256, 5), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("flag", [True, False])
+def test_ela(dtype, flag):
+    from adrefine.nn.modules.block import ELA_HSFPN
+    run_fixture("ela" if flag else "ela_noflag", ELA_HSFPN(128, flag), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fusion(dtype):
+    from adrefine.nn.modules.block import Fusion
+    run_fixture("fusion", Fusion([128, 128]), dtype, list_input=True)
+
+
+def test_no_relayout_copies():
+    import adrefine.kernels as K
+    from adrefine.nn.modules.block import C3k2_MLCA
+    K.relayout_count[0] = 0
+    run_fixture("c3k2_mlca", C3k2_MLCA(128, 128, 1, False), torch.bfloat16)
+    assert K.relayout_count[0] == 0

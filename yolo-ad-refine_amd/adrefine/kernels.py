@@ -22,6 +22,7 @@ STATS_ROWS = 256  # rows per chunk for adr_nc_reduce
 
 # counts layout fix-ups (should stay 0 on the hot path; tests assert it)
 relayout_count = [0]
+_TRACE_RELAYOUT = bool(int(__import__("os").environ.get("ADR_TRACE_RELAYOUT", "0")))
 
 
 def dcode(dtype) -> int:
@@ -50,6 +51,9 @@ def nhwc(t: torch.Tensor):
     vec = 16 // t.element_size()
     if not ok or t.data_ptr() % 16 or s3 % vec:
         relayout_count[0] += 1
+        if _TRACE_RELAYOUT:
+            import traceback
+            traceback.print_stack(limit=6)
         t = t.contiguous(memory_format=torch.channels_last)
         s3 = t.stride(3)
     return t, t.data_ptr(), s3
@@ -87,6 +91,10 @@ def unpack_weight_grad(dw_krsc: torch.Tensor, shape, cpad: int = 0, transpose_kc
     out = torch.empty(shape, dtype=torch.float32, device=dw_krsc.device)
     lib.adr_unpack_weight_grad(fptr(dw_krsc), fptr(out), K, C, max(C, cpad), RS, transpose_kc, 0, stream())
     return out
+
+
+def _pair(v):
+    return (v, v) if isinstance(v, int) else (int(v[0]), int(v[1]))
 
 
 def conv_desc(n, h, w, c, xcs, k, r, s, sh, sw, ph, pw, ycs, dtype):
@@ -129,7 +137,8 @@ class Conv2dFn(torch.autograd.Function):
         if C != Cp:
             raise RuntimeError(f"Conv2dFn: input has {C} channels, weight expects {Cw} (padded {Cp})")
         wp = pack_weight(w, dtype, cpad)
-        d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, stride, stride, pad, pad, K, dtype)
+        (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+        d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, K, dtype)
         y = empty_act(N, K, Ho, Wo, dtype, x.device)
         stats = None
         if want_stats:
@@ -149,15 +158,16 @@ class Conv2dFn(torch.autograd.Function):
     def backward(ctx, dy, _dstats):
         x, wp = ctx.saved_tensors
         stride, pad, cpad, wshape, has_b = ctx.meta
+        (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
         dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
         N, C, H, W = x.shape
         K, _, R, S = wshape
         _, xp, xcs = nhwc(x)
-        d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, stride, stride, pad, pad, dycs, x.dtype)
+        d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = empty_act(N, C, H, W, x.dtype, x.device)
-            d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, stride, stride, pad, pad, dycs, x.dtype)
+            d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
             lib.adr_conv2d_dgrad(ctypes.byref(d2), ctypes.c_void_p(dyp), fptr(wp), None,
                                  ctypes.c_void_p(dx.data_ptr()), 0, stream())
         if ctx.needs_input_grad[1]:
@@ -361,3 +371,521 @@ def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool):
 
 def gn_act(y, gn: torch.nn.Module, act: str):
     return GNActFn.apply(y, gn.weight, gn.bias, gn.num_groups, act, gn.eps)
+
+
+# ---------------------------------------------------------------------------------------------------------
+# elementwise glue
+# ---------------------------------------------------------------------------------------------------------
+EW_COPY, EW_AXPBY, EW_MUL, EW_FMA, EW_ACT, EW_ACT_BWD, EW_ADD3 = range(7)
+
+
+def _ew(op, out, a, b=None, c=None, act=0, ca=None, cb=None, accumulate=0):
+    """Launch adr_ew over same-shaped NHWC views (a, b, c, out are (tensor, ptr, cs) triples or None)."""
+    t = a[0]
+    N, C, H, W = t.shape
+    lib.adr_ew(dcode(t.dtype), op, act, ctypes.c_void_p(a[1]), a[2], ctypes.c_void_p(b[1]) if b else None,
+               b[2] if b else 0, ctypes.c_void_p(c[1]) if c else None, c[2] if c else 0, ctypes.c_void_p(out[1]),
+               out[2], N * H * W, C, fptr(ca), fptr(cb), accumulate, stream())
+
+
+def _v(t):
+    return nhwc(t)
+
+
+def _new_like(t):
+    n, c, h, w = t.shape
+    return empty_act(n, c, h, w, t.dtype, t.device)
+
+
+class CatFn(torch.autograd.Function):
+    """torch.cat(xs, dim=1) on NHWC: one copy per piece into the concat buffer; backward = zero-copy slices."""
+
+    @staticmethod
+    def forward(ctx, *xs):
+        t0 = xs[0]
+        N, _, H, W = t0.shape
+        Ctot = sum(x.shape[1] for x in xs)
+        out = empty_act(N, Ctot, H, W, t0.dtype, t0.device)
+        off = 0
+        sizes = []
+        for x in xs:
+            v = _v(x)
+            o = out[:, off:off + x.shape[1]]
+            _ew(EW_COPY, (o, o.data_ptr(), Ctot), v)
+            sizes.append(x.shape[1])
+            off += x.shape[1]
+        ctx.sizes = sizes
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy, _, _ = _v(dy)
+        outs, off = [], 0
+        for s in ctx.sizes:
+            outs.append(dy[:, off:off + s])
+            off += s
+        return tuple(outs)
+
+
+def cat(xs):
+    return CatFn.apply(*xs)
+
+
+def zero_(t):
+    """Zero a device tensor's storage span with hipMemsetAsync (via libadr)."""
+    lib.adr_memset_zero(ctypes.c_void_p(t.data_ptr()), t.numel() * t.element_size(), stream())
+    return t
+
+
+class SplitFn(torch.autograd.Function):
+    """x.split(sizes, dim=1) as zero-copy NHWC views; backward assembles the piece gradients into one NHWC
+    gradient buffer with libadr copies (absent pieces are zero-filled), keeping grads channels_last."""
+
+    @staticmethod
+    def forward(ctx, x, sizes):
+        ctx.set_materialize_grads(False)
+        ctx.meta = (tuple(sizes), x.shape, x.dtype)
+        outs, off = [], 0
+        for sz in sizes:
+            outs.append(x[:, off:off + sz])
+            off += sz
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        sizes, shape, dtype = ctx.meta
+        N, C, H, W = shape
+        dev = next(g for g in grads if g is not None).device
+        dx = empty_act(N, C, H, W, dtype, dev)
+        off = 0
+        for g, sz in zip(grads, sizes):
+            piece = dx[:, off:off + sz]
+            if g is None:
+                # zero the slice: o = 0*piece + 0*piece would read garbage; copy from a zero tensor instead
+                z = zero_(empty_act(N, sz, H, W, dtype, dev))
+                _ew(EW_COPY, (piece, piece.data_ptr(), C), _v(z))
+            else:
+                _ew(EW_COPY, (piece, piece.data_ptr(), C), _v(g.to(dtype) if g.dtype != dtype else g))
+            off += sz
+        return dx, None
+
+
+def split(x, sizes):
+    return SplitFn.apply(x, list(sizes))
+
+
+class AddFn(torch.autograd.Function):
+    """a + b (+ c)."""
+
+    @staticmethod
+    def forward(ctx, a, b, c=None):
+        va, vb = _v(a), _v(b)
+        out = _new_like(va[0])
+        if c is None:
+            _ew(EW_AXPBY, (out, out.data_ptr(), out.shape[1]), va, vb)
+        else:
+            _ew(EW_ADD3, (out, out.data_ptr(), out.shape[1]), va, vb, _v(c))
+        ctx.three = c is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        return (dy, dy, dy) if ctx.three else (dy, dy, None)
+
+
+def add(a, b, c=None):
+    return AddFn.apply(a, b, c)
+
+
+class MulFn(torch.autograd.Function):
+    """a * b (Multiply, block.py:1442-1447)."""
+
+    @staticmethod
+    def forward(ctx, a, b):
+        va, vb = _v(a), _v(b)
+        out = _new_like(va[0])
+        _ew(EW_MUL, (out, out.data_ptr(), out.shape[1]), va, vb)
+        ctx.save_for_backward(va[0], vb[0])
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, b = ctx.saved_tensors
+        vd = _v(dy)
+        da = db = None
+        if ctx.needs_input_grad[0]:
+            da = _new_like(a)
+            _ew(EW_MUL, (da, da.data_ptr(), da.shape[1]), vd, _v(b))
+        if ctx.needs_input_grad[1]:
+            db = _new_like(b)
+            _ew(EW_MUL, (db, db.data_ptr(), db.shape[1]), vd, _v(a))
+        return da, db
+
+
+def mul(a, b):
+    return MulFn.apply(a, b)
+
+
+class FmaFn(torch.autograd.Function):
+    """a + b * c (gated residual, CrossTaskInteraction head.py:744-745)."""
+
+    @staticmethod
+    def forward(ctx, a, b, c):
+        va, vb, vc = _v(a), _v(b), _v(c)
+        out = _new_like(va[0])
+        _ew(EW_FMA, (out, out.data_ptr(), out.shape[1]), va, vb, vc)
+        ctx.save_for_backward(vb[0], vc[0])
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        b, c = ctx.saved_tensors
+        vd = _v(dy)
+        db = _new_like(b)
+        _ew(EW_MUL, (db, db.data_ptr(), db.shape[1]), vd, _v(c))
+        dc = _new_like(c)
+        _ew(EW_MUL, (dc, dc.data_ptr(), dc.shape[1]), vd, _v(b))
+        return dy, db, dc
+
+
+def fma(a, b, c):
+    return FmaFn.apply(a, b, c)
+
+
+class ActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, act):
+        vx = _v(x)
+        out = _new_like(vx[0])
+        _ew(EW_ACT, (out, out.data_ptr(), out.shape[1]), vx, act=ACT[act])
+        ctx.save_for_backward(vx[0])
+        ctx.act = act
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        dx = _new_like(x)
+        _ew(EW_ACT_BWD, (dx, dx.data_ptr(), dx.shape[1]), _v(x), _v(dy), act=ACT[ctx.act])
+        return dx, None
+
+
+def act(x, name):
+    return x if name == "none" else ActFn.apply(x, name)
+
+
+def _reduce_dot(x, dy, sum_n, sum_c, which=0):
+    """sum over pixels of x*dy (which=0) or dy (which=1), per (n, c), optionally collapsed over n / c."""
+    N, C, H, W = dy.shape
+    vd = _v(dy)
+    vx = _v(x) if x is not None else (None, 0, 0)
+    chunks = lib.adr_nc_reduce_chunks(H * W, STATS_ROWS)
+    part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dy.device)
+    lib.adr_dot_reduce(dcode(dy.dtype), ctypes.c_void_p(vx[1]) if x is not None else None, vx[2],
+                       ctypes.c_void_p(vd[1]), vd[2], N, H * W, C, STATS_ROWS, fptr(part), stream())
+    out = torch.empty((1 if sum_n else N) * (1 if sum_c else C), dtype=torch.float32, device=dy.device)
+    lib.adr_nc_collapse(fptr(part), N, chunks, C, which, fptr(out), int(sum_n), int(sum_c), 0, stream())
+    return out
+
+
+class ScaleFn(torch.autograd.Function):
+    """x * g (+ res) with g a device tensor broadcast as: 'scalar' (shape ()), 'n' (N,), 'c' (C,), 'nc' (N, C)."""
+
+    @staticmethod
+    def forward(ctx, x, g, res, mode):
+        vx = _v(x)
+        N, C, H, W = x.shape
+        gs = g.detach().float().contiguous()
+        gns, gcs = {"scalar": (0, 0), "n": (1, 0), "c": (0, 1), "nc": (C, 1)}[mode]
+        out = _new_like(vx[0])
+        vr = _v(res) if res is not None else None
+        lib.adr_bcast_mul(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], fptr(gs), gns, gcs,
+                          ctypes.c_void_p(vr[1]) if vr else None, vr[2] if vr else 0, ctypes.c_void_p(out.data_ptr()),
+                          C, N, H * W, C, 0, stream())
+        ctx.save_for_backward(vx[0], gs)
+        ctx.meta = (mode, g.shape, res is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gs = ctx.saved_tensors
+        mode, gshape, has_res = ctx.meta
+        N, C, H, W = x.shape
+        vd = _v(dy)
+        dx = dg = None
+        if ctx.needs_input_grad[0]:
+            dx = _new_like(x)
+            gns, gcs = {"scalar": (0, 0), "n": (1, 0), "c": (0, 1), "nc": (C, 1)}[mode]
+            lib.adr_bcast_mul(dcode(x.dtype), ctypes.c_void_p(vd[1]), vd[2], fptr(gs), gns, gcs, None, 0,
+                              ctypes.c_void_p(dx.data_ptr()), C, N, H * W, C, 0, stream())
+        if ctx.needs_input_grad[1]:
+            sum_n = mode in ("scalar", "c")
+            sum_c = mode in ("scalar", "n")
+            dg = _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape)
+        return dx, dg, (dy if has_res else None), None
+
+
+def scale(x, g, mode, res=None):
+    return ScaleFn.apply(x, g, res, mode)
+
+
+class WeightedSumFn(torch.autograd.Function):
+    """sum_i w[i] * x_i (+ base) with w a learnable device vector (PFF stage_attention, block.py:2626-2628)."""
+
+    @staticmethod
+    def forward(ctx, w, base, *xs):
+        wd = w.detach().float().contiguous()
+        out = _new_like(xs[0])
+        vo = (out, out.data_ptr(), out.shape[1])
+        # o = w0*x0 + (base or 0)*1 ; then o += w_i * x_i
+        v0 = _v(xs[0])
+        if base is not None:
+            _ew(EW_AXPBY, vo, v0, _v(base), ca=wd[0:1])
+        else:
+            _ew(EW_AXPBY, vo, v0, v0, ca=wd[0:1], cb=torch.zeros(1, device=w.device))
+        for i in range(1, len(xs)):
+            vi = _v(xs[i])
+            _ew(EW_AXPBY, vo, vi, vi, ca=wd[i:i + 1], cb=torch.zeros(1, device=w.device), accumulate=1)
+        ctx.save_for_backward(wd, *[_v(x)[0] for x in xs])
+        ctx.has_base = base is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        wd, *xs = ctx.saved_tensors
+        vd = _v(dy)
+        dxs = []
+        for i, x in enumerate(xs):
+            d = _new_like(x)
+            _ew(EW_AXPBY, (d, d.data_ptr(), d.shape[1]), vd, vd, ca=wd[i:i + 1], cb=torch.zeros(1, device=dy.device))
+            dxs.append(d)
+        dw = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs]) if ctx.needs_input_grad[0] else None
+        return (dw, dy if ctx.has_base else None, *dxs)
+
+
+def weighted_sum(w, xs, base=None):
+    return WeightedSumFn.apply(w, base, *xs)
+
+
+class FusionFn(torch.autograd.Function):
+    """Fusion('bifpn'): w = relu(fw)/(sum+1e-4); out = sum_i w_i x_i (block.py:1532-1535)."""
+
+    @staticmethod
+    def forward(ctx, fw, *xs):
+        fwd = fw.detach().float().contiguous()
+        w = torch.empty_like(fwd)
+        lib.adr_fusion_weights(fptr(fwd), fwd.numel(), 1e-4, fptr(w), stream())
+        out = _new_like(xs[0])
+        vo = (out, out.data_ptr(), out.shape[1])
+        v = [_v(x) for x in xs]
+        _ew(EW_AXPBY, vo, v[0], v[1], ca=w[0:1], cb=w[1:2])
+        for i in range(2, len(xs)):
+            _ew(EW_AXPBY, vo, v[i], v[i], ca=w[i:i + 1], cb=torch.zeros(1, device=fw.device), accumulate=1)
+        ctx.save_for_backward(fwd, w, *[t[0] for t in v])
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        fwd, w, *xs = ctx.saved_tensors
+        vd = _v(dy)
+        z = torch.zeros(1, device=dy.device)
+        dxs = []
+        for i, x in enumerate(xs):
+            d = _new_like(x)
+            _ew(EW_AXPBY, (d, d.data_ptr(), d.shape[1]), vd, vd, ca=w[i:i + 1], cb=z)
+            dxs.append(d)
+        dwn = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs])
+        dfw = torch.empty_like(fwd)
+        lib.adr_fusion_weights_bwd(fptr(fwd), fwd.numel(), 1e-4, fptr(dwn), fptr(dfw), stream())
+        return (dfw, *dxs)
+
+
+def fusion(fw, xs):
+    return FusionFn.apply(fw, *xs)
+
+
+# ---------------------------------------------------------------------------------------------------------
+# pooling
+# ---------------------------------------------------------------------------------------------------------
+
+
+class MaxPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, k):
+        vx = _v(x)
+        N, C, H, W = x.shape
+        y = _new_like(vx[0])
+        arg = torch.empty(N * H * W * C, dtype=torch.uint8, device=x.device)
+        lib.adr_maxpool(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(y.data_ptr()), C, fptr(arg),
+                        N, H, W, C, k, stream())
+        ctx.save_for_backward(arg)
+        ctx.meta = (k, x.shape, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (arg,) = ctx.saved_tensors
+        k, shape, dtype = ctx.meta
+        N, C, H, W = shape
+        vd = _v(dy)
+        dx = empty_act(N, C, H, W, dtype, dy.device)
+        lib.adr_maxpool_bwd(dcode(dtype), ctypes.c_void_p(vd[1]), vd[2], fptr(arg), ctypes.c_void_p(dx.data_ptr()), C,
+                            N, H, W, C, k, 0, stream())
+        return dx, None
+
+
+def maxpool(x, k):
+    return MaxPoolFn.apply(x, k)
+
+
+class MLCAFn(torch.autograd.Function):
+    """res + MLCA(y) (block.py:1540-1594) — 3 fused kernels forward, 3 (+2 tiny) backward."""
+
+    @staticmethod
+    def forward(ctx, y, res, wl, wg, local_weight):
+        vy = _v(y)
+        N, C, H, W = y.shape
+        dev = y.device
+        f = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731
+        local, att, sig_l, sig_g = f(N, 25, C), f(N, 25, C), f(N, 25 * C), f(N, C)
+        out = _new_like(vy[0])
+        vr = _v(res) if res is not None else None
+        wlf, wgf = wl.detach().float().contiguous().view(-1), wg.detach().float().contiguous().view(-1)
+        k = wlf.numel()
+        lib.adr_mlca_fwd(dcode(y.dtype), ctypes.c_void_p(vy[1]), vy[2], ctypes.c_void_p(vr[1]) if vr else None,
+                         vr[2] if vr else 0, ctypes.c_void_p(out.data_ptr()), C, N, H, W, C, fptr(wlf), fptr(wgf), k,
+                         float(local_weight), fptr(local), fptr(att), fptr(sig_l), fptr(sig_g), stream())
+        ctx.save_for_backward(vy[0], wlf, wgf, local, att, sig_l, sig_g)
+        ctx.meta = (local_weight, res is not None, wl.shape, wg.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, wlf, wgf, local, att, sig_l, sig_g = ctx.saved_tensors
+        lw, has_res, wls, wgs = ctx.meta
+        N, C, H, W = y.shape
+        vd, vy = _v(dout), _v(y)
+        dy = _new_like(y)
+        k = wlf.numel()
+        dwl = torch.empty(k, dtype=torch.float32, device=y.device)
+        dwg = torch.empty(k, dtype=torch.float32, device=y.device)
+        wsb = lib.adr_mlca_bwd_workspace(N, C, k)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=y.device)
+        lib.adr_mlca_bwd(dcode(y.dtype), ctypes.c_void_p(vy[1]), vy[2], ctypes.c_void_p(vd[1]), vd[2],
+                         ctypes.c_void_p(dy.data_ptr()), C, N, H, W, C, fptr(wlf), fptr(wgf), k, float(lw),
+                         fptr(local), fptr(att), fptr(sig_l), fptr(sig_g), fptr(dwl), fptr(dwg), fptr(ws), wsb,
+                         stream())
+        return dy, (dout if has_res else None), dwl.view(wls), dwg.view(wgs), None
+
+
+def mlca(y, res, wl, wg, local_weight=0.5):
+    return MLCAFn.apply(y, res, wl, wg, local_weight)
+
+
+class AxisMeanFn(torch.autograd.Function):
+    """Row means over W and column means over H, written as NHWC 'images':
+    layout 'ela'   -> (2N, C, L, 1): rows [0,N) hold the H-means (L=H), rows [N,2N) the W-means (needs H == W)
+    layout 'coord' -> (N, C, H+W, 1): per image rows [0,H) H-means then [H,H+W) W-means (CoordAtt cat)."""
+
+    @staticmethod
+    def forward(ctx, x, layout):
+        vx = _v(x)
+        N, C, H, W = x.shape
+        dev = x.device
+        if layout == "ela":
+            if H != W:
+                raise RuntimeError("ELA_HSFPN shares one Conv1d over both axes; this build needs H == W")
+            out = empty_act(2 * N, C, H, 1, x.dtype, dev)
+            oh, ohn = out.data_ptr(), H * C
+            ow, own = out.data_ptr() + N * H * C * out.element_size(), W * C
+        else:
+            out = empty_act(N, C, H + W, 1, x.dtype, dev)
+            oh, ohn = out.data_ptr(), (H + W) * C
+            ow, own = out.data_ptr() + H * C * out.element_size(), (H + W) * C
+        lib.adr_axis_mean(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], N, H, W, C, ctypes.c_void_p(oh), ohn,
+                          ctypes.c_void_p(ow), own, stream())
+        ctx.meta = (layout, x.shape, x.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        layout, shape, dtype = ctx.meta
+        N, C, H, W = shape
+        dy = dy.contiguous(memory_format=torch.channels_last) if not _is_dense_nhwc(dy) else dy
+        es = dy.element_size()
+        if layout == "ela":
+            dh, dhn, dw, dwn = dy.data_ptr(), H * C, dy.data_ptr() + N * H * C * es, W * C
+        else:
+            dh, dhn, dw, dwn = dy.data_ptr(), (H + W) * C, dy.data_ptr() + H * C * es, (H + W) * C
+        dx = empty_act(N, C, H, W, dtype, dy.device)
+        lib.adr_axis_mean_bwd(dcode(dtype), ctypes.c_void_p(dh), dhn, ctypes.c_void_p(dw), dwn,
+                              ctypes.c_void_p(dx.data_ptr()), C, N, H, W, C, 0, stream())
+        return dx, None
+
+
+def _is_dense_nhwc(t):
+    n, c, h, w = t.shape
+    return t.stride() == (h * w * c, 1, w * c, c) or t.is_contiguous(memory_format=torch.channels_last)
+
+
+def axis_mean(x, layout):
+    return AxisMeanFn.apply(x, layout)
+
+
+class GateFn(torch.autograd.Function):
+    """out = (x if x is not None else 1) * a_h[n,h,c] * a_w[n,w,c], with a = the (.., L, 1) planes produced in
+    the AxisMeanFn layouts ('ela': a is (2N, C, L, 1); 'coord': a_h / a_w are (N, C, H+W, 1) tensors)."""
+
+    @staticmethod
+    def forward(ctx, x, ah_t, aw_t, layout, shape):
+        N, C, H, W = shape
+        dtype = ah_t.dtype
+        ah_t = ah_t if _is_dense_nhwc(ah_t) else ah_t.contiguous(memory_format=torch.channels_last)
+        aw_t = aw_t if _is_dense_nhwc(aw_t) else aw_t.contiguous(memory_format=torch.channels_last)
+        es = ah_t.element_size()
+        if layout == "ela":
+            ah, ahn = ah_t.data_ptr(), H * C
+            aw, awn = aw_t.data_ptr() + N * H * C * es, W * C
+        else:
+            ah, ahn = ah_t.data_ptr(), (H + W) * C
+            aw, awn = aw_t.data_ptr() + H * C * es, (H + W) * C
+        vx = _v(x) if x is not None else (None, 0, 0)
+        out = empty_act(N, C, H, W, dtype, ah_t.device)
+        lib.adr_gate(dcode(dtype), ctypes.c_void_p(vx[1]) if x is not None else None, vx[2], ctypes.c_void_p(ah), ahn,
+                     ctypes.c_void_p(aw), awn, ctypes.c_void_p(out.data_ptr()), C, N, H, W, C, stream())
+        ctx.save_for_backward(*( [vx[0]] if x is not None else []), ah_t, aw_t)
+        ctx.meta = (layout, shape, x is not None, (ah, ahn, aw, awn))
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        layout, shape, has_x, (ah, ahn, aw, awn) = ctx.meta
+        saved = ctx.saved_tensors
+        x = saved[0] if has_x else None
+        ah_t, aw_t = saved[-2], saved[-1]
+        N, C, H, W = shape
+        vd = _v(dout)
+        dtype = ah_t.dtype
+        es = ah_t.element_size()
+        if layout == "ela":
+            da = torch.empty_like(ah_t, memory_format=torch.channels_last)
+            dah, dahn, daw, dawn = da.data_ptr(), H * C, da.data_ptr() + N * H * C * es, W * C
+            dah_t = daw_t = None
+        else:
+            dah_t = torch.zeros_like(ah_t, memory_format=torch.channels_last)
+            daw_t = torch.zeros_like(aw_t, memory_format=torch.channels_last)
+            dah, dahn = dah_t.data_ptr(), (H + W) * C
+            daw, dawn = daw_t.data_ptr() + H * C * es, (H + W) * C
+        dx = empty_act(N, C, H, W, dtype, dout.device) if has_x else None
+        vx = _v(x) if has_x else (None, 0, 0)
+        lib.adr_gate_bwd(dcode(dtype), ctypes.c_void_p(vx[1]) if has_x else None, vx[2], ctypes.c_void_p(ah), ahn,
+                         ctypes.c_void_p(aw), awn, ctypes.c_void_p(vd[1]), vd[2],
+                         ctypes.c_void_p(dx.data_ptr()) if has_x else None, C, ctypes.c_void_p(dah), dahn,
+                         ctypes.c_void_p(daw), dawn, N, H, W, C, 0, stream())
+        if layout == "ela":
+            return dx, da, None, None, None
+        return dx, dah_t, daw_t, None, None
+
+
+def gate(x, ah, aw, layout, shape):
+    return GateFn.apply(x, ah, aw, layout, shape)

@@ -34,7 +34,7 @@ def _ctype(t: str):
             return ctypes.c_char_p
         return ctypes.c_void_p
     return {"int": ctypes.c_int, "double": ctypes.c_double, "float": ctypes.c_float, "size_t": ctypes.c_size_t,
-            "long": ctypes.c_long, "int64_t": ctypes.c_int64, "void": None}[base]
+            "long": ctypes.c_long, "uint8_t": ctypes.c_uint8, "int64_t": ctypes.c_int64, "void": None}[base]
 
 
 def parse_header(path=HEADER):
@@ -83,6 +83,7 @@ class _Lib:
 
 
 _NONSTATUS = {"adr_abi_version", "adr_conv2d_fwd_stat_tiles", "adr_nc_reduce_chunks"}
+_ = _NONSTATUS
 
 lib = _Lib()
 assert lib.lib.adr_abi_version() == 1, "ABI version mismatch"

@@ -26,3 +26,13 @@ int check_launch(const char* what) {
 
 extern "C" int adr_abi_version(void) { return ADR_ABI_VERSION; }
 extern "C" const char* adr_last_error(void) { return adr::g_err; }
+
+extern "C" int adr_memset_zero(void* ptr, size_t bytes, void* stream) {
+  if (!ptr || !bytes) return ADR_OK;
+  hipError_t e = hipMemsetAsync(ptr, 0, bytes, (hipStream_t)stream);
+  if (e != hipSuccess) {
+    adr::set_error("adr_memset_zero: %s", hipGetErrorString(e));
+    return ADR_ERR_LAUNCH;
+  }
+  return ADR_OK;
+}

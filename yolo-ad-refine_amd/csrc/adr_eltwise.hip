@@ -1,0 +1,276 @@
+// Elementwise / broadcast kernels over NHWC views (16-byte vectorised, grid-stride).
+//
+// Covers the reference's glue arithmetic on the hot path: channel concat (torch.cat in C2f/SPPF/C2PSA,
+// block.py:244-247, 194-196), residual adds (Bottleneck block.py:353), Multiply / Add (block.py:1442-1453),
+// Fusion('bifpn') weighted sums (block.py:1532-1535), gates x + a*sigmoid(b) (head.py:739-747),
+// activations (SiLU/GELU/ReLU/Sigmoid/Hardswish), per-image / per-channel broadcast multiplies
+// (TaskDecomposition head.py:657-664, Scale head.py:797) and their backward reductions.
+#include "adr_common.h"
+
+namespace adr {
+
+template <typename T> struct VecIO {
+  static constexpr int V = 16 / sizeof(T);
+  __device__ static void load(const T* p, float* f) {
+    u32x4 v = ld16(p);
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int i = 0; i < V; ++i) f[i] = to_f(e[i]);
+  }
+  __device__ static void store(T* p, const float* f) {
+    u32x4 v;
+    T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+    for (int i = 0; i < V; ++i) e[i] = from_f<T>(f[i]);
+    st16(p, v);
+  }
+};
+
+// op codes for the n-ary kernel:
+//  0 copy          : o = a
+//  1 axpby         : o = ca*a + cb*b               (ca/cb device scalars, null = 1)
+//  2 mul           : o = a*b
+//  3 fma           : o = a + b*c
+//  4 act           : o = act(a)
+//  5 act_bwd       : o = d(=b) * act'(a)
+//  6 add3          : o = a + b + c
+//  7 mul_bwd_pair  : o = d*b (gradient of a in a*b);   (same as mul)
+enum EwOp { EW_COPY = 0, EW_AXPBY = 1, EW_MUL = 2, EW_FMA = 3, EW_ACT = 4, EW_ACT_BWD = 5, EW_ADD3 = 6 };
+
+template <typename T>
+__global__ void __launch_bounds__(256) ew_kernel(int op, int act, const T* a, int acs, const T* b, int bcs, const T* c,
+                                                 int ccs, T* o, int ocs, long npix, int C, const float* ca,
+                                                 const float* cb, int accumulate) {
+  constexpr int V = VecIO<T>::V;
+  const int G = C / V;
+  const long total = npix * G;
+  const float sa = ca ? *ca : 1.f, sb = cb ? *cb : 1.f;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long pix = i / G;
+    int c0 = (int)(i % G) * V;
+    float fa[V], fb[V], fc[V], fo[V];
+    VecIO<T>::load(a + pix * acs + c0, fa);
+    if (op == EW_AXPBY || op == EW_MUL || op == EW_FMA || op == EW_ACT_BWD || op == EW_ADD3)
+      VecIO<T>::load(b + pix * bcs + c0, fb);
+    if (op == EW_FMA || op == EW_ADD3) VecIO<T>::load(c + pix * ccs + c0, fc);
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float r;
+      switch (op) {
+        case EW_COPY: r = fa[k]; break;
+        case EW_AXPBY: r = sa * fa[k] + sb * fb[k]; break;
+        case EW_MUL: r = fa[k] * fb[k]; break;
+        case EW_FMA: r = fa[k] + fb[k] * fc[k]; break;
+        case EW_ACT: r = act_fwd(act, fa[k]); break;
+        case EW_ACT_BWD: r = fb[k] * act_bwd(act, fa[k]); break;
+        default: r = fa[k] + fb[k] + fc[k]; break;
+      }
+      fo[k] = r;
+    }
+    if (accumulate) {
+      float fp[V];
+      VecIO<T>::load(o + pix * ocs + c0, fp);
+#pragma unroll
+      for (int k = 0; k < V; ++k) fo[k] += fp[k];
+    }
+    VecIO<T>::store(o + pix * ocs + c0, fo);
+  }
+}
+
+// o = x * g[n*gns + c*gcs] (+ res) ; g fp32
+template <typename T>
+__global__ void __launch_bounds__(256) bcast_mul_kernel(const T* x, int xcs, const float* g, int gns, int gcs,
+                                                        const T* res, int rcs, T* o, int ocs, long npix, int HW, int C,
+                                                        int accumulate) {
+  constexpr int V = VecIO<T>::V;
+  const int G = C / V;
+  const long total = npix * G;
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
+    long pix = i / G;
+    int c0 = (int)(i % G) * V;
+    int n = (int)(pix / HW);
+    float fx[V], fo[V];
+    VecIO<T>::load(x + pix * xcs + c0, fx);
+#pragma unroll
+    for (int k = 0; k < V; ++k) fo[k] = fx[k] * g[(long)n * gns + (long)(c0 + k) * gcs];
+    if (res) {
+      float fr[V];
+      VecIO<T>::load(res + pix * rcs + c0, fr);
+#pragma unroll
+      for (int k = 0; k < V; ++k) fo[k] += fr[k];
+    }
+    if (accumulate) {
+      float fp[V];
+      VecIO<T>::load(o + pix * ocs + c0, fp);
+#pragma unroll
+      for (int k = 0; k < V; ++k) fo[k] += fp[k];
+    }
+    VecIO<T>::store(o + pix * ocs + c0, fo);
+  }
+}
+
+// out[n][c] = sum over chunks of partial[n][chunk][which][c], then optionally summed over n and/or c
+__global__ void nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n,
+                                   int sum_c, int accumulate) {
+  // one thread per output element; tiny
+  int outN = sum_n ? 1 : N, outC = sum_c ? 1 : C;
+  int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= outN * outC) return;
+  int on = idx / outC, oc = idx % outC;
+  double s = 0.0;
+  int n0 = sum_n ? 0 : on, n1 = sum_n ? N : on + 1;
+  int c0 = sum_c ? 0 : oc, c1 = sum_c ? C : oc + 1;
+  for (int n = n0; n < n1; ++n)
+    for (int ch = 0; ch < chunks; ++ch) {
+      const float* p = partial + ((long)n * chunks + ch) * 2 * C + (long)which * C;
+      for (int c = c0; c < c1; ++c) s += p[c];
+    }
+  out[idx] = accumulate ? out[idx] + (float)s : (float)s;
+}
+
+// partial[n][chunk][0][c] = sum x*dz ; [1][c] = sum dz   (per image, per channel)
+template <typename T>
+__global__ void __launch_bounds__(256) dot_reduce_kernel(const T* __restrict__ x, int xcs, const T* __restrict__ dz,
+                                                         int dcs, int HW, int C, int rows_per_chunk, int chunks,
+                                                         float* __restrict__ partial) {
+  constexpr int V = VecIO<T>::V;
+  __shared__ float sh[2][256 * V];
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  const int G = C / V;
+  const int rpp = 256 / G;
+  const int t = threadIdx.x;
+  const int cg = t % G, r0 = t / G;
+  float s1[V], s2[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const int rbeg = chunk * rows_per_chunk, rend = min(HW, rbeg + rows_per_chunk);
+  if (r0 < rpp) {
+    for (int r = rbeg + r0; r < rend; r += rpp) {
+      long pix = (long)n * HW + r;
+      float fx[V], fd[V];
+      if (x) VecIO<T>::load(x + pix * xcs + cg * V, fx);
+      VecIO<T>::load(dz + pix * dcs + cg * V, fd);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        s1[e] += x ? fx[e] * fd[e] : 0.f;
+        s2[e] += fd[e];
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    sh[0][t * V + e] = s1[e];
+    sh[1][t * V + e] = s2[e];
+  }
+  __syncthreads();
+  float* out = partial + ((long)n * chunks + chunk) * 2 * C;
+  for (int c = t; c < C; c += 256) {
+    int g = c / V, e = c % V;
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < rpp; ++r) {
+      a += sh[0][(g + r * G) * V + e];
+      b += sh[1][(g + r * G) * V + e];
+    }
+    out[c] = a;
+    out[C + c] = b;
+  }
+}
+
+// BiFPN fusion weights: w = relu(fw) / (sum relu(fw) + eps)   (block.py:1532-1535), and its backward
+__global__ void fusion_weights_kernel(const float* fw, int n, float eps, float* w) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += fmaxf(fw[i], 0.f);
+  for (int i = 0; i < n; ++i) w[i] = fmaxf(fw[i], 0.f) / (s + eps);
+}
+__global__ void fusion_weights_bwd_kernel(const float* fw, int n, float eps, const float* dw, float* dfw) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  float s = 0.f;
+  for (int i = 0; i < n; ++i) s += fmaxf(fw[i], 0.f);
+  float d = s + eps;
+  float dot = 0.f;
+  for (int i = 0; i < n; ++i) dot += dw[i] * fmaxf(fw[i], 0.f);
+  for (int i = 0; i < n; ++i) {
+    float g = dw[i] / d - dot / (d * d);  // d w_i / d r_j summed: dw_i/d - sum_k dw_k r_k / d^2
+    dfw[i] = fw[i] > 0.f ? g : 0.f;
+  }
+}
+
+static int ew_grid(long work) {
+  long b = (work + 255) / 256;
+  if (b > 32768) b = 32768;
+  if (b < 1) b = 1;
+  return (int)b;
+}
+
+}  // namespace adr
+
+using namespace adr;
+
+extern "C" int adr_ew(int dtype, int op, int act, const void* a, int acs, const void* b, int bcs, const void* c,
+                      int ccs, void* o, int ocs, long npix, int C, const float* ca, const float* cb, int accumulate,
+                      void* stream) {
+  int v = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % v == 0 && acs % v == 0 && ocs % v == 0 && (!b || bcs % v == 0) && (!c || ccs % v == 0),
+              "adr_ew: C=%d / strides must be multiples of %d", C, v);
+  ADR_REQUIRE(((uintptr_t)a | (uintptr_t)o | (uintptr_t)b | (uintptr_t)c) % 16 == 0, "adr_ew: pointers not 16B aligned");
+  int g = ew_grid(npix * (C / v));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(ew_kernel<__bf16>, dim3(g), dim3(256), 0, st, op, act, (const __bf16*)a, acs,
+                       (const __bf16*)b, bcs, (const __bf16*)c, ccs, (__bf16*)o, ocs, npix, C, ca, cb, accumulate);
+  else
+    hipLaunchKernelGGL(ew_kernel<float>, dim3(g), dim3(256), 0, st, op, act, (const float*)a, acs, (const float*)b,
+                       bcs, (const float*)c, ccs, (float*)o, ocs, npix, C, ca, cb, accumulate);
+  return check_launch("adr_ew");
+}
+
+extern "C" int adr_bcast_mul(int dtype, const void* x, int xcs, const float* g, int gns, int gcs, const void* res,
+                             int rcs, void* o, int ocs, int N, int HW, int C, int accumulate, void* stream) {
+  int v = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % v == 0 && xcs % v == 0 && ocs % v == 0 && (!res || rcs % v == 0), "adr_bcast_mul: misaligned");
+  long npix = (long)N * HW;
+  int grid = ew_grid(npix * (C / v));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(bcast_mul_kernel<__bf16>, dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, g, gns, gcs,
+                       (const __bf16*)res, rcs, (__bf16*)o, ocs, npix, HW, C, accumulate);
+  else
+    hipLaunchKernelGGL(bcast_mul_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, xcs, g, gns, gcs,
+                       (const float*)res, rcs, (float*)o, ocs, npix, HW, C, accumulate);
+  return check_launch("adr_bcast_mul");
+}
+
+extern "C" int adr_dot_reduce(int dtype, const void* x, int xcs, const void* dz, int dcs, int N, int HW, int C,
+                              int rows_per_chunk, float* partial, void* stream) {
+  int v = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % v == 0 && C / v <= 256 && (!x || xcs % v == 0) && dcs % v == 0, "adr_dot_reduce: C=%d", C);
+  int chunks = cdiv(HW, rows_per_chunk);
+  dim3 grid(chunks, N);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(dot_reduce_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dz,
+                       dcs, HW, C, rows_per_chunk, chunks, partial);
+  else
+    hipLaunchKernelGGL(dot_reduce_kernel<float>, grid, dim3(256), 0, st, (const float*)x, xcs, (const float*)dz, dcs,
+                       HW, C, rows_per_chunk, chunks, partial);
+  return check_launch("adr_dot_reduce");
+}
+
+extern "C" int adr_nc_collapse(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n,
+                               int sum_c, int accumulate, void* stream) {
+  int outn = (sum_n ? 1 : N) * (sum_c ? 1 : C);
+  hipLaunchKernelGGL(nc_collapse_kernel, dim3(cdiv(outn, 256)), dim3(256), 0, (hipStream_t)stream, partial, N, chunks,
+                     C, which, out, sum_n, sum_c, accumulate);
+  return check_launch("adr_nc_collapse");
+}
+
+extern "C" int adr_fusion_weights(const float* fw, int n, float eps, float* w, void* stream) {
+  hipLaunchKernelGGL(fusion_weights_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, fw, n, eps, w);
+  return check_launch("adr_fusion_weights");
+}
+
+extern "C" int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream) {
+  hipLaunchKernelGGL(fusion_weights_bwd_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, fw, n, eps, dw, dfw);
+  return check_launch("adr_fusion_weights_bwd");
+}
