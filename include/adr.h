@@ -169,6 +169,40 @@ int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout, int dcs, v
                  const float* att, const float* sig_l, const float* sig_g, float* dwl, float* dwg, float* ws,
                  size_t ws_bytes, void* stream);
 
+/* ---------------------------------------------------------------------------------------------------------
+ * AYHead (nn/modules/head.py:1049-1252).
+ * DyDCNv2 / mmcv ModulatedDeformConv2d (head.py:751-782), 3x3, stride 1, pad 1, deform_groups 1. `om` holds
+ * the spatial_conv_offset output: channels [0,18) offsets (2k = dy, 2k+1 = dx), [18,27) mask LOGITS (the
+ * sigmoid of head.py:1156 is applied inside). cols: [N*H*W][9][C]. dx32: fp32 NHWC accumulation buffer
+ * (zeroed by the caller; float atomics). dom receives d(offset) and d(mask logit) in the om layout. */
+int adr_dcn_im2col(int dtype, const void* x, int xcs, const void* om, int omcs, void* cols, int N, int H, int W,
+                   int C, void* stream);
+int adr_dcn_col2im(int dtype, const void* x, int xcs, const void* om, int omcs, const void* dcols, float* dx32,
+                   void* dom, int domcs, int N, int H, int W, int C, void* stream);
+/* W (Cout, C, 3, 3) fp32 -> [(tap*C + c)][Cout] operand for dcols = dy x W. */
+int adr_dcn_weight_t(int dtype, const float* w, void* out, int Cout, int C, void* stream);
+/* Per-image 2-layer gate MLP on pooled vectors: out = act2(W2 act1(W1 (in*in_scale) + b1) + b2);
+ * act: 0 none, 3 relu, 4 sigmoid, 6 softmax. TaskDecomposition la_conv1/2 (head.py:633-650),
+ * AdaptiveDynamicTanh importance_gate (block.py:2521-2531). */
+int adr_gate_mlp(const float* in, float in_scale, int N, int Cin, const float* W1, const float* b1, int H1, int act1,
+                 const float* W2, const float* b2, int H2, int act2, float* hidden, float* out, void* stream);
+int adr_gate_mlp_bwd(const float* in, float in_scale, int N, int Cin, const float* W1, int H1, int act1,
+                     const float* W2, int H2, int act2, const float* hidden, const float* out, const float* dout,
+                     float* din, float* dW1, float* db1, float* dW2, float* db2, void* stream);
+/* o (+)= g[n*gns + c*gcs] * s broadcast over pixels (adjoint of a global average pool). */
+int adr_bcast_fill(int dtype, const float* g, int gns, int gcs, float s, void* o, int ocs, int N, int HW, int C,
+                   int accumulate, void* stream);
+/* o = x * p[pixel] (cls_prob gate, head.py:1172) and its backward (dx, dp = sum_c dout*x). */
+int adr_mul_pixel(int dtype, const void* x, int xcs, const void* p, int pcs, void* o, int ocs, long npix, int C,
+                  void* stream);
+int adr_mul_pixel_bwd(int dtype, const void* x, int xcs, const void* p, int pcs, const void* dout, int dcs, void* dx,
+                      int ocs, void* dp, int dpcs, long npix, int C, void* stream);
+/* Eval decode (head.py:1181-1204): 3 level outputs (B, 4*reg_max+nc, Hi, Wi) NHWC -> y (B, 4+nc, A) fp32
+ * = [xywh * stride (DFL expectation, dist2bbox), sigmoid(cls)]. */
+int adr_detect_decode(int dtype, const void* f0, const void* f1, const void* f2, int cs0, int cs1, int cs2, int H0,
+                      int W0, int H1, int W1, int H2, int W2, float s0, float s1, float s2, int B, int nc, int reg_max,
+                      float* y, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

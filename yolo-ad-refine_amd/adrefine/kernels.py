@@ -889,3 +889,236 @@ class GateFn(torch.autograd.Function):
 
 def gate(x, ah, aw, layout, shape):
     return GateFn.apply(x, ah, aw, layout, shape)
+
+
+# ---------------------------------------------------------------------------------------------------------
+# head helpers
+# ---------------------------------------------------------------------------------------------------------
+
+
+class GapFn(torch.autograd.Function):
+    """Global average pool -> (N, C) fp32 (F.adaptive_avg_pool2d(x, 1), head.py:1142)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        N, C, H, W = x.shape
+        s = _reduce_dot(None, x, False, False, which=1).view(N, C)
+        ctx.meta = (x.shape, x.dtype)
+        return _vec_affine(s, 1.0 / (H * W))
+
+    @staticmethod
+    def backward(ctx, dg):
+        (N, C, H, W), dtype = ctx.meta
+        dx = empty_act(N, C, H, W, dtype, dg.device)
+        dgc = dg.float().contiguous()
+        lib.adr_bcast_fill(dcode(dtype), fptr(dgc), C, 1, 1.0 / (H * W), ctypes.c_void_p(dx.data_ptr()), C, N, H * W,
+                           C, 0, stream())
+        return dx
+
+
+def _vec_affine(v, s):
+    """out = v * s for a small contiguous fp32 vector (adr_bcast_fill on a one-pixel 'image')."""
+    n = v.numel()
+    out = torch.empty_like(v)
+    lib.adr_bcast_fill(F32, fptr(v.contiguous()), 0, 1, float(s), fptr(out), n, 1, 1, n, 0, stream())
+    return out
+
+
+def gap(x):
+    return GapFn.apply(x)
+
+
+class GateMLPFn(torch.autograd.Function):
+    """act2(W2 act1(W1 v + b1) + b2) per image on pooled vectors v (N, Cin) fp32."""
+
+    ACTS = {"none": 0, "relu": 3, "sigmoid": 4, "softmax": 6}
+
+    @staticmethod
+    def forward(ctx, v, W1, b1, W2, b2, act1, act2):
+        N, Cin = v.shape
+        H1, H2 = W1.shape[0], W2.shape[0]
+        vv = v.float().contiguous()
+        w1 = W1.detach().float().contiguous().view(H1, -1)
+        w2 = W2.detach().float().contiguous().view(H2, -1)
+        b1f = b1.detach().float().contiguous() if b1 is not None else None
+        b2f = b2.detach().float().contiguous() if b2 is not None else None
+        hidden = torch.empty(N, H1, dtype=torch.float32, device=v.device)
+        out = torch.empty(N, H2, dtype=torch.float32, device=v.device)
+        a1, a2 = GateMLPFn.ACTS[act1], GateMLPFn.ACTS[act2]
+        lib.adr_gate_mlp(fptr(vv), 1.0, N, Cin, fptr(w1), fptr(b1f), H1, a1, fptr(w2), fptr(b2f), H2, a2,
+                         fptr(hidden), fptr(out), stream())
+        ctx.save_for_backward(vv, w1, w2, hidden, out)
+        ctx.meta = (a1, a2, W1.shape, W2.shape, b1 is not None, b2 is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        vv, w1, w2, hidden, out = ctx.saved_tensors
+        a1, a2, s1, s2, hb1, hb2 = ctx.meta
+        N, Cin = vv.shape
+        H1, H2 = w1.shape[0], w2.shape[0]
+        d = dout.float().contiguous()
+        dev = vv.device
+        din = torch.empty_like(vv)
+        dW1 = torch.empty(H1, Cin, dtype=torch.float32, device=dev)
+        db1 = torch.empty(H1, dtype=torch.float32, device=dev)
+        dW2 = torch.empty(H2, H1, dtype=torch.float32, device=dev)
+        db2 = torch.empty(H2, dtype=torch.float32, device=dev)
+        lib.adr_gate_mlp_bwd(fptr(vv), 1.0, N, Cin, fptr(w1), H1, a1, fptr(w2), H2, a2, fptr(hidden), fptr(out),
+                             fptr(d), fptr(din), fptr(dW1), fptr(db1), fptr(dW2), fptr(db2), stream())
+        return din, dW1.view(s1), db1 if hb1 else None, dW2.view(s2), db2 if hb2 else None, None, None
+
+
+def gate_mlp(v, W1, b1, W2, b2, act1, act2):
+    return GateMLPFn.apply(v, W1, b1, W2, b2, act1, act2)
+
+
+def padded_conv2d(x, w, b, stride, pad, kpad):
+    """Dense conv whose output channels are zero-padded to `kpad` (27 -> 32 offset/mask conv; 1 -> 8 cls_prob)
+    so every NHWC row stays 16-byte aligned; returns the (N, kpad, H, W) tensor (extra channels are 0)."""
+    return PaddedConvFn.apply(x, w, b, stride, pad, kpad)
+
+
+class PaddedConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, b, stride, pad, kpad):
+        dtype = x.dtype
+        x, xp, xcs = nhwc(x)
+        N, C, H, W = x.shape
+        K, _, R, S = w.shape
+        RS = R * S
+        wp = torch.empty(kpad * RS * C, dtype=dtype, device=x.device)
+        zero_(wp)
+        wf = w.detach().float().contiguous()
+        lib.adr_pack_weight(dcode(dtype), fptr(wf), fptr(wp), K, C, C, RS, 0, stream())
+        bp = zero_(torch.empty(kpad, dtype=torch.float32, device=x.device))
+        if b is not None:
+            lib.adr_cast(F32, fptr(b.detach().float().contiguous()), F32, fptr(bp), K, stream())
+        d, Ho, Wo = conv_desc(N, H, W, C, xcs, kpad, R, S, stride, stride, pad, pad, kpad, dtype)
+        y = empty_act(N, kpad, Ho, Wo, dtype, x.device)
+        lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(xp), fptr(wp), fptr(bp), ctypes.c_void_p(y.data_ptr()),
+                           None, 0, stream())
+        ctx.save_for_backward(x, wp)
+        ctx.meta = (stride, pad, kpad, w.shape, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wp = ctx.saved_tensors
+        stride, pad, kpad, wshape, has_b = ctx.meta
+        dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
+        N, C, H, W = x.shape
+        K, _, R, S = wshape
+        _, xp, xcs = nhwc(x)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = empty_act(N, C, H, W, x.dtype, x.device)
+            d2, _, _ = conv_desc(N, H, W, C, C, kpad, R, S, stride, stride, pad, pad, dycs, x.dtype)
+            lib.adr_conv2d_dgrad(ctypes.byref(d2), ctypes.c_void_p(dyp), fptr(wp), None, ctypes.c_void_p(dx.data_ptr()),
+                                 0, stream())
+        d, Ho, Wo = conv_desc(N, H, W, C, xcs, kpad, R, S, stride, stride, pad, pad, dycs, x.dtype)
+        if ctx.needs_input_grad[1]:
+            dwk = _wgrad(d, xp, dyp, kpad, C, R * S, x.device)
+            dw = unpack_weight_grad(dwk, wshape)  # first K rows of the [kpad][RS][C] gradient
+        if has_b and ctx.needs_input_grad[2]:
+            db = _bias_grad(dy, kpad, N, Ho * Wo, dycs)[:K]
+        return dx, dw, db, None, None, None
+
+
+class DCNFn(torch.autograd.Function):
+    """mmcv ModulatedDeformConv2d(C, Cout, 3, 1, 1, bias=False) with offsets / mask logits from `om`."""
+
+    @staticmethod
+    def forward(ctx, x, om, w):
+        dtype = x.dtype
+        x, xp, xcs = nhwc(x)
+        om, omp, omcs = nhwc(om)
+        N, C, H, W = x.shape
+        Cout = w.shape[0]
+        cols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=x.device)
+        lib.adr_dcn_im2col(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(cols), N, H, W, C,
+                           stream())
+        wp = pack_weight(w, dtype)  # KRSC [co][tap][c] == 1x1 weight over the [tap][c] columns
+        d, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, Cout, dtype)
+        y = empty_act(N, Cout, H, W, dtype, x.device)
+        lib.adr_conv2d_fwd(ctypes.byref(d), fptr(cols), fptr(wp), None, ctypes.c_void_p(y.data_ptr()), None, 0,
+                           stream())
+        ctx.save_for_backward(x, om, cols, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, om, cols, w = ctx.saved_tensors
+        dtype = x.dtype
+        _, xp, xcs = nhwc(x)
+        _, omp, omcs = nhwc(om)
+        dy, dyp, dycs = nhwc(dy.to(dtype) if dy.dtype != dtype else dy)
+        N, C, H, W = x.shape
+        Cout = w.shape[0]
+        dev = x.device
+        # dcols = dy x W^T  (1x1 GEMM: Cin = Cout, K = 9C)
+        wt = torch.empty(9 * C * Cout, dtype=dtype, device=dev)
+        lib.adr_dcn_weight_t(dcode(dtype), fptr(w.detach().float().contiguous()), fptr(wt), Cout, C, stream())
+        dcols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=dev)
+        d, _, _ = conv_desc(N, H, W, Cout, dycs, 9 * C, 1, 1, 1, 1, 0, 0, 9 * C, dtype)
+        lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(dyp), fptr(wt), None, fptr(dcols), None, 0, stream())
+        dw = None
+        if ctx.needs_input_grad[2]:
+            dwd, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, dycs, dtype)
+            dwk = _wgrad(dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, dev)
+            dw = unpack_weight_grad(dwk, w.shape)
+        dx32 = zero_(torch.empty(N * H * W * C, dtype=torch.float32, device=dev))
+        dom = zero_(empty_act(N, om.shape[1], H, W, dtype, dev))
+        lib.adr_dcn_col2im(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(dcols), fptr(dx32),
+                           ctypes.c_void_p(dom.data_ptr()), om.shape[1], N, H, W, C, stream())
+        dx = empty_act(N, C, H, W, dtype, dev)
+        lib.adr_cast(F32, fptr(dx32), dcode(dtype), ctypes.c_void_p(dx.data_ptr()), N * H * W * C, stream())
+        return dx, dom, dw
+
+
+def dcn(x, om, w):
+    return DCNFn.apply(x, om, w)
+
+
+class MulPixelFn(torch.autograd.Function):
+    """x * p[:, 0:1] (per-pixel scalar from channel 0 of p)."""
+
+    @staticmethod
+    def forward(ctx, x, p):
+        vx, vp = _v(x), _v(p)
+        N, C, H, W = x.shape
+        out = _new_like(vx[0])
+        lib.adr_mul_pixel(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vp[1]), vp[2],
+                          ctypes.c_void_p(out.data_ptr()), C, N * H * W, C, stream())
+        ctx.save_for_backward(vx[0], vp[0])
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, p = ctx.saved_tensors
+        vx, vp, vd = _v(x), _v(p), _v(dout)
+        N, C, H, W = x.shape
+        dx = _new_like(x)
+        dp = zero_(_new_like(p))
+        lib.adr_mul_pixel_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vp[1]), vp[2],
+                              ctypes.c_void_p(vd[1]), vd[2], ctypes.c_void_p(dx.data_ptr()), C,
+                              ctypes.c_void_p(dp.data_ptr()), p.shape[1], N * H * W, C, stream())
+        return dx, dp
+
+
+def mul_pixel(x, p):
+    return MulPixelFn.apply(x, p)
+
+
+def detect_decode(feats, strides, nc, reg_max=16):
+    """Eval-branch decode of AYHead (head.py:1181-1204) -> y (B, 4+nc, A) fp32."""
+    vs = [_v(f) for f in feats]
+    B = feats[0].shape[0]
+    A = sum(f.shape[2] * f.shape[3] for f in feats)
+    y = torch.empty(B, 4 + nc, A, dtype=torch.float32, device=feats[0].device)
+    (f0, f1, f2) = vs
+    lib.adr_detect_decode(dcode(feats[0].dtype), ctypes.c_void_p(f0[1]), ctypes.c_void_p(f1[1]), ctypes.c_void_p(f2[1]),
+                          f0[2], f1[2], f2[2], feats[0].shape[2], feats[0].shape[3], feats[1].shape[2],
+                          feats[1].shape[3], feats[2].shape[2], feats[2].shape[3], float(strides[0]), float(strides[1]),
+                          float(strides[2]), B, nc, reg_max, fptr(y), stream())
+    return y

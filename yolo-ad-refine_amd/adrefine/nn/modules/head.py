@@ -1,0 +1,234 @@
+"""AYHead (alias of AYHead1) and its parts — HIP-backed drop-ins for the reference's
+ultralytics/nn/modules/head.py:600-1252 with identical class names, constructor signatures and parameter
+names (state_dict keys). Output contract (head.py:1178-1204, WENTI:71-88): train -> list of (B, no, H, W);
+eval -> (y (B, 4+nc, A) fp32, list) or y when `export`.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+import torch.nn as nn
+
+from ... import kernels as K
+from .block import DFL
+from .conv import Conv2d, autopad
+
+__all__ = ("Conv_GN", "TaskDecomposition", "CoordAtt", "CrossTaskInteraction", "DyDCNv2", "Scale", "ResidualBlockGN",
+           "AYHead1", "AYHead")
+
+
+class Conv_GN(nn.Module):  # noqa: N801
+    """Conv2d(no bias) -> GroupNorm(16) -> SiLU (head.py:607-620)."""
+
+    default_act = "silu"
+
+    def __init__(self, c1, c2, k=1, s=1, p=None, g=1, d=1, act=True):
+        super().__init__()
+        self.conv = Conv2d(c1, c2, k, s, autopad(k, p, d), groups=g, dilation=d, bias=False)
+        self.gn = nn.GroupNorm(16, c2)
+        self.act_name = "silu" if act is True else ("none" if act is False else act)
+
+    def forward(self, x):
+        y, _ = K.conv2d(x, self.conv.weight, None, self.conv.stride[0], self.conv.padding[0])
+        return K.gn_act(y, self.gn, self.act_name)
+
+
+class TaskDecomposition(nn.Module):
+    """Layer-attention gated 1x1 (head.py:626-669). With stacked_convs=1 the gate is one scalar per image, so
+    conv(feat, s_b * W) == s_b * conv(feat, W): run the shared 1x1 on the MFMA engine and scale per image."""
+
+    def __init__(self, feat_channels, stacked_convs, la_down_rate=8):
+        super().__init__()
+        self.feat_channels = feat_channels
+        self.stacked_convs = stacked_convs
+        self.in_channels = feat_channels * stacked_convs
+        self.la_conv1 = nn.Conv2d(self.in_channels, self.in_channels // la_down_rate, 1)
+        self.relu = nn.ReLU(inplace=True)
+        self.la_conv2 = nn.Conv2d(self.in_channels // la_down_rate, self.stacked_convs, 1, padding=0)
+        self.sigmoid = nn.Sigmoid()
+        self.reduction_conv = Conv_GN(self.in_channels, self.feat_channels, 1)
+        nn.init.normal_(self.la_conv1.weight.data, mean=0, std=0.001)
+        nn.init.normal_(self.la_conv2.weight.data, mean=0, std=0.001)
+        nn.init.zeros_(self.la_conv2.bias.data)
+        nn.init.normal_(self.reduction_conv.conv.weight.data, mean=0, std=0.01)
+
+    def forward(self, feat, avg_feat=None):
+        if self.stacked_convs != 1:
+            raise NotImplementedError("AYHead uses TaskDecomposition(stacked_convs=1)")
+        if avg_feat is None:
+            avg_feat = K.gap(feat)
+        s = K.gate_mlp(avg_feat, self.la_conv1.weight, self.la_conv1.bias, self.la_conv2.weight, self.la_conv2.bias,
+                       "relu", "sigmoid")  # (N, 1)
+        y, _ = K.conv2d(feat, self.reduction_conv.conv.weight, None, 1, 0)
+        y = K.scale(y, s.view(-1), "n")
+        return K.gn_act(y, self.reduction_conv.gn, "silu")
+
+
+class CoordAtt(nn.Module):
+    """Coordinate attention (head.py:671-707)."""
+
+    def __init__(self, inp, oup, reduction=32):
+        super().__init__()
+        mip = max(8, inp // reduction)
+        self.conv1 = Conv2d(inp, mip, kernel_size=1, stride=1, padding=0)
+        self.bn1 = nn.BatchNorm2d(mip, eps=1e-3, momentum=0.03)  # initialize_weights (torch_utils.py:430-432)
+        self.act = nn.Hardswish()
+        self.conv_h = Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
+        self.conv_w = Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
+
+    def forward(self, x):
+        y = K.axis_mean(x, "coord")  # (N, C, H+W, 1): [row means ; column means]
+        y, _ = K.conv2d(y, self.conv1.weight, self.conv1.bias, 1, 0)
+        y = K.bn_act(y, None, self.bn1, "hswish", self.training)
+        a_h = K.act(K.conv2d(y, self.conv_h.weight, self.conv_h.bias, 1, 0)[0], "sigmoid")
+        a_w = K.act(K.conv2d(y, self.conv_w.weight, self.conv_w.bias, 1, 0)[0], "sigmoid")
+        return K.gate(x, a_h, a_w, "coord", x.shape)
+
+
+class CrossTaskInteraction(nn.Module):
+    """head.py:722-747."""
+
+    def __init__(self, channels):
+        super().__init__()
+        self.cls_to_reg = Conv2d(channels, channels, 1)
+        self.reg_to_cls = Conv2d(channels, channels, 1)
+        self.cls_gate = nn.Sequential(Conv2d(channels * 2, channels, 1), nn.Sigmoid())
+        self.reg_gate = nn.Sequential(Conv2d(channels * 2, channels, 1), nn.Sigmoid())
+
+    def forward(self, cls_feat, reg_feat):
+        c2r = self.cls_to_reg(cls_feat)
+        r2c = self.reg_to_cls(reg_feat)
+        cg = K.act(self.cls_gate[0](K.cat([cls_feat, r2c])), "sigmoid")
+        rg = K.act(self.reg_gate[0](K.cat([reg_feat, c2r])), "sigmoid")
+        return K.fma(cls_feat, r2c, cg), K.fma(reg_feat, c2r, rg)
+
+
+class _DCNWeight(nn.Module):
+    """Parameter holder with mmcv ModulatedDeformConv2d's names (weight; bias absent when a norm follows)."""
+
+    def __init__(self, cin, cout, k=3):
+        super().__init__()
+        self.in_channels, self.out_channels, self.kernel_size = cin, cout, (k, k)
+        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        self.register_parameter("bias", None)
+        nn.init.uniform_(self.weight, -1.0 / math.sqrt(cin * k * k), 1.0 / math.sqrt(cin * k * k))
+
+
+class DyDCNv2(nn.Module):
+    """ModulatedDeformConv2d(3x3, s1, p1, no bias) + GroupNorm(16) (head.py:751-782)."""
+
+    def __init__(self, in_channels, out_channels, stride=1, norm_cfg=None):
+        super().__init__()
+        if stride != 1:
+            raise NotImplementedError("DyDCNv2 stride != 1 is not on the AYHead path")
+        self.with_norm = True
+        self.conv = _DCNWeight(in_channels, out_channels)
+        self.norm = nn.GroupNorm(16, out_channels)
+
+    def forward(self, x, om):
+        """`om`: the spatial_conv_offset output (offsets [0,18) and mask LOGITS [18,27); sigmoid fused)."""
+        return K.gn_act(K.dcn(x, om, self.conv.weight), self.norm, "none")
+
+
+class Scale(nn.Module):
+    """Learnable scalar (head.py:785-798)."""
+
+    def __init__(self, scale: float = 1.0):
+        super().__init__()
+        self.scale = nn.Parameter(torch.tensor(scale, dtype=torch.float))
+
+    def forward(self, x):
+        return K.scale(x, self.scale, "scalar")
+
+
+class ResidualBlockGN(nn.Module):
+    """head.py:1031-1047."""
+
+    def __init__(self, c1, c2, k=3, s=1, p=None, act=True):
+        super().__init__()
+        self.conv1 = Conv_GN(c1, c2, k, s, p=p, act=act)
+        self.conv2 = Conv_GN(c2, c2, k, s, p=p, act=act)
+        self.shortcut = nn.Identity() if c1 == c2 and s == 1 else Conv_GN(c1, c2, 1, s, act=False)
+
+    def forward(self, x):
+        res = x if isinstance(self.shortcut, nn.Identity) else self.shortcut(x)
+        return K.add(self.conv2(self.conv1(x)), res)
+
+
+class AYHead1(nn.Module):
+    """AD-Refine detection head (head.py:1049-1252)."""
+
+    dynamic = False
+    export = False
+    shape = None
+    anchors = torch.empty(0)
+    strides = torch.empty(0)
+    format = None
+
+    def __init__(self, nc=80, ch=()):
+        super().__init__()
+        self.nc = nc
+        self.nl = len(ch)
+        self.reg_max = 16
+        self.no = nc + self.reg_max * 4
+        self.stride = torch.zeros(self.nl)
+        self.ch = ch
+        hidc = max(ch) if ch else 512
+        task_ch = hidc // 2
+        self.stems = nn.ModuleList(Conv_GN(self.ch[i], hidc, 1) for i in range(self.nl))
+        self.share_conv = nn.Sequential(Conv_GN(hidc, task_ch, 3), Conv_GN(task_ch, task_ch, 3))
+        self.cls_decomp = TaskDecomposition(feat_channels=task_ch, stacked_convs=1, la_down_rate=16)
+        self.reg_decomp = TaskDecomposition(feat_channels=task_ch, stacked_convs=1, la_down_rate=16)
+        self.rep_block_cls = ResidualBlockGN(task_ch, task_ch)
+        self.coord_attention_reg = CoordAtt(task_ch, task_ch)
+        self.cross_task = CrossTaskInteraction(task_ch)
+        self.spatial_conv_offset = Conv2d(task_ch, 3 * 3 * 3, 3, padding=1)
+        self.offset_dim = 2 * 3 * 3
+        self.DyDCNV2 = DyDCNv2(task_ch, task_ch)
+        self.cls_prob_conv = nn.Sequential(Conv2d(task_ch, task_ch // 2, 1), nn.ReLU(),
+                                           Conv2d(task_ch // 2, 1, 3, padding=1), nn.Sigmoid())
+        self.cv2 = Conv2d(task_ch, 4 * self.reg_max, 1)
+        self.cv3 = Conv2d(task_ch, self.nc, 1)
+        self.scale = nn.ModuleList([Scale(1.0) for _ in range(self.nl)])
+        self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
+        self.initialize_biases()
+
+    def _level(self, x, i):
+        ax = self.stems[i](x)
+        feat = self.share_conv(ax)
+        avg = K.gap(feat)
+        cls_f = self.cls_decomp(feat, avg)
+        reg_f = self.reg_decomp(feat, avg)
+        cls_f, reg_f = self.cross_task(cls_f, reg_f)
+        cls_e = self.rep_block_cls(cls_f)
+        so = self.spatial_conv_offset
+        om = K.padded_conv2d(feat, so.weight, so.bias, 1, 1, 32)  # 27 channels padded to 32
+        r = self.DyDCNV2(reg_f, om)
+        r = self.coord_attention_reg(r)
+        c0, c2 = self.cls_prob_conv[0], self.cls_prob_conv[2]
+        cp = K.act(K.conv2d(feat, c0.weight, c0.bias, 1, 0)[0], "relu")
+        cp = K.act(K.padded_conv2d(cp, c2.weight, c2.bias, 1, 1, 8), "sigmoid")  # channel 0 valid
+        reg_out = self.scale[i](self.cv2(r))
+        cls_out = self.cv3(K.mul_pixel(cls_e, cp))
+        return K.cat([reg_out, cls_out])
+
+    def forward(self, x):
+        outputs = [self._level(x[i], i) for i in range(self.nl)]
+        if self.training:
+            return outputs
+        y = K.detect_decode(outputs, [float(s) for s in self.stride], self.nc, self.reg_max)
+        return y if self.export else (y, outputs)
+
+    def initialize_biases(self):
+        """head.py:1206-1228: default strides [8, 16, 32], cv2 bias 1.0, cv3 bias prior 0.01."""
+        if (self.stride == 0).all():
+            self.stride = torch.tensor([8, 16, 32, 64, 128][: self.nl], dtype=torch.float32)
+        self.cv2.bias.data.fill_(1.0)
+        self.cv3.bias.data.fill_(-math.log((1 - 0.01) / 0.01))
+
+    def bias_init(self):
+        self.initialize_biases()
+
+
+AYHead = AYHead1

@@ -1,0 +1,445 @@
+// AYHead-specific kernels (reference nn/modules/head.py:1049-1252):
+//   * modulated deformable im2col / col2im for DyDCNv2 (mmcv ModulatedDeformConv2d semantics, head.py:751-782):
+//       offset channel 2k = dy, 2k+1 = dx, mask logit channel 2K+k (sigmoid applied here, head.py:1156);
+//       sample (h - pad + i + dy, w - pad + j + dx); value 0 unless -1 < py < H and -1 < px < W; each bilinear
+//       corner bounds-checked. The GEMM halves (columns x W, dy x W^T, dy^T x columns) run on the MFMA engine.
+//   * tiny per-image gate MLPs on pooled vectors: TaskDecomposition la_conv1/la_conv2 (head.py:633-650) and
+//     AdaptiveDynamicTanh importance_gate (block.py:2521-2531), forward + backward.
+//   * broadcast fill (the adjoint of a global average pool) and per-pixel scalar multiply (cls_prob gate,
+//     head.py:1172).
+//   * detect decode for eval: DFL softmax-expectation + dist2bbox(xywh) * stride + sigmoid(cls)
+//     (head.py:1181-1204, 1236-1252; block.py:63-81; tal.py:303-327).
+#include "adr_common.h"
+
+namespace adr {
+
+// ---------------- DCNv2 ----------------
+// bilinear corner weights and validity for sample point (py, px); corners (y0,x0),(y0,x0+1),(y0+1,x0),(y0+1,x0+1)
+__device__ __forceinline__ bool dcn_sample(float py, float px, int H, int W, int& y0, int& x0, float* wts, bool* v) {
+  float fy = floorf(py), fx = floorf(px);
+  y0 = (int)fy;
+  x0 = (int)fx;
+  float ly = py - fy, lx = px - fx, hy = 1.f - ly, hx = 1.f - lx;
+  bool inside = (py > -1.f) && (px > -1.f) && (py < (float)H) && (px < (float)W);
+  v[0] = inside && y0 >= 0 && x0 >= 0;
+  v[1] = inside && y0 >= 0 && x0 + 1 <= W - 1;
+  v[2] = inside && y0 + 1 <= H - 1 && x0 >= 0;
+  v[3] = inside && y0 + 1 <= H - 1 && x0 + 1 <= W - 1;
+  wts[0] = v[0] ? hy * hx : 0.f;
+  wts[1] = v[1] ? hy * lx : 0.f;
+  wts[2] = v[2] ? ly * hx : 0.f;
+  wts[3] = v[3] ? ly * lx : 0.f;
+  return inside;
+}
+
+// cols[pix][t][c] = mask * bilinear(x, p); thread per (pix, tap, channel-vector)
+template <typename T>
+__global__ void __launch_bounds__(256) dcn_im2col_kernel(const T* x, int xcs, const T* om, int omcs, T* cols, int N,
+                                                         int H, int W, int C) {
+  constexpr int V = 16 / sizeof(T);
+  const int G = C / V;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)N * H * W * 9 * G;
+  if (i >= total) return;
+  int g = (int)(i % G);
+  long r = i / G;
+  int t = (int)(r % 9);
+  long pix = r / 9;
+  int w = (int)(pix % W);
+  long r2 = pix / W;
+  int h = (int)(r2 % H);
+  int n = (int)(r2 / H);
+  const T* o = om + pix * omcs;
+  float dy = to_f(o[2 * t]), dx = to_f(o[2 * t + 1]);
+  float m = 1.f / (1.f + __expf(-to_f(o[18 + t])));
+  float py = (float)(h - 1 + t / 3) + dy, px = (float)(w - 1 + t % 3) + dx;
+  int y0, x0;
+  float wt[4];
+  bool vq[4];
+  dcn_sample(py, px, H, W, y0, x0, wt, vq);
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  const T* xb = x + (long)n * H * W * xcs + g * V;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if (!vq[q]) continue;
+    int yy = y0 + (q >> 1), xx = x0 + (q & 1);
+    u32x4 v = ld16(xb + ((long)yy * W + xx) * xcs);
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int k = 0; k < V; ++k) acc[k] += wt[q] * to_f(e[k]);
+  }
+  u32x4 ov;
+  T* oe = reinterpret_cast<T*>(&ov);
+#pragma unroll
+  for (int k = 0; k < V; ++k) oe[k] = from_f<T>(acc[k] * m);
+  st16(cols + (pix * 9 + t) * C + g * V, ov);
+}
+
+// thread per (pix, tap): d_offset, d_mask_logit; atomics of dval into dx32 (fp32, NHWC dense N*H*W*C)
+template <typename T>
+__global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, const T* om, int omcs, const T* dcols,
+                                                         float* dx32, T* dom, int domcs, int N, int H, int W, int C) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)N * H * W * 9;
+  if (i >= total) return;
+  int t = (int)(i % 9);
+  long pix = i / 9;
+  int w = (int)(pix % W);
+  long r2 = pix / W;
+  int h = (int)(r2 % H);
+  int n = (int)(r2 / H);
+  const T* o = om + pix * omcs;
+  float oy = to_f(o[2 * t]), ox = to_f(o[2 * t + 1]);
+  float m = 1.f / (1.f + __expf(-to_f(o[18 + t])));
+  float py = (float)(h - 1 + t / 3) + oy, px = (float)(w - 1 + t % 3) + ox;
+  int y0, x0;
+  float wt[4];
+  bool ok[4];
+  bool inside = dcn_sample(py, px, H, W, y0, x0, wt, ok);
+  float ly = py - floorf(py), lx = px - floorf(px);
+  // d weight / d py and d px for each corner (mmcv dmcn_get_coordinate_weight)
+  float dwy[4] = {-(1.f - lx), -lx, (1.f - lx), lx};
+  float dwx[4] = {-(1.f - ly), (1.f - ly), -ly, ly};
+  const T* xb = x + (long)n * H * W * xcs;
+  const T* dc = dcols + (pix * 9 + t) * C;
+  float dmask = 0.f, dpy = 0.f, dpx = 0.f;
+  for (int c = 0; c < C; ++c) {
+    float g = to_f(dc[c]);
+    if (g == 0.f) continue;
+    float val = 0.f, sy = 0.f, sx = 0.f;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      if (!ok[q]) continue;
+      int yy = y0 + (q >> 1), xx = x0 + (q & 1);
+      long off = ((long)yy * W + xx);
+      float v = to_f(xb[off * xcs + c]);
+      val += wt[q] * v;
+      sy += dwy[q] * v;
+      sx += dwx[q] * v;
+      atomicAdd(dx32 + ((long)n * H * W + off) * C + c, g * m * wt[q]);
+    }
+    dmask += g * val;
+    dpy += g * m * sy;
+    dpx += g * m * sx;
+  }
+  T* d = dom + pix * domcs;
+  d[2 * t] = from_f<T>(inside ? dpy : 0.f);
+  d[2 * t + 1] = from_f<T>(inside ? dpx : 0.f);
+  d[18 + t] = from_f<T>(dmask * m * (1.f - m));
+}
+
+// W (Cout, C, 3, 3) fp32 -> W^T as a 1x1-conv weight [(t*C + c)][co] in dtype
+template <typename T>
+__global__ void dcn_wT_kernel(const float* w, T* out, int Cout, int C) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)Cout * C * 9;
+  if (i >= total) return;
+  int co = (int)(i % Cout);
+  long r = i / Cout;  // r = t*C + c
+  int c = (int)(r % C);
+  int t = (int)(r / C);
+  out[i] = from_f<T>(w[((long)co * C + c) * 9 + t]);
+}
+
+// ---------------- tiny gate MLP: out = act2(W2 act1(W1 (in*scale) + b1) + b2) per image ----------------
+// act: 0 none, 3 relu, 4 sigmoid, 6 softmax (over the output vector)
+__device__ __forceinline__ float gact(int a, float v) {
+  if (a == 3) return v > 0.f ? v : 0.f;
+  if (a == 4) return 1.f / (1.f + __expf(-v));
+  return v;
+}
+
+__global__ void __launch_bounds__(256) gate_mlp_kernel(const float* in, float in_scale, int Cin, const float* W1,
+                                                       const float* b1, int H1, int act1, const float* W2,
+                                                       const float* b2, int H2, int act2, float* hidden, float* out) {
+  int n = blockIdx.x;
+  extern __shared__ float sm[];
+  float* xin = sm;            // Cin
+  float* hid = sm + Cin;      // H1
+  float* o = sm + Cin + H1;   // H2
+  for (int c = threadIdx.x; c < Cin; c += 256) xin[c] = in[(long)n * Cin + c] * in_scale;
+  __syncthreads();
+  for (int j = threadIdx.x; j < H1; j += 256) {
+    float s = b1 ? b1[j] : 0.f;
+    for (int c = 0; c < Cin; ++c) s += W1[(long)j * Cin + c] * xin[c];
+    hid[j] = gact(act1, s);
+    hidden[(long)n * H1 + j] = hid[j];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < H2; j += 256) {
+    float s = b2 ? b2[j] : 0.f;
+    for (int c = 0; c < H1; ++c) s += W2[(long)j * H1 + c] * hid[c];
+    o[j] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (act2 == 6) {
+      float mx = -INFINITY;
+      for (int j = 0; j < H2; ++j) mx = fmaxf(mx, o[j]);
+      float z = 0.f;
+      for (int j = 0; j < H2; ++j) z += __expf(o[j] - mx);
+      for (int j = 0; j < H2; ++j) out[(long)n * H2 + j] = __expf(o[j] - mx) / z;
+    } else {
+      for (int j = 0; j < H2; ++j) out[(long)n * H2 + j] = gact(act2, o[j]);
+    }
+  }
+}
+
+// backward: given dout (N,H2) -> din (N,Cin) (times in_scale), per-image partial dW1/db1/dW2/db2 summed in-kernel
+// over images by a single block (N small, deterministic order).
+__global__ void __launch_bounds__(256) gate_mlp_bwd_kernel(const float* in, float in_scale, int Cin, const float* W1,
+                                                           int H1, int act1, const float* W2, int H2, int act2,
+                                                           const float* hidden, const float* out, const float* dout,
+                                                           int N, float* din, float* dW1, float* db1, float* dW2,
+                                                           float* db2) {
+  extern __shared__ float sm[];
+  float* dz2 = sm;        // H2
+  float* dh = sm + H2;    // H1
+  // zero weight grads
+  for (int i = threadIdx.x; i < H1 * Cin; i += 256) dW1[i] = 0.f;
+  for (int i = threadIdx.x; i < H1; i += 256) db1[i] = 0.f;
+  for (int i = threadIdx.x; i < H2 * H1; i += 256) dW2[i] = 0.f;
+  for (int i = threadIdx.x; i < H2; i += 256) db2[i] = 0.f;
+  __syncthreads();
+  for (int n = 0; n < N; ++n) {
+    const float* o = out + (long)n * H2;
+    const float* d = dout + (long)n * H2;
+    if (threadIdx.x == 0) {
+      if (act2 == 6) {
+        float dot = 0.f;
+        for (int j = 0; j < H2; ++j) dot += d[j] * o[j];
+        for (int j = 0; j < H2; ++j) dz2[j] = o[j] * (d[j] - dot);
+      } else if (act2 == 4) {
+        for (int j = 0; j < H2; ++j) dz2[j] = d[j] * o[j] * (1.f - o[j]);
+      } else {
+        for (int j = 0; j < H2; ++j) dz2[j] = d[j];
+      }
+    }
+    __syncthreads();
+    const float* hid = hidden + (long)n * H1;
+    for (int c = threadIdx.x; c < H1; c += 256) {
+      float s = 0.f;
+      for (int j = 0; j < H2; ++j) {
+        s += W2[(long)j * H1 + c] * dz2[j];
+        dW2[(long)j * H1 + c] += dz2[j] * hid[c];
+      }
+      float hv = hid[c];
+      dh[c] = (act1 == 3) ? (hv > 0.f ? s : 0.f) : (act1 == 4 ? s * hv * (1.f - hv) : s);
+    }
+    for (int j = threadIdx.x; j < H2; j += 256) db2[j] += dz2[j];
+    __syncthreads();
+    const float* xin = in + (long)n * Cin;
+    for (int c = threadIdx.x; c < Cin; c += 256) {
+      float s = 0.f;
+      for (int j = 0; j < H1; ++j) {
+        s += W1[(long)j * Cin + c] * dh[j];
+        dW1[(long)j * Cin + c] += dh[j] * xin[c] * in_scale;
+      }
+      din[(long)n * Cin + c] = s * in_scale;
+    }
+    for (int j = threadIdx.x; j < H1; j += 256) db1[j] += dh[j];
+    __syncthreads();
+  }
+}
+
+// o[n, pix, c] (+)= g[n*gns + c*gcs] * s
+template <typename T>
+__global__ void __launch_bounds__(256) bcast_fill_kernel(const float* g, int gns, int gcs, float s, T* o, int ocs,
+                                                         long npix, int HW, int C, int accumulate) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = npix * C;
+  if (i >= total) return;
+  int c = (int)(i % C);
+  long pix = i / C;
+  int n = (int)(pix / HW);
+  float v = g[(long)n * gns + (long)c * gcs] * s;
+  T* q = o + pix * ocs + c;
+  *q = from_f<T>(accumulate ? to_f(*q) + v : v);
+}
+
+// o = x * p[pix] (p: channel 0 of a view) ; bwd: dx = dout*p ; dp[pix] = sum_c dout*x
+template <typename T>
+__global__ void __launch_bounds__(256) mul_pixel_kernel(const T* x, int xcs, const T* p, int pcs, T* o, int ocs,
+                                                        long npix, int C) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix * C) return;
+  int c = (int)(i % C);
+  long pix = i / C;
+  o[pix * ocs + c] = from_f<T>(to_f(x[pix * xcs + c]) * to_f(p[pix * pcs]));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) mul_pixel_bwd_kernel(const T* x, int xcs, const T* p, int pcs, const T* dout,
+                                                            int dcs, T* dx, int ocs, T* dp, int dpcs, long npix, int C) {
+  long pix = (long)blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+  int lane = threadIdx.x & 63;
+  if (pix >= npix) return;
+  float pv = to_f(p[pix * pcs]);
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) {
+    float d = to_f(dout[pix * dcs + c]);
+    s += d * to_f(x[pix * xcs + c]);
+    dx[pix * ocs + c] = from_f<T>(d * pv);
+  }
+  s = wave_sum(s);
+  if (lane == 0) dp[pix * dpcs] = from_f<T>(s);
+}
+
+// ---------------- eval decode ----------------
+// feats: nl NHWC tensors (B, no, H_i, W_i) of dtype T; y (B, 4+nc, A) fp32
+template <typename T>
+__global__ void __launch_bounds__(256) detect_decode_kernel(const T* f0, const T* f1, const T* f2, int cs0, int cs1,
+                                                            int cs2, int H0, int W0, int H1, int W1, int H2, int W2,
+                                                            float s0, float s1, float s2, int B, int nc, int reg_max,
+                                                            float* y) {
+  int A = H0 * W0 + H1 * W1 + H2 * W2;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * A) return;
+  int a = (int)(i % A);
+  int b = (int)(i / A);
+  const T* f;
+  int cs, W, HW, loc;
+  float st;
+  if (a < H0 * W0) { f = f0; cs = cs0; W = W0; HW = H0 * W0; loc = a; st = s0; }
+  else if (a < H0 * W0 + H1 * W1) { f = f1; cs = cs1; W = W1; HW = H1 * W1; loc = a - H0 * W0; st = s1; }
+  else { f = f2; cs = cs2; W = W2; HW = H2 * W2; loc = a - H0 * W0 - H1 * W1; st = s2; }
+  const T* p = f + ((long)b * HW + loc) * cs;
+  float ax = (float)(loc % W) + 0.5f, ay = (float)(loc / W) + 0.5f;
+  float d[4];
+  for (int k = 0; k < 4; ++k) {
+    float mx = -INFINITY;
+    for (int j = 0; j < reg_max; ++j) mx = fmaxf(mx, to_f(p[k * reg_max + j]));
+    float z = 0.f, e = 0.f;
+    for (int j = 0; j < reg_max; ++j) {
+      float ex = __expf(to_f(p[k * reg_max + j]) - mx);
+      z += ex;
+      e += ex * (float)j;
+    }
+    d[k] = e / z;
+  }
+  float x1 = ax - d[0], y1 = ay - d[1], x2 = ax + d[2], y2 = ay + d[3];
+  long base = (long)b * (4 + nc) * A + a;
+  y[base] = (x1 + x2) * 0.5f * st;
+  y[base + A] = (y1 + y2) * 0.5f * st;
+  y[base + 2L * A] = (x2 - x1) * st;
+  y[base + 3L * A] = (y2 - y1) * st;
+  for (int c = 0; c < nc; ++c) y[base + (long)(4 + c) * A] = 1.f / (1.f + __expf(-to_f(p[4 * reg_max + c])));
+}
+
+}  // namespace adr
+
+using namespace adr;
+
+extern "C" int adr_dcn_im2col(int dtype, const void* x, int xcs, const void* om, int omcs, void* cols, int N, int H,
+                              int W, int C, void* stream) {
+  int v = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % v == 0 && xcs % v == 0, "dcn_im2col: C=%d", C);
+  ADR_REQUIRE(omcs >= 27, "dcn_im2col: offset/mask tensor needs >= 27 channels");
+  long total = (long)N * H * W * 9 * (C / v);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(dcn_im2col_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)x, xcs,
+                       (const __bf16*)om, omcs, (__bf16*)cols, N, H, W, C);
+  else
+    hipLaunchKernelGGL(dcn_im2col_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)x, xcs,
+                       (const float*)om, omcs, (float*)cols, N, H, W, C);
+  return check_launch("adr_dcn_im2col");
+}
+
+extern "C" int adr_dcn_col2im(int dtype, const void* x, int xcs, const void* om, int omcs, const void* dcols,
+                              float* dx32, void* dom, int domcs, int N, int H, int W, int C, void* stream) {
+  long total = (long)N * H * W * 9;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(dcn_col2im_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)x, xcs,
+                       (const __bf16*)om, omcs, (const __bf16*)dcols, dx32, (__bf16*)dom, domcs, N, H, W, C);
+  else
+    hipLaunchKernelGGL(dcn_col2im_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)x, xcs,
+                       (const float*)om, omcs, (const float*)dcols, dx32, (float*)dom, domcs, N, H, W, C);
+  return check_launch("adr_dcn_col2im");
+}
+
+extern "C" int adr_dcn_weight_t(int dtype, const float* w, void* out, int Cout, int C, void* stream) {
+  long total = (long)Cout * C * 9;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(dcn_wT_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, w, (__bf16*)out, Cout, C);
+  else
+    hipLaunchKernelGGL(dcn_wT_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, w, (float*)out, Cout, C);
+  return check_launch("adr_dcn_weight_t");
+}
+
+extern "C" int adr_gate_mlp(const float* in, float in_scale, int N, int Cin, const float* W1, const float* b1, int H1,
+                            int act1, const float* W2, const float* b2, int H2, int act2, float* hidden, float* out,
+                            void* stream) {
+  size_t sm = (Cin + H1 + H2) * sizeof(float);
+  hipLaunchKernelGGL(gate_mlp_kernel, dim3(N), dim3(256), sm, (hipStream_t)stream, in, in_scale, Cin, W1, b1, H1, act1,
+                     W2, b2, H2, act2, hidden, out);
+  return check_launch("adr_gate_mlp");
+}
+
+extern "C" int adr_gate_mlp_bwd(const float* in, float in_scale, int N, int Cin, const float* W1, int H1, int act1,
+                                const float* W2, int H2, int act2, const float* hidden, const float* out,
+                                const float* dout, float* din, float* dW1, float* db1, float* dW2, float* db2,
+                                void* stream) {
+  size_t sm = (H1 + H2) * sizeof(float);
+  hipLaunchKernelGGL(gate_mlp_bwd_kernel, dim3(1), dim3(256), sm, (hipStream_t)stream, in, in_scale, Cin, W1, H1, act1,
+                     W2, H2, act2, hidden, out, dout, N, din, dW1, db1, dW2, db2);
+  return check_launch("adr_gate_mlp_bwd");
+}
+
+extern "C" int adr_bcast_fill(int dtype, const float* g, int gns, int gcs, float s, void* o, int ocs, int N, int HW,
+                              int C, int accumulate, void* stream) {
+  long npix = (long)N * HW;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(bcast_fill_kernel<__bf16>, dim3(cdiv(npix * C, 256)), dim3(256), 0, st, g, gns, gcs, s,
+                       (__bf16*)o, ocs, npix, HW, C, accumulate);
+  else
+    hipLaunchKernelGGL(bcast_fill_kernel<float>, dim3(cdiv(npix * C, 256)), dim3(256), 0, st, g, gns, gcs, s,
+                       (float*)o, ocs, npix, HW, C, accumulate);
+  return check_launch("adr_bcast_fill");
+}
+
+extern "C" int adr_mul_pixel(int dtype, const void* x, int xcs, const void* p, int pcs, void* o, int ocs, long npix,
+                             int C, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(mul_pixel_kernel<__bf16>, dim3(cdiv(npix * C, 256)), dim3(256), 0, st, (const __bf16*)x, xcs,
+                       (const __bf16*)p, pcs, (__bf16*)o, ocs, npix, C);
+  else
+    hipLaunchKernelGGL(mul_pixel_kernel<float>, dim3(cdiv(npix * C, 256)), dim3(256), 0, st, (const float*)x, xcs,
+                       (const float*)p, pcs, (float*)o, ocs, npix, C);
+  return check_launch("adr_mul_pixel");
+}
+
+extern "C" int adr_mul_pixel_bwd(int dtype, const void* x, int xcs, const void* p, int pcs, const void* dout, int dcs,
+                                 void* dx, int ocs, void* dp, int dpcs, long npix, int C, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g(cdiv(npix, 4));
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(mul_pixel_bwd_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)p, pcs,
+                       (const __bf16*)dout, dcs, (__bf16*)dx, ocs, (__bf16*)dp, dpcs, npix, C);
+  else
+    hipLaunchKernelGGL(mul_pixel_bwd_kernel<float>, g, dim3(256), 0, st, (const float*)x, xcs, (const float*)p, pcs,
+                       (const float*)dout, dcs, (float*)dx, ocs, (float*)dp, dpcs, npix, C);
+  return check_launch("adr_mul_pixel_bwd");
+}
+
+extern "C" int adr_detect_decode(int dtype, const void* f0, const void* f1, const void* f2, int cs0, int cs1, int cs2,
+                                 int H0, int W0, int H1, int W1, int H2, int W2, float s0, float s1, float s2, int B,
+                                 int nc, int reg_max, float* y, void* stream) {
+  long total = (long)B * (H0 * W0 + H1 * W1 + H2 * W2);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(detect_decode_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)f0,
+                       (const __bf16*)f1, (const __bf16*)f2, cs0, cs1, cs2, H0, W0, H1, W1, H2, W2, s0, s1, s2, B, nc,
+                       reg_max, y);
+  else
+    hipLaunchKernelGGL(detect_decode_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)f0,
+                       (const float*)f1, (const float*)f2, cs0, cs1, cs2, H0, W0, H1, W1, H2, W2, s0, s1, s2, B, nc,
+                       reg_max, y);
+  return check_launch("adr_detect_decode");
+}
