@@ -203,6 +203,52 @@ int adr_detect_decode(int dtype, const void* f0, const void* f1, const void* f2,
                       int W0, int H1, int W1, int H2, int W2, float s0, float s1, float s2, int B, int nc, int reg_max,
                       float* y, void* stream);
 
+/* ---------------------------------------------------------------------------------------------------------
+ * C2PTSSA (nn/modules/block.py:2376-2710).
+ * Depthwise k x k conv + bias, stride 1, pad k/2 (ProgressiveFeatureFusion :2589-2593, EDFFN :2387);
+ * weights (C, 1, k, k) fp32. dw / dx may be NULL to skip. */
+int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w, const float* b, void* y, int ycs, int N, int H,
+                   int W, int C, int k, void* stream);
+size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k);
+int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* w, void* dx, int ocs,
+                   float* dw, int N, int H, int W, int C, int k, int accumulate, float* ws, size_t ws_bytes,
+                   void* stream);
+/* AdaptiveDynamicTanh (:2493-2577): y = (sum_i tanh(alpha_i x) imp[n,i]) * w[c] + b[c]; imp from adr_gate_mlp. */
+int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alphas, const float* imp, const float* w,
+                 const float* b, void* y, int ycs, int N, int HW, int C, void* stream);
+size_t adr_adyt_bwd_workspace(int N, int HW, int C);
+int adr_adyt_bwd(int dtype, const void* x, int xcs, const void* dout, int dcs, const float* alphas, const float* imp,
+                 const float* w, void* dx, int ocs, float* dimp, float* dalpha, float* dw, float* db, int N, int HW,
+                 int C, float* ws, size_t ws_bytes, void* stream);
+/* TSSA token statistics for one scale (:2465-2477): q/k/v rows [b*Ntok + n] with channel stride cs, head h at
+ * channels [h*D, (h+1)*D); out row of (b, n) is b*oimg + n (so the 3 scales stack into one buffer as
+ * torch.stack(dim=1) does). Saves Pi/ss [B][heads][Ntok], attn [B][heads][D]. */
+int adr_tssa_fwd(int dtype, const void* q, const void* k, const void* v, int cs, int B, int Ntok, int heads, int D,
+                 const float* temp, void* out, int ocs, int oimg, float* Pi, float* ss, float* attn, void* stream);
+int adr_tssa_bwd(int dtype, const void* q, const void* k, const void* v, int cs, int B, int Ntok, int heads, int D,
+                 const float* temp, const void* dout, int dcs, int dimg, const float* Pi, const float* ss,
+                 const float* attn, void* dq, void* dk, void* dv, int gcs, float* dtemp, float* ws, void* stream);
+/* mean over S stacked token groups (fused_features.view(B, S, HW, C).mean(1), :2484-2486); backward spreads. */
+int adr_group_mean(int dtype, const void* x, int xcs, int S, int HW, void* y, int ycs, int B, int C, int backward,
+                   void* stream);
+/* EDFFN 8x8-patch rfft2 * fft -> irfft2 (:2399-2413) as M_c = sum_uv fft[c,uv] basis[uv] (64x64, fp32). */
+int adr_edffn_build(const float* w, const float* basis, int C, int nuv, float* M, void* stream);
+int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, void* y, int ycs, int N, int H, int W, int C,
+                  void* stream);
+size_t adr_edffn_bwd_workspace(int N, int H, int W, int C);
+int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* M, const float* basis,
+                  int nuv, void* dx, int ocs, float* dw, int N, int H, int W, int C, float* ws, size_t ws_bytes,
+                  void* stream);
+/* Flash attention, head_dim 64 (nn.MultiheadAttention core in CrossScaleAttentionTSSA, :2432/:2484):
+ * o = softmax(q k^T * scale) v per (image, head); rows [b*L + l], channel strides cs / ocs, q/k/v channel
+ * offsets qo/ko/vo (+ h*64). lse [B][heads][L] (natural log) is saved for the backward. */
+int adr_attn_fwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo, void* o,
+                 int ocs, int B, int L, int heads, int head_dim, float scale, float* lse, void* stream);
+int adr_attn_bwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo,
+                 const void* o, int ocs, const void* dout, int dcs, const float* lse, void* dq, void* dk, void* dv,
+                 int gcs, int gqo, int gko, int gvo, int B, int L, int heads, int head_dim, float scale,
+                 float* dvec_ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -103,3 +103,9 @@ def test_ayhead_train(dtype):
     m = AYHead(80, [128, 128, 128])
     m.stride = torch.tensor([8.0, 16.0, 32.0])
     run_fixture("ayhead", m, dtype, list_input=True)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c2ptssa(dtype):
+    from adrefine.nn.modules.block import C2PTSSA
+    run_fixture("c2ptssa", C2PTSSA(256, 256, 1), dtype)

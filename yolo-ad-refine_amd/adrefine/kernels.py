@@ -1122,3 +1122,344 @@ def detect_decode(feats, strides, nc, reg_max=16):
                           feats[1].shape[3], feats[2].shape[2], feats[2].shape[3], float(strides[0]), float(strides[1]),
                           float(strides[2]), B, nc, reg_max, fptr(y), stream())
     return y
+
+
+# ---------------------------------------------------------------------------------------------------------
+# C2PTSSA helpers
+# ---------------------------------------------------------------------------------------------------------
+
+
+class DWConvFn(torch.autograd.Function):
+    """Depthwise k x k conv (groups = C), stride 1, pad k//2, optional bias."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, k):
+        vx = _v(x)
+        N, C, H, W = x.shape
+        wf = w.detach().float().contiguous()
+        bf = b.detach().float().contiguous() if b is not None else None
+        y = _new_like(vx[0])
+        lib.adr_dwconv_fwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], fptr(wf), fptr(bf),
+                           ctypes.c_void_p(y.data_ptr()), C, N, H, W, C, k, stream())
+        ctx.save_for_backward(vx[0], wf)
+        ctx.meta = (k, w.shape, b is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wf = ctx.saved_tensors
+        k, wshape, has_b = ctx.meta
+        N, C, H, W = x.shape
+        vx, vd = _v(x), _v(dy)
+        dx = _new_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty(C * k * k, dtype=torch.float32, device=x.device) if ctx.needs_input_grad[1] else None
+        wsb = lib.adr_dwconv_wgrad_workspace(N, H, W, C, k)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=x.device)
+        lib.adr_dwconv_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]), vd[2], fptr(wf),
+                           ctypes.c_void_p(dx.data_ptr()) if dx is not None else None, C, fptr(dw), N, H, W, C, k, 0,
+                           fptr(ws), wsb, stream())
+        db = _bias_grad(vd[0], C, N, H * W, vd[2]) if has_b and ctx.needs_input_grad[2] else None
+        return dx, (dw.view(wshape) if dw is not None else None), db, None
+
+
+def dwconv(x, w, b, k):
+    return DWConvFn.apply(x, w, b, k)
+
+
+class ADyTFn(torch.autograd.Function):
+    """AdaptiveDynamicTanh apply (block.py:2547-2575) given the softmax importance imp (N, 3)."""
+
+    @staticmethod
+    def forward(ctx, x, alphas, imp, w, b):
+        vx = _v(x)
+        N, C, H, W = x.shape
+        a = alphas.detach().float().contiguous().view(-1)
+        im = imp.detach().float().contiguous()
+        wf, bf = w.detach().float().contiguous(), b.detach().float().contiguous()
+        y = _new_like(vx[0])
+        lib.adr_adyt_fwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], fptr(a), fptr(im), fptr(wf), fptr(bf),
+                         ctypes.c_void_p(y.data_ptr()), C, N, H * W, C, stream())
+        ctx.save_for_backward(vx[0], a, im, wf)
+        ctx.ashape = alphas.shape
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, a, im, wf = ctx.saved_tensors
+        N, C, H, W = x.shape
+        vx, vd = _v(x), _v(dy)
+        dev = x.device
+        dx = _new_like(x)
+        dimp = torch.empty(N, 3, dtype=torch.float32, device=dev)
+        da = torch.empty(3, dtype=torch.float32, device=dev)
+        dw = torch.empty(C, dtype=torch.float32, device=dev)
+        db = torch.empty(C, dtype=torch.float32, device=dev)
+        wsb = lib.adr_adyt_bwd_workspace(N, H * W, C)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
+        lib.adr_adyt_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]), vd[2], fptr(a), fptr(im),
+                         fptr(wf), ctypes.c_void_p(dx.data_ptr()), C, fptr(dimp), fptr(da), fptr(dw), fptr(db), N,
+                         H * W, C, fptr(ws), wsb, stream())
+        return dx, da.view(ctx.ashape), dimp, dw, db
+
+
+def adyt(x, alphas, imp, w, b):
+    return ADyTFn.apply(x, alphas, imp, w, b)
+
+
+def tokens(x):
+    """(B, C, H, W) NHWC -> (B, C, H*W, 1) NHWC token view (same memory)."""
+    B, C, H, W = x.shape
+    t, _, cs = _v(x)
+    if cs != C:
+        t = t.contiguous(memory_format=torch.channels_last)
+        relayout_count[0] += 1
+    return t.as_strided((B, C, H * W, 1), (H * W * C, 1, C, C))
+
+
+def untokens(t, H, W):
+    B, C, N, _ = t.shape
+    t, _, cs = _v(t)
+    if cs != C:
+        t = t.contiguous(memory_format=torch.channels_last)
+        relayout_count[0] += 1
+    return t.as_strided((B, C, H, W), (H * W * C, 1, W * C, C))
+
+
+class TSSAStackFn(torch.autograd.Function):
+    """Per-scale TSSA (block.py:2465-2477) for S scales, written stacked as (B, C, S*N, 1) tokens
+    (torch.stack(scale_features, 1).view(B, S*N, C), :2482-2484)."""
+
+    @staticmethod
+    def forward(ctx, temps, heads, *qkvs):
+        S = len(qkvs)
+        B, C3, N, _ = qkvs[0].shape
+        C = C3 // 3
+        D = C // heads
+        dtype = qkvs[0].dtype
+        dev = qkvs[0].device
+        out = empty_act(B, C, S * N, 1, dtype, dev)
+        tf = temps.detach().float().contiguous().view(S, heads)
+        Pi = torch.empty(S, B, heads, N, dtype=torch.float32, device=dev)
+        ss = torch.empty_like(Pi)
+        att = torch.empty(S, B, heads, D, dtype=torch.float32, device=dev)
+        es = out.element_size()
+        saved = []
+        for s, qkv in enumerate(qkvs):
+            t, p, cs = _v(qkv)
+            saved.append(t)
+            lib.adr_tssa_fwd(dcode(dtype), ctypes.c_void_p(p), ctypes.c_void_p(p + C * es), ctypes.c_void_p(p + 2 * C * es),
+                             cs, B, N, heads, D, fptr(tf[s]), ctypes.c_void_p(out.data_ptr() + s * N * C * es), C,
+                             S * N, fptr(Pi[s]), fptr(ss[s]), fptr(att[s]), stream())
+        ctx.save_for_backward(tf, Pi, ss, att, *saved)
+        ctx.meta = (heads, temps.shape)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        tf, Pi, ss, att, *qkvs = ctx.saved_tensors
+        heads, tshape = ctx.meta
+        S = len(qkvs)
+        B, C3, N, _ = qkvs[0].shape
+        C, D = C3 // 3, C3 // 3 // heads
+        dtype = qkvs[0].dtype
+        dev = qkvs[0].device
+        dd, ddp, dcs = _v(dout)
+        es = dd.element_size()
+        dtemp = torch.empty(S, heads, dtype=torch.float32, device=dev)
+        ws = torch.empty(B * heads, dtype=torch.float32, device=dev)
+        grads = []
+        for s, qkv in enumerate(qkvs):
+            _, p, cs = _v(qkv)
+            g = empty_act(B, C3, N, 1, dtype, dev)
+            gp = g.data_ptr()
+            lib.adr_tssa_bwd(dcode(dtype), ctypes.c_void_p(p), ctypes.c_void_p(p + C * es), ctypes.c_void_p(p + 2 * C * es),
+                             cs, B, N, heads, D, fptr(tf[s]), ctypes.c_void_p(ddp + s * N * C * es), dcs, S * N,
+                             fptr(Pi[s]), fptr(ss[s]), fptr(att[s]), ctypes.c_void_p(gp), ctypes.c_void_p(gp + C * es),
+                             ctypes.c_void_p(gp + 2 * C * es), C3, fptr(dtemp[s]), fptr(ws), stream())
+            grads.append(g)
+        return (dtemp.view(tshape), None, *grads)
+
+
+def tssa_stack(temps, heads, qkvs):
+    return TSSAStackFn.apply(temps, heads, *qkvs)
+
+
+class AttnFn(torch.autograd.Function):
+    """softmax(q k^T / sqrt(d)) v for the packed in_proj output qkv (B, 3E, L, 1) -> (B, E, L, 1)."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads):
+        t, p, cs = _v(qkv)
+        B, C3, L, _ = qkv.shape
+        E = C3 // 3
+        hd = E // heads
+        o = empty_act(B, E, L, 1, qkv.dtype, qkv.device)
+        lse = torch.empty(B * heads * L, dtype=torch.float32, device=qkv.device)
+        lib.adr_attn_fwd(dcode(qkv.dtype), ctypes.c_void_p(p), ctypes.c_void_p(p), ctypes.c_void_p(p), cs, 0, E, 2 * E,
+                         ctypes.c_void_p(o.data_ptr()), E, B, L, heads, hd, float(hd ** -0.5), fptr(lse), stream())
+        ctx.save_for_backward(t, o, lse)
+        ctx.heads = heads
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        t, o, lse = ctx.saved_tensors
+        heads = ctx.heads
+        _, p, cs = _v(t)
+        dd, ddp, dcs = _v(do)
+        B, C3, L, _ = t.shape
+        E = C3 // 3
+        hd = E // heads
+        g = empty_act(B, C3, L, 1, t.dtype, t.device)
+        dvec = torch.empty(B * heads * L, dtype=torch.float32, device=t.device)
+        gp = g.data_ptr()
+        lib.adr_attn_bwd(dcode(t.dtype), ctypes.c_void_p(p), ctypes.c_void_p(p), ctypes.c_void_p(p), cs, 0, E, 2 * E,
+                         ctypes.c_void_p(o.data_ptr()), E, ctypes.c_void_p(ddp), dcs, fptr(lse), ctypes.c_void_p(gp),
+                         ctypes.c_void_p(gp), ctypes.c_void_p(gp), C3, 0, E, 2 * E, B, L, heads, hd, float(hd ** -0.5),
+                         fptr(dvec), stream())
+        return g, None
+
+
+def attention(qkv, heads):
+    return AttnFn.apply(qkv, heads)
+
+
+class GroupMeanFn(torch.autograd.Function):
+    """(B, C, S*N, 1) -> mean over the S stacked groups -> (B, C, N, 1)."""
+
+    @staticmethod
+    def forward(ctx, x, S):
+        t, p, cs = _v(x)
+        B, C, SN, _ = x.shape
+        N = SN // S
+        y = empty_act(B, C, N, 1, x.dtype, x.device)
+        lib.adr_group_mean(dcode(x.dtype), ctypes.c_void_p(p), cs, S, N, ctypes.c_void_p(y.data_ptr()), C, B, C, 0,
+                           stream())
+        ctx.meta = (S, x.shape, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        S, shape, dtype = ctx.meta
+        B, C, SN, _ = shape
+        t, p, cs = _v(dy)
+        dx = empty_act(B, C, SN, 1, dtype, dy.device)
+        lib.adr_group_mean(dcode(dtype), ctypes.c_void_p(p), cs, S, SN // S, ctypes.c_void_p(dx.data_ptr()), C, B, C, 1,
+                           stream())
+        return dx, None
+
+
+def group_mean(x, S):
+    return GroupMeanFn.apply(x, S)
+
+
+class AdaPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, oh, ow):
+        t, p, cs = _v(x)
+        N, C, H, W = x.shape
+        y = empty_act(N, C, oh, ow, x.dtype, x.device)
+        lib.adr_adapool(dcode(x.dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(y.data_ptr()), C, oh, ow,
+                        stream())
+        ctx.meta = (x.shape, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (N, C, H, W), dtype = ctx.meta
+        t, p, cs = _v(dy)
+        dx = empty_act(N, C, H, W, dtype, dy.device)
+        lib.adr_adapool_bwd(dcode(dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(dx.data_ptr()), C,
+                            dy.shape[2], dy.shape[3], 0, stream())
+        return dx, None, None
+
+
+def adaptive_avg_pool(x, oh, ow):
+    return AdaPoolFn.apply(x, oh, ow)
+
+
+class BilinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, oh, ow):
+        t, p, cs = _v(x)
+        N, C, H, W = x.shape
+        y = empty_act(N, C, oh, ow, x.dtype, x.device)
+        lib.adr_bilinear(dcode(x.dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(y.data_ptr()), C, oh, ow,
+                         stream())
+        ctx.meta = (x.shape, x.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (N, C, H, W), dtype = ctx.meta
+        t, p, cs = _v(dy)
+        dx = empty_act(N, C, H, W, dtype, dy.device)
+        lib.adr_bilinear_bwd(dcode(dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(dx.data_ptr()), C,
+                             dy.shape[2], dy.shape[3], 0, stream())
+        return dx, None, None
+
+
+def bilinear(x, oh, ow):
+    return BilinearFn.apply(x, oh, ow)
+
+
+_EDFFN_BASIS = {}
+
+
+def edffn_basis(device, ps=8):
+    """B[uv][i][j] = (irfft2(e_uv * rfft2(e_j)))_i for the 8x8 patch, (8 x 5) half spectrum, float64 host
+    construction (numpy pocketfft, the same C2R convention torch.fft uses) -> fp32 device constant."""
+    key = (str(device), ps)
+    if key not in _EDFFN_BASIS:
+        import numpy as np
+        nv = ps // 2 + 1
+        eye = np.eye(ps * ps).reshape(ps * ps, ps, ps)
+        spec = np.fft.rfft2(eye)
+        B = np.empty((ps * nv, ps * ps, ps * ps))
+        for u in range(ps):
+            for v in range(nv):
+                filt = np.zeros((ps, nv))
+                filt[u, v] = 1.0
+                y = np.fft.irfft2(spec * filt, s=(ps, ps)).reshape(ps * ps, ps * ps)  # [j][i]
+                B[u * nv + v] = y.T
+        _EDFFN_BASIS[key] = torch.from_numpy(B.astype(np.float32)).to(device)
+    return _EDFFN_BASIS[key]
+
+
+class EDFFNFilterFn(torch.autograd.Function):
+    """Reflect-pad to a multiple of 8, per-patch rfft2 * fft -> irfft2, crop (block.py:2399-2413)."""
+
+    @staticmethod
+    def forward(ctx, x, fft):
+        t, p, cs = _v(x)
+        N, C, H, W = x.shape
+        basis = edffn_basis(x.device)
+        wf = fft.detach().float().contiguous().view(C, -1)
+        M = torch.empty(C, 64, 64, dtype=torch.float32, device=x.device)
+        lib.adr_edffn_build(fptr(wf), fptr(basis), C, wf.shape[1], fptr(M), stream())
+        y = empty_act(N, C, H, W, x.dtype, x.device)
+        lib.adr_edffn_fwd(dcode(x.dtype), ctypes.c_void_p(p), cs, fptr(M), ctypes.c_void_p(y.data_ptr()), C, N, H, W, C,
+                          stream())
+        ctx.save_for_backward(t, M)
+        ctx.meta = (fft.shape, wf.shape[1])
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        t, M = ctx.saved_tensors
+        fshape, nuv = ctx.meta
+        N, C, H, W = t.shape
+        _, p, cs = _v(t)
+        dd, dp, dcs = _v(dy)
+        basis = edffn_basis(t.device)
+        dx = empty_act(N, C, H, W, t.dtype, t.device)
+        dw = torch.empty(C, nuv, dtype=torch.float32, device=t.device)
+        wsb = lib.adr_edffn_bwd_workspace(N, H, W, C)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=t.device)
+        lib.adr_edffn_bwd(dcode(t.dtype), ctypes.c_void_p(p), cs, ctypes.c_void_p(dp), dcs, fptr(M), fptr(basis), nuv,
+                          ctypes.c_void_p(dx.data_ptr()), C, fptr(dw), N, H, W, C, fptr(ws), wsb, stream())
+        return dx, dw.view(fshape)
+
+
+def edffn_filter(x, fft):
+    return EDFFNFilterFn.apply(x, fft)

@@ -213,3 +213,180 @@ class DFL(nn.Module):
         self.conv = nn.Conv2d(c1, 1, 1, bias=False).requires_grad_(False)
         self.conv.weight.data[:] = torch.arange(c1, dtype=torch.float).view(1, c1, 1, 1)
         self.c1 = c1
+
+
+# ------------------------------------------------------------------------------------------------------------
+# C2PTSSA (reference block.py:2376-2710)
+# ------------------------------------------------------------------------------------------------------------
+
+
+def _linear(x_tok, lin_w, lin_b):
+    """nn.Linear over a (B, C, N, 1) NHWC token tensor as a 1x1 implicit GEMM."""
+    y, _ = K.conv2d(x_tok, lin_w.unsqueeze(-1).unsqueeze(-1), lin_b, 1, 0)
+    return y
+
+
+class EDFFN(nn.Module):
+    """Frequency-domain gated FFN (reference block.py:2376-2415)."""
+
+    def __init__(self, dim, ffn_expansion_factor=2, bias=False):
+        super().__init__()
+        hidden = int(dim * ffn_expansion_factor)
+        self.patch_size = 8
+        self.dim = dim
+        self.project_in = nn.Conv2d(dim, hidden * 2, kernel_size=1, bias=bias)
+        self.dwconv = nn.Conv2d(hidden * 2, hidden * 2, kernel_size=3, stride=1, padding=1, groups=hidden * 2,
+                                bias=bias)
+        self.fft = nn.Parameter(torch.ones((dim, 1, 1, self.patch_size, self.patch_size // 2 + 1)))
+        self.project_out = nn.Conv2d(hidden, dim, kernel_size=1, bias=bias)
+
+    def forward(self, x):
+        x, _ = K.conv2d(x, self.project_in.weight, self.project_in.bias, 1, 0)
+        x = K.dwconv(x, self.dwconv.weight, self.dwconv.bias, 3)
+        x1, x2 = K.split(x, (x.shape[1] // 2, x.shape[1] // 2))
+        x = K.mul(K.act(x1, "gelu"), x2)
+        x, _ = K.conv2d(x, self.project_out.weight, self.project_out.bias, 1, 0)
+        return K.edffn_filter(x, self.fft)  # computed in fp32 inside the kernel (reference :2407 .float())
+
+
+class CrossScaleAttentionTSSA(nn.Module):
+    """Multi-scale TSSA + cross-scale multi-head attention (reference block.py:2417-2491)."""
+
+    def __init__(self, dim, num_heads=8, qkv_bias=False, attn_drop=0.0, proj_drop=0.0, scales=(1, 2, 4), **kwargs):
+        super().__init__()
+        self.heads = num_heads
+        self.scales = list(scales)
+        self.dim = dim
+        self.head_dim = dim // num_heads
+        self.qkv_projections = nn.ModuleList([nn.Linear(dim, dim * 3, bias=qkv_bias) for _ in self.scales])
+        self.cross_scale_fusion = nn.MultiheadAttention(embed_dim=dim, num_heads=num_heads, dropout=attn_drop,
+                                                        batch_first=True)
+        self.temps = nn.Parameter(torch.ones(len(self.scales), num_heads, 1))
+        self.to_out = nn.Sequential(nn.Linear(dim, dim), nn.Dropout(proj_drop))
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        qkvs = []
+        for s, proj in zip(self.scales, self.qkv_projections):
+            xs = x if s == 1 else K.bilinear(K.adaptive_avg_pool(x, H // s, W // s), H, W)
+            qkvs.append(_linear(K.tokens(xs), proj.weight, proj.bias))
+        st = K.tssa_stack(self.temps, self.heads, qkvs)  # (B, C, S*HW, 1)
+        mha = self.cross_scale_fusion
+        qkv = _linear(st, mha.in_proj_weight, mha.in_proj_bias)
+        o = K.attention(qkv, self.heads)
+        o = _linear(o, mha.out_proj.weight, mha.out_proj.bias)
+        fused = K.group_mean(o, len(self.scales))
+        return _linear(fused, self.to_out[0].weight, self.to_out[0].bias)  # (B, C, HW, 1) tokens
+
+
+class AdaptiveDynamicTanh(nn.Module):
+    """Reference block.py:2493-2577 (channels_first)."""
+
+    def __init__(self, normalized_shape, num_scales=3):
+        super().__init__()
+        if num_scales != 3:
+            raise NotImplementedError("libadr ADyT kernels implement num_scales=3 (the reference default)")
+        self.normalized_shape = normalized_shape
+        self.num_scales = num_scales
+        self.alphas = nn.Parameter(torch.linspace(0.3, 1.0, num_scales).view(1, num_scales, 1, 1))
+        self.scale_weights = nn.Parameter(torch.ones(num_scales) / num_scales)  # unused by the reference forward
+        self.weight = nn.Parameter(torch.ones(normalized_shape))
+        self.bias = nn.Parameter(torch.zeros(normalized_shape))
+        self.importance_gate = nn.Sequential(nn.AdaptiveAvgPool2d(1), nn.Conv2d(normalized_shape, normalized_shape // 4, 1),
+                                             nn.ReLU(inplace=True), nn.Conv2d(normalized_shape // 4, num_scales, 1),
+                                             nn.Softmax(dim=1))
+
+    def forward(self, x):
+        g1, g3 = self.importance_gate[1], self.importance_gate[3]
+        imp = K.gate_mlp(K.gap(x), g1.weight, g1.bias, g3.weight, g3.bias, "relu", "softmax")  # (N, 3)
+        return K.adyt(x, self.alphas, imp, self.weight, self.bias)
+
+
+class ProgressiveFeatureFusion(nn.Module):
+    """Reference block.py:2579-2630."""
+
+    def __init__(self, dim, num_stages=3):
+        super().__init__()
+        self.num_stages = num_stages
+        self.stages = nn.ModuleList()
+        for _ in range(num_stages):
+            self.stages.append(nn.ModuleDict({
+                "conv": nn.Conv2d(dim, dim, 3, padding=1, groups=dim),
+                "norm": nn.BatchNorm2d(dim, eps=1e-3, momentum=0.03),
+                "activation": nn.GELU(),
+                "channel_mix": nn.Conv2d(dim, dim, 1),
+                "spatial_mix": nn.Conv2d(dim, dim, 7, padding=3, groups=dim),
+            }))
+        self.stage_fusion = nn.ModuleList([nn.Conv2d(dim * 2, dim, 1) for _ in range(num_stages - 1)])
+        self.stage_attention = nn.Parameter(torch.ones(num_stages) / num_stages)
+
+    def forward(self, x):
+        outs = []
+        cur = x
+        for i, st in enumerate(self.stages):
+            t = K.dwconv(cur, st["conv"].weight, st["conv"].bias, 3)
+            t = K.bn_act(t, None, st["norm"], "gelu", self.training)
+            cm, _ = K.conv2d(t, st["channel_mix"].weight, st["channel_mix"].bias, 1, 0)
+            sm = K.dwconv(t, st["spatial_mix"].weight, st["spatial_mix"].bias, 7)
+            out = K.add(cm, sm, cur)
+            outs.append(out)
+            if i < self.num_stages - 1:
+                sf = self.stage_fusion[i]
+                cur, _ = K.conv2d(K.cat([cur, out]), sf.weight, sf.bias, 1, 0)
+        return K.weighted_sum(self.stage_attention, outs, base=x)
+
+
+class ProgressiveTSSA_Fusion(nn.Module):  # noqa: N801
+    """Reference block.py:2632-2698."""
+
+    def __init__(self, c, attn_ratio=0.5, num_heads=4, shortcut=True):
+        super().__init__()
+        self.c = c
+        self.add = shortcut
+        self.progressive_fusion1 = ProgressiveFeatureFusion(c, num_stages=3)
+        self.progressive_fusion2 = ProgressiveFeatureFusion(c, num_stages=3)
+        self.dyt1 = AdaptiveDynamicTanh(c, num_scales=3)
+        self.dyt2 = AdaptiveDynamicTanh(c, num_scales=3)
+        self.attn = CrossScaleAttentionTSSA(c, num_heads=num_heads, scales=[1, 2, 4])
+        self.ffn = EDFFN(c, ffn_expansion_factor=2, bias=False)
+        self.residual_weight1 = nn.Parameter(torch.tensor(0.1))
+        self.residual_weight2 = nn.Parameter(torch.tensor(0.1))
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        identity = x
+        x = self.progressive_fusion1(x)
+        a = K.untokens(self.attn(self.dyt1(x)), H, W)
+        x = K.scale(a, self.residual_weight1, "scalar", res=identity) if self.add else a
+        x = self.progressive_fusion2(x)
+        f = self.ffn(self.dyt2(x))
+        return K.scale(f, self.residual_weight2, "scalar", res=x) if self.add else f
+
+
+class C2PSA(nn.Module):
+    """Split / concat frame of C2PSA (reference block.py:1010-1045) with the attention blocks in self.m."""
+
+    def __init__(self, c1, c2, n=1, e=0.5):
+        super().__init__()
+        assert c1 == c2
+        self.c = int(c1 * e)
+        self.cv1 = Conv(c1, 2 * self.c, 1, 1)
+        self.cv2 = Conv(2 * self.c, c1, 1)
+        self.m = nn.Sequential()
+
+    def forward(self, x):
+        a, b = K.split(self.cv1(x), (self.c, self.c))
+        b = self.m(b)
+        return self.cv2(K.cat([a, b]))
+
+
+class C2ProgressiveTSSA_Fusion(C2PSA):
+    """Reference block.py:2700-2710 (alias C2PTSSA)."""
+
+    def __init__(self, c1, c2, n=1, e=0.5):
+        super().__init__(c1, c2, n, e)
+        self.m = nn.Sequential(*(ProgressiveTSSA_Fusion(self.c, attn_ratio=0.5, num_heads=max(1, self.c // 64))
+                                 for _ in range(n)))
+
+
+C2PTSSA = C2ProgressiveTSSA_Fusion

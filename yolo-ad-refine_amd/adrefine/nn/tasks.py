@@ -1,0 +1,196 @@
+"""Model graph: yaml -> module list, and the forward driver — drop-in for the reference's
+ultralytics/nn/tasks.py (parse_model :943-1108, DetectionModel :309-398, BaseModel._predict_once :141-168).
+
+The channel arithmetic, repeat handling, `head_channel` / `fusion_mode` string resolution and the
+per-module argument rules are restated from parse_model, so the reference's z-yaml configs build the same
+layers with the same state_dict keys (541 for the 701 yaml). Layer classes resolve to the HIP-backed modules
+of adrefine.nn.modules; `nn.X` rows resolve to the HIP drop-ins for nn.Conv2d / nn.ConvTranspose2d.
+"""
+from __future__ import annotations
+
+import ast
+import contextlib
+import math
+import re
+from copy import deepcopy
+from pathlib import Path
+
+import torch
+import torch.nn as nn
+import yaml
+
+from .. import kernels as K
+from .modules import block, conv, head
+
+# name -> class, mirroring the reference's tasks.py import list for the modules on this path
+_REGISTRY = {
+    "Conv": conv.Conv, "Bottleneck": block.Bottleneck, "C2f": block.C2f, "C3": block.C3, "C3k2": block.C3k2,
+    "SPPF": block.SPPF, "C3k2_MLCA": block.C3k2_MLCA, "C2PTSSA": block.C2PTSSA, "C2PSA": block.C2PSA,
+    "ELA_HSFPN": block.ELA_HSFPN, "Multiply": block.Multiply, "Add": block.Add, "Fusion": block.Fusion,
+    "AYHead": head.AYHead, "AYHead1": head.AYHead1,
+}
+_NN = {"Conv2d": conv.Conv2d, "ConvTranspose2d": conv.ConvTranspose2d}
+
+_CH_MODULES = {"Conv", "Bottleneck", "SPPF", "C2f", "C3", "C3k2", "C3k2_MLCA", "C2PTSSA", "C2PSA",
+               "C2TSSA_DYT_Mona_EDFFN", "nn.Conv2d", "nn.ConvTranspose2d"}
+_REPEAT_MODULES = {"C2f", "C3", "C3k2", "C3k2_MLCA", "C2PTSSA", "C2PSA", "C2TSSA_DYT_Mona_EDFFN"}
+
+
+def register(name, cls):
+    """Register an extra module class for yaml lookup (e.g. the 697 Mona variant)."""
+    _REGISTRY[name] = cls
+
+
+def make_divisible(x, divisor):
+    if isinstance(divisor, torch.Tensor):
+        divisor = int(divisor.max())
+    return math.ceil(x / divisor) * divisor
+
+
+def guess_model_scale(model_path):
+    """tasks.py:1140-1155."""
+    with contextlib.suppress(AttributeError):
+        return re.search(r"yolo[v]?\d+([nslmx])", Path(model_path).stem).group(1)
+    return ""
+
+
+def yaml_model_load(path):
+    """tasks.py:1110-1124 (without the hub download / -p6 renames): dict + scale guessed from the file name."""
+    path = Path(path)
+    d = yaml.safe_load(path.read_text())
+    d["scale"] = guess_model_scale(path)
+    d["yaml_file"] = str(path)
+    return d
+
+
+def _resolve(m):
+    if m.startswith("nn."):
+        name = m[3:]
+        if name in _NN:
+            return _NN[name]
+        raise NotImplementedError(f"{m}: no HIP drop-in on the AD-Refine hot path")
+    if m not in _REGISTRY:
+        raise NotImplementedError(f"module '{m}' is not on the AD-Refine hot path (registered: {sorted(_REGISTRY)})")
+    return _REGISTRY[m]
+
+
+def parse_model(d, ch, verbose=False):
+    """Restatement of the reference parse_model (tasks.py:943-1108) for the modules this build provides."""
+    nc, scales = d.get("nc"), d.get("scales")
+    head_channel, fusion_mode = d.get("head_channel"), d.get("fusion_mode")
+    depth, width = d.get("depth_multiple", 1.0), d.get("width_multiple", 1.0)
+    max_channels = float("inf")
+    scale = d.get("scale")
+    if scales:
+        if not scale:
+            scale = tuple(scales.keys())[0]  # tasks.py:952-957 (the reference warns and assumes the first)
+        depth, width, max_channels = scales[scale]
+    local = {"nc": nc, "head_channel": head_channel, "fusion_mode": fusion_mode}
+    ch = [ch]
+    layers, save, c2 = [], [], ch[-1]
+    for i, (f, n, m, args) in enumerate(d["backbone"] + d["head"]):
+        mod = _resolve(m)
+        args = list(args)
+        for j, a in enumerate(args):
+            if isinstance(a, str):
+                with contextlib.suppress(ValueError):
+                    args[j] = local[a] if a in local else ast.literal_eval(a)
+        n = n_ = max(round(n * depth), 1) if n > 1 else n
+        if m in _CH_MODULES:
+            c1, c2 = ch[f], args[0]
+            if c2 != nc:
+                c2 = make_divisible(min(c2, max_channels) * width, 8)
+            args = [c1, c2, *args[1:]]
+            if m in _REPEAT_MODULES:
+                args.insert(2, n)
+                n = 1
+            if m == "C3k2" and scale in "mlx":
+                args[3] = True
+        elif m == "ELA_HSFPN":
+            args = [ch[f], *args]
+            c2 = ch[f]
+        elif m in ("Multiply", "Add"):
+            c2 = ch[f[0]]
+        elif m == "Fusion":
+            inc = [ch[x] for x in f]
+            args.insert(0, inc)
+            mode = args[1] if len(args) > 1 else "bifpn"
+            c2 = sum(inc) if mode == "concat" else inc[0]
+        elif m in ("AYHead", "AYHead1"):
+            args.append([ch[x] for x in f])
+        else:
+            c2 = ch[f]
+        m_ = nn.Sequential(*(mod(*args) for _ in range(n))) if n > 1 else mod(*args)
+        t = m
+        m_.np = sum(x.numel() for x in m_.parameters())
+        m_.i, m_.f, m_.type = i, f, t
+        if verbose:
+            print(f"{i:>3}{str(f):>20}{n_:>3}{m_.np:10.0f}  {t:<45}{str(args):<30}")
+        save.extend(x % i for x in ([f] if isinstance(f, int) else f) if x != -1)
+        layers.append(m_)
+        if i == 0:
+            ch = []
+        ch.append(c2)
+    return nn.Sequential(*layers), sorted(save)
+
+
+def initialize_weights(model):
+    """torch_utils.py:426-436: BatchNorm2d eps 1e-3 / momentum 0.03 (already the defaults of this build's BNs)."""
+    for m in model.modules():
+        if type(m) is nn.BatchNorm2d:
+            m.eps, m.momentum = 1e-3, 0.03
+
+
+class DetectionModel(nn.Module):
+    """YOLO detection model (tasks.py:309-398). Compute dtype: float32 (parity) or bfloat16 (performance);
+    parameters stay fp32. Input: float images (B, 3, H, W) in [0, 1] on a ROCm device."""
+
+    def __init__(self, cfg="yolo11-701-YOLO-AD-Refine.yaml", ch=3, nc=None, verbose=False, compute_dtype=torch.float32):
+        super().__init__()
+        self.yaml = cfg if isinstance(cfg, dict) else yaml_model_load(cfg)
+        ch = self.yaml["ch"] = self.yaml.get("ch", ch)
+        if nc and nc != self.yaml["nc"]:
+            self.yaml["nc"] = nc
+        self.model, self.save = parse_model(deepcopy(self.yaml), ch=ch, verbose=verbose)
+        self.names = {i: f"{i}" for i in range(self.yaml["nc"])}
+        self.inplace = self.yaml.get("inplace", True)
+        m = self.model[-1]
+        if isinstance(m, head.AYHead1):
+            # AYHead is not a Detect subclass: the reference skips the stride probe (tasks.py:335) and the head
+            # sets [8, 16, 32] itself (head.py:1209-1211)
+            self.stride = m.stride
+        else:
+            self.stride = torch.Tensor([32])
+        initialize_weights(self)
+        self.compute_dtype = compute_dtype
+        self.args = None
+
+    def forward(self, x, *args, **kwargs):
+        if isinstance(x, dict):
+            return self.loss(x, *args, **kwargs)
+        return self.predict(x, *args, **kwargs)
+
+    def predict(self, x, profile=False, visualize=False, augment=False, embed=None):
+        return self._predict_once(x)
+
+    def _predict_once(self, x):
+        """tasks.py:141-168 layer routing by m.f with the save list."""
+        if x.dim() == 4 and x.shape[1] == 3:
+            x = K.image_to_nhwc(x, self.compute_dtype, cpad=8)
+        y = []
+        for m in self.model:
+            if m.f != -1:
+                x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+            x = m(x)
+            y.append(x if m.i in self.save else None)
+        return x
+
+    def loss(self, batch, preds=None):
+        if getattr(self, "criterion", None) is None:
+            self.criterion = self.init_criterion()
+        preds = self.forward(batch["img"]) if preds is None else preds
+        return self.criterion(preds, batch)
+
+    def init_criterion(self):
+        from ..utils.loss import v8DetectionLoss
+        return v8DetectionLoss(self)

@@ -1,0 +1,773 @@
+// C2PTSSA building blocks (reference nn/modules/block.py:2376-2710), forward + backward, NHWC:
+//   * depthwise k x k conv + bias (ProgressiveFeatureFusion :2589-2593, EDFFN dwconv :2387, MonaOp mona.py:15-17)
+//   * AdaptiveDynamicTanh apply: out = (sum_i tanh(alpha_i x) * imp[n,i]) * w[c] + b[c]  (:2547-2575)
+//   * TSSA token statistics per (image, head) (CrossScaleAttentionTSSA :2465-2477):
+//       qn = q / max(|q|, 1e-12); Pi = softmax_tokens(temp * sum_d qn^2); attn[d] = 1 / (1 + sum_n Pi k^2);
+//       out = -v * Pi * attn
+//   * mean over the stacked scales (:2484-2486)
+//   * EDFFN 8x8-patch spectral filter as a per-channel 64x64 real operator (:2399-2413): reflect pad to a
+//     multiple of 8, y_patch = M_c x_patch with M_c = sum_uv fft[c,u,v] B_uv (B_uv = irfft2(e_uv * rfft2(.)),
+//     a constant basis built once on the host in float64), crop. Backward folds the reflected border and
+//     returns dfft[c,uv] = <B_uv, sum_patches dy x^T>.
+#include "adr_common.h"
+
+namespace adr {
+
+// ---------------- depthwise conv ----------------
+template <typename T>
+__global__ void __launch_bounds__(256) dw_fwd_kernel(const T* x, int xcs, const float* w, const float* b, T* y, int ycs,
+                                                     int N, int H, int W, int C, int k) {
+  constexpr int V = 16 / sizeof(T);
+  const int G = C / V;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)N * H * W * G;
+  if (i >= total) return;
+  int g = (int)(i % G);
+  long pix = i / G;
+  int ww = (int)(pix % W);
+  long r = pix / W;
+  int hh = (int)(r % H);
+  int n = (int)(r / H);
+  int p = k / 2, c0 = g * V;
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = b ? b[c0 + e] : 0.f;
+  for (int dy = 0; dy < k; ++dy) {
+    int ih = hh + dy - p;
+    if (ih < 0 || ih >= H) continue;
+    for (int dx = 0; dx < k; ++dx) {
+      int iw = ww + dx - p;
+      if (iw < 0 || iw >= W) continue;
+      u32x4 v = ld16(x + (((long)n * H + ih) * W + iw) * xcs + c0);
+      const T* e = reinterpret_cast<const T*>(&v);
+      int t = dy * k + dx;
+#pragma unroll
+      for (int q = 0; q < V; ++q) acc[q] += to_f(e[q]) * w[(c0 + q) * k * k + t];
+    }
+  }
+  u32x4 o;
+  T* oe = reinterpret_cast<T*>(&o);
+#pragma unroll
+  for (int q = 0; q < V; ++q) oe[q] = from_f<T>(acc[q]);
+  st16(y + pix * ycs + c0, o);
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dw_bwd_x_kernel(const T* dy, int dcs, const float* w, T* dx, int ocs, int N, int H,
+                                                       int W, int C, int k, int accumulate) {
+  constexpr int V = 16 / sizeof(T);
+  const int G = C / V;
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)N * H * W * G;
+  if (i >= total) return;
+  int g = (int)(i % G);
+  long pix = i / G;
+  int ww = (int)(pix % W);
+  long r = pix / W;
+  int hh = (int)(r % H);
+  int n = (int)(r / H);
+  int p = k / 2, c0 = g * V;
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  for (int ky = 0; ky < k; ++ky) {
+    int oh = hh - ky + p;
+    if (oh < 0 || oh >= H) continue;
+    for (int kx = 0; kx < k; ++kx) {
+      int ow = ww - kx + p;
+      if (ow < 0 || ow >= W) continue;
+      u32x4 v = ld16(dy + (((long)n * H + oh) * W + ow) * dcs + c0);
+      const T* e = reinterpret_cast<const T*>(&v);
+      int t = ky * k + kx;
+#pragma unroll
+      for (int q = 0; q < V; ++q) acc[q] += to_f(e[q]) * w[(c0 + q) * k * k + t];
+    }
+  }
+  u32x4 o;
+  T* oe = reinterpret_cast<T*>(&o);
+  if (accumulate) {
+    u32x4 pv = ld16(dx + pix * ocs + c0);
+    const T* pe = reinterpret_cast<const T*>(&pv);
+#pragma unroll
+    for (int q = 0; q < V; ++q) acc[q] += to_f(pe[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < V; ++q) oe[q] = from_f<T>(acc[q]);
+  st16(dx + pix * ocs + c0, o);
+}
+
+// partial[chunk][t][c] = sum over the chunk's pixels of dy * x(shifted by tap t); grid (chunks, k*k)
+template <typename T>
+__global__ void __launch_bounds__(256) dw_bwd_w_kernel(const T* x, int xcs, const T* dy, int dcs, int N, int H, int W,
+                                                       int C, int k, int rows_per_chunk, float* partial) {
+  constexpr int V = 16 / sizeof(T);
+  __shared__ float sh[256 * V];
+  const int chunk = blockIdx.x, t = blockIdx.y;
+  const int G = C / V, rpp = 256 / G;
+  const int tid = threadIdx.x, g = tid % G, r0 = tid / G;
+  const int ky = t / k, kx = t % k, p = k / 2;
+  long npix = (long)N * H * W;
+  long beg = (long)chunk * rows_per_chunk, end = beg + rows_per_chunk;
+  if (end > npix) end = npix;
+  float acc[V];
+#pragma unroll
+  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  if (r0 < rpp) {
+    for (long pix = beg + r0; pix < end; pix += rpp) {
+      int ww = (int)(pix % W);
+      long r = pix / W;
+      int hh = (int)(r % H);
+      int n = (int)(r / H);
+      int ih = hh + ky - p, iw = ww + kx - p;
+      if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+      u32x4 dv = ld16(dy + pix * dcs + g * V);
+      u32x4 xv = ld16(x + (((long)n * H + ih) * W + iw) * xcs + g * V);
+      const T* de = reinterpret_cast<const T*>(&dv);
+      const T* xe = reinterpret_cast<const T*>(&xv);
+#pragma unroll
+      for (int q = 0; q < V; ++q) acc[q] += to_f(de[q]) * to_f(xe[q]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < V; ++q) sh[tid * V + q] = acc[q];
+  __syncthreads();
+  for (int c = tid; c < C; c += 256) {
+    int gg = c / V, e = c % V;
+    float s = 0.f;
+    for (int rr = 0; rr < rpp; ++rr) s += sh[(gg + rr * G) * V + e];
+    partial[((long)chunk * k * k + t) * C + c] = s;
+  }
+}
+
+// dw[c][t] = sum_chunks partial[chunk][t][c]
+__global__ void dw_w_reduce_kernel(const float* partial, int chunks, int C, int kk, float* dw) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * kk) return;
+  int c = i / kk, t = i % kk;
+  float s = 0.f;
+  for (int ch = 0; ch < chunks; ++ch) s += partial[((long)ch * kk + t) * C + c];
+  dw[i] = s;
+}
+
+// ---------------- AdaptiveDynamicTanh ----------------
+template <typename T>
+__global__ void __launch_bounds__(256) adyt_fwd_kernel(const T* x, int xcs, const float* alphas, const float* imp,
+                                                       const float* w, const float* b, T* y, int ycs, long npix, int HW,
+                                                       int C) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= npix * C) return;
+  int c = (int)(i % C);
+  long pix = i / C;
+  int n = (int)(pix / HW);
+  float xv = to_f(x[pix * xcs + c]);
+  float s = 0.f;
+  for (int j = 0; j < 3; ++j) s += tanhf(alphas[j] * xv) * imp[n * 3 + j];
+  y[pix * ycs + c] = from_f<T>(s * w[c] + b[c]);
+}
+
+// dx, and partial[n][chunk][8][C]: {sum t_j w dout (j<3), sum x(1-t_j^2) w dout (j<3), sum S dout, sum dout}
+template <typename T>
+__global__ void __launch_bounds__(256) adyt_bwd_kernel(const T* x, int xcs, const T* dout, int dcs, const float* alphas,
+                                                       const float* imp, const float* w, T* dx, int ocs, int HW, int C,
+                                                       int rows_per_chunk, int chunks, float* partial) {
+  __shared__ float sh[8][256];
+  const int chunk = blockIdx.x, n = blockIdx.y;
+  int tid = threadIdx.x;
+  int cpt = C < 256 ? C : 256;  // threads over channels
+  int rpp = 256 / cpt;
+  int c = tid % cpt, r0 = tid / cpt;
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  float a[3] = {alphas[0], alphas[1], alphas[2]};
+  float im[3] = {imp[n * 3], imp[n * 3 + 1], imp[n * 3 + 2]};
+  int rbeg = chunk * rows_per_chunk, rend = min(HW, rbeg + rows_per_chunk);
+  if (r0 < rpp) {
+    for (int cc = c; cc < C; cc += cpt) {
+      float wc = w[cc];
+      for (int r = rbeg + r0; r < rend; r += rpp) {
+        long pix = (long)n * HW + r;
+        float xv = to_f(x[pix * xcs + cc]);
+        float d = to_f(dout[pix * dcs + cc]);
+        float g = 0.f, S = 0.f;
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+          float t = tanhf(a[j] * xv);
+          float sech2 = 1.f - t * t;
+          g += a[j] * sech2 * im[j];
+          S += t * im[j];
+          if (cc == c) {
+            acc[j] += t * wc * d;
+            acc[3 + j] += xv * sech2 * wc * d;
+          }
+        }
+        if (cc == c) {
+          acc[6] += S * d;
+          acc[7] += d;
+        }
+        dx[pix * ocs + cc] = from_f<T>(g * wc * d);
+      }
+    }
+  }
+  // only channels c < cpt were accumulated; C <= 256 is required by the host wrapper
+  for (int q = 0; q < 8; ++q) sh[q][tid] = acc[q];
+  __syncthreads();
+  if (tid < cpt) {
+    float* out = partial + ((long)n * chunks + chunk) * 8 * C;
+    for (int q = 0; q < 8; ++q) {
+      float s = 0.f;
+      for (int rr = 0; rr < rpp; ++rr) s += sh[q][tid + rr * cpt];
+      out[q * C + tid] = s;
+    }
+  }
+}
+
+// collapse: dimp[n][j] = sum_{chunk,c} P0..2 ; dalpha[j] = sum_{n,chunk,c} P3..5 * imp[n][j] ; dw[c] = sum P6 ;
+// db[c] = sum P7
+__global__ void adyt_collapse_kernel(const float* partial, const float* imp, int N, int chunks, int C, float* dimp,
+                                     float* dalpha, float* dw, float* db) {
+  int tid = threadIdx.x;
+  for (int c = tid; c < C; c += blockDim.x) {
+    float sw = 0.f, sb = 0.f;
+    for (int n = 0; n < N; ++n)
+      for (int ch = 0; ch < chunks; ++ch) {
+        const float* p = partial + ((long)n * chunks + ch) * 8 * C;
+        sw += p[6 * C + c];
+        sb += p[7 * C + c];
+      }
+    dw[c] = sw;
+    db[c] = sb;
+  }
+  if (tid < 3) {
+    int j = tid;
+    double da = 0.0;
+    for (int n = 0; n < N; ++n) {
+      double di = 0.0, dan = 0.0;
+      for (int ch = 0; ch < chunks; ++ch) {
+        const float* p = partial + ((long)n * chunks + ch) * 8 * C;
+        for (int c = 0; c < C; ++c) {
+          di += p[j * C + c];
+          dan += p[(3 + j) * C + c];
+        }
+      }
+      dimp[n * 3 + j] = (float)di;
+      da += dan * imp[n * 3 + j];
+    }
+    dalpha[j] = (float)da;
+  }
+}
+
+// ---------------- TSSA (one block per (image, head)) ----------------
+// q/k/v: [b][tok][*] rows with channel stride cs; head h uses channels [h*D, (h+1)*D) of each
+template <typename T>
+__global__ void __launch_bounds__(256) tssa_fwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok, int D,
+                                                       const float* temp, T* out, int ocs, int oimg, int heads,
+                                                       float* Pi_out, float* ss_out, float* attn_out) {
+  int b = blockIdx.x / heads, h = blockIdx.x % heads;
+  extern __shared__ float sm[];
+  float* Pi = sm;             // Ntok
+  float* red = sm + Ntok;     // 256
+  float* dots = red + 256;    // D
+  float tp = temp[h];
+  const long base = (long)b * Ntok;
+  // pass 1: ss and logits
+  float mx = -INFINITY;
+  for (int n = threadIdx.x; n < Ntok; n += 256) {
+    const T* qr = q + (base + n) * cs + h * D;
+    float s2 = 0.f;
+    for (int d = 0; d < D; ++d) {
+      float t = to_f(qr[d]);
+      s2 += t * t;
+    }
+    float r = fmaxf(sqrtf(s2), 1e-12f);
+    float ss = 0.f;
+    for (int d = 0; d < D; ++d) {
+      float t = to_f(qr[d]) / r;
+      ss += t * t;
+    }
+    ss_out[((long)b * heads + h) * Ntok + n] = ss;
+    float l = ss * tp;
+    Pi[n] = l;
+    mx = fmaxf(mx, l);
+  }
+  red[threadIdx.x] = mx;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  mx = red[0];
+  __syncthreads();
+  float z = 0.f;
+  for (int n = threadIdx.x; n < Ntok; n += 256) {
+    float e = __expf(Pi[n] - mx);
+    Pi[n] = e;
+    z += e;
+  }
+  red[threadIdx.x] = z;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  z = red[0];
+  __syncthreads();
+  for (int n = threadIdx.x; n < Ntok; n += 256) {
+    Pi[n] /= z;
+    Pi_out[((long)b * heads + h) * Ntok + n] = Pi[n];
+  }
+  __syncthreads();
+  // pass 2: dots[d] = sum_n Pi k^2 -> attn
+  for (int d = threadIdx.x; d < D; d += 256) {
+    float s = 0.f;
+    for (int n = 0; n < Ntok; ++n) {
+      float t = to_f(k[(base + n) * cs + h * D + d]);
+      s += Pi[n] * t * t;
+    }
+    float a = 1.f / (1.f + s);
+    dots[d] = a;
+    attn_out[((long)b * heads + h) * D + d] = a;
+  }
+  __syncthreads();
+  // pass 3: out = -v * Pi * attn
+  for (long i = threadIdx.x; i < (long)Ntok * D; i += 256) {
+    int n = (int)(i / D), d = (int)(i % D);
+    float vv = to_f(v[(base + n) * cs + h * D + d]);
+    out[((long)b * oimg + n) * ocs + h * D + d] = from_f<T>(-vv * Pi[n] * dots[d]);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) tssa_bwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok, int D,
+                                                       const float* temp, const T* dout, int dcs, int dimg, int heads,
+                                                       const float* Pi_in, const float* ss_in, const float* attn_in,
+                                                       T* dq, T* dk, T* dv, int gcs, float* dtemp_part) {
+  int b = blockIdx.x / heads, h = blockIdx.x % heads;
+  extern __shared__ float sm[];
+  float* dPi = sm;              // Ntok
+  float* red = sm + Ntok;       // 256
+  float* dattn = red + 256;     // D
+  float* ddots = dattn + D;     // D
+  const long base = (long)b * Ntok;
+  const float* Pi = Pi_in + ((long)b * heads + h) * Ntok;
+  const float* ss = ss_in + ((long)b * heads + h) * Ntok;
+  const float* attn = attn_in + ((long)b * heads + h) * D;
+  float tp = temp[h];
+  // dattn[d] = sum_n -dout v Pi ; dv = -dout Pi attn
+  for (int d = threadIdx.x; d < D; d += 256) {
+    float s = 0.f;
+    for (int n = 0; n < Ntok; ++n) {
+      float go = to_f(dout[((long)b * dimg + n) * dcs + h * D + d]);
+      float vv = to_f(v[(base + n) * cs + h * D + d]);
+      s += -go * vv * Pi[n];
+      dv[(base + n) * gcs + h * D + d] = from_f<T>(-go * Pi[n] * attn[d]);
+    }
+    dattn[d] = s;
+    ddots[d] = -s * attn[d] * attn[d];
+  }
+  __syncthreads();
+  // dPi[n] = sum_d (-dout v attn) + sum_d ddots k^2 ; dk = ddots * Pi * 2k
+  float part = 0.f;
+  for (int n = threadIdx.x; n < Ntok; n += 256) {
+    float s = 0.f;
+    for (int d = 0; d < D; ++d) {
+      float go = to_f(dout[((long)b * dimg + n) * dcs + h * D + d]);
+      float vv = to_f(v[(base + n) * cs + h * D + d]);
+      float kk = to_f(k[(base + n) * cs + h * D + d]);
+      s += -go * vv * attn[d] + ddots[d] * kk * kk;
+      dk[(base + n) * gcs + h * D + d] = from_f<T>(ddots[d] * Pi[n] * 2.f * kk);
+    }
+    dPi[n] = s;
+    part += Pi[n] * s;
+  }
+  red[threadIdx.x] = part;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  float dot = red[0];
+  __syncthreads();
+  // softmax backward -> dl ; dtemp partial ; dss -> dq
+  float tpart = 0.f;
+  for (int n = threadIdx.x; n < Ntok; n += 256) {
+    float dl = Pi[n] * (dPi[n] - dot);
+    tpart += dl * ss[n];
+    float dss = dl * tp;
+    const T* qr = q + (base + n) * cs + h * D;
+    float s2 = 0.f;
+    for (int d = 0; d < D; ++d) {
+      float t = to_f(qr[d]);
+      s2 += t * t;
+    }
+    float nrm = sqrtf(s2);
+    float r = fmaxf(nrm, 1e-12f);
+    // dqn = 2 qn dss ; dq = dqn / r - (nrm > eps) * q (q . dqn) / r^3
+    float qdq = 0.f;
+    for (int d = 0; d < D; ++d) {
+      float t = to_f(qr[d]);
+      qdq += t * (2.f * (t / r) * dss);
+    }
+    for (int d = 0; d < D; ++d) {
+      float t = to_f(qr[d]);
+      float dqn = 2.f * (t / r) * dss;
+      float g = dqn / r - (nrm > 1e-12f ? t * qdq / (r * r * r) : 0.f);
+      dq[(base + n) * gcs + h * D + d] = from_f<T>(g);
+    }
+  }
+  red[threadIdx.x] = tpart;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dtemp_part[(long)b * heads + h] = red[0];
+}
+
+// dtemp[s][h] = sum_b part[b][h]
+__global__ void tssa_temp_reduce_kernel(const float* part, int B, int heads, float* dtemp) {
+  int h = threadIdx.x;
+  if (h >= heads) return;
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) s += part[b * heads + h];
+  dtemp[h] = s;
+}
+
+// ---------------- mean over S stacked token groups ----------------
+template <typename T>
+__global__ void __launch_bounds__(256) group_mean_kernel(const T* x, int xcs, int S, int HW, T* y, int ycs, long B,
+                                                         int C, int backward) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (!backward) {
+    if (i >= B * HW * C) return;
+    int c = (int)(i % C);
+    long r = i / C;
+    int n = (int)(r % HW);
+    long b = r / HW;
+    float s = 0.f;
+    for (int g = 0; g < S; ++g) s += to_f(x[((b * S + g) * HW + n) * xcs + c]);
+    y[(b * HW + n) * ycs + c] = from_f<T>(s / (float)S);
+  } else {  // y: [B][S*HW] grad, x: [B][HW] upstream
+    if (i >= B * S * HW * C) return;
+    int c = (int)(i % C);
+    long r = i / C;
+    int n = (int)(r % HW);
+    long bg = r / HW;
+    long b = bg / S;
+    y[(bg * HW + n) * ycs + c] = from_f<T>(to_f(x[(b * HW + n) * xcs + c]) / (float)S);
+  }
+}
+
+// ---------------- EDFFN spectral patch filter ----------------
+__device__ __forceinline__ int reflect_idx(int j, int n) { return j < n ? j : 2 * (n - 1) - j; }
+
+// M[c][i][j] = sum_uv w[c][uv] * B[uv][i][j]
+__global__ void edffn_build_kernel(const float* w, const float* Bm, int C, int nuv, float* M) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)C * 4096) return;
+  int c = (int)(i / 4096), e = (int)(i % 4096);
+  float s = 0.f;
+  for (int u = 0; u < nuv; ++u) s += w[c * nuv + u] * Bm[(long)u * 4096 + e];
+  M[i] = s;
+}
+
+// block per (n, patch); y[pix] = M_c x_patch for unpadded pixels
+template <typename T>
+__global__ void __launch_bounds__(256) edffn_apply_kernel(const T* x, int xcs, const float* M, T* y, int ycs, int H,
+                                                          int W, int C, int transpose) {
+  extern __shared__ float xs[];  // [64][C]
+  int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8;
+  int n = blockIdx.x / (ph_n * pw_n);
+  int pp = blockIdx.x % (ph_n * pw_n);
+  int py = pp / pw_n, px = pp % pw_n;
+  for (int i = threadIdx.x; i < 64 * C; i += 256) {
+    int pos = i / C, c = i % C;
+    int yy = py * 8 + pos / 8, xx = px * 8 + pos % 8;
+    float v = 0.f;
+    if (!transpose) {
+      int sy = reflect_idx(yy, H), sx = reflect_idx(xx, W);
+      v = to_f(x[(((long)n * H + sy) * W + sx) * xcs + c]);
+    } else if (yy < H && xx < W) {  // backward: upstream grad only lives on the cropped (real) pixels
+      v = to_f(x[(((long)n * H + yy) * W + xx) * xcs + c]);
+    }
+    xs[pos * C + c] = v;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 64 * C; i += 256) {
+    int pos = i / C, c = i % C;
+    int yy = py * 8 + pos / 8, xx = px * 8 + pos % 8;
+    const float* Mc = M + (long)c * 4096;
+    float s = 0.f;
+    if (!transpose) {
+      if (yy >= H || xx >= W) continue;
+      for (int j = 0; j < 64; ++j) s += Mc[pos * 64 + j] * xs[j * C + c];
+      y[(((long)n * H + yy) * W + xx) * ycs + c] = from_f<T>(s);
+    } else {
+      // dX_pad[pos] = sum_i M[i][pos] dY[i]; written to a padded fp32 scratch (y reinterpreted)
+      for (int j = 0; j < 64; ++j) s += Mc[j * 64 + pos] * xs[j * C + c];
+      float* scratch = reinterpret_cast<float*>(y);
+      int Hp = ph_n * 8, Wp = pw_n * 8;
+      scratch[(((long)n * Hp + yy) * Wp + xx) * C + c] = s;
+    }
+  }
+}
+
+// fold reflected padding: dx[n,h,w,c] = sum of padded-grid grads whose reflect source is (h, w)
+template <typename T>
+__global__ void __launch_bounds__(256) edffn_fold_kernel(const float* dpad, int H, int W, int C, long N, T* dx, int ocs) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= N * H * W * C) return;
+  int c = (int)(i % C);
+  long pix = i / C;
+  int w = (int)(pix % W);
+  long r = pix / W;
+  int h = (int)(r % H);
+  long n = r / H;
+  int Hp = (H + 7) / 8 * 8, Wp = (W + 7) / 8 * 8;
+  float s = 0.f;
+  for (int a = 0; a < 2; ++a) {
+    int yy = a == 0 ? h : 2 * (H - 1) - h;
+    if (a == 1 && (yy < H || yy >= Hp)) continue;
+    for (int bb = 0; bb < 2; ++bb) {
+      int xx = bb == 0 ? w : 2 * (W - 1) - w;
+      if (bb == 1 && (xx < W || xx >= Wp)) continue;
+      s += dpad[((n * Hp + yy) * Wp + xx) * C + c];
+    }
+  }
+  dx[pix * ocs + c] = from_f<T>(s);
+}
+
+// dM[c][i][j] = sum over (n, patch) dY_patch[i] * X_patch[j]  (block per (c, i); threads over j)
+template <typename T>
+__global__ void __launch_bounds__(64) edffn_dM_kernel(const T* x, int xcs, const T* dy, int dcs, long N, int H, int W,
+                                                      int C, float* dM) {
+  int c = blockIdx.x / 64, i = blockIdx.x % 64;
+  int j = threadIdx.x;
+  int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8;
+  float s = 0.f;
+  for (long n = 0; n < N; ++n)
+    for (int py = 0; py < ph_n; ++py)
+      for (int px = 0; px < pw_n; ++px) {
+        int yi = py * 8 + i / 8, xi = px * 8 + i % 8;
+        if (yi >= H || xi >= W) continue;  // output pixel cropped away: no gradient
+        float g = to_f(dy[(((long)n * H + yi) * W + xi) * dcs + c]);
+        int yj = reflect_idx(py * 8 + j / 8, H), xj = reflect_idx(px * 8 + j % 8, W);
+        s += g * to_f(x[(((long)n * H + yj) * W + xj) * xcs + c]);
+      }
+  dM[((long)c * 64 + i) * 64 + j] = s;
+}
+
+// dw[c][uv] = sum_e B[uv][e] dM[c][e]
+__global__ void edffn_dw_kernel(const float* dM, const float* Bm, int C, int nuv, float* dw) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * nuv) return;
+  int c = i / nuv, u = i % nuv;
+  float s = 0.f;
+  for (int e = 0; e < 4096; ++e) s += Bm[(long)u * 4096 + e] * dM[(long)c * 4096 + e];
+  dw[i] = s;
+}
+
+}  // namespace adr
+
+using namespace adr;
+
+#define TDISPATCH(dtype, KERN, grid, block, sm, ...)                                                    \
+  do {                                                                                                  \
+    if ((dtype) == ADR_BF16) hipLaunchKernelGGL(KERN<__bf16>, grid, block, sm, st, __VA_ARGS__);         \
+    else hipLaunchKernelGGL(KERN<float>, grid, block, sm, st, __VA_ARGS__);                             \
+  } while (0)
+
+extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w, const float* b, void* y, int ycs,
+                              int N, int H, int W, int C, int k, void* stream) {
+  int v = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % v == 0 && xcs % v == 0 && ycs % v == 0 && k % 2 == 1, "dwconv: C=%d k=%d", C, k);
+  hipStream_t st = (hipStream_t)stream;
+  long total = (long)N * H * W * (C / v);
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(dw_fwd_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)x, xcs, w, b,
+                       (__bf16*)y, ycs, N, H, W, C, k);
+  else
+    hipLaunchKernelGGL(dw_fwd_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)x, xcs, w, b,
+                       (float*)y, ycs, N, H, W, C, k);
+  return check_launch("adr_dwconv_fwd");
+}
+
+extern "C" size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k) {
+  long npix = (long)N * H * W;
+  int chunks = cdiv(npix, 1024);
+  return (size_t)chunks * k * k * C * sizeof(float);
+}
+
+extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* w, void* dx,
+                              int ocs, float* dw, int N, int H, int W, int C, int k, int accumulate, float* ws,
+                              size_t ws_bytes, void* stream) {
+  int v = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % v == 0 && C / v <= 256, "dwconv_bwd: C=%d", C);
+  hipStream_t st = (hipStream_t)stream;
+  long total = (long)N * H * W * (C / v);
+  if (dx) {
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL(dw_bwd_x_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)dy, dcs, w,
+                         (__bf16*)dx, ocs, N, H, W, C, k, accumulate);
+    else
+      hipLaunchKernelGGL(dw_bwd_x_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)dy, dcs, w,
+                         (float*)dx, ocs, N, H, W, C, k, accumulate);
+  }
+  if (dw) {
+    ADR_REQUIRE(ws_bytes >= adr_dwconv_wgrad_workspace(N, H, W, C, k), "dwconv_bwd: workspace");
+    long npix = (long)N * H * W;
+    int chunks = cdiv(npix, 1024);
+    dim3 g(chunks, k * k);
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL(dw_bwd_w_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dy, dcs, N,
+                         H, W, C, k, 1024, ws);
+    else
+      hipLaunchKernelGGL(dw_bwd_w_kernel<float>, g, dim3(256), 0, st, (const float*)x, xcs, (const float*)dy, dcs, N, H,
+                         W, C, k, 1024, ws);
+    hipLaunchKernelGGL(dw_w_reduce_kernel, dim3(cdiv(C * k * k, 256)), dim3(256), 0, st, ws, chunks, C, k * k, dw);
+  }
+  return check_launch("adr_dwconv_bwd");
+}
+
+extern "C" int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alphas, const float* imp, const float* w,
+                            const float* b, void* y, int ycs, int N, int HW, int C, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  long npix = (long)N * HW;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(adyt_fwd_kernel<__bf16>, dim3(cdiv(npix * C, 256)), dim3(256), 0, st, (const __bf16*)x, xcs,
+                       alphas, imp, w, b, (__bf16*)y, ycs, npix, HW, C);
+  else
+    hipLaunchKernelGGL(adyt_fwd_kernel<float>, dim3(cdiv(npix * C, 256)), dim3(256), 0, st, (const float*)x, xcs, alphas,
+                       imp, w, b, (float*)y, ycs, npix, HW, C);
+  return check_launch("adr_adyt_fwd");
+}
+
+extern "C" size_t adr_adyt_bwd_workspace(int N, int HW, int C) {
+  return (size_t)N * cdiv(HW, 256) * 8 * C * sizeof(float);
+}
+
+extern "C" int adr_adyt_bwd(int dtype, const void* x, int xcs, const void* dout, int dcs, const float* alphas,
+                            const float* imp, const float* w, void* dx, int ocs, float* dimp, float* dalpha, float* dw,
+                            float* db, int N, int HW, int C, float* ws, size_t ws_bytes, void* stream) {
+  ADR_REQUIRE(C <= 256, "adyt_bwd: C=%d > 256", C);
+  ADR_REQUIRE(ws_bytes >= adr_adyt_bwd_workspace(N, HW, C), "adyt_bwd: workspace");
+  hipStream_t st = (hipStream_t)stream;
+  int chunks = cdiv(HW, 256);
+  dim3 g(chunks, N);
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(adyt_bwd_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dout, dcs,
+                       alphas, imp, w, (__bf16*)dx, ocs, HW, C, 256, chunks, ws);
+  else
+    hipLaunchKernelGGL(adyt_bwd_kernel<float>, g, dim3(256), 0, st, (const float*)x, xcs, (const float*)dout, dcs,
+                       alphas, imp, w, (float*)dx, ocs, HW, C, 256, chunks, ws);
+  hipLaunchKernelGGL(adyt_collapse_kernel, dim3(1), dim3(256), 0, st, ws, imp, N, chunks, C, dimp, dalpha, dw, db);
+  return check_launch("adr_adyt_bwd");
+}
+
+extern "C" int adr_tssa_fwd(int dtype, const void* q, const void* k, const void* v, int cs, int B, int Ntok, int heads,
+                            int D, const float* temp, void* out, int ocs, int oimg, float* Pi, float* ss, float* attn,
+                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  size_t sm = (Ntok + 256 + D) * sizeof(float);
+  ADR_REQUIRE(sm <= 64 * 1024, "tssa: Ntok=%d too large", Ntok);
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(tssa_fwd_kernel<__bf16>, dim3(B * heads), dim3(256), sm, st, (const __bf16*)q, (const __bf16*)k,
+                       (const __bf16*)v, cs, Ntok, D, temp, (__bf16*)out, ocs, oimg, heads, Pi, ss, attn);
+  else
+    hipLaunchKernelGGL(tssa_fwd_kernel<float>, dim3(B * heads), dim3(256), sm, st, (const float*)q, (const float*)k,
+                       (const float*)v, cs, Ntok, D, temp, (float*)out, ocs, oimg, heads, Pi, ss, attn);
+  return check_launch("adr_tssa_fwd");
+}
+
+extern "C" int adr_tssa_bwd(int dtype, const void* q, const void* k, const void* v, int cs, int B, int Ntok, int heads,
+                            int D, const float* temp, const void* dout, int dcs, int dimg, const float* Pi,
+                            const float* ss,
+                            const float* attn, void* dq, void* dk, void* dv, int gcs, float* dtemp, float* ws,
+                            void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  size_t sm = (Ntok + 256 + 2 * D) * sizeof(float);
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(tssa_bwd_kernel<__bf16>, dim3(B * heads), dim3(256), sm, st, (const __bf16*)q, (const __bf16*)k,
+                       (const __bf16*)v, cs, Ntok, D, temp, (const __bf16*)dout, dcs, dimg, heads, Pi, ss, attn,
+                       (__bf16*)dq,
+                       (__bf16*)dk, (__bf16*)dv, gcs, ws);
+  else
+    hipLaunchKernelGGL(tssa_bwd_kernel<float>, dim3(B * heads), dim3(256), sm, st, (const float*)q, (const float*)k,
+                       (const float*)v, cs, Ntok, D, temp, (const float*)dout, dcs, dimg, heads, Pi, ss, attn, (float*)dq,
+                       (float*)dk, (float*)dv, gcs, ws);
+  hipLaunchKernelGGL(tssa_temp_reduce_kernel, dim3(1), dim3(64), 0, st, ws, B, heads, dtemp);
+  return check_launch("adr_tssa_bwd");
+}
+
+extern "C" int adr_group_mean(int dtype, const void* x, int xcs, int S, int HW, void* y, int ycs, int B, int C,
+                              int backward, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  long total = (long)B * (backward ? S : 1) * HW * C;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(group_mean_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)x, xcs, S,
+                       HW, (__bf16*)y, ycs, (long)B, C, backward);
+  else
+    hipLaunchKernelGGL(group_mean_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)x, xcs, S, HW,
+                       (float*)y, ycs, (long)B, C, backward);
+  return check_launch("adr_group_mean");
+}
+
+extern "C" int adr_edffn_build(const float* w, const float* basis, int C, int nuv, float* M, void* stream) {
+  hipLaunchKernelGGL(edffn_build_kernel, dim3(cdiv((long)C * 4096, 256)), dim3(256), 0, (hipStream_t)stream, w, basis,
+                     C, nuv, M);
+  return check_launch("adr_edffn_build");
+}
+
+extern "C" int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, void* y, int ycs, int N, int H, int W,
+                             int C, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int np = ((H + 7) / 8) * ((W + 7) / 8);
+  size_t sm = 64 * C * sizeof(float);
+  ADR_REQUIRE(sm <= 64 * 1024, "edffn: C=%d too large", C);
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(edffn_apply_kernel<__bf16>, dim3(N * np), dim3(256), sm, st, (const __bf16*)x, xcs, M,
+                       (__bf16*)y, ycs, H, W, C, 0);
+  else
+    hipLaunchKernelGGL(edffn_apply_kernel<float>, dim3(N * np), dim3(256), sm, st, (const float*)x, xcs, M, (float*)y,
+                       ycs, H, W, C, 0);
+  return check_launch("adr_edffn_fwd");
+}
+
+extern "C" size_t adr_edffn_bwd_workspace(int N, int H, int W, int C) {
+  size_t hp = (H + 7) / 8 * 8, wp = (W + 7) / 8 * 8;
+  return ((size_t)N * hp * wp * C + (size_t)C * 4096) * sizeof(float);
+}
+
+extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* M,
+                             const float* basis, int nuv, void* dx, int ocs, float* dw, int N, int H, int W, int C,
+                             float* ws, size_t ws_bytes, void* stream) {
+  ADR_REQUIRE(ws_bytes >= adr_edffn_bwd_workspace(N, H, W, C), "edffn_bwd: workspace");
+  hipStream_t st = (hipStream_t)stream;
+  int np = ((H + 7) / 8) * ((W + 7) / 8);
+  size_t sm = 64 * C * sizeof(float);
+  float* dpad = ws;
+  float* dM = ws + (size_t)N * ((H + 7) / 8 * 8) * ((W + 7) / 8 * 8) * C;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(edffn_apply_kernel<__bf16>, dim3(N * np), dim3(256), sm, st, (const __bf16*)dy, dcs, M,
+                       (__bf16*)dpad, 0, H, W, C, 1);
+  else
+    hipLaunchKernelGGL(edffn_apply_kernel<float>, dim3(N * np), dim3(256), sm, st, (const float*)dy, dcs, M,
+                       (float*)dpad, 0, H, W, C, 1);
+  long total = (long)N * H * W * C;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(edffn_fold_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, dpad, H, W, C, (long)N,
+                       (__bf16*)dx, ocs);
+  else
+    hipLaunchKernelGGL(edffn_fold_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, dpad, H, W, C, (long)N,
+                       (float*)dx, ocs);
+  if (dw) {
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL(edffn_dM_kernel<__bf16>, dim3(C * 64), dim3(64), 0, st, (const __bf16*)x, xcs,
+                         (const __bf16*)dy, dcs, (long)N, H, W, C, dM);
+    else
+      hipLaunchKernelGGL(edffn_dM_kernel<float>, dim3(C * 64), dim3(64), 0, st, (const float*)x, xcs, (const float*)dy,
+                         dcs, (long)N, H, W, C, dM);
+    hipLaunchKernelGGL(edffn_dw_kernel, dim3(cdiv(C * nuv, 256)), dim3(256), 0, st, dM, basis, C, nuv, dw);
+  }
+  return check_launch("adr_edffn_bwd");
+}
