@@ -249,6 +249,19 @@ int adr_attn_bwd(int dtype, const void* q, const void* k, const void* v, int cs,
                  int gcs, int gqo, int gko, int gvo, int B, int L, int heads, int head_dim, float scale,
                  float* dvec_ws, void* stream);
 
+/* ---------------------------------------------------------------------------------------------------------
+ * v8DetectionLoss (utils/loss.py:355-520) + TaskAlignedAssigner(topk 10, alpha 0.5, beta 6) (utils/tal.py)
+ * + BboxLoss 0.5 CIoU + 0.5 NWD, DFLoss, SlideLoss BCE — value and gradient in one call, no host sync.
+ * f0..f2: the three AYHead train outputs (B, 4*16+nc, Hi, Wi) NHWC; gt: (B, nmax, 5) fp32 device rows
+ * [cls, x1, y1, x2, y2] in pixels (the reference's preprocess output, loss.py:392-408; zero rows = padding);
+ * g0..g2 receive d(out[3]) / d(f) * grad_scale / B (dense NHWC, row stride 4*16+nc).
+ * out (5 floats): box*7.5, cls*0.5, dfl*1.5 (the reference's loss.detach()), (sum)*B, number of positives. */
+size_t adr_det_loss_workspace(int B, int nmax, int A);
+int adr_det_loss(int dtype, const void* f0, const void* f1, const void* f2, int cs0, int cs1, int cs2, int H0, int W0,
+                 int H1, int W1, int H2, int W2, float s0, float s1, float s2, int B, int nc, const float* gt,
+                 int nmax, void* g0, void* g1, void* g2, float grad_scale, float box_gain, float cls_gain,
+                 float dfl_gain, float* out, void* ws, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,585 @@
+// v8DetectionLoss for AYHead outputs (reference utils/loss.py:355-520) with TaskAlignedAssigner
+// (utils/tal.py:13-265), BboxLoss = 0.5 CIoU + 0.5 NWD (loss.py:264-311, metrics.py:74-125, 539-564),
+// DFLoss (loss.py:238-261) and SlideLoss(BCEWithLogits) (loss.py:18-42) — forward value AND the gradient
+// w.r.t. the three head outputs, all on the GPU with no host synchronisation.
+//
+// Pipeline (all deterministic: fixed-order block reductions, no atomics):
+//   decode   pbox[b][a] (grid units) = anchor -+ DFL expectation of the 4x16 box logits
+//   metrics  per (b, gt j, a): in-gt test (eps 1e-9), CIoU(gt, pbox*stride).clamp(0), align = s^0.5 * u^6
+//   topk     per (b, j): top-10 of align with the exact selection PyTorch's CPU topk makes for k*64 <= n
+//            (std::partial_sort == libstdc++ heap-select), so equal-metric ties pick the same anchors
+//   assign   per (b, a): fg / multi-gt resolution by first argmax of overlaps / target gt index (first argmax)
+//   norm     per (b, j): max align / max overlap over the gt's positives
+//   fg pass  per (b, a): target score norm, CIoU / NWD / DFL of positives -> block partials
+//   cls pass per (b, a): SlideLoss-modulated BCE over nc classes (mu = max(0.2, mean CIoU of positives)),
+//            and the full 4*reg_max + nc gradient row for the anchor.
+#include "adr_common.h"
+
+namespace adr {
+
+static constexpr float kEps = 1e-7f;
+static constexpr int RM = 16;  // reg_max
+static constexpr int TOPK = 10;
+
+struct Levels {
+  const void* f[3];
+  int cs[3];
+  int H[3], W[3];
+  float st[3];
+  int A;
+};
+
+__device__ __forceinline__ void anchor_of(const Levels& L, int a, int& lvl, int& loc) {
+  int n0 = L.H[0] * L.W[0], n1 = L.H[1] * L.W[1];
+  if (a < n0) { lvl = 0; loc = a; }
+  else if (a < n0 + n1) { lvl = 1; loc = a - n0; }
+  else { lvl = 2; loc = a - n0 - n1; }
+}
+
+template <typename T>
+__device__ __forceinline__ const T* feat_row(const Levels& L, int b, int a, int& lvl, float& ax, float& ay) {
+  int loc;
+  anchor_of(L, a, lvl, loc);
+  int W = L.W[lvl], HW = L.H[lvl] * W;
+  ax = (float)(loc % W) + 0.5f;
+  ay = (float)(loc / W) + 0.5f;
+  return reinterpret_cast<const T*>(L.f[lvl]) + ((long)b * HW + loc) * L.cs[lvl];
+}
+
+// CIoU value (metrics.py:74-125, xywh=False, CIoU=True, eps=1e-7); box = x1, y1, x2, y2
+__device__ __forceinline__ float ciou(const float* a, const float* b) {
+  float w1 = a[2] - a[0], h1 = a[3] - a[1] + kEps;
+  float w2 = b[2] - b[0], h2 = b[3] - b[1] + kEps;
+  float iw = fmaxf(fminf(a[2], b[2]) - fmaxf(a[0], b[0]), 0.f);
+  float ih = fmaxf(fminf(a[3], b[3]) - fmaxf(a[1], b[1]), 0.f);
+  float inter = iw * ih;
+  float uni = w1 * h1 + w2 * h2 - inter + kEps;
+  float iou = inter / uni;
+  float cw = fmaxf(a[2], b[2]) - fminf(a[0], b[0]);
+  float ch = fmaxf(a[3], b[3]) - fminf(a[1], b[1]);
+  float c2 = cw * cw + ch * ch + kEps;
+  float sx = b[0] + b[2] - a[0] - a[2], sy = b[1] + b[3] - a[1] - a[3];
+  float rho2 = (sx * sx + sy * sy) / 4.f;
+  const float k4 = 4.f / (3.14159265358979323846f * 3.14159265358979323846f);
+  float dv = atanf(w2 / h2) - atanf(w1 / h1);
+  float v = k4 * dv * dv;
+  float alpha = v / (v - iou + (1.f + kEps));
+  return iou - (rho2 / c2 + v * alpha);
+}
+
+// d/d(a) of CIoU(a, b) (alpha treated as a constant, as the reference computes it under no_grad)
+__device__ __forceinline__ void ciou_grad(const float* a, const float* b, float* g) {
+  float w1 = a[2] - a[0], h1 = a[3] - a[1] + kEps;
+  float w2 = b[2] - b[0], h2 = b[3] - b[1] + kEps;
+  float mnx = fminf(a[2], b[2]), mxx = fmaxf(a[0], b[0]);
+  float mny = fminf(a[3], b[3]), mxy = fmaxf(a[1], b[1]);
+  float iwr = mnx - mxx, ihr = mny - mxy;
+  float iw = fmaxf(iwr, 0.f), ih = fmaxf(ihr, 0.f);
+  float inter = iw * ih;
+  float uni = w1 * h1 + w2 * h2 - inter + kEps;
+  float iou = inter / uni;
+  // torch.minimum / maximum split the gradient on ties; clamp(min=0) passes it where the input >= 0
+  auto tie_lt = [](float p, float q) { return p < q ? 1.f : (p == q ? 0.5f : 0.f); };
+  float diw[4] = {-tie_lt(b[0], a[0]), 0.f, tie_lt(a[2], b[2]), 0.f};  // d iw / d (x1, y1, x2, y2)
+  float dih[4] = {0.f, -tie_lt(b[1], a[1]), 0.f, tie_lt(a[3], b[3])};
+  float miw = iwr >= 0.f ? 1.f : 0.f, mih = ihr >= 0.f ? 1.f : 0.f;
+  float dinter[4], duni[4];
+  float dw1[4] = {-1.f, 0.f, 1.f, 0.f}, dh1[4] = {0.f, -1.f, 0.f, 1.f};
+  for (int k = 0; k < 4; ++k) {
+    dinter[k] = miw * diw[k] * ih + mih * dih[k] * iw;
+    duni[k] = dw1[k] * h1 + dh1[k] * w1 - dinter[k];
+  }
+  float cw = fmaxf(a[2], b[2]) - fminf(a[0], b[0]);
+  float ch = fmaxf(a[3], b[3]) - fminf(a[1], b[1]);
+  float dcw[4] = {-tie_lt(a[0], b[0]), 0.f, tie_lt(b[2], a[2]), 0.f};
+  float dch[4] = {0.f, -tie_lt(a[1], b[1]), 0.f, tie_lt(b[3], a[3])};
+  float c2 = cw * cw + ch * ch + kEps;
+  float sx = b[0] + b[2] - a[0] - a[2], sy = b[1] + b[3] - a[1] - a[3];
+  float rho2 = (sx * sx + sy * sy) / 4.f;
+  float drho[4] = {-sx / 2.f, -sy / 2.f, -sx / 2.f, -sy / 2.f};
+  const float k4 = 4.f / (3.14159265358979323846f * 3.14159265358979323846f);
+  float dv_ = atanf(w2 / h2) - atanf(w1 / h1);
+  float v = k4 * dv_ * dv_;
+  float alpha = v / (v - iou + (1.f + kEps));
+  float den = w1 * w1 + h1 * h1;
+  float dv_dw1 = -2.f * k4 * dv_ * h1 / den, dv_dh1 = 2.f * k4 * dv_ * w1 / den;
+  for (int k = 0; k < 4; ++k) {
+    float dc2 = 2.f * cw * dcw[k] + 2.f * ch * dch[k];
+    float diou = (dinter[k] * uni - inter * duni[k]) / (uni * uni);
+    float dr = (drho[k] * c2 - rho2 * dc2) / (c2 * c2);
+    float dv = dv_dw1 * dw1[k] + dv_dh1 * dh1[k];
+    g[k] = diou - dr - alpha * dv;
+  }
+}
+
+// NWD (metrics.py:539-564, constant 12.8) and its gradient w.r.t. a
+__device__ __forceinline__ float nwd(const float* a, const float* b, float* g) {
+  float w1 = a[2] - a[0], h1 = a[3] - a[1] + kEps;
+  float w2 = b[2] - b[0], h2 = b[3] - b[1] + kEps;
+  float cx1 = a[0] + w1 / 2.f, cy1 = a[1] + h1 / 2.f, cx2 = b[0] + w2 / 2.f, cy2 = b[1] + h2 / 2.f;
+  float cd = (cx1 - cx2) * (cx1 - cx2) + (cy1 - cy2) * (cy1 - cy2) + kEps;
+  float whd = ((w1 - w2) * (w1 - w2) + (h1 - h2) * (h1 - h2)) / 4.f;
+  float W2 = cd + whd;
+  float s = sqrtf(W2);
+  float r = expf(-s / 12.8f);
+  if (g) {
+    float dW2 = r * (-1.f / 12.8f) * 0.5f / s;
+    float dcx[4] = {0.5f, 0.f, 0.5f, 0.f}, dcy[4] = {0.f, 0.5f, 0.f, 0.5f};
+    float dw1[4] = {-1.f, 0.f, 1.f, 0.f}, dh1[4] = {0.f, -1.f, 0.f, 1.f};
+    for (int k = 0; k < 4; ++k) {
+      float d = 2.f * (cx1 - cx2) * dcx[k] + 2.f * (cy1 - cy2) * dcy[k] + ((w1 - w2) * dw1[k] + (h1 - h2) * dh1[k]) / 2.f;
+      g[k] = dW2 * d;
+    }
+  }
+  return r;
+}
+
+// ---- decode ----
+template <typename T>
+__global__ void __launch_bounds__(256) loss_decode_kernel(Levels L, int B, float* pbox) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * L.A) return;
+  int a = (int)(i % L.A), b = (int)(i / L.A);
+  int lvl;
+  float ax, ay;
+  const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
+  float d[4];
+  for (int k = 0; k < 4; ++k) {
+    float mx = -INFINITY;
+    for (int j = 0; j < RM; ++j) mx = fmaxf(mx, to_f(p[k * RM + j]));
+    float z = 0.f, e = 0.f;
+    for (int j = 0; j < RM; ++j) {
+      float ex = expf(to_f(p[k * RM + j]) - mx);
+      z += ex;
+      e += ex * (float)j;
+    }
+    d[k] = e / z;
+  }
+  float* o = pbox + i * 4;
+  o[0] = ax - d[0];
+  o[1] = ay - d[1];
+  o[2] = ax + d[2];
+  o[3] = ay + d[3];
+}
+
+// ---- TAL metrics: gt (B, nmax, 5) = [cls, x1, y1, x2, y2] pixels; mask_gt = box sum > 0 ----
+template <typename T>
+__global__ void __launch_bounds__(256) tal_metrics_kernel(Levels L, int B, int nmax, int nc, const float* gt,
+                                                          const float* pbox, float* align, float* ovl,
+                                                          uint8_t* flags) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long total = (long)B * nmax * L.A;
+  if (i >= total) return;
+  int a = (int)(i % L.A);
+  long r = i / L.A;
+  int j = (int)(r % nmax), b = (int)(r / nmax);
+  const float* g = gt + ((long)b * nmax + j) * 5;
+  float gb[4] = {g[1], g[2], g[3], g[4]};
+  bool mgt = (gb[0] + gb[1] + gb[2] + gb[3]) > 0.f;
+  int lvl;
+  float ax, ay;
+  const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
+  float st = L.st[lvl];
+  float px = ax * st, py = ay * st;
+  float dmin = fminf(fminf(px - gb[0], py - gb[1]), fminf(gb[2] - px, gb[3] - py));
+  bool in = dmin > 1e-9f;
+  float al = 0.f, ov = 0.f;
+  if (in && mgt) {
+    const float* pb = pbox + ((long)b * L.A + a) * 4;
+    float pd[4] = {pb[0] * st, pb[1] * st, pb[2] * st, pb[3] * st};
+    ov = fmaxf(ciou(gb, pd), 0.f);
+    int cls = (int)g[0];
+    float logit = to_f(p[4 * RM + cls]);
+    float sc = 1.f / (1.f + expf(-logit));
+    al = sqrtf(sc) * powf(ov, 6.f);
+  }
+  align[i] = al;
+  ovl[i] = ov;
+  flags[i] = (uint8_t)((in ? 1 : 0) | (mgt ? 4 : 0));
+}
+
+// ---- top-k as std::partial_sort (libstdc++ __heap_select) with comp(x, y) = x.v > y.v ----
+struct KV {
+  float v;
+  int i;
+};
+__device__ __forceinline__ bool cmpg(const KV& x, const KV& y) { return x.v > y.v; }
+
+__device__ void adjust_heap(KV* f, int hole, int len, KV value) {
+  const int top = hole;
+  int second = hole;
+  while (second < (len - 1) / 2) {
+    second = 2 * (second + 1);
+    if (cmpg(f[second], f[second - 1])) second--;
+    f[hole] = f[second];
+    hole = second;
+  }
+  if ((len & 1) == 0 && second == (len - 2) / 2) {
+    second = 2 * (second + 1);
+    f[hole] = f[second - 1];
+    hole = second - 1;
+  }
+  int parent = (hole - 1) / 2;
+  while (hole > top && cmpg(f[parent], value)) {
+    f[hole] = f[parent];
+    hole = parent;
+    parent = (hole - 1) / 2;
+  }
+  f[hole] = value;
+}
+
+__global__ void __launch_bounds__(64) tal_topk_kernel(const float* align, uint8_t* flags, int rows, int A) {
+  int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  const float* m = align + (long)r * A;
+  uint8_t* fl = flags + (long)r * A;
+  bool mgt = (fl[0] & 4) != 0;
+  if (!mgt) return;  // topk_mask false: indices masked to 0, and mask_gt zeroes the row anyway
+  if (A <= TOPK) {
+    for (int a = 0; a < A; ++a) fl[a] |= 2;
+    return;
+  }
+  KV h[TOPK];
+  for (int k = 0; k < TOPK; ++k) h[k] = KV{m[k], k};
+  // make_heap
+  for (int parent = (TOPK - 2) / 2;; --parent) {
+    adjust_heap(h, parent, TOPK, h[parent]);
+    if (parent == 0) break;
+  }
+  for (int a = TOPK; a < A; ++a) {
+    float v = m[a];
+    if (v > h[0].v) adjust_heap(h, 0, TOPK, KV{v, a});  // __pop_heap(first, middle, i): top replaced by *i
+  }
+  for (int k = 0; k < TOPK; ++k) fl[h[k].i] |= 2;
+}
+
+// ---- assign: per (b, a) ----
+__global__ void __launch_bounds__(256) tal_assign_kernel(const uint8_t* flags, const float* ovl, int B, int nmax,
+                                                         int A, int* tgi, uint8_t* fg) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)B * A) return;
+  int a = (int)(i % A), b = (int)(i / A);
+  int cnt = 0, first = -1;
+  for (int j = 0; j < nmax; ++j) {
+    uint8_t f = flags[((long)b * nmax + j) * A + a];
+    if ((f & 7) == 7) {  // topk & in_gts & mask_gt
+      cnt++;
+      if (first < 0) first = j;
+    }
+  }
+  int t = 0;
+  if (cnt > 1) {  // multi-gt: one-hot of overlaps.argmax over all gts (first max)
+    float best = -INFINITY;
+    for (int j = 0; j < nmax; ++j) {
+      float o = ovl[((long)b * nmax + j) * A + a];
+      if (o > best) {
+        best = o;
+        t = j;
+      }
+    }
+  } else if (cnt == 1) {
+    t = first;
+  }
+  tgi[i] = t;
+  fg[i] = cnt > 0 ? 1 : 0;
+}
+
+// ---- per-gt normalisers: pos_align = max over own positives of align, pos_ov = max of overlaps ----
+__global__ void __launch_bounds__(256) tal_norm_kernel(const float* align, const float* ovl, const int* tgi,
+                                                       const uint8_t* fg, int B, int nmax, int A, float* pos) {
+  int r = blockIdx.x;  // (b, j)
+  int b = r / nmax, j = r % nmax;
+  __shared__ float sa[256], so[256];
+  float ma = 0.f, mo = 0.f;  // masked values are 0 (align * mask_pos), so the max starts at 0
+  for (int a = threadIdx.x; a < A; a += 256) {
+    long ba = (long)b * A + a;
+    if (fg[ba] && tgi[ba] == j) {
+      ma = fmaxf(ma, align[(long)r * A + a]);
+      mo = fmaxf(mo, ovl[(long)r * A + a]);
+    }
+  }
+  sa[threadIdx.x] = ma;
+  so[threadIdx.x] = mo;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      sa[threadIdx.x] = fmaxf(sa[threadIdx.x], sa[threadIdx.x + o]);
+      so[threadIdx.x] = fmaxf(so[threadIdx.x], so[threadIdx.x + o]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    pos[r * 2] = sa[0];
+    pos[r * 2 + 1] = so[0];
+  }
+}
+
+// ---- fg pass: per (b, a); block partials [blk][6] = {sum tscore, sum (1-ciou)w, sum (1-nwd)w, sum dfl w,
+//      sum ciou, n_fg} ----
+template <typename T>
+__global__ void __launch_bounds__(256) loss_fg_kernel(Levels L, int B, int nmax, const float* gt, const float* pbox,
+                                                      const float* align, const int* tgi, const uint8_t* fg,
+                                                      const float* pos, float* tnorm, float* part) {
+  __shared__ float sh[6][256];
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  float acc[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (i < (long)B * L.A) {
+    int a = (int)(i % L.A), b = (int)(i / L.A);
+    float nrm = 0.f;
+    if (fg[i]) {
+      int j = tgi[i];
+      long r = (long)b * nmax + j;
+      float pa = pos[r * 2], po = pos[r * 2 + 1];
+      nrm = align[r * L.A + a] * po / (pa + 1e-9f);
+      int lvl;
+      float ax, ay;
+      const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
+      float st = L.st[lvl];
+      const float* g = gt + r * 5;
+      float tb[4] = {g[1] / st, g[2] / st, g[3] / st, g[4] / st};
+      const float* pb = pbox + i * 4;
+      float pbv[4] = {pb[0], pb[1], pb[2], pb[3]};
+      float ci = ciou(pbv, tb);
+      float nw = nwd(pbv, tb, nullptr);
+      // DFL (targets clamp to reg_max - 1 - 0.01)
+      float t[4] = {ax - tb[0], ay - tb[1], tb[2] - ax, tb[3] - ay};
+      float dfl = 0.f;
+      for (int k = 0; k < 4; ++k) {
+        float tk = fminf(fmaxf(t[k], 0.f), (float)(RM - 1) - 0.01f);
+        int tl = (int)tk;
+        float wl = (float)(tl + 1) - tk, wr = 1.f - wl;
+        float mx = -INFINITY;
+        for (int q = 0; q < RM; ++q) mx = fmaxf(mx, to_f(p[k * RM + q]));
+        float z = 0.f;
+        for (int q = 0; q < RM; ++q) z += expf(to_f(p[k * RM + q]) - mx);
+        float lse = mx + logf(z);
+        dfl += (lse - to_f(p[k * RM + tl])) * wl + (lse - to_f(p[k * RM + tl + 1])) * wr;
+      }
+      dfl *= 0.25f;
+      acc[0] = nrm;
+      acc[1] = (1.f - ci) * nrm;
+      acc[2] = (1.f - nw) * nrm;
+      acc[3] = dfl * nrm;
+      acc[4] = ci;
+      acc[5] = 1.f;
+    }
+    tnorm[i] = nrm;
+  }
+  for (int q = 0; q < 6; ++q) sh[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int q = 0; q < 6; ++q) sh[q][threadIdx.x] += sh[q][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    for (int q = 0; q < 6; ++q) part[(long)blockIdx.x * 6 + q] = sh[q][0];
+}
+
+// scal[0] = tss = max(sum tscore, 1); scal[1] = mu; scal[2..4] = box_iou, box_nwd, dfl sums (pre-gain)
+__global__ void loss_scalars_kernel(const float* part, int nblk, float* scal) {
+  if (threadIdx.x != 0) return;
+  double s[6] = {0, 0, 0, 0, 0, 0};
+  for (int k = 0; k < nblk; ++k)
+    for (int q = 0; q < 6; ++q) s[q] += part[(long)k * 6 + q];
+  float tss = fmaxf((float)s[0], 1.f);
+  float mu = s[5] > 0 ? (float)(s[4] / s[5]) : -1.f;
+  if (mu < 0.2f) mu = 0.2f;
+  scal[0] = tss;
+  scal[1] = mu;
+  scal[2] = (float)s[1];
+  scal[3] = (float)s[2];
+  scal[4] = (float)s[3];
+  scal[5] = (float)s[5];
+}
+
+// ---- cls pass + gradient rows: per (b, a); block partial of sum bce*mod ----
+template <typename T>
+__global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, int B, int nmax, int nc, float gscale,
+                                                            const float* gt, const float* pbox, const int* tgi,
+                                                            const uint8_t* fg, const float* tnorm, const float* scal,
+                                                            float* part, float box_gain, float cls_gain,
+                                                            float dfl_gain) {
+  __shared__ float sh[256];
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  float acc = 0.f;
+  if (i < (long)B * L.A) {
+    int a = (int)(i % L.A), b = (int)(i / L.A);
+    float tss = scal[0], mu = scal[1];
+    int lvl;
+    float ax, ay;
+    const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
+    T* gp = const_cast<T*>(feat_row<T>(G, b, a, lvl, ax, ay));
+    bool isfg = fg[i] != 0;
+    int lab = -1;
+    float nrm = tnorm[i];
+    long r = 0;
+    if (isfg) {
+      r = (long)b * nmax + tgi[i];
+      lab = (int)gt[r * 5];
+    }
+    float e21 = expf(1.f - mu);
+    float cscale = gscale * cls_gain / tss;
+    for (int c = 0; c < nc; ++c) {
+      float x = to_f(p[4 * RM + c]);
+      float t = (c == lab) ? nrm : 0.f;
+      float bce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
+      float mod = (t <= mu - 0.1f) ? 1.f : ((t < mu) ? e21 : expf(-(t - 1.f)));
+      acc += bce * mod;
+      float sg = 1.f / (1.f + expf(-x));
+      gp[4 * RM + c] = from_f<T>((sg - t) * mod * cscale);
+    }
+    // box + dfl gradient rows
+    float gbox[4] = {0.f, 0.f, 0.f, 0.f};
+    float gl[4][RM];
+    for (int k = 0; k < 4; ++k)
+      for (int q = 0; q < RM; ++q) gl[k][q] = 0.f;
+    if (isfg) {
+      float st = L.st[lvl];
+      const float* g = gt + r * 5;
+      float tb[4] = {g[1] / st, g[2] / st, g[3] / st, g[4] / st};
+      const float* pb = pbox + i * 4;
+      float pbv[4] = {pb[0], pb[1], pb[2], pb[3]};
+      float gc[4], gn[4];
+      ciou_grad(pbv, tb, gc);
+      nwd(pbv, tb, gn);
+      float wb = gscale * box_gain * 0.5f * nrm / tss;
+      for (int k = 0; k < 4; ++k) gbox[k] = -wb * (gc[k] + gn[k]);
+      // d/d dist: x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3
+      float gd[4] = {-gbox[0], -gbox[1], gbox[2], gbox[3]};
+      float t[4] = {ax - tb[0], ay - tb[1], tb[2] - ax, tb[3] - ay};
+      float wd = gscale * dfl_gain * 0.25f * nrm / tss;
+      for (int k = 0; k < 4; ++k) {
+        float mx = -INFINITY;
+        for (int q = 0; q < RM; ++q) mx = fmaxf(mx, to_f(p[k * RM + q]));
+        float z = 0.f, e = 0.f;
+        float s[RM];
+        for (int q = 0; q < RM; ++q) {
+          s[q] = expf(to_f(p[k * RM + q]) - mx);
+          z += s[q];
+        }
+        for (int q = 0; q < RM; ++q) {
+          s[q] /= z;
+          e += s[q] * (float)q;
+        }
+        float tk = fminf(fmaxf(t[k], 0.f), (float)(RM - 1) - 0.01f);
+        int tl = (int)tk;
+        float wl = (float)(tl + 1) - tk, wr = 1.f - wl;
+        for (int q = 0; q < RM; ++q) {
+          float gdist = gd[k] * s[q] * ((float)q - e);
+          float gdfl = wd * (s[q] - (q == tl ? wl : 0.f) - (q == tl + 1 ? wr : 0.f));
+          gl[k][q] = gdist + gdfl;
+        }
+      }
+    }
+    for (int k = 0; k < 4; ++k)
+      for (int q = 0; q < RM; ++q) gp[k * RM + q] = from_f<T>(gl[k][q]);
+  }
+  sh[threadIdx.x] = acc;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
+}
+
+// out[0..2] = (box, cls, dfl) after gains; out[3] = (sum) * B ; out[4] = n_fg
+__global__ void loss_final_kernel(const float* part, int nblk, const float* scal, int B, float box_gain,
+                                  float cls_gain, float dfl_gain, float* out) {
+  if (threadIdx.x != 0) return;
+  double s = 0;
+  for (int k = 0; k < nblk; ++k) s += part[k];
+  float tss = scal[0];
+  float box = 0.f, dfl = 0.f;
+  if (scal[5] > 0) {
+    box = 0.5f * (scal[2] / tss) + 0.5f * (scal[3] / tss);
+    dfl = scal[4] / tss;
+  }
+  float cls = (float)(s / tss);
+  out[0] = box * box_gain;
+  out[1] = cls * cls_gain;
+  out[2] = dfl * dfl_gain;
+  out[3] = (out[0] + out[1] + out[2]) * (float)B;
+  out[4] = scal[5];
+}
+
+}  // namespace adr
+
+using namespace adr;
+
+extern "C" size_t adr_det_loss_workspace(int B, int nmax, int A) {
+  size_t n = (size_t)B * A;
+  size_t rows = (size_t)B * nmax;
+  size_t nblk = (n + 255) / 256;
+  return n * 4 * 4                 // pbox
+         + rows * A * 4 * 2        // align, overlaps
+         + rows * A                // flags
+         + n * 4                   // tgi
+         + n                       // fg
+         + rows * 2 * 4            // pos
+         + n * 4                   // tnorm
+         + nblk * 6 * 4 + 64       // fg partials + scalars
+         + nblk * 4 + 256;         // cls partials
+}
+
+extern "C" int adr_det_loss(int dtype, const void* f0, const void* f1, const void* f2, int cs0, int cs1, int cs2,
+                            int H0, int W0, int H1, int W1, int H2, int W2, float s0, float s1, float s2, int B, int nc,
+                            const float* gt, int nmax, void* g0, void* g1, void* g2, float grad_scale, float box_gain,
+                            float cls_gain, float dfl_gain, float* out, void* ws, size_t ws_bytes, void* stream) {
+  Levels L;
+  L.f[0] = f0; L.f[1] = f1; L.f[2] = f2;
+  L.cs[0] = cs0; L.cs[1] = cs1; L.cs[2] = cs2;
+  L.H[0] = H0; L.H[1] = H1; L.H[2] = H2;
+  L.W[0] = W0; L.W[1] = W1; L.W[2] = W2;
+  L.st[0] = s0; L.st[1] = s1; L.st[2] = s2;
+  L.A = H0 * W0 + H1 * W1 + H2 * W2;
+  Levels G = L;
+  G.f[0] = g0; G.f[1] = g1; G.f[2] = g2;
+  G.cs[0] = 4 * RM + nc; G.cs[1] = 4 * RM + nc; G.cs[2] = 4 * RM + nc;
+  int A = L.A;
+  ADR_REQUIRE(ws_bytes >= adr_det_loss_workspace(B, nmax, A), "det_loss: workspace");
+  ADR_REQUIRE(cs0 >= 4 * RM + nc && cs1 >= 4 * RM + nc && cs2 >= 4 * RM + nc, "det_loss: head rows too short");
+  hipStream_t st = (hipStream_t)stream;
+  char* w = (char*)ws;
+  size_t n = (size_t)B * A, rows = (size_t)B * nmax;
+  float* pbox = (float*)w; w += n * 16;
+  float* align = (float*)w; w += rows * A * 4;
+  float* ovl = (float*)w; w += rows * A * 4;
+  uint8_t* flags = (uint8_t*)w; w += rows * A;
+  w = (char*)(((uintptr_t)w + 15) & ~(uintptr_t)15);
+  int* tgi = (int*)w; w += n * 4;
+  uint8_t* fg = (uint8_t*)w; w += n;
+  w = (char*)(((uintptr_t)w + 15) & ~(uintptr_t)15);
+  float* pos = (float*)w; w += rows * 8;
+  float* tnorm = (float*)w; w += n * 4;
+  int nblk = cdiv((long)n, 256);
+  float* part = (float*)w; w += (size_t)nblk * 24;
+  float* scal = (float*)w; w += 64;
+  float* part2 = (float*)w;
+  (void)w;
+#define LDISPATCH(KERN, grid, block, ...)                                                 \
+  do {                                                                                    \
+    if (dtype == ADR_BF16) hipLaunchKernelGGL(KERN<__bf16>, grid, block, 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERN<float>, grid, block, 0, st, __VA_ARGS__);                \
+  } while (0)
+  LDISPATCH(loss_decode_kernel, dim3(cdiv((long)n, 256)), dim3(256), L, B, pbox);
+  if (nmax > 0) {
+    long tot = (long)rows * A;
+    LDISPATCH(tal_metrics_kernel, dim3(cdiv(tot, 256)), dim3(256), L, B, nmax, nc, gt, pbox, align, ovl, flags);
+    hipLaunchKernelGGL(tal_topk_kernel, dim3(cdiv((long)rows, 64)), dim3(64), 0, st, align, flags, (int)rows, A);
+    hipLaunchKernelGGL(tal_assign_kernel, dim3(cdiv((long)n, 256)), dim3(256), 0, st, flags, ovl, B, nmax, A, tgi, fg);
+    hipLaunchKernelGGL(tal_norm_kernel, dim3((unsigned)rows), dim3(256), 0, st, align, ovl, tgi, fg, B, nmax, A, pos);
+  } else {
+    hipMemsetAsync(fg, 0, n, st);
+    hipMemsetAsync(tgi, 0, n * 4, st);
+  }
+  LDISPATCH(loss_fg_kernel, dim3(nblk), dim3(256), L, B, nmax, gt, pbox, align, tgi, fg, pos, tnorm, part);
+  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(64), 0, st, part, nblk, scal);
+  LDISPATCH(loss_cls_grad_kernel, dim3(nblk), dim3(256), L, G, B, nmax, nc, grad_scale, gt, pbox, tgi, fg, tnorm, scal,
+            part2, box_gain, cls_gain, dfl_gain);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, st, part2, nblk, scal, B, box_gain, cls_gain, dfl_gain,
+                     out);
+#undef LDISPATCH
+  return check_launch("adr_det_loss");
+}
