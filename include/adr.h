@@ -126,6 +126,8 @@ int adr_dot_reduce(int dtype, const void* x, int xcs, const void* dz, int dcs, i
                    int rows_per_chunk, float* partial, void* stream);
 int adr_nc_collapse(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n, int sum_c,
                     int accumulate, void* stream);
+/* y += a*x over n fp32 values (gradient accumulation into the trainer's flat gradient arena). */
+int adr_axpy(long n, float a, const float* x, float* y, void* stream);
 /* BiFPN weights w = relu(fw)/(sum relu(fw)+eps) and backward (block.py:1532-1535). */
 int adr_fusion_weights(const float* fw, int n, float eps, float* w, void* stream);
 int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream);
@@ -261,6 +263,23 @@ int adr_det_loss(int dtype, const void* f0, const void* f1, const void* f2, int 
                  int H1, int W1, int H2, int W2, float s0, float s1, float s2, int B, int nc, const float* gt,
                  int nmax, void* g0, void* g1, void* g2, float grad_scale, float box_gain, float cls_gain,
                  float dfl_gain, float* out, void* ws, size_t ws_bytes, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------
+ * Trainer tail (engine/trainer.py:580-588, 753-813; utils/torch_utils.py:521-546) over a chunk table:
+ * entry = {float* p; const float* g; float* momentum_buf; float* ema; int64 n; int group; int pad}
+ * (group 0 decayed weights, 1 norm weights, 2 biases, 3 buffers / frozen: EMA only);
+ * chunk = {int entry; int pad; int64 start; int64 len}. Both tables live in device memory.
+ * adr_opt_step: clip_grad_norm_(10) + SGD(momentum, nesterov, per-group lr / weight decay) + EMA
+ * (ema = d*ema + (1-d)*p after the update); norm_out (optional) receives the pre-clip total norm. */
+int adr_opt_entry_size(void);
+int adr_opt_chunk_size(void);
+int adr_opt_step(const void* tab, const void* chunks, int nchunks, float* partial, float max_norm, float lr0,
+                 float lr1, float lr2, float wd0, float wd1, float wd2, float momentum, int nesterov, int first,
+                 float ema_decay, float* norm_out, void* stream);
+/* gradient (or, when g == NULL, value) gather into / scatter from a flat fp32 buffer at per-entry offsets
+ * (the DDP all-reduce bucket). */
+int adr_flat_copy(const void* tab, const void* chunks, int nchunks, float* flat, const int64_t* offsets,
+                  int to_flat, void* stream);
 
 #ifdef __cplusplus
 }

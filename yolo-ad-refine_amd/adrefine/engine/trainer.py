@@ -1,0 +1,152 @@
+"""Training step for the AD-Refine hot path — the reference trainer's step semantics
+(engine/trainer.py:383-398, optimizer_step :580-588, build_optimizer :753-813, ModelEMA torch_utils.py:521-546,
+DDP :217-273) on libadr_hip:
+
+  zero the flat fp32 gradient arena (one hipMemsetAsync)
+  forward + v8DetectionLoss + backward   (HIP kernels; every parameter gradient is accumulated by its
+                                          kernel straight into the arena — no per-parameter grad tensors)
+  [DDP] all-reduce SUM of the arena over RCCL (== the reference's loss*world_size followed by DDP's average)
+  clip_grad_norm_(10) + SGD(momentum, nesterov=True, 3 param groups) + EMA   (one fused multi-tensor pair)
+
+Parameters that never receive a gradient (e.g. AdaptiveDynamicTanh.scale_weights, unused by the reference's
+forward) are skipped by SGD exactly like torch.optim.SGD skips p.grad is None.
+Mixed precision: the reference runs fp16 autocast + GradScaler; this build computes in bf16 (fp32 exponent
+range), so no loss scaling is needed and the GradScaler is the identity.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from .. import kernels as K
+from ..native import lib
+
+_NORM_TYPES = tuple(v for k, v in nn.__dict__.items() if "Norm" in k and isinstance(v, type))
+_ENTRY = np.dtype([("p", "<u8"), ("g", "<u8"), ("b", "<u8"), ("e", "<u8"), ("n", "<i8"), ("grp", "<i4"),
+                   ("pad", "<i4")])
+_CHUNK = np.dtype([("e", "<i4"), ("p", "<i4"), ("s", "<i8"), ("l", "<i8")])
+
+
+def param_groups(model):
+    """build_optimizer grouping (trainer.py:781-789): 'bias' in name -> g2; norm-layer weights -> g1; else g0."""
+    g = [], [], []
+    for mname, module in model.named_modules():
+        for pname, p in module.named_parameters(recurse=False):
+            if not p.requires_grad:
+                continue
+            full = f"{mname}.{pname}" if mname else pname
+            if "bias" in full:
+                g[2].append((full, p))
+            elif isinstance(module, _NORM_TYPES):
+                g[1].append((full, p))
+            else:
+                g[0].append((full, p))
+    return g
+
+
+class FusedTrainer:
+    """One process per GPU. `step(batch)` = zero grads + fwd + loss + bwd (+ all-reduce) + clip + SGD + EMA;
+    returns the loss items (device tensor, no host sync)."""
+
+    CHUNK = 1 << 16
+
+    def __init__(self, model, lr0=0.01, momentum=0.937, weight_decay=5e-4, nbs=64, batch_size=64, world_size=1,
+                 process_group=None, ema=True, ema_decay=0.9999, ema_tau=2000, max_norm=10.0):
+        self.model = model
+        self.world_size = world_size
+        self.pg = process_group
+        self.momentum = momentum
+        self.max_norm = max_norm
+        accumulate = max(round(nbs / batch_size), 1)
+        self.wd = weight_decay * batch_size * accumulate / nbs  # trainer.py:305-306
+        self.lr = [lr0, lr0, lr0]
+        self.dev = dev = next(model.parameters()).device
+        groups = param_groups(model)
+        self.entries = [(name, p, gi, True) for gi, lst in enumerate(groups) for name, p in lst]
+        self.nparam = sum(p.numel() for _, p, _, _ in self.entries)
+        self.grad = torch.zeros(self.nparam, dtype=torch.float32, device=dev)
+        self.mom = torch.zeros(self.nparam, dtype=torch.float32, device=dev)
+        off = 0
+        self._goff = []
+        for _, p, _, _ in self.entries:
+            p._adr_grad = self.grad[off:off + p.numel()]
+            p._adr_used = False
+            self._goff.append(off)
+            off += p.numel()
+        # EMA over every floating state entry (params + BN running stats), buffers as group 3
+        self.use_ema = ema
+        pset = {id(p) for _, p, _, _ in self.entries}
+        for k, v in model.state_dict(keep_vars=True).items():
+            if v.dtype.is_floating_point and id(v) not in pset:
+                self.entries.append((k, v, 3, False))
+                self._goff.append(-1)
+        ntot = sum(t.numel() for _, t, _, _ in self.entries)
+        self.ema_flat = torch.empty(ntot, dtype=torch.float32, device=dev) if ema else None
+        self._eoff, chunks, off = [], [], 0
+        for ei, (_, t, _, _) in enumerate(self.entries):
+            self._eoff.append(off)
+            n = t.numel()
+            for s in range(0, n, self.CHUNK):
+                chunks.append((ei, 0, s, min(self.CHUNK, n - s)))
+            if ema:
+                self.ema_flat[off:off + n].copy_(t.detach().reshape(-1))
+            off += n
+        self.nchunks = len(chunks)
+        assert lib.adr_opt_entry_size() == _ENTRY.itemsize and lib.adr_opt_chunk_size() == _CHUNK.itemsize
+        self.chunks_dev = torch.from_numpy(np.array(chunks, dtype=_CHUNK).view(np.uint8).copy()).to(dev)
+        self.partial = torch.empty(self.nchunks, dtype=torch.float32, device=dev)
+        self.norm = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.tab_dev = None
+        self.updates = 0
+        self.ema_decay = ema_decay
+        self.ema_tau = ema_tau
+
+    def _build_table(self):
+        tab = np.zeros(len(self.entries), dtype=_ENTRY)
+        for ei, (_, t, g, isp) in enumerate(self.entries):
+            used = isp and getattr(t, "_adr_used", False)
+            tab["p"][ei] = t.data_ptr()
+            tab["g"][ei] = self.grad.data_ptr() + 4 * self._goff[ei] if used else 0
+            tab["b"][ei] = self.mom.data_ptr() + 4 * self._goff[ei] if isp else 0
+            tab["e"][ei] = self.ema_flat.data_ptr() + 4 * self._eoff[ei] if self.use_ema else 0
+            tab["n"][ei] = t.numel()
+            tab["grp"][ei] = g if used else 3
+        self.tab_dev = torch.from_numpy(tab.view(np.uint8).copy()).to(self.dev)
+
+    def forward_backward(self, batch):
+        K.zero_(self.grad)
+        self.model.train()
+        loss, items = self.model(batch)
+        loss.backward()
+        return items
+
+    def step(self, batch):
+        items = self.forward_backward(batch)
+        if self.world_size > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.pg)
+        if self.tab_dev is None:  # the set of parameters that receive gradients is static: build once
+            self._build_table()
+        d = self.ema_decay * (1 - math.exp(-(self.updates + 1) / self.ema_tau))
+        lib.adr_opt_step(K.fptr(self.tab_dev), K.fptr(self.chunks_dev), self.nchunks, K.fptr(self.partial),
+                         float(self.max_norm), float(self.lr[0]), float(self.lr[1]), float(self.lr[2]), float(self.wd),
+                         0.0, 0.0, float(self.momentum), 1, int(self.updates == 0), float(d), K.fptr(self.norm),
+                         K.stream())
+        self.updates += 1
+        return items.detach()
+
+    def param_grad(self, name):
+        for ei, (n, t, _, isp) in enumerate(self.entries):
+            if n == name and isp:
+                return self.grad[self._goff[ei]:self._goff[ei] + t.numel()].view(t.shape)
+        raise KeyError(name)
+
+    def ema_state_dict(self):
+        out = {}
+        for ei, (name, t, _, _) in enumerate(self.entries):
+            off = self._eoff[ei]
+            out[name] = self.ema_flat[off:off + t.numel()].view(t.shape)
+        return out

@@ -67,6 +67,51 @@ def fptr(t):
     return None if t is None else ctypes.c_void_p(t.data_ptr())
 
 
+def _target(t):
+    """The Parameter owning gradient-arena storage for t (t itself, or the base of a reshaped view)."""
+    if t is None:
+        return None
+    if hasattr(t, "_adr_grad"):
+        return t
+    b = getattr(t, "_base", None)
+    if b is not None and hasattr(b, "_adr_grad"):
+        return b
+    return None
+
+
+def sink(t, g):
+    """Route a parameter gradient: accumulate into the trainer's flat fp32 gradient arena when the parameter
+    has one (returns None to autograd), otherwise hand it back to autograd unchanged."""
+    if g is None:
+        return None
+    tgt = _target(t)
+    if tgt is None:
+        return g
+    gc = g.detach().float()
+    if not gc.is_contiguous():
+        relayout_count[0] += 1
+        gc = gc.contiguous()
+    if gc.numel() != tgt.numel():
+        raise RuntimeError("sink: gradient size mismatch")
+    lib.adr_axpy(gc.numel(), 1.0, fptr(gc), fptr(tgt._adr_grad), stream())
+    tgt._adr_used = True
+    return None
+
+
+def sink_unpack(t, dw_krsc, shape, cpad=0):
+    """unpack_weight_grad straight into the gradient arena (accumulate) when t has one."""
+    tgt = _target(t)
+    if tgt is None:
+        return unpack_weight_grad(dw_krsc, shape, cpad)
+    K_, C_ = shape[0], shape[1]
+    RS = 1
+    for d in shape[2:]:
+        RS *= d
+    lib.adr_unpack_weight_grad(fptr(dw_krsc), fptr(tgt._adr_grad), K_, C_, max(C_, cpad), RS, 0, 1, stream())
+    tgt._adr_used = True
+    return None
+
+
 def pack_weight(w: torch.Tensor, dtype, cpad: int = 0, transpose_kc: int = 0):
     """(K, C, R, S) fp32 parameter -> KRSC operand in the compute dtype (channel-padded to cpad)."""
     K, C = w.shape[0], w.shape[1]
@@ -149,6 +194,7 @@ class Conv2dFn(torch.autograd.Function):
                            fptr(stats), 0, stream())
         ctx.save_for_backward(x, wp)
         ctx.meta = (stride, pad, cpad, w.shape, b is not None)
+        ctx.pw, ctx.pb = w, b
         if stats is None:
             stats = torch.empty(0, device=x.device)
         ctx.mark_non_differentiable(stats)
@@ -172,9 +218,9 @@ class Conv2dFn(torch.autograd.Function):
                                  ctypes.c_void_p(dx.data_ptr()), 0, stream())
         if ctx.needs_input_grad[1]:
             dwk = _wgrad(d, xp, dyp, K, C, R * S, x.device)
-            dw = unpack_weight_grad(dwk, wshape, cpad)
+            dw = sink_unpack(ctx.pw, dwk, wshape, cpad)
         if has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad(dy, K, N, Ho * Wo, dycs)
+            db = sink(ctx.pb, _bias_grad(dy, K, N, Ho * Wo, dycs))
         return dx, dw, db, None, None, None, None
 
 
@@ -199,6 +245,7 @@ class ConvT2dFn(torch.autograd.Function):
                              0, stream())
         ctx.save_for_backward(x, wp)
         ctx.meta = (stride, pad, w.shape, b is not None, Ho, Wo)
+        ctx.pw, ctx.pb = w, b
         return y
 
     @staticmethod
@@ -219,9 +266,9 @@ class ConvT2dFn(torch.autograd.Function):
             # equivalent conv: input = dy_T (N, Ho, Wo, Co), output grad = x_T (N, H, W, Ci)
             d, _, _ = conv_desc(N, Ho, Wo, Co, dycs, Ci, R, S, stride, stride, pad, pad, xcs, x.dtype)
             dwk = _wgrad(d, dyp, xp, Ci, Co, R * S, x.device)
-            dw = unpack_weight_grad(dwk, wshape)
+            dw = sink_unpack(ctx.pw, dwk, wshape)
         if has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad(dy, Co, N, Ho * Wo, dycs)
+            db = sink(ctx.pb, _bias_grad(dy, Co, N, Ho * Wo, dycs))
         return dx, dw, db, None, None, None
 
 
@@ -254,6 +301,7 @@ class BNActFn(torch.autograd.Function):
                            fptr(scale), fptr(shift), 0, ACT[act], N, HW, C, stream())
         ctx.save_for_backward(y, scale, shift, mean, rstd, gamma)
         ctx.meta = (act, training)
+        ctx.pbeta = beta
         return z
 
     @staticmethod
@@ -278,7 +326,7 @@ class BNActFn(torch.autograd.Function):
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
                                fptr(Cc), 0, 0, ACT[act], N, HW, C, 0, stream())
-        return dy, None, dgamma, dbeta, None, None, None, None, None, None
+        return dy, None, sink(gamma, dgamma), sink(ctx.pbeta, dbeta), None, None, None, None, None, None
 
 
 class GNActFn(torch.autograd.Function):
@@ -307,6 +355,7 @@ class GNActFn(torch.autograd.Function):
                            fptr(scale), fptr(shift), 1, ACT[act], N, HW, C, stream())
         ctx.save_for_backward(y, scale, shift, mean, rstd, gamma)
         ctx.meta = (groups, act)
+        ctx.pbeta = beta
         return z
 
     @staticmethod
@@ -334,7 +383,7 @@ class GNActFn(torch.autograd.Function):
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
                                fptr(Cc), 1, 1, ACT[act], N, HW, C, 0, stream())
-        return dy, dgamma, dbeta, None, None, None
+        return dy, sink(gamma, dgamma), sink(ctx.pbeta, dbeta), None, None, None
 
 
 def image_to_nhwc(img: torch.Tensor, dtype, cpad=8):
@@ -604,6 +653,7 @@ class ScaleFn(torch.autograd.Function):
                           C, N, H * W, C, 0, stream())
         ctx.save_for_backward(vx[0], gs)
         ctx.meta = (mode, g.shape, res is not None)
+        ctx.pg = g
         return out
 
     @staticmethod
@@ -621,7 +671,7 @@ class ScaleFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             sum_n = mode in ("scalar", "c")
             sum_c = mode in ("scalar", "n")
-            dg = _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape)
+            dg = sink(ctx.pg, _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape))
         return dx, dg, (dy if has_res else None), None
 
 
@@ -648,6 +698,7 @@ class WeightedSumFn(torch.autograd.Function):
             _ew(EW_AXPBY, vo, vi, vi, ca=wd[i:i + 1], cb=torch.zeros(1, device=w.device), accumulate=1)
         ctx.save_for_backward(wd, *[_v(x)[0] for x in xs])
         ctx.has_base = base is not None
+        ctx.pw = w
         return out
 
     @staticmethod
@@ -660,7 +711,7 @@ class WeightedSumFn(torch.autograd.Function):
             _ew(EW_AXPBY, (d, d.data_ptr(), d.shape[1]), vd, vd, ca=wd[i:i + 1], cb=torch.zeros(1, device=dy.device))
             dxs.append(d)
         dw = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs]) if ctx.needs_input_grad[0] else None
-        return (dw, dy if ctx.has_base else None, *dxs)
+        return (sink(ctx.pw, dw), dy if ctx.has_base else None, *dxs)
 
 
 def weighted_sum(w, xs, base=None):
@@ -682,6 +733,7 @@ class FusionFn(torch.autograd.Function):
         for i in range(2, len(xs)):
             _ew(EW_AXPBY, vo, v[i], v[i], ca=w[i:i + 1], cb=torch.zeros(1, device=fw.device), accumulate=1)
         ctx.save_for_backward(fwd, w, *[t[0] for t in v])
+        ctx.pfw = fw
         return out
 
     @staticmethod
@@ -697,7 +749,7 @@ class FusionFn(torch.autograd.Function):
         dwn = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs])
         dfw = torch.empty_like(fwd)
         lib.adr_fusion_weights_bwd(fptr(fwd), fwd.numel(), 1e-4, fptr(dwn), fptr(dfw), stream())
-        return (dfw, *dxs)
+        return (sink(ctx.pfw, dfw), *dxs)
 
 
 def fusion(fw, xs):
@@ -757,6 +809,7 @@ class MLCAFn(torch.autograd.Function):
                          float(local_weight), fptr(local), fptr(att), fptr(sig_l), fptr(sig_g), stream())
         ctx.save_for_backward(vy[0], wlf, wgf, local, att, sig_l, sig_g)
         ctx.meta = (local_weight, res is not None, wl.shape, wg.shape)
+        ctx.pwl, ctx.pwg = wl, wg
         return out
 
     @staticmethod
@@ -775,7 +828,7 @@ class MLCAFn(torch.autograd.Function):
                          ctypes.c_void_p(dy.data_ptr()), C, N, H, W, C, fptr(wlf), fptr(wgf), k, float(lw),
                          fptr(local), fptr(att), fptr(sig_l), fptr(sig_g), fptr(dwl), fptr(dwg), fptr(ws), wsb,
                          stream())
-        return dy, (dout if has_res else None), dwl.view(wls), dwg.view(wgs), None
+        return dy, (dout if has_res else None), sink(ctx.pwl, dwl.view(wls)), sink(ctx.pwg, dwg.view(wgs)), None
 
 
 def mlca(y, res, wl, wg, local_weight=0.5):
@@ -949,6 +1002,7 @@ class GateMLPFn(torch.autograd.Function):
                          fptr(hidden), fptr(out), stream())
         ctx.save_for_backward(vv, w1, w2, hidden, out)
         ctx.meta = (a1, a2, W1.shape, W2.shape, b1 is not None, b2 is not None)
+        ctx.params = (W1, b1, W2, b2)
         return out
 
     @staticmethod
@@ -966,7 +1020,9 @@ class GateMLPFn(torch.autograd.Function):
         db2 = torch.empty(H2, dtype=torch.float32, device=dev)
         lib.adr_gate_mlp_bwd(fptr(vv), 1.0, N, Cin, fptr(w1), H1, a1, fptr(w2), H2, a2, fptr(hidden), fptr(out),
                              fptr(d), fptr(din), fptr(dW1), fptr(db1), fptr(dW2), fptr(db2), stream())
-        return din, dW1.view(s1), db1 if hb1 else None, dW2.view(s2), db2 if hb2 else None, None, None
+        W1p, b1p, W2p, b2p = ctx.params
+        return (din, sink(W1p, dW1.view(s1)), sink(b1p, db1) if hb1 else None, sink(W2p, dW2.view(s2)),
+                sink(b2p, db2) if hb2 else None, None, None)
 
 
 def gate_mlp(v, W1, b1, W2, b2, act1, act2):
@@ -1000,6 +1056,7 @@ class PaddedConvFn(torch.autograd.Function):
                            None, 0, stream())
         ctx.save_for_backward(x, wp)
         ctx.meta = (stride, pad, kpad, w.shape, b is not None)
+        ctx.pw, ctx.pb = w, b
         return y
 
     @staticmethod
@@ -1019,9 +1076,9 @@ class PaddedConvFn(torch.autograd.Function):
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, kpad, R, S, stride, stride, pad, pad, dycs, x.dtype)
         if ctx.needs_input_grad[1]:
             dwk = _wgrad(d, xp, dyp, kpad, C, R * S, x.device)
-            dw = unpack_weight_grad(dwk, wshape)  # first K rows of the [kpad][RS][C] gradient
+            dw = sink_unpack(ctx.pw, dwk, wshape)  # first K rows of the [kpad][RS][C] gradient
         if has_b and ctx.needs_input_grad[2]:
-            db = _bias_grad(dy, kpad, N, Ho * Wo, dycs)[:K]
+            db = sink(ctx.pb, _bias_grad(dy, kpad, N, Ho * Wo, dycs)[:K])
         return dx, dw, db, None, None, None
 
 
@@ -1044,6 +1101,7 @@ class DCNFn(torch.autograd.Function):
         lib.adr_conv2d_fwd(ctypes.byref(d), fptr(cols), fptr(wp), None, ctypes.c_void_p(y.data_ptr()), None, 0,
                            stream())
         ctx.save_for_backward(x, om, cols, w)
+        ctx.pw = w
         return y
 
     @staticmethod
@@ -1066,7 +1124,7 @@ class DCNFn(torch.autograd.Function):
         if ctx.needs_input_grad[2]:
             dwd, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, dycs, dtype)
             dwk = _wgrad(dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, dev)
-            dw = unpack_weight_grad(dwk, w.shape)
+            dw = sink_unpack(ctx.pw, dwk, w.shape)
         dx32 = zero_(torch.empty(N * H * W * C, dtype=torch.float32, device=dev))
         dom = zero_(empty_act(N, om.shape[1], H, W, dtype, dev))
         lib.adr_dcn_col2im(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(dcols), fptr(dx32),
@@ -1143,6 +1201,7 @@ class DWConvFn(torch.autograd.Function):
                            ctypes.c_void_p(y.data_ptr()), C, N, H, W, C, k, stream())
         ctx.save_for_backward(vx[0], wf)
         ctx.meta = (k, w.shape, b is not None)
+        ctx.pw, ctx.pb = w, b
         return y
 
     @staticmethod
@@ -1159,7 +1218,7 @@ class DWConvFn(torch.autograd.Function):
                            ctypes.c_void_p(dx.data_ptr()) if dx is not None else None, C, fptr(dw), N, H, W, C, k, 0,
                            fptr(ws), wsb, stream())
         db = _bias_grad(vd[0], C, N, H * W, vd[2]) if has_b and ctx.needs_input_grad[2] else None
-        return dx, (dw.view(wshape) if dw is not None else None), db, None
+        return dx, (sink(ctx.pw, dw.view(wshape)) if dw is not None else None), sink(ctx.pb, db), None
 
 
 def dwconv(x, w, b, k):
@@ -1181,6 +1240,7 @@ class ADyTFn(torch.autograd.Function):
                          ctypes.c_void_p(y.data_ptr()), C, N, H * W, C, stream())
         ctx.save_for_backward(vx[0], a, im, wf)
         ctx.ashape = alphas.shape
+        ctx.params = (alphas, w, b)
         return y
 
     @staticmethod
@@ -1199,7 +1259,8 @@ class ADyTFn(torch.autograd.Function):
         lib.adr_adyt_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]), vd[2], fptr(a), fptr(im),
                          fptr(wf), ctypes.c_void_p(dx.data_ptr()), C, fptr(dimp), fptr(da), fptr(dw), fptr(db), N,
                          H * W, C, fptr(ws), wsb, stream())
-        return dx, da.view(ctx.ashape), dimp, dw, db
+        pa, pw, pb = ctx.params
+        return dx, sink(pa, da.view(ctx.ashape)), dimp, sink(pw, dw), sink(pb, db)
 
 
 def adyt(x, alphas, imp, w, b):
@@ -1252,6 +1313,7 @@ class TSSAStackFn(torch.autograd.Function):
                              S * N, fptr(Pi[s]), fptr(ss[s]), fptr(att[s]), stream())
         ctx.save_for_backward(tf, Pi, ss, att, *saved)
         ctx.meta = (heads, temps.shape)
+        ctx.pt = temps
         return out
 
     @staticmethod
@@ -1277,7 +1339,7 @@ class TSSAStackFn(torch.autograd.Function):
                              fptr(Pi[s]), fptr(ss[s]), fptr(att[s]), ctypes.c_void_p(gp), ctypes.c_void_p(gp + C * es),
                              ctypes.c_void_p(gp + 2 * C * es), C3, fptr(dtemp[s]), fptr(ws), stream())
             grads.append(g)
-        return (dtemp.view(tshape), None, *grads)
+        return (sink(ctx.pt, dtemp.view(tshape)), None, *grads)
 
 
 def tssa_stack(temps, heads, qkvs):
@@ -1442,6 +1504,7 @@ class EDFFNFilterFn(torch.autograd.Function):
                           stream())
         ctx.save_for_backward(t, M)
         ctx.meta = (fft.shape, wf.shape[1])
+        ctx.pf = fft
         return y
 
     @staticmethod
@@ -1458,7 +1521,7 @@ class EDFFNFilterFn(torch.autograd.Function):
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=t.device)
         lib.adr_edffn_bwd(dcode(t.dtype), ctypes.c_void_p(p), cs, ctypes.c_void_p(dp), dcs, fptr(M), fptr(basis), nuv,
                           ctypes.c_void_p(dx.data_ptr()), C, fptr(dw), N, H, W, C, fptr(ws), wsb, stream())
-        return dx, dw.view(fshape)
+        return dx, sink(ctx.pf, dw.view(fshape))
 
 
 def edffn_filter(x, fft):

@@ -196,6 +196,11 @@ __global__ void fusion_weights_bwd_kernel(const float* fw, int n, float eps, con
   }
 }
 
+__global__ void axpy_kernel(long n, float a, const float* x, float* y) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] += a * x[i];
+}
+
 static int ew_grid(long work) {
   long b = (work + 255) / 256;
   if (b > 32768) b = 32768;
@@ -273,4 +278,10 @@ extern "C" int adr_fusion_weights(const float* fw, int n, float eps, float* w, v
 extern "C" int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream) {
   hipLaunchKernelGGL(fusion_weights_bwd_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, fw, n, eps, dw, dfw);
   return check_launch("adr_fusion_weights_bwd");
+}
+
+extern "C" int adr_axpy(long n, float a, const float* x, float* y, void* stream) {
+  if (n <= 0) return ADR_OK;
+  hipLaunchKernelGGL(axpy_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, n, a, x, y);
+  return check_launch("adr_axpy");
 }

@@ -1,0 +1,124 @@
+// Fused trainer tail (reference engine/trainer.py:580-588 optimizer_step, :753-813 build_optimizer,
+// utils/torch_utils.py:521-546 ModelEMA): multi-tensor gradient-norm clip (clip_grad_norm_ max_norm 10),
+// SGD with Nesterov momentum and per-group weight decay / lr (torch.optim.SGD semantics), and the EMA of every
+// floating-point model state entry, in two launches over a chunk table. Deterministic: the global norm is a
+// fixed-order reduction of per-chunk partials, recomputed identically by every block.
+#include "adr_common.h"
+
+namespace adr {
+
+struct OptEntry {
+  float* p;          // parameter or buffer (fp32)
+  const float* g;    // gradient (null: no update, e.g. buffers / frozen params)
+  float* buf;        // momentum buffer
+  float* ema;        // EMA copy (null: none)
+  long n;
+  int group;         // 0 decay weights, 1 norm weights, 2 biases, 3 buffer / frozen (EMA only)
+  int pad;
+};
+
+struct OptChunk {
+  int entry;
+  int pad;
+  long start, len;
+};
+
+__global__ void __launch_bounds__(256) grad_sqnorm_kernel(const OptEntry* tab, const OptChunk* chunks, float* partial) {
+  const OptChunk ck = chunks[blockIdx.x];
+  const OptEntry e = tab[ck.entry];
+  __shared__ double sh[256];
+  double s = 0.0;
+  if (e.g && e.group < 3)
+    for (long i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
+      double v = e.g[i];
+      s += v * v;
+    }
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) partial[blockIdx.x] = (float)sh[0];
+}
+
+// lr[3], wd[3] per group; clip coef from partials; EMA decay d (host-computed from the update count)
+__global__ void __launch_bounds__(256) sgd_ema_kernel(const OptEntry* tab, const OptChunk* chunks, int nchunks,
+                                                      const float* partial, float max_norm, float lr0, float lr1,
+                                                      float lr2, float wd0, float wd1, float wd2, float momentum,
+                                                      int nesterov, int first, float ema_d, float* norm_out) {
+  __shared__ double sh[256];
+  __shared__ float coef_s;
+  double s = 0.0;
+  for (int k = threadIdx.x; k < nchunks; k += 256) s += partial[k];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    float tn = (float)sqrt(sh[0]);
+    float c = max_norm > 0.f ? max_norm / (tn + 1e-6f) : 1.f;
+    coef_s = c < 1.f ? c : 1.f;
+    if (blockIdx.x == 0 && norm_out) norm_out[0] = tn;
+  }
+  __syncthreads();
+  const float coef = coef_s;
+  const OptChunk ck = chunks[blockIdx.x];
+  const OptEntry e = tab[ck.entry];
+  const float lr = e.group == 0 ? lr0 : (e.group == 1 ? lr1 : lr2);
+  const float wd = e.group == 0 ? wd0 : (e.group == 1 ? wd1 : wd2);
+  for (long i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
+    float p = e.p[i];
+    if (e.g && e.group < 3) {
+      float g = e.g[i] * coef;
+      if (wd != 0.f) g += wd * p;
+      float b = first ? g : momentum * e.buf[i] + g;
+      e.buf[i] = b;
+      float step = nesterov ? g + momentum * b : b;
+      p -= lr * step;
+      e.p[i] = p;
+    }
+    if (e.ema) e.ema[i] = ema_d * e.ema[i] + (1.f - ema_d) * p;
+  }
+}
+
+// gather scattered tensors into a flat buffer (DDP bucket) or scatter back
+__global__ void __launch_bounds__(256) flat_copy_kernel(const OptEntry* tab, const OptChunk* chunks, float* flat,
+                                                        const long* offsets, int to_flat) {
+  const OptChunk ck = chunks[blockIdx.x];
+  const OptEntry e = tab[ck.entry];
+  long off = offsets[ck.entry];
+  for (long i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
+    if (to_flat) flat[off + i] = e.g ? e.g[i] : e.p[i];
+    else e.p[i] = flat[off + i];
+  }
+}
+
+}  // namespace adr
+
+using namespace adr;
+
+extern "C" int adr_opt_entry_size(void) { return (int)sizeof(OptEntry); }
+extern "C" int adr_opt_chunk_size(void) { return (int)sizeof(OptChunk); }
+
+extern "C" int adr_opt_step(const void* tab, const void* chunks, int nchunks, float* partial, float max_norm, float lr0,
+                            float lr1, float lr2, float wd0, float wd1, float wd2, float momentum, int nesterov,
+                            int first, float ema_decay, float* norm_out, void* stream) {
+  ADR_REQUIRE(nchunks > 0, "opt_step: empty chunk table");
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(nchunks), dim3(256), 0, st, (const OptEntry*)tab,
+                     (const OptChunk*)chunks, partial);
+  hipLaunchKernelGGL(sgd_ema_kernel, dim3(nchunks), dim3(256), 0, st, (const OptEntry*)tab, (const OptChunk*)chunks,
+                     nchunks, partial, max_norm, lr0, lr1, lr2, wd0, wd1, wd2, momentum, nesterov, first, ema_decay,
+                     norm_out);
+  return check_launch("adr_opt_step");
+}
+
+extern "C" int adr_flat_copy(const void* tab, const void* chunks, int nchunks, float* flat, const int64_t* offsets,
+                             int to_flat, void* stream) {
+  hipLaunchKernelGGL(flat_copy_kernel, dim3(nchunks), dim3(256), 0, (hipStream_t)stream, (const OptEntry*)tab,
+                     (const OptChunk*)chunks, flat, (const long*)offsets, to_flat);
+  return check_launch("adr_flat_copy");
+}
