@@ -1,0 +1,151 @@
+"""Benchmark: YOLO-AD-Refine-n training step (fwd + TAL/DFL/CIoU+NWD loss + bwd + clip + SGD + EMA) on synthetic
+640x640 batches, bs 64 per GPU (BASELINE.json configs[2] per GPU; configs[3] = 8 GPUs x 64 via DDP/RCCL).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--bs 64] [--img 640] [--dtype bf16|fp32]
+  N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Prints ONE JSON line on rank 0 (value = images/s summed over all ranks; max-over-ranks timing).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "yolo-ad-refine_amd"))
+sys.path.insert(1, str(ROOT / "oracle"))
+
+CFG = ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
+BF16_MFMA_PEAK_TF = 2500.0  # dense bf16 MFMA (spec, no sparsity)
+F32_MFMA_PEAK_TF = 157.3
+
+
+def synthetic_batch(bs, img, seed, device):
+    import torch
+    from recipe import synthetic_images, synthetic_labels
+    from adrefine.utils.loss import preprocess_targets
+    x = synthetic_images(bs, img, seed=seed).to(device)
+    lab = synthetic_labels(bs, 80, seed=seed + 1)
+    gt = preprocess_targets(lab["batch_idx"], lab["cls"], lab["bboxes"], bs, (img, img)).to(device)
+    return {"img": x, "gt": gt}, lab
+
+
+def cpu_baseline(bs=2, img=640, budget_s=20.0):
+    """The CPU oracle (oracle/adr_oracle.py, a pure-PyTorch restatement pinned to the reference) timed on the host
+    cores: fwd + v8DetectionLoss + bwd for bs-image batches at img^2, until ~budget_s of work."""
+    import torch
+    import yaml
+    import adr_oracle as O
+    from recipe import recipe_state_dict, synthetic_images, synthetic_labels
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    d = yaml.safe_load(CFG.read_text())
+    layers, save = O.parse(d, 3, None)
+    import adrefine.nn.tasks as T  # only for the key/shape list (no GPU work)
+    spec = [(k, tuple(v.shape)) for k, v in T.DetectionModel(str(CFG)).state_dict().items()]
+    P = recipe_state_dict(spec)
+    for k, v in P.items():
+        if v.dtype.is_floating_point and "running" not in k and not k.endswith("dfl.conv.weight"):
+            v.requires_grad_(True)
+    x = synthetic_images(bs, img, seed=0)
+    lab = synthetic_labels(bs, 80, seed=1)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        preds = O.forward(P, layers, save, x, train=True)
+        loss, _ = O.detection_loss(preds, lab["batch_idx"], lab["cls"], lab["bboxes"])
+        loss.backward()
+        for v in P.values():
+            if v.grad is not None:
+                v.grad = None
+        n += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * bs / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} steps x {bs} images @{img}^2 (fwd+loss+bwd, fp32, torch CPU {threads} threads)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--bs", type=int, default=64)
+    ap.add_argument("--img", type=int, default=640)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import adrefine.kernels as K
+    from adrefine.engine.trainer import FusedTrainer
+    from adrefine.nn.tasks import DetectionModel
+
+    dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
+    torch.manual_seed(0)
+    model = DetectionModel(str(CFG), compute_dtype=dtype).to(dev)
+    if world > 1:  # same initial weights on every rank (DDP broadcasts rank 0's parameters at construction)
+        for p in model.parameters():
+            dist.broadcast(p.data, 0)
+    tr = FusedTrainer(model, batch_size=args.bs, world_size=world)
+    batch, _ = synthetic_batch(args.bs, args.img, seed=1000 * rank, device=dev)  # rank's shard of the stream
+
+    for _ in range(args.warmup):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    K.timing_begin()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        items = tr.step(batch)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ktimes = K.timing_end()
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t)
+    ips = world * args.bs * args.steps / dt
+    if rank == 0:
+        finite = bool(torch.isfinite(items).all())
+        roof = K.roofline_report(ktimes, dtype, HBM_PEAK_GBS, BF16_MFMA_PEAK_TF if dtype == torch.bfloat16 else F32_MFMA_PEAK_TF)
+        cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(budget_s=args.cpu_budget)
+        out = {
+            "metric": "images/sec whole-node (640x640) fwd+bwd, YOLO-AD-Refine-n at 1/2/4/8 GPU",
+            "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+            "config": {"workload": f"yolo11-701-YOLO-AD-Refine.yaml (n) train step bs={args.bs}/GPU "
+                                   f"{args.img}x{args.img}, synthetic COCO-shape labels, TAL+DFL+CIoU/NWD loss, "
+                                   f"SGD+EMA", "global_batch": world * args.bs, "img": args.img,
+                       "parallelism": f"dp{world}"},
+            "roofline": roof, "cpu_baseline": cpu, "loss_finite": finite,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -25,6 +25,72 @@ relayout_count = [0]
 _TRACE_RELAYOUT = bool(int(__import__("os").environ.get("ADR_TRACE_RELAYOUT", "0")))
 
 
+# ---------------------------------------------------------------------------------------------------------
+# live per-kernel timing with HIP events on the launch stream (bench.py roofline); off unless timing_begin()
+# ---------------------------------------------------------------------------------------------------------
+_TIMING = None
+
+
+def timing_begin():
+    global _TIMING
+    _TIMING = []
+
+
+def timing_end():
+    global _TIMING
+    recs, _TIMING = _TIMING, None
+    if not recs:
+        return []
+    torch.cuda.synchronize()
+    return [(tag, nbytes, flops, e0.elapsed_time(e1) * 1e-3) for tag, nbytes, flops, e0, e1 in recs]
+
+
+def _t0(tag, nbytes, flops):
+    if _TIMING is None:
+        return None
+    e0 = torch.cuda.Event(enable_timing=True)
+    e0.record()
+    return (tag, nbytes, flops, e0)
+
+
+def _t1(tok):
+    if tok is not None:
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record()
+        _TIMING.append((*tok, e1))
+
+
+def _bn_of(n):
+    return 16 if n <= 16 else 32 if n <= 32 else 64 if n <= 64 else 128
+
+
+def roofline_report(recs, dtype, hbm_gbs, mfma_tf):
+    """Dominant kernel family by total measured time -> achieved algorithmic GB/s and TF/s vs peaks."""
+    if not recs:
+        return None
+    agg = {}
+    for tag, nb, fl, t in recs:
+        a = agg.setdefault(tag, [0, 0.0, 0.0, 0.0])
+        a[0] += 1
+        a[1] += nb
+        a[2] += fl
+        a[3] += t
+    tag, (cnt, nb, fl, t) = max(agg.items(), key=lambda kv: kv[1][3])
+    gbs = nb / t / 1e9
+    tfs = fl / t / 1e12
+    ridge = mfma_tf * 1e12 / (hbm_gbs * 1e9)
+    ai = fl / max(nb, 1)
+    bound = "mfma" if ai > ridge else "hbm"
+    achieved, peak, unit = (tfs, mfma_tf, "TFLOP/s") if bound == "mfma" else (gbs, hbm_gbs, "GB/s")
+    total_t = sum(v[3] for v in agg.values())
+    return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": None, "kernel": tag, "launches": cnt,
+            "avg_us": round(1e6 * t / cnt, 2), "alg_bytes_per_launch": int(nb / cnt),
+            "alg_flops_per_launch": int(fl / cnt), "achieved_gbs": round(gbs, 1), "achieved_tfs": round(tfs, 2),
+            "share_of_timed_gemm_time": round(t / total_t, 3),
+            "families": {k: {"launches": v[0], "ms_total": round(1e3 * v[3], 3)} for k, v in sorted(agg.items())}}
+
+
 def dcode(dtype) -> int:
     if dtype == torch.float32:
         return F32
@@ -190,8 +256,12 @@ class Conv2dFn(torch.autograd.Function):
             tiles = lib.adr_conv2d_fwd_stat_tiles(ctypes.byref(d))
             stats = torch.empty(tiles * 2 * K, dtype=torch.float32, device=x.device)
         bf = b.detach().float().contiguous() if b is not None else None
+        es = x.element_size()
+        tok = _t0(f"gemm_fwd<{'bf16' if es == 2 else 'f32'},BN={_bn_of(K)}>",
+                  es * (N * H * W * C + K * R * S * C + N * Ho * Wo * K), 2 * N * Ho * Wo * K * R * S * C)
         lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(xp), fptr(wp), fptr(bf), ctypes.c_void_p(y.data_ptr()),
                            fptr(stats), 0, stream())
+        _t1(tok)
         ctx.save_for_backward(x, wp)
         ctx.meta = (stride, pad, cpad, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
@@ -214,10 +284,18 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = empty_act(N, C, H, W, x.dtype, x.device)
             d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
+            es = x.element_size()
+            tok = _t0(f"gemm_dgrad<{'bf16' if es == 2 else 'f32'},BN={_bn_of(C)}>",
+                      es * (N * H * W * C + K * R * S * C + N * Ho * Wo * K), 2 * N * Ho * Wo * K * R * S * C)
             lib.adr_conv2d_dgrad(ctypes.byref(d2), ctypes.c_void_p(dyp), fptr(wp), None,
                                  ctypes.c_void_p(dx.data_ptr()), 0, stream())
+            _t1(tok)
         if ctx.needs_input_grad[1]:
+            es = x.element_size()
+            tok = _t0(f"gemm_wgrad<{'bf16' if es == 2 else 'f32'}>",
+                      es * (N * H * W * C + N * Ho * Wo * K) + 4 * K * R * S * C, 2 * N * Ho * Wo * K * R * S * C)
             dwk = _wgrad(d, xp, dyp, K, C, R * S, x.device)
+            _t1(tok)
             dw = sink_unpack(ctx.pw, dwk, wshape, cpad)
         if has_b and ctx.needs_input_grad[2]:
             db = sink(ctx.pb, _bias_grad(dy, K, N, Ho * Wo, dycs))
