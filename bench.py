@@ -18,7 +18,6 @@ from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "yolo-ad-refine_amd"))
-sys.path.insert(1, str(ROOT / "oracle"))
 
 CFG = ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
@@ -26,21 +25,12 @@ BF16_MFMA_PEAK_TF = 2500.0  # dense bf16 MFMA (spec, no sparsity)
 F32_MFMA_PEAK_TF = 157.3
 
 
-def synthetic_batch(bs, img, seed, device):
-    import torch
-    from recipe import synthetic_images, synthetic_labels
-    from adrefine.utils.loss import preprocess_targets
-    x = synthetic_images(bs, img, seed=seed).to(device)
-    lab = synthetic_labels(bs, 80, seed=seed + 1)
-    gt = preprocess_targets(lab["batch_idx"], lab["cls"], lab["bboxes"], bs, (img, img)).to(device)
-    return {"img": x, "gt": gt}, lab
-
-
 def cpu_baseline(bs=2, img=640, budget_s=20.0):
     """The CPU oracle (oracle/adr_oracle.py, a pure-PyTorch restatement pinned to the reference) timed on the host
     cores: fwd + v8DetectionLoss + bwd for bs-image batches at img^2, until ~budget_s of work."""
     import torch
     import yaml
+    sys.path.insert(1, str(ROOT / "oracle"))  # the oracle is the CPU baseline leg only
     import adr_oracle as O
     from recipe import recipe_state_dict, synthetic_images, synthetic_labels
     threads = min(16, os.cpu_count() or 1)
@@ -95,6 +85,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
     import adrefine.kernels as K
     from adrefine.engine.trainer import FusedTrainer
+    from adrefine.data.synthetic import train_batch
     from adrefine.nn.tasks import DetectionModel
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
@@ -104,7 +95,7 @@ def main():
         for p in model.parameters():
             dist.broadcast(p.data, 0)
     tr = FusedTrainer(model, batch_size=args.bs, world_size=world)
-    batch, _ = synthetic_batch(args.bs, args.img, seed=1000 * rank, device=dev)  # rank's shard of the stream
+    batch, _ = train_batch(args.bs, args.img, seed=1000 * rank, device=dev)  # rank's shard of the stream
 
     for _ in range(args.warmup):
         tr.step(batch)
@@ -116,6 +107,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         items = tr.step(batch)
+    t_host = time.perf_counter() - t0  # host-side enqueue time (launch-bound if close to the step time)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -141,6 +133,7 @@ def main():
                                    f"SGD+EMA", "global_batch": world * args.bs, "img": args.img,
                        "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "loss_finite": finite,
+            "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -281,6 +281,18 @@ int adr_opt_step(const void* tab, const void* chunks, int nchunks, float* partia
 int adr_flat_copy(const void* tab, const void* chunks, int nchunks, float* flat, const int64_t* offsets,
                   int to_flat, void* stream);
 
+/* ---------------------------------------------------------------------------------------------------------
+ * Batched NMS: replaces utils/ops.py:163-312 non_max_suppression (agnostic=False, classes=None, nm=0,
+ * labels=()) with its torchvision.ops.nms call. y = decoded head output (B, 4+nc, A) fp32, rows xywh then class
+ * scores. multi != 0: every (anchor, class) with score > conf (multi_label=True, the val path); else best class.
+ * agnostic: one NMS over all classes (single-label only); class_mask[nc] (nullable): the `classes` filter.
+ * out (B, max_det, 6) rows x1 y1 x2 y2 conf cls in the reference's output order; nout[B] valid rows per image.
+ * Requires A <= 16384, nc <= 1024, max_det <= 300. */
+size_t adr_nms_workspace(int B, int nc, int A, int multi, int max_det);
+int adr_nms(const float* y, int B, int nc, int A, float conf, float iou, int multi, int agnostic,
+            const unsigned char* class_mask, int max_det, int max_nms, float max_wh, float* out, int* nout, void* ws,
+            size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -88,11 +88,20 @@ def main():
     tasks, block, conv, head, uloss, uops = _import_reference()
     OUT.mkdir(parents=True, exist_ok=True)
     torch.set_num_threads(8)
-    manifest = {"generator": "oracle/gen_golden.py", "reference": "wcq99681-svg/YOLO-AD-Refine @ 2025-12-26",
-                "torch": torch.__version__, "fixtures": {}}
+    only_nms = "--only-nms" in sys.argv
+    if only_nms:
+        manifest = json.loads((OUT / "MANIFEST.json").read_text())
+    else:
+        manifest = {"generator": "oracle/gen_golden.py", "reference": "wcq99681-svg/YOLO-AD-Refine @ 2025-12-26",
+                    "torch": torch.__version__, "fixtures": {}}
 
     def note(name, what, cites, unpinned=False):
         manifest["fixtures"][name] = {"what": what, "reference": cites, "unpinned_3rdparty": unpinned}
+
+    if only_nms:
+        nms_fixtures(uops, note)
+        (OUT / "MANIFEST.json").write_text(json.dumps(manifest, indent=1))
+        return
 
     # ---------------- per-module fixtures (train mode, bs 2, real channel counts, small spatial) ---------------
     m = conv.Conv(16, 32, 3, 2)
@@ -220,7 +229,14 @@ def main():
         note(f"loss_{S}_bs{bs}", "v8DetectionLoss on seeded randn head outputs (x2 on box channels)",
              "utils/loss.py:419-520, tal.py:39-265, metrics.py:74-125,539-564")
 
-    # ---------------- NMS -----------------------------------------------------------------------------------------
+    nms_fixtures(uops, note)
+
+    (OUT / "MANIFEST.json").write_text(json.dumps(manifest, indent=1))
+    print("wrote", len(list(OUT.glob("*.npz"))), "fixtures to", OUT)
+
+
+def nms_fixtures(uops, note):
+    """utils/ops.py:163-312 on the exactly-reproducible synthetic predictions (recipe.synthetic_predictions)."""
     pred = synthetic_predictions(2, 8400, 80, 640, seed=7)
     for name, conf, iou, ml in (("predict", 0.25, 0.7, False), ("val", 0.001, 0.7, True), ("tight", 0.25, 0.45, False)):
         # max_time_img raised so the reference's wall-clock cut-off (ops.py:234, 308-310) cannot truncate the
@@ -231,9 +247,6 @@ def main():
         np.savez_compressed(OUT / f"nms_{name}.npz", **d)
         note(f"nms_{name}", f"non_max_suppression(conf={conf}, iou={iou}, multi_label={ml}) on seed-7 predictions",
              "utils/ops.py:163-312 -> torchvision.ops.nms (restated)", True)
-
-    (OUT / "MANIFEST.json").write_text(json.dumps(manifest, indent=1))
-    print("wrote", len(list(OUT.glob("*.npz"))), "fixtures to", OUT)
 
 
 if __name__ == "__main__":

@@ -93,10 +93,33 @@ def synthetic_labels(bs: int, nc: int = 80, seed: int = 1, mean_n: float = 7.3, 
 
 
 def synthetic_predictions(bs: int, na: int, nc: int = 80, img: int = 640, seed: int = 7):
-    """Eval-head-shaped predictions (bs, 4+nc, na) for NMS parity: xywh boxes in pixels + sigmoid scores
-    drawn so that conf 0.001 / 0.25 leave thousands / hundreds of candidates with heavy overlap."""
+    """Eval-head-shaped predictions (bs, 4+nc, na) for NMS parity: xywh boxes in pixels + class scores.
+
+    Built from torch.rand / randperm with exactly-rounded arithmetic only (no exp/log/sigmoid/randn, whose CPU
+    vector code paths differ in the last ulp between ISAs), so any host regenerates identical bits and the
+    NMS comparison can be bit-exact. Half the anchors are jittered copies of 64 "object" boxes per image, so
+    suppression is real; scores are distinct within an image (a permutation raised to the 16th power), so the
+    reference's unstable argsort cannot reorder ties. conf 0.25 keeps almost every anchor (single-label),
+    conf 0.001 keeps about a third of all (anchor, class) pairs and exercises the max_nms cut."""
     g = torch.Generator().manual_seed(seed)
     xy = torch.rand(bs, 2, na, generator=g) * img
-    wh = torch.exp(math.log(4) + (math.log(300) - math.log(4)) * torch.rand(bs, 2, na, generator=g))
-    logits = torch.randn(bs, nc, na, generator=g) * 2.0 - 5.0
-    return torch.cat((xy, wh, torch.sigmoid(logits)), 1)
+    u = torch.rand(bs, 2, na, generator=g)
+    wh = 4 + 296 * (u * u * u)
+    nobj = 64
+    obj_xy = torch.rand(bs, 2, nobj, generator=g) * img
+    ov = torch.rand(bs, 2, nobj, generator=g)
+    obj_wh = 16 + 200 * (ov * ov)
+    pick = torch.randint(0, nobj, (bs, na), generator=g)
+    jit = torch.rand(bs, 4, na, generator=g)
+    clustered = torch.rand(bs, na, generator=g) < 0.5
+    cxy = torch.gather(obj_xy, 2, pick[:, None].expand(bs, 2, na)) + (jit[:, :2] - 0.5) * 8
+    cwh = torch.gather(obj_wh, 2, pick[:, None].expand(bs, 2, na)) * (0.9 + 0.2 * jit[:, 2:])
+    xy = torch.where(clustered[:, None], cxy, xy)
+    wh = torch.where(clustered[:, None], cwh, wh)
+    n = nc * na
+    r = torch.stack([(torch.randperm(n, generator=g).to(torch.float32) + 0.5) / n for _ in range(bs)])
+    s = r * r
+    s = s * s
+    s = s * s
+    s = s * s
+    return torch.cat((xy, wh, s.view(bs, nc, na)), 1)

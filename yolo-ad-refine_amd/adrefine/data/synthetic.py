@@ -1,0 +1,42 @@
+"""Synthetic COCO-shape training batches — the bench's input stream. No dataset is
+available offline: images are torch.rand (already /255-normalised, as after detect/train.py:57-59) and labels
+follow COCO's per-image statistics, packed like YOLODataset.collate_fn (data/dataset.py:230-246):
+batch_idx (N,), cls (N, 1), bboxes (N, 4) normalised xywh. The test oracle generates the same stream from the
+same recipe (tests/test_synthetic.py checks they agree)."""
+from __future__ import annotations
+
+import math
+
+import torch
+
+
+def images(bs: int, size: int, seed: int = 0) -> torch.Tensor:
+    g = torch.Generator().manual_seed(seed)
+    return torch.rand(bs, 3, size, size, generator=g)
+
+
+def labels(bs: int, nc: int = 80, seed: int = 1, mean_n: float = 7.3, max_n: int = 93):
+    """Per image n ~ Poisson(mean_n) clipped to [1, max_n]; cls ~ U{0..nc-1}; centre ~ U(0.05, 0.95)^2;
+    w, h = exp(U(ln 0.02, ln 0.6)) shrunk to stay inside the image."""
+    g = torch.Generator().manual_seed(seed)
+    counts = torch.poisson(torch.full((bs,), mean_n), generator=g).clamp(1, max_n).long()
+    bi, cl, bx = [], [], []
+    lo, hi = math.log(0.02), math.log(0.6)
+    for j in range(bs):
+        n = int(counts[j])
+        c = torch.randint(0, nc, (n,), generator=g)
+        ctr = 0.05 + 0.9 * torch.rand(n, 2, generator=g)
+        wh = torch.exp(lo + (hi - lo) * torch.rand(n, 2, generator=g))
+        wh = torch.minimum(wh, 2 * torch.minimum(ctr, 1 - ctr))
+        bi.append(torch.full((n,), float(j)))
+        cl.append(c.float().view(-1, 1))
+        bx.append(torch.cat((ctr, wh), 1))
+    return {"batch_idx": torch.cat(bi), "cls": torch.cat(cl), "bboxes": torch.cat(bx)}
+
+
+def train_batch(bs: int, img: int, seed: int, device, nc: int = 80):
+    """Device-resident batch for FusedTrainer.step: {'img': (bs,3,img,img) fp32, 'gt': (bs, nmax, 5)}."""
+    from ..utils.loss import preprocess_targets
+    lab = labels(bs, nc, seed=seed + 1)
+    gt = preprocess_targets(lab["batch_idx"], lab["cls"], lab["bboxes"], bs, (img, img)).to(device)
+    return {"img": images(bs, img, seed=seed).to(device), "gt": gt}, lab

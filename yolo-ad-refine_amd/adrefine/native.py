@@ -8,8 +8,8 @@ import re
 from pathlib import Path
 
 _HERE = Path(__file__).resolve().parent
-LIB_PATH = _HERE / "lib" / "libadr_hip.so"
-HEADER = _HERE.parents[1] / "include" / "adr.h"
+LIB_PATH = Path(os.environ.get("ADR_LIB", _HERE / "lib" / "libadr_hip.so"))  # ADR_LIB: A/B builds (dev)
+HEADER = Path(os.environ["ADR_HEADER"]) if "ADR_HEADER" in os.environ else _HERE.parents[1] / "include" / "adr.h"
 if not HEADER.exists():  # installed layout: header shipped next to the library
     HEADER = _HERE / "lib" / "adr.h"
 

@@ -14,86 +14,60 @@
 namespace adr {
 
 // ---------------- depthwise conv ----------------
-template <typename T>
-__global__ void __launch_bounds__(256) dw_fwd_kernel(const T* x, int xcs, const float* w, const float* b, T* y, int ycs,
-                                                     int N, int H, int W, int C, int k) {
+// depthwise k x k, stride 1, pad k/2. BWD = false: y = dwconv(x, w) + b; BWD = true: dx (+)= dwconv^T(dy, w)
+// (taps mirrored). The block stages w tap-major ([t][c]) in LDS so each tap is two 16-byte LDS reads per
+// 8-channel vector instead of eight strided global loads.
+template <typename T, bool BWD>
+__global__ void __launch_bounds__(256) dw_kernel(const T* __restrict__ x, int xcs, const float* __restrict__ w,
+                                                 const float* __restrict__ b, T* __restrict__ y, int ycs, int N, int H,
+                                                 int W, int C, int k, int accumulate) {
   constexpr int V = 16 / sizeof(T);
-  const int G = C / V;
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * H * W * G;
-  if (i >= total) return;
-  int g = (int)(i % G);
-  long pix = i / G;
-  int ww = (int)(pix % W);
-  long r = pix / W;
-  int hh = (int)(r % H);
-  int n = (int)(r / H);
-  int p = k / 2, c0 = g * V;
-  float acc[V];
-#pragma unroll
-  for (int e = 0; e < V; ++e) acc[e] = b ? b[c0 + e] : 0.f;
-  for (int dy = 0; dy < k; ++dy) {
-    int ih = hh + dy - p;
-    if (ih < 0 || ih >= H) continue;
-    for (int dx = 0; dx < k; ++dx) {
-      int iw = ww + dx - p;
-      if (iw < 0 || iw >= W) continue;
-      u32x4 v = ld16(x + (((long)n * H + ih) * W + iw) * xcs + c0);
-      const T* e = reinterpret_cast<const T*>(&v);
-      int t = dy * k + dx;
-#pragma unroll
-      for (int q = 0; q < V; ++q) acc[q] += to_f(e[q]) * w[(c0 + q) * k * k + t];
-    }
+  extern __shared__ float wl[];  // [k*k][C]
+  const int kk = k * k;
+  for (int i = threadIdx.x; i < kk * C; i += 256) {
+    const int c = i / kk, t = i % kk;
+    wl[t * C + c] = w[i];
   }
-  u32x4 o;
-  T* oe = reinterpret_cast<T*>(&o);
-#pragma unroll
-  for (int q = 0; q < V; ++q) oe[q] = from_f<T>(acc[q]);
-  st16(y + pix * ycs + c0, o);
-}
-
-template <typename T>
-__global__ void __launch_bounds__(256) dw_bwd_x_kernel(const T* dy, int dcs, const float* w, T* dx, int ocs, int N, int H,
-                                                       int W, int C, int k, int accumulate) {
-  constexpr int V = 16 / sizeof(T);
-  const int G = C / V;
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * H * W * G;
+  __syncthreads();
+  const unsigned G = C / V;
+  const unsigned total = (unsigned)N * H * W * G;
+  const unsigned i = blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
-  int g = (int)(i % G);
-  long pix = i / G;
-  int ww = (int)(pix % W);
-  long r = pix / W;
-  int hh = (int)(r % H);
-  int n = (int)(r / H);
-  int p = k / 2, c0 = g * V;
+  const unsigned pix = i / G;
+  const int c0 = (int)(i - pix * G) * V;
+  const int ww = (int)(pix % (unsigned)W);
+  const unsigned r = pix / (unsigned)W;
+  const int hh = (int)(r % (unsigned)H);
+  const int n = (int)(r / (unsigned)H);
+  const int p = k / 2;
   float acc[V];
 #pragma unroll
-  for (int e = 0; e < V; ++e) acc[e] = 0.f;
+  for (int e = 0; e < V; ++e) acc[e] = (!BWD && b) ? b[c0 + e] : 0.f;
   for (int ky = 0; ky < k; ++ky) {
-    int oh = hh - ky + p;
-    if (oh < 0 || oh >= H) continue;
+    const int ih = BWD ? hh - ky + p : hh + ky - p;
+    if (ih < 0 || ih >= H) continue;
     for (int kx = 0; kx < k; ++kx) {
-      int ow = ww - kx + p;
-      if (ow < 0 || ow >= W) continue;
-      u32x4 v = ld16(dy + (((long)n * H + oh) * W + ow) * dcs + c0);
+      const int iw = BWD ? ww - kx + p : ww + kx - p;
+      if (iw < 0 || iw >= W) continue;
+      const u32x4 v = ld16(x + ((long)(n * H + ih) * W + iw) * xcs + c0);
       const T* e = reinterpret_cast<const T*>(&v);
-      int t = ky * k + kx;
+      const float* wt = wl + (ky * k + kx) * C + c0;
 #pragma unroll
-      for (int q = 0; q < V; ++q) acc[q] += to_f(e[q]) * w[(c0 + q) * k * k + t];
+      for (int q = 0; q < V; ++q) acc[q] += to_f(e[q]) * wt[q];
     }
   }
-  u32x4 o;
-  T* oe = reinterpret_cast<T*>(&o);
-  if (accumulate) {
-    u32x4 pv = ld16(dx + pix * ocs + c0);
+  T* dst = y + (long)pix * ycs + c0;
+  if (BWD && accumulate) {
+    const u32x4 pv = ld16(dst);
     const T* pe = reinterpret_cast<const T*>(&pv);
 #pragma unroll
     for (int q = 0; q < V; ++q) acc[q] += to_f(pe[q]);
   }
+  u32x4 o;
+  T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
   for (int q = 0; q < V; ++q) oe[q] = from_f<T>(acc[q]);
-  st16(dx + pix * ocs + c0, o);
+  st16(dst, o);
 }
 
 // partial[chunk][t][c] = sum over the chunk's pixels of dy * x(shifted by tap t); grid (chunks, k*k)
@@ -224,37 +198,57 @@ __global__ void __launch_bounds__(256) adyt_bwd_kernel(const T* x, int xcs, cons
 
 // collapse: dimp[n][j] = sum_{chunk,c} P0..2 ; dalpha[j] = sum_{n,chunk,c} P3..5 * imp[n][j] ; dw[c] = sum P6 ;
 // db[c] = sum P7
-__global__ void adyt_collapse_kernel(const float* partial, const float* imp, int N, int chunks, int C, float* dimp,
-                                     float* dalpha, float* dw, float* db) {
-  int tid = threadIdx.x;
-  for (int c = tid; c < C; c += blockDim.x) {
-    float sw = 0.f, sb = 0.f;
-    for (int n = 0; n < N; ++n)
-      for (int ch = 0; ch < chunks; ++ch) {
-        const float* p = partial + ((long)n * chunks + ch) * 8 * C;
-        sw += p[6 * C + c];
-        sb += p[7 * C + c];
-      }
-    dw[c] = sw;
-    db[c] = sb;
-  }
-  if (tid < 3) {
-    int j = tid;
-    double da = 0.0;
-    for (int n = 0; n < N; ++n) {
-      double di = 0.0, dan = 0.0;
-      for (int ch = 0; ch < chunks; ++ch) {
-        const float* p = partial + ((long)n * chunks + ch) * 8 * C;
-        for (int c = 0; c < C; ++c) {
-          di += p[j * C + c];
-          dan += p[(3 + j) * C + c];
-        }
-      }
-      dimp[n * 3 + j] = (float)di;
-      da += dan * imp[n * 3 + j];
+// collapse of the per-(image, chunk) partials of adyt_bwd. Blocks [0, 3N): (n, j) -> dimp[n][j] and the
+// per-image alpha term dan[n][j]; blocks [3N, 3N + C): channel c -> dw[c], db[c]. Fixed-order tree reductions.
+__global__ void __launch_bounds__(256) adyt_collapse_kernel(const float* partial, int N, int chunks, int C,
+                                                            float* dimp, float* dan, float* dw, float* db) {
+  __shared__ double r1[256], r2[256];
+  const int tid = threadIdx.x;
+  double s1 = 0.0, s2 = 0.0;
+  if (blockIdx.x < 3 * N) {
+    const int n = blockIdx.x / 3, j = blockIdx.x % 3;
+    for (int it = tid; it < chunks * C; it += 256) {
+      const int ch = it / C, c = it % C;
+      const float* p = partial + ((long)n * chunks + ch) * 8 * C;
+      s1 += p[j * C + c];
+      s2 += p[(3 + j) * C + c];
     }
-    dalpha[j] = (float)da;
+  } else {
+    const int c = blockIdx.x - 3 * N;
+    for (int it = tid; it < N * chunks; it += 256) {
+      const float* p = partial + (long)it * 8 * C;
+      s1 += p[6 * C + c];
+      s2 += p[7 * C + c];
+    }
   }
+  r1[tid] = s1;
+  r2[tid] = s2;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      r1[tid] += r1[tid + o];
+      r2[tid] += r2[tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    if (blockIdx.x < 3 * N) {
+      dimp[blockIdx.x] = (float)r1[0];
+      dan[blockIdx.x] = (float)r2[0];
+    } else {
+      dw[blockIdx.x - 3 * N] = (float)r1[0];
+      db[blockIdx.x - 3 * N] = (float)r2[0];
+    }
+  }
+}
+
+// dalpha[j] = sum_n dan[n][j] * imp[n][j]
+__global__ void adyt_alpha_kernel(const float* dan, const float* imp, int N, float* dalpha) {
+  const int j = threadIdx.x;
+  if (j >= 3) return;
+  double da = 0.0;
+  for (int n = 0; n < N; ++n) da += (double)dan[n * 3 + j] * imp[n * 3 + j];
+  dalpha[j] = (float)da;
 }
 
 // ---------------- TSSA (one block per (image, head)) ----------------
@@ -583,12 +577,14 @@ extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w,
   ADR_REQUIRE(C % v == 0 && xcs % v == 0 && ycs % v == 0 && k % 2 == 1, "dwconv: C=%d k=%d", C, k);
   hipStream_t st = (hipStream_t)stream;
   long total = (long)N * H * W * (C / v);
+  size_t sm = (size_t)k * k * C * sizeof(float);
+  ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(dw_fwd_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)x, xcs, w, b,
-                       (__bf16*)y, ycs, N, H, W, C, k);
+    hipLaunchKernelGGL((dw_kernel<__bf16, false>), dim3(cdiv(total, 256)), dim3(256), sm, st, (const __bf16*)x, xcs, w,
+                       b, (__bf16*)y, ycs, N, H, W, C, k, 0);
   else
-    hipLaunchKernelGGL(dw_fwd_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)x, xcs, w, b,
-                       (float*)y, ycs, N, H, W, C, k);
+    hipLaunchKernelGGL((dw_kernel<float, false>), dim3(cdiv(total, 256)), dim3(256), sm, st, (const float*)x, xcs, w,
+                       b, (float*)y, ycs, N, H, W, C, k, 0);
   return check_launch("adr_dwconv_fwd");
 }
 
@@ -606,12 +602,14 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
   hipStream_t st = (hipStream_t)stream;
   long total = (long)N * H * W * (C / v);
   if (dx) {
+    size_t sm = (size_t)k * k * C * sizeof(float);
+    ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv_bwd: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
     if (dtype == ADR_BF16)
-      hipLaunchKernelGGL(dw_bwd_x_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)dy, dcs, w,
-                         (__bf16*)dx, ocs, N, H, W, C, k, accumulate);
+      hipLaunchKernelGGL((dw_kernel<__bf16, true>), dim3(cdiv(total, 256)), dim3(256), sm, st, (const __bf16*)dy, dcs,
+                         w, nullptr, (__bf16*)dx, ocs, N, H, W, C, k, accumulate);
     else
-      hipLaunchKernelGGL(dw_bwd_x_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)dy, dcs, w,
-                         (float*)dx, ocs, N, H, W, C, k, accumulate);
+      hipLaunchKernelGGL((dw_kernel<float, true>), dim3(cdiv(total, 256)), dim3(256), sm, st, (const float*)dy, dcs,
+                         w, nullptr, (float*)dx, ocs, N, H, W, C, k, accumulate);
   }
   if (dw) {
     ADR_REQUIRE(ws_bytes >= adr_dwconv_wgrad_workspace(N, H, W, C, k), "dwconv_bwd: workspace");
@@ -643,7 +641,7 @@ extern "C" int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alph
 }
 
 extern "C" size_t adr_adyt_bwd_workspace(int N, int HW, int C) {
-  return (size_t)N * cdiv(HW, 256) * 8 * C * sizeof(float);
+  return ((size_t)N * cdiv(HW, 256) * 8 * C + (size_t)N * 3) * sizeof(float);
 }
 
 extern "C" int adr_adyt_bwd(int dtype, const void* x, int xcs, const void* dout, int dcs, const float* alphas,
@@ -660,7 +658,9 @@ extern "C" int adr_adyt_bwd(int dtype, const void* x, int xcs, const void* dout,
   else
     hipLaunchKernelGGL(adyt_bwd_kernel<float>, g, dim3(256), 0, st, (const float*)x, xcs, (const float*)dout, dcs,
                        alphas, imp, w, (float*)dx, ocs, HW, C, 256, chunks, ws);
-  hipLaunchKernelGGL(adyt_collapse_kernel, dim3(1), dim3(256), 0, st, ws, imp, N, chunks, C, dimp, dalpha, dw, db);
+  float* dan = ws + (size_t)N * chunks * 8 * C;
+  hipLaunchKernelGGL(adyt_collapse_kernel, dim3(3 * N + C), dim3(256), 0, st, ws, N, chunks, C, dimp, dan, dw, db);
+  hipLaunchKernelGGL(adyt_alpha_kernel, dim3(1), dim3(64), 0, st, dan, imp, N, dalpha);
   return check_launch("adr_adyt_bwd");
 }
 

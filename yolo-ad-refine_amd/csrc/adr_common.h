@@ -36,6 +36,18 @@ template <typename T> struct Vec16 { static constexpr int N = 16 / sizeof(T); };
 
 __device__ __forceinline__ u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
 __device__ __forceinline__ void st16(void* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
+// VEC consecutive fp32 coefficients (16-byte aligned: VEC-multiple channel offsets into torch allocations)
+template <int VEC>
+__device__ __forceinline__ void ld_coef(const float* p, float* out) {
+#pragma unroll
+  for (int k = 0; k < VEC; k += 4) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(p + k);
+    out[k] = v[0];
+    out[k + 1] = v[1];
+    out[k + 2] = v[2];
+    out[k + 3] = v[3];
+  }
+}
 
 // ---- activations (shared by norm epilogues and elementwise kernels) ----
 enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_RELU = 3, ACT_SIGMOID = 4, ACT_HSWISH = 5 };

@@ -109,23 +109,31 @@ __global__ void __launch_bounds__(256) bcast_mul_kernel(const T* x, int xcs, con
   }
 }
 
-// out[n][c] = sum over chunks of partial[n][chunk][which][c], then optionally summed over n and/or c
-__global__ void nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n,
-                                   int sum_c, int accumulate) {
-  // one thread per output element; tiny
-  int outN = sum_n ? 1 : N, outC = sum_c ? 1 : C;
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= outN * outC) return;
-  int on = idx / outC, oc = idx % outC;
+// out[n][c] = sum over chunks of partial[n][chunk][which][c], then optionally summed over n and/or c.
+// One workgroup per output element, fixed-order tree reduction (deterministic).
+__global__ void __launch_bounds__(256) nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which,
+                                                          float* out, int sum_n, int sum_c, int accumulate) {
+  const int outC = sum_c ? 1 : C;
+  const int idx = blockIdx.x;
+  const int on = idx / outC, oc = idx % outC;
+  const int nn = sum_n ? N : 1, ncc = sum_c ? C : 1;
+  const int n0 = sum_n ? 0 : on, c0 = sum_c ? 0 : oc;
+  const long items = (long)nn * chunks * ncc;
   double s = 0.0;
-  int n0 = sum_n ? 0 : on, n1 = sum_n ? N : on + 1;
-  int c0 = sum_c ? 0 : oc, c1 = sum_c ? C : oc + 1;
-  for (int n = n0; n < n1; ++n)
-    for (int ch = 0; ch < chunks; ++ch) {
-      const float* p = partial + ((long)n * chunks + ch) * 2 * C + (long)which * C;
-      for (int c = c0; c < c1; ++c) s += p[c];
-    }
-  out[idx] = accumulate ? out[idx] + (float)s : (float)s;
+  for (long it = threadIdx.x; it < items; it += 256) {
+    const int c = c0 + (int)(it % ncc);
+    const long r = it / ncc;
+    const int ch = (int)(r % chunks), n = n0 + (int)(r / chunks);
+    s += partial[((long)n * chunks + ch) * 2 * C + (long)which * C + c];
+  }
+  __shared__ double sh[256];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[idx] = accumulate ? out[idx] + (float)sh[0] : (float)sh[0];
 }
 
 // partial[n][chunk][0][c] = sum x*dz ; [1][c] = sum dz   (per image, per channel)
@@ -265,7 +273,7 @@ extern "C" int adr_dot_reduce(int dtype, const void* x, int xcs, const void* dz,
 extern "C" int adr_nc_collapse(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n,
                                int sum_c, int accumulate, void* stream) {
   int outn = (sum_n ? 1 : N) * (sum_c ? 1 : C);
-  hipLaunchKernelGGL(nc_collapse_kernel, dim3(cdiv(outn, 256)), dim3(256), 0, (hipStream_t)stream, partial, N, chunks,
+  hipLaunchKernelGGL(nc_collapse_kernel, dim3(outn), dim3(256), 0, (hipStream_t)stream, partial, N, chunks,
                      C, which, out, sum_n, sum_c, accumulate);
   return check_launch("adr_nc_collapse");
 }

@@ -17,6 +17,7 @@
 // FWD epilogue optionally adds a bias and emits per-(row-tile, channel) partial sum / sum-of-squares of the
 // stored values for a following train-mode BatchNorm (deterministic: fixed-order reduction later).
 #include "adr_common.h"
+#include "adr_wgrad.h"
 
 namespace adr {
 
@@ -45,6 +46,17 @@ template <typename T> struct Cfg;
 template <> struct Cfg<__bf16> { static constexpr int BK = 32, VEC = 8, LDA = 40; };
 template <> struct Cfg<float> { static constexpr int BK = 16, VEC = 4, LDA = 20; };
 
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+__device__ __forceinline__ v4s tr_read16(const void* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+}
+// reduction index kk = 8g + 4h + q (MFMA k-slot of lane group g, element 4h + q) -> LDS row: the two groups of
+// each 32-lane half read 8 consecutive rows per transposed read (conflict-free with an odd-32-byte pitch)
+__device__ __forceinline__ int trb_row(int kk) {
+  return (kk & 3) + 4 * ((kk >> 3) & 1) + 8 * ((kk >> 2) & 1) + 16 * (kk >> 4);
+}
+
 template <typename T, int BN, int MODE>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   constexpr int BM = 128, BK = Cfg<T>::BK, VEC = Cfg<T>::VEC, LDA = Cfg<T>::LDA;
@@ -58,8 +70,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   constexpr int B_TOT = (MODE == MODE_FWD) ? BN * KCH : BK * (BN / VEC);
   constexpr int B_CH = (B_TOT + 255) / 256;
 
+  // bf16 DGRAD: the weight tile arrives as [co = reduction][ci = column] rows; it is stored row-for-row (no
+  // scalar transposition) at permuted rows and read back with ds_read_b64_tr_b16 (see adr_wgrad.hip)
+  constexpr bool TRB = (MODE == MODE_DGRAD) && (sizeof(T) == 2);
+  constexpr int PB = ((BN / 16) % 2 == 1) ? BN : BN + 16;  // TRB row pitch: odd multiple of 32 bytes
+  constexpr int BS_SIZE = (TRB && BK * PB > BN * LDA) ? BK * PB : BN * LDA;
   __shared__ __attribute__((aligned(16))) T As[BM * LDA];
-  __shared__ __attribute__((aligned(16))) T Bs[BN * LDA];
+  __shared__ __attribute__((aligned(16))) T Bs[BS_SIZE];
   __shared__ float red[2][WAVES_M][BN];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -209,6 +226,15 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
           st16(&Bs[row * LDA + kc * VEC], rb[i]);
         }
       }
+    } else if constexpr (TRB) {
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        int q = tid + 256 * i;
+        if (q < B_TOT) {
+          int kl = q / (BN / VEC), cch = q % (BN / VEC);
+          st16(&Bs[trb_row(kl) * PB + cch * VEC], rb[i]);
+        }
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < B_CH; ++i) {
@@ -243,9 +269,21 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
 #pragma unroll
       for (int i = 0; i < TM; ++i)
         fa[i] = *reinterpret_cast<const bf16x8*>(&As[(wr0 + i * 16 + (lane & 15)) * LDA + 8 * (lane >> 4)]);
+      if constexpr (TRB) {
+        // lane (g, q4, p4): k-slot (g, 4h + q4) lives at LDS row trb_row(8g + 4h + q4), column 4*p4
+        const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+        const T* b0 = &Bs[trb_row(8 * g + q4) * PB + wc0 + 4 * p4];
+        const T* b1 = &Bs[trb_row(8 * g + 4 + q4) * PB + wc0 + 4 * p4];
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[(wc0 + j * 16 + (lane & 15)) * LDA + 8 * (lane >> 4)]);
+        for (int j = 0; j < TN; ++j) {
+          v4s both[2] = {tr_read16(b0 + j * 16), tr_read16(b1 + j * 16)};
+          fb[j] = *reinterpret_cast<bf16x8*>(both);
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[(wc0 + j * 16 + (lane & 15)) * LDA + 8 * (lane >> 4)]);
+      }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -340,13 +378,20 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   }
 }
 
-// deterministic reduction of WGRAD split partials: dw[i] (+)= sum_s part[s][i]
-__global__ void wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw, long n, int splits,
-                                    int accumulate) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+// deterministic reduction of WGRAD split partials: dw[i] (+)= sum_s part[s][i]. One float per thread
+// (coalesced across the wave), eight independent loads in flight, combined in a fixed order.
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
+                                                           long n, int splits, int accumulate) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += part[(long)k * n + i];
+  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int k = 0;
+  for (; k + 8 <= splits; k += 8) {
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] += part[(long)(k + u) * n + i];
+  }
+  for (int u = 0; k < splits; ++k, ++u) acc[u] += part[(long)k * n + i];
+  float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   dw[i] = accumulate ? dw[i] + s : s;
 }
 
@@ -457,6 +502,10 @@ static int wgrad_splits(const adr_conv_desc* d, int* bn_out, int* ntiles_out) {
 }
 
 extern "C" size_t adr_conv2d_wgrad_workspace(const adr_conv_desc* d) {
+  if (d->dtype == ADR_BF16) {
+    WgPlan p = wgrad_bf16_plan(d);
+    return p.splits > 1 ? (size_t)p.splits * d->k * d->r * d->s * d->c * sizeof(float) : 0;
+  }
   int bn, nt;
   int splits = wgrad_splits(d, &bn, &nt);
   return (size_t)splits * d->k * d->r * d->s * d->c * sizeof(float);
@@ -467,6 +516,19 @@ extern "C" int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const voi
   GemmArgs g{};
   int rc = fill_common(d, g);
   if (rc) return rc;
+  hipStream_t st = (hipStream_t)stream;
+  const long nout = (long)d->k * d->r * d->s * d->c;
+  if (d->dtype == ADR_BF16) {
+    WgPlan p = wgrad_bf16_plan(d);
+    if (p.splits == 1) return wgrad_bf16_launch(d, x, dy, dw, accumulate, p, st);
+    size_t need = (size_t)p.splits * nout * sizeof(float);
+    ADR_REQUIRE(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+    rc = wgrad_bf16_launch(d, x, dy, (float*)ws, 0, p, st);
+    if (rc) return rc;
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(nout, 256)), dim3(256), 0, st, (const float*)ws, dw, nout,
+                       p.splits, accumulate);
+    return check_launch("adr_conv2d_wgrad");
+  }
   int bn, ntiles;
   int splits = wgrad_splits(d, &bn, &ntiles);
   size_t need = (size_t)splits * d->k * d->r * d->s * d->c * sizeof(float);
@@ -482,20 +544,16 @@ extern "C" int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const voi
   g.ktiles = (int)(per / BK);
   g.ntiles = ntiles;
   dim3 grid(cdiv(d->k, 128) * ntiles, splits);
-  hipStream_t st = (hipStream_t)stream;
   if (splits > 1 || accumulate) {
-    // every (co, tap, ci) inside [K x RSC] is written by exactly one block per split
-    if (d->dtype == ADR_BF16) launch_bn<__bf16, MODE_WGRAD>(bn, grid, g, st);
-    else launch_bn<float, MODE_WGRAD>(bn, grid, g, st);
+    // every (co, tap, ci) inside [K x RSC] is written by exactly one block per split (fp32 parity path)
+    launch_bn<float, MODE_WGRAD>(bn, grid, g, st);
     rc = check_launch("adr_conv2d_wgrad");
     if (rc) return rc;
-    long n = (long)d->k * d->r * d->s * d->c;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, st, (const float*)ws, dw, n, splits,
-                       accumulate);
+    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(nout, 256)), dim3(256), 0, st, (const float*)ws, dw, nout,
+                       splits, accumulate);
   } else {
     g.out = dw;
-    if (d->dtype == ADR_BF16) launch_bn<__bf16, MODE_WGRAD>(bn, grid, g, st);
-    else launch_bn<float, MODE_WGRAD>(bn, grid, g, st);
+    launch_bn<float, MODE_WGRAD>(bn, grid, g, st);
   }
   return check_launch("adr_conv2d_wgrad");
 }

@@ -77,57 +77,63 @@ __global__ void __launch_bounds__(256) dcn_im2col_kernel(const T* x, int xcs, co
   st16(cols + (pix * 9 + t) * C + g * V, ov);
 }
 
-// thread per (pix, tap): d_offset, d_mask_logit; atomics of dval into dx32 (fp32, NHWC dense N*H*W*C)
+// one wave per output pixel, lanes over channels: every (tap, corner) touches 64 contiguous channels, so the
+// x reads, the dcols reads and the fp32 scatter atomics into dx32 (NHWC dense N*H*W*C) are all coalesced;
+// d_offset / d_mask_logit are wave reductions over channels.
 template <typename T>
 __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, const T* om, int omcs, const T* dcols,
                                                          float* dx32, T* dom, int domcs, int N, int H, int W, int C) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * H * W * 9;
-  if (i >= total) return;
-  int t = (int)(i % 9);
-  long pix = i / 9;
-  int w = (int)(pix % W);
-  long r2 = pix / W;
-  int h = (int)(r2 % H);
-  int n = (int)(r2 / H);
+  const long pix = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (pix >= (long)N * H * W) return;
+  const int w = (int)(pix % W);
+  const long r2 = pix / W;
+  const int h = (int)(r2 % H);
+  const int n = (int)(r2 / H);
   const T* o = om + pix * omcs;
-  float oy = to_f(o[2 * t]), ox = to_f(o[2 * t + 1]);
-  float m = 1.f / (1.f + __expf(-to_f(o[18 + t])));
-  float py = (float)(h - 1 + t / 3) + oy, px = (float)(w - 1 + t % 3) + ox;
-  int y0, x0;
-  float wt[4];
-  bool ok[4];
-  bool inside = dcn_sample(py, px, H, W, y0, x0, wt, ok);
-  float ly = py - floorf(py), lx = px - floorf(px);
-  // d weight / d py and d px for each corner (mmcv dmcn_get_coordinate_weight)
-  float dwy[4] = {-(1.f - lx), -lx, (1.f - lx), lx};
-  float dwx[4] = {-(1.f - ly), (1.f - ly), -ly, ly};
   const T* xb = x + (long)n * H * W * xcs;
-  const T* dc = dcols + (pix * 9 + t) * C;
-  float dmask = 0.f, dpy = 0.f, dpx = 0.f;
-  for (int c = 0; c < C; ++c) {
-    float g = to_f(dc[c]);
-    if (g == 0.f) continue;
-    float val = 0.f, sy = 0.f, sx = 0.f;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      if (!ok[q]) continue;
-      int yy = y0 + (q >> 1), xx = x0 + (q & 1);
-      long off = ((long)yy * W + xx);
-      float v = to_f(xb[off * xcs + c]);
-      val += wt[q] * v;
-      sy += dwy[q] * v;
-      sx += dwx[q] * v;
-      atomicAdd(dx32 + ((long)n * H * W + off) * C + c, g * m * wt[q]);
-    }
-    dmask += g * val;
-    dpy += g * m * sy;
-    dpx += g * m * sx;
-  }
+  float* dxb = dx32 + (long)n * H * W * C;
   T* d = dom + pix * domcs;
-  d[2 * t] = from_f<T>(inside ? dpy : 0.f);
-  d[2 * t + 1] = from_f<T>(inside ? dpx : 0.f);
-  d[18 + t] = from_f<T>(dmask * m * (1.f - m));
+  for (int t = 0; t < 9; ++t) {
+    const float oy = to_f(o[2 * t]), ox = to_f(o[2 * t + 1]);
+    const float m = 1.f / (1.f + __expf(-to_f(o[18 + t])));
+    const float py = (float)(h - 1 + t / 3) + oy, px = (float)(w - 1 + t % 3) + ox;
+    int y0, x0;
+    float wt[4];
+    bool ok[4];
+    const bool inside = dcn_sample(py, px, H, W, y0, x0, wt, ok);
+    const float ly = py - floorf(py), lx = px - floorf(px);
+    // d weight / d py and d px for each corner (mmcv dmcn_get_coordinate_weight)
+    const float dwy[4] = {-(1.f - lx), -lx, (1.f - lx), lx};
+    const float dwx[4] = {-(1.f - ly), (1.f - ly), -ly, ly};
+    const T* dc = dcols + (pix * 9 + t) * C;
+    float dmask = 0.f, dpy = 0.f, dpx = 0.f;
+    for (int c = lane; c < C; c += 64) {
+      const float g = to_f(dc[c]);
+      float val = 0.f, sy = 0.f, sx = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (!ok[q]) continue;
+        const long off = (long)(y0 + (q >> 1)) * W + x0 + (q & 1);
+        const float v = to_f(xb[off * xcs + c]);
+        val += wt[q] * v;
+        sy += dwy[q] * v;
+        sx += dwx[q] * v;
+        unsafeAtomicAdd(dxb + off * C + c, g * m * wt[q]);
+      }
+      dmask += g * val;
+      dpy += g * m * sy;
+      dpx += g * m * sx;
+    }
+    dmask = wave_sum(dmask);
+    dpy = wave_sum(dpy);
+    dpx = wave_sum(dpx);
+    if (lane == 0) {
+      d[2 * t] = from_f<T>(inside ? dpy : 0.f);
+      d[2 * t + 1] = from_f<T>(inside ? dpx : 0.f);
+      d[18 + t] = from_f<T>(dmask * m * (1.f - m));
+    }
+  }
 }
 
 // W (Cout, C, 3, 3) fp32 -> W^T as a 1x1-conv weight [(t*C + c)][co] in dtype
@@ -350,13 +356,13 @@ extern "C" int adr_dcn_im2col(int dtype, const void* x, int xcs, const void* om,
 
 extern "C" int adr_dcn_col2im(int dtype, const void* x, int xcs, const void* om, int omcs, const void* dcols,
                               float* dx32, void* dom, int domcs, int N, int H, int W, int C, void* stream) {
-  long total = (long)N * H * W * 9;
+  long npix = (long)N * H * W;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(dcn_col2im_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)x, xcs,
+    hipLaunchKernelGGL(dcn_col2im_kernel<__bf16>, dim3(cdiv(npix, 4)), dim3(256), 0, st, (const __bf16*)x, xcs,
                        (const __bf16*)om, omcs, (const __bf16*)dcols, dx32, (__bf16*)dom, domcs, N, H, W, C);
   else
-    hipLaunchKernelGGL(dcn_col2im_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)x, xcs,
+    hipLaunchKernelGGL(dcn_col2im_kernel<float>, dim3(cdiv(npix, 4)), dim3(256), 0, st, (const float*)x, xcs,
                        (const float*)om, omcs, (const float*)dcols, dx32, (float*)dom, domcs, N, H, W, C);
   return check_launch("adr_dcn_col2im");
 }

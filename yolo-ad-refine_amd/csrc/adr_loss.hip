@@ -228,29 +228,45 @@ __device__ void adjust_heap(KV* f, int hole, int len, KV value) {
   f[hole] = value;
 }
 
-__global__ void __launch_bounds__(64) tal_topk_kernel(const float* align, uint8_t* flags, int rows, int A) {
-  int r = blockIdx.x * blockDim.x + threadIdx.x;
+// One wave per (image, gt) row, same sequence of heap operations as the scalar heap-select: candidates are
+// screened 64 at a time against the current heap top (a ballot), and only those that beat it are inserted,
+// in index order, by lane 0 on an LDS heap — so the selected set, ties included, is exactly libstdc++'s.
+__global__ void __launch_bounds__(256) tal_topk_kernel(const float* align, uint8_t* flags, int rows, int A) {
+  __shared__ KV heap[4][TOPK];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int r = blockIdx.x * 4 + wave;
   if (r >= rows) return;
   const float* m = align + (long)r * A;
   uint8_t* fl = flags + (long)r * A;
-  bool mgt = (fl[0] & 4) != 0;
+  const bool mgt = (fl[0] & 4) != 0;
   if (!mgt) return;  // topk_mask false: indices masked to 0, and mask_gt zeroes the row anyway
   if (A <= TOPK) {
-    for (int a = 0; a < A; ++a) fl[a] |= 2;
+    for (int a = lane; a < A; a += 64) fl[a] |= 2;
     return;
   }
-  KV h[TOPK];
-  for (int k = 0; k < TOPK; ++k) h[k] = KV{m[k], k};
-  // make_heap
-  for (int parent = (TOPK - 2) / 2;; --parent) {
-    adjust_heap(h, parent, TOPK, h[parent]);
-    if (parent == 0) break;
+  KV* h = heap[wave];
+  if (lane == 0) {
+    for (int k = 0; k < TOPK; ++k) h[k] = KV{m[k], k};
+    for (int parent = (TOPK - 2) / 2;; --parent) {  // make_heap
+      adjust_heap(h, parent, TOPK, h[parent]);
+      if (parent == 0) break;
+    }
   }
-  for (int a = TOPK; a < A; ++a) {
-    float v = m[a];
-    if (v > h[0].v) adjust_heap(h, 0, TOPK, KV{v, a});  // __pop_heap(first, middle, i): top replaced by *i
+  __builtin_amdgcn_wave_barrier();
+  for (int a0 = TOPK; a0 < A; a0 += 64) {
+    const int a = a0 + lane;
+    const float v = a < A ? m[a] : -INFINITY;
+    unsigned long long cand = __ballot(v > h[0].v);
+    while (cand) {
+      const int j = __ffsll((long long)cand) - 1;
+      cand &= cand - 1;
+      const float vj = __shfl(v, j, 64);
+      if (lane == 0 && vj > h[0].v) adjust_heap(h, 0, TOPK, KV{vj, a0 + j});  // __pop_heap(first, middle, i)
+      __builtin_amdgcn_wave_barrier();
+      cand &= __ballot(v > h[0].v);  // the top only rises: drop lanes that no longer beat it
+    }
   }
-  for (int k = 0; k < TOPK; ++k) fl[h[k].i] |= 2;
+  if (lane < TOPK) fl[h[lane].i] |= 2;
 }
 
 // ---- assign: per (b, a) ----
@@ -567,7 +583,7 @@ extern "C" int adr_det_loss(int dtype, const void* f0, const void* f1, const voi
   if (nmax > 0) {
     long tot = (long)rows * A;
     LDISPATCH(tal_metrics_kernel, dim3(cdiv(tot, 256)), dim3(256), L, B, nmax, nc, gt, pbox, align, ovl, flags);
-    hipLaunchKernelGGL(tal_topk_kernel, dim3(cdiv((long)rows, 64)), dim3(64), 0, st, align, flags, (int)rows, A);
+    hipLaunchKernelGGL(tal_topk_kernel, dim3(cdiv((long)rows, 4)), dim3(256), 0, st, align, flags, (int)rows, A);
     hipLaunchKernelGGL(tal_assign_kernel, dim3(cdiv((long)n, 256)), dim3(256), 0, st, flags, ovl, B, nmax, A, tgi, fg);
     hipLaunchKernelGGL(tal_norm_kernel, dim3((unsigned)rows), dim3(256), 0, st, align, ovl, tgi, fg, B, nmax, A, pos);
   } else {

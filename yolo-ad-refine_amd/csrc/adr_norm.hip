@@ -213,55 +213,80 @@ __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restric
   }
 }
 
-// GroupNorm backward finalize: one block; loops over images for dgamma/dbeta.
-__global__ void __launch_bounds__(256) gn_bwd_finalize_kernel(const float* __restrict__ partial, int N, int chunks,
-                                                              int C, int G, double count,
-                                                              const float* __restrict__ mean,
-                                                              const float* __restrict__ rstd,
-                                                              const float* __restrict__ gamma, float* dgamma,
-                                                              float* dbeta, float* A, float* B, float* Cc) {
-  int cpg = C / G;
+// GroupNorm backward finalize, per image (grid N): channel sums over chunks -> group sums -> dx coefficients
+// A, B, C (dx = A*g + B*x + C with per-(n,c) coefficients).
+__global__ void __launch_bounds__(256) gn_bwd_coef_kernel(const float* __restrict__ partial, int chunks, int C, int G,
+                                                          double count, const float* __restrict__ mean,
+                                                          const float* __restrict__ rstd,
+                                                          const float* __restrict__ gamma, float* A, float* B,
+                                                          float* Cc) {
+  const int n = blockIdx.x, cpg = C / G;
+  __shared__ double sa[1024], sg[1024];
   __shared__ double s1[64], s2[64];
   for (int c = threadIdx.x; c < C; c += 256) {
-    if (dgamma) dgamma[c] = 0.f;
-    if (dbeta) dbeta[c] = 0.f;
+    const int g = c / cpg;
+    const double mu = mean[n * G + g], rs = rstd[n * G + g];
+    double a = 0.0, b = 0.0;
+    for (int ch = 0; ch < chunks; ++ch) {
+      const float* p = partial + ((long)n * chunks + ch) * 2 * C;
+      a += p[c];
+      b += p[C + c];
+    }
+    const double gm = gamma ? gamma[c] : 1.0;
+    sa[c] = gm * a;                  // sum dxhat
+    sg[c] = gm * (b - mu * a) * rs;  // sum dxhat * xhat
   }
   __syncthreads();
-  for (int n = 0; n < N; ++n) {
-    // per-channel sums for image n
-    for (int g = threadIdx.x; g < G; g += 256) {
-      double mu = mean[n * G + g], rs = rstd[n * G + g];
-      double S1 = 0.0, S2 = 0.0;
-      for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-        double a = 0.0, b = 0.0;
-        for (int ch = 0; ch < chunks; ++ch) {
-          const float* p = partial + ((long)n * chunks + ch) * 2 * C;
-          a += p[c];
-          b += p[C + c];
-        }
-        double gm = gamma ? gamma[c] : 1.0;
-        double sgx = (b - mu * a) * rs;  // sum g * xhat for channel c
-        if (dgamma) dgamma[c] += (float)sgx;
-        if (dbeta) dbeta[c] += (float)a;
-        S1 += gm * a;    // sum dxhat
-        S2 += gm * sgx;  // sum dxhat * xhat
-      }
-      s1[g] = S1;
-      s2[g] = S2;
+  for (int g = threadIdx.x; g < G; g += 256) {
+    double S1 = 0.0, S2 = 0.0;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      S1 += sa[c];
+      S2 += sg[c];
+    }
+    s1[g] = S1;
+    s2[g] = S2;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int g = c / cpg;
+    const double mu = mean[n * G + g], rs = rstd[n * G + g];
+    const double gm = gamma ? gamma[c] : 1.0;
+    const double Bk = -rs * rs * s2[g] / count;
+    A[n * C + c] = (float)(rs * gm);
+    B[n * C + c] = (float)Bk;
+    Cc[n * C + c] = (float)(-rs * s1[g] / count - Bk * mu);
+  }
+}
+
+// GroupNorm dgamma / dbeta, per channel (grid C): fixed-order reduction over (image, chunk) of
+// (sum g*x - mu_n * sum g) * rstd_n and sum g.
+__global__ void __launch_bounds__(256) gn_bwd_param_kernel(const float* __restrict__ partial, int N, int chunks, int C,
+                                                           int G, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, float* dgamma,
+                                                           float* dbeta) {
+  const int c = blockIdx.x, g = c / (C / G);
+  double sgx = 0.0, sb = 0.0;
+  for (int it = threadIdx.x; it < N * chunks; it += 256) {
+    const int n = it / chunks;
+    const float* p = partial + (long)it * 2 * C;
+    const double a = p[c], b = p[C + c];
+    sgx += (b - (double)mean[n * G + g] * a) * (double)rstd[n * G + g];
+    sb += a;
+  }
+  __shared__ double r1[256], r2[256];
+  r1[threadIdx.x] = sgx;
+  r2[threadIdx.x] = sb;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) {
+      r1[threadIdx.x] += r1[threadIdx.x + o];
+      r2[threadIdx.x] += r2[threadIdx.x + o];
     }
     __syncthreads();
-    for (int c = threadIdx.x; c < C; c += 256) {
-      int g = c / cpg;
-      double mu = mean[n * G + g], rs = rstd[n * G + g];
-      double gm = gamma ? gamma[c] : 1.0;
-      double Ak = rs * gm;
-      double Bk = -rs * rs * s2[g] / count;
-      double Ck = -rs * s1[g] / count - Bk * mu;
-      A[n * C + c] = (float)Ak;
-      B[n * C + c] = (float)Bk;
-      Cc[n * C + c] = (float)Ck;
-    }
-    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = (float)r1[0];
+    if (dbeta) dbeta[c] = (float)r2[0];
   }
 }
 
@@ -272,21 +297,23 @@ __global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x
                                                          const float* __restrict__ shift, int per_sample, int act,
                                                          long npix, int HW, int C) {
   constexpr int VEC = 16 / sizeof(T);
-  const int G = C / VEC;
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = npix * G;
-  for (; i < total; i += (long)gridDim.x * blockDim.x) {
-    long pix = i / G;
-    int c0 = (int)(i % G) * VEC;
-    int n = (int)(pix / HW);
-    u32x4 v = ld16(x + pix * xcs + xco + c0);
+  const unsigned G = C / VEC;
+  const unsigned total = (unsigned)(npix * G);  // host guarantees < 2^32
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned pix = i / G;
+    const int c0 = (int)(i - pix * G) * VEC;
+    const int n = (int)(pix / (unsigned)HW);
+    const u32x4 v = ld16(x + (long)pix * xcs + xco + c0);
     const T* e = reinterpret_cast<const T*>(&v);
+    const int base = per_sample ? n * C + c0 : c0;
+    float sc[VEC], sh[VEC];
+    ld_coef<VEC>(scale + base, sc);
+    ld_coef<VEC>(shift + base, sh);
     u32x4 o;
     T* oe = reinterpret_cast<T*>(&o);
-    int base = per_sample ? n * C + c0 : c0;
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(act_fwd(act, to_f(e[k]) * scale[base + k] + shift[base + k]));
-    st16(z + pix * zcs + zco + c0, o);
+    for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(act_fwd(act, to_f(e[k]) * sc[k] + sh[k]));
+    st16(z + (long)pix * zcs + zco + c0, o);
   }
 }
 
@@ -303,33 +330,38 @@ __global__ void __launch_bounds__(256) affine_act_bwd_kernel(const T* __restrict
                                                              int coef_per_sample, int act, long npix, int HW, int C,
                                                              int accumulate) {
   constexpr int VEC = 16 / sizeof(T);
-  const int G = C / VEC;
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = npix * G;
-  for (; i < total; i += (long)gridDim.x * blockDim.x) {
-    long pix = i / G;
-    int c0 = (int)(i % G) * VEC;
-    int n = (int)(pix / HW);
-    u32x4 xv = ld16(x + pix * xcs + xco + c0);
-    u32x4 dv = ld16(dz + pix * dcs + dco + c0);
+  const unsigned G = C / VEC;
+  const unsigned total = (unsigned)(npix * G);  // host guarantees < 2^32
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const unsigned pix = i / G;
+    const int c0 = (int)(i - pix * G) * VEC;
+    const int n = (int)(pix / (unsigned)HW);
+    const u32x4 xv = ld16(x + (long)pix * xcs + xco + c0);
+    const u32x4 dv = ld16(dz + (long)pix * dcs + dco + c0);
     const T* xe = reinterpret_cast<const T*>(&xv);
     const T* de = reinterpret_cast<const T*>(&dv);
+    u32x4 prev = {0u, 0u, 0u, 0u};
+    if (accumulate) prev = ld16(dx + (long)pix * ocs + oco + c0);
+    const T* pe = reinterpret_cast<const T*>(&prev);
+    const int sb = per_sample ? n * C + c0 : c0;
+    const int cb = coef_per_sample ? n * C + c0 : c0;
+    float sc[VEC], sh[VEC], ca[VEC], cbv[VEC], cc[VEC];
+    ld_coef<VEC>(scale + sb, sc);
+    ld_coef<VEC>(shift + sb, sh);
+    ld_coef<VEC>(A + cb, ca);
+    ld_coef<VEC>(B + cb, cbv);
+    ld_coef<VEC>(Cc + cb, cc);
     u32x4 o;
     T* oe = reinterpret_cast<T*>(&o);
-    u32x4 prev;
-    if (accumulate) prev = ld16(dx + pix * ocs + oco + c0);
-    const T* pe = reinterpret_cast<const T*>(&prev);
-    int sb = per_sample ? n * C + c0 : c0;
-    int cb = coef_per_sample ? n * C + c0 : c0;
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
-      float xf = to_f(xe[k]);
-      float g = to_f(de[k]) * act_bwd(act, xf * scale[sb + k] + shift[sb + k]);
-      float r = A[cb + k] * g + B[cb + k] * xf + Cc[cb + k];
+      const float xf = to_f(xe[k]);
+      const float g = to_f(de[k]) * act_bwd(act, xf * sc[k] + sh[k]);
+      float r = ca[k] * g + cbv[k] * xf + cc[k];
       if (accumulate) r += to_f(pe[k]);
       oe[k] = from_f<T>(r);
     }
-    st16(dx + pix * ocs + oco + c0, o);
+    st16(dx + (long)pix * ocs + oco + c0, o);
   }
 }
 
@@ -417,9 +449,13 @@ extern "C" int adr_gn_finalize(const float* partial, int N, int chunks, int C, i
 extern "C" int adr_gn_bwd_finalize(const float* partial, int N, int chunks, int C, int G, double count,
                                    const float* mean, const float* rstd, const float* gamma, float* dgamma,
                                    float* dbeta, float* A, float* B, float* Cc, void* stream) {
-  ADR_REQUIRE(G <= 64 && C % G == 0, "gn_bwd_finalize: G=%d C=%d", G, C);
-  hipLaunchKernelGGL(gn_bwd_finalize_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, partial, N, chunks, C, G,
-                     count, mean, rstd, gamma, dgamma, dbeta, A, B, Cc);
+  ADR_REQUIRE(G <= 64 && C <= 1024 && C % G == 0, "gn_bwd_finalize: G=%d C=%d", G, C);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(gn_bwd_coef_kernel, dim3(N), dim3(256), 0, st, partial, chunks, C, G, count, mean, rstd, gamma, A,
+                     B, Cc);
+  if (dgamma || dbeta)
+    hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(C), dim3(256), 0, st, partial, N, chunks, C, G, mean, rstd, dgamma,
+                       dbeta);
   return check_launch("adr_gn_bwd_finalize");
 }
 
@@ -430,6 +466,7 @@ extern "C" int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* 
   ADR_REQUIRE(C % vec == 0 && xcs % vec == 0 && xco % vec == 0 && zcs % vec == 0 && zco % vec == 0,
               "affine_act: misaligned view (C=%d)", C);
   long npix = (long)N * HW;
+  ADR_REQUIRE(npix * (C / vec) < (1l << 32), "affine_act: %ld vectors exceed the 32-bit index range", npix * (C / vec));
   int grid = grid_for(npix * (C / vec));
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)
@@ -450,6 +487,8 @@ extern "C" int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, co
                   ocs % vec == 0 && oco % vec == 0,
               "affine_act_bwd: misaligned view");
   long npix = (long)N * HW;
+  ADR_REQUIRE(npix * (C / vec) < (1l << 32), "affine_act_bwd: %ld vectors exceed the 32-bit index range",
+              npix * (C / vec));
   int grid = grid_for(npix * (C / vec));
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)

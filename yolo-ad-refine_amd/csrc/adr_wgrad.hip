@@ -1,0 +1,267 @@
+// bf16 weight-gradient GEMM for NHWC convolutions (the WGRAD third of adr_gemm.hip's engine, re-tiled):
+//   dw[co][tap][ci] = sum_p dy[p][co] * x[n, oy*s-p+kh, ox*s-p+kw, ci]        (p = (n, oy, ox), split over p)
+// Both operands arrive as [p][channel] rows (channels contiguous in HBM). They are staged into LDS as
+// plain row images — 16-byte global loads stored as 16-byte LDS writes, no scalar transposition — and the
+// MFMA fragments, which need 8 consecutive reduction rows per lane, are read with gfx950's transposing
+// ds_read_b64_tr_b16 (two 4-row reads per fragment).
+//
+// MFMA v_mfma_f32_16x16x32_bf16: lane l supplies A[l&15][k(8(l>>4)+j)] and B[k(8(l>>4)+j)][l&15], j < 8.
+// The k-slot -> LDS-row map is a free permutation shared by A and B: slot (g = l>>4, j) reads row
+// 4g + j (j < 4) and 16 + 4g + (j-4) (j >= 4), so the two 16-lane groups of each 32-lane half read 8
+// consecutive rows; with the row pitch an odd multiple of 32 bytes those 8 rows hit 8 disjoint bank windows
+// (conflict-free, MI355X bank = (addr/4) % 64 for tr reads).
+//
+// Tile: BM output channels x BN input channels of one tap. 4 waves as WM x WN spatial x WK reduction
+// slices (WK > 1 for thin tiles, combined through LDS at the end). Split over p for parallelism; split
+// partials are reduced in fixed order by adr_gemm.hip's wgrad_reduce (deterministic).
+#include "adr_common.h"
+#include "adr_wgrad.h"
+
+namespace adr {
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
+
+struct WgArgs {
+  const __bf16* x;
+  const __bf16* dy;
+  float* out;  // [split][K][RS][C] partials (or dw itself when splits == 1 and not accumulating)
+  int n, h, w, c, xcs, xco;
+  int k, r, s, sh, sw, ph, pw, ho, wo, ycs, yco;
+  long red_total;
+  long red_per_split;
+  int ksteps;
+  int ctiles;  // input-channel tiles per tap
+  int accumulate;
+};
+
+__device__ __forceinline__ v4s tr_read(const __bf16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
+  constexpr int WM = BM / 16 < 2 ? BM / 16 : 2;
+  constexpr int WN = BN / 16 < 2 ? BN / 16 : 2;
+  constexpr int WK = 4 / (WM * WN);
+  constexpr int R = 32 * WK;  // reduction rows per k-step
+  constexpr int WROWS = BM / WM, WCOLS = BN / WN;
+  constexpr int TM = WROWS / 16, TN = WCOLS / 16;
+  // row pitch (elements): odd multiple of 16 elements (32 bytes)
+  constexpr int PA = ((BM / 16) % 2 == 1) ? BM : BM + 16;
+  constexpr int PB = ((BN / 16) % 2 == 1) ? BN : BN + 16;
+  constexpr int A_CHT = R * BM / 8, B_CHT = R * BN / 8;  // 16-byte chunks per k-step
+  constexpr int A_CH = (A_CHT + 255) / 256, B_CH = (B_CHT + 255) / 256;
+
+  __shared__ __attribute__((aligned(16))) __bf16 As[R * PA];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[R * PB];
+  __shared__ float red[WK > 1 ? (WK - 1) * BM * BN : 1];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wk = wave / (WM * WN), wmn = wave % (WM * WN), wm = wmn / WN, wn = wmn % WN;
+  const int RS = a.r * a.s;
+  // blockIdx.x -> (co tile, tap, ci tile); blockIdx.y = split
+  int bid = blockIdx.x;
+  const int ct = bid % a.ctiles;
+  bid /= a.ctiles;
+  const int tap = bid % RS;
+  const int mt = bid / RS;
+  const int m0 = mt * BM, c0 = ct * BN;
+  const int kh = tap / a.s, kw = tap % a.s;
+  const long pbeg = (long)blockIdx.y * a.red_per_split;
+  const long pend = min(a.red_total, pbeg + a.red_per_split);
+  const int hw = a.ho * a.wo;
+
+  u32x4 ra[A_CH], rb[B_CH];
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+
+  auto load = [&](int t) {
+    const long p0 = pbeg + (long)t * R;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int q = tid + 256 * i;
+      const int pl = q / (BM / 8), cc = q % (BM / 8);
+      const long p = p0 + pl;
+      const int co = m0 + cc * 8;
+      const bool ok = q < A_CHT && p < pend && co < a.k;
+      ra[i] = ok ? ld16(a.dy + p * a.ycs + a.yco + co) : zero;
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int q = tid + 256 * i;
+      const int pl = q / (BN / 8), cc = q % (BN / 8);
+      const long p = p0 + pl;
+      const int ci = c0 + cc * 8;
+      bool ok = q < B_CHT && p < pend && ci < a.c;
+      const long pp = ok ? p : 0;
+      const int img = (int)(pp / hw), rem = (int)(pp % hw);
+      const int oy = rem / a.wo, ox = rem % a.wo;
+      const int iy = oy * a.sh - a.ph + kh, ix = ox * a.sw - a.pw + kw;
+      ok = ok && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
+      rb[i] = ok ? ld16(a.x + ((long)(img * a.h + iy) * a.w + ix) * a.xcs + a.xco + ci) : zero;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int q = tid + 256 * i;
+      if (q < A_CHT) st16(&As[(q / (BM / 8)) * PA + (q % (BM / 8)) * 8], ra[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int q = tid + 256 * i;
+      if (q < B_CHT) st16(&Bs[(q / (BN / 8)) * PB + (q % (BN / 8)) * 8], rb[i]);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read addressing: lane (g, q4, p4) -> row rb + 4g + q4 (+16), column base + 4*p4
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  const int row0 = 32 * wk + 4 * g + q4;
+  const __bf16* a_base = As + row0 * PA + wm * WROWS + 4 * p4;
+  const __bf16* b_base = Bs + row0 * PB + wn * WCOLS + 4 * p4;
+
+  const int ksteps = a.ksteps;
+  if (ksteps > 0) {
+    load(0);
+    store();
+    __syncthreads();
+  }
+  for (int t = 0; t < ksteps; ++t) {
+    if (t + 1 < ksteps) load(t + 1);
+    bf16x8 fa[TM], fb[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      v4s lo = tr_read(a_base + i * 16);
+      v4s hi = tr_read(a_base + 16 * PA + i * 16);
+      v4s both[2] = {lo, hi};
+      fa[i] = *reinterpret_cast<bf16x8*>(both);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      v4s lo = tr_read(b_base + j * 16);
+      v4s hi = tr_read(b_base + 16 * PB + j * 16);
+      v4s both[2] = {lo, hi};
+      fb[j] = *reinterpret_cast<bf16x8*>(both);
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    __syncthreads();
+    if (t + 1 < ksteps) {
+      store();
+      __syncthreads();
+    }
+  }
+
+  // combine the WK reduction slices (waves wk > 0 publish, wave-slice 0 sums)
+  if constexpr (WK > 1) {
+    if (wk > 0) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rr = wm * WROWS + i * 16 + 4 * (lane >> 4) + e, cc = wn * WCOLS + j * 16 + (lane & 15);
+            red[(wk - 1) * BM * BN + rr * BN + cc] = acc[i][j][e];
+          }
+    }
+    __syncthreads();
+    if (wk > 0) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = wm * WROWS + i * 16 + 4 * (lane >> 4) + e, cc = wn * WCOLS + j * 16 + (lane & 15);
+#pragma unroll
+          for (int s2 = 0; s2 < WK - 1; ++s2) acc[i][j][e] += red[s2 * BM * BN + rr * BN + cc];
+        }
+  }
+  float* part = a.out + (long)blockIdx.y * a.k * ((long)RS * a.c);
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int ci = c0 + wn * WCOLS + j * 16 + (lane & 15);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = m0 + wm * WROWS + i * 16 + 4 * (lane >> 4) + e;
+        if (co < a.k && ci < a.c) {
+          float* o = part + ((long)co * RS + tap) * a.c + ci;
+          *o = a.accumulate ? *o + acc[i][j][e] : acc[i][j][e];
+        }
+      }
+    }
+}
+
+static int wg_pick16(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128; }
+
+template <int BM>
+static void launch_bm(int bn, dim3 grid, const WgArgs& g, hipStream_t st) {
+  switch (bn) {
+    case 16: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 16>), grid, dim3(256), 0, st, g); break;
+    case 32: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 32>), grid, dim3(256), 0, st, g); break;
+    case 64: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 64>), grid, dim3(256), 0, st, g); break;
+    default: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 128>), grid, dim3(256), 0, st, g); break;
+  }
+}
+
+// tiles, k-step rows and split count for a bf16 WGRAD; splits bounded so the fp32 partials stay small
+
+WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
+  WgPlan p;
+  p.bm = wg_pick16(d->k);
+  p.bn = wg_pick16(d->c);
+  const int wm = p.bm / 16 < 2 ? p.bm / 16 : 2, wn = p.bn / 16 < 2 ? p.bn / 16 : 2;
+  p.R = 32 * (4 / (wm * wn));
+  const long red = (long)d->n * d->ho * d->wo;
+  const long outsz = (long)d->k * d->r * d->s * d->c;
+  p.tiles = cdiv(d->k, p.bm) * d->r * d->s * cdiv(d->c, p.bn);
+  long s = (512 + p.tiles - 1) / p.tiles;                   // ~2 workgroups per CU
+  const long by_work = red / ((long)p.R * 32);              // >= 32 k-steps per split
+  const long by_bytes = (24l << 20) / (outsz * 4);          // <= 24 MB of partials (stays in L2/MALL)
+  if (s > by_work) s = by_work;
+  if (s > by_bytes) s = by_bytes;
+  if (s < 1) s = 1;
+  if (s > 65535) s = 65535;
+  long per = (red + s - 1) / s;
+  per = (per + p.R - 1) / p.R * p.R;
+  p.splits = (int)((red + per - 1) / per);
+  p.per = per;
+  return p;
+}
+
+int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
+                      const WgPlan& p, hipStream_t st) {
+  WgArgs g;
+  g.x = (const __bf16*)x;
+  g.dy = (const __bf16*)dy;
+  g.out = out;
+  g.n = d->n; g.h = d->h; g.w = d->w; g.c = d->c; g.xcs = d->x_cstride; g.xco = d->x_coff;
+  g.k = d->k; g.r = d->r; g.s = d->s; g.sh = d->stride_h; g.sw = d->stride_w; g.ph = d->pad_h; g.pw = d->pad_w;
+  g.ho = d->ho; g.wo = d->wo; g.ycs = d->y_cstride; g.yco = d->y_coff;
+  g.red_total = (long)d->n * d->ho * d->wo;
+  g.red_per_split = p.per;
+  g.ksteps = (int)(p.per / p.R);
+  g.ctiles = cdiv(d->c, p.bn);
+  g.accumulate = accumulate;
+  dim3 grid(p.tiles, p.splits);
+  switch (p.bm) {
+    case 16: launch_bm<16>(p.bn, grid, g, st); break;
+    case 32: launch_bm<32>(p.bn, grid, g, st); break;
+    case 64: launch_bm<64>(p.bn, grid, g, st); break;
+    default: launch_bm<128>(p.bn, grid, g, st); break;
+  }
+  return check_launch("adr_conv2d_wgrad(bf16)");
+}
+
+}  // namespace adr
