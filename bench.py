@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0)
+    ap.add_argument("--no-graph", action="store_true", help="launch every kernel from Python (no hipGraph replay)")
+    ap.add_argument("--roofline-steps", type=int, default=2)
     args = ap.parse_args()
 
     import torch
@@ -99,11 +101,13 @@ def main():
 
     for _ in range(args.warmup):
         tr.step(batch)
+    if not args.no_graph:
+        tr.capture(batch)  # fwd+loss+bwd and the optimizer tail as two hipGraphs (all-reduce between them)
+        tr.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    K.timing_begin()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         items = tr.step(batch)
@@ -113,7 +117,14 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    # per-kernel durations for the roofline: HIP events on the launch stream around every conv-GEMM launch of
+    # the same step, run eagerly right after the timed replays (a graph replay cannot be split per kernel)
+    graphs, tr.graphs = tr.graphs, None
+    K.timing_begin()
+    for _ in range(args.roofline_steps):
+        tr.step(batch)
     ktimes = K.timing_end()
+    tr.graphs = graphs
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -133,7 +144,7 @@ def main():
                                    f"SGD+EMA", "global_batch": world * args.bs, "img": args.img,
                        "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "loss_finite": finite,
-            "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3),
+            "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3), "hipgraph": not args.no_graph,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

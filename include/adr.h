@@ -62,6 +62,14 @@ int adr_conv2d_dgrad(const adr_conv_desc* d, const void* dy, const void* w, cons
 size_t adr_conv2d_wgrad_workspace(const adr_conv_desc* d);
 int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const void* dy, float* dw, int accumulate,
                      void* ws, size_t ws_bytes, void* stream);
+/* The two phases of adr_conv2d_wgrad, for callers that schedule (or time) them separately:
+ * partials writes [splits][k][r][s][c] fp32 slabs to `out` (splits = adr_conv2d_wgrad_splits(d); with one
+ * split `out` may be dw itself, accumulate allowed for bf16), adr_wgrad_reduce sums the slabs in a fixed
+ * order into dw (+= if accumulate). */
+int adr_conv2d_wgrad_splits(const adr_conv_desc* d);
+int adr_conv2d_wgrad_partials(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
+                              void* stream);
+int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accumulate, void* stream);
 
 
 /* ---------------------------------------------------------------------------------------------------------
@@ -270,12 +278,16 @@ int adr_det_loss(int dtype, const void* f0, const void* f1, const void* f2, int 
  * (group 0 decayed weights, 1 norm weights, 2 biases, 3 buffers / frozen: EMA only);
  * chunk = {int entry; int pad; int64 start; int64 len}. Both tables live in device memory.
  * adr_opt_step: clip_grad_norm_(10) + SGD(momentum, nesterov, per-group lr / weight decay) + EMA
- * (ema = d*ema + (1-d)*p after the update); norm_out (optional) receives the pre-clip total norm. */
+ * (ema = d*ema + (1-d)*p after the update); norm_out (optional) receives the pre-clip total norm.
+ * hyper is DEVICE memory: [lr0, lr1, lr2, wd0, wd1, wd2, momentum, nesterov, first, ema_decay] (first != 0:
+ * momentum buffer initialised to the gradient), so a captured hipGraph of the step follows the schedule. */
 int adr_opt_entry_size(void);
 int adr_opt_chunk_size(void);
-int adr_opt_step(const void* tab, const void* chunks, int nchunks, float* partial, float max_norm, float lr0,
-                 float lr1, float lr2, float wd0, float wd1, float wd2, float momentum, int nesterov, int first,
-                 float ema_decay, float* norm_out, void* stream);
+int adr_opt_step(const void* tab, const void* chunks, int nchunks, float* partial, float max_norm,
+                 const float* hyper, float* norm_out, void* stream);
+/* dst[0..n) = vals[0..n) (host array, n <= 16) as a stream-ordered kernel (values travel as kernel
+ * arguments: no host buffer lifetime to manage, safe to enqueue ahead of a graph replay). */
+int adr_set_f32(float* dst, const float* vals, int n, void* stream);
 /* gradient (or, when g == NULL, value) gather into / scatter from a flat fp32 buffer at per-entry offsets
  * (the DDP all-reduce bucket). */
 int adr_flat_copy(const void* tab, const void* chunks, int nchunks, float* flat, const int64_t* offsets,

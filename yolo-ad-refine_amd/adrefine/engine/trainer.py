@@ -8,6 +8,11 @@ DDP :217-273) on libadr_hip:
   [DDP] all-reduce SUM of the arena over RCCL (== the reference's loss*world_size followed by DDP's average)
   clip_grad_norm_(10) + SGD(momentum, nesterov=True, 3 param groups) + EMA   (one fused multi-tensor pair)
 
+The step can be captured once into HIP graphs (`capture(batch)`, torch.cuda.CUDAGraph over hipGraph): one graph
+for zero + forward + loss + backward, one for the optimizer tail, with the RCCL all-reduce between them. Replay
+costs two launches per step instead of ~2000 kernel launches from Python. Per-step scalars (lr per group,
+EMA decay, first-step flag) live in a device vector written by a stream-ordered kernel before each replay.
+
 Parameters that never receive a gradient (e.g. AdaptiveDynamicTanh.scale_weights, unused by the reference's
 forward) are skipped by SGD exactly like torch.optim.SGD skips p.grad is None.
 Mixed precision: the reference runs fp16 autocast + GradScaler; this build computes in bf16 (fp32 exponent
@@ -15,6 +20,7 @@ range), so no loss scaling is needed and the GradScaler is the identity.
 """
 from __future__ import annotations
 
+import ctypes
 import math
 
 import numpy as np
@@ -103,6 +109,8 @@ class FusedTrainer:
         self.updates = 0
         self.ema_decay = ema_decay
         self.ema_tau = ema_tau
+        self.hyper = torch.zeros(16, dtype=torch.float32, device=dev)
+        self.graphs = None
 
     def _build_table(self):
         tab = np.zeros(len(self.entries), dtype=_ENTRY)
@@ -123,20 +131,86 @@ class FusedTrainer:
         loss.backward()
         return items
 
-    def step(self, batch):
-        items = self.forward_backward(batch)
+    def _set_hyper(self):
+        d = self.ema_decay * (1 - math.exp(-(self.updates + 1) / self.ema_tau))
+        vals = [self.lr[0], self.lr[1], self.lr[2], self.wd, 0.0, 0.0, self.momentum, 1.0,
+                1.0 if self.updates == 0 else 0.0, d]
+        arr = (ctypes.c_float * len(vals))(*vals)
+        lib.adr_set_f32(K.fptr(self.hyper), ctypes.cast(arr, ctypes.c_void_p), len(vals), K.stream())
+
+    def _allreduce(self):
         if self.world_size > 1:
             import torch.distributed as dist
             dist.all_reduce(self.grad, op=dist.ReduceOp.SUM, group=self.pg)
-        if self.tab_dev is None:  # the set of parameters that receive gradients is static: build once
-            self._build_table()
-        d = self.ema_decay * (1 - math.exp(-(self.updates + 1) / self.ema_tau))
+
+    def _opt(self):
         lib.adr_opt_step(K.fptr(self.tab_dev), K.fptr(self.chunks_dev), self.nchunks, K.fptr(self.partial),
-                         float(self.max_norm), float(self.lr[0]), float(self.lr[1]), float(self.lr[2]), float(self.wd),
-                         0.0, 0.0, float(self.momentum), 1, int(self.updates == 0), float(d), K.fptr(self.norm),
-                         K.stream())
+                         float(self.max_norm), K.fptr(self.hyper), K.fptr(self.norm), K.stream())
+
+    def _prepare(self, batch):
+        """{'img', 'gt'} on the device; 'gt' (B, nmax, 5) built from the collate_fn keys when absent."""
+        img = batch["img"]
+        gt = batch.get("gt")
+        if gt is None:
+            from ..utils.loss import preprocess_targets
+            gt = preprocess_targets(batch["batch_idx"], batch["cls"], batch["bboxes"], img.shape[0],
+                                    (img.shape[2], img.shape[3]))
+        return {"img": img.to(self.dev, non_blocking=True), "gt": gt.to(self.dev, non_blocking=True).float()}
+
+    def step(self, batch):
+        """zero grads + fwd + loss + bwd (+ all-reduce) + clip + SGD + EMA; returns the loss items (device)."""
+        self._set_hyper()
+        if self.graphs is not None:
+            g_fb, g_opt, items = self.graphs
+            if batch is not self.static_batch:
+                b = self._prepare(batch)
+                self.static_batch["img"].copy_(b["img"], non_blocking=True)
+                gt, sgt = b["gt"], self.static_batch["gt"]
+                if gt.shape[1] > sgt.shape[1]:
+                    raise RuntimeError(f"captured step holds {sgt.shape[1]} targets per image, batch has {gt.shape[1]}")
+                sgt.zero_()  # padded rows are masked out by the assigner (mask_gt), as the reference's own padding
+                sgt[:, :gt.shape[1]].copy_(gt, non_blocking=True)
+            g_fb.replay()
+            self._allreduce()
+            g_opt.replay()
+        else:
+            items = self.forward_backward(batch)
+            self._allreduce()
+            if self.tab_dev is None:  # the set of parameters that receive gradients is static: build once
+                self._build_table()
+            self._opt()
         self.updates += 1
         return items.detach()
+
+    def capture(self, batch, max_targets=None):
+        """Capture the step into HIP graphs. Call after at least one eager step (lazy caches, the parameter
+        table). The batch becomes the graph's static input (targets padded to max_targets per image); later
+        `step(b)` copies b into it."""
+        assert self.tab_dev is not None, "run one eager step before capture()"
+        b = self._prepare(batch)
+        gt = b["gt"]
+        cap = max(max_targets or gt.shape[1], gt.shape[1])
+        sgt = torch.zeros(gt.shape[0], cap, 5, dtype=torch.float32, device=self.dev)
+        sgt[:, :gt.shape[1]].copy_(gt)
+        self.static_batch = {"img": b["img"].clone(), "gt": sgt}
+        # warm-up on the capture side stream mutates BN running stats: snapshot and restore them
+        bufs = list(self.model.buffers())
+        saved = [t.clone() for t in bufs]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            self.forward_backward(self.static_batch)
+        torch.cuda.current_stream().wait_stream(s)
+        for t, v in zip(bufs, saved):
+            t.copy_(v)
+        g_fb, g_opt = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g_fb):
+            items = self.forward_backward(self.static_batch)
+        with torch.cuda.graph(g_opt):
+            self._opt()
+        self.graphs = (g_fb, g_opt, items)
+        torch.cuda.synchronize()
+        return self.static_batch
 
     def param_grad(self, name):
         for ei, (n, t, _, isp) in enumerate(self.entries):

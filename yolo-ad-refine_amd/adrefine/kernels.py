@@ -87,8 +87,9 @@ def roofline_report(recs, dtype, hbm_gbs, mfma_tf):
             "frac": round(achieved / peak, 4), "traffic": None, "kernel": tag, "launches": cnt,
             "avg_us": round(1e6 * t / cnt, 2), "alg_bytes_per_launch": int(nb / cnt),
             "alg_flops_per_launch": int(fl / cnt), "achieved_gbs": round(gbs, 1), "achieved_tfs": round(tfs, 2),
-            "share_of_timed_gemm_time": round(t / total_t, 3),
-            "families": {k: {"launches": v[0], "ms_total": round(1e3 * v[3], 3)} for k, v in sorted(agg.items())}}
+            "share_of_timed_conv_time": round(t / total_t, 3),
+            "kernels": {k: {"launches": v[0], "ms_total": round(1e3 * v[3], 3), "avg_us": round(1e6 * v[3] / v[0], 2)}
+                        for k, v in sorted(agg.items(), key=lambda kv: -kv[1][3])}}
 
 
 def dcode(dtype) -> int:
@@ -215,12 +216,55 @@ def conv_desc(n, h, w, c, xcs, k, r, s, sh, sw, ph, pw, ycs, dtype):
     return d, ho, wo
 
 
+def _gemm_symbol(dtype_code, bn, mode):
+    """Kernel symbol of adr_gemm.hip's gemm_kernel<T, BN, MODE> as rocprofv3 reports it."""
+    t = "DF16b" if dtype_code == BF16 else "f"
+    return f"_ZN3adr11gemm_kernelI{t}Li{bn}ELi{mode}EEEvNS_8GemmArgsE"
+
+
+def _conv_work(d):
+    """(algorithmic bytes, flops) of one dense conv contraction: x, w, y each touched once."""
+    es = 2 if d.dtype == BF16 else 4
+    nbytes = es * (d.n * d.h * d.w * d.c + d.k * d.r * d.s * d.c + d.n * d.ho * d.wo * d.k)
+    return nbytes, 2 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c
+
+
+def conv_fwd(d, xp, wp, bias, yp, stats=None, accumulate=0):
+    tok = _t0(_gemm_symbol(d.dtype, _bn_of(d.k), 0), *_conv_work(d))
+    lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(wp), bias, ctypes.c_void_p(yp), stats,
+                       int(accumulate), stream())
+    _t1(tok)
+
+
+def conv_dgrad(d, dyp, wp, bias, dxp, accumulate=0):
+    tok = _t0(_gemm_symbol(d.dtype, _bn_of(d.c), 1), *_conv_work(d))
+    lib.adr_conv2d_dgrad(ctypes.byref(d), ctypes.c_void_p(dyp), ctypes.c_void_p(wp), bias, ctypes.c_void_p(dxp),
+                         int(accumulate), stream())
+    _t1(tok)
+
+
 def _wgrad(d, xp, dyp, K, C, RS, device):
-    dw = torch.empty(K * RS * C, dtype=torch.float32, device=device)
-    ws_bytes = lib.adr_conv2d_wgrad_workspace(ctypes.byref(d))
-    ws = torch.empty(max(ws_bytes // 4, 1), dtype=torch.float32, device=device)
-    lib.adr_conv2d_wgrad(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(dw), 0, fptr(ws),
-                         ws_bytes, stream())
+    """dw (K, RS, C) fp32 = WGRAD partial GEMM (+ the fixed-order split reduction when split)."""
+    n = K * RS * C
+    dw = torch.empty(n, dtype=torch.float32, device=device)
+    splits = lib.adr_conv2d_wgrad_splits(ctypes.byref(d))
+    es = 2 if d.dtype == BF16 else 4
+    name = (f"void adr::wgrad_bf16_kernel<{_bn_of(K)}, {_bn_of(C)}>(adr::WgArgs)" if d.dtype == BF16
+            else _gemm_symbol(F32, _bn_of(C), 2))
+    work = (es * (d.n * d.h * d.w * d.c + d.n * d.ho * d.wo * d.k) + 4 * n, 2 * d.n * d.ho * d.wo * d.k * RS * d.c)
+    if splits == 1:
+        tok = _t0(name, *work)
+        lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(dw), 0,
+                                      stream())
+        _t1(tok)
+        return dw
+    ws = torch.empty(splits * n, dtype=torch.float32, device=device)
+    tok = _t0(name, *work)
+    lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(ws), 0, stream())
+    _t1(tok)
+    tok = _t0("adr::wgrad_reduce_kernel(float const*, float*, long, int, int)", 4 * n * (splits + 1), n * splits)
+    lib.adr_wgrad_reduce(fptr(ws), fptr(dw), n, splits, 0, stream())
+    _t1(tok)
     return dw
 
 
@@ -256,12 +300,7 @@ class Conv2dFn(torch.autograd.Function):
             tiles = lib.adr_conv2d_fwd_stat_tiles(ctypes.byref(d))
             stats = torch.empty(tiles * 2 * K, dtype=torch.float32, device=x.device)
         bf = b.detach().float().contiguous() if b is not None else None
-        es = x.element_size()
-        tok = _t0(f"gemm_fwd<{'bf16' if es == 2 else 'f32'},BN={_bn_of(K)}>",
-                  es * (N * H * W * C + K * R * S * C + N * Ho * Wo * K), 2 * N * Ho * Wo * K * R * S * C)
-        lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(xp), fptr(wp), fptr(bf), ctypes.c_void_p(y.data_ptr()),
-                           fptr(stats), 0, stream())
-        _t1(tok)
+        conv_fwd(d, xp, wp.data_ptr(), fptr(bf), y.data_ptr(), fptr(stats))
         ctx.save_for_backward(x, wp)
         ctx.meta = (stride, pad, cpad, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
@@ -284,18 +323,9 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = empty_act(N, C, H, W, x.dtype, x.device)
             d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
-            es = x.element_size()
-            tok = _t0(f"gemm_dgrad<{'bf16' if es == 2 else 'f32'},BN={_bn_of(C)}>",
-                      es * (N * H * W * C + K * R * S * C + N * Ho * Wo * K), 2 * N * Ho * Wo * K * R * S * C)
-            lib.adr_conv2d_dgrad(ctypes.byref(d2), ctypes.c_void_p(dyp), fptr(wp), None,
-                                 ctypes.c_void_p(dx.data_ptr()), 0, stream())
-            _t1(tok)
+            conv_dgrad(d2, dyp, wp.data_ptr(), None, dx.data_ptr())
         if ctx.needs_input_grad[1]:
-            es = x.element_size()
-            tok = _t0(f"gemm_wgrad<{'bf16' if es == 2 else 'f32'}>",
-                      es * (N * H * W * C + N * Ho * Wo * K) + 4 * K * R * S * C, 2 * N * Ho * Wo * K * R * S * C)
             dwk = _wgrad(d, xp, dyp, K, C, R * S, x.device)
-            _t1(tok)
             dw = sink_unpack(ctx.pw, dwk, wshape, cpad)
         if has_b and ctx.needs_input_grad[2]:
             db = sink(ctx.pb, _bias_grad(dy, K, N, Ho * Wo, dycs))
@@ -319,8 +349,7 @@ class ConvT2dFn(torch.autograd.Function):
         if (h2, w2) != (H, W):
             raise RuntimeError("ConvT2dFn: inconsistent geometry")
         bf = b.detach().float().contiguous() if b is not None else None
-        lib.adr_conv2d_dgrad(ctypes.byref(d), ctypes.c_void_p(xp), fptr(wp), fptr(bf), ctypes.c_void_p(y.data_ptr()),
-                             0, stream())
+        conv_dgrad(d, xp, wp.data_ptr(), fptr(bf), y.data_ptr())
         ctx.save_for_backward(x, wp)
         ctx.meta = (stride, pad, w.shape, b is not None, Ho, Wo)
         ctx.pw, ctx.pb = w, b
@@ -338,8 +367,7 @@ class ConvT2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = empty_act(N, Ci, H, W, x.dtype, x.device)
             d, _, _ = conv_desc(N, Ho, Wo, Co, dycs, Ci, R, S, stride, stride, pad, pad, Ci, x.dtype)
-            lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(dyp), fptr(wp), None, ctypes.c_void_p(dx.data_ptr()),
-                               None, 0, stream())
+            conv_fwd(d, dyp, wp.data_ptr(), None, dx.data_ptr())
         if ctx.needs_input_grad[1]:
             # equivalent conv: input = dy_T (N, Ho, Wo, Co), output grad = x_T (N, H, W, Ci)
             d, _, _ = conv_desc(N, Ho, Wo, Co, dycs, Ci, R, S, stride, stride, pad, pad, xcs, x.dtype)
@@ -1130,8 +1158,7 @@ class PaddedConvFn(torch.autograd.Function):
             lib.adr_cast(F32, fptr(b.detach().float().contiguous()), F32, fptr(bp), K, stream())
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, kpad, R, S, stride, stride, pad, pad, kpad, dtype)
         y = empty_act(N, kpad, Ho, Wo, dtype, x.device)
-        lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(xp), fptr(wp), fptr(bp), ctypes.c_void_p(y.data_ptr()),
-                           None, 0, stream())
+        conv_fwd(d, xp, wp.data_ptr(), fptr(bp), y.data_ptr())
         ctx.save_for_backward(x, wp)
         ctx.meta = (stride, pad, kpad, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
@@ -1149,8 +1176,7 @@ class PaddedConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = empty_act(N, C, H, W, x.dtype, x.device)
             d2, _, _ = conv_desc(N, H, W, C, C, kpad, R, S, stride, stride, pad, pad, dycs, x.dtype)
-            lib.adr_conv2d_dgrad(ctypes.byref(d2), ctypes.c_void_p(dyp), fptr(wp), None, ctypes.c_void_p(dx.data_ptr()),
-                                 0, stream())
+            conv_dgrad(d2, dyp, wp.data_ptr(), None, dx.data_ptr())
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, kpad, R, S, stride, stride, pad, pad, dycs, x.dtype)
         if ctx.needs_input_grad[1]:
             dwk = _wgrad(d, xp, dyp, kpad, C, R * S, x.device)
@@ -1176,8 +1202,7 @@ class DCNFn(torch.autograd.Function):
         wp = pack_weight(w, dtype)  # KRSC [co][tap][c] == 1x1 weight over the [tap][c] columns
         d, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, Cout, dtype)
         y = empty_act(N, Cout, H, W, dtype, x.device)
-        lib.adr_conv2d_fwd(ctypes.byref(d), fptr(cols), fptr(wp), None, ctypes.c_void_p(y.data_ptr()), None, 0,
-                           stream())
+        conv_fwd(d, cols.data_ptr(), wp.data_ptr(), None, y.data_ptr())
         ctx.save_for_backward(x, om, cols, w)
         ctx.pw = w
         return y
@@ -1197,7 +1222,7 @@ class DCNFn(torch.autograd.Function):
         lib.adr_dcn_weight_t(dcode(dtype), fptr(w.detach().float().contiguous()), fptr(wt), Cout, C, stream())
         dcols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=dev)
         d, _, _ = conv_desc(N, H, W, Cout, dycs, 9 * C, 1, 1, 1, 1, 0, 0, 9 * C, dtype)
-        lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(dyp), fptr(wt), None, fptr(dcols), None, 0, stream())
+        conv_fwd(d, dyp, wt.data_ptr(), None, dcols.data_ptr())
         dw = None
         if ctx.needs_input_grad[2]:
             dwd, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, dycs, dtype)

@@ -502,58 +502,62 @@ static int wgrad_splits(const adr_conv_desc* d, int* bn_out, int* ntiles_out) {
 }
 
 extern "C" size_t adr_conv2d_wgrad_workspace(const adr_conv_desc* d) {
-  if (d->dtype == ADR_BF16) {
-    WgPlan p = wgrad_bf16_plan(d);
-    return p.splits > 1 ? (size_t)p.splits * d->k * d->r * d->s * d->c * sizeof(float) : 0;
-  }
   int bn, nt;
-  int splits = wgrad_splits(d, &bn, &nt);
+  const int splits = d->dtype == ADR_BF16 ? wgrad_bf16_plan(d).splits : wgrad_splits(d, &bn, &nt);
   return (size_t)splits * d->k * d->r * d->s * d->c * sizeof(float);
 }
 
-extern "C" int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const void* dy, float* dw, int accumulate,
-                                void* ws, size_t ws_bytes, void* stream) {
+extern "C" int adr_conv2d_wgrad_splits(const adr_conv_desc* d) {
+  if (d->dtype == ADR_BF16) return wgrad_bf16_plan(d).splits;
+  int bn, nt;
+  return wgrad_splits(d, &bn, &nt);
+}
+
+extern "C" int adr_conv2d_wgrad_partials(const adr_conv_desc* d, const void* x, const void* dy, float* out,
+                                         int accumulate, void* stream) {
   GemmArgs g{};
   int rc = fill_common(d, g);
   if (rc) return rc;
   hipStream_t st = (hipStream_t)stream;
-  const long nout = (long)d->k * d->r * d->s * d->c;
   if (d->dtype == ADR_BF16) {
     WgPlan p = wgrad_bf16_plan(d);
-    if (p.splits == 1) return wgrad_bf16_launch(d, x, dy, dw, accumulate, p, st);
-    size_t need = (size_t)p.splits * nout * sizeof(float);
-    ADR_REQUIRE(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu bytes", ws_bytes, need);
-    rc = wgrad_bf16_launch(d, x, dy, (float*)ws, 0, p, st);
-    if (rc) return rc;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(nout, 256)), dim3(256), 0, st, (const float*)ws, dw, nout,
-                       p.splits, accumulate);
-    return check_launch("adr_conv2d_wgrad");
+    ADR_REQUIRE(!accumulate || p.splits == 1, "conv wgrad partials: accumulate needs a single split");
+    return wgrad_bf16_launch(d, x, dy, out, accumulate, p, st);
   }
   int bn, ntiles;
   int splits = wgrad_splits(d, &bn, &ntiles);
-  size_t need = (size_t)splits * d->k * d->r * d->s * d->c * sizeof(float);
-  ADR_REQUIRE(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+  ADR_REQUIRE(!accumulate, "conv wgrad partials: fp32 path writes (no accumulate)");
   int BK = bk_of(d->dtype);
   long red = (long)d->n * d->ho * d->wo;
   long per = (red + splits - 1) / splits;
   per = (per + BK - 1) / BK * BK;
-  g.x = x; g.dy = dy; g.out = ws;
+  g.x = x; g.dy = dy; g.out = out;
   g.M = d->k; g.N = d->r * d->s * d->c;
   g.red_total = red;
   g.red_per_split = (int)per;
   g.ktiles = (int)(per / BK);
   g.ntiles = ntiles;
-  dim3 grid(cdiv(d->k, 128) * ntiles, splits);
-  if (splits > 1 || accumulate) {
-    // every (co, tap, ci) inside [K x RSC] is written by exactly one block per split (fp32 parity path)
-    launch_bn<float, MODE_WGRAD>(bn, grid, g, st);
-    rc = check_launch("adr_conv2d_wgrad");
-    if (rc) return rc;
-    hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(nout, 256)), dim3(256), 0, st, (const float*)ws, dw, nout,
-                       splits, accumulate);
-  } else {
-    g.out = dw;
-    launch_bn<float, MODE_WGRAD>(bn, grid, g, st);
-  }
-  return check_launch("adr_conv2d_wgrad");
+  // every (co, tap, ci) inside [K x RSC] is written by exactly one block per split
+  launch_bn<float, MODE_WGRAD>(bn, dim3(cdiv(d->k, 128) * ntiles, splits), g, st);
+  return check_launch("adr_conv2d_wgrad_partials");
+}
+
+extern "C" int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accumulate, void* stream) {
+  ADR_REQUIRE(n > 0 && splits >= 1, "wgrad_reduce: n=%ld splits=%d", n, splits);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, part, dw, n, splits,
+                     accumulate);
+  return check_launch("adr_wgrad_reduce");
+}
+
+extern "C" int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const void* dy, float* dw, int accumulate,
+                                void* ws, size_t ws_bytes, void* stream) {
+  const int splits = adr_conv2d_wgrad_splits(d);
+  const long nout = (long)d->k * d->r * d->s * d->c;
+  if (splits == 1 && (d->dtype == ADR_BF16 || !accumulate))
+    return adr_conv2d_wgrad_partials(d, x, dy, dw, accumulate, stream);
+  size_t need = (size_t)splits * nout * sizeof(float);
+  ADR_REQUIRE(ws && ws_bytes >= need, "conv wgrad: workspace %zu < %zu bytes", ws_bytes, need);
+  int rc = adr_conv2d_wgrad_partials(d, x, dy, (float*)ws, 0, stream);
+  if (rc) return rc;
+  return adr_wgrad_reduce((const float*)ws, dw, nout, splits, accumulate, stream);
 }

@@ -42,11 +42,14 @@ __global__ void __launch_bounds__(256) grad_sqnorm_kernel(const OptEntry* tab, c
   if (threadIdx.x == 0) partial[blockIdx.x] = (float)sh[0];
 }
 
-// lr[3], wd[3] per group; clip coef from partials; EMA decay d (host-computed from the update count)
+// hyper (device): [lr0, lr1, lr2, wd0, wd1, wd2, momentum, nesterov, first, ema_d] — read from memory so a
+// captured graph of the step picks up the per-step schedule; clip coefficient from the partials
 __global__ void __launch_bounds__(256) sgd_ema_kernel(const OptEntry* tab, const OptChunk* chunks, int nchunks,
-                                                      const float* partial, float max_norm, float lr0, float lr1,
-                                                      float lr2, float wd0, float wd1, float wd2, float momentum,
-                                                      int nesterov, int first, float ema_d, float* norm_out) {
+                                                      const float* partial, float max_norm,
+                                                      const float* __restrict__ hyper, float* norm_out) {
+  const float lr0 = hyper[0], lr1 = hyper[1], lr2 = hyper[2], wd0 = hyper[3], wd1 = hyper[4], wd2 = hyper[5];
+  const float momentum = hyper[6], ema_d = hyper[9];
+  const int nesterov = hyper[7] != 0.f, first = hyper[8] != 0.f;
   __shared__ double sh[256];
   __shared__ float coef_s;
   double s = 0.0;
@@ -103,17 +106,30 @@ using namespace adr;
 extern "C" int adr_opt_entry_size(void) { return (int)sizeof(OptEntry); }
 extern "C" int adr_opt_chunk_size(void) { return (int)sizeof(OptChunk); }
 
-extern "C" int adr_opt_step(const void* tab, const void* chunks, int nchunks, float* partial, float max_norm, float lr0,
-                            float lr1, float lr2, float wd0, float wd1, float wd2, float momentum, int nesterov,
-                            int first, float ema_decay, float* norm_out, void* stream) {
+extern "C" int adr_opt_step(const void* tab, const void* chunks, int nchunks, float* partial, float max_norm,
+                            const float* hyper, float* norm_out, void* stream) {
   ADR_REQUIRE(nchunks > 0, "opt_step: empty chunk table");
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(grad_sqnorm_kernel, dim3(nchunks), dim3(256), 0, st, (const OptEntry*)tab,
                      (const OptChunk*)chunks, partial);
   hipLaunchKernelGGL(sgd_ema_kernel, dim3(nchunks), dim3(256), 0, st, (const OptEntry*)tab, (const OptChunk*)chunks,
-                     nchunks, partial, max_norm, lr0, lr1, lr2, wd0, wd1, wd2, momentum, nesterov, first, ema_decay,
-                     norm_out);
+                     nchunks, partial, max_norm, hyper, norm_out);
   return check_launch("adr_opt_step");
+}
+
+struct F32x16 {
+  float v[16];
+};
+__global__ void set_f32_kernel(float* dst, F32x16 vals, int n) {
+  if ((int)threadIdx.x < n) dst[threadIdx.x] = vals.v[threadIdx.x];
+}
+
+extern "C" int adr_set_f32(float* dst, const float* vals, int n, void* stream) {
+  ADR_REQUIRE(n >= 0 && n <= 16, "set_f32: n=%d > 16", n);
+  F32x16 v{};
+  for (int i = 0; i < n; ++i) v.v[i] = vals[i];
+  hipLaunchKernelGGL(set_f32_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dst, v, n);
+  return check_launch("adr_set_f32");
 }
 
 extern "C" int adr_flat_copy(const void* tab, const void* chunks, int nchunks, float* flat, const int64_t* offsets,
