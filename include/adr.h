@@ -88,13 +88,13 @@ int adr_bn_finalize(const float* partial, int P, int C, double count, const floa
                     float* scale, float* shift, float* mean, float* rstd, void* stream);
 int adr_bn_bwd_finalize(const float* partial, int P, int C, double count, const float* mean, const float* rstd,
                         const float* gamma, float* dgamma, float* dbeta, float* A, float* B, float* Cc,
-                        int training, void* stream);
+                        int training, int accumulate, void* stream);
 int adr_gn_finalize(const float* partial, int N, int chunks, int C, int G, double count, const float* gamma,
                     const float* beta, float eps, float* scale, float* shift, float* mean, float* rstd,
                     void* stream);
 int adr_gn_bwd_finalize(const float* partial, int N, int chunks, int C, int G, double count, const float* mean,
                         const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* A, float* B,
-                        float* Cc, void* stream);
+                        float* Cc, int accumulate, void* stream);
 /* z = act(x * scale + shift), scale/shift per channel or (per_sample) per (image, channel). */
 int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco, const float* scale,
                    const float* shift, int per_sample, int act, int N, int HW, int C, void* stream);
@@ -198,7 +198,7 @@ int adr_gate_mlp(const float* in, float in_scale, int N, int Cin, const float* W
                  const float* W2, const float* b2, int H2, int act2, float* hidden, float* out, void* stream);
 int adr_gate_mlp_bwd(const float* in, float in_scale, int N, int Cin, const float* W1, int H1, int act1,
                      const float* W2, int H2, int act2, const float* hidden, const float* out, const float* dout,
-                     float* din, float* dW1, float* db1, float* dW2, float* db2, void* stream);
+                     float* din, float* dW1, float* db1, float* dW2, float* db2, int accumulate, void* stream);
 /* o (+)= g[n*gns + c*gcs] * s broadcast over pixels (adjoint of a global average pool). */
 int adr_bcast_fill(int dtype, const float* g, int gns, int gcs, float s, void* o, int ocs, int N, int HW, int C,
                    int accumulate, void* stream);
@@ -221,8 +221,8 @@ int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w, const floa
                    int W, int C, int k, void* stream);
 size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k);
 int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* w, void* dx, int ocs,
-                   float* dw, int N, int H, int W, int C, int k, int accumulate, float* ws, size_t ws_bytes,
-                   void* stream);
+                   float* dw, int N, int H, int W, int C, int k, int accumulate, int dw_accumulate, float* ws,
+                   size_t ws_bytes, void* stream);
 /* AdaptiveDynamicTanh (:2493-2577): y = (sum_i tanh(alpha_i x) imp[n,i]) * w[c] + b[c]; imp from adr_gate_mlp. */
 int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alphas, const float* imp, const float* w,
                  const float* b, void* y, int ycs, int N, int HW, int C, void* stream);
@@ -247,8 +247,8 @@ int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, void* y, in
                   void* stream);
 size_t adr_edffn_bwd_workspace(int N, int H, int W, int C);
 int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* M, const float* basis,
-                  int nuv, void* dx, int ocs, float* dw, int N, int H, int W, int C, float* ws, size_t ws_bytes,
-                  void* stream);
+                  int nuv, void* dx, int ocs, float* dw, int N, int H, int W, int C, int dw_accumulate, float* ws,
+                  size_t ws_bytes, void* stream);
 /* Flash attention, head_dim 64 (nn.MultiheadAttention core in CrossScaleAttentionTSSA, :2432/:2484):
  * o = softmax(q k^T * scale) v per (image, head); rows [b*L + l], channel strides cs / ocs, q/k/v channel
  * offsets qo/ko/vo (+ h*64). lse [B][heads][L] (natural log) is saved for the backward. */

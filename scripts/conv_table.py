@@ -1,0 +1,41 @@
+"""Per-conv-shape timing table of one eager train step (HIP events around every conv GEMM launch).
+usage: python scripts/conv_table.py [--bs 64] [--steps 2]   (GPU)"""
+import argparse
+import sys
+from collections import defaultdict
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT / "yolo-ad-refine_amd"))
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--bs", type=int, default=64)
+ap.add_argument("--steps", type=int, default=2)
+args = ap.parse_args()
+
+import torch
+import adrefine.kernels as K
+from adrefine.engine.trainer import FusedTrainer
+from adrefine.data.synthetic import train_batch
+from adrefine.nn.tasks import DetectionModel
+
+dev = torch.device("cuda", 0)
+model = DetectionModel(str(ROOT / "tests/configs/yolo11-701-YOLO-AD-Refine.yaml"), compute_dtype=torch.bfloat16).to(dev)
+tr = FusedTrainer(model, batch_size=args.bs)
+batch, _ = train_batch(args.bs, 640, seed=0, device=dev)
+for _ in range(2):
+    tr.step(batch)
+torch.cuda.synchronize()
+K.timing_begin()
+for _ in range(args.steps):
+    tr.step(batch)
+K.timing_end()
+agg = defaultdict(lambda: [0, 0, 0.0, 0.0])
+for tag, shape, nb, fl, t in K.timing_detail():
+    a = agg[shape if "reduce" not in tag else shape + " [reduce]"]
+    a[0] += 1; a[1] += nb; a[2] += fl; a[3] += t
+tot = sum(v[3] for v in agg.values()) / args.steps
+print(f"conv total per step: {1e3 * tot:.2f} ms")
+for shape, (n, nb, fl, t) in sorted(agg.items(), key=lambda kv: -kv[1][3]):
+    print(f"{1e3 * t / args.steps:7.3f} ms {n // args.steps:3d}x {1e6 * t / n:8.1f}us {nb / t / 1e9:7.0f} GB/s "
+          f"{fl / t / 1e12:6.1f} TF/s  {shape}")

@@ -38,26 +38,37 @@ def timing_begin():
 
 def timing_end():
     global _TIMING
+    global _DETAIL
     recs, _TIMING = _TIMING, None
     if not recs:
         return []
     torch.cuda.synchronize()
-    return [(tag, nbytes, flops, e0.elapsed_time(e1) * 1e-3) for tag, nbytes, flops, e0, e1 in recs]
+    _DETAIL = [(tag, shape, nb, fl, e0.elapsed_time(e1) * 1e-3) for tag, nb, fl, e0, e1, shape in recs]
+    return [(tag, nbytes, flops, e0.elapsed_time(e1) * 1e-3) for tag, nbytes, flops, e0, e1, _ in recs]
 
 
-def _t0(tag, nbytes, flops):
+def timing_detail():
+    """After timing_end(): per-launch (tag, shape, bytes, flops, seconds) of the last timed region."""
+    return _DETAIL
+
+
+_DETAIL = []
+
+
+def _t0(tag, nbytes, flops, shape=""):
     if _TIMING is None:
         return None
     e0 = torch.cuda.Event(enable_timing=True)
     e0.record()
-    return (tag, nbytes, flops, e0)
+    return (tag, nbytes, flops, e0, shape)
 
 
 def _t1(tok):
     if tok is not None:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
-        _TIMING.append((*tok, e1))
+        tag, nb, fl, e0, shape = tok
+        _TIMING.append((tag, nb, fl, e0, e1, shape))
 
 
 def _bn_of(n):
@@ -165,6 +176,25 @@ def sink(t, g):
     return None
 
 
+def grad_dst(t, numel, device):
+    """Where a kernel should write the gradient of parameter t: (tensor-or-None, ptr, accumulate). With a trainer
+    arena the kernel accumulates straight into t's arena slice (no temporary, no axpy launch) and autograd gets
+    None; otherwise a fresh fp32 buffer is returned for autograd."""
+    tgt = _target(t)
+    if tgt is not None:
+        if tgt.numel() != numel:
+            raise RuntimeError("grad_dst: gradient size mismatch")
+        tgt._adr_used = True
+        return None, fptr(tgt._adr_grad), 1
+    out = torch.empty(numel, dtype=torch.float32, device=device)
+    return out, fptr(out), 0
+
+
+def grad_ret(t, buf):
+    """The autograd return value for a grad_dst destination (reshaped to the parameter)."""
+    return None if buf is None else buf.view(t.shape)
+
+
 def sink_unpack(t, dw_krsc, shape, cpad=0):
     """unpack_weight_grad straight into the gradient arena (accumulate) when t has one."""
     tgt = _target(t)
@@ -222,6 +252,11 @@ def _gemm_symbol(dtype_code, bn, mode):
     return f"_ZN3adr11gemm_kernelI{t}Li{bn}ELi{mode}EEEvNS_8GemmArgsE"
 
 
+def _shape(d, mode):
+    return (f"{mode} n{d.n} {d.h}x{d.w} c{d.c}/{d.x_cstride} -> k{d.k}/{d.y_cstride} {d.r}x{d.s} "
+            f"s{d.stride_h} o{d.ho}x{d.wo}")
+
+
 def _conv_work(d):
     """(algorithmic bytes, flops) of one dense conv contraction: x, w, y each touched once."""
     es = 2 if d.dtype == BF16 else 4
@@ -230,14 +265,14 @@ def _conv_work(d):
 
 
 def conv_fwd(d, xp, wp, bias, yp, stats=None, accumulate=0):
-    tok = _t0(_gemm_symbol(d.dtype, _bn_of(d.k), 0), *_conv_work(d))
+    tok = _t0(_gemm_symbol(d.dtype, _bn_of(d.k), 0), *_conv_work(d), _shape(d, "fwd") if _TIMING is not None else "")
     lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(wp), bias, ctypes.c_void_p(yp), stats,
                        int(accumulate), stream())
     _t1(tok)
 
 
 def conv_dgrad(d, dyp, wp, bias, dxp, accumulate=0):
-    tok = _t0(_gemm_symbol(d.dtype, _bn_of(d.c), 1), *_conv_work(d))
+    tok = _t0(_gemm_symbol(d.dtype, _bn_of(d.c), 1), *_conv_work(d), _shape(d, "dgrad") if _TIMING is not None else "")
     lib.adr_conv2d_dgrad(ctypes.byref(d), ctypes.c_void_p(dyp), ctypes.c_void_p(wp), bias, ctypes.c_void_p(dxp),
                          int(accumulate), stream())
     _t1(tok)
@@ -252,28 +287,35 @@ def _wgrad(d, xp, dyp, K, C, RS, device):
     name = (f"void adr::wgrad_bf16_kernel<{_bn_of(K)}, {_bn_of(C)}>(adr::WgArgs)" if d.dtype == BF16
             else _gemm_symbol(F32, _bn_of(C), 2))
     work = (es * (d.n * d.h * d.w * d.c + d.n * d.ho * d.wo * d.k) + 4 * n, 2 * d.n * d.ho * d.wo * d.k * RS * d.c)
+    shp = _shape(d, f"wgrad/{splits}") if _TIMING is not None else ""
     if splits == 1:
-        tok = _t0(name, *work)
+        tok = _t0(name, *work, shp)
         lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(dw), 0,
                                       stream())
         _t1(tok)
         return dw
     ws = torch.empty(splits * n, dtype=torch.float32, device=device)
-    tok = _t0(name, *work)
+    tok = _t0(name, *work, shp)
     lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(ws), 0, stream())
     _t1(tok)
-    tok = _t0("adr::wgrad_reduce_kernel(float const*, float*, long, int, int)", 4 * n * (splits + 1), n * splits)
+    tok = _t0("adr::wgrad_reduce_kernel(float const*, float*, long, int, int)", 4 * n * (splits + 1), n * splits, shp)
     lib.adr_wgrad_reduce(fptr(ws), fptr(dw), n, splits, 0, stream())
     _t1(tok)
     return dw
 
 
-def _bias_grad(dy, K, N, HW, cs):
+def _bias_grad(dy, K, N, HW, cs, param=None):
+    """Per-channel sum of dy. With `param`, accumulates into its gradient destination (grad_dst) and returns
+    the autograd value; otherwise returns a fresh (K,) tensor."""
     dt = dcode(dy.dtype)
     chunks = lib.adr_nc_reduce_chunks(HW, STATS_ROWS)
     part = torch.empty(N * chunks * 2 * K, dtype=torch.float32, device=dy.device)
     lib.adr_nc_reduce(dt, 0, ctypes.c_void_p(dy.data_ptr()), cs, 0, None, 0, 0, None, None, 0, 0, N, HW, K,
                       STATS_ROWS, fptr(part), stream())
+    if param is not None:
+        db, p, acc = grad_dst(param, K, dy.device)
+        lib.adr_partial_sum(fptr(part), N * chunks, K, 0, p, acc, stream())
+        return grad_ret(param, db)
     db = torch.empty(K, dtype=torch.float32, device=dy.device)
     lib.adr_partial_sum(fptr(part), N * chunks, K, 0, fptr(db), 0, stream())
     return db
@@ -328,7 +370,7 @@ class Conv2dFn(torch.autograd.Function):
             dwk = _wgrad(d, xp, dyp, K, C, R * S, x.device)
             dw = sink_unpack(ctx.pw, dwk, wshape, cpad)
         if has_b and ctx.needs_input_grad[2]:
-            db = sink(ctx.pb, _bias_grad(dy, K, N, Ho * Wo, dycs))
+            db = _bias_grad(dy, K, N, Ho * Wo, dycs, ctx.pb)
         return dx, dw, db, None, None, None, None
 
 
@@ -374,7 +416,7 @@ class ConvT2dFn(torch.autograd.Function):
             dwk = _wgrad(d, dyp, xp, Ci, Co, R * S, x.device)
             dw = sink_unpack(ctx.pw, dwk, wshape)
         if has_b and ctx.needs_input_grad[2]:
-            db = sink(ctx.pb, _bias_grad(dy, Co, N, Ho * Wo, dycs))
+            db = _bias_grad(dy, Co, N, Ho * Wo, dycs, ctx.pb)
         return dx, dw, db, None, None, None
 
 
@@ -425,14 +467,18 @@ class BNActFn(torch.autograd.Function):
         lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale), fptr(shift),
                           0, ACT[act], N, HW, C, STATS_ROWS, fptr(part), stream())
         f = lambda: torch.empty(C, dtype=torch.float32, device=dev)  # noqa: E731
-        dgamma, dbeta, A, B, Cc = f(), f(), f(), f(), f()
+        A, B, Cc = f(), f(), f()
+        dgamma, pg, acc_g = grad_dst(gamma, C, dev)
+        dbeta, pb, acc_b = grad_dst(ctx.pbeta, C, dev)
+        if acc_g != acc_b:
+            raise RuntimeError("BN gamma/beta gradients must share one destination kind")
         lib.adr_bn_bwd_finalize(fptr(part), N * chunks, C, float(N * HW), fptr(mean), fptr(rstd), fptr(gamma.detach()),
-                                fptr(dgamma), fptr(dbeta), fptr(A), fptr(B), fptr(Cc), int(training), stream())
+                                pg, pb, fptr(A), fptr(B), fptr(Cc), int(training), acc_g, stream())
         dy = empty_act(N, C, H, W, y.dtype, dev)
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
                                fptr(Cc), 0, 0, ACT[act], N, HW, C, 0, stream())
-        return dy, None, sink(gamma, dgamma), sink(ctx.pbeta, dbeta), None, None, None, None, None, None
+        return dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None, None
 
 
 class GNActFn(torch.autograd.Function):
@@ -478,18 +524,20 @@ class GNActFn(torch.autograd.Function):
         part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
         lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale), fptr(shift),
                           1, ACT[act], N, HW, C, STATS_ROWS, fptr(part), stream())
-        dgamma = torch.empty(C, dtype=torch.float32, device=dev)
-        dbeta = torch.empty(C, dtype=torch.float32, device=dev)
+        dgamma, pg, acc_g = grad_dst(gamma, C, dev)
+        dbeta, pb, acc_b = grad_dst(ctx.pbeta, C, dev)
+        if acc_g != acc_b:
+            raise RuntimeError("GN gamma/beta gradients must share one destination kind")
         A = torch.empty(N * C, dtype=torch.float32, device=dev)
         B = torch.empty(N * C, dtype=torch.float32, device=dev)
         Cc = torch.empty(N * C, dtype=torch.float32, device=dev)
         lib.adr_gn_bwd_finalize(fptr(part), N, chunks, C, groups, float(HW * (C // groups)), fptr(mean), fptr(rstd),
-                                fptr(gamma.detach()), fptr(dgamma), fptr(dbeta), fptr(A), fptr(B), fptr(Cc), stream())
+                                fptr(gamma.detach()), pg, pb, fptr(A), fptr(B), fptr(Cc), acc_g, stream())
         dy = empty_act(N, C, H, W, y.dtype, dev)
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
                                fptr(Cc), 1, 1, ACT[act], N, HW, C, 0, stream())
-        return dy, sink(gamma, dgamma), sink(ctx.pbeta, dbeta), None, None, None
+        return dy, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None
 
 
 def image_to_nhwc(img: torch.Tensor, dtype, cpad=8):
@@ -1120,15 +1168,17 @@ class GateMLPFn(torch.autograd.Function):
         d = dout.float().contiguous()
         dev = vv.device
         din = torch.empty_like(vv)
-        dW1 = torch.empty(H1, Cin, dtype=torch.float32, device=dev)
-        db1 = torch.empty(H1, dtype=torch.float32, device=dev)
-        dW2 = torch.empty(H2, H1, dtype=torch.float32, device=dev)
-        db2 = torch.empty(H2, dtype=torch.float32, device=dev)
-        lib.adr_gate_mlp_bwd(fptr(vv), 1.0, N, Cin, fptr(w1), H1, a1, fptr(w2), H2, a2, fptr(hidden), fptr(out),
-                             fptr(d), fptr(din), fptr(dW1), fptr(db1), fptr(dW2), fptr(db2), stream())
         W1p, b1p, W2p, b2p = ctx.params
-        return (din, sink(W1p, dW1.view(s1)), sink(b1p, db1) if hb1 else None, sink(W2p, dW2.view(s2)),
-                sink(b2p, db2) if hb2 else None, None, None)
+        dW1, p1, acc = grad_dst(W1p, H1 * Cin, dev)
+        dW2, p2, acc2 = grad_dst(W2p, H2 * H1, dev)
+        db1, pb1, acc3 = grad_dst(b1p, H1, dev) if hb1 else (None, None, acc)
+        db2, pb2, acc4 = grad_dst(b2p, H2, dev) if hb2 else (None, None, acc)
+        if len({acc, acc2, acc3, acc4}) != 1:
+            raise RuntimeError("gate_mlp: parameter gradients must share one destination kind")
+        lib.adr_gate_mlp_bwd(fptr(vv), 1.0, N, Cin, fptr(w1), H1, a1, fptr(w2), H2, a2, fptr(hidden), fptr(out),
+                             fptr(d), fptr(din), p1, pb1, p2, pb2, acc, stream())
+        return (din, grad_ret(W1p, dW1), grad_ret(b1p, db1) if hb1 else None, grad_ret(W2p, dW2),
+                grad_ret(b2p, db2) if hb2 else None, None, None)
 
 
 def gate_mlp(v, W1, b1, W2, b2, act1, act2):
@@ -1314,14 +1364,14 @@ class DWConvFn(torch.autograd.Function):
         N, C, H, W = x.shape
         vx, vd = _v(x), _v(dy)
         dx = _new_like(x) if ctx.needs_input_grad[0] else None
-        dw = torch.empty(C * k * k, dtype=torch.float32, device=x.device) if ctx.needs_input_grad[1] else None
+        dw, pdw, dacc = grad_dst(ctx.pw, C * k * k, x.device) if ctx.needs_input_grad[1] else (None, None, 0)
         wsb = lib.adr_dwconv_wgrad_workspace(N, H, W, C, k)
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=x.device)
         lib.adr_dwconv_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]), vd[2], fptr(wf),
-                           ctypes.c_void_p(dx.data_ptr()) if dx is not None else None, C, fptr(dw), N, H, W, C, k, 0,
-                           fptr(ws), wsb, stream())
-        db = _bias_grad(vd[0], C, N, H * W, vd[2]) if has_b and ctx.needs_input_grad[2] else None
-        return dx, (sink(ctx.pw, dw.view(wshape)) if dw is not None else None), sink(ctx.pb, db), None
+                           ctypes.c_void_p(dx.data_ptr()) if dx is not None else None, C, pdw, N, H, W, C, k, 0,
+                           dacc, fptr(ws), wsb, stream())
+        db = _bias_grad(vd[0], C, N, H * W, vd[2], ctx.pb) if has_b and ctx.needs_input_grad[2] else None
+        return dx, grad_ret(ctx.pw, dw), db, None
 
 
 def dwconv(x, w, b, k):
@@ -1619,12 +1669,12 @@ class EDFFNFilterFn(torch.autograd.Function):
         dd, dp, dcs = _v(dy)
         basis = edffn_basis(t.device)
         dx = empty_act(N, C, H, W, t.dtype, t.device)
-        dw = torch.empty(C, nuv, dtype=torch.float32, device=t.device)
+        dw, pdw, acc = grad_dst(ctx.pf, C * nuv, t.device)
         wsb = lib.adr_edffn_bwd_workspace(N, H, W, C)
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=t.device)
         lib.adr_edffn_bwd(dcode(t.dtype), ctypes.c_void_p(p), cs, ctypes.c_void_p(dp), dcs, fptr(M), fptr(basis), nuv,
-                          ctypes.c_void_p(dx.data_ptr()), C, fptr(dw), N, H, W, C, fptr(ws), wsb, stream())
-        return dx, sink(ctx.pf, dw.view(fshape))
+                          ctypes.c_void_p(dx.data_ptr()), C, pdw, N, H, W, C, acc, fptr(ws), wsb, stream())
+        return dx, grad_ret(ctx.pf, dw)
 
 
 def edffn_filter(x, fft):

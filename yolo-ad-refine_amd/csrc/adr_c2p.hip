@@ -114,13 +114,13 @@ __global__ void __launch_bounds__(256) dw_bwd_w_kernel(const T* x, int xcs, cons
 }
 
 // dw[c][t] = sum_chunks partial[chunk][t][c]
-__global__ void dw_w_reduce_kernel(const float* partial, int chunks, int C, int kk, float* dw) {
+__global__ void dw_w_reduce_kernel(const float* partial, int chunks, int C, int kk, float* dw, int accumulate) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= C * kk) return;
   int c = i / kk, t = i % kk;
   float s = 0.f;
   for (int ch = 0; ch < chunks; ++ch) s += partial[((long)ch * kk + t) * C + c];
-  dw[i] = s;
+  dw[i] = accumulate ? dw[i] + s : s;
 }
 
 // ---------------- AdaptiveDynamicTanh ----------------
@@ -465,43 +465,50 @@ __global__ void edffn_build_kernel(const float* w, const float* Bm, int C, int n
   M[i] = s;
 }
 
-// block per (n, patch); y[pix] = M_c x_patch for unpadded pixels
+// y_patch = M_c x_patch for every 8x8 patch of channel c (transpose: M_c^T, the backward).
+// Block = one channel x EDFFN_PPB patches; lane = patch position: the lane keeps its row (column for the
+// transpose) of M_c in 64 registers, the wave stages each patch's 64 inputs in LDS and every lane reads them
+// back as broadcasts, so M is read from memory once per block instead of once per output element.
+// Forward: x reflect-padded, y written on the real (cropped) pixels. Transpose: dy read on the real pixels
+// (zero elsewhere), written to the padded fp32 scratch [N][Hp][Wp][C] for the fold.
+constexpr int EDFFN_PPB = 64;
+
 template <typename T>
-__global__ void __launch_bounds__(256) edffn_apply_kernel(const T* x, int xcs, const float* M, T* y, int ycs, int H,
-                                                          int W, int C, int transpose) {
-  extern __shared__ float xs[];  // [64][C]
-  int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8;
-  int n = blockIdx.x / (ph_n * pw_n);
-  int pp = blockIdx.x % (ph_n * pw_n);
-  int py = pp / pw_n, px = pp % pw_n;
-  for (int i = threadIdx.x; i < 64 * C; i += 256) {
-    int pos = i / C, c = i % C;
-    int yy = py * 8 + pos / 8, xx = px * 8 + pos % 8;
+__global__ void __launch_bounds__(256) edffn_apply_kernel(const T* x, int xcs, const float* M, T* y, int ycs, int N,
+                                                          int H, int W, int C, int transpose) {
+  __shared__ float xs[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int c = blockIdx.x % C, chunk = blockIdx.x / C;
+  const int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8, npatch = N * ph_n * pw_n;
+  const float* Mc = M + (long)c * 4096;
+  float mr[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) mr[j] = transpose ? Mc[j * 64 + lane] : Mc[lane * 64 + j];
+  const int dy_ = lane / 8, dx_ = lane % 8;
+  const int pend = min(npatch, (chunk + 1) * EDFFN_PPB);
+  for (int pp = chunk * EDFFN_PPB + wave; pp < pend; pp += 4) {
+    const int n = pp / (ph_n * pw_n), q = pp % (ph_n * pw_n);
+    const int yy = (q / pw_n) * 8 + dy_, xx = (q % pw_n) * 8 + dx_;
     float v = 0.f;
     if (!transpose) {
-      int sy = reflect_idx(yy, H), sx = reflect_idx(xx, W);
-      v = to_f(x[(((long)n * H + sy) * W + sx) * xcs + c]);
-    } else if (yy < H && xx < W) {  // backward: upstream grad only lives on the cropped (real) pixels
+      v = to_f(x[(((long)n * H + reflect_idx(yy, H)) * W + reflect_idx(xx, W)) * xcs + c]);
+    } else if (yy < H && xx < W) {
       v = to_f(x[(((long)n * H + yy) * W + xx) * xcs + c]);
     }
-    xs[pos * C + c] = v;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 64 * C; i += 256) {
-    int pos = i / C, c = i % C;
-    int yy = py * 8 + pos / 8, xx = px * 8 + pos % 8;
-    const float* Mc = M + (long)c * 4096;
+    xs[wave][lane] = v;
+    __builtin_amdgcn_wave_barrier();
     float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 64; j += 4) {
+      const float4 b = *reinterpret_cast<const float4*>(&xs[wave][j]);
+      s += mr[j] * b.x + mr[j + 1] * b.y + mr[j + 2] * b.z + mr[j + 3] * b.w;
+    }
+    __builtin_amdgcn_wave_barrier();
     if (!transpose) {
-      if (yy >= H || xx >= W) continue;
-      for (int j = 0; j < 64; ++j) s += Mc[pos * 64 + j] * xs[j * C + c];
-      y[(((long)n * H + yy) * W + xx) * ycs + c] = from_f<T>(s);
+      if (yy < H && xx < W) y[(((long)n * H + yy) * W + xx) * ycs + c] = from_f<T>(s);
     } else {
-      // dX_pad[pos] = sum_i M[i][pos] dY[i]; written to a padded fp32 scratch (y reinterpreted)
-      for (int j = 0; j < 64; ++j) s += Mc[j * 64 + pos] * xs[j * C + c];
       float* scratch = reinterpret_cast<float*>(y);
-      int Hp = ph_n * 8, Wp = pw_n * 8;
-      scratch[(((long)n * Hp + yy) * Wp + xx) * C + c] = s;
+      scratch[(((long)n * ph_n * 8 + yy) * (pw_n * 8) + xx) * C + c] = s;
     }
   }
 }
@@ -531,34 +538,51 @@ __global__ void __launch_bounds__(256) edffn_fold_kernel(const float* dpad, int 
   dx[pix * ocs + c] = from_f<T>(s);
 }
 
-// dM[c][i][j] = sum over (n, patch) dY_patch[i] * X_patch[j]  (block per (c, i); threads over j)
+// dw[c][uv] = sum_{i,j} B[uv][i][j] dM[c][i][j],  dM[c][i][j] = sum over (n, patch) dY_patch[i] * X_patch[j].
+// Block per channel: lane j accumulates column j of dM over the wave's patches (64 registers, dY broadcast from
+// LDS), the four waves' partials are summed in LDS in a fixed order, and the block contracts dM with the
+// basis in place (no dM round trip through memory).
 template <typename T>
-__global__ void __launch_bounds__(64) edffn_dM_kernel(const T* x, int xcs, const T* dy, int dcs, long N, int H, int W,
-                                                      int C, float* dM) {
-  int c = blockIdx.x / 64, i = blockIdx.x % 64;
-  int j = threadIdx.x;
-  int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8;
-  float s = 0.f;
-  for (long n = 0; n < N; ++n)
-    for (int py = 0; py < ph_n; ++py)
-      for (int px = 0; px < pw_n; ++px) {
-        int yi = py * 8 + i / 8, xi = px * 8 + i % 8;
-        if (yi >= H || xi >= W) continue;  // output pixel cropped away: no gradient
-        float g = to_f(dy[(((long)n * H + yi) * W + xi) * dcs + c]);
-        int yj = reflect_idx(py * 8 + j / 8, H), xj = reflect_idx(px * 8 + j % 8, W);
-        s += g * to_f(x[(((long)n * H + yj) * W + xj) * xcs + c]);
-      }
-  dM[((long)c * 64 + i) * 64 + j] = s;
-}
-
-// dw[c][uv] = sum_e B[uv][e] dM[c][e]
-__global__ void edffn_dw_kernel(const float* dM, const float* Bm, int C, int nuv, float* dw) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= C * nuv) return;
-  int c = i / nuv, u = i % nuv;
-  float s = 0.f;
-  for (int e = 0; e < 4096; ++e) s += Bm[(long)u * 4096 + e] * dM[(long)c * 4096 + e];
-  dw[i] = s;
+__global__ void __launch_bounds__(256) edffn_dw_kernel(const T* x, int xcs, const T* dy, int dcs, int N, int H, int W,
+                                                       int C, const float* Bm, int nuv, float* dw, int accumulate) {
+  __shared__ float sdy[4][64];
+  __shared__ float dM[4][4096];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
+  const int c = blockIdx.x;
+  const int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8, npatch = N * ph_n * pw_n;
+  float acc[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) acc[i] = 0.f;
+  const int dy_ = lane / 8, dx_ = lane % 8;
+  for (int pp = wave; pp < npatch; pp += 4) {
+    const int n = pp / (ph_n * pw_n), q = pp % (ph_n * pw_n);
+    const int yy = (q / pw_n) * 8 + dy_, xx = (q % pw_n) * 8 + dx_;
+    const float xv = to_f(x[(((long)n * H + reflect_idx(yy, H)) * W + reflect_idx(xx, W)) * xcs + c]);
+    sdy[wave][lane] = (yy < H && xx < W) ? to_f(dy[(((long)n * H + yy) * W + xx) * dcs + c]) : 0.f;
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < 64; i += 4) {
+      const float4 g = *reinterpret_cast<const float4*>(&sdy[wave][i]);
+      acc[i] += g.x * xv;
+      acc[i + 1] += g.y * xv;
+      acc[i + 2] += g.z * xv;
+      acc[i + 3] += g.w * xv;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+#pragma unroll
+  for (int i = 0; i < 64; ++i) dM[wave][i * 64 + lane] = acc[i];
+  __syncthreads();
+  for (int e = tid; e < 4096; e += 256) dM[0][e] = (dM[0][e] + dM[1][e]) + (dM[2][e] + dM[3][e]);
+  __syncthreads();
+  // dw[uv] = sum_e B[uv][e] dM[e]: wave per uv (strided), lanes over e, fixed-order wave reduction
+  for (int u = wave; u < nuv; u += 4) {
+    const float* b = Bm + (long)u * 4096;
+    float s = 0.f;
+    for (int e = lane; e < 4096; e += 64) s += b[e] * dM[0][e];
+    s = wave_sum(s);
+    if (lane == 0) dw[c * nuv + u] = accumulate ? dw[c * nuv + u] + s : s;
+  }
 }
 
 }  // namespace adr
@@ -595,8 +619,8 @@ extern "C" size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k) 
 }
 
 extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* w, void* dx,
-                              int ocs, float* dw, int N, int H, int W, int C, int k, int accumulate, float* ws,
-                              size_t ws_bytes, void* stream) {
+                              int ocs, float* dw, int N, int H, int W, int C, int k, int accumulate,
+                              int dw_accumulate, float* ws, size_t ws_bytes, void* stream) {
   int v = dtype == ADR_BF16 ? 8 : 4;
   ADR_REQUIRE(C % v == 0 && C / v <= 256, "dwconv_bwd: C=%d", C);
   hipStream_t st = (hipStream_t)stream;
@@ -622,7 +646,8 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
     else
       hipLaunchKernelGGL(dw_bwd_w_kernel<float>, g, dim3(256), 0, st, (const float*)x, xcs, (const float*)dy, dcs, N, H,
                          W, C, k, 1024, ws);
-    hipLaunchKernelGGL(dw_w_reduce_kernel, dim3(cdiv(C * k * k, 256)), dim3(256), 0, st, ws, chunks, C, k * k, dw);
+    hipLaunchKernelGGL(dw_w_reduce_kernel, dim3(cdiv(C * k * k, 256)), dim3(256), 0, st, ws, chunks, C, k * k, dw,
+                       dw_accumulate);
   }
   return check_launch("adr_dwconv_bwd");
 }
@@ -721,38 +746,38 @@ extern "C" int adr_edffn_build(const float* w, const float* basis, int C, int nu
 extern "C" int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, void* y, int ycs, int N, int H, int W,
                              int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  int np = ((H + 7) / 8) * ((W + 7) / 8);
-  size_t sm = 64 * C * sizeof(float);
-  ADR_REQUIRE(sm <= 64 * 1024, "edffn: C=%d too large", C);
+  ADR_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && H >= 4 && W >= 4, "edffn: N=%d H=%d W=%d C=%d", N, H, W, C);
+  const long np = (long)N * ((H + 7) / 8) * ((W + 7) / 8);
+  dim3 grid((unsigned)(cdiv(np, EDFFN_PPB) * C));
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(edffn_apply_kernel<__bf16>, dim3(N * np), dim3(256), sm, st, (const __bf16*)x, xcs, M,
-                       (__bf16*)y, ycs, H, W, C, 0);
+    hipLaunchKernelGGL(edffn_apply_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)x, xcs, M, (__bf16*)y, ycs,
+                       N, H, W, C, 0);
   else
-    hipLaunchKernelGGL(edffn_apply_kernel<float>, dim3(N * np), dim3(256), sm, st, (const float*)x, xcs, M, (float*)y,
-                       ycs, H, W, C, 0);
+    hipLaunchKernelGGL(edffn_apply_kernel<float>, grid, dim3(256), 0, st, (const float*)x, xcs, M, (float*)y, ycs, N,
+                       H, W, C, 0);
   return check_launch("adr_edffn_fwd");
 }
 
 extern "C" size_t adr_edffn_bwd_workspace(int N, int H, int W, int C) {
   size_t hp = (H + 7) / 8 * 8, wp = (W + 7) / 8 * 8;
-  return ((size_t)N * hp * wp * C + (size_t)C * 4096) * sizeof(float);
+  return (size_t)N * hp * wp * C * sizeof(float);
 }
 
 extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* M,
                              const float* basis, int nuv, void* dx, int ocs, float* dw, int N, int H, int W, int C,
-                             float* ws, size_t ws_bytes, void* stream) {
+                             int dw_accumulate, float* ws, size_t ws_bytes, void* stream) {
   ADR_REQUIRE(ws_bytes >= adr_edffn_bwd_workspace(N, H, W, C), "edffn_bwd: workspace");
+  ADR_REQUIRE(N > 0 && H >= 4 && W >= 4 && C > 0, "edffn_bwd: N=%d H=%d W=%d C=%d", N, H, W, C);
   hipStream_t st = (hipStream_t)stream;
-  int np = ((H + 7) / 8) * ((W + 7) / 8);
-  size_t sm = 64 * C * sizeof(float);
+  const long np = (long)N * ((H + 7) / 8) * ((W + 7) / 8);
+  dim3 grid((unsigned)(cdiv(np, EDFFN_PPB) * C));
   float* dpad = ws;
-  float* dM = ws + (size_t)N * ((H + 7) / 8 * 8) * ((W + 7) / 8 * 8) * C;
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(edffn_apply_kernel<__bf16>, dim3(N * np), dim3(256), sm, st, (const __bf16*)dy, dcs, M,
-                       (__bf16*)dpad, 0, H, W, C, 1);
+    hipLaunchKernelGGL(edffn_apply_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)dy, dcs, M, (__bf16*)dpad, 0,
+                       N, H, W, C, 1);
   else
-    hipLaunchKernelGGL(edffn_apply_kernel<float>, dim3(N * np), dim3(256), sm, st, (const float*)dy, dcs, M,
-                       (float*)dpad, 0, H, W, C, 1);
+    hipLaunchKernelGGL(edffn_apply_kernel<float>, grid, dim3(256), 0, st, (const float*)dy, dcs, M, (float*)dpad, 0,
+                       N, H, W, C, 1);
   long total = (long)N * H * W * C;
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(edffn_fold_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, dpad, H, W, C, (long)N,
@@ -762,12 +787,11 @@ extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, 
                        (float*)dx, ocs);
   if (dw) {
     if (dtype == ADR_BF16)
-      hipLaunchKernelGGL(edffn_dM_kernel<__bf16>, dim3(C * 64), dim3(64), 0, st, (const __bf16*)x, xcs,
-                         (const __bf16*)dy, dcs, (long)N, H, W, C, dM);
+      hipLaunchKernelGGL(edffn_dw_kernel<__bf16>, dim3(C), dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dy,
+                         dcs, N, H, W, C, basis, nuv, dw, dw_accumulate);
     else
-      hipLaunchKernelGGL(edffn_dM_kernel<float>, dim3(C * 64), dim3(64), 0, st, (const float*)x, xcs, (const float*)dy,
-                         dcs, (long)N, H, W, C, dM);
-    hipLaunchKernelGGL(edffn_dw_kernel, dim3(cdiv(C * nuv, 256)), dim3(256), 0, st, dM, basis, C, nuv, dw);
+      hipLaunchKernelGGL(edffn_dw_kernel<float>, dim3(C), dim3(256), 0, st, (const float*)x, xcs, (const float*)dy, dcs,
+                         N, H, W, C, basis, nuv, dw, dw_accumulate);
   }
   return check_launch("adr_edffn_bwd");
 }

@@ -77,62 +77,123 @@ __global__ void __launch_bounds__(256) dcn_im2col_kernel(const T* x, int xcs, co
   st16(cols + (pix * 9 + t) * C + g * V, ov);
 }
 
-// one wave per output pixel, lanes over channels: every (tap, corner) touches 64 contiguous channels, so the
-// x reads, the dcols reads and the fp32 scatter atomics into dx32 (NHWC dense N*H*W*C) are all coalesced;
-// d_offset / d_mask_logit are wave reductions over channels.
+// col2im, one kernel, lanes over channels (64-channel contiguous loads and adds).
+// A wave walks a vertical strip of sampling pixels (column w, rows h0..h0+DCN_SL-1). The bilinear-corner
+// contributions of its current pixel land, for offsets within +-2 pixels, inside a 7x7 cell neighbourhood,
+// which the wave keeps as a PRIVATE rolling window in LDS (7 rows x 7 columns x 64 channels fp32, ring-indexed
+// by row): adds are plain ds_read/ds_write read-modify-writes in program order, no LDS atomics (which run ~30x
+// slower than plain LDS traffic on this part). When the strip advances a row, the row leaving the window is
+// flushed to dx32 with one global float atomic per (cell, channel). Per sampling pixel that is ~7 global
+// atomics per channel instead of 36 (9 taps x 4 corners) for a per-corner global scatter. Corners beyond the
+// window go straight to dx32. The same pass computes d_offset / d_mask_logit from the corner values (DPP wave
+// sums). All loads of a tap group are unconditional at clamped addresses (masked afterwards), so they are in
+// flight together instead of each waiting behind a branch.
+constexpr int DCN_SL = 40;             // strip length (rows per wave)
+constexpr int DCN_WIN = 7;             // window rows / columns (pixel +-3)
+constexpr int DCN_CC = 64;             // channels per pass (= lanes)
+constexpr int DCN_WPB = 4;             // waves per block
+
 template <typename T>
 __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, const T* om, int omcs, const T* dcols,
                                                          float* dx32, T* dom, int domcs, int N, int H, int W, int C) {
-  const long pix = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  if (pix >= (long)N * H * W) return;
-  const int w = (int)(pix % W);
-  const long r2 = pix / W;
-  const int h = (int)(r2 % H);
-  const int n = (int)(r2 / H);
-  const T* o = om + pix * omcs;
+  __shared__ float winbuf[DCN_WPB][DCN_WIN * DCN_WIN * DCN_CC];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float* win = winbuf[wave];
+  const int nstrip = (H + DCN_SL - 1) / DCN_SL;
+  const long sid = (long)blockIdx.x * DCN_WPB + wave;  // (n, strip, w) with w fastest
+  if (sid >= (long)N * nstrip * W) return;
+  const int w = (int)(sid % W);
+  const long r = sid / W;
+  const int strip = (int)(r % nstrip), n = (int)(r / nstrip);
+  const int hb = strip * DCN_SL, he = min(H, hb + DCN_SL);
   const T* xb = x + (long)n * H * W * xcs;
   float* dxb = dx32 + (long)n * H * W * C;
-  T* d = dom + pix * domcs;
-  for (int t = 0; t < 9; ++t) {
-    const float oy = to_f(o[2 * t]), ox = to_f(o[2 * t + 1]);
-    const float m = 1.f / (1.f + __expf(-to_f(o[18 + t])));
-    const float py = (float)(h - 1 + t / 3) + oy, px = (float)(w - 1 + t % 3) + ox;
-    int y0, x0;
-    float wt[4];
-    bool ok[4];
-    const bool inside = dcn_sample(py, px, H, W, y0, x0, wt, ok);
-    const float ly = py - floorf(py), lx = px - floorf(px);
-    // d weight / d py and d px for each corner (mmcv dmcn_get_coordinate_weight)
-    const float dwy[4] = {-(1.f - lx), -lx, (1.f - lx), lx};
-    const float dwx[4] = {-(1.f - ly), (1.f - ly), -ly, ly};
-    const T* dc = dcols + (pix * 9 + t) * C;
-    float dmask = 0.f, dpy = 0.f, dpx = 0.f;
-    for (int c = lane; c < C; c += 64) {
-      const float g = to_f(dc[c]);
-      float val = 0.f, sy = 0.f, sx = 0.f;
+  const int wx0 = w - DCN_WIN / 2;  // window column 0
+  auto flush_row = [&](int y, int c) {  // add window row y to dx32 and clear it
+    float* row = win + (y % DCN_WIN + DCN_WIN) % DCN_WIN * DCN_WIN * DCN_CC;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        if (!ok[q]) continue;
-        const long off = (long)(y0 + (q >> 1)) * W + x0 + (q & 1);
-        const float v = to_f(xb[off * xcs + c]);
-        val += wt[q] * v;
-        sy += dwy[q] * v;
-        sx += dwx[q] * v;
-        unsafeAtomicAdd(dxb + off * C + c, g * m * wt[q]);
+    for (int j = 0; j < DCN_WIN; ++j) {
+      const float v = row[j * DCN_CC + lane];
+      const int xx = wx0 + j;
+      if (y >= 0 && y < H && xx >= 0 && xx < W && c < C && v != 0.f) unsafeAtomicAdd(dxb + ((long)y * W + xx) * C + c, v);
+      row[j * DCN_CC + lane] = 0.f;
+    }
+  };
+  for (int c0 = 0; c0 < C; c0 += DCN_CC) {
+    const int c = c0 + lane;
+    const int cc = min(c, C - 1);
+    for (int i = 0; i < DCN_WIN * DCN_WIN; ++i) win[i * DCN_CC + lane] = 0.f;
+    for (int h = hb; h < he; ++h) {
+      if (h > hb) flush_row(h - 1 - DCN_WIN / 2, c);  // row h-4 leaves the window (its slot becomes row h+3)
+      const long pix = ((long)n * H + h) * W + w;
+      const float omv = lane < 27 ? to_f(om[pix * omcs + lane]) : 0.f;
+      T* d = dom + pix * domcs;
+#pragma unroll 1
+      for (int tg = 0; tg < 3; ++tg) {
+        int y0[3], x0[3];
+        float wt[3][4], ly[3], lx[3], m[3], g[3], xv[3][4];
+        bool ok[3][4];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int t = tg * 3 + u;
+          const float oy = lane_f(omv, 2 * t), ox = lane_f(omv, 2 * t + 1);
+          m[u] = 1.f / (1.f + __expf(-lane_f(omv, 18 + t)));
+          const float py = (float)(h - 1 + tg) + oy, px = (float)(w - 1 + u) + ox;
+          dcn_sample(py, px, H, W, y0[u], x0[u], wt[u], ok[u]);
+          ly[u] = py - floorf(py);
+          lx[u] = px - floorf(px);
+        }
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          g[u] = to_f(dcols[(pix * 9 + tg * 3 + u) * C + cc]);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int yy = min(max(y0[u] + (q >> 1), 0), H - 1), xx = min(max(x0[u] + (q & 1), 0), W - 1);
+            const float v = to_f(xb[((long)yy * W + xx) * xcs + cc]);
+            xv[u][q] = ok[u][q] ? v : 0.f;
+          }
+        }
+        if (c >= C) g[0] = g[1] = g[2] = 0.f;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int t = tg * 3 + u;
+          // d weight / d py and d px for each corner (mmcv dmcn_get_coordinate_weight)
+          const float dwy[4] = {-(1.f - lx[u]), -lx[u], (1.f - lx[u]), lx[u]};
+          const float dwx[4] = {-(1.f - ly[u]), (1.f - ly[u]), -ly[u], ly[u]};
+          float val = 0.f, sy = 0.f, sx = 0.f;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            val += wt[u][q] * xv[u][q];
+            sy += dwy[q] * xv[u][q];
+            sx += dwx[q] * xv[u][q];
+          }
+          const float gm = g[u] * m[u];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (!ok[u][q]) continue;  // wave-uniform (depends on the pixel and tap only)
+            const int yy = y0[u] + (q >> 1), xx = x0[u] + (q & 1);
+            const int dyw = yy - h, dxw = xx - wx0;
+            if (dyw >= -(DCN_WIN / 2) && dyw <= DCN_WIN / 2 && dxw >= 0 && dxw < DCN_WIN) {
+              float* cell = win + ((yy % DCN_WIN) * DCN_WIN + dxw) * DCN_CC + lane;
+              *cell += gm * wt[u][q];
+            } else if (c < C) {
+              unsafeAtomicAdd(dxb + ((long)yy * W + xx) * C + c, gm * wt[u][q]);
+            }
+          }
+          const float spy = wave_sum_dpp(gm * sy), spx = wave_sum_dpp(gm * sx), smk = wave_sum_dpp(g[u] * val);
+          if (lane == 0) {
+            const bool first = c0 == 0, last = c0 + DCN_CC >= C;
+            const float a = first ? 0.f : to_f(d[2 * t]), b = first ? 0.f : to_f(d[2 * t + 1]);
+            d[2 * t] = from_f<T>(a + spy);
+            d[2 * t + 1] = from_f<T>(b + spx);
+            // d mask logit: raw channel sum across chunks, times sigmoid'(logit) on the last chunk
+            const float e = (first ? 0.f : to_f(d[18 + t])) + smk;
+            d[18 + t] = from_f<T>(last ? e * m[u] * (1.f - m[u]) : e);
+          }
+        }
       }
-      dmask += g * val;
-      dpy += g * m * sy;
-      dpx += g * m * sx;
     }
-    dmask = wave_sum(dmask);
-    dpy = wave_sum(dpy);
-    dpx = wave_sum(dpx);
-    if (lane == 0) {
-      d[2 * t] = from_f<T>(inside ? dpy : 0.f);
-      d[2 * t + 1] = from_f<T>(inside ? dpx : 0.f);
-      d[18 + t] = from_f<T>(dmask * m * (1.f - m));
-    }
+    for (int y = he - 1 - DCN_WIN / 2; y <= he - 1 + DCN_WIN / 2; ++y) flush_row(y, c);
   }
 }
 
@@ -193,61 +254,67 @@ __global__ void __launch_bounds__(256) gate_mlp_kernel(const float* in, float in
   }
 }
 
-// backward: given dout (N,H2) -> din (N,Cin) (times in_scale), per-image partial dW1/db1/dW2/db2 summed in-kernel
-// over images by a single block (N small, deterministic order).
+// backward: given dout (N,H2) -> din (N,Cin) (times in_scale) and dW1/db1/dW2/db2 summed over images.
+// One block, every phase thread-parallel over its outputs; the image sums run in a fixed order (deterministic).
+// accumulate: weight/bias gradients are added to the destination (the trainer's gradient arena).
 __global__ void __launch_bounds__(256) gate_mlp_bwd_kernel(const float* in, float in_scale, int Cin, const float* W1,
                                                            int H1, int act1, const float* W2, int H2, int act2,
                                                            const float* hidden, const float* out, const float* dout,
                                                            int N, float* din, float* dW1, float* db1, float* dW2,
-                                                           float* db2) {
+                                                           float* db2, int accumulate) {
   extern __shared__ float sm[];
-  float* dz2 = sm;        // H2
-  float* dh = sm + H2;    // H1
-  // zero weight grads
-  for (int i = threadIdx.x; i < H1 * Cin; i += 256) dW1[i] = 0.f;
-  for (int i = threadIdx.x; i < H1; i += 256) db1[i] = 0.f;
-  for (int i = threadIdx.x; i < H2 * H1; i += 256) dW2[i] = 0.f;
-  for (int i = threadIdx.x; i < H2; i += 256) db2[i] = 0.f;
-  __syncthreads();
-  for (int n = 0; n < N; ++n) {
+  float* dz2 = sm;           // [N][H2]
+  float* dh = sm + N * H2;   // [N][H1]
+  const int tid = threadIdx.x;
+  for (int n = tid; n < N; n += 256) {
     const float* o = out + (long)n * H2;
     const float* d = dout + (long)n * H2;
-    if (threadIdx.x == 0) {
-      if (act2 == 6) {
-        float dot = 0.f;
-        for (int j = 0; j < H2; ++j) dot += d[j] * o[j];
-        for (int j = 0; j < H2; ++j) dz2[j] = o[j] * (d[j] - dot);
-      } else if (act2 == 4) {
-        for (int j = 0; j < H2; ++j) dz2[j] = d[j] * o[j] * (1.f - o[j]);
-      } else {
-        for (int j = 0; j < H2; ++j) dz2[j] = d[j];
-      }
-    }
-    __syncthreads();
-    const float* hid = hidden + (long)n * H1;
-    for (int c = threadIdx.x; c < H1; c += 256) {
-      float s = 0.f;
-      for (int j = 0; j < H2; ++j) {
-        s += W2[(long)j * H1 + c] * dz2[j];
-        dW2[(long)j * H1 + c] += dz2[j] * hid[c];
-      }
-      float hv = hid[c];
-      dh[c] = (act1 == 3) ? (hv > 0.f ? s : 0.f) : (act1 == 4 ? s * hv * (1.f - hv) : s);
-    }
-    for (int j = threadIdx.x; j < H2; j += 256) db2[j] += dz2[j];
-    __syncthreads();
-    const float* xin = in + (long)n * Cin;
-    for (int c = threadIdx.x; c < Cin; c += 256) {
-      float s = 0.f;
-      for (int j = 0; j < H1; ++j) {
-        s += W1[(long)j * Cin + c] * dh[j];
-        dW1[(long)j * Cin + c] += dh[j] * xin[c] * in_scale;
-      }
-      din[(long)n * Cin + c] = s * in_scale;
-    }
-    for (int j = threadIdx.x; j < H1; j += 256) db1[j] += dh[j];
-    __syncthreads();
+    float dot = 0.f;
+    if (act2 == 6)
+      for (int j = 0; j < H2; ++j) dot += d[j] * o[j];
+    for (int j = 0; j < H2; ++j)
+      dz2[n * H2 + j] = act2 == 6 ? o[j] * (d[j] - dot) : (act2 == 4 ? d[j] * o[j] * (1.f - o[j]) : d[j]);
   }
+  __syncthreads();
+  for (int i = tid; i < N * H1; i += 256) {
+    const int n = i / H1, c = i % H1;
+    float s = 0.f;
+    for (int j = 0; j < H2; ++j) s += W2[(long)j * H1 + c] * dz2[n * H2 + j];
+    const float hv = hidden[i];
+    dh[i] = (act1 == 3) ? (hv > 0.f ? s : 0.f) : (act1 == 4 ? s * hv * (1.f - hv) : s);
+  }
+  __syncthreads();
+  for (int i = tid; i < N * Cin; i += 256) {
+    const int n = i / Cin, c = i % Cin;
+    float s = 0.f;
+    for (int j = 0; j < H1; ++j) s += W1[(long)j * Cin + c] * dh[n * H1 + j];
+    din[i] = s * in_scale;
+  }
+  for (int i = tid; i < H1 * Cin; i += 256) {
+    const int j = i / Cin, c = i % Cin;
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += dh[n * H1 + j] * in[(long)n * Cin + c];
+    s *= in_scale;
+    dW1[i] = accumulate ? dW1[i] + s : s;
+  }
+  for (int i = tid; i < H2 * H1; i += 256) {
+    const int j = i / H1, c = i % H1;
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += dz2[n * H2 + j] * hidden[(long)n * H1 + c];
+    dW2[i] = accumulate ? dW2[i] + s : s;
+  }
+  if (db1)
+    for (int j = tid; j < H1; j += 256) {
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s += dh[n * H1 + j];
+      db1[j] = accumulate ? db1[j] + s : s;
+    }
+  if (db2)
+    for (int j = tid; j < H2; j += 256) {
+      float s = 0.f;
+      for (int n = 0; n < N; ++n) s += dz2[n * H2 + j];
+      db2[j] = accumulate ? db2[j] + s : s;
+    }
 }
 
 // o[n, pix, c] (+)= g[n*gns + c*gcs] * s
@@ -356,14 +423,18 @@ extern "C" int adr_dcn_im2col(int dtype, const void* x, int xcs, const void* om,
 
 extern "C" int adr_dcn_col2im(int dtype, const void* x, int xcs, const void* om, int omcs, const void* dcols,
                               float* dx32, void* dom, int domcs, int N, int H, int W, int C, void* stream) {
-  long npix = (long)N * H * W;
+  ADR_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && omcs >= 27 && domcs >= 27, "dcn_col2im: bad geometry");
+  const long waves = (long)N * cdiv(H, DCN_SL) * W;
+  ADR_REQUIRE(waves / DCN_WPB < (1l << 31), "dcn_col2im: grid too large");
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(dcn_col2im_kernel<__bf16>, dim3(cdiv(npix, 4)), dim3(256), 0, st, (const __bf16*)x, xcs,
-                       (const __bf16*)om, omcs, (const __bf16*)dcols, dx32, (__bf16*)dom, domcs, N, H, W, C);
+    hipLaunchKernelGGL(dcn_col2im_kernel<__bf16>, dim3(cdiv(waves, DCN_WPB)), dim3(64 * DCN_WPB), 0, st,
+                       (const __bf16*)x, xcs, (const __bf16*)om, omcs, (const __bf16*)dcols, dx32, (__bf16*)dom, domcs,
+                       N, H, W, C);
   else
-    hipLaunchKernelGGL(dcn_col2im_kernel<float>, dim3(cdiv(npix, 4)), dim3(256), 0, st, (const float*)x, xcs,
-                       (const float*)om, omcs, (const float*)dcols, dx32, (float*)dom, domcs, N, H, W, C);
+    hipLaunchKernelGGL(dcn_col2im_kernel<float>, dim3(cdiv(waves, DCN_WPB)), dim3(64 * DCN_WPB), 0, st,
+                       (const float*)x, xcs, (const float*)om, omcs, (const float*)dcols, dx32, (float*)dom, domcs, N,
+                       H, W, C);
   return check_launch("adr_dcn_col2im");
 }
 
@@ -389,10 +460,11 @@ extern "C" int adr_gate_mlp(const float* in, float in_scale, int N, int Cin, con
 extern "C" int adr_gate_mlp_bwd(const float* in, float in_scale, int N, int Cin, const float* W1, int H1, int act1,
                                 const float* W2, int H2, int act2, const float* hidden, const float* out,
                                 const float* dout, float* din, float* dW1, float* db1, float* dW2, float* db2,
-                                void* stream) {
-  size_t sm = (H1 + H2) * sizeof(float);
+                                int accumulate, void* stream) {
+  size_t sm = (size_t)N * (H1 + H2) * sizeof(float);
+  ADR_REQUIRE(sm <= 64 * 1024, "gate_mlp_bwd: N=%d H1=%d H2=%d exceed the LDS budget", N, H1, H2);
   hipLaunchKernelGGL(gate_mlp_bwd_kernel, dim3(1), dim3(256), sm, (hipStream_t)stream, in, in_scale, Cin, W1, H1, act1,
-                     W2, H2, act2, hidden, out, dout, N, din, dW1, db1, dW2, db2);
+                     W2, H2, act2, hidden, out, dout, N, din, dW1, db1, dW2, db2, accumulate);
   return check_launch("adr_gate_mlp_bwd");
 }
 

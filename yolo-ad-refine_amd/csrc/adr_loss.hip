@@ -392,12 +392,35 @@ __global__ void __launch_bounds__(256) loss_fg_kernel(Levels L, int B, int nmax,
     for (int q = 0; q < 6; ++q) part[(long)blockIdx.x * 6 + q] = sh[q][0];
 }
 
+// fixed-order block reduction of Q per-block partial columns (double), thread t sums rows t, t+256, ...
+template <int Q>
+__device__ __forceinline__ void reduce_partials(const float* part, int nblk, double* out) {
+  __shared__ double sh[Q][256];
+  double s[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) s[q] = 0.0;
+  for (int k = threadIdx.x; k < nblk; k += 256)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) s[q] += part[(long)k * Q + q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) sh[q][threadIdx.x] = s[q];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) sh[q][threadIdx.x] += sh[q][threadIdx.x + o];
+    __syncthreads();
+  }
+#pragma unroll
+  for (int q = 0; q < Q; ++q) out[q] = sh[q][0];
+}
+
+// out[0..2] = (box, cls, dfl) after gains; out[3] = (sum) * B ; out[4] = n_fg
 // scal[0] = tss = max(sum tscore, 1); scal[1] = mu; scal[2..4] = box_iou, box_nwd, dfl sums (pre-gain)
-__global__ void loss_scalars_kernel(const float* part, int nblk, float* scal) {
+__global__ void __launch_bounds__(256) loss_scalars_kernel(const float* part, int nblk, float* scal) {
+  double s[6];
+  reduce_partials<6>(part, nblk, s);
   if (threadIdx.x != 0) return;
-  double s[6] = {0, 0, 0, 0, 0, 0};
-  for (int k = 0; k < nblk; ++k)
-    for (int q = 0; q < 6; ++q) s[q] += part[(long)k * 6 + q];
   float tss = fmaxf((float)s[0], 1.f);
   float mu = s[5] > 0 ? (float)(s[4] / s[5]) : -1.f;
   if (mu < 0.2f) mu = 0.2f;
@@ -409,7 +432,42 @@ __global__ void loss_scalars_kernel(const float* part, int nblk, float* scal) {
   scal[5] = (float)s[5];
 }
 
-// ---- cls pass + gradient rows: per (b, a); block partial of sum bce*mod ----
+// 8 consecutive row elements <-> fp32 (one 16-byte access for bf16, two for fp32)
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    u32x4 r = ld16(p);
+    const T* e = reinterpret_cast<const T*>(&r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = to_f(e[k]);
+  } else {
+    u32x4 r0 = ld16(p), r1 = ld16(p + 4);
+    const float* a = reinterpret_cast<const float*>(&r0);
+    const float* b = reinterpret_cast<const float*>(&r1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[k] = a[k]; v[4 + k] = b[k]; }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    u32x4 r;
+    T* e = reinterpret_cast<T*>(&r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = from_f<T>(v[k]);
+    st16(p, r);
+  } else {
+    st16(p, *reinterpret_cast<const u32x4*>(v));
+    st16(p + 4, *reinterpret_cast<const u32x4*>(v + 4));
+  }
+}
+
+// ---- cls pass + gradient rows. 16 lanes per anchor row: lanes 0..11 each own 8 class channels (BCE x SlideLoss
+//      weight and its gradient), lanes 12..15 own one ltrb side each (16 DFL bins: DFL + CIoU/NWD gradient through
+//      the softmax expectation), so every access is a 16-byte vector of one row. A block walks 256 anchors;
+//      block partial of sum bce*mod in a fixed-order tree. ----
+constexpr int CLS_ANCHORS_PER_BLOCK = 256;
+
 template <typename T>
 __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, int B, int nmax, int nc, float gscale,
                                                             const float* gt, const float* pbox, const int* tgi,
@@ -417,79 +475,94 @@ __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, 
                                                             float* part, float box_gain, float cls_gain,
                                                             float dfl_gain) {
   __shared__ float sh[256];
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int slot = threadIdx.x & 15, sub = threadIdx.x >> 4;
+  const float tss = scal[0], mu = scal[1];
+  const float e21 = expf(1.f - mu);
+  const float cscale = gscale * cls_gain / tss;
+  const long nanch = (long)B * L.A;
   float acc = 0.f;
-  if (i < (long)B * L.A) {
-    int a = (int)(i % L.A), b = (int)(i / L.A);
-    float tss = scal[0], mu = scal[1];
+  for (int it = 0; it < CLS_ANCHORS_PER_BLOCK / 16; ++it) {
+    const long i = (long)blockIdx.x * CLS_ANCHORS_PER_BLOCK + it * 16 + sub;
+    if (i >= nanch) break;
+    const int a = (int)(i % L.A), b = (int)(i / L.A);
     int lvl;
     float ax, ay;
     const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
     T* gp = const_cast<T*>(feat_row<T>(G, b, a, lvl, ax, ay));
-    bool isfg = fg[i] != 0;
-    int lab = -1;
-    float nrm = tnorm[i];
+    const bool isfg = fg[i] != 0;
+    const float nrm = tnorm[i];
     long r = 0;
+    int lab = -1;
     if (isfg) {
       r = (long)b * nmax + tgi[i];
       lab = (int)gt[r * 5];
     }
-    float e21 = expf(1.f - mu);
-    float cscale = gscale * cls_gain / tss;
-    for (int c = 0; c < nc; ++c) {
-      float x = to_f(p[4 * RM + c]);
-      float t = (c == lab) ? nrm : 0.f;
-      float bce = fmaxf(x, 0.f) - x * t + log1pf(expf(-fabsf(x)));
-      float mod = (t <= mu - 0.1f) ? 1.f : ((t < mu) ? e21 : expf(-(t - 1.f)));
-      acc += bce * mod;
-      float sg = 1.f / (1.f + expf(-x));
-      gp[4 * RM + c] = from_f<T>((sg - t) * mod * cscale);
-    }
-    // box + dfl gradient rows
-    float gbox[4] = {0.f, 0.f, 0.f, 0.f};
-    float gl[4][RM];
-    for (int k = 0; k < 4; ++k)
-      for (int q = 0; q < RM; ++q) gl[k][q] = 0.f;
-    if (isfg) {
-      float st = L.st[lvl];
-      const float* g = gt + r * 5;
-      float tb[4] = {g[1] / st, g[2] / st, g[3] / st, g[4] / st};
-      const float* pb = pbox + i * 4;
-      float pbv[4] = {pb[0], pb[1], pb[2], pb[3]};
-      float gc[4], gn[4];
-      ciou_grad(pbv, tb, gc);
-      nwd(pbv, tb, gn);
-      float wb = gscale * box_gain * 0.5f * nrm / tss;
-      for (int k = 0; k < 4; ++k) gbox[k] = -wb * (gc[k] + gn[k]);
-      // d/d dist: x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3
-      float gd[4] = {-gbox[0], -gbox[1], gbox[2], gbox[3]};
-      float t[4] = {ax - tb[0], ay - tb[1], tb[2] - ax, tb[3] - ay};
-      float wd = gscale * dfl_gain * 0.25f * nrm / tss;
-      for (int k = 0; k < 4; ++k) {
+    if (slot < 12) {
+      const int c0 = slot * 8;
+      if (c0 < nc) {
+        float x[8], g[8];
+        load8<T>(p + 4 * RM + c0, x);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float t = (c0 + k == lab) ? nrm : 0.f;
+          const float bce = fmaxf(x[k], 0.f) - x[k] * t + log1pf(expf(-fabsf(x[k])));
+          const float mod = (t <= mu - 0.1f) ? 1.f : ((t < mu) ? e21 : expf(-(t - 1.f)));
+          acc += bce * mod;
+          const float sg = 1.f / (1.f + expf(-x[k]));
+          g[k] = (sg - t) * mod * cscale;
+        }
+        store8<T>(gp + 4 * RM + c0, g);
+      }
+    } else {
+      const int k = slot - 12;
+      float gl[RM];
+#pragma unroll
+      for (int q = 0; q < RM; ++q) gl[q] = 0.f;
+      if (isfg) {
+        const float st = L.st[lvl];
+        const float* gg = gt + r * 5;
+        const float tb[4] = {gg[1] / st, gg[2] / st, gg[3] / st, gg[4] / st};
+        const float* pb = pbox + i * 4;
+        float pbv[4] = {pb[0], pb[1], pb[2], pb[3]};
+        float gc[4], gn[4];
+        ciou_grad(pbv, tb, gc);
+        nwd(pbv, tb, gn);
+        const float wb = gscale * box_gain * 0.5f * nrm / tss;
+        // d/d dist: x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3
+        const float gbk = -wb * (gc[k] + gn[k]);
+        const float gdk = (k < 2) ? -gbk : gbk;
+        const float tt = (k == 0) ? ax - tb[0] : (k == 1) ? ay - tb[1] : (k == 2) ? tb[2] - ax : tb[3] - ay;
+        const float wd = gscale * dfl_gain * 0.25f * nrm / tss;
+        float lg[RM];
+        load8<T>(p + k * RM, lg);
+        load8<T>(p + k * RM + 8, lg + 8);
         float mx = -INFINITY;
-        for (int q = 0; q < RM; ++q) mx = fmaxf(mx, to_f(p[k * RM + q]));
-        float z = 0.f, e = 0.f;
-        float s[RM];
+#pragma unroll
+        for (int q = 0; q < RM; ++q) mx = fmaxf(mx, lg[q]);
+        float z = 0.f, e = 0.f, sv[RM];
+#pragma unroll
         for (int q = 0; q < RM; ++q) {
-          s[q] = expf(to_f(p[k * RM + q]) - mx);
-          z += s[q];
+          sv[q] = expf(lg[q] - mx);
+          z += sv[q];
         }
+#pragma unroll
         for (int q = 0; q < RM; ++q) {
-          s[q] /= z;
-          e += s[q] * (float)q;
+          sv[q] /= z;
+          e += sv[q] * (float)q;
         }
-        float tk = fminf(fmaxf(t[k], 0.f), (float)(RM - 1) - 0.01f);
-        int tl = (int)tk;
-        float wl = (float)(tl + 1) - tk, wr = 1.f - wl;
+        const float tk = fminf(fmaxf(tt, 0.f), (float)(RM - 1) - 0.01f);
+        const int tl = (int)tk;
+        const float wl = (float)(tl + 1) - tk, wr = 1.f - wl;
+#pragma unroll
         for (int q = 0; q < RM; ++q) {
-          float gdist = gd[k] * s[q] * ((float)q - e);
-          float gdfl = wd * (s[q] - (q == tl ? wl : 0.f) - (q == tl + 1 ? wr : 0.f));
-          gl[k][q] = gdist + gdfl;
+          const float gdist = gdk * sv[q] * ((float)q - e);
+          const float gdfl = wd * (sv[q] - (q == tl ? wl : 0.f) - (q == tl + 1 ? wr : 0.f));
+          gl[q] = gdist + gdfl;
         }
       }
+      store8<T>(gp + k * RM, gl);
+      store8<T>(gp + k * RM + 8, gl + 8);
     }
-    for (int k = 0; k < 4; ++k)
-      for (int q = 0; q < RM; ++q) gp[k * RM + q] = from_f<T>(gl[k][q]);
   }
   sh[threadIdx.x] = acc;
   __syncthreads();
@@ -500,12 +573,11 @@ __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, 
   if (threadIdx.x == 0) part[blockIdx.x] = sh[0];
 }
 
-// out[0..2] = (box, cls, dfl) after gains; out[3] = (sum) * B ; out[4] = n_fg
-__global__ void loss_final_kernel(const float* part, int nblk, const float* scal, int B, float box_gain,
-                                  float cls_gain, float dfl_gain, float* out) {
+__global__ void __launch_bounds__(256) loss_final_kernel(const float* part, int nblk, const float* scal, int B,
+                                                         float box_gain, float cls_gain, float dfl_gain, float* out) {
+  double s;
+  reduce_partials<1>(part, nblk, &s);
   if (threadIdx.x != 0) return;
-  double s = 0;
-  for (int k = 0; k < nblk; ++k) s += part[k];
   float tss = scal[0];
   float box = 0.f, dfl = 0.f;
   if (scal[5] > 0) {
@@ -591,10 +663,11 @@ extern "C" int adr_det_loss(int dtype, const void* f0, const void* f1, const voi
     hipMemsetAsync(tgi, 0, n * 4, st);
   }
   LDISPATCH(loss_fg_kernel, dim3(nblk), dim3(256), L, B, nmax, gt, pbox, align, tgi, fg, pos, tnorm, part);
-  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(64), 0, st, part, nblk, scal);
-  LDISPATCH(loss_cls_grad_kernel, dim3(nblk), dim3(256), L, G, B, nmax, nc, grad_scale, gt, pbox, tgi, fg, tnorm, scal,
+  hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(256), 0, st, part, nblk, scal);
+  ADR_REQUIRE(nc % 8 == 0 && nc <= 96, "det_loss: nc=%d (needs a multiple of 8, at most 96)", nc);
+  LDISPATCH(loss_cls_grad_kernel, dim3(cdiv((long)n, CLS_ANCHORS_PER_BLOCK)), dim3(256), L, G, B, nmax, nc, grad_scale, gt, pbox, tgi, fg, tnorm, scal,
             part2, box_gain, cls_gain, dfl_gain);
-  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(64), 0, st, part2, nblk, scal, B, box_gain, cls_gain, dfl_gain,
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, part2, (int)cdiv((long)n, CLS_ANCHORS_PER_BLOCK), scal, B, box_gain, cls_gain, dfl_gain,
                      out);
 #undef LDISPATCH
   return check_launch("adr_det_loss");

@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
                                                               const float* __restrict__ rstd,
                                                               const float* __restrict__ gamma, float* dgamma,
                                                               float* dbeta, float* A, float* B, float* Cc,
-                                                              int training) {
+                                                              int training, int accumulate) {
   int c = blockIdx.x;
   double a = 0.0, b = 0.0;
   for (int p = threadIdx.x; p < P; p += 256) {
@@ -163,8 +163,8 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
     double mu = mean[c], rs = rstd[c], g = gamma ? gamma[c] : 1.0;
     double sg = a;                   // sum g
     double sgx = (b - mu * a) * rs;  // sum g * xhat
-    if (dgamma) dgamma[c] = (float)sgx;
-    if (dbeta) dbeta[c] = (float)sg;
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)sgx : (float)sgx;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)sg : (float)sg;
     double Ak = g * rs;
     if (training) {
       double Bk = -Ak * rs * sgx / count;
@@ -263,7 +263,7 @@ __global__ void __launch_bounds__(256) gn_bwd_coef_kernel(const float* __restric
 __global__ void __launch_bounds__(256) gn_bwd_param_kernel(const float* __restrict__ partial, int N, int chunks, int C,
                                                            int G, const float* __restrict__ mean,
                                                            const float* __restrict__ rstd, float* dgamma,
-                                                           float* dbeta) {
+                                                           float* dbeta, int accumulate) {
   const int c = blockIdx.x, g = c / (C / G);
   double sgx = 0.0, sb = 0.0;
   for (int it = threadIdx.x; it < N * chunks; it += 256) {
@@ -285,8 +285,8 @@ __global__ void __launch_bounds__(256) gn_bwd_param_kernel(const float* __restri
     __syncthreads();
   }
   if (threadIdx.x == 0) {
-    if (dgamma) dgamma[c] = (float)r1[0];
-    if (dbeta) dbeta[c] = (float)r2[0];
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)r1[0] : (float)r1[0];
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)r2[0] : (float)r2[0];
   }
 }
 
@@ -431,9 +431,9 @@ extern "C" int adr_bn_finalize(const float* partial, int P, int C, double count,
 
 extern "C" int adr_bn_bwd_finalize(const float* partial, int P, int C, double count, const float* mean,
                                    const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* A,
-                                   float* B, float* Cc, int training, void* stream) {
+                                   float* B, float* Cc, int training, int accumulate, void* stream) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, P, C, count, mean,
-                     rstd, gamma, dgamma, dbeta, A, B, Cc, training);
+                     rstd, gamma, dgamma, dbeta, A, B, Cc, training, accumulate);
   return check_launch("adr_bn_bwd_finalize");
 }
 
@@ -448,14 +448,14 @@ extern "C" int adr_gn_finalize(const float* partial, int N, int chunks, int C, i
 
 extern "C" int adr_gn_bwd_finalize(const float* partial, int N, int chunks, int C, int G, double count,
                                    const float* mean, const float* rstd, const float* gamma, float* dgamma,
-                                   float* dbeta, float* A, float* B, float* Cc, void* stream) {
+                                   float* dbeta, float* A, float* B, float* Cc, int accumulate, void* stream) {
   ADR_REQUIRE(G <= 64 && C <= 1024 && C % G == 0, "gn_bwd_finalize: G=%d C=%d", G, C);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(gn_bwd_coef_kernel, dim3(N), dim3(256), 0, st, partial, chunks, C, G, count, mean, rstd, gamma, A,
                      B, Cc);
   if (dgamma || dbeta)
     hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(C), dim3(256), 0, st, partial, N, chunks, C, G, mean, rstd, dgamma,
-                       dbeta);
+                       dbeta, accumulate);
   return check_launch("adr_gn_bwd_finalize");
 }
 

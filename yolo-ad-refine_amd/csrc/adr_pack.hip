@@ -103,10 +103,54 @@ __global__ void image_to_nhwc_kernel(const float* __restrict__ src, T* __restric
   dst[i] = from_f<T>(v);
 }
 
+// vector form (W % 4 == 0, Cp == 8): a thread turns 4 consecutive pixels of C planes into 4 NHWC rows of 8
+// channels (float4 plane reads, 16-byte row stores)
+template <typename T>
+__global__ void __launch_bounds__(256) image_to_nhwc8_kernel(const float* __restrict__ src, T* __restrict__ dst, int N,
+                                                             int C, int H, int W) {
+  const long q = (long)blockIdx.x * blockDim.x + threadIdx.x;  // pixel quad
+  const long nq = (long)N * H * W / 4;
+  if (q >= nq) return;
+  const long pix = q * 4;
+  const long HW = (long)H * W;
+  const long b = pix / HW, hw = pix % HW;
+  float v[4][8];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    float4 f = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (c < C) f = *reinterpret_cast<const float4*>(src + (b * C + c) * HW + hw);
+    v[0][c] = f.x; v[1][c] = f.y; v[2][c] = f.z; v[3][c] = f.w;
+  }
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    T* o = dst + (pix + p) * 8;
+    if constexpr (sizeof(T) == 2) {
+      u32x4 r;
+      T* e = reinterpret_cast<T*>(&r);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) e[c] = from_f<T>(v[p][c]);
+      st16(o, r);
+    } else {
+      st16(o, *reinterpret_cast<const u32x4*>(&v[p][0]));
+      st16(o + 4, *reinterpret_cast<const u32x4*>(&v[p][4]));
+    }
+  }
+}
+
 extern "C" int adr_image_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cp,
                                  void* stream) {
   long n = (long)N * H * W * Cp;
   hipStream_t st = (hipStream_t)stream;
+  if (Cp == 8 && C <= 8 && W % 4 == 0) {
+    const long nq = (long)N * H * W / 4;
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL(image_to_nhwc8_kernel<__bf16>, dim3(cdiv(nq, 256)), dim3(256), 0, st, src, (__bf16*)dst, N, C,
+                         H, W);
+    else
+      hipLaunchKernelGGL(image_to_nhwc8_kernel<float>, dim3(cdiv(nq, 256)), dim3(256), 0, st, src, (float*)dst, N, C, H,
+                         W);
+    return check_launch("adr_image_to_nhwc");
+  }
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(image_to_nhwc_kernel<__bf16>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (__bf16*)dst, N, C, H,
                        W, Cp);
