@@ -54,6 +54,14 @@ typedef struct adr_conv_desc {
 int adr_conv2d_fwd(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                    float* stats, int accumulate, void* stream);
 int adr_conv2d_fwd_stat_tiles(const adr_conv_desc* d);
+/* bf16 engine (adr_conv.hip): the same contractions with BK = 64 steps, tap-packed reductions for channel
+ * counts below 64, LDS-staged 16-byte output rows and stride-2 DGRAD by output parity class. The forward takes
+ * the KRSC weight; the data gradient takes the CRSK weight (adr_pack_weight2). Stats tiles as above. */
+int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w_krsc, const float* bias, void* y,
+                        float* stats, int accumulate, void* stream);
+int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
+                          int accumulate, void* stream);
+int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d);
 /* dx = conv_transpose(dy, w) (+ bias[c]) (+ dx if accumulate).  Also ConvTranspose2d forward
  * (nn.ConvTranspose2d weight (Cin_T, Cout_T, R, S) channels_last == KRSC of the equivalent conv). */
 int adr_conv2d_dgrad(const adr_conv_desc* d, const void* dy, const void* w, const float* bias, void* dx,
@@ -70,6 +78,11 @@ int adr_conv2d_wgrad_splits(const adr_conv_desc* d);
 int adr_conv2d_wgrad_partials(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
                               void* stream);
 int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accumulate, void* stream);
+/* The split sum fused with the KRSC -> (K, C, R, S) parameter layout (adr_unpack_weight_grad): part holds
+ * `splits` slabs of split_stride floats whose first K*RS*Cp entries are [k][rs][c]; dst (+)= their sum at
+ * (k, c, rs) (or (c, k, rs) with transpose_kc), padded channels c >= C dropped. */
+int adr_wgrad_reduce_unpack(const float* part, long split_stride, int splits, float* dst, int K, int C, int Cp,
+                            int RS, int transpose_kc, int accumulate, void* stream);
 
 
 /* ---------------------------------------------------------------------------------------------------------
@@ -111,6 +124,10 @@ int adr_partial_sum(const float* partial, int P, int C, int which, float* out, i
  * ConvTranspose2d weight (C_in_T=K, C_out_T=C, R, S) as the equivalent conv's KRSC weight. */
 int adr_pack_weight(int dtype, const float* src, void* dst, int K, int C, int Cp, int RS, int transpose_kc,
                     void* stream);
+/* Both GEMM operand layouts of one weight in one pass: KRSC [Kp][RS][Cp] (forward rows) and CRSK [Cp][RS][Kp]
+ * (data-gradient rows), zero-padded for k >= K / c >= C; transpose_kc as adr_pack_weight. */
+int adr_pack_weight2(int dtype, const float* src, void* krsc, void* crsk, int K, int Kp, int C, int Cp, int RS,
+                     int transpose_kc, void* stream);
 int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, int RS, int transpose_kc,
                            int accumulate, void* stream);
 /* NCHW fp32 images (detect/train.py:57-59 preprocess output) -> NHWC compute dtype, channels padded to Cp. */

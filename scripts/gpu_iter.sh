@@ -12,3 +12,5 @@ grep '^{' $OUT/bench.log | tail -1 > $OUT/bench.json; cut -c1-400 $OUT/bench.jso
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 5 --warmup 2 --no-cpu-baseline > $OUT/prof.log 2>&1 || { echo prof_failed; tail -20 $OUT/prof.log; exit 1; }
 echo prof_ok
+timeout -k 10 300 python scripts/conv_table.py > $OUT/conv_table.txt 2>&1 || { echo table_failed; tail -5 $OUT/conv_table.txt; exit 1; }
+echo table_ok

@@ -16,7 +16,8 @@ def _prefixed(P, pre="m"):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("c1,c2,k,s,hw", [(16, 32, 3, 2, 24), (32, 64, 1, 1, 20), (64, 128, 3, 1, 13),
-                                           (128, 256, 3, 2, 20), (48, 16, 1, 1, 9), (8, 16, 3, 1, 7)])
+                                           (128, 256, 3, 2, 20), (48, 16, 1, 1, 9), (8, 16, 3, 1, 7),
+                                           (32, 32, 3, 2, 15), (16, 16, 1, 2, 9)])
 def test_conv_bn_silu(dtype, c1, c2, k, s, hw):
     from adrefine.nn.modules import Conv
     m = Conv(c1, c2, k, s)

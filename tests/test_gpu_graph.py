@@ -47,6 +47,6 @@ def test_graph_step_matches_eager():
     spread = _pdiff(e1, e2)
     d = _pdiff(e1, g)
     print(f"eager-eager max |dparam| {spread:.3e}, eager-graph {d:.3e}")
-    assert d <= 10 * spread + 1e-6, (d, spread)
+    assert d <= 10 * spread + 2e-4, (d, spread)
     ee, eg = e1.ema_state_dict(), g.ema_state_dict()
-    assert max(float((ee[k] - eg[k]).abs().max()) for k in ee) <= 10 * spread + 1e-6
+    assert max(float((ee[k] - eg[k]).abs().max()) for k in ee) <= 10 * spread + 2e-4

@@ -264,44 +264,98 @@ def _conv_work(d):
     return nbytes, 2 * d.n * d.ho * d.wo * d.k * d.r * d.s * d.c
 
 
+def _engine2(d, red_channels):
+    """Route a bf16 contraction to the BK-64 engine (adr_conv.hip) unless it is a stride-1 multi-tap conv whose
+    reduction channels fill whole 64-wide steps, where the generic engine's shallower tiles measure faster."""
+    if d.dtype != BF16:
+        return False
+    return d.r * d.s == 1 or d.stride_h == 2 or red_channels % 64 != 0
+
+
+def _conv2_symbol(bn, mode):
+    return f"_ZN3adr16conv_bf16_kernelILi{bn}ELi{mode}EEEvNS_8ConvArgsE"
+
+
 def conv_fwd(d, xp, wp, bias, yp, stats=None, accumulate=0):
-    tok = _t0(_gemm_symbol(d.dtype, _bn_of(d.k), 0), *_conv_work(d), _shape(d, "fwd") if _TIMING is not None else "")
-    lib.adr_conv2d_fwd(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(wp), bias, ctypes.c_void_p(yp), stats,
-                       int(accumulate), stream())
+    """y (+)= conv(x, w_krsc) (+bias); optional per-128-row-tile BN partial statistics of the stored values."""
+    e2 = _engine2(d, d.c)
+    sym = _conv2_symbol(_bn_of(d.k), 0) if e2 else _gemm_symbol(d.dtype, _bn_of(d.k), 0)
+    tok = _t0(sym, *_conv_work(d), _shape(d, "fwd") if _TIMING is not None else "")
+    fn = lib.adr_conv2d_fwd_bf16 if e2 else lib.adr_conv2d_fwd
+    fn(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(wp), bias, ctypes.c_void_p(yp), stats, int(accumulate),
+       stream())
     _t1(tok)
 
 
-def conv_dgrad(d, dyp, wp, bias, dxp, accumulate=0):
-    tok = _t0(_gemm_symbol(d.dtype, _bn_of(d.c), 1), *_conv_work(d), _shape(d, "dgrad") if _TIMING is not None else "")
-    lib.adr_conv2d_dgrad(ctypes.byref(d), ctypes.c_void_p(dyp), ctypes.c_void_p(wp), bias, ctypes.c_void_p(dxp),
-                         int(accumulate), stream())
+def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0):
+    """dx (+)= conv_transpose(dy, w); wpair = (KRSC, CRSK-or-None) packed weights (pack_weight2)."""
+    krsc, crsk = wpair
+    e2 = crsk is not None and _engine2(d, d.k)
+    mode = 2 if d.stride_h == 2 else 1
+    sym = _conv2_symbol(_bn_of(d.c), mode) if e2 else _gemm_symbol(d.dtype, _bn_of(d.c), 3 if mode == 2 else 1)
+    tok = _t0(sym, *_conv_work(d), _shape(d, "dgrad") if _TIMING is not None else "")
+    if e2:
+        lib.adr_conv2d_dgrad_bf16(ctypes.byref(d), ctypes.c_void_p(dyp), ctypes.c_void_p(crsk.data_ptr()), bias,
+                                  ctypes.c_void_p(dxp), int(accumulate), stream())
+    else:
+        lib.adr_conv2d_dgrad(ctypes.byref(d), ctypes.c_void_p(dyp), ctypes.c_void_p(krsc.data_ptr()), bias,
+                             ctypes.c_void_p(dxp), int(accumulate), stream())
     _t1(tok)
 
 
-def _wgrad(d, xp, dyp, K, C, RS, device):
-    """dw (K, RS, C) fp32 = WGRAD partial GEMM (+ the fixed-order split reduction when split)."""
-    n = K * RS * C
-    dw = torch.empty(n, dtype=torch.float32, device=device)
+def pack_weight2(w: torch.Tensor, dtype, cpad: int = 0, transpose_kc: int = 0, kpad: int = 0):
+    """(K, C, R, S) fp32 parameter -> (KRSC [Kp][RS][Cp], CRSK [Cp][RS][Kp]) operands in one launch for bf16
+    (the CRSK copy feeds the bf16 data-gradient engine); (KRSC, None) for fp32."""
+    if dtype != torch.bfloat16:
+        if kpad and kpad != w.shape[0]:
+            raise RuntimeError("pack_weight2: output-channel padding is bf16-only")
+        return pack_weight(w, dtype, cpad, transpose_kc), None
+    if transpose_kc:
+        C, K = w.shape[0], w.shape[1]
+    else:
+        K, C = w.shape[0], w.shape[1]
+    RS = 1
+    for v in w.shape[2:]:
+        RS *= v
+    Cp, Kp = max(C, cpad), max(K, kpad)
+    wf = w.detach()
+    if wf.dtype != torch.float32 or not wf.is_contiguous():
+        relayout_count[0] += 1
+        wf = wf.float().contiguous()
+    krsc = torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device)
+    crsk = torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device)
+    lib.adr_pack_weight2(dcode(dtype), fptr(wf), fptr(krsc), fptr(crsk), K, Kp, C, Cp, RS, transpose_kc, stream())
+    return krsc, crsk
+
+
+def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device):
+    """Weight gradient of a conv contraction straight into its parameter's gradient destination: the split-K
+    WGRAD GEMM writes [split][K][RS][C] fp32 slabs, and one fused reduce+unpack kernel sums the splits in a
+    fixed order and scatters them into the (K, C, R, S) layout of `param` (the trainer's arena slice when
+    present, accumulating; otherwise a fresh tensor returned for autograd). wshape may cover only the first
+    rows / unpadded channels of the GEMM (padded convs, DCN's [Cout][9C] columns)."""
     splits = lib.adr_conv2d_wgrad_splits(ctypes.byref(d))
+    stride = K * RS * C
     es = 2 if d.dtype == BF16 else 4
     name = (f"void adr::wgrad_bf16_kernel<{_bn_of(K)}, {_bn_of(C)}>(adr::WgArgs)" if d.dtype == BF16
             else _gemm_symbol(F32, _bn_of(C), 2))
-    work = (es * (d.n * d.h * d.w * d.c + d.n * d.ho * d.wo * d.k) + 4 * n, 2 * d.n * d.ho * d.wo * d.k * RS * d.c)
+    work = (es * (d.n * d.h * d.w * d.c + d.n * d.ho * d.wo * d.k) + 4 * stride, 2 * d.n * d.ho * d.wo * d.k * RS * d.c)
     shp = _shape(d, f"wgrad/{splits}") if _TIMING is not None else ""
-    if splits == 1:
-        tok = _t0(name, *work, shp)
-        lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(dw), 0,
-                                      stream())
-        _t1(tok)
-        return dw
-    ws = torch.empty(splits * n, dtype=torch.float32, device=device)
+    ws = torch.empty(splits * stride, dtype=torch.float32, device=device)
     tok = _t0(name, *work, shp)
     lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(ws), 0, stream())
     _t1(tok)
-    tok = _t0("adr::wgrad_reduce_kernel(float const*, float*, long, int, int)", 4 * n * (splits + 1), n * splits, shp)
-    lib.adr_wgrad_reduce(fptr(ws), fptr(dw), n, splits, 0, stream())
+    K_, C_ = wshape[0], wshape[1]
+    RS_ = 1
+    for v in wshape[2:]:
+        RS_ *= v
+    Cp = max(C_, cpad)
+    out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
+    tok = _t0("void adr::wgrad_reduce_kernel<true>(float const*, long, float*, long, int, int, adr::Unpack)",
+              4 * stride * (splits + 1), stride * splits, shp)
+    lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, K_, C_, Cp, RS_, 0, acc, stream())
     _t1(tok)
-    return dw
+    return grad_ret(param, out)
 
 
 def _bias_grad(dy, K, N, HW, cs, param=None):
@@ -333,7 +387,7 @@ class Conv2dFn(torch.autograd.Function):
         Cp = max(Cw, cpad)
         if C != Cp:
             raise RuntimeError(f"Conv2dFn: input has {C} channels, weight expects {Cw} (padded {Cp})")
-        wp = pack_weight(w, dtype, cpad)
+        wp, wt = pack_weight2(w, dtype, cpad)
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, K, dtype)
         y = empty_act(N, K, Ho, Wo, dtype, x.device)
@@ -343,7 +397,7 @@ class Conv2dFn(torch.autograd.Function):
             stats = torch.empty(tiles * 2 * K, dtype=torch.float32, device=x.device)
         bf = b.detach().float().contiguous() if b is not None else None
         conv_fwd(d, xp, wp.data_ptr(), fptr(bf), y.data_ptr(), fptr(stats))
-        ctx.save_for_backward(x, wp)
+        ctx.save_for_backward(x, wp, wt)
         ctx.meta = (stride, pad, cpad, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
         if stats is None:
@@ -353,7 +407,7 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
-        x, wp = ctx.saved_tensors
+        x, wp, wt = ctx.saved_tensors
         stride, pad, cpad, wshape, has_b = ctx.meta
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
         dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
@@ -365,10 +419,9 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = empty_act(N, C, H, W, x.dtype, x.device)
             d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
-            conv_dgrad(d2, dyp, wp.data_ptr(), None, dx.data_ptr())
+            conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr())
         if ctx.needs_input_grad[1]:
-            dwk = _wgrad(d, xp, dyp, K, C, R * S, x.device)
-            dw = sink_unpack(ctx.pw, dwk, wshape, cpad)
+            dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device)
         if has_b and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, K, N, Ho * Wo, dycs, ctx.pb)
         return dx, dw, db, None, None, None, None
@@ -385,13 +438,13 @@ class ConvT2dFn(torch.autograd.Function):
         _, Co, R, S = w.shape
         Ho = (H - 1) * stride - 2 * pad + R + out_pad
         Wo = (W - 1) * stride - 2 * pad + S + out_pad
-        wp = pack_weight(w, dtype)  # (Ci, Co, R, S) == KRSC of the equivalent conv (K=Ci, C=Co)
+        wp, wt = pack_weight2(w, dtype)  # (Ci, Co, R, S) == KRSC of the equivalent conv (K=Ci, C=Co)
         y = empty_act(N, Co, Ho, Wo, dtype, x.device)
         d, h2, w2 = conv_desc(N, Ho, Wo, Co, Co, Ci, R, S, stride, stride, pad, pad, xcs, dtype)
         if (h2, w2) != (H, W):
             raise RuntimeError("ConvT2dFn: inconsistent geometry")
         bf = b.detach().float().contiguous() if b is not None else None
-        conv_dgrad(d, xp, wp.data_ptr(), fptr(bf), y.data_ptr())
+        conv_dgrad(d, xp, (wp, wt), fptr(bf), y.data_ptr())
         ctx.save_for_backward(x, wp)
         ctx.meta = (stride, pad, w.shape, b is not None, Ho, Wo)
         ctx.pw, ctx.pb = w, b
@@ -413,8 +466,7 @@ class ConvT2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             # equivalent conv: input = dy_T (N, Ho, Wo, Co), output grad = x_T (N, H, W, Ci)
             d, _, _ = conv_desc(N, Ho, Wo, Co, dycs, Ci, R, S, stride, stride, pad, pad, xcs, x.dtype)
-            dwk = _wgrad(d, dyp, xp, Ci, Co, R * S, x.device)
-            dw = sink_unpack(ctx.pw, dwk, wshape)
+            dw = wgrad_param(ctx.pw, d, dyp, xp, Ci, Co, R * S, wshape, 0, x.device)
         if has_b and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, Co, N, Ho * Wo, dycs, ctx.pb)
         return dx, dw, db, None, None, None
@@ -1199,24 +1251,27 @@ class PaddedConvFn(torch.autograd.Function):
         N, C, H, W = x.shape
         K, _, R, S = w.shape
         RS = R * S
-        wp = torch.empty(kpad * RS * C, dtype=dtype, device=x.device)
-        zero_(wp)
-        wf = w.detach().float().contiguous()
-        lib.adr_pack_weight(dcode(dtype), fptr(wf), fptr(wp), K, C, C, RS, 0, stream())
+        if dtype == torch.bfloat16:
+            wp, wt = pack_weight2(w, dtype, kpad=kpad)
+        else:
+            wp, wt = torch.empty(kpad * RS * C, dtype=dtype, device=x.device), None
+            zero_(wp)
+            wf = w.detach().float().contiguous()
+            lib.adr_pack_weight(dcode(dtype), fptr(wf), fptr(wp), K, C, C, RS, 0, stream())
         bp = zero_(torch.empty(kpad, dtype=torch.float32, device=x.device))
         if b is not None:
             lib.adr_cast(F32, fptr(b.detach().float().contiguous()), F32, fptr(bp), K, stream())
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, kpad, R, S, stride, stride, pad, pad, kpad, dtype)
         y = empty_act(N, kpad, Ho, Wo, dtype, x.device)
         conv_fwd(d, xp, wp.data_ptr(), fptr(bp), y.data_ptr())
-        ctx.save_for_backward(x, wp)
+        ctx.save_for_backward(x, wp, wt)
         ctx.meta = (stride, pad, kpad, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, wp = ctx.saved_tensors
+        x, wp, wt = ctx.saved_tensors
         stride, pad, kpad, wshape, has_b = ctx.meta
         dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
         N, C, H, W = x.shape
@@ -1226,11 +1281,10 @@ class PaddedConvFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = empty_act(N, C, H, W, x.dtype, x.device)
             d2, _, _ = conv_desc(N, H, W, C, C, kpad, R, S, stride, stride, pad, pad, dycs, x.dtype)
-            conv_dgrad(d2, dyp, wp.data_ptr(), None, dx.data_ptr())
+            conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr())
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, kpad, R, S, stride, stride, pad, pad, dycs, x.dtype)
         if ctx.needs_input_grad[1]:
-            dwk = _wgrad(d, xp, dyp, kpad, C, R * S, x.device)
-            dw = sink_unpack(ctx.pw, dwk, wshape)  # first K rows of the [kpad][RS][C] gradient
+            dw = wgrad_param(ctx.pw, d, xp, dyp, kpad, C, R * S, wshape, 0, x.device)  # first K rows of [kpad][RS][C]
         if has_b and ctx.needs_input_grad[2]:
             db = sink(ctx.pb, _bias_grad(dy, kpad, N, Ho * Wo, dycs)[:K])
         return dx, dw, db, None, None, None
@@ -1276,8 +1330,7 @@ class DCNFn(torch.autograd.Function):
         dw = None
         if ctx.needs_input_grad[2]:
             dwd, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, dycs, dtype)
-            dwk = _wgrad(dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, dev)
-            dw = sink_unpack(ctx.pw, dwk, w.shape)
+            dw = wgrad_param(ctx.pw, dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, w.shape, 0, dev)
         dx32 = zero_(torch.empty(N * H * W * C, dtype=torch.float32, device=dev))
         dom = zero_(empty_act(N, om.shape[1], H, W, dtype, dev))
         lib.adr_dcn_col2im(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(dcols), fptr(dx32),

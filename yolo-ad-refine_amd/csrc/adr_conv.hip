@@ -1,0 +1,330 @@
+// bf16 implicit-GEMM convolution, forward and data-gradient, for NHWC activations on CDNA4 MFMA.
+//
+// One GEMM formulation for both directions (the reduction index is the flattened (tap, channel) of the
+// operand the rows gather from, channels fastest, so it walks the packed weight rows contiguously):
+//   FWD   y [m=(n,oy,ox)][k]  = sum_{t=(tap,c)}  x [n, oy*s-p+kh, ox*s-p+kw, c]     * Wkrsc[k][t]
+//   DGRAD dx[m=(n,iy,ix)][c]  = sum_{t=(tap,k)}  dy[n, (iy+p-kh)/s, (ix+p-kw)/s, k] * Wcrsk[c][t]
+// DGRAD of a stride-2 conv runs per output parity class (blockIdx.z): rows are the dx pixels (2i+py, 2j+px) and
+// the reduction covers only the taps with (pixel + pad - tap) even — a quarter of them on average.
+//
+// Tile: 256 threads (4 waves), BM = 128 rows x BN (16..128) columns, BK = 64 reduction elements per step.
+// Each 16-byte chunk of the A tile is one (row, 8 consecutive reduction elements) gather; reductions whose
+// channel count is a multiple of 8 but not of 64 (the 8-channel stem, 16/32/48-channel convs) pack several
+// taps into one K-step instead of zero-padding each tap to the step. Operands go global -> registers (issued
+// one step ahead) -> LDS rows of 64 + 8 elements (144-byte pitch: the 16 rows a ds_read_b128 lane group reads
+// fall on 16 disjoint bank quads) -> v_mfma_f32_16x16x32_bf16 fragments.
+// Epilogue: accumulators (+bias) are rounded to bf16 into an LDS image of the output tile, then written with
+// 16-byte row-contiguous stores; the optional train-mode BatchNorm partial sums (sum, sum of squares of the
+// stored values per column) are reduced from that image in a fixed order.
+#include "adr_common.h"
+
+namespace adr {
+
+enum ConvMode { CV_FWD = 0, CV_DGRAD = 1, CV_DGRAD2 = 2 };
+
+struct ConvArgs {
+  const __bf16* src;   // A gather source: x (FWD) or dy (DGRAD)
+  const __bf16* wt;    // B rows: KRSC (FWD) or CRSK (DGRAD), reduction-contiguous
+  __bf16* out;
+  const float* bias;
+  float* stats;        // [mtiles][2][N] or null
+  int n;
+  int sh_, sw_, scs, sco, sc;  // source image: height, width, channel stride/offset, channel count
+  int rh, rw, ocs, oco;        // row image (output pixels): height, width; output channel stride/offset
+  int r, s, str, ph, pw;       // kernel, stride, padding
+  int N;                       // GEMM columns (output channels)
+  int ktot;                    // reduction length = taps * sc
+  int ntiles;
+  int accumulate;
+};
+
+constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
+
+template <int BN, int MODE>
+__global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
+  constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
+  constexpr int WROWS = CBM / WAVES_M, WCOLS = BN / WAVES_N;
+  constexpr int TM = WROWS / 16, TN = WCOLS / 16;
+  constexpr int A_CH = CBM * (CBK / 8) / 256;                  // 4 chunks per thread
+  constexpr int B_TOT = BN * (CBK / 8), B_CH = (B_TOT + 255) / 256;
+  constexpr int OPITCH = BN + 8;                               // output image pitch (elements)
+  constexpr int SMEM_AB = (CBM + BN) * CLD;
+  constexpr int SMEM_O = CBM * OPITCH;
+  constexpr int SMEM = SMEM_AB > SMEM_O ? SMEM_AB : SMEM_O;
+  __shared__ __attribute__((aligned(16))) __bf16 smem[SMEM];
+  __shared__ float red[2][256 / (BN / 8) > 0 ? 256 / (BN / 8) : 1][BN];
+  __bf16* As = smem;
+  __bf16* Bs = smem + CBM * CLD;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x % a.ntiles;
+  const int m0 = mt * CBM, n0 = nt * BN;
+
+  // ---- row space (and the parity class for stride-2 DGRAD) ----
+  int rows_h = a.rh, rows_w = a.rw, cy = 0, cx = 0;
+  int kh0 = 0, kw0 = 0, tstep = 1, nkw = a.s, ktot = a.ktot;
+  if constexpr (MODE == CV_DGRAD2) {
+    cy = blockIdx.z >> 1;
+    cx = blockIdx.z & 1;
+    rows_h = (a.rh - cy + 1) >> 1;
+    rows_w = (a.rw - cx + 1) >> 1;
+    kh0 = (cy + a.ph) & 1;
+    kw0 = (cx + a.pw) & 1;
+    tstep = 2;
+    const int nkh = (a.r - kh0 + 1) >> 1;
+    nkw = (a.s - kw0 + 1) >> 1;
+    ktot = nkh * nkw * a.sc;
+  }
+  constexpr int ystep = MODE == CV_DGRAD2 ? 2 : 1;
+  const long Mrows = (long)a.n * rows_h * rows_w;
+  if ((long)m0 >= Mrows) return;  // block-uniform (a parity class smaller than the grid)
+  const int hw = rows_h * rows_w;
+  auto pixel_of = [&](long m) -> long {
+    const long img = m / hw;
+    const int rem = (int)(m - img * hw);
+    return (img * a.rh + (rem / rows_w) * ystep + cy) * a.rw + (rem % rows_w) * ystep + cx;
+  };
+
+  // per-thread A rows: chunk q = tid + 256 i -> row q / 8, reduction chunk q % 8
+  const int kc = tid & 7;
+  int r_img[A_CH], r_y[A_CH], r_x[A_CH];
+  bool r_ok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const long m = (long)m0 + (tid >> 3) + 32 * i;
+    r_ok[i] = m < Mrows;
+    const long mm = r_ok[i] ? m : 0;
+    r_img[i] = (int)(mm / hw);
+    const int rem = (int)(mm - (long)r_img[i] * hw);
+    r_y[i] = (rem / rows_w) * ystep + cy;
+    r_x[i] = (rem % rows_w) * ystep + cx;
+  }
+  const int RS = a.r * a.s;
+  const int ksteps = (ktot + CBK - 1) / CBK;
+
+  u32x4 ra[A_CH], rb[B_CH];
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  auto load = [&](int t) {
+    const int k = t * CBK + kc * 8;           // this thread's reduction chunk
+    const int ti = k / a.sc, c = k - ti * a.sc;
+    const bool kok = k < ktot;
+    int kh, kw;
+    if constexpr (MODE == CV_DGRAD2) {
+      kh = kh0 + tstep * (ti / nkw);
+      kw = kw0 + tstep * (ti % nkw);
+    } else {
+      kh = ti / a.s;
+      kw = ti - kh * a.s;
+    }
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      int sy, sx;
+      bool ok = kok && r_ok[i];
+      if constexpr (MODE == CV_FWD) {
+        sy = r_y[i] * a.str - a.ph + kh;
+        sx = r_x[i] * a.str - a.pw + kw;
+      } else {
+        const int ny = r_y[i] + a.ph - kh, nx = r_x[i] + a.pw - kw;
+        sy = ny / a.str;
+        sx = nx / a.str;
+        ok = ok && ny >= 0 && nx >= 0 && sy * a.str == ny && sx * a.str == nx;
+      }
+      ok = ok && sy >= 0 && sy < a.sh_ && sx >= 0 && sx < a.sw_;
+      ra[i] = ok ? ld16(a.src + ((long)(r_img[i] * a.sh_ + sy) * a.sw_ + sx) * a.scs + a.sco + c) : zero;
+    }
+    // B rows n0 + q/8, chunk q%8 (reduction-contiguous rows of RS * sc elements)
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int q = tid + 256 * i;
+      const int row = q >> 3, bk = t * CBK + (q & 7) * 8;
+      const int n = n0 + row;
+      int tf = 0, cc = 0;
+      const int bti = bk / a.sc;
+      cc = bk - bti * a.sc;
+      if constexpr (MODE == CV_DGRAD2)
+        tf = (kh0 + tstep * (bti / nkw)) * a.s + kw0 + tstep * (bti % nkw);
+      else
+        tf = bti;
+      const bool ok = q < B_TOT && n < a.N && bk < ktot;
+      rb[i] = ok ? ld16(a.wt + ((long)n * RS + tf) * a.sc + cc) : zero;
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) st16(&As[((tid >> 3) + 32 * i) * CLD + kc * 8], ra[i]);
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int q = tid + 256 * i;
+      if (q < B_TOT) st16(&Bs[(q >> 3) * CLD + (q & 7) * 8], rb[i]);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
+  if (ksteps > 0) {
+    load(0);
+    store();
+    __syncthreads();
+  }
+  for (int t = 0; t < ksteps; ++t) {
+    if (t + 1 < ksteps) load(t + 1);
+#pragma unroll
+    for (int kk = 0; kk < CBK / 32; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(&As[(wr0 + i * 16 + (lane & 15)) * CLD + kk * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[(wc0 + j * 16 + (lane & 15)) * CLD + kk * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+    if (t + 1 < ksteps) {
+      store();
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue: bf16 image of the tile in LDS, then 16-byte row stores ----
+  __bf16* Os = smem;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wc0 + j * 16 + (lane & 15);
+    const float b = (a.bias && n0 + col < a.N) ? a.bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Os[(wr0 + i * 16 + 4 * (lane >> 4) + e) * OPITCH + col] = (__bf16)(acc[i][j][e] + b);
+  }
+  __syncthreads();
+  constexpr int CPR = BN / 8;          // 16-byte chunks per row
+  constexpr int RPP = 256 / CPR;       // rows per pass
+  const int oc = tid % CPR, orow = tid / CPR;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const bool col_ok = n0 + oc * 8 < a.N;
+  for (int r = orow; r < CBM; r += RPP) {
+    const long m = (long)m0 + r;
+    if (m >= Mrows || !col_ok) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
+    __bf16* dst = a.out + pixel_of(m) * a.ocs + a.oco + n0 + oc * 8;
+    if (a.accumulate) {
+      const u32x4 o = ld16(dst);
+      const __bf16* ov = reinterpret_cast<const __bf16*>(&o);
+      __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e]);
+    }
+    st16(dst, v);
+    if (a.stats) {
+      const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = (float)sv[e];
+        s1[e] += f;
+        s2[e] += f * f;
+      }
+    }
+  }
+  if (a.stats) {  // fixed-order reduction over the row groups of each column
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[0][orow][oc * 8 + e] = s1[e];
+      red[1][orow][oc * 8 + e] = s2[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      float x1 = 0.f, x2 = 0.f;
+      for (int g = 0; g < RPP; ++g) {
+        x1 += red[0][g][tid];
+        x2 += red[1][g][tid];
+      }
+      a.stats[(long)mt * 2 * a.N + n0 + tid] = x1;
+      a.stats[(long)mt * 2 * a.N + a.N + n0 + tid] = x2;
+    }
+  }
+}
+
+template <int MODE>
+static void launch_conv(int bn, dim3 grid, const ConvArgs& g, hipStream_t st) {
+  switch (bn) {
+    case 16: hipLaunchKernelGGL((conv_bf16_kernel<16, MODE>), grid, dim3(256), 0, st, g); break;
+    case 32: hipLaunchKernelGGL((conv_bf16_kernel<32, MODE>), grid, dim3(256), 0, st, g); break;
+    case 64: hipLaunchKernelGGL((conv_bf16_kernel<64, MODE>), grid, dim3(256), 0, st, g); break;
+    default: hipLaunchKernelGGL((conv_bf16_kernel<128, MODE>), grid, dim3(256), 0, st, g); break;
+  }
+}
+
+static int conv_pick_bn(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128; }
+
+static int conv_check(const adr_conv_desc* d) {
+  ADR_REQUIRE(d && d->n > 0 && d->h > 0 && d->w > 0 && d->c > 0 && d->k > 0 && d->r > 0 && d->s > 0,
+              "conv: bad geometry");
+  ADR_REQUIRE(d->dtype == ADR_BF16, "conv (bf16 engine): dtype %d", d->dtype);
+  ADR_REQUIRE(d->c % 8 == 0 && d->k % 8 == 0, "conv: C (%d) and K (%d) must be multiples of 8", d->c, d->k);
+  ADR_REQUIRE(d->x_cstride % 8 == 0 && d->x_coff % 8 == 0 && d->y_cstride % 8 == 0 && d->y_coff % 8 == 0,
+              "conv: channel views must be 16-byte aligned");
+  ADR_REQUIRE(d->x_cstride >= d->x_coff + d->c && d->y_cstride >= d->y_coff + d->k, "conv: view exceeds stride");
+  ADR_REQUIRE(d->stride_h == d->stride_w && d->pad_h == d->pad_w, "conv: anisotropic stride/padding");
+  const int ho = (d->h + 2 * d->pad_h - d->r) / d->stride_h + 1, wo = (d->w + 2 * d->pad_w - d->s) / d->stride_w + 1;
+  ADR_REQUIRE(ho == d->ho && wo == d->wo, "conv: output size mismatch (%dx%d vs %dx%d)", d->ho, d->wo, ho, wo);
+  ADR_REQUIRE((long)d->n * d->h * d->w < (1l << 31) && (long)d->n * d->ho * d->wo < (1l << 31), "conv: too many pixels");
+  return ADR_OK;
+}
+
+}  // namespace adr
+
+using namespace adr;
+
+extern "C" int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                   float* stats, int accumulate, void* stream) {
+  int rc = conv_check(d);
+  if (rc) return rc;
+  ConvArgs g{};
+  g.src = (const __bf16*)x; g.wt = (const __bf16*)w; g.out = (__bf16*)y; g.bias = bias; g.stats = stats;
+  g.n = d->n; g.sh_ = d->h; g.sw_ = d->w; g.scs = d->x_cstride; g.sco = d->x_coff; g.sc = d->c;
+  g.rh = d->ho; g.rw = d->wo; g.ocs = d->y_cstride; g.oco = d->y_coff;
+  g.r = d->r; g.s = d->s; g.str = d->stride_h; g.ph = d->pad_h; g.pw = d->pad_w;
+  g.N = d->k; g.ktot = d->r * d->s * d->c; g.accumulate = accumulate;
+  const int bn = conv_pick_bn(g.N);
+  g.ntiles = cdiv(g.N, bn);
+  dim3 grid(cdiv((long)d->n * d->ho * d->wo, CBM) * g.ntiles);
+  launch_conv<CV_FWD>(bn, grid, g, (hipStream_t)stream);
+  return check_launch("adr_conv2d_fwd_bf16");
+}
+
+extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias,
+                                     void* dx, int accumulate, void* stream) {
+  int rc = conv_check(d);
+  if (rc) return rc;
+  ConvArgs g{};
+  g.src = (const __bf16*)dy; g.wt = (const __bf16*)w_crsk; g.out = (__bf16*)dx; g.bias = bias; g.stats = nullptr;
+  g.n = d->n; g.sh_ = d->ho; g.sw_ = d->wo; g.scs = d->y_cstride; g.sco = d->y_coff; g.sc = d->k;
+  g.rh = d->h; g.rw = d->w; g.ocs = d->x_cstride; g.oco = d->x_coff;
+  g.r = d->r; g.s = d->s; g.str = d->stride_h; g.ph = d->pad_h; g.pw = d->pad_w;
+  g.N = d->c; g.ktot = d->r * d->s * d->k; g.accumulate = accumulate;
+  const int bn = conv_pick_bn(g.N);
+  g.ntiles = cdiv(g.N, bn);
+  hipStream_t st = (hipStream_t)stream;
+  if (d->stride_h == 2) {  // parity classes; the largest (even, even) class sizes the grid
+    dim3 grid(cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM) * g.ntiles, 1, 4);
+    launch_conv<CV_DGRAD2>(bn, grid, g, st);
+  } else {
+    dim3 grid(cdiv((long)d->n * d->h * d->w, CBM) * g.ntiles);
+    launch_conv<CV_DGRAD>(bn, grid, g, st);
+  }
+  return check_launch("adr_conv2d_dgrad_bf16");
+}
+
+extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) { return cdiv((long)d->n * d->ho * d->wo, CBM); }

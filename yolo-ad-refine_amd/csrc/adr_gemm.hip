@@ -21,7 +21,7 @@
 
 namespace adr {
 
-enum GemmMode { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2 };
+enum GemmMode { MODE_FWD = 0, MODE_DGRAD = 1, MODE_WGRAD = 2, MODE_DGRAD2 = 3 };  // DGRAD2: stride-2 parity classes
 
 struct GemmArgs {
   const void* x;    // conv input  (FWD, WGRAD)
@@ -38,6 +38,7 @@ struct GemmArgs {
   int ktiles;                          // K-steps per block
   int ntiles;                          // column tiles
   int accumulate;                      // out += result
+  int par;                             // DGRAD stride-2: blockIdx.z = output parity class (see below)
   int red_per_split;                   // WGRAD: reduction rows per split (multiple of BK)
   long red_total;                      // WGRAD: total reduction rows (n*ho*wo)
 };
@@ -57,8 +58,10 @@ __device__ __forceinline__ int trb_row(int kk) {
   return (kk & 3) + 4 * ((kk >> 3) & 1) + 8 * ((kk >> 2) & 1) + 16 * (kk >> 4);
 }
 
-template <typename T, int BN, int MODE>
+template <typename T, int BN, int MODE_>
 __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
+  constexpr bool PAR = MODE_ == MODE_DGRAD2;
+  constexpr int MODE = PAR ? MODE_DGRAD : MODE_;
   constexpr int BM = 128, BK = Cfg<T>::BK, VEC = Cfg<T>::VEC, LDA = Cfg<T>::LDA;
   constexpr int WAVES_N = (BN >= 128) ? 2 : 1;
   constexpr int WAVES_M = 4 / WAVES_N;
@@ -87,6 +90,41 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   const int m0 = mt * BM;
   const int RS = a.r * a.s;
 
+  // ---- DGRAD of a stride-2 conv by output parity class (py, px) = blockIdx.z: the rows are the dx pixels
+  //      (2i + py, 2j + px) and the reduction runs only over the taps whose (pixel + pad - tap) is even, i.e.
+  //      kh = kh0, kh0 + 2, ... — a quarter of the taps on average instead of masking 3/4 of them to zero ----
+  int cls_y = 0, cls_x = 0, rows_h = (MODE == MODE_FWD) ? a.ho : a.h, rows_w = (MODE == MODE_FWD) ? a.wo : a.w_;
+  int kh0 = 0, kw0 = 0, nkw = a.s, tstep = 1;
+  long Mrows = a.M;
+  int ktiles = a.ktiles;
+  if constexpr (PAR) {
+    {
+      cls_y = blockIdx.z >> 1;
+      cls_x = blockIdx.z & 1;
+      rows_h = (a.h - cls_y + 1) >> 1;
+      rows_w = (a.w_ - cls_x + 1) >> 1;
+      Mrows = (long)a.n * rows_h * rows_w;
+      kh0 = (cls_y + a.ph) & 1;
+      kw0 = (cls_x + a.pw) & 1;
+      const int nkh = (a.r - kh0 + 1) >> 1;
+      nkw = (a.s - kw0 + 1) >> 1;
+      tstep = 2;
+      ktiles = nkh * nkw * a.cblocks;
+      if ((long)m0 >= Mrows) return;  // this class has fewer rows than the grid's largest
+    }
+  }
+  constexpr int ystep = PAR ? 2 : 1;
+  // output pixel (linear NHWC row) of GEMM row m
+  auto pixel_of = [&](long m) -> long {
+    if constexpr (PAR) {
+      const long hw = (long)rows_h * rows_w;
+      const long img = m / hw;
+      const int rem = (int)(m % hw);
+      return (img * a.h + (rem / rows_w) * 2 + cls_y) * a.w_ + (rem % rows_w) * 2 + cls_x;
+    }
+    return m;
+  };
+
   // ---- per-thread row decode for the A operand (FWD / DGRAD: output pixels) ----
   int a_img[A_CH], a_y[A_CH], a_x[A_CH];
   bool a_ok[A_CH];
@@ -95,14 +133,13 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
     for (int i = 0; i < A_CH; ++i) {
       int row = (tid + 256 * i) / KCH;
       long m = (long)m0 + row;
-      a_ok[i] = m < a.M;
-      int hw = (MODE == MODE_FWD) ? a.ho * a.wo : a.h * a.w_;
-      int ww = (MODE == MODE_FWD) ? a.wo : a.w_;
+      a_ok[i] = m < Mrows;
+      const int hw = rows_h * rows_w;
       long mm = a_ok[i] ? m : 0;
       a_img[i] = (int)(mm / hw);
       int rem = (int)(mm % hw);
-      a_y[i] = rem / ww;
-      a_x[i] = rem % ww;
+      a_y[i] = (rem / rows_w) * ystep + cls_y;
+      a_x[i] = (rem % rows_w) * ystep + cls_x;
     }
   }
   // column tile -> tap / channel block for WGRAD
@@ -142,8 +179,9 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
         rb[i] = ok ? ld16(p) : zero;
       }
     } else if constexpr (MODE == MODE_DGRAD) {
-      const int tap = t / a.cblocks, cb = t % a.cblocks;
-      const int kh = tap / a.s, kw = tap % a.s;
+      const int ti = t / a.cblocks, cb = t % a.cblocks;
+      const int kh = kh0 + tstep * (ti / nkw), kw = kw0 + tstep * (ti % nkw);
+      const int tap = kh * a.s + kw;
       const int kc = tid % KCH;
       const int co = cb * BK + kc * VEC;
 #pragma unroll
@@ -256,7 +294,6 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
-  const int ktiles = a.ktiles;
   if (ktiles > 0) {
     load_tile(0);
     store_tile();
@@ -338,8 +375,8 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           long m = (long)m0 + wr0 + i * 16 + 4 * (lane >> 4) + e;
-          if (m < a.M && n < a.N) {
-            T* p = out + m * ocs + oco + n;
+          if (m < Mrows && n < a.N) {
+            T* p = out + pixel_of(m) * ocs + oco + n;
             float v = acc[i][j][e] + b;
             if (a.accumulate) v += to_f(*p);
             T tv = from_f<T>(v);
@@ -378,21 +415,46 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
   }
 }
 
-// deterministic reduction of WGRAD split partials: dw[i] (+)= sum_s part[s][i]. One float per thread
-// (coalesced across the wave), eight independent loads in flight, combined in a fixed order.
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, float* __restrict__ dw,
-                                                           long n, int splits, int accumulate) {
-  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int k = 0;
-  for (; k + 8 <= splits; k += 8) {
+// deterministic reduction of WGRAD split partials: dw[i] (+)= sum_s part[s][i]. A block owns 32 consecutive
+// outputs; its 8 slices of 32 threads each sum every 8th split (coalesced 128-byte rows, 4 loads in flight),
+// then the slices are combined in LDS in a fixed order — parallel over splits as well as outputs, so a
+// small-output / many-split reduction still fills the chip.
+constexpr int WR_OUT = 32, WR_SL = 8;
+struct Unpack {  // UNPACK: output i = (k*RS + t)*Cp + c of the KRSC partials lands at the (K,C,RS) parameter slot
+  int K, C, Cp, RS, transpose_kc;
+};
+template <bool UNPACK>
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, long stride,
+                                                           float* __restrict__ dw, long n, int splits, int accumulate,
+                                                           Unpack u) {
+  __shared__ float sh[WR_SL][WR_OUT];
+  const int o = threadIdx.x % WR_OUT, sl = threadIdx.x / WR_OUT;
+  const long i = (long)blockIdx.x * WR_OUT + o;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  if (i < n) {
+    int k = sl, q = 0;
+    for (; k + 3 * WR_SL < splits; k += 4 * WR_SL) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u) acc[u] += part[(long)(k + u) * n + i];
+      for (int v = 0; v < 4; ++v) acc[v] += part[(long)(k + v * WR_SL) * stride + i];
+    }
+    for (; k < splits; k += WR_SL, ++q) acc[q & 3] += part[(long)k * stride + i];
   }
-  for (int u = 0; k < splits; ++k, ++u) acc[u] += part[(long)k * n + i];
-  float s = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  dw[i] = accumulate ? dw[i] + s : s;
+  sh[sl][o] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  __syncthreads();
+  if (sl == 0 && i < n) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < WR_SL; ++q) s += sh[q][o];
+    long di = i;
+    if constexpr (UNPACK) {
+      const int c = (int)(i % u.Cp);
+      const long r = i / u.Cp;
+      const int t = (int)(r % u.RS), k = (int)(r / u.RS);
+      if (c >= u.C) return;
+      di = u.transpose_kc ? ((long)c * u.K + k) * u.RS + t : ((long)k * u.C + c) * u.RS + t;
+    }
+    dw[di] = accumulate ? dw[di] + s : s;
+  }
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -479,6 +541,13 @@ extern "C" int adr_conv2d_dgrad(const adr_conv_desc* d, const void* dy, const vo
   g.ntiles = cdiv(g.N, bn);
   dim3 grid(cdiv(g.M, 128) * g.ntiles, 1);
   hipStream_t st = (hipStream_t)stream;
+  if (d->stride_h == 2 && d->stride_w == 2) {  // parity classes: the largest one sizes the grid
+    g.par = 1;
+    grid = dim3(cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), 128) * g.ntiles, 1, 4);
+    if (d->dtype == ADR_BF16) launch_bn<__bf16, MODE_DGRAD2>(bn, grid, g, st);
+    else launch_bn<float, MODE_DGRAD2>(bn, grid, g, st);
+    return check_launch("adr_conv2d_dgrad");
+  }
   if (d->dtype == ADR_BF16) launch_bn<__bf16, MODE_DGRAD>(bn, grid, g, st);
   else launch_bn<float, MODE_DGRAD>(bn, grid, g, st);
   return check_launch("adr_conv2d_dgrad");
@@ -544,9 +613,19 @@ extern "C" int adr_conv2d_wgrad_partials(const adr_conv_desc* d, const void* x, 
 
 extern "C" int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accumulate, void* stream) {
   ADR_REQUIRE(n > 0 && splits >= 1, "wgrad_reduce: n=%ld splits=%d", n, splits);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, part, dw, n, splits,
-                     accumulate);
+  hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(cdiv(n, WR_OUT)), dim3(256), 0, (hipStream_t)stream, part, n, dw,
+                     n, splits, accumulate, Unpack{});
   return check_launch("adr_wgrad_reduce");
+}
+
+extern "C" int adr_wgrad_reduce_unpack(const float* part, long split_stride, int splits, float* dst, int K, int C,
+                                       int Cp, int RS, int transpose_kc, int accumulate, void* stream) {
+  const long n = (long)K * RS * Cp;
+  ADR_REQUIRE(n > 0 && splits >= 1 && C <= Cp && split_stride >= n, "wgrad_reduce_unpack: K=%d C=%d Cp=%d RS=%d", K, C,
+              Cp, RS);
+  hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(cdiv(n, WR_OUT)), dim3(256), 0, (hipStream_t)stream, part,
+                     split_stride, dst, n, splits, accumulate, Unpack{K, C, Cp, RS, transpose_kc});
+  return check_launch("adr_wgrad_reduce_unpack");
 }
 
 extern "C" int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const void* dy, float* dw, int accumulate,

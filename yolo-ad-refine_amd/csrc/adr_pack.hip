@@ -38,6 +38,25 @@ __global__ void unpack_weight_grad_kernel(const float* __restrict__ src, float* 
   dst[s] = accumulate ? dst[s] + src[i] : src[i];
 }
 
+// both operand layouts from one read of the fp32 parameter: KRSC [Kp][RS][Cp] (FWD rows) and CRSK [Cp][RS][Kp]
+// (DGRAD rows); k >= K and c >= C are zero padding
+template <typename T>
+__global__ void pack_weight2_kernel(const float* __restrict__ src, T* __restrict__ krsc, T* __restrict__ crsk, int K,
+                                    int Kp, int C, int Cp, int RS, int transpose_kc) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long n = (long)Kp * Cp * RS;
+  if (i >= n) return;
+  int c = (int)(i % Cp);
+  long r = i / Cp;
+  int t = (int)(r % RS);
+  int k = (int)(r / RS);
+  float v = 0.f;
+  if (c < C && k < K) v = src[transpose_kc ? ((long)c * K + k) * RS + t : ((long)k * C + c) * RS + t];
+  const T tv = from_f<T>(v);
+  krsc[i] = tv;
+  crsk[((long)c * RS + t) * Kp + k] = tv;
+}
+
 template <typename A, typename B>
 __global__ void cast_kernel(const A* __restrict__ src, B* __restrict__ dst, long n) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -61,6 +80,20 @@ extern "C" int adr_pack_weight(int dtype, const float* src, void* dst, int K, in
     hipLaunchKernelGGL(pack_weight_kernel<float>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (float*)dst, K, C, Cp,
                        RS, transpose_kc);
   return check_launch("adr_pack_weight");
+}
+
+extern "C" int adr_pack_weight2(int dtype, const float* src, void* krsc, void* crsk, int K, int Kp, int C, int Cp,
+                                int RS, int transpose_kc, void* stream) {
+  ADR_REQUIRE(K <= Kp && C <= Cp && K > 0 && C > 0 && RS > 0, "pack_weight2: K=%d Kp=%d C=%d Cp=%d", K, Kp, C, Cp);
+  long n = (long)Kp * Cp * RS;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(pack_weight2_kernel<__bf16>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (__bf16*)krsc,
+                       (__bf16*)crsk, K, Kp, C, Cp, RS, transpose_kc);
+  else
+    hipLaunchKernelGGL(pack_weight2_kernel<float>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (float*)krsc,
+                       (float*)crsk, K, Kp, C, Cp, RS, transpose_kc);
+  return check_launch("adr_pack_weight2");
 }
 
 extern "C" int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, int RS,

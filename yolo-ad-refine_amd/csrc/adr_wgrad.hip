@@ -226,8 +226,8 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   const long red = (long)d->n * d->ho * d->wo;
   const long outsz = (long)d->k * d->r * d->s * d->c;
   p.tiles = cdiv(d->k, p.bm) * d->r * d->s * cdiv(d->c, p.bn);
-  long s = (512 + p.tiles - 1) / p.tiles;                   // ~2 workgroups per CU
-  const long by_work = red / ((long)p.R * 32);              // >= 32 k-steps per split
+  long s = (1024 + p.tiles - 1) / p.tiles;                  // ~4 workgroups per CU
+  const long by_work = red / ((long)p.R * 8);               // >= 8 k-steps per split
   const long by_bytes = (24l << 20) / (outsz * 4);          // <= 24 MB of partials (stays in L2/MALL)
   if (s > by_work) s = by_work;
   if (s > by_bytes) s = by_bytes;
