@@ -57,7 +57,7 @@ class FusedTrainer:
     """One process per GPU. `step(batch)` = zero grads + fwd + loss + bwd (+ all-reduce) + clip + SGD + EMA;
     returns the loss items (device tensor, no host sync)."""
 
-    CHUNK = 1 << 16
+    CHUNK = 1 << 12  # elements per optimizer block: ~1.6k blocks for the n model (16 per thread, 4 in flight)
 
     def __init__(self, model, lr0=0.01, momentum=0.937, weight_decay=5e-4, nbs=64, batch_size=64, world_size=1,
                  process_group=None, ema=True, ema_decay=0.9999, ema_tau=2000, max_norm=10.0):

@@ -72,6 +72,8 @@ class _Lib:
         ret = self.protos[name][0]
         if ret is ctypes.c_int and name not in _NONSTATUS:
             def call(*a):
+                if OP_TRACE is not None:
+                    return _traced(name, fn, a)
                 rc = fn(*a)
                 if rc != 0:
                     raise RuntimeError(f"{name}: {self.lib.adr_last_error().decode()}")
@@ -80,6 +82,27 @@ class _Lib:
             return call
         setattr(self, name, fn)
         return fn
+
+
+# Development op tracer (scripts/op_table.py): when OP_TRACE is a list, every status-returning entry point is
+# bracketed by HIP events on the current stream and recorded as (name, caller, int args, event0, event1).
+OP_TRACE = None
+
+
+def _traced(name, fn, a):
+    import sys
+
+    import torch
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    rc = fn(*a)
+    e1.record()
+    if rc != 0:
+        raise RuntimeError(f"{name}: {lib.lib.adr_last_error().decode()}")
+    caller = f"{sys._getframe(2).f_code.co_name}<{sys._getframe(3).f_code.co_name}"
+    ints = tuple(v for v in a if isinstance(v, int) and not isinstance(v, bool) and abs(v) < (1 << 31))
+    OP_TRACE.append((name, caller, ints, e0, e1))
+    return rc
 
 
 _NONSTATUS = {"adr_abi_version", "adr_conv2d_fwd_stat_tiles", "adr_conv2d_fwd_bf16_stat_tiles", "adr_conv2d_wgrad_splits", "adr_nc_reduce_chunks", "adr_opt_entry_size",

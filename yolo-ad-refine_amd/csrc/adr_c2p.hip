@@ -17,11 +17,12 @@ namespace adr {
 // depthwise k x k, stride 1, pad k/2. BWD = false: y = dwconv(x, w) + b; BWD = true: dx (+)= dwconv^T(dy, w)
 // (taps mirrored). The block stages w tap-major ([t][c]) in LDS so each tap is two 16-byte LDS reads per
 // 8-channel vector instead of eight strided global loads.
-template <typename T, bool BWD>
+template <typename T, bool BWD, int KS>
 __global__ void __launch_bounds__(256) dw_kernel(const T* __restrict__ x, int xcs, const float* __restrict__ w,
                                                  const float* __restrict__ b, T* __restrict__ y, int ycs, int N, int H,
-                                                 int W, int C, int k, int accumulate) {
+                                                 int W, int C, int kr, int accumulate) {
   constexpr int V = 16 / sizeof(T);
+  const int k = KS > 0 ? KS : kr;
   extern __shared__ float wl[];  // [k*k][C]
   const int kk = k * k;
   for (int i = threadIdx.x; i < kk * C; i += 256) {
@@ -35,27 +36,32 @@ __global__ void __launch_bounds__(256) dw_kernel(const T* __restrict__ x, int xc
   if (i >= total) return;
   const unsigned pix = i / G;
   const int c0 = (int)(i - pix * G) * V;
-  const int ww = (int)(pix % (unsigned)W);
-  const unsigned r = pix / (unsigned)W;
-  const int hh = (int)(r % (unsigned)H);
-  const int n = (int)(r / (unsigned)H);
+  int n, hh, ww;
+  pix_nhw(pix, H, W, n, hh, ww);
   const int p = k / 2;
   float acc[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) acc[e] = (!BWD && b) ? b[c0 + e] : 0.f;
-  for (int ky = 0; ky < k; ++ky) {
-    const int ih = BWD ? hh - ky + p : hh + ky - p;
-    if (ih < 0 || ih >= H) continue;
-    for (int kx = 0; kx < k; ++kx) {
-      const int iw = BWD ? ww - kx + p : ww + kx - p;
-      if (iw < 0 || iw >= W) continue;
-      const u32x4 v = ld16(x + ((long)(n * H + ih) * W + iw) * xcs + c0);
-      const T* e = reinterpret_cast<const T*>(&v);
-      const float* wt = wl + (ky * k + kx) * C + c0;
+  const T* xb = x + (long)n * H * W * xcs + c0;
 #pragma unroll
-      for (int q = 0; q < V; ++q) acc[q] += to_f(e[q]) * wt[q];
+  for (int ky = 0; ky < (KS > 0 ? KS : 1); ++ky)
+    for (int ky2 = 0; ky2 < (KS > 0 ? 1 : k); ++ky2) {
+      const int kyy = KS > 0 ? ky : ky2;
+      const int ih = BWD ? hh - kyy + p : hh + kyy - p;
+      if (ih < 0 || ih >= H) continue;
+#pragma unroll
+      for (int kx = 0; kx < (KS > 0 ? KS : 1); ++kx)
+        for (int kx2 = 0; kx2 < (KS > 0 ? 1 : k); ++kx2) {
+          const int kxx = KS > 0 ? kx : kx2;
+          const int iw = BWD ? ww - kxx + p : ww + kxx - p;
+          if (iw < 0 || iw >= W) continue;
+          const u32x4 v = ld16(xb + ((long)ih * W + iw) * xcs);
+          const T* e = reinterpret_cast<const T*>(&v);
+          const float* wt = wl + (kyy * k + kxx) * C + c0;
+#pragma unroll
+          for (int q = 0; q < V; ++q) acc[q] += to_f(e[q]) * wt[q];
+        }
     }
-  }
   T* dst = y + (long)pix * ycs + c0;
   if (BWD && accumulate) {
     const u32x4 pv = ld16(dst);
@@ -80,26 +86,35 @@ __global__ void __launch_bounds__(256) dw_bwd_w_kernel(const T* x, int xcs, cons
   const int G = C / V, rpp = 256 / G;
   const int tid = threadIdx.x, g = tid % G, r0 = tid / G;
   const int ky = t / k, kx = t % k, p = k / 2;
-  long npix = (long)N * H * W;
-  long beg = (long)chunk * rows_per_chunk, end = beg + rows_per_chunk;
-  if (end > npix) end = npix;
+  const int npix = N * H * W;
+  const int beg = chunk * rows_per_chunk, end = min(npix, beg + rows_per_chunk);
   float acc[V];
 #pragma unroll
   for (int e = 0; e < V; ++e) acc[e] = 0.f;
   if (r0 < rpp) {
-    for (long pix = beg + r0; pix < end; pix += rpp) {
-      int ww = (int)(pix % W);
-      long r = pix / W;
-      int hh = (int)(r % H);
-      int n = (int)(r / H);
-      int ih = hh + ky - p, iw = ww + kx - p;
-      if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
-      u32x4 dv = ld16(dy + pix * dcs + g * V);
-      u32x4 xv = ld16(x + (((long)n * H + ih) * W + iw) * xcs + g * V);
-      const T* de = reinterpret_cast<const T*>(&dv);
-      const T* xe = reinterpret_cast<const T*>(&xv);
+    int n, hh, ww;
+    pix_nhw(beg + r0, H, W, n, hh, ww);
+    const int dw_ = rpp % W, dh_ = rpp / W;  // advance (n, hh, ww) by rpp pixels without dividing
+    for (int pix = beg + r0; pix < end; pix += rpp) {
+      const int ih = hh + ky - p, iw = ww + kx - p;
+      if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+        const u32x4 dv = ld16(dy + (long)pix * dcs + g * V);
+        const u32x4 xv = ld16(x + (((long)n * H + ih) * W + iw) * xcs + g * V);
+        const T* de = reinterpret_cast<const T*>(&dv);
+        const T* xe = reinterpret_cast<const T*>(&xv);
 #pragma unroll
-      for (int q = 0; q < V; ++q) acc[q] += to_f(de[q]) * to_f(xe[q]);
+        for (int q = 0; q < V; ++q) acc[q] += to_f(de[q]) * to_f(xe[q]);
+      }
+      ww += dw_;
+      hh += dh_;
+      if (ww >= W) {
+        ww -= W;
+        ++hh;
+      }
+      while (hh >= H) {
+        hh -= H;
+        ++n;
+      }
     }
   }
 #pragma unroll
@@ -595,6 +610,19 @@ using namespace adr;
     else hipLaunchKernelGGL(KERN<float>, grid, block, sm, st, __VA_ARGS__);                             \
   } while (0)
 
+template <typename T, bool BWD>
+static void dw_launch(int k, dim3 grid, size_t sm, hipStream_t st, const T* x, int xcs, const float* w, const float* b,
+                      T* y, int ycs, int N, int H, int W, int C, int acc) {
+  if (k == 3)
+    hipLaunchKernelGGL((dw_kernel<T, BWD, 3>), grid, dim3(256), sm, st, x, xcs, w, b, y, ycs, N, H, W, C, k, acc);
+  else if (k == 5)
+    hipLaunchKernelGGL((dw_kernel<T, BWD, 5>), grid, dim3(256), sm, st, x, xcs, w, b, y, ycs, N, H, W, C, k, acc);
+  else if (k == 7)
+    hipLaunchKernelGGL((dw_kernel<T, BWD, 7>), grid, dim3(256), sm, st, x, xcs, w, b, y, ycs, N, H, W, C, k, acc);
+  else
+    hipLaunchKernelGGL((dw_kernel<T, BWD, 0>), grid, dim3(256), sm, st, x, xcs, w, b, y, ycs, N, H, W, C, k, acc);
+}
+
 extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w, const float* b, void* y, int ycs,
                               int N, int H, int W, int C, int k, void* stream) {
   int v = dtype == ADR_BF16 ? 8 : 4;
@@ -604,11 +632,11 @@ extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w,
   size_t sm = (size_t)k * k * C * sizeof(float);
   ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL((dw_kernel<__bf16, false>), dim3(cdiv(total, 256)), dim3(256), sm, st, (const __bf16*)x, xcs, w,
-                       b, (__bf16*)y, ycs, N, H, W, C, k, 0);
+    dw_launch<__bf16, false>(k, dim3(cdiv(total, 256)), sm, st, (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, N, H, W,
+                             C, 0);
   else
-    hipLaunchKernelGGL((dw_kernel<float, false>), dim3(cdiv(total, 256)), dim3(256), sm, st, (const float*)x, xcs, w,
-                       b, (float*)y, ycs, N, H, W, C, k, 0);
+    dw_launch<float, false>(k, dim3(cdiv(total, 256)), sm, st, (const float*)x, xcs, w, b, (float*)y, ycs, N, H, W, C,
+                            0);
   return check_launch("adr_dwconv_fwd");
 }
 
@@ -629,11 +657,11 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
     size_t sm = (size_t)k * k * C * sizeof(float);
     ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv_bwd: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
     if (dtype == ADR_BF16)
-      hipLaunchKernelGGL((dw_kernel<__bf16, true>), dim3(cdiv(total, 256)), dim3(256), sm, st, (const __bf16*)dy, dcs,
-                         w, nullptr, (__bf16*)dx, ocs, N, H, W, C, k, accumulate);
+      dw_launch<__bf16, true>(k, dim3(cdiv(total, 256)), sm, st, (const __bf16*)dy, dcs, w, nullptr, (__bf16*)dx, ocs, N,
+                              H, W, C, accumulate);
     else
-      hipLaunchKernelGGL((dw_kernel<float, true>), dim3(cdiv(total, 256)), dim3(256), sm, st, (const float*)dy, dcs,
-                         w, nullptr, (float*)dx, ocs, N, H, W, C, k, accumulate);
+      dw_launch<float, true>(k, dim3(cdiv(total, 256)), sm, st, (const float*)dy, dcs, w, nullptr, (float*)dx, ocs, N, H,
+                             W, C, accumulate);
   }
   if (dw) {
     ADR_REQUIRE(ws_bytes >= adr_dwconv_wgrad_workspace(N, H, W, C, k), "dwconv_bwd: workspace");

@@ -84,6 +84,94 @@ __device__ __forceinline__ float act_bwd(int act, float v) {
   }
 }
 
+// Thread -> (channel group, pixel row) mapping for 256-thread NHWC elementwise kernels: G = C / vector width
+// lanes per pixel, 256 / G pixels per block pass; the channel group is fixed for the thread's whole loop (so
+// per-channel coefficients load once) and the loop has no integer division. Host guarantees G <= 256.
+struct PixLanes {
+  int cg, r0, rpb;
+  bool active;
+  __device__ explicit PixLanes(int G) {
+    const int t = threadIdx.x;
+    rpb = 256 / G;
+    cg = t % G;
+    r0 = t / G;
+    active = r0 < rpb;
+  }
+};
+
+// (image, row, column) of a flattened NHWC pixel index (< 2^32) with 32-bit unsigned divisions
+__device__ __forceinline__ void pix_nhw(long pix, int H, int W, int& n, int& h, int& w) {
+  const unsigned p = (unsigned)pix;
+  const unsigned r = p / (unsigned)W;
+  w = (int)(p - r * (unsigned)W);
+  n = (int)(r / (unsigned)H);
+  h = (int)(r - (unsigned)n * (unsigned)H);
+}
+
+// VW consecutive channels per thread: one 16-byte access when VW * sizeof(T) == 16, scalar otherwise (the host
+// picks VW = 1 for views whose channel strides / offsets are not vector multiples).
+template <typename T, int VW>
+__device__ __forceinline__ void vload(const T* p, float* f) {
+  if constexpr (VW * sizeof(T) == 16) {
+    const u32x4 v = ld16(p);
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int i = 0; i < VW; ++i) f[i] = to_f(e[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VW; ++i) f[i] = to_f(p[i]);
+  }
+}
+template <typename T, int VW>
+__device__ __forceinline__ void vstore(T* p, const float* f) {
+  if constexpr (VW * sizeof(T) == 16) {
+    u32x4 v;
+    T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+    for (int i = 0; i < VW; ++i) e[i] = from_f<T>(f[i]);
+    st16(p, v);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VW; ++i) p[i] = from_f<T>(f[i]);
+  }
+}
+// optional accumulate into dst, then store
+template <typename T, int VW>
+__device__ __forceinline__ void vstore_acc(T* p, float* f, int accumulate) {
+  if (accumulate) {
+    float o[VW];
+    vload<T, VW>(p, o);
+#pragma unroll
+    for (int i = 0; i < VW; ++i) f[i] += o[i];
+  }
+  vstore<T, VW>(p, f);
+}
+
+// thread -> (channel group, pixel lane); loops: for (pix = first; pix < npix; pix += step) for (cg ...) — the
+// channel loop runs once unless C / VW > 256
+struct PoolLanes {
+  int cg0, cstep, r0, rpb;
+  bool active;
+  __device__ explicit PoolLanes(int G) {
+    const int t = threadIdx.x;
+    if (G <= 256) {
+      rpb = 256 / G;
+      cg0 = t % G;
+      r0 = t / G;
+      cstep = G;
+    } else {
+      rpb = 1;
+      cg0 = t;
+      r0 = 0;
+      cstep = 256;
+    }
+    active = r0 < rpb;
+  }
+};
+#define POOL_LOOP(L, npix, G)                                                                        \
+  for (long pix = (long)blockIdx.x * (L).rpb + (L).r0; pix < (npix); pix += (long)gridDim.x * (L).rpb) \
+    for (int cg = (L).cg0; cg < (G); cg += (L).cstep)
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // wave-level sum (64 lanes)

@@ -42,12 +42,11 @@ __global__ void __launch_bounds__(256) ew_kernel(int op, int act, const T* a, in
                                                  int ccs, T* o, int ocs, long npix, int C, const float* ca,
                                                  const float* cb, int accumulate) {
   constexpr int V = VecIO<T>::V;
-  const int G = C / V;
-  const long total = npix * G;
+  const PixLanes L(C / V);
+  if (!L.active) return;
+  const int c0 = L.cg * V;
   const float sa = ca ? *ca : 1.f, sb = cb ? *cb : 1.f;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    long pix = i / G;
-    int c0 = (int)(i % G) * V;
+  for (long pix = (long)blockIdx.x * L.rpb + L.r0; pix < npix; pix += (long)gridDim.x * L.rpb) {
     float fa[V], fb[V], fc[V], fo[V];
     VecIO<T>::load(a + pix * acs + c0, fa);
     if (op == EW_AXPBY || op == EW_MUL || op == EW_FMA || op == EW_ACT_BWD || op == EW_ADD3)
@@ -83,12 +82,11 @@ __global__ void __launch_bounds__(256) bcast_mul_kernel(const T* x, int xcs, con
                                                         const T* res, int rcs, T* o, int ocs, long npix, int HW, int C,
                                                         int accumulate) {
   constexpr int V = VecIO<T>::V;
-  const int G = C / V;
-  const long total = npix * G;
-  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long)gridDim.x * blockDim.x) {
-    long pix = i / G;
-    int c0 = (int)(i % G) * V;
-    int n = (int)(pix / HW);
+  const PixLanes L(C / V);
+  if (!L.active) return;
+  const int c0 = L.cg * V;
+  for (long pix = (long)blockIdx.x * L.rpb + L.r0; pix < npix; pix += (long)gridDim.x * L.rpb) {
+    const int n = (int)((unsigned long)pix / (unsigned)HW);
     float fx[V], fo[V];
     VecIO<T>::load(x + pix * xcs + c0, fx);
 #pragma unroll
@@ -110,26 +108,37 @@ __global__ void __launch_bounds__(256) bcast_mul_kernel(const T* x, int xcs, con
 }
 
 // out[n][c] = sum over chunks of partial[n][chunk][which][c], then optionally summed over n and/or c.
-// One workgroup per output element, fixed-order tree reduction (deterministic).
-__global__ void __launch_bounds__(256) nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which,
-                                                          float* out, int sum_n, int sum_c, int accumulate) {
+// One workgroup per output element (NT threads: 1024 when everything collapses to a scalar), fixed-order
+// per-thread strides + tree combine (deterministic); four loads in flight per thread.
+template <int NT>
+__global__ void __launch_bounds__(NT) nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which,
+                                                         float* out, int sum_n, int sum_c, int accumulate) {
   const int outC = sum_c ? 1 : C;
   const int idx = blockIdx.x;
   const int on = idx / outC, oc = idx % outC;
   const int nn = sum_n ? N : 1, ncc = sum_c ? C : 1;
   const int n0 = sum_n ? 0 : on, c0 = sum_c ? 0 : oc;
-  const long items = (long)nn * chunks * ncc;
+  const int items = nn * chunks * ncc;
+  auto at = [&](int it) {
+    const int r = it / ncc;
+    const int c = c0 + (it - r * ncc);
+    const int n = n0 + r / chunks, ch = r % chunks;
+    return partial[((long)n * chunks + ch) * 2 * C + (long)which * C + c];
+  };
   double s = 0.0;
-  for (long it = threadIdx.x; it < items; it += 256) {
-    const int c = c0 + (int)(it % ncc);
-    const long r = it / ncc;
-    const int ch = (int)(r % chunks), n = n0 + (int)(r / chunks);
-    s += partial[((long)n * chunks + ch) * 2 * C + (long)which * C + c];
+  int it = threadIdx.x;
+  for (; it + 3 * NT < items; it += 4 * NT) {
+    const float a = at(it), b = at(it + NT), c = at(it + 2 * NT), d = at(it + 3 * NT);
+    s += (double)a;
+    s += (double)b;
+    s += (double)c;
+    s += (double)d;
   }
-  __shared__ double sh[256];
+  for (; it < items; it += NT) s += (double)at(it);
+  __shared__ double sh[NT];
   sh[threadIdx.x] = s;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = NT / 2; o > 0; o >>= 1) {
     if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
     __syncthreads();
   }
@@ -209,8 +218,9 @@ __global__ void axpy_kernel(long n, float a, const float* x, float* y) {
   if (i < n) y[i] += a * x[i];
 }
 
-static int ew_grid(long work) {
-  long b = (work + 255) / 256;
+static int ew_grid(long npix, int G) {
+  const long rpb = 256 / G;  // pixels per block pass (PixLanes)
+  long b = (npix + rpb - 1) / rpb;
   if (b > 32768) b = 32768;
   if (b < 1) b = 1;
   return (int)b;
@@ -227,7 +237,8 @@ extern "C" int adr_ew(int dtype, int op, int act, const void* a, int acs, const 
   ADR_REQUIRE(C % v == 0 && acs % v == 0 && ocs % v == 0 && (!b || bcs % v == 0) && (!c || ccs % v == 0),
               "adr_ew: C=%d / strides must be multiples of %d", C, v);
   ADR_REQUIRE(((uintptr_t)a | (uintptr_t)o | (uintptr_t)b | (uintptr_t)c) % 16 == 0, "adr_ew: pointers not 16B aligned");
-  int g = ew_grid(npix * (C / v));
+  ADR_REQUIRE(C / v <= 256, "adr_ew: C=%d too wide", C);
+  int g = ew_grid(npix, C / v);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(ew_kernel<__bf16>, dim3(g), dim3(256), 0, st, op, act, (const __bf16*)a, acs,
@@ -243,7 +254,8 @@ extern "C" int adr_bcast_mul(int dtype, const void* x, int xcs, const float* g, 
   int v = dtype == ADR_BF16 ? 8 : 4;
   ADR_REQUIRE(C % v == 0 && xcs % v == 0 && ocs % v == 0 && (!res || rcs % v == 0), "adr_bcast_mul: misaligned");
   long npix = (long)N * HW;
-  int grid = ew_grid(npix * (C / v));
+  ADR_REQUIRE(C / v <= 256, "adr_bcast_mul: C=%d too wide", C);
+  int grid = ew_grid(npix, C / v);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(bcast_mul_kernel<__bf16>, dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, g, gns, gcs,
@@ -273,8 +285,12 @@ extern "C" int adr_dot_reduce(int dtype, const void* x, int xcs, const void* dz,
 extern "C" int adr_nc_collapse(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n,
                                int sum_c, int accumulate, void* stream) {
   int outn = (sum_n ? 1 : N) * (sum_c ? 1 : C);
-  hipLaunchKernelGGL(nc_collapse_kernel, dim3(outn), dim3(256), 0, (hipStream_t)stream, partial, N, chunks,
-                     C, which, out, sum_n, sum_c, accumulate);
+  if (outn == 1)
+    hipLaunchKernelGGL(nc_collapse_kernel<1024>, dim3(1), dim3(1024), 0, (hipStream_t)stream, partial, N, chunks, C,
+                       which, out, sum_n, sum_c, accumulate);
+  else
+    hipLaunchKernelGGL(nc_collapse_kernel<256>, dim3(outn), dim3(256), 0, (hipStream_t)stream, partial, N, chunks, C,
+                       which, out, sum_n, sum_c, accumulate);
   return check_launch("adr_nc_collapse");
 }
 

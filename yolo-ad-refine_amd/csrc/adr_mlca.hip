@@ -12,6 +12,7 @@
 // sigmoids / both Conv1d(1,1,k) (weight grads per image, summed later), bwd3 forms
 // dy = dout * up(att) + adjoint_pool(dlocal).  All deterministic (no atomics).
 #include "adr_common.h"
+#include <initializer_list>
 
 namespace adr {
 
@@ -19,18 +20,43 @@ static constexpr int LS = 5;  // local_size
 __device__ __forceinline__ int a_s(int o, int in, int out) { return (int)(((long)o * in) / out); }
 __device__ __forceinline__ int a_e(int o, int in, int out) { return (int)(((long)(o + 1) * in + out - 1) / out); }
 
-// fwd1: grid (25, N); local fp32 [N][25][C]
-template <typename T>
+// fwd1: grid (25, N); local fp32 [N][25][C]. Threads = channel groups (VW channels) x pixel splits of the bin,
+// fixed-order LDS combine.
+template <typename T, int VW>
 __global__ void __launch_bounds__(256) mlca_pool_kernel(const T* x, int xcs, int H, int W, int C, float* local) {
-  int p = blockIdx.x, n = blockIdx.y;
-  int i = p / LS, j = p % LS;
-  int hs = a_s(i, H, LS), he = a_e(i, H, LS), ws = a_s(j, W, LS), we = a_e(j, W, LS);
-  float inv = 1.f / (float)((he - hs) * (we - ws));
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f;
-    for (int h = hs; h < he; ++h)
-      for (int w = ws; w < we; ++w) s += to_f(x[(((long)n * H + h) * W + w) * xcs + c]);
-    local[((long)n * LS * LS + p) * C + c] = s * inv;
+  __shared__ float red[256 * VW];
+  const int p = blockIdx.x, n = blockIdx.y;
+  const int i = p / LS, j = p % LS;
+  const int hs = a_s(i, H, LS), he = a_e(i, H, LS), ws = a_s(j, W, LS), we = a_e(j, W, LS);
+  const int bw = we - ws, cnt = (he - hs) * bw;
+  const float inv = 1.f / (float)cnt;
+  const int G = C / VW;
+  for (int cb = 0; cb < G; cb += 256) {
+    const int gn = min(256, G - cb), S = 256 / gn;
+    const int cg = cb + threadIdx.x % gn, sp = threadIdx.x / gn, c0 = cg * VW;
+    float s[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) s[e] = 0.f;
+    if (sp < S)
+      for (int q = sp; q < cnt; q += S) {
+        const int h = hs + q / bw, w = ws + q % bw;
+        float v[VW];
+        vload<T, VW>(x + (((long)n * H + h) * W + w) * xcs + c0, v);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) s[e] += v[e];
+      }
+#pragma unroll
+    for (int e = 0; e < VW; ++e) red[threadIdx.x * VW + e] = s[e];
+    __syncthreads();
+    if (threadIdx.x < gn) {
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        float t = 0.f;
+        for (int r = 0; r < S; ++r) t += red[(r * gn + threadIdx.x) * VW + e];
+        local[((long)n * LS * LS + p) * C + c0 + e] = t * inv;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -97,52 +123,94 @@ __global__ void mlca_gsum_kernel(const float* datt, int N, int C, float* S) {
   S[idx] = s;
 }
 
-__device__ __forceinline__ float up_att(const float* A, int C, int h, int w, int H, int W, int c) {
-  int is = a_s(h, LS, H), ie = a_e(h, LS, H), js = a_s(w, LS, W), je = a_e(w, LS, W);
-  float s = 0.f;
+// up(att)[h][w][c0..c0+VW) = mean of att over the 5x5 bins in pixel (h, w)'s window
+template <int VW>
+__device__ __forceinline__ void up_att(const float* A, int C, int h, int w, int H, int W, int c0, float* out) {
+  const int is = a_s(h, LS, H), ie = a_e(h, LS, H), js = a_s(w, LS, W), je = a_e(w, LS, W);
+#pragma unroll
+  for (int e = 0; e < VW; ++e) out[e] = 0.f;
   for (int i = is; i < ie; ++i)
-    for (int j = js; j < je; ++j) s += A[(i * LS + j) * C + c];
-  return s / (float)((ie - is) * (je - js));
+    for (int j = js; j < je; ++j) {
+      const float* a = A + (i * LS + j) * C + c0;
+#pragma unroll
+      for (int e = 0; e < VW; ++e) out[e] += a[e];
+    }
+  const float inv = 1.f / (float)((ie - is) * (je - js));
+#pragma unroll
+  for (int e = 0; e < VW; ++e) out[e] *= inv;
 }
 
 // fwd3: out = res + y * up(att)
-template <typename T>
+template <typename T, int VW>
 __global__ void __launch_bounds__(256) mlca_apply_kernel(const T* y, int ycs, const T* res, int rcs, const float* att,
                                                          T* out, int ocs, int N, int H, int W, int C) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * H * W * C;
-  if (i >= total) return;
-  int c = (int)(i % C);
-  long pix = i / C;
-  int w = (int)(pix % W);
-  long r = pix / W;
-  int h = (int)(r % H);
-  int n = (int)(r / H);
-  float a = up_att(att + (long)n * LS * LS * C, C, h, w, H, W, c);
-  float v = to_f(y[pix * ycs + c]) * a;
-  if (res) v += to_f(res[pix * rcs + c]);
-  out[pix * ocs + c] = from_f<T>(v);
+  const int G = C / VW;
+  const PoolLanes L(G);
+  if (!L.active) return;
+  const long npix = (long)N * H * W;
+  POOL_LOOP(L, npix, G) {
+    int n, h, w;
+    pix_nhw(pix, H, W, n, h, w);
+    const int c0 = cg * VW;
+    float a[VW], v[VW];
+    up_att<VW>(att + (long)n * LS * LS * C, C, h, w, H, W, c0, a);
+    vload<T, VW>(y + pix * ycs + c0, v);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) v[e] *= a[e];
+    if (res) {
+      float r[VW];
+      vload<T, VW>(res + pix * rcs + c0, r);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) v[e] += r[e];
+    }
+    vstore<T, VW>(out + pix * ocs + c0, v);
+  }
 }
 
-// bwd1: datt[n][p][c] = sum over pixels whose up-window includes bin p of dout*y / window_count ; grid (25, N)
-template <typename T>
+// bwd1: datt[n][p][c] = sum over pixels whose up-window includes bin p of dout*y / window_count ; grid (25, N).
+// The pixels of bin (bi, bj) lie in a rectangle one row / column wider than the bin's pooling window.
+template <typename T, int VW>
 __global__ void __launch_bounds__(256) mlca_bwd_bins_kernel(const T* y, int ycs, const T* dout, int dcs, int H, int W,
                                                             int C, float* datt) {
-  int p = blockIdx.x, n = blockIdx.y;
-  int bi = p / LS, bj = p % LS;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    float s = 0.f;
-    for (int h = 0; h < H; ++h) {
-      int is = a_s(h, LS, H), ie = a_e(h, LS, H);
-      if (bi < is || bi >= ie) continue;
-      for (int w = 0; w < W; ++w) {
-        int js = a_s(w, LS, W), je = a_e(w, LS, W);
-        if (bj < js || bj >= je) continue;
-        long pix = ((long)n * H + h) * W + w;
-        s += to_f(dout[pix * dcs + c]) * to_f(y[pix * ycs + c]) / (float)((ie - is) * (je - js));
+  __shared__ float red[256 * VW];
+  const int p = blockIdx.x, n = blockIdx.y;
+  const int bi = p / LS, bj = p % LS;
+  const int h0 = max(0, a_s(bi, H, LS) - 1), h1 = min(H, a_e(bi, H, LS) + 1);
+  const int w0 = max(0, a_s(bj, W, LS) - 1), w1 = min(W, a_e(bj, W, LS) + 1);
+  const int rw = w1 - w0, cnt = (h1 - h0) * rw;
+  const int G = C / VW;
+  for (int cb = 0; cb < G; cb += 256) {
+    const int gn = min(256, G - cb), S = 256 / gn;
+    const int cg = cb + threadIdx.x % gn, sp = threadIdx.x / gn, c0 = cg * VW;
+    float s[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) s[e] = 0.f;
+    if (sp < S)
+      for (int q = sp; q < cnt; q += S) {
+        const int h = h0 + q / rw, w = w0 + q % rw;
+        const int is = a_s(h, LS, H), ie = a_e(h, LS, H);
+        const int js = a_s(w, LS, W), je = a_e(w, LS, W);
+        if (bi < is || bi >= ie || bj < js || bj >= je) continue;
+        const float inv = 1.f / (float)((ie - is) * (je - js));
+        const long pix = ((long)n * H + h) * W + w;
+        float d[VW], v[VW];
+        vload<T, VW>(dout + pix * dcs + c0, d);
+        vload<T, VW>(y + pix * ycs + c0, v);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) s[e] += d[e] * v[e] * inv;
+      }
+#pragma unroll
+    for (int e = 0; e < VW; ++e) red[threadIdx.x * VW + e] = s[e];
+    __syncthreads();
+    if (threadIdx.x < gn) {
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        float t = 0.f;
+        for (int r = 0; r < S; ++r) t += red[(r * gn + threadIdx.x) * VW + e];
+        datt[((long)n * LS * LS + p) * C + c0 + e] = t;
       }
     }
-    datt[((long)n * LS * LS + p) * C + c] = s;
+    __syncthreads();
   }
 }
 
@@ -225,32 +293,42 @@ __global__ void __launch_bounds__(256) mlca_att_bwd_kernel(const float* local, c
 }
 
 // bwd3: dy = dout * up(att) + pool_adjoint(dlocal)
-template <typename T>
+template <typename T, int VW>
 __global__ void __launch_bounds__(256) mlca_bwd_y_kernel(const T* dout, int dcs, const float* att, const float* dlocal,
                                                          T* dy, int ocs, int N, int H, int W, int C) {
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  long total = (long)N * H * W * C;
-  if (i >= total) return;
-  int c = (int)(i % C);
-  long pix = i / C;
-  int w = (int)(pix % W);
-  long r = pix / W;
-  int h = (int)(r % H);
-  int n = (int)(r / H);
-  float a = up_att(att + (long)n * LS * LS * C, C, h, w, H, W, c);
-  float g = to_f(dout[pix * dcs + c]) * a;
-  // adaptive pool H -> 5 adjoint: bins (bi, bj) whose window contains (h, w)
-  const float* DL = dlocal + (long)n * LS * LS * C;
-  for (int bi = 0; bi < LS; ++bi) {
-    int hs = a_s(bi, H, LS), he = a_e(bi, H, LS);
-    if (h < hs || h >= he) continue;
-    for (int bj = 0; bj < LS; ++bj) {
-      int ws = a_s(bj, W, LS), we = a_e(bj, W, LS);
-      if (w < ws || w >= we) continue;
-      g += DL[(bi * LS + bj) * C + c] / (float)((he - hs) * (we - ws));
+  const int G = C / VW;
+  const PoolLanes L(G);
+  if (!L.active) return;
+  const long npix = (long)N * H * W;
+  POOL_LOOP(L, npix, G) {
+    int n, h, w;
+    pix_nhw(pix, H, W, n, h, w);
+    const int c0 = cg * VW;
+    float a[VW], g[VW];
+    up_att<VW>(att + (long)n * LS * LS * C, C, h, w, H, W, c0, a);
+    vload<T, VW>(dout + pix * dcs + c0, g);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) g[e] *= a[e];
+    // adaptive pool H -> 5 adjoint: bins (bi, bj) whose window contains (h, w); candidates around h*5/H
+    const float* DL = dlocal + (long)n * LS * LS * C + c0;
+    // (for H, W >= 2*LS a pixel lies in at most the bins next to floor(h*LS/H); smaller maps scan all bins)
+    const int bic = h * LS / H, bjc = w * LS / W;
+    const int bi0 = H < 2 * LS ? 0 : max(0, bic - 1), bi1 = H < 2 * LS ? LS - 1 : min(LS - 1, bic + 1);
+    const int bj0 = W < 2 * LS ? 0 : max(0, bjc - 1), bj1 = W < 2 * LS ? LS - 1 : min(LS - 1, bjc + 1);
+    for (int bi = bi0; bi <= bi1; ++bi) {
+      const int hs = a_s(bi, H, LS), he = a_e(bi, H, LS);
+      if (h < hs || h >= he) continue;
+      for (int bj = bj0; bj <= bj1; ++bj) {
+        const int ws = a_s(bj, W, LS), we = a_e(bj, W, LS);
+        if (w < ws || w >= we) continue;
+        const float inv = 1.f / (float)((he - hs) * (we - ws));
+        const float* d = DL + (bi * LS + bj) * C;
+#pragma unroll
+        for (int e = 0; e < VW; ++e) g[e] += d[e] * inv;
+      }
     }
+    vstore<T, VW>(dy + pix * ocs + c0, g);
   }
-  dy[pix * ocs + c] = from_f<T>(g);
 }
 
 __global__ void sum_rows_kernel(const float* part, int rows, int cols, float* out) {
@@ -265,28 +343,49 @@ __global__ void sum_rows_kernel(const float* part, int rows, int cols, float* ou
 
 using namespace adr;
 
+// VW = 16 / sizeof(T) channels per thread when C, the channel strides and the pointers allow 16-byte accesses
+static bool mlca_vec(int dtype, int C, std::initializer_list<long> strides, std::initializer_list<const void*> ptrs) {
+  const int vw = dtype == ADR_BF16 ? 8 : 4;
+  if (C % vw) return false;
+  for (long s : strides)
+    if (s % vw) return false;
+  for (const void* p : ptrs)
+    if ((uintptr_t)p % 16) return false;
+  return true;
+}
+static dim3 mlca_grid(long npix, int dtype, bool v, int C) {
+  const int G = C / (v ? (dtype == ADR_BF16 ? 8 : 4) : 1);
+  const long rpb = G <= 256 ? 256 / G : 1;
+  long b = (npix + rpb - 1) / rpb;
+  return dim3((unsigned)(b > 65536 ? 65536 : (b < 1 ? 1 : b)));
+}
+// launches KERN<TT, VW> with TT bound to the storage type inside the argument list
+#define MLCA_DISPATCH(dtype, v, KERN, grid, ...)                                                  \
+  do {                                                                                          \
+    if ((dtype) == ADR_BF16) {                                                                  \
+      using TT = __bf16;                                                                        \
+      if (v) hipLaunchKernelGGL((KERN<TT, 8>), grid, dim3(256), 0, st, __VA_ARGS__);            \
+      else hipLaunchKernelGGL((KERN<TT, 1>), grid, dim3(256), 0, st, __VA_ARGS__);              \
+    } else {                                                                                    \
+      using TT = float;                                                                         \
+      if (v) hipLaunchKernelGGL((KERN<TT, 4>), grid, dim3(256), 0, st, __VA_ARGS__);            \
+      else hipLaunchKernelGGL((KERN<TT, 1>), grid, dim3(256), 0, st, __VA_ARGS__);              \
+    }                                                                                           \
+  } while (0)
+
 extern "C" int adr_mlca_fwd(int dtype, const void* y, int ycs, const void* res, int rcs, void* out, int ocs, int N,
                             int H, int W, int C, const float* wl, const float* wg, int k, float local_weight,
                             float* local, float* att, float* sig_l, float* sig_g, void* stream) {
   ADR_REQUIRE(k % 2 == 1 && k <= 15, "mlca: k=%d", k);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(mlca_pool_kernel<__bf16>, dim3(LS * LS, N), dim3(256), 0, st, (const __bf16*)y, ycs, H, W, C,
-                       local);
-  else
-    hipLaunchKernelGGL(mlca_pool_kernel<float>, dim3(LS * LS, N), dim3(256), 0, st, (const float*)y, ycs, H, W, C,
-                       local);
+  const bool v = mlca_vec(dtype, C, {ycs, rcs, ocs}, {y, res, out});
+  MLCA_DISPATCH(dtype, v, mlca_pool_kernel, dim3(LS * LS, N), (const TT*)y, ycs, H, W, C, local);
   size_t sm = 2 * C * sizeof(float);
   hipLaunchKernelGGL(mlca_att_kernel, dim3(N), dim3(256), sm, st, local, C, wl, wg, k, sig_l, sig_g);
   long natt = (long)N * LS * LS * C;
   hipLaunchKernelGGL(mlca_mix_kernel, dim3(cdiv(natt, 256)), dim3(256), 0, st, sig_l, sig_g, N, C, local_weight, att);
-  long total = (long)N * H * W * C;
-  if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(mlca_apply_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)y, ycs,
-                       (const __bf16*)res, rcs, att, (__bf16*)out, ocs, N, H, W, C);
-  else
-    hipLaunchKernelGGL(mlca_apply_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)y, ycs,
-                       (const float*)res, rcs, att, (float*)out, ocs, N, H, W, C);
+  MLCA_DISPATCH(dtype, v, mlca_apply_kernel, mlca_grid((long)N * H * W, dtype, v, C), (const TT*)y, ycs,
+                (const TT*)res, rcs, att, (TT*)out, ocs, N, H, W, C);
   return check_launch("adr_mlca_fwd");
 }
 
@@ -305,24 +404,16 @@ extern "C" int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout,
   float* dwl_part = dlocal + (size_t)N * LS * LS * C;
   float* dwg_part = dwl_part + (size_t)N * k;
   float* S = dwg_part + (size_t)N * k;
-  if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(mlca_bwd_bins_kernel<__bf16>, dim3(LS * LS, N), dim3(256), 0, st, (const __bf16*)y, ycs,
-                       (const __bf16*)dout, dcs, H, W, C, datt);
-  else
-    hipLaunchKernelGGL(mlca_bwd_bins_kernel<float>, dim3(LS * LS, N), dim3(256), 0, st, (const float*)y, ycs,
-                       (const float*)dout, dcs, H, W, C, datt);
+  const bool v = mlca_vec(dtype, C, {ycs, dcs, ocs}, {y, dout, dy});
+  MLCA_DISPATCH(dtype, v, mlca_bwd_bins_kernel, dim3(LS * LS, N), (const TT*)y, ycs, (const TT*)dout, dcs, H, W, C,
+                datt);
   size_t sm = (2 * C + LS * LS * C + 512) * sizeof(float);
   ADR_REQUIRE(sm <= 160 * 1024, "mlca_bwd: C=%d too large for the per-image LDS plan", C);
   hipLaunchKernelGGL(mlca_gsum_kernel, dim3(cdiv(LS * C, 256)), dim3(256), 0, st, datt, N, C, S);
   hipLaunchKernelGGL(mlca_att_bwd_kernel, dim3(N), dim3(256), sm, st, local, datt, sig_l, sig_g, S, N, C, wl, wg, k,
                      local_weight, dlocal, dwl_part, dwg_part);
-  long total = (long)N * H * W * C;
-  if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(mlca_bwd_y_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)dout, dcs,
-                       att, dlocal, (__bf16*)dy, ocs, N, H, W, C);
-  else
-    hipLaunchKernelGGL(mlca_bwd_y_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)dout, dcs,
-                       att, dlocal, (float*)dy, ocs, N, H, W, C);
+  MLCA_DISPATCH(dtype, v, mlca_bwd_y_kernel, mlca_grid((long)N * H * W, dtype, v, C), (const TT*)dout, dcs, att,
+                dlocal, (TT*)dy, ocs, N, H, W, C);
   hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(64), 0, st, dwl_part, N, k, dwl);
   hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(64), 0, st, dwg_part, N, k, dwg);
   return check_launch("adr_mlca_bwd");

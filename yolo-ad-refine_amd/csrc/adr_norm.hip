@@ -297,23 +297,31 @@ __global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x
                                                          const float* __restrict__ shift, int per_sample, int act,
                                                          long npix, int HW, int C) {
   constexpr int VEC = 16 / sizeof(T);
-  const unsigned G = C / VEC;
-  const unsigned total = (unsigned)(npix * G);  // host guarantees < 2^32
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const unsigned pix = i / G;
-    const int c0 = (int)(i - pix * G) * VEC;
-    const int n = (int)(pix / (unsigned)HW);
-    const u32x4 v = ld16(x + (long)pix * xcs + xco + c0);
+  const PixLanes L(C / VEC);
+  if (!L.active) return;
+  const int c0 = L.cg * VEC;
+  float sc[VEC], sh[VEC];
+  int ncur = -1;
+  if (!per_sample) {
+    ld_coef<VEC>(scale + c0, sc);
+    ld_coef<VEC>(shift + c0, sh);
+  }
+  for (long pix = (long)blockIdx.x * L.rpb + L.r0; pix < npix; pix += (long)gridDim.x * L.rpb) {
+    const u32x4 v = ld16(x + pix * xcs + xco + c0);
+    if (per_sample) {
+      const int n = (int)((unsigned long)pix / (unsigned)HW);
+      if (n != ncur) {
+        ncur = n;
+        ld_coef<VEC>(scale + n * C + c0, sc);
+        ld_coef<VEC>(shift + n * C + c0, sh);
+      }
+    }
     const T* e = reinterpret_cast<const T*>(&v);
-    const int base = per_sample ? n * C + c0 : c0;
-    float sc[VEC], sh[VEC];
-    ld_coef<VEC>(scale + base, sc);
-    ld_coef<VEC>(shift + base, sh);
     u32x4 o;
     T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
     for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(act_fwd(act, to_f(e[k]) * sc[k] + sh[k]));
-    st16(z + (long)pix * zcs + zco + c0, o);
+    st16(z + pix * zcs + zco + c0, o);
   }
 }
 
@@ -330,27 +338,42 @@ __global__ void __launch_bounds__(256) affine_act_bwd_kernel(const T* __restrict
                                                              int coef_per_sample, int act, long npix, int HW, int C,
                                                              int accumulate) {
   constexpr int VEC = 16 / sizeof(T);
-  const unsigned G = C / VEC;
-  const unsigned total = (unsigned)(npix * G);  // host guarantees < 2^32
-  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
-    const unsigned pix = i / G;
-    const int c0 = (int)(i - pix * G) * VEC;
-    const int n = (int)(pix / (unsigned)HW);
-    const u32x4 xv = ld16(x + (long)pix * xcs + xco + c0);
-    const u32x4 dv = ld16(dz + (long)pix * dcs + dco + c0);
+  const PixLanes L(C / VEC);
+  if (!L.active) return;
+  const int c0 = L.cg * VEC;
+  float sc[VEC], sh[VEC], ca[VEC], cbv[VEC], cc[VEC];
+  int ns = -1, nc = -1;
+  if (!per_sample) {
+    ld_coef<VEC>(scale + c0, sc);
+    ld_coef<VEC>(shift + c0, sh);
+  }
+  if (!coef_per_sample) {
+    ld_coef<VEC>(A + c0, ca);
+    ld_coef<VEC>(B + c0, cbv);
+    ld_coef<VEC>(Cc + c0, cc);
+  }
+  for (long pix = (long)blockIdx.x * L.rpb + L.r0; pix < npix; pix += (long)gridDim.x * L.rpb) {
+    const u32x4 xv = ld16(x + pix * xcs + xco + c0);
+    const u32x4 dv = ld16(dz + pix * dcs + dco + c0);
+    u32x4 prev = {0u, 0u, 0u, 0u};
+    if (accumulate) prev = ld16(dx + pix * ocs + oco + c0);
+    if (per_sample || coef_per_sample) {
+      const int n = (int)((unsigned long)pix / (unsigned)HW);
+      if (per_sample && n != ns) {
+        ns = n;
+        ld_coef<VEC>(scale + n * C + c0, sc);
+        ld_coef<VEC>(shift + n * C + c0, sh);
+      }
+      if (coef_per_sample && n != nc) {
+        nc = n;
+        ld_coef<VEC>(A + n * C + c0, ca);
+        ld_coef<VEC>(B + n * C + c0, cbv);
+        ld_coef<VEC>(Cc + n * C + c0, cc);
+      }
+    }
     const T* xe = reinterpret_cast<const T*>(&xv);
     const T* de = reinterpret_cast<const T*>(&dv);
-    u32x4 prev = {0u, 0u, 0u, 0u};
-    if (accumulate) prev = ld16(dx + (long)pix * ocs + oco + c0);
     const T* pe = reinterpret_cast<const T*>(&prev);
-    const int sb = per_sample ? n * C + c0 : c0;
-    const int cb = coef_per_sample ? n * C + c0 : c0;
-    float sc[VEC], sh[VEC], ca[VEC], cbv[VEC], cc[VEC];
-    ld_coef<VEC>(scale + sb, sc);
-    ld_coef<VEC>(shift + sb, sh);
-    ld_coef<VEC>(A + cb, ca);
-    ld_coef<VEC>(B + cb, cbv);
-    ld_coef<VEC>(Cc + cb, cc);
     u32x4 o;
     T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
@@ -361,7 +384,7 @@ __global__ void __launch_bounds__(256) affine_act_bwd_kernel(const T* __restrict
       if (accumulate) r += to_f(pe[k]);
       oe[k] = from_f<T>(r);
     }
-    st16(dx + (long)pix * ocs + oco + c0, o);
+    st16(dx + pix * ocs + oco + c0, o);
   }
 }
 
@@ -375,8 +398,9 @@ __global__ void __launch_bounds__(256) partial_sum_kernel(const float* __restric
   if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)a : (float)a;
 }
 
-static int grid_for(long work) {
-  long b = (work + 255) / 256;
+static int grid_for(long npix, int G) {
+  const long rpb = 256 / G;  // pixels per block pass (PixLanes)
+  long b = (npix + rpb - 1) / rpb;
   if (b > 65536) b = 65536;
   if (b < 1) b = 1;
   return (int)b;
@@ -466,8 +490,8 @@ extern "C" int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* 
   ADR_REQUIRE(C % vec == 0 && xcs % vec == 0 && xco % vec == 0 && zcs % vec == 0 && zco % vec == 0,
               "affine_act: misaligned view (C=%d)", C);
   long npix = (long)N * HW;
-  ADR_REQUIRE(npix * (C / vec) < (1l << 32), "affine_act: %ld vectors exceed the 32-bit index range", npix * (C / vec));
-  int grid = grid_for(npix * (C / vec));
+  ADR_REQUIRE(C / vec <= 256, "affine_act: C=%d too wide", C);
+  int grid = grid_for(npix, C / vec);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(affine_act_kernel<__bf16>, dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, xco,
@@ -487,9 +511,8 @@ extern "C" int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, co
                   ocs % vec == 0 && oco % vec == 0,
               "affine_act_bwd: misaligned view");
   long npix = (long)N * HW;
-  ADR_REQUIRE(npix * (C / vec) < (1l << 32), "affine_act_bwd: %ld vectors exceed the 32-bit index range",
-              npix * (C / vec));
-  int grid = grid_for(npix * (C / vec));
+  ADR_REQUIRE(C / vec <= 256, "affine_act_bwd: C=%d too wide", C);
+  int grid = grid_for(npix, C / vec);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(affine_act_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, xco,

@@ -28,11 +28,16 @@ __global__ void __launch_bounds__(256) grad_sqnorm_kernel(const OptEntry* tab, c
   const OptEntry e = tab[ck.entry];
   __shared__ double sh[256];
   double s = 0.0;
-  if (e.g && e.group < 3)
-    for (long i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
-      double v = e.g[i];
-      s += v * v;
+  if (e.g && e.group < 3) {
+    const long end = ck.start + ck.len;
+    for (long i0 = ck.start + threadIdx.x; i0 < end; i0 += 1024) {
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = i0 + 256 * u < end ? e.g[i0 + 256 * u] : 0.f;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += (double)v[u] * v[u];
     }
+  }
   sh[threadIdx.x] = s;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
@@ -72,18 +77,38 @@ __global__ void __launch_bounds__(256) sgd_ema_kernel(const OptEntry* tab, const
   const OptEntry e = tab[ck.entry];
   const float lr = e.group == 0 ? lr0 : (e.group == 1 ? lr1 : lr2);
   const float wd = e.group == 0 ? wd0 : (e.group == 1 ? wd1 : wd2);
-  for (long i = ck.start + threadIdx.x; i < ck.start + ck.len; i += 256) {
-    float p = e.p[i];
-    if (e.g && e.group < 3) {
-      float g = e.g[i] * coef;
-      if (wd != 0.f) g += wd * p;
-      float b = first ? g : momentum * e.buf[i] + g;
-      e.buf[i] = b;
-      float step = nesterov ? g + momentum * b : b;
-      p -= lr * step;
-      e.p[i] = p;
+  // U elements per thread per round, all loads issued before any store (the four arrays are distinct
+  // allocations, but the compiler cannot know that), so a round keeps 4*U loads in flight per lane
+  constexpr int U = 4;
+  const bool upd = e.g && e.group < 3;
+  const long end = ck.start + ck.len;
+  for (long i0 = ck.start + threadIdx.x; i0 < end; i0 += 256 * U) {
+    float p[U], g[U], b[U], m[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + 256 * u;
+      const bool in = i < end;
+      p[u] = in ? e.p[i] : 0.f;
+      g[u] = in && upd ? e.g[i] : 0.f;
+      b[u] = in && upd && !first ? e.buf[i] : 0.f;
+      m[u] = in && e.ema ? e.ema[i] : 0.f;
     }
-    if (e.ema) e.ema[i] = ema_d * e.ema[i] + (1.f - ema_d) * p;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long i = i0 + 256 * u;
+      if (i >= end) break;
+      float pv = p[u];
+      if (upd) {
+        float gv = g[u] * coef;
+        if (wd != 0.f) gv += wd * pv;
+        const float bv = first ? gv : momentum * b[u] + gv;
+        e.buf[i] = bv;
+        const float step = nesterov ? gv + momentum * bv : bv;
+        pv -= lr * step;
+        e.p[i] = pv;
+      }
+      if (e.ema) e.ema[i] = ema_d * m[u] + (1.f - ema_d) * pv;
+    }
   }
 }
 
