@@ -61,6 +61,27 @@ def cpu_baseline(bs=2, img=640, budget_s=20.0):
             "sample": f"{n} steps x {bs} images @{img}^2 (fwd+loss+bwd, fp32, torch CPU {threads} threads)"}
 
 
+def pmc_traffic(symbol):
+    """HBM bytes per launch of `symbol` from the committed PMC passes (profiles/pmc_traffic.json, written by
+    scripts/pmc_traffic.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this same bench); (None, None)
+    when the kernel was not covered."""
+    import subprocess
+    f = ROOT / "profiles" / "pmc_traffic.json"
+    if not f.exists():
+        return None, None
+    doc = json.loads(f.read_text())
+    name = symbol
+    if symbol.startswith("_Z"):
+        try:
+            name = subprocess.run(["c++filt", symbol], capture_output=True, text=True, timeout=10).stdout.strip()
+        except (OSError, subprocess.SubprocessError):
+            return None, None
+    rec = doc["kernels"].get(name)
+    if rec is None:
+        return None, None
+    return rec["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json ({rec['launches']} launches)"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -133,6 +154,8 @@ def main():
     if rank == 0:
         finite = bool(torch.isfinite(items).all())
         roof = K.roofline_report(ktimes, dtype, HBM_PEAK_GBS, BF16_MFMA_PEAK_TF if dtype == torch.bfloat16 else F32_MFMA_PEAK_TF)
+        if roof is not None:
+            roof["traffic"], roof["traffic_source"] = pmc_traffic(roof["kernel"])
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(budget_s=args.cpu_budget)
         out = {
             "metric": "images/sec whole-node (640x640) fwd+bwd, YOLO-AD-Refine-n at 1/2/4/8 GPU",
