@@ -311,6 +311,43 @@ int adr_flat_copy(const void* tab, const void* chunks, int nchunks, float* flat,
                   int to_flat, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------
+ * 697 L10 variant C2TSSA_DYT_Mona_EDFFN (nn/modules/block.py:1624-1709, nn/modules/mona.py) — adr_mona.hip.
+ * DynamicTanh (block.py:1624-1641): y = tanh(alpha x) w[c] + b[c]; backward writes dx and (+)= dalpha (scalar),
+ * dw, db (accumulate) through a fixed-order two-stage reduction in ws. */
+int adr_dyt_fwd(int dtype, const void* x, int xcs, const float* alpha, const float* w, const float* b, void* y,
+                int ycs, long npix, int C, void* stream);
+size_t adr_dyt_bwd_workspace(long npix, int C);
+int adr_dyt_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* alpha, const float* w,
+                void* dx, int ocs, float* dalpha, float* dw, float* db, int accumulate, long npix, int C, float* ws,
+                size_t ws_bytes, void* stream);
+/* Mona prologue (mona.py:5-10, 55-58): y = LayerNorm_C(x; lw, lb, eps) * gamma[c] + x * gammax[c] per pixel;
+ * saves per-pixel mean / rstd. C / (8 bf16 | 4 fp32) must be 8, 16, 32 or 64. */
+int adr_ln_mix_fwd(int dtype, const void* x, int xcs, const float* lw, const float* lb, const float* gamma,
+                   const float* gammax, void* y, int ycs, float* mean, float* rstd, long npix, int C, float eps,
+                   void* stream);
+size_t adr_ln_mix_bwd_workspace(long npix, int C);
+int adr_ln_mix_bwd(int dtype, const void* x, int xcs, const void* dz, int dcs, const float* lw, const float* lb,
+                   const float* gamma, const float* gammax, const float* mean, const float* rstd, void* dx, int ocs,
+                   float* dlw, float* dlb, float* dgamma, float* dgammax, int accumulate, long npix, int C, float* ws,
+                   size_t ws_bytes, void* stream);
+/* AttentionTSSA core (block.py:1646-1683) on the qkv-linear output tokens w (B, N, H*D), token stride cs:
+ * F.normalize over tokens, softmax over HEADS, out = -w * Pi * attn. state = adr_tssa1_state_floats floats
+ * saved by the forward for the backward. D = 64. */
+size_t adr_tssa1_state_floats(int B, int N, int H, int D);
+int adr_tssa1_fwd(int dtype, const void* w, int cs, int B, int N, int H, int D, const float* temp, void* out, int ocs,
+                  float* state, void* stream);
+size_t adr_tssa1_bwd_workspace(int B, int N, int H, int D);
+int adr_tssa1_bwd(int dtype, const void* w, int cs, int B, int N, int H, int D, const float* temp,
+                  const float* state, const void* g, int gcs, void* dw, int dwcs, float* dtemp, int accumulate,
+                  float* ws, size_t ws_bytes, void* stream);
+/* Dropout (Mona.dropout, mona.py:44/63) with a counter-based hash mask keyed by the DEVICE seed (so a captured
+ * graph draws a fresh mask per replay once adr_seed_advance is captured with it); the backward is the same
+ * call on the gradient with the same seed. */
+int adr_dropout(int dtype, const void* x, int xcs, void* y, int ycs, long npix, int C, float p, const int64_t* seed,
+                void* stream);
+int adr_seed_advance(int64_t* seed, void* stream);
+
+/* ---------------------------------------------------------------------------------------------------------
  * Batched NMS: replaces utils/ops.py:163-312 non_max_suppression (agnostic=False, classes=None, nm=0,
  * labels=()) with its torchvision.ops.nms call. y = decoded head output (B, 4+nc, A) fp32, rows xywh then class
  * scores. multi != 0: every (anchor, class) with score > conf (multi_label=True, the val path); else best class.

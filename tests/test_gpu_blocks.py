@@ -113,3 +113,30 @@ def test_ayhead_train(dtype):
 def test_c2ptssa(dtype):
     from adrefine.nn.modules.block import C2PTSSA
     run_fixture("c2ptssa", C2PTSSA(256, 256, 1), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c2tssa_mona(dtype):
+    """697 L10 variant (DynamicTanh, AttentionTSSA, Mona x2, EDFFN); Mona dropout p=0 as in the fixture."""
+    from adrefine.nn.modules.block import C2TSSA_DYT_Mona_EDFFN
+    m = C2TSSA_DYT_Mona_EDFFN(256, 256, 1)
+    for mm in m.modules():
+        if isinstance(mm, torch.nn.Dropout):
+            mm.p = 0.0
+    run_fixture("c2tssa_mona", m, dtype)
+
+
+def test_mona_dropout_mask():
+    """Mona dropout in training: ~p of the elements zeroed, survivors scaled by 1/(1-p), fresh mask per call,
+    backward routes through the same mask."""
+    from adrefine import kernels as K
+    x = torch.ones(4, 64, 20, 20, device="cuda").contiguous(memory_format=torch.channels_last).requires_grad_()
+    seed = torch.tensor([12345], dtype=torch.int64, device="cuda")
+    y1 = K.dropout(x, 0.1, seed, True)
+    y2 = K.dropout(x, 0.1, seed, True)
+    frac = float((y1 == 0).float().mean())
+    assert abs(frac - 0.1) < 0.01, frac
+    assert torch.allclose(y1[y1 != 0], torch.full_like(y1[y1 != 0], 1 / 0.9))
+    assert not torch.equal(y1, y2)
+    y1.backward(torch.ones_like(y1))
+    assert torch.equal((x.grad != 0), (y1 != 0))

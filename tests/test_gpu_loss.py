@@ -56,11 +56,19 @@ def test_loss_bf16_close():
     assert abs(float(loss) - float(g["loss"])) <= 0.03 * float(g["loss"])
 
 
-def test_network_train_step_loss_and_grads():
-    """Whole 701 network: train fwd + loss + bwd at 320^2 bs2 vs the reference (fp32 parity mode)."""
+_YAMLS = {"701": "yolo11-701-YOLO-AD-Refine.yaml", "697": "yolo11-697-newfpn+mona+AYHead+mlca3.yaml"}
+
+
+@pytest.mark.parametrize("tag", ["701", "697"])
+def test_network_train_step_loss_and_grads(tag):
+    """Whole network (701, and the 697 Mona L10 variant with Mona dropout disabled as in its fixture): train
+    fwd + loss + bwd at 320^2 bs2 vs the reference (fp32 parity mode)."""
     from adrefine.nn.tasks import DetectionModel
-    g = golden("net701_train_320")
-    m = DetectionModel(str(ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml"))
+    g = golden(f"net{tag}_train_320")
+    m = DetectionModel(str(ROOT / "tests" / "configs" / _YAMLS[tag]))
+    for mm in m.modules():
+        if isinstance(mm, torch.nn.Dropout):
+            mm.p = 0.0
     load_recipe_into(m)
     m = m.cuda().train()
     x = synthetic_images(2, 320, seed=int(g["img_seed"])).cuda()

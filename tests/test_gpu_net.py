@@ -1,4 +1,5 @@
-"""GPU parity: the whole YOLO-AD-Refine-n network (701 yaml) against reference-generated fixtures."""
+"""GPU parity: the whole YOLO-AD-Refine-n network (701 yaml, and the 697 Mona variant) against reference-generated
+fixtures."""
 import pytest
 import torch
 
@@ -8,19 +9,20 @@ from recipe import synthetic_images
 
 pytestmark = pytest.mark.gpu
 CFG = ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml"
+CFG697 = ROOT / "tests" / "configs" / "yolo11-697-newfpn+mona+AYHead+mlca3.yaml"
 
 
-def _model(dtype=torch.float32):
+def _model(dtype=torch.float32, cfg=CFG):
     from adrefine.nn.tasks import DetectionModel
-    m = DetectionModel(str(CFG), compute_dtype=dtype)
+    m = DetectionModel(str(cfg), compute_dtype=dtype)
     load_recipe_into(m)
     return m.cuda()
 
 
-@pytest.mark.parametrize("S", [320, 640])
-def test_eval_forward(S):
-    g = golden(f"net701_eval_{S}")
-    m = _model().eval()
+@pytest.mark.parametrize("tag,S", [("701", 320), ("701", 640), ("697", 320)])
+def test_eval_forward(tag, S):
+    g = golden(f"net{tag}_eval_{S}")
+    m = _model(cfg=CFG697 if tag == "697" else CFG).eval()
     x = synthetic_images(1, S, seed=int(g["img_seed"])).cuda()
     with torch.no_grad():
         y, feats = m(x)

@@ -1732,3 +1732,170 @@ class EDFFNFilterFn(torch.autograd.Function):
 
 def edffn_filter(x, fft):
     return EDFFNFilterFn.apply(x, fft)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# 697 L10 variant: DynamicTanh, Mona norm-mix, AttentionTSSA core, dropout (adr_mona.hip)
+# ------------------------------------------------------------------------------------------------------------
+
+
+def _f32(t):
+    return t.detach().float().contiguous()
+
+
+class DyTFn(torch.autograd.Function):
+    """DynamicTanh (block.py:1624-1641, channels_first): tanh(alpha x) * w[c] + b[c]."""
+
+    @staticmethod
+    def forward(ctx, x, alpha, w, b):
+        vx = _v(x)
+        N, C, H, W = x.shape
+        af, wf, bf = _f32(alpha), _f32(w), _f32(b)
+        y = _new_like(vx[0])
+        lib.adr_dyt_fwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], fptr(af), fptr(wf), fptr(bf),
+                        ctypes.c_void_p(y.data_ptr()), C, N * H * W, C, stream())
+        ctx.save_for_backward(vx[0], af, wf)
+        ctx.params = (alpha, w, b)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, af, wf = ctx.saved_tensors
+        pa, pw, pb = ctx.params
+        N, C, H, W = x.shape
+        vx, vd = _v(x), _v(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
+        dev = x.device
+        dx = _new_like(x)
+        # the three parameter gradients share one destination kind (all in the arena, or all fresh)
+        da, pda, acc = grad_dst(pa, 1, dev)
+        dw, pdw, acc_w = grad_dst(pw, C, dev)
+        db, pdb, acc_b = grad_dst(pb, C, dev)
+        if not acc == acc_w == acc_b:
+            raise RuntimeError("DynamicTanh parameter gradients must share one destination kind")
+        wsb = lib.adr_dyt_bwd_workspace(N * H * W, C)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
+        lib.adr_dyt_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]), vd[2], fptr(af),
+                        fptr(wf), ctypes.c_void_p(dx.data_ptr()), C, pda, pdw, pdb, acc, N * H * W, C, fptr(ws), wsb,
+                        stream())
+        return dx, grad_ret(pa, da), grad_ret(pw, dw), grad_ret(pb, db)
+
+
+def dyt(x, alpha, w, b):
+    return DyTFn.apply(x, alpha, w, b)
+
+
+class LnMixFn(torch.autograd.Function):
+    """Mona prologue (mona.py:5-10, 55-58): LayerNorm2d(x) * gamma + x * gammax (LayerNorm over channels)."""
+
+    @staticmethod
+    def forward(ctx, x, lw, lb, gamma, gammax, eps):
+        vx = _v(x)
+        N, C, H, W = x.shape
+        dev = x.device
+        ps = [_f32(p).view(-1) for p in (lw, lb, gamma, gammax)]
+        y = _new_like(vx[0])
+        mean = torch.empty(N * H * W, dtype=torch.float32, device=dev)
+        rstd = torch.empty_like(mean)
+        lib.adr_ln_mix_fwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], *[fptr(p) for p in ps],
+                           ctypes.c_void_p(y.data_ptr()), C, fptr(mean), fptr(rstd), N * H * W, C, float(eps),
+                           stream())
+        ctx.save_for_backward(vx[0], *ps, mean, rstd)
+        ctx.params = (lw, lb, gamma, gammax)
+        return y
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, lw, lb, gm, gx, mean, rstd = ctx.saved_tensors
+        N, C, H, W = x.shape
+        dev = x.device
+        vx, vd = _v(x), _v(dz.to(x.dtype) if dz.dtype != x.dtype else dz)
+        dx = _new_like(x)
+        dsts = [grad_dst(p, C, dev) for p in ctx.params]
+        if len({d[2] for d in dsts}) != 1:
+            raise RuntimeError("Mona norm parameter gradients must share one destination kind")
+        wsb = lib.adr_ln_mix_bwd_workspace(N * H * W, C)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
+        lib.adr_ln_mix_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]), vd[2], fptr(lw),
+                           fptr(lb), fptr(gm), fptr(gx), fptr(mean), fptr(rstd), ctypes.c_void_p(dx.data_ptr()), C,
+                           *[d[1] for d in dsts], dsts[0][2], N * H * W, C, fptr(ws), wsb, stream())
+        return (dx, *[grad_ret(p, d[0]) for p, d in zip(ctx.params, dsts)], None)
+
+
+def ln_mix(x, lw, lb, gamma, gammax, eps=1e-5):
+    return LnMixFn.apply(x, lw, lb, gamma, gammax, eps)
+
+
+class TSSA1Fn(torch.autograd.Function):
+    """AttentionTSSA core (block.py:1655-1683) on (B, C, N, 1) token tensors: w -> -w * Pi * attn."""
+
+    @staticmethod
+    def forward(ctx, w, temp, heads):
+        t, p, cs = _v(w)
+        B, C, N, _ = w.shape
+        D = C // heads
+        dev = w.device
+        tf = _f32(temp).view(-1)
+        state = torch.empty(lib.adr_tssa1_state_floats(B, N, heads, D), dtype=torch.float32, device=dev)
+        out = empty_act(B, C, N, 1, w.dtype, dev)
+        lib.adr_tssa1_fwd(dcode(w.dtype), ctypes.c_void_p(p), cs, B, N, heads, D, fptr(tf),
+                          ctypes.c_void_p(out.data_ptr()), C, fptr(state), stream())
+        ctx.save_for_backward(t, tf, state)
+        ctx.meta = heads
+        ctx.pt = temp
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        t, tf, state = ctx.saved_tensors
+        heads = ctx.meta
+        B, C, N, _ = t.shape
+        D = C // heads
+        dev = t.device
+        _, p, cs = _v(t)
+        _, gp, gcs = _v(dout.to(t.dtype) if dout.dtype != t.dtype else dout)
+        dw = empty_act(B, C, N, 1, t.dtype, dev)
+        dtemp, pdt, acc = grad_dst(ctx.pt, heads, dev)
+        wsb = lib.adr_tssa1_bwd_workspace(B, N, heads, D)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
+        lib.adr_tssa1_bwd(dcode(t.dtype), ctypes.c_void_p(p), cs, B, N, heads, D, fptr(tf), fptr(state),
+                          ctypes.c_void_p(gp), gcs, ctypes.c_void_p(dw.data_ptr()), C, pdt, acc, fptr(ws), wsb,
+                          stream())
+        return dw, grad_ret(ctx.pt, dtemp), None
+
+
+def tssa1(w, temp, heads):
+    return TSSA1Fn.apply(w, temp, heads)
+
+
+class DropoutFn(torch.autograd.Function):
+    """Inverted dropout with a hash mask keyed by a device seed (advanced on the device after each use, so a
+    captured graph draws a new mask per replay); the backward re-derives the same mask."""
+
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        vx = _v(x)
+        N, C, H, W = x.shape
+        y = _new_like(vx[0])
+        snap = seed.clone()  # this call's seed, for the backward
+        lib.adr_dropout(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(y.data_ptr()), C, N * H * W, C,
+                        float(p), ctypes.c_void_p(snap.data_ptr()), stream())
+        lib.adr_seed_advance(ctypes.c_void_p(seed.data_ptr()), stream())
+        ctx.save_for_backward(snap)
+        ctx.p = p
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (snap,) = ctx.saved_tensors
+        vd = _v(dy)
+        N, C, H, W = dy.shape
+        dx = _new_like(vd[0])
+        lib.adr_dropout(dcode(dy.dtype), ctypes.c_void_p(vd[1]), vd[2], ctypes.c_void_p(dx.data_ptr()), C, N * H * W,
+                        C, float(ctx.p), ctypes.c_void_p(snap.data_ptr()), stream())
+        return dx, None, None
+
+
+def dropout(x, p, seed, training):
+    if not training or p == 0.0:
+        return x
+    return DropoutFn.apply(x, p, seed)

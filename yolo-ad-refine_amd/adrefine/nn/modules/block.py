@@ -13,9 +13,11 @@ import torch.nn as nn
 
 from ... import kernels as K
 from .conv import Conv, Conv2d
+from .mona import Mona
 
 __all__ = ("Bottleneck", "C2f", "C3", "C3k", "C3k2", "SPPF", "MLCA", "Bottleneck_MLCA", "C3k_MLCA", "C3k2_MLCA",
-           "ELA_HSFPN", "Multiply", "Add", "Fusion", "DFL")
+           "ELA_HSFPN", "Multiply", "Add", "Fusion", "DFL", "C2PTSSA", "DynamicTanh", "AttentionTSSA",
+           "TSSAlock_DYT_Mona_EDFFN", "C2TSSA_DYT_Mona_EDFFN")
 
 
 class Bottleneck(nn.Module):
@@ -390,3 +392,76 @@ class C2ProgressiveTSSA_Fusion(C2PSA):
 
 
 C2PTSSA = C2ProgressiveTSSA_Fusion
+
+
+# ------------------------------------------------------------------------------------------------------------
+# 697 L10 variant: C2TSSA_DYT_Mona_EDFFN (reference block.py:1624-1709)
+# ------------------------------------------------------------------------------------------------------------
+
+
+class DynamicTanh(nn.Module):
+    """Reference block.py:1624-1644: tanh(alpha x) * weight + bias (channels_first on this path)."""
+
+    def __init__(self, normalized_shape, channels_last, alpha_init_value=0.5):
+        super().__init__()
+        if channels_last:
+            raise NotImplementedError("the AD-Refine path uses DynamicTanh(channels_last=False) on NCHW maps")
+        self.normalized_shape = normalized_shape
+        self.alpha_init_value = alpha_init_value
+        self.channels_last = channels_last
+        self.alpha = nn.Parameter(torch.ones(1) * alpha_init_value)
+        self.weight = nn.Parameter(torch.ones(normalized_shape))
+        self.bias = nn.Parameter(torch.zeros(normalized_shape))
+
+    def forward(self, x):
+        return K.dyt(x, self.alpha, self.weight, self.bias)
+
+
+class AttentionTSSA(nn.Module):
+    """Reference block.py:1646-1683 over (B, C, N, 1) token tensors: qkv linear -> TSSA core -> to_out."""
+
+    def __init__(self, dim, num_heads=8, qkv_bias=False, attn_drop=0.0, proj_drop=0.0, **kwargs):
+        super().__init__()
+        if attn_drop or proj_drop:
+            raise NotImplementedError("AttentionTSSA dropout is 0 on the AD-Refine path")
+        self.heads = num_heads
+        self.qkv = nn.Linear(dim, dim, bias=qkv_bias)
+        self.temp = nn.Parameter(torch.ones(num_heads, 1))
+        self.to_out = nn.Sequential(nn.Linear(dim, dim), nn.Dropout(proj_drop))
+
+    def forward(self, x_tok):
+        w = _linear(x_tok, self.qkv.weight, self.qkv.bias)
+        return _linear(K.tssa1(w, self.temp, self.heads), self.to_out[0].weight, self.to_out[0].bias)
+
+
+class TSSAlock_DYT_Mona_EDFFN(nn.Module):  # noqa: N801 (reference name)
+    """Reference block.py:1685-1703 (a PSABlock whose attn / ffn are replaced; attribute order as there, so the
+    state_dict key order matches)."""
+
+    def __init__(self, c, attn_ratio=0.5, num_heads=4, shortcut=True):
+        super().__init__()
+        self.attn = AttentionTSSA(c, num_heads=num_heads)
+        self.ffn = EDFFN(c, ffn_expansion_factor=2, bias=False)
+        self.add = shortcut
+        self.dyt1 = DynamicTanh(normalized_shape=c, channels_last=False)
+        self.dyt2 = DynamicTanh(normalized_shape=c, channels_last=False)
+        self.mona1 = Mona(c)
+        self.mona2 = Mona(c)
+
+    def forward(self, x):
+        B, C, H, W = x.shape
+        a = K.untokens(self.attn(K.tokens(self.dyt1(x))), H, W)
+        x = K.add(x, a) if self.add else a
+        x = self.mona1(x)
+        f = self.ffn(self.dyt2(x))
+        x = K.add(x, f) if self.add else f
+        return self.mona2(x)
+
+
+class C2TSSA_DYT_Mona_EDFFN(C2PSA):  # noqa: N801
+    """Reference block.py:1705-1709."""
+
+    def __init__(self, c1, c2, n=1, e=0.5):
+        super().__init__(c1, c2, n, e)
+        self.m = nn.Sequential(*(TSSAlock_DYT_Mona_EDFFN(self.c, attn_ratio=0.5, num_heads=self.c // 64)
+                                 for _ in range(n)))

@@ -27,7 +27,7 @@ _REGISTRY = {
     "Conv": conv.Conv, "Bottleneck": block.Bottleneck, "C2f": block.C2f, "C3": block.C3, "C3k2": block.C3k2,
     "SPPF": block.SPPF, "C3k2_MLCA": block.C3k2_MLCA, "C2PTSSA": block.C2PTSSA, "C2PSA": block.C2PSA,
     "ELA_HSFPN": block.ELA_HSFPN, "Multiply": block.Multiply, "Add": block.Add, "Fusion": block.Fusion,
-    "AYHead": head.AYHead, "AYHead1": head.AYHead1,
+    "AYHead": head.AYHead, "AYHead1": head.AYHead1, "C2TSSA_DYT_Mona_EDFFN": block.C2TSSA_DYT_Mona_EDFFN,
 }
 _NN = {"Conv2d": conv.Conv2d, "ConvTranspose2d": conv.ConvTranspose2d}
 
