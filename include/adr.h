@@ -128,6 +128,11 @@ int adr_pack_weight(int dtype, const float* src, void* dst, int K, int C, int Cp
  * (data-gradient rows), zero-padded for k >= K / c >= C; transpose_kc as adr_pack_weight. */
 int adr_pack_weight2(int dtype, const float* src, void* krsc, void* crsk, int K, int Kp, int C, int Cp, int RS,
                      int transpose_kc, void* stream);
+/* Many adr_pack_weight2 calls in one launch: table = nchunks device rows {const float* src; void* krsc;
+ * void* crsk; int K, Kp, C, Cp, RS, transpose_kc; long start, len;} (adr_pack_chunk_size() bytes each), each row
+ * packing elements [start, start+len) of one weight (the trainer packs every conv weight once per step). */
+int adr_pack_chunk_size(void);
+int adr_pack_weight2_batched(int dtype, const void* table, int nchunks, void* stream);
 int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, int RS, int transpose_kc,
                            int accumulate, void* stream);
 /* NCHW fp32 images (detect/train.py:57-59 preprocess output) -> NHWC compute dtype, channels padded to Cp. */

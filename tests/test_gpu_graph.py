@@ -40,13 +40,35 @@ def test_graph_step_matches_eager():
     b2 = {"img": synthetic_images(2, 320, seed=5).cuda(), **synthetic_labels(2, 80, seed=6)}
     seq = [b1, b1, b2, b1]
     e1, o1 = _run(seq, False)
-    e2, _ = _run(seq, False)
+    e2, o2 = _run(seq, False)
     g, og = _run(seq, True)
-    for a, b in zip(o1, og):
-        assert torch.allclose(a, b, rtol=1e-4, atol=1e-5), (a, b)
+    for a, b, c in zip(o1, og, o2):
+        item_spread = float((a - c).abs().max())
+        assert float((a - b).abs().max()) <= 10 * item_spread + 2e-4 * float(a.abs().max()), (a, b, c)
     spread = _pdiff(e1, e2)
     d = _pdiff(e1, g)
     print(f"eager-eager max |dparam| {spread:.3e}, eager-graph {d:.3e}")
     assert d <= 10 * spread + 2e-4, (d, spread)
     ee, eg = e1.ema_state_dict(), g.ema_state_dict()
     assert max(float((ee[k] - eg[k]).abs().max()) for k in ee) <= 10 * spread + 2e-4
+
+
+def test_pack_cache_matches_direct_packing():
+    """The trainer's batched once-per-step weight packing (PackCache.pack_all) produces exactly the operands a
+    per-call adr_pack_weight2 would, for every recorded conv weight, after an optimizer update."""
+    from adrefine import kernels as K
+    from adrefine.engine.trainer import FusedTrainer
+    from adrefine.nn.tasks import DetectionModel
+    m = DetectionModel(str(CFG), compute_dtype=torch.bfloat16)
+    load_recipe_into(m)
+    tr = FusedTrainer(m.cuda(), batch_size=2)
+    b = {"img": synthetic_images(2, 320, seed=0).cuda(), **synthetic_labels(2, 80, seed=1)}
+    tr.step(b)
+    tr.step(b)  # second step runs on pack_all's buffers; the weights have moved since
+    assert len(tr.packs.specs) > 50
+    tr.packs.pack_all()
+    torch.cuda.synchronize()
+    for (wid, cpad, tkc, kpad), sp in tr.packs.specs.items():
+        w = sp[0]
+        kr, cr = K.pack_weight2(w, torch.bfloat16, cpad, tkc, kpad)  # no active cache here: direct pack
+        assert torch.equal(kr, sp[7]) and torch.equal(cr, sp[8]), tuple(w.shape)

@@ -111,6 +111,7 @@ class FusedTrainer:
         self.ema_tau = ema_tau
         self.hyper = torch.zeros(16, dtype=torch.float32, device=dev)
         self.graphs = None
+        self.packs = K.PackCache()
 
     def _build_table(self):
         tab = np.zeros(len(self.entries), dtype=_ENTRY)
@@ -127,8 +128,10 @@ class FusedTrainer:
     def forward_backward(self, batch):
         K.zero_(self.grad)
         self.model.train()
-        loss, items = self.model(batch)
-        loss.backward()
+        with K.pack_scope(self.packs):
+            self.packs.pack_all()  # every conv weight's bf16 operand copies, one launch (no-op on the first step)
+            loss, items = self.model(batch)
+            loss.backward()
         return items
 
     def _set_hyper(self):
@@ -179,6 +182,7 @@ class FusedTrainer:
             if self.tab_dev is None:  # the set of parameters that receive gradients is static: build once
                 self._build_table()
             self._opt()
+        self.packs.valid = False  # weights changed: the next forward repacks
         self.updates += 1
         return items.detach()
 

@@ -303,9 +303,75 @@ def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0):
     _t1(tok)
 
 
+class PackCache:
+    """Per-trainer cache of the bf16 conv operand copies (KRSC + CRSK) of every conv weight. The first step
+    records each (weight, layout) pair and packs it into a persistent buffer; from then on `pack_all()` repacks
+    all of them in ONE batched launch at the start of the step (inside the captured graph), and pack_weight2
+    returns the cached buffers until the optimizer invalidates them."""
+
+    CHUNK = 1 << 13
+
+    def __init__(self):
+        self.specs = {}
+        self.valid = False
+        self.table = None
+        self.nchunks = 0
+        self.tab_dev = None
+
+    def _build(self):
+        import numpy as np
+        dt = np.dtype([("src", "<u8"), ("krsc", "<u8"), ("crsk", "<u8"), ("K", "<i4"), ("Kp", "<i4"), ("C", "<i4"),
+                       ("Cp", "<i4"), ("RS", "<i4"), ("tkc", "<i4"), ("start", "<i8"), ("len", "<i8")])
+        assert dt.itemsize == lib.adr_pack_chunk_size()
+        rows = []
+        for sp in self.specs.values():
+            w, K, Kp, C, Cp, RS, tkc, krsc, crsk = sp
+            n = Kp * RS * Cp
+            for st in range(0, n, self.CHUNK):
+                rows.append((w.data_ptr(), krsc.data_ptr(), crsk.data_ptr(), K, Kp, C, Cp, RS, tkc, st,
+                             min(self.CHUNK, n - st)))
+        tab = np.array(rows, dtype=dt)
+        dev = next(iter(self.specs.values()))[0].device
+        self.tab_dev = torch.from_numpy(tab.view(np.uint8).copy()).to(dev)
+        self.nchunks = len(rows)
+        self.table = len(self.specs)
+
+    def pack_all(self):
+        if not self.specs:
+            return
+        if self.table != len(self.specs):
+            self._build()
+        lib.adr_pack_weight2_batched(BF16, fptr(self.tab_dev), self.nchunks, stream())
+        self.valid = True
+
+
+_PACK = None  # the active PackCache (set by the trainer around its forward/backward)
+
+
+def pack_scope(cache):
+    """Context manager activating a PackCache."""
+    import contextlib
+
+    @contextlib.contextmanager
+    def _cm():
+        global _PACK
+        prev, _PACK = _PACK, cache
+        try:
+            yield cache
+        finally:
+            _PACK = prev
+    return _cm()
+
+
 def pack_weight2(w: torch.Tensor, dtype, cpad: int = 0, transpose_kc: int = 0, kpad: int = 0):
     """(K, C, R, S) fp32 parameter -> (KRSC [Kp][RS][Cp], CRSK [Cp][RS][Kp]) operands in one launch for bf16
-    (the CRSK copy feeds the bf16 data-gradient engine); (KRSC, None) for fp32."""
+    (the CRSK copy feeds the bf16 data-gradient engine); (KRSC, None) for fp32. Under an active PackCache the
+    operands come from (or are recorded into) its persistent buffers."""
+    pc = _PACK
+    key = (id(w), cpad, transpose_kc, kpad)
+    if pc is not None and dtype == torch.bfloat16 and pc.valid and key in pc.specs:
+        sp = pc.specs[key]
+        return sp[7], sp[8]
     if dtype != torch.bfloat16:
         if kpad and kpad != w.shape[0]:
             raise RuntimeError("pack_weight2: output-channel padding is bf16-only")
@@ -319,11 +385,20 @@ def pack_weight2(w: torch.Tensor, dtype, cpad: int = 0, transpose_kc: int = 0, k
         RS *= v
     Cp, Kp = max(C, cpad), max(K, kpad)
     wf = w.detach()
-    if wf.dtype != torch.float32 or not wf.is_contiguous():
+    direct = wf.dtype == torch.float32 and wf.is_contiguous()
+    if not direct:
         relayout_count[0] += 1
         wf = wf.float().contiguous()
-    krsc = torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device)
-    crsk = torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device)
+    if pc is not None and direct and w.is_leaf:  # record: persistent buffers, repacked by pack_all
+        sp = pc.specs.get(key)
+        if sp is None:
+            sp = (w, K, Kp, C, Cp, RS, transpose_kc, torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device),
+                  torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device))
+            pc.specs[key] = sp
+        krsc, crsk = sp[7], sp[8]
+    else:
+        krsc = torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device)
+        crsk = torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device)
     lib.adr_pack_weight2(dcode(dtype), fptr(wf), fptr(krsc), fptr(crsk), K, Kp, C, Cp, RS, transpose_kc, stream())
     return krsc, crsk
 
@@ -634,6 +709,18 @@ def gn_act(y, gn: torch.nn.Module, act: str):
 EW_COPY, EW_AXPBY, EW_MUL, EW_FMA, EW_ACT, EW_ACT_BWD, EW_ADD3 = range(7)
 
 
+_CONSTS = {}
+
+
+def _const(value, device):
+    """A cached 1-element fp32 device tensor (kernel scalar operands; no fill launch per use)."""
+    key = (float(value), str(device))
+    t = _CONSTS.get(key)
+    if t is None:
+        t = _CONSTS[key] = torch.full((1,), float(value), dtype=torch.float32, device=device)
+    return t
+
+
 def _ew(op, out, a, b=None, c=None, act=0, ca=None, cb=None, accumulate=0):
     """Launch adr_ew over same-shaped NHWC views (a, b, c, out are (tensor, ptr, cs) triples or None)."""
     t = a[0]
@@ -898,10 +985,10 @@ class WeightedSumFn(torch.autograd.Function):
         if base is not None:
             _ew(EW_AXPBY, vo, v0, _v(base), ca=wd[0:1])
         else:
-            _ew(EW_AXPBY, vo, v0, v0, ca=wd[0:1], cb=torch.zeros(1, device=w.device))
+            _ew(EW_AXPBY, vo, v0, v0, ca=wd[0:1], cb=_const(0.0, w.device))
         for i in range(1, len(xs)):
             vi = _v(xs[i])
-            _ew(EW_AXPBY, vo, vi, vi, ca=wd[i:i + 1], cb=torch.zeros(1, device=w.device), accumulate=1)
+            _ew(EW_AXPBY, vo, vi, vi, ca=wd[i:i + 1], cb=_const(0.0, w.device), accumulate=1)
         ctx.save_for_backward(wd, *[_v(x)[0] for x in xs])
         ctx.has_base = base is not None
         ctx.pw = w
@@ -914,7 +1001,7 @@ class WeightedSumFn(torch.autograd.Function):
         dxs = []
         for i, x in enumerate(xs):
             d = _new_like(x)
-            _ew(EW_AXPBY, (d, d.data_ptr(), d.shape[1]), vd, vd, ca=wd[i:i + 1], cb=torch.zeros(1, device=dy.device))
+            _ew(EW_AXPBY, (d, d.data_ptr(), d.shape[1]), vd, vd, ca=wd[i:i + 1], cb=_const(0.0, dy.device))
             dxs.append(d)
         dw = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs]) if ctx.needs_input_grad[0] else None
         return (sink(ctx.pw, dw), dy if ctx.has_base else None, *dxs)
@@ -937,7 +1024,7 @@ class FusionFn(torch.autograd.Function):
         v = [_v(x) for x in xs]
         _ew(EW_AXPBY, vo, v[0], v[1], ca=w[0:1], cb=w[1:2])
         for i in range(2, len(xs)):
-            _ew(EW_AXPBY, vo, v[i], v[i], ca=w[i:i + 1], cb=torch.zeros(1, device=fw.device), accumulate=1)
+            _ew(EW_AXPBY, vo, v[i], v[i], ca=w[i:i + 1], cb=_const(0.0, fw.device), accumulate=1)
         ctx.save_for_backward(fwd, w, *[t[0] for t in v])
         ctx.pfw = fw
         return out
@@ -946,7 +1033,7 @@ class FusionFn(torch.autograd.Function):
     def backward(ctx, dy):
         fwd, w, *xs = ctx.saved_tensors
         vd = _v(dy)
-        z = torch.zeros(1, device=dy.device)
+        z = _const(0.0, dy.device)
         dxs = []
         for i, x in enumerate(xs):
             d = _new_like(x)

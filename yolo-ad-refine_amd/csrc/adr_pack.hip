@@ -57,6 +57,33 @@ __global__ void pack_weight2_kernel(const float* __restrict__ src, T* __restrict
   crsk[((long)c * RS + t) * Kp + k] = tv;
 }
 
+// batched pack2: one block per chunk row of the table (a chunk = up to PACK_CHUNK elements of one weight)
+struct PackChunk {
+  const float* src;
+  void* krsc;
+  void* crsk;
+  int K, Kp, C, Cp, RS, tkc;
+  long start, len;
+};
+
+template <typename T>
+__global__ void __launch_bounds__(256) pack_weight2_batched_kernel(const PackChunk* tab) {
+  const PackChunk e = tab[blockIdx.x];
+  T* krsc = (T*)e.krsc;
+  T* crsk = (T*)e.crsk;
+  for (long i = e.start + threadIdx.x; i < e.start + e.len; i += 256) {
+    const int c = (int)(i % e.Cp);
+    const long r = i / e.Cp;
+    const int t = (int)(r % e.RS);
+    const int k = (int)(r / e.RS);
+    float v = 0.f;
+    if (c < e.C && k < e.K) v = e.src[e.tkc ? ((long)c * e.K + k) * e.RS + t : ((long)k * e.C + c) * e.RS + t];
+    const T tv = from_f<T>(v);
+    krsc[i] = tv;
+    crsk[((long)c * e.RS + t) * e.Kp + k] = tv;
+  }
+}
+
 template <typename A, typename B>
 __global__ void cast_kernel(const A* __restrict__ src, B* __restrict__ dst, long n) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -94,6 +121,18 @@ extern "C" int adr_pack_weight2(int dtype, const float* src, void* krsc, void* c
     hipLaunchKernelGGL(pack_weight2_kernel<float>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (float*)krsc,
                        (float*)crsk, K, Kp, C, Cp, RS, transpose_kc);
   return check_launch("adr_pack_weight2");
+}
+
+extern "C" int adr_pack_chunk_size(void) { return (int)sizeof(PackChunk); }
+
+extern "C" int adr_pack_weight2_batched(int dtype, const void* table, int nchunks, void* stream) {
+  ADR_REQUIRE(nchunks > 0, "pack_weight2_batched: empty table");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(pack_weight2_batched_kernel<__bf16>, dim3(nchunks), dim3(256), 0, st, (const PackChunk*)table);
+  else
+    hipLaunchKernelGGL(pack_weight2_batched_kernel<float>, dim3(nchunks), dim3(256), 0, st, (const PackChunk*)table);
+  return check_launch("adr_pack_weight2_batched");
 }
 
 extern "C" int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, int RS,
