@@ -51,8 +51,13 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   constexpr int SMEM_AB = (CBM + BN) * CLD;
   constexpr int SMEM_O = CBM * OPITCH;
   constexpr int SMEM = SMEM_AB > SMEM_O ? SMEM_AB : SMEM_O;
-  __shared__ __attribute__((aligned(16))) __bf16 smem[SMEM];
-  __shared__ float red[2][256 / (BN / 8) > 0 ? 256 / (BN / 8) : 1][BN];
+  constexpr int RG = 256 / (BN / 8);                           // row groups of the stats epilogue
+  constexpr int SMEM_BYTES = SMEM * 2 > 2 * RG * BN * 4 ? SMEM * 2 : 2 * RG * BN * 4;
+  // one LDS arena: A/B tiles in the main loop, the bf16 output image in the epilogue, then (aliased, after a
+  // barrier) the stats row-group sums — keeps LDS at the tile size so more blocks fit per CU
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[SMEM_BYTES];
+  __bf16* smem = reinterpret_cast<__bf16*>(lds_raw);
+  float (*red)[RG][BN] = reinterpret_cast<float (*)[RG][BN]>(lds_raw);
   __bf16* As = smem;
   __bf16* Bs = smem + CBM * CLD;
 
@@ -105,18 +110,34 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
 
   u32x4 ra[A_CH], rb[B_CH];
   const u32x4 zero = {0u, 0u, 0u, 0u};
-  auto load = [&](int t) {
-    const int k = t * CBK + kc * 8;           // this thread's reduction chunk
-    const int ti = k / a.sc, c = k - ti * a.sc;
-    const bool kok = k < ktot;
-    int kh, kw;
-    if constexpr (MODE == CV_DGRAD2) {
-      kh = kh0 + tstep * (ti / nkw);
-      kw = kw0 + tstep * (ti % nkw);
-    } else {
-      kh = ti / a.s;
-      kw = ti - kh * a.s;
+  // Reduction-position decoder, advanced by CBK per k-step without integer division: this thread's chunk sits
+  // at k = t*CBK + kc*8 = (tap ta, channel ca); (kh, kw) are the tap's kernel coordinates. The B rows use the
+  // same chunk position (q & 7 == kc for every B chunk of the thread), so one decoder serves both operands.
+  const int ntaps = ktot / a.sc;
+  int ta = (kc * 8) / a.sc, ca = kc * 8 - ta * a.sc;
+  int kh, kw;
+  if constexpr (MODE == CV_DGRAD2) {
+    kh = kh0 + tstep * (ta / nkw);
+    kw = kw0 + tstep * (ta % nkw);
+  } else {
+    kh = ta / a.s;
+    kw = ta - kh * a.s;
+  }
+  auto advance = [&]() {
+    ca += CBK;
+    while (ca >= a.sc) {
+      ca -= a.sc;
+      ++ta;
+      kw += tstep;
+      if (kw >= a.s) {
+        kw = kw0;
+        kh += tstep;
+      }
     }
+  };
+  auto load = [&]() {
+    const bool kok = ta < ntaps;
+    const int c = ca;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       int sy, sx;
@@ -124,31 +145,36 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
       if constexpr (MODE == CV_FWD) {
         sy = r_y[i] * a.str - a.ph + kh;
         sx = r_x[i] * a.str - a.pw + kw;
+      } else if constexpr (MODE == CV_DGRAD2) {
+        // parity class: ny, nx are even by construction
+        const int ny = r_y[i] + a.ph - kh, nx = r_x[i] + a.pw - kw;
+        sy = ny >> 1;
+        sx = nx >> 1;
+        ok = ok && ny >= 0 && nx >= 0;
       } else {
         const int ny = r_y[i] + a.ph - kh, nx = r_x[i] + a.pw - kw;
-        sy = ny / a.str;
-        sx = nx / a.str;
-        ok = ok && ny >= 0 && nx >= 0 && sy * a.str == ny && sx * a.str == nx;
+        if (a.str == 1) {
+          sy = ny;
+          sx = nx;
+        } else {
+          sy = ny / a.str;
+          sx = nx / a.str;
+          ok = ok && ny >= 0 && nx >= 0 && sy * a.str == ny && sx * a.str == nx;
+        }
       }
       ok = ok && sy >= 0 && sy < a.sh_ && sx >= 0 && sx < a.sw_;
       ra[i] = ok ? ld16(a.src + ((long)(r_img[i] * a.sh_ + sy) * a.sw_ + sx) * a.scs + a.sco + c) : zero;
     }
-    // B rows n0 + q/8, chunk q%8 (reduction-contiguous rows of RS * sc elements)
+    // B rows n0 + q/8 (reduction-contiguous rows of RS * sc elements), at this thread's chunk position
+    const int tf = MODE == CV_DGRAD2 ? kh * a.s + kw : ta;
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int q = tid + 256 * i;
-      const int row = q >> 3, bk = t * CBK + (q & 7) * 8;
-      const int n = n0 + row;
-      int tf = 0, cc = 0;
-      const int bti = bk / a.sc;
-      cc = bk - bti * a.sc;
-      if constexpr (MODE == CV_DGRAD2)
-        tf = (kh0 + tstep * (bti / nkw)) * a.s + kw0 + tstep * (bti % nkw);
-      else
-        tf = bti;
-      const bool ok = q < B_TOT && n < a.N && bk < ktot;
-      rb[i] = ok ? ld16(a.wt + ((long)n * RS + tf) * a.sc + cc) : zero;
+      const int n = n0 + (q >> 3);
+      const bool ok = q < B_TOT && n < a.N && kok;
+      rb[i] = ok ? ld16(a.wt + ((long)n * RS + tf) * a.sc + c) : zero;
     }
+    advance();
   };
   auto store = [&]() {
 #pragma unroll
@@ -167,12 +193,12 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
   if (ksteps > 0) {
-    load(0);
+    load();
     store();
     __syncthreads();
   }
   for (int t = 0; t < ksteps; ++t) {
-    if (t + 1 < ksteps) load(t + 1);
+    if (t + 1 < ksteps) load();
 #pragma unroll
     for (int kk = 0; kk < CBK / 32; ++kk) {
       bf16x8 fa[TM], fb[TN];
@@ -238,6 +264,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     }
   }
   if (a.stats) {  // fixed-order reduction over the row groups of each column
+    __syncthreads();  // every thread is done reading the output image that `red` aliases
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       red[0][orow][oc * 8 + e] = s1[e];

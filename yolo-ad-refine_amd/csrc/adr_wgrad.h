@@ -3,6 +3,16 @@
 #include "adr_common.h"
 
 namespace adr {
+// sub-steps per WGRAD k-step for a BM x BN tile: enough that a wave issues ~32 MFMAs between barriers, at
+// most 128 reduction rows per step
+__host__ __device__ constexpr int wg_ku(int bm, int bn) {
+  const int wm = bm / 16 < 2 ? bm / 16 : 2, wn = bn / 16 < 2 ? bn / 16 : 2;
+  const int wk = 4 / (wm * wn), tm = bm / wm / 16, tn = bn / wn / 16;
+  (void)tm;
+  (void)tn;
+  (void)wk;
+  return 1;  // measured: deeper k-steps (2-4 sub-steps) are neutral on the 80x80 shapes and cost splits on 20x20
+}
 struct WgPlan {
   int bm, bn, R, tiles, splits;
   long per;  // reduction rows per split (multiple of R)

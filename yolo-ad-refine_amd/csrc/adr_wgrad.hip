@@ -44,7 +44,8 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
   constexpr int WM = BM / 16 < 2 ? BM / 16 : 2;
   constexpr int WN = BN / 16 < 2 ? BN / 16 : 2;
   constexpr int WK = 4 / (WM * WN);
-  constexpr int R = 32 * WK;  // reduction rows per k-step
+  constexpr int KU = wg_ku(BM, BN);  // 32*WK-row sub-steps per k-step (>= ~16-32 MFMAs per wave per barrier)
+  constexpr int R = 32 * WK * KU;    // reduction rows per k-step
   constexpr int WROWS = BM / WM, WCOLS = BN / WN;
   constexpr int TM = WROWS / 16, TN = WCOLS / 16;
   // row pitch (elements): odd multiple of 16 elements (32 bytes)
@@ -74,6 +75,19 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
 
   u32x4 ra[A_CH], rb[B_CH];
   const u32x4 zero = {0u, 0u, 0u, 0u};
+  // per B chunk: the output pixel (img, oy, ox) of its reduction row, advanced by R rows per k-step without
+  // integer division (the row of a chunk is fixed across steps: pl = q / (BN / 8))
+  int b_img[B_CH], b_oy[B_CH], b_ox[B_CH];
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) {
+    const int q = tid + 256 * i;
+    const long p = pbeg + q / (BN / 8);
+    const int pi = (int)(p < a.red_total ? p : 0);
+    b_img[i] = pi / hw;
+    const int rem = pi - b_img[i] * hw;
+    b_oy[i] = rem / a.wo;
+    b_ox[i] = rem - b_oy[i] * a.wo;
+  }
 
   auto load = [&](int t) {
     const long p0 = pbeg + (long)t * R;
@@ -93,12 +107,17 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
       const long p = p0 + pl;
       const int ci = c0 + cc * 8;
       bool ok = q < B_CHT && p < pend && ci < a.c;
-      const long pp = ok ? p : 0;
-      const int img = (int)(pp / hw), rem = (int)(pp % hw);
-      const int oy = rem / a.wo, ox = rem % a.wo;
-      const int iy = oy * a.sh - a.ph + kh, ix = ox * a.sw - a.pw + kw;
+      const int iy = b_oy[i] * a.sh - a.ph + kh, ix = b_ox[i] * a.sw - a.pw + kw;
       ok = ok && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
-      rb[i] = ok ? ld16(a.x + ((long)(img * a.h + iy) * a.w + ix) * a.xcs + a.xco + ci) : zero;
+      rb[i] = ok ? ld16(a.x + ((long)(b_img[i] * a.h + iy) * a.w + ix) * a.xcs + a.xco + ci) : zero;
+      b_ox[i] += R;  // next k-step's row
+      while (b_ox[i] >= a.wo) {
+        b_ox[i] -= a.wo;
+        if (++b_oy[i] >= a.ho) {
+          b_oy[i] = 0;
+          ++b_img[i];
+        }
+      }
     }
   };
   auto store = [&]() {
@@ -134,25 +153,31 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
   }
   for (int t = 0; t < ksteps; ++t) {
     if (t + 1 < ksteps) load(t + 1);
-    bf16x8 fa[TM], fb[TN];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      v4s lo = tr_read(a_base + i * 16);
-      v4s hi = tr_read(a_base + 16 * PA + i * 16);
-      v4s both[2] = {lo, hi};
-      fa[i] = *reinterpret_cast<bf16x8*>(both);
+    for (int u = 0; u < KU; ++u) {
+      const __bf16* ab = a_base + u * 32 * WK * PA;
+      const __bf16* bb = b_base + u * 32 * WK * PB;
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        v4s lo = tr_read(ab + i * 16);
+        v4s hi = tr_read(ab + 16 * PA + i * 16);
+        v4s both[2] = {lo, hi};
+        fa[i] = *reinterpret_cast<bf16x8*>(both);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        v4s lo = tr_read(bb + j * 16);
+        v4s hi = tr_read(bb + 16 * PB + j * 16);
+        v4s both[2] = {lo, hi};
+        fb[j] = *reinterpret_cast<bf16x8*>(both);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      v4s lo = tr_read(b_base + j * 16);
-      v4s hi = tr_read(b_base + 16 * PB + j * 16);
-      v4s both[2] = {lo, hi};
-      fb[j] = *reinterpret_cast<bf16x8*>(both);
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     __syncthreads();
     if (t + 1 < ksteps) {
       store();
@@ -222,7 +247,7 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   p.bm = wg_pick16(d->k);
   p.bn = wg_pick16(d->c);
   const int wm = p.bm / 16 < 2 ? p.bm / 16 : 2, wn = p.bn / 16 < 2 ? p.bn / 16 : 2;
-  p.R = 32 * (4 / (wm * wn));
+  p.R = 32 * (4 / (wm * wn)) * wg_ku(p.bm, p.bn);
   const long red = (long)d->n * d->ho * d->wo;
   const long outsz = (long)d->k * d->r * d->s * d->c;
   p.tiles = cdiv(d->k, p.bm) * d->r * d->s * cdiv(d->c, p.bn);
