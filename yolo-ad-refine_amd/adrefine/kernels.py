@@ -265,11 +265,10 @@ def _conv_work(d):
 
 
 def _engine2(d, red_channels):
-    """Route a bf16 contraction to the BK-64 engine (adr_conv.hip) unless it is a stride-1 multi-tap conv whose
-    reduction channels fill whole 64-wide steps, where the generic engine's shallower tiles measure faster."""
-    if d.dtype != BF16:
-        return False
-    return d.r * d.s == 1 or d.stride_h == 2 or red_channels % 64 != 0
+    """Every bf16 contraction runs on the BK-64 engine (adr_conv.hip); with its division-free tap decoder it
+    measures faster than the generic engine on every shape of the step (scripts/conv_s1.sh, conv_shapes.sh).
+    Anisotropic stride / padding (the ELA 7x1 Conv1d) stays on the generic engine."""
+    return d.dtype == BF16 and d.stride_h == d.stride_w and d.pad_h == d.pad_w
 
 
 def _conv2_symbol(bn, mode):

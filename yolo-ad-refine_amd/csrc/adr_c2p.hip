@@ -128,6 +128,50 @@ __global__ void __launch_bounds__(256) dw_bwd_w_kernel(const T* x, int xcs, cons
   }
 }
 
+// Whole-image depthwise weight gradient: block per (image, CB-channel slab). The zero-padded input image and
+// dy are staged in LDS once; each thread then accumulates (tap, channel pair) sums over all pixels from LDS.
+// partial[n][t][c]; the fixed-order reduce over images follows (dw_w_reduce_kernel with chunks = N).
+template <typename T, int CB>
+__global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, const T* dy, int dcs, int H, int W,
+                                                           int C, int k, float* partial) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
+  const int n = blockIdx.x, cb0 = blockIdx.y * CB, p = k / 2;
+  const int Hp = H + 2 * p, Wp = W + 2 * p;
+  T* xs = reinterpret_cast<T*>(dwsm);
+  T* ds = xs + (long)Hp * Wp * CB;
+  const T* xb = x + (long)n * H * W * xcs;
+  const T* db = dy + (long)n * H * W * dcs;
+  for (int i = threadIdx.x; i < Hp * Wp * CB; i += 256) {
+    const int pp = i / CB, c = i % CB;
+    const int yy = pp / Wp - p, xx = pp % Wp - p;
+    float v = 0.f;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W && cb0 + c < C) v = to_f(xb[((long)yy * W + xx) * xcs + cb0 + c]);
+    xs[i] = from_f<T>(v);
+  }
+  for (int i = threadIdx.x; i < H * W * CB; i += 256) {
+    const int pp = i / CB, c = i % CB;
+    ds[i] = from_f<T>(cb0 + c < C ? to_f(db[(long)pp * dcs + cb0 + c]) : 0.f);
+  }
+  __syncthreads();
+  const int kk = k * k;
+  for (int pr = threadIdx.x; pr < kk * (CB / 2); pr += 256) {
+    const int t = pr / (CB / 2), c = 2 * (pr % (CB / 2));
+    const int ky = t / k, kx = t % k;
+    float a0 = 0.f, a1 = 0.f;
+    for (int y = 0; y < H; ++y) {
+      const T* dr = ds + (long)y * W * CB + c;
+      const T* xr = xs + ((long)(y + ky) * Wp + kx) * CB + c;
+      for (int xx = 0; xx < W; ++xx) {
+        a0 += to_f(dr[xx * CB]) * to_f(xr[xx * CB]);
+        a1 += to_f(dr[xx * CB + 1]) * to_f(xr[xx * CB + 1]);
+      }
+    }
+    float* o = partial + ((long)n * kk + t) * C + cb0 + c;
+    if (cb0 + c < C) o[0] = a0;
+    if (cb0 + c + 1 < C) o[1] = a1;
+  }
+}
+
 // dw[c][t] = sum_chunks partial[chunk][t][c]
 __global__ void dw_w_reduce_kernel(const float* partial, int chunks, int C, int kk, float* dw, int accumulate) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -268,172 +312,183 @@ __global__ void adyt_alpha_kernel(const float* dan, const float* imp, int N, flo
 
 // ---------------- TSSA (one block per (image, head)) ----------------
 // q/k/v: [b][tok][*] rows with channel stride cs; head h uses channels [h*D, (h+1)*D) of each
-template <typename T>
-__global__ void __launch_bounds__(256) tssa_fwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok, int D,
+// Per-(image, head) block; threads = TPP tokens x LD lanes, a lane holding VW consecutive channels of the head
+// (D = LD * VW): every q/k/v/dout access is a 16-byte vector, per-token sums over d are LD-lane xor shuffles,
+// per-channel sums over tokens go through one LDS pass (chan_sum).
+template <typename T, int VW, int LD>
+__global__ void __launch_bounds__(256) tssa_fwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok,
                                                        const float* temp, T* out, int ocs, int oimg, int heads,
                                                        float* Pi_out, float* ss_out, float* attn_out) {
-  int b = blockIdx.x / heads, h = blockIdx.x % heads;
-  extern __shared__ float sm[];
-  float* Pi = sm;             // Ntok
-  float* red = sm + Ntok;     // 256
-  float* dots = red + 256;    // D
-  float tp = temp[h];
-  const long base = (long)b * Ntok;
-  // pass 1: ss and logits
+  constexpr int TPP = 256 / LD, D = LD * VW;
+  extern __shared__ float Pi[];  // Ntok
+  __shared__ float red[256 * VW];
+  __shared__ float at[D];
+  __shared__ float sh[256];
+  const int b = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int lane = threadIdx.x % LD, r0 = threadIdx.x / LD, c0 = h * D + lane * VW;
+  const long base = (long)b * Ntok, bh = (long)b * heads + h;
+  const float tp = temp[h];
+  // pass 1: ss = sum_d (q / max(|q|, eps))^2 and the logits
   float mx = -INFINITY;
-  for (int n = threadIdx.x; n < Ntok; n += 256) {
-    const T* qr = q + (base + n) * cs + h * D;
+  for (int n = r0; n < Ntok; n += TPP) {
+    float qv[VW];
+    vload<T, VW>(q + (base + n) * cs + c0, qv);
     float s2 = 0.f;
-    for (int d = 0; d < D; ++d) {
-      float t = to_f(qr[d]);
-      s2 += t * t;
+#pragma unroll
+    for (int e = 0; e < VW; ++e) s2 += qv[e] * qv[e];
+    const float r = fmaxf(sqrtf(tok_sum<LD>(s2)), 1e-12f);
+    float ssp = 0.f;
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      const float t = qv[e] / r;
+      ssp += t * t;
     }
-    float r = fmaxf(sqrtf(s2), 1e-12f);
-    float ss = 0.f;
-    for (int d = 0; d < D; ++d) {
-      float t = to_f(qr[d]) / r;
-      ss += t * t;
+    const float ss = tok_sum<LD>(ssp);
+    if (lane == 0) {
+      ss_out[bh * Ntok + n] = ss;
+      Pi[n] = ss * tp;
     }
-    ss_out[((long)b * heads + h) * Ntok + n] = ss;
-    float l = ss * tp;
-    Pi[n] = l;
-    mx = fmaxf(mx, l);
+    mx = fmaxf(mx, ss * tp);
   }
-  red[threadIdx.x] = mx;
+  sh[threadIdx.x] = mx;
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    if (threadIdx.x < o) sh[threadIdx.x] = fmaxf(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
-  mx = red[0];
+  mx = sh[0];
   __syncthreads();
   float z = 0.f;
   for (int n = threadIdx.x; n < Ntok; n += 256) {
-    float e = __expf(Pi[n] - mx);
+    const float e = __expf(Pi[n] - mx);
     Pi[n] = e;
     z += e;
   }
-  red[threadIdx.x] = z;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  z = red[0];
-  __syncthreads();
+  z = block_sum256(z, sh);
   for (int n = threadIdx.x; n < Ntok; n += 256) {
     Pi[n] /= z;
-    Pi_out[((long)b * heads + h) * Ntok + n] = Pi[n];
+    Pi_out[bh * Ntok + n] = Pi[n];
   }
   __syncthreads();
   // pass 2: dots[d] = sum_n Pi k^2 -> attn
-  for (int d = threadIdx.x; d < D; d += 256) {
-    float s = 0.f;
-    for (int n = 0; n < Ntok; ++n) {
-      float t = to_f(k[(base + n) * cs + h * D + d]);
-      s += Pi[n] * t * t;
-    }
-    float a = 1.f / (1.f + s);
-    dots[d] = a;
-    attn_out[((long)b * heads + h) * D + d] = a;
+  float p[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) p[e] = 0.f;
+  for (int n = r0; n < Ntok; n += TPP) {
+    float kv[VW];
+    vload<T, VW>(k + (base + n) * cs + c0, kv);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) p[e] += Pi[n] * kv[e] * kv[e];
+  }
+  chan_sum<VW, LD>(p, red, at);
+  if (threadIdx.x < D) {
+    const float a = 1.f / (1.f + at[threadIdx.x]);
+    at[threadIdx.x] = a;
+    attn_out[bh * D + threadIdx.x] = a;
   }
   __syncthreads();
   // pass 3: out = -v * Pi * attn
-  for (long i = threadIdx.x; i < (long)Ntok * D; i += 256) {
-    int n = (int)(i / D), d = (int)(i % D);
-    float vv = to_f(v[(base + n) * cs + h * D + d]);
-    out[((long)b * oimg + n) * ocs + h * D + d] = from_f<T>(-vv * Pi[n] * dots[d]);
+  for (int n = r0; n < Ntok; n += TPP) {
+    float vv[VW];
+    vload<T, VW>(v + (base + n) * cs + c0, vv);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) vv[e] = -vv[e] * Pi[n] * at[lane * VW + e];
+    vstore<T, VW>(out + ((long)b * oimg + n) * ocs + c0, vv);
   }
 }
 
-template <typename T>
-__global__ void __launch_bounds__(256) tssa_bwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok, int D,
+template <typename T, int VW, int LD>
+__global__ void __launch_bounds__(256) tssa_bwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok,
                                                        const float* temp, const T* dout, int dcs, int dimg, int heads,
                                                        const float* Pi_in, const float* ss_in, const float* attn_in,
                                                        T* dq, T* dk, T* dv, int gcs, float* dtemp_part) {
-  int b = blockIdx.x / heads, h = blockIdx.x % heads;
-  extern __shared__ float sm[];
-  float* dPi = sm;              // Ntok
-  float* red = sm + Ntok;       // 256
-  float* dattn = red + 256;     // D
-  float* ddots = dattn + D;     // D
-  const long base = (long)b * Ntok;
-  const float* Pi = Pi_in + ((long)b * heads + h) * Ntok;
-  const float* ss = ss_in + ((long)b * heads + h) * Ntok;
-  const float* attn = attn_in + ((long)b * heads + h) * D;
-  float tp = temp[h];
+  constexpr int TPP = 256 / LD, D = LD * VW;
+  extern __shared__ float dPi[];  // Ntok
+  __shared__ float red[256 * VW];
+  __shared__ float dd[D];
+  __shared__ float sh[256];
+  const int b = blockIdx.x / heads, h = blockIdx.x % heads;
+  const int lane = threadIdx.x % LD, r0 = threadIdx.x / LD, c0 = h * D + lane * VW;
+  const long base = (long)b * Ntok, bh = (long)b * heads + h;
+  const float* Pi = Pi_in + bh * Ntok;
+  const float* ss = ss_in + bh * Ntok;
+  const float* attn = attn_in + bh * D;
+  const float tp = temp[h];
+  float at[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) at[e] = attn[lane * VW + e];
   // dattn[d] = sum_n -dout v Pi ; dv = -dout Pi attn
-  for (int d = threadIdx.x; d < D; d += 256) {
-    float s = 0.f;
-    for (int n = 0; n < Ntok; ++n) {
-      float go = to_f(dout[((long)b * dimg + n) * dcs + h * D + d]);
-      float vv = to_f(v[(base + n) * cs + h * D + d]);
-      s += -go * vv * Pi[n];
-      dv[(base + n) * gcs + h * D + d] = from_f<T>(-go * Pi[n] * attn[d]);
+  float p[VW];
+#pragma unroll
+  for (int e = 0; e < VW; ++e) p[e] = 0.f;
+  for (int n = r0; n < Ntok; n += TPP) {
+    float g[VW], vv[VW], o[VW];
+    vload<T, VW>(dout + ((long)b * dimg + n) * dcs + c0, g);
+    vload<T, VW>(v + (base + n) * cs + c0, vv);
+    const float pn = Pi[n];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      p[e] -= g[e] * vv[e] * pn;
+      o[e] = -g[e] * pn * at[e];
     }
-    dattn[d] = s;
-    ddots[d] = -s * attn[d] * attn[d];
+    vstore<T, VW>(dv + (base + n) * gcs + c0, o);
   }
+  chan_sum<VW, LD>(p, red, dd);
+  if (threadIdx.x < D) dd[threadIdx.x] = -dd[threadIdx.x] * attn[threadIdx.x] * attn[threadIdx.x];  // ddots
   __syncthreads();
-  // dPi[n] = sum_d (-dout v attn) + sum_d ddots k^2 ; dk = ddots * Pi * 2k
+  // dPi[n] = sum_d (-dout v attn + ddots k^2) ; dk = ddots * Pi * 2k
   float part = 0.f;
-  for (int n = threadIdx.x; n < Ntok; n += 256) {
-    float s = 0.f;
-    for (int d = 0; d < D; ++d) {
-      float go = to_f(dout[((long)b * dimg + n) * dcs + h * D + d]);
-      float vv = to_f(v[(base + n) * cs + h * D + d]);
-      float kk = to_f(k[(base + n) * cs + h * D + d]);
-      s += -go * vv * attn[d] + ddots[d] * kk * kk;
-      dk[(base + n) * gcs + h * D + d] = from_f<T>(ddots[d] * Pi[n] * 2.f * kk);
+  for (int n = r0; n < Ntok; n += TPP) {
+    float g[VW], vv[VW], kv[VW], o[VW];
+    vload<T, VW>(dout + ((long)b * dimg + n) * dcs + c0, g);
+    vload<T, VW>(v + (base + n) * cs + c0, vv);
+    vload<T, VW>(k + (base + n) * cs + c0, kv);
+    const float pn = Pi[n];
+    float sp = 0.f;
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      const float ddv = dd[lane * VW + e];
+      sp += -g[e] * vv[e] * at[e] + ddv * kv[e] * kv[e];
+      o[e] = ddv * pn * 2.f * kv[e];
     }
-    dPi[n] = s;
-    part += Pi[n] * s;
+    vstore<T, VW>(dk + (base + n) * gcs + c0, o);
+    const float s = tok_sum<LD>(sp);
+    if (lane == 0) {
+      dPi[n] = s;
+      part += pn * s;
+    }
   }
-  red[threadIdx.x] = part;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  float dot = red[0];
-  __syncthreads();
+  const float dot = block_sum256(part, sh);
   // softmax backward -> dl ; dtemp partial ; dss -> dq
   float tpart = 0.f;
-  for (int n = threadIdx.x; n < Ntok; n += 256) {
-    float dl = Pi[n] * (dPi[n] - dot);
-    tpart += dl * ss[n];
-    float dss = dl * tp;
-    const T* qr = q + (base + n) * cs + h * D;
+  for (int n = r0; n < Ntok; n += TPP) {
+    const float dl = Pi[n] * (dPi[n] - dot);
+    if (lane == 0) tpart += dl * ss[n];
+    const float dss = dl * tp;
+    float qv[VW];
+    vload<T, VW>(q + (base + n) * cs + c0, qv);
     float s2 = 0.f;
-    for (int d = 0; d < D; ++d) {
-      float t = to_f(qr[d]);
-      s2 += t * t;
-    }
-    float nrm = sqrtf(s2);
-    float r = fmaxf(nrm, 1e-12f);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) s2 += qv[e] * qv[e];
+    const float nrm = sqrtf(tok_sum<LD>(s2));
+    const float r = fmaxf(nrm, 1e-12f);
     // dqn = 2 qn dss ; dq = dqn / r - (nrm > eps) * q (q . dqn) / r^3
-    float qdq = 0.f;
-    for (int d = 0; d < D; ++d) {
-      float t = to_f(qr[d]);
-      qdq += t * (2.f * (t / r) * dss);
+    float qp = 0.f;
+#pragma unroll
+    for (int e = 0; e < VW; ++e) qp += qv[e] * (2.f * (qv[e] / r) * dss);
+    const float qdq = tok_sum<LD>(qp);
+    float o[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) {
+      const float dqn = 2.f * (qv[e] / r) * dss;
+      o[e] = dqn / r - (nrm > 1e-12f ? qv[e] * qdq / (r * r * r) : 0.f);
     }
-    for (int d = 0; d < D; ++d) {
-      float t = to_f(qr[d]);
-      float dqn = 2.f * (t / r) * dss;
-      float g = dqn / r - (nrm > 1e-12f ? t * qdq / (r * r * r) : 0.f);
-      dq[(base + n) * gcs + h * D + d] = from_f<T>(g);
-    }
+    vstore<T, VW>(dq + (base + n) * gcs + c0, o);
   }
-  red[threadIdx.x] = tpart;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) dtemp_part[(long)b * heads + h] = red[0];
+  tpart = block_sum256(tpart, sh);
+  if (threadIdx.x == 0) dtemp_part[bh] = tpart;
 }
 
-// dtemp[s][h] = sum_b part[b][h]
 __global__ void tssa_temp_reduce_kernel(const float* part, int B, int heads, float* dtemp) {
   int h = threadIdx.x;
   if (h >= heads) return;
@@ -640,9 +695,17 @@ extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w,
   return check_launch("adr_dwconv_fwd");
 }
 
+static constexpr int DW_CB_BF16 = 16, DW_CB_F32 = 8;
+static size_t dw_img_smem(int dtype, int H, int W, int k) {
+  const int p = k / 2;
+  const size_t cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
+  return ((size_t)(H + 2 * p) * (W + 2 * p) + (size_t)H * W) * cb * es;
+}
+
 extern "C" size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k) {
   long npix = (long)N * H * W;
   int chunks = cdiv(npix, 1024);
+  if (chunks < N) chunks = N;  // the whole-image kernel writes one partial row per image
   return (size_t)chunks * k * k * C * sizeof(float);
 }
 
@@ -668,7 +731,16 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
     long npix = (long)N * H * W;
     int chunks = cdiv(npix, 1024);
     dim3 g(chunks, k * k);
-    if (dtype == ADR_BF16)
+    const size_t ism = dw_img_smem(dtype, H, W, k);
+    if (ism <= 64 * 1024) {  // small maps (the 20x20 C2PTSSA / EDFFN / Mona path): whole image in LDS
+      chunks = N;
+      if (dtype == ADR_BF16)
+        hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), ism, st,
+                           (const __bf16*)x, xcs, (const __bf16*)dy, dcs, H, W, C, k, ws);
+      else
+        hipLaunchKernelGGL((dw_wgrad_img_kernel<float, DW_CB_F32>), dim3(N, cdiv(C, DW_CB_F32)), dim3(256), ism, st,
+                           (const float*)x, xcs, (const float*)dy, dcs, H, W, C, k, ws);
+    } else if (dtype == ADR_BF16)
       hipLaunchKernelGGL(dw_bwd_w_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dy, dcs, N,
                          H, W, C, k, 1024, ws);
     else
@@ -721,14 +793,17 @@ extern "C" int adr_tssa_fwd(int dtype, const void* q, const void* k, const void*
                             int D, const float* temp, void* out, int ocs, int oimg, float* Pi, float* ss, float* attn,
                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  size_t sm = (Ntok + 256 + D) * sizeof(float);
+  const int vw = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(D == 64 && cs % vw == 0 && ocs % vw == 0, "tssa: head dim %d (64 supported) / strides", D);
+  const size_t sm = Ntok * sizeof(float);
   ADR_REQUIRE(sm <= 64 * 1024, "tssa: Ntok=%d too large", Ntok);
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(tssa_fwd_kernel<__bf16>, dim3(B * heads), dim3(256), sm, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, cs, Ntok, D, temp, (__bf16*)out, ocs, oimg, heads, Pi, ss, attn);
+    hipLaunchKernelGGL((tssa_fwd_kernel<__bf16, 8, 8>), dim3(B * heads), dim3(256), sm, st, (const __bf16*)q,
+                       (const __bf16*)k, (const __bf16*)v, cs, Ntok, temp, (__bf16*)out, ocs, oimg, heads, Pi, ss,
+                       attn);
   else
-    hipLaunchKernelGGL(tssa_fwd_kernel<float>, dim3(B * heads), dim3(256), sm, st, (const float*)q, (const float*)k,
-                       (const float*)v, cs, Ntok, D, temp, (float*)out, ocs, oimg, heads, Pi, ss, attn);
+    hipLaunchKernelGGL((tssa_fwd_kernel<float, 4, 16>), dim3(B * heads), dim3(256), sm, st, (const float*)q,
+                       (const float*)k, (const float*)v, cs, Ntok, temp, (float*)out, ocs, oimg, heads, Pi, ss, attn);
   return check_launch("adr_tssa_fwd");
 }
 
@@ -738,16 +813,18 @@ extern "C" int adr_tssa_bwd(int dtype, const void* q, const void* k, const void*
                             const float* attn, void* dq, void* dk, void* dv, int gcs, float* dtemp, float* ws,
                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  size_t sm = (Ntok + 256 + 2 * D) * sizeof(float);
+  const int vw = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(D == 64 && cs % vw == 0 && dcs % vw == 0 && gcs % vw == 0, "tssa_bwd: head dim %d / strides", D);
+  const size_t sm = Ntok * sizeof(float);
+  ADR_REQUIRE(sm <= 64 * 1024, "tssa_bwd: Ntok=%d too large", Ntok);
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(tssa_bwd_kernel<__bf16>, dim3(B * heads), dim3(256), sm, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, cs, Ntok, D, temp, (const __bf16*)dout, dcs, dimg, heads, Pi, ss, attn,
-                       (__bf16*)dq,
-                       (__bf16*)dk, (__bf16*)dv, gcs, ws);
+    hipLaunchKernelGGL((tssa_bwd_kernel<__bf16, 8, 8>), dim3(B * heads), dim3(256), sm, st, (const __bf16*)q,
+                       (const __bf16*)k, (const __bf16*)v, cs, Ntok, temp, (const __bf16*)dout, dcs, dimg, heads, Pi,
+                       ss, attn, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, gcs, ws);
   else
-    hipLaunchKernelGGL(tssa_bwd_kernel<float>, dim3(B * heads), dim3(256), sm, st, (const float*)q, (const float*)k,
-                       (const float*)v, cs, Ntok, D, temp, (const float*)dout, dcs, dimg, heads, Pi, ss, attn, (float*)dq,
-                       (float*)dk, (float*)dv, gcs, ws);
+    hipLaunchKernelGGL((tssa_bwd_kernel<float, 4, 16>), dim3(B * heads), dim3(256), sm, st, (const float*)q,
+                       (const float*)k, (const float*)v, cs, Ntok, temp, (const float*)dout, dcs, dimg, heads, Pi, ss,
+                       attn, (float*)dq, (float*)dk, (float*)dv, gcs, ws);
   hipLaunchKernelGGL(tssa_temp_reduce_kernel, dim3(1), dim3(64), 0, st, ws, B, heads, dtemp);
   return check_launch("adr_tssa_bwd");
 }

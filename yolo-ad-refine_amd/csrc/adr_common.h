@@ -172,6 +172,45 @@ struct PoolLanes {
   for (long pix = (long)blockIdx.x * (L).rpb + (L).r0; pix < (npix); pix += (long)gridDim.x * (L).rpb) \
     for (int cg = (L).cg0; cg < (G); cg += (L).cstep)
 
+// ---- token x channel-group lane layouts (LD lanes per token, VW channels per lane, 256 threads) ----
+template <int LD>
+__device__ __forceinline__ float tok_sum(float v) {
+#pragma unroll
+  for (int o = LD / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// block-wide sum of one float per thread (256 threads), result broadcast
+__device__ __forceinline__ float block_sum256(float v, float* sh) {
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float r = sh[0];
+  __syncthreads();
+  return r;
+}
+
+// per-channel (d) sum over the block's token rows: red has 256 * VW floats; result in dsum[D]
+template <int VW, int LD>
+__device__ __forceinline__ void chan_sum(const float* part, float* red, float* dsum) {
+  constexpr int TPP = 256 / LD;
+  const int lane = threadIdx.x % LD;
+#pragma unroll
+  for (int e = 0; e < VW; ++e) red[threadIdx.x * VW + e] = part[e];
+  __syncthreads();
+  for (int d = threadIdx.x; d < LD * VW; d += 256) {
+    const int ln = d / VW, e = d % VW;
+    float t = 0.f;
+    for (int r = 0; r < TPP; ++r) t += red[(r * LD + ln) * VW + e];
+    dsum[d] = t;
+  }
+  (void)lane;
+  __syncthreads();
+}
+
 inline int cdiv(long a, long b) { return (int)((a + b - 1) / b); }
 
 // wave-level sum (64 lanes)
