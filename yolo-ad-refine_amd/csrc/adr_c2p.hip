@@ -128,47 +128,129 @@ __global__ void __launch_bounds__(256) dw_bwd_w_kernel(const T* x, int xcs, cons
   }
 }
 
-// Whole-image depthwise weight gradient: block per (image, CB-channel slab). The zero-padded input image and
-// dy are staged in LDS once; each thread then accumulates (tap, channel pair) sums over all pixels from LDS.
-// partial[n][t][c]; the fixed-order reduce over images follows (dw_w_reduce_kernel with chunks = N).
+// Whole-image depthwise kernels for small maps (the 20x20 C2PTSSA / EDFFN / Mona path): block per (image,
+// CB-channel slab); the zero-padded input image (and dy) are staged once in LDS as bf16/fp32 rows of CB
+// channels, every LDS access is one 16-byte vector of VW channels.
+template <typename T>
+__device__ __forceinline__ void stage_img(const T* src, int cs, int H, int W, int pad, int cb0, int C, int CB, T* dst) {
+  constexpr int VW = 16 / sizeof(T);
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad, nv = CB / VW;
+  for (int i = threadIdx.x; i < Hp * Wp * nv; i += blockDim.x) {
+    const int pp = i / nv, cv = i % nv;
+    const int yy = pp / Wp - pad, xx = pp % Wp - pad;
+    const int c = cb0 + cv * VW;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W && c < C) v = ld16(src + ((long)yy * W + xx) * cs + c);
+    *reinterpret_cast<u32x4*>(dst + (long)pp * CB + cv * VW) = v;
+  }
+}
+
+// y = dwconv(x, w) (+b) or dx (+)= dwconv^T(dy, w): items (pixel, VW-channel vector), taps from the LDS image
+template <typename T, bool BWD, int CB>
+__global__ void __launch_bounds__(256) dw_img_kernel(const T* x, int xcs, const float* w, const float* b, T* y,
+                                                     int ycs, int H, int W, int C, int k, int accumulate) {
+  constexpr int VW = 16 / sizeof(T), NV = CB / VW;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
+  const int n = blockIdx.x, cb0 = blockIdx.y * CB, p = k / 2, kk = k * k;
+  const int Wp = W + 2 * p;
+  float* wl = reinterpret_cast<float*>(dwsm);                        // [kk][CB]
+  T* xs = reinterpret_cast<T*>(dwsm + (size_t)kk * CB * sizeof(float));
+  for (int i = threadIdx.x; i < kk * CB; i += 256) {
+    const int t = i / CB, c = cb0 + i % CB;
+    wl[i] = c < C ? w[(long)c * kk + t] : 0.f;
+  }
+  stage_img<T>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
+  __syncthreads();
+  for (int it = threadIdx.x; it < H * W * NV; it += 256) {
+    const int pix = it / NV, cv = it % NV, c = cb0 + cv * VW;
+    if (c >= C) continue;
+    const int oy = pix / W, ox = pix % W;
+    float acc[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) acc[e] = (!BWD && b) ? b[c + e] : 0.f;
+    for (int ky = 0; ky < k; ++ky)
+      for (int kx = 0; kx < k; ++kx) {
+        // forward: x[oy + ky - p][ox + kx - p] = padded row oy + ky; data gradient: taps mirrored
+        const int py = BWD ? oy + 2 * p - ky : oy + ky, px = BWD ? ox + 2 * p - kx : ox + kx;
+        const u32x4 v = *reinterpret_cast<const u32x4*>(xs + ((long)py * Wp + px) * CB + cv * VW);
+        const T* e8 = reinterpret_cast<const T*>(&v);
+        const float* wt = wl + (ky * k + kx) * CB + cv * VW;
+#pragma unroll
+        for (int e = 0; e < VW; ++e) acc[e] += to_f(e8[e]) * wt[e];
+      }
+    T* dst = y + ((long)n * H * W + pix) * ycs + c;
+    if (BWD && accumulate) {
+      const u32x4 pv = ld16(dst);
+      const T* pe = reinterpret_cast<const T*>(&pv);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) acc[e] += to_f(pe[e]);
+    }
+    u32x4 o;
+    T* oe = reinterpret_cast<T*>(&o);
+#pragma unroll
+    for (int e = 0; e < VW; ++e) oe[e] = from_f<T>(acc[e]);
+    st16(dst, o);
+  }
+}
+
+// weight gradient: items (tap, VW-channel vector, pixel split PS), partial sums combined in LDS in fixed order;
+// partial[n][t][c]
 template <typename T, int CB>
 __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, const T* dy, int dcs, int H, int W,
                                                            int C, int k, float* partial) {
+  constexpr int VW = 16 / sizeof(T), NV = CB / VW;
   extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
-  const int n = blockIdx.x, cb0 = blockIdx.y * CB, p = k / 2;
+  const int n = blockIdx.x, cb0 = blockIdx.y * CB, p = k / 2, kk = k * k;
   const int Hp = H + 2 * p, Wp = W + 2 * p;
   T* xs = reinterpret_cast<T*>(dwsm);
   T* ds = xs + (long)Hp * Wp * CB;
-  const T* xb = x + (long)n * H * W * xcs;
-  const T* db = dy + (long)n * H * W * dcs;
-  for (int i = threadIdx.x; i < Hp * Wp * CB; i += 256) {
-    const int pp = i / CB, c = i % CB;
-    const int yy = pp / Wp - p, xx = pp % Wp - p;
-    float v = 0.f;
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W && cb0 + c < C) v = to_f(xb[((long)yy * W + xx) * xcs + cb0 + c]);
-    xs[i] = from_f<T>(v);
-  }
-  for (int i = threadIdx.x; i < H * W * CB; i += 256) {
-    const int pp = i / CB, c = i % CB;
-    ds[i] = from_f<T>(cb0 + c < C ? to_f(db[(long)pp * dcs + cb0 + c]) : 0.f);
-  }
+  float* red = reinterpret_cast<float*>(ds + (long)H * W * CB);  // [256][VW]
+  stage_img<T>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
+  stage_img<T>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
   __syncthreads();
-  const int kk = k * k;
-  for (int pr = threadIdx.x; pr < kk * (CB / 2); pr += 256) {
-    const int t = pr / (CB / 2), c = 2 * (pr % (CB / 2));
-    const int ky = t / k, kx = t % k;
-    float a0 = 0.f, a1 = 0.f;
-    for (int y = 0; y < H; ++y) {
-      const T* dr = ds + (long)y * W * CB + c;
-      const T* xr = xs + ((long)(y + ky) * Wp + kx) * CB + c;
-      for (int xx = 0; xx < W; ++xx) {
-        a0 += to_f(dr[xx * CB]) * to_f(xr[xx * CB]);
-        a1 += to_f(dr[xx * CB + 1]) * to_f(xr[xx * CB + 1]);
+  const int pairs = kk * NV;
+  int PS = 1;  // pixel splits per (tap, vector): a power of two, so split groups never straddle a 256 pass
+  while (PS * 2 * pairs <= 256) PS *= 2;
+  for (int base = 0; base < pairs * PS; base += 256) {
+    const int it = base + threadIdx.x;
+    const int pr = it / PS, ps = it % PS;
+    float acc[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) acc[e] = 0.f;
+    if (pr < pairs) {
+      const int t = pr / NV, cv = pr % NV, ky = t / k, kx = t % k;
+      int oy = 0, ox = ps;  // (oy, ox) of pix, stepped by PS without dividing
+      while (ox >= W) {
+        ox -= W;
+        ++oy;
+      }
+      for (int pix = ps; pix < H * W; pix += PS) {
+        const u32x4 dv = *reinterpret_cast<const u32x4*>(ds + (long)pix * CB + cv * VW);
+        const u32x4 xv = *reinterpret_cast<const u32x4*>(xs + ((long)(oy + ky) * Wp + ox + kx) * CB + cv * VW);
+        const T* d8 = reinterpret_cast<const T*>(&dv);
+        const T* x8 = reinterpret_cast<const T*>(&xv);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) acc[e] += to_f(d8[e]) * to_f(x8[e]);
+        ox += PS;
+        while (ox >= W) {
+          ox -= W;
+          ++oy;
+        }
       }
     }
-    float* o = partial + ((long)n * kk + t) * C + cb0 + c;
-    if (cb0 + c < C) o[0] = a0;
-    if (cb0 + c + 1 < C) o[1] = a1;
+#pragma unroll
+    for (int e = 0; e < VW; ++e) red[threadIdx.x * VW + e] = acc[e];
+    __syncthreads();
+    if (ps == 0 && pr < pairs) {
+      const int t = pr / NV, cv = pr % NV, c = cb0 + cv * VW;
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        float s2 = 0.f;
+        for (int q = 0; q < PS; ++q) s2 += red[(threadIdx.x + q) * VW + e];
+        if (c + e < C) partial[((long)n * kk + t) * C + c + e] = s2;
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -612,46 +694,73 @@ __global__ void __launch_bounds__(256) edffn_fold_kernel(const float* dpad, int 
 // Block per channel: lane j accumulates column j of dM over the wave's patches (64 registers, dY broadcast from
 // LDS), the four waves' partials are summed in LDS in a fixed order, and the block contracts dM with the
 // basis in place (no dM round trip through memory).
+// dM partial per (channel, patch split): grid (C, EDFFN_DWS); 4 waves x patch stride, two patches' loads in
+// flight per iteration; part[(split * C + c) * 4096 + e]
+constexpr int EDFFN_DWS = 8;
 template <typename T>
 __global__ void __launch_bounds__(256) edffn_dw_kernel(const T* x, int xcs, const T* dy, int dcs, int N, int H, int W,
-                                                       int C, const float* Bm, int nuv, float* dw, int accumulate) {
-  __shared__ float sdy[4][64];
+                                                       int C, float* part) {
+  __shared__ float sdy[4][2][64];
   __shared__ float dM[4][4096];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, tid = threadIdx.x;
-  const int c = blockIdx.x;
+  const int c = blockIdx.x, sp = blockIdx.y;
   const int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8, npatch = N * ph_n * pw_n;
+  const int per = (npatch + EDFFN_DWS - 1) / EDFFN_DWS, pbeg = sp * per, pend = min(npatch, pbeg + per);
   float acc[64];
 #pragma unroll
   for (int i = 0; i < 64; ++i) acc[i] = 0.f;
   const int dy_ = lane / 8, dx_ = lane % 8;
-  for (int pp = wave; pp < npatch; pp += 4) {
+  auto fetch = [&](int pp, float& xv, float& gv) {
+    xv = 0.f;
+    gv = 0.f;
+    if (pp >= pend) return;
     const int n = pp / (ph_n * pw_n), q = pp % (ph_n * pw_n);
     const int yy = (q / pw_n) * 8 + dy_, xx = (q % pw_n) * 8 + dx_;
-    const float xv = to_f(x[(((long)n * H + reflect_idx(yy, H)) * W + reflect_idx(xx, W)) * xcs + c]);
-    sdy[wave][lane] = (yy < H && xx < W) ? to_f(dy[(((long)n * H + yy) * W + xx) * dcs + c]) : 0.f;
+    xv = to_f(x[(((long)n * H + reflect_idx(yy, H)) * W + reflect_idx(xx, W)) * xcs + c]);
+    gv = (yy < H && xx < W) ? to_f(dy[(((long)n * H + yy) * W + xx) * dcs + c]) : 0.f;
+  };
+  for (int pp = pbeg + wave; pp < pend; pp += 8) {
+    float x0, g0, x1, g1;
+    fetch(pp, x0, g0);
+    fetch(pp + 4, x1, g1);
+    sdy[wave][0][lane] = g0;
+    sdy[wave][1][lane] = g1;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int i = 0; i < 64; i += 4) {
-      const float4 g = *reinterpret_cast<const float4*>(&sdy[wave][i]);
-      acc[i] += g.x * xv;
-      acc[i + 1] += g.y * xv;
-      acc[i + 2] += g.z * xv;
-      acc[i + 3] += g.w * xv;
+      const float4 a = *reinterpret_cast<const float4*>(&sdy[wave][0][i]);
+      const float4 b = *reinterpret_cast<const float4*>(&sdy[wave][1][i]);
+      acc[i] += a.x * x0 + b.x * x1;
+      acc[i + 1] += a.y * x0 + b.y * x1;
+      acc[i + 2] += a.z * x0 + b.z * x1;
+      acc[i + 3] += a.w * x0 + b.w * x1;
     }
     __builtin_amdgcn_wave_barrier();
   }
 #pragma unroll
   for (int i = 0; i < 64; ++i) dM[wave][i * 64 + lane] = acc[i];
   __syncthreads();
-  for (int e = tid; e < 4096; e += 256) dM[0][e] = (dM[0][e] + dM[1][e]) + (dM[2][e] + dM[3][e]);
+  float* out = part + ((long)sp * C + c) * 4096;
+  for (int e = tid; e < 4096; e += 256) out[e] = (dM[0][e] + dM[1][e]) + (dM[2][e] + dM[3][e]);
+}
+
+// dw[c][uv] (+)= sum_e B[uv][e] * sum_split part[split][c][e]: block per channel, fixed order
+__global__ void __launch_bounds__(256) edffn_dw_fin_kernel(const float* part, int C, const float* Bm, int nuv,
+                                                           float* dw, int accumulate) {
+  __shared__ float dM[4096];
+  const int c = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int e = threadIdx.x; e < 4096; e += 256) {
+    float sacc = 0.f;
+    for (int sp = 0; sp < EDFFN_DWS; ++sp) sacc += part[((long)sp * C + c) * 4096 + e];
+    dM[e] = sacc;
+  }
   __syncthreads();
-  // dw[uv] = sum_e B[uv][e] dM[e]: wave per uv (strided), lanes over e, fixed-order wave reduction
   for (int u = wave; u < nuv; u += 4) {
     const float* b = Bm + (long)u * 4096;
-    float s = 0.f;
-    for (int e = lane; e < 4096; e += 64) s += b[e] * dM[0][e];
-    s = wave_sum(s);
-    if (lane == 0) dw[c * nuv + u] = accumulate ? dw[c * nuv + u] + s : s;
+    float sacc = 0.f;
+    for (int e = lane; e < 4096; e += 64) sacc += b[e] * dM[e];
+    sacc = wave_sum(sacc);
+    if (lane == 0) dw[c * nuv + u] = accumulate ? dw[c * nuv + u] + sacc : sacc;
   }
 }
 
@@ -664,6 +773,29 @@ using namespace adr;
     if ((dtype) == ADR_BF16) hipLaunchKernelGGL(KERN<__bf16>, grid, block, sm, st, __VA_ARGS__);         \
     else hipLaunchKernelGGL(KERN<float>, grid, block, sm, st, __VA_ARGS__);                             \
   } while (0)
+
+static constexpr int DW_CB_BF16 = 16, DW_CB_F32 = 8;
+static size_t dw_img_smem(int dtype, int H, int W, int k) {  // weight-gradient kernel
+  const int p = k / 2;
+  const size_t cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
+  return ((size_t)(H + 2 * p) * (W + 2 * p) + (size_t)H * W) * cb * es + 256 * 16;
+}
+static size_t dw_fwd_smem(int dtype, int H, int W, int k) {  // forward / data-gradient kernel
+  const int p = k / 2;
+  const size_t cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
+  return (size_t)k * k * cb * 4 + (size_t)(H + 2 * p) * (W + 2 * p) * cb * es;
+}
+template <bool BWD>
+static void dw_img_launch(int dtype, hipStream_t st, const void* x, int xcs, const float* w, const float* b, void* y,
+                          int ycs, int N, int H, int W, int C, int k, int acc) {
+  const size_t sm = dw_fwd_smem(dtype, H, W, k);
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
+                       (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, H, W, C, k, acc);
+  else
+    hipLaunchKernelGGL((dw_img_kernel<float, BWD, DW_CB_F32>), dim3(N, cdiv(C, DW_CB_F32)), dim3(256), sm, st,
+                       (const float*)x, xcs, w, b, (float*)y, ycs, H, W, C, k, acc);
+}
 
 template <typename T, bool BWD>
 static void dw_launch(int k, dim3 grid, size_t sm, hipStream_t st, const T* x, int xcs, const float* w, const float* b,
@@ -686,20 +818,15 @@ extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w,
   long total = (long)N * H * W * (C / v);
   size_t sm = (size_t)k * k * C * sizeof(float);
   ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
-  if (dtype == ADR_BF16)
+  if (dw_fwd_smem(dtype, H, W, k) <= 64 * 1024 && xcs % v == 0 && ycs % v == 0) {
+    dw_img_launch<false>(dtype, st, x, xcs, w, b, y, ycs, N, H, W, C, k, 0);
+  } else if (dtype == ADR_BF16)
     dw_launch<__bf16, false>(k, dim3(cdiv(total, 256)), sm, st, (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, N, H, W,
                              C, 0);
   else
     dw_launch<float, false>(k, dim3(cdiv(total, 256)), sm, st, (const float*)x, xcs, w, b, (float*)y, ycs, N, H, W, C,
                             0);
   return check_launch("adr_dwconv_fwd");
-}
-
-static constexpr int DW_CB_BF16 = 16, DW_CB_F32 = 8;
-static size_t dw_img_smem(int dtype, int H, int W, int k) {
-  const int p = k / 2;
-  const size_t cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
-  return ((size_t)(H + 2 * p) * (W + 2 * p) + (size_t)H * W) * cb * es;
 }
 
 extern "C" size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k) {
@@ -719,7 +846,9 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
   if (dx) {
     size_t sm = (size_t)k * k * C * sizeof(float);
     ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv_bwd: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
-    if (dtype == ADR_BF16)
+    if (dw_fwd_smem(dtype, H, W, k) <= 64 * 1024 && dcs % v == 0 && ocs % v == 0)
+      dw_img_launch<true>(dtype, st, dy, dcs, w, nullptr, dx, ocs, N, H, W, C, k, accumulate);
+    else if (dtype == ADR_BF16)
       dw_launch<__bf16, true>(k, dim3(cdiv(total, 256)), sm, st, (const __bf16*)dy, dcs, w, nullptr, (__bf16*)dx, ocs, N,
                               H, W, C, accumulate);
     else
@@ -732,7 +861,7 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
     int chunks = cdiv(npix, 1024);
     dim3 g(chunks, k * k);
     const size_t ism = dw_img_smem(dtype, H, W, k);
-    if (ism <= 64 * 1024) {  // small maps (the 20x20 C2PTSSA / EDFFN / Mona path): whole image in LDS
+    if (ism <= 64 * 1024 && xcs % v == 0 && dcs % v == 0) {  // small maps (the 20x20 C2PTSSA / EDFFN / Mona path): whole image in LDS
       chunks = N;
       if (dtype == ADR_BF16)
         hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), ism, st,
@@ -863,9 +992,14 @@ extern "C" int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, 
   return check_launch("adr_edffn_fwd");
 }
 
+static size_t edffn_pad_floats(int N, int H, int W, int C) {
+  const size_t hp = (H + 7) / 8 * 8, wp = (W + 7) / 8 * 8;
+  return (size_t)N * hp * wp * C;
+}
+
+// padded dx scratch + the per-split spectral-weight partials
 extern "C" size_t adr_edffn_bwd_workspace(int N, int H, int W, int C) {
-  size_t hp = (H + 7) / 8 * 8, wp = (W + 7) / 8 * 8;
-  return (size_t)N * hp * wp * C * sizeof(float);
+  return (edffn_pad_floats(N, H, W, C) + (size_t)EDFFN_DWS * C * 4096) * sizeof(float);
 }
 
 extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* M,
@@ -891,12 +1025,14 @@ extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, 
     hipLaunchKernelGGL(edffn_fold_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, dpad, H, W, C, (long)N,
                        (float*)dx, ocs);
   if (dw) {
+    float* part = ws + edffn_pad_floats(N, H, W, C);
     if (dtype == ADR_BF16)
-      hipLaunchKernelGGL(edffn_dw_kernel<__bf16>, dim3(C), dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dy,
-                         dcs, N, H, W, C, basis, nuv, dw, dw_accumulate);
+      hipLaunchKernelGGL(edffn_dw_kernel<__bf16>, dim3(C, EDFFN_DWS), dim3(256), 0, st, (const __bf16*)x, xcs,
+                         (const __bf16*)dy, dcs, N, H, W, C, part);
     else
-      hipLaunchKernelGGL(edffn_dw_kernel<float>, dim3(C), dim3(256), 0, st, (const float*)x, xcs, (const float*)dy, dcs,
-                         N, H, W, C, basis, nuv, dw, dw_accumulate);
+      hipLaunchKernelGGL(edffn_dw_kernel<float>, dim3(C, EDFFN_DWS), dim3(256), 0, st, (const float*)x, xcs,
+                         (const float*)dy, dcs, N, H, W, C, part);
+    hipLaunchKernelGGL(edffn_dw_fin_kernel, dim3(C), dim3(256), 0, st, part, C, basis, nuv, dw, dw_accumulate);
   }
   return check_launch("adr_edffn_bwd");
 }
