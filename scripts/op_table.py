@@ -13,7 +13,7 @@ sys.path.insert(0, str(ROOT / "yolo-ad-refine_amd"))
 ap = argparse.ArgumentParser()
 ap.add_argument("--bs", type=int, default=64)
 ap.add_argument("--steps", type=int, default=1)
-ap.add_argument("--top", type=int, default=80)
+ap.add_argument("--top", type=int, default=150)
 args = ap.parse_args()
 
 import torch
@@ -34,13 +34,38 @@ for _ in range(args.steps):
     tr.step(batch)
 torch.cuda.synchronize()
 recs, NV.OP_TRACE = NV.OP_TRACE, None
-by_site = defaultdict(lambda: [0, 0.0])
+
+
+def est_bytes(name, ints):
+    """Algorithmic HBM bytes of the streaming entry points (integer arguments in call order; pointers dropped;
+    the trailing stream handle is dropped too)."""
+    ints = ints[:-1] if ints and ints[-1] == 0 else ints
+    try:
+        es = 2 if ints[0] == 1 else 4
+        if name == "adr_affine_act" and len(ints) == 10:
+            N, HW, C = ints[7:10]
+            return 2 * N * HW * C * es
+        if name == "adr_affine_act_bwd" and len(ints) == 14:
+            N, HW, C, acc = ints[10:14]
+            return (3 + acc) * N * HW * C * es
+        if name == "adr_nc_reduce" and len(ints) == 12:
+            mode, (N, HW, C) = ints[1], ints[8:11]
+            return (2 if mode == 1 else 1) * N * HW * C * es
+        if name == "adr_ew" and len(ints) == 10:
+            op, npix, C, acc = ints[1], ints[7], ints[8], ints[9]
+            ops = {0: 2, 1: 3, 2: 3, 3: 4, 4: 2, 5: 3, 6: 4}[op] + acc
+            return ops * npix * C * es
+    except (IndexError, KeyError):
+        pass
+    return None
+by_site = defaultdict(lambda: [0, 0.0, 0])
 by_name = defaultdict(lambda: [0, 0.0])
 for name, caller, ints, e0, e1 in recs:
     t = e0.elapsed_time(e1) * 1e-3
     a = by_site[(name, caller, ints)]
     a[0] += 1
     a[1] += t
+    a[2] += est_bytes(name, ints) or 0
     b = by_name[name]
     b[0] += 1
     b[1] += t
@@ -50,5 +75,14 @@ print("--- by entry point ---")
 for name, (n, t) in sorted(by_name.items(), key=lambda kv: -kv[1][1]):
     print(f"{1e3 * t / args.steps:7.3f} ms {n // args.steps:4d}x {1e6 * t / n:8.1f}us  {name}")
 print("--- by call site ---")
-for (name, caller, ints), (n, t) in sorted(by_site.items(), key=lambda kv: -kv[1][1])[:args.top]:
-    print(f"{1e3 * t / args.steps:7.3f} ms {n // args.steps:3d}x {1e6 * t / n:8.1f}us  {name} [{caller}] {ints}")
+for (name, caller, ints), (n, t, nb) in sorted(by_site.items(), key=lambda kv: -kv[1][1])[:args.top]:
+    bw = f"{nb / t / 1e9:6.0f} GB/s" if nb else "          "
+    print(f"{1e3 * t / args.steps:7.3f} ms {n // args.steps:3d}x {1e6 * t / n:8.1f}us {bw}  {name} [{caller}] {ints}")
+print("--- streaming entry points: achieved bandwidth by name ---")
+agg = defaultdict(lambda: [0.0, 0])
+for (name, caller, ints), (n, t, nb) in by_site.items():
+    if nb:
+        agg[name][0] += t
+        agg[name][1] += nb
+for name, (t, nb) in sorted(agg.items(), key=lambda kv: -kv[1][0]):
+    print(f"{1e3 * t / args.steps:7.3f} ms  {nb / t / 1e9:6.0f} GB/s  {nb / args.steps / 1e6:8.1f} MB/step  {name}")

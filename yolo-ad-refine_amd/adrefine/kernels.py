@@ -18,7 +18,10 @@ from .native import ConvDesc, lib
 
 F32, BF16 = 0, 1
 ACT = {"none": 0, "silu": 1, "gelu": 2, "relu": 3, "sigmoid": 4, "hswish": 5}
-STATS_ROWS = 256  # rows per chunk for adr_nc_reduce
+def _stats_rows(N, HW):
+    """Rows per adr_nc_reduce chunk. Measured (scripts/ab_bench.sh): a fixed 256 beats shrinking the chunks on
+    the small maps — the extra partial rows cost more in the BN/GN finalize than the fuller reduce grid gains."""
+    return 256
 
 # counts layout fix-ups (should stay 0 on the hot path; tests assert it)
 relayout_count = [0]
@@ -436,10 +439,10 @@ def _bias_grad(dy, K, N, HW, cs, param=None):
     """Per-channel sum of dy. With `param`, accumulates into its gradient destination (grad_dst) and returns
     the autograd value; otherwise returns a fresh (K,) tensor."""
     dt = dcode(dy.dtype)
-    chunks = lib.adr_nc_reduce_chunks(HW, STATS_ROWS)
+    chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
     part = torch.empty(N * chunks * 2 * K, dtype=torch.float32, device=dy.device)
     lib.adr_nc_reduce(dt, 0, ctypes.c_void_p(dy.data_ptr()), cs, 0, None, 0, 0, None, None, 0, 0, N, HW, K,
-                      STATS_ROWS, fptr(part), stream())
+                      _stats_rows(N, HW), fptr(part), stream())
     if param is not None:
         db, p, acc = grad_dst(param, K, dy.device)
         lib.adr_partial_sum(fptr(part), N * chunks, K, 0, p, acc, stream())
@@ -560,10 +563,10 @@ class BNActFn(torch.autograd.Function):
         scale, shift, mean, rstd = f(), f(), f(), f()
         if training:
             if stats is None or stats.numel() == 0:
-                chunks = lib.adr_nc_reduce_chunks(HW, STATS_ROWS)
+                chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
                 stats = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
                 lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, N, HW,
-                                  C, STATS_ROWS, fptr(stats), stream())
+                                  C, _stats_rows(N, HW), fptr(stats), stream())
             P = stats.numel() // (2 * C)
         else:
             P = 0
@@ -588,10 +591,10 @@ class BNActFn(torch.autograd.Function):
         HW = H * W
         dev = y.device
         dt = dcode(y.dtype)
-        chunks = lib.adr_nc_reduce_chunks(HW, STATS_ROWS)
+        chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
         part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
         lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale), fptr(shift),
-                          0, ACT[act], N, HW, C, STATS_ROWS, fptr(part), stream())
+                          0, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
         f = lambda: torch.empty(C, dtype=torch.float32, device=dev)  # noqa: E731
         A, B, Cc = f(), f(), f()
         dgamma, pg, acc_g = grad_dst(gamma, C, dev)
@@ -617,10 +620,10 @@ class GNActFn(torch.autograd.Function):
         N, C, H, W = y.shape
         HW = H * W
         dev = y.device
-        chunks = lib.adr_nc_reduce_chunks(HW, STATS_ROWS)
+        chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
         part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
         lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, N, HW, C,
-                          STATS_ROWS, fptr(part), stream())
+                          _stats_rows(N, HW), fptr(part), stream())
         scale = torch.empty(N * C, dtype=torch.float32, device=dev)
         shift = torch.empty(N * C, dtype=torch.float32, device=dev)
         mean = torch.empty(N * groups, dtype=torch.float32, device=dev)
@@ -646,10 +649,10 @@ class GNActFn(torch.autograd.Function):
         HW = H * W
         dev = y.device
         dt = dcode(y.dtype)
-        chunks = lib.adr_nc_reduce_chunks(HW, STATS_ROWS)
+        chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
         part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
         lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale), fptr(shift),
-                          1, ACT[act], N, HW, C, STATS_ROWS, fptr(part), stream())
+                          1, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
         dgamma, pg, acc_g = grad_dst(gamma, C, dev)
         dbeta, pb, acc_b = grad_dst(ctx.pbeta, C, dev)
         if acc_g != acc_b:
@@ -920,10 +923,10 @@ def _reduce_dot(x, dy, sum_n, sum_c, which=0):
     N, C, H, W = dy.shape
     vd = _v(dy)
     vx = _v(x) if x is not None else (None, 0, 0)
-    chunks = lib.adr_nc_reduce_chunks(H * W, STATS_ROWS)
+    chunks = lib.adr_nc_reduce_chunks(H * W, _stats_rows(N, H * W))
     part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dy.device)
     lib.adr_dot_reduce(dcode(dy.dtype), ctypes.c_void_p(vx[1]) if x is not None else None, vx[2],
-                       ctypes.c_void_p(vd[1]), vd[2], N, H * W, C, STATS_ROWS, fptr(part), stream())
+                       ctypes.c_void_p(vd[1]), vd[2], N, H * W, C, _stats_rows(N, H * W), fptr(part), stream())
     out = torch.empty((1 if sum_n else N) * (1 if sum_c else C), dtype=torch.float32, device=dy.device)
     lib.adr_nc_collapse(fptr(part), N, chunks, C, which, fptr(out), int(sum_n), int(sum_c), 0, stream())
     return out

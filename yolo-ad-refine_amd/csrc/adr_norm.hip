@@ -180,22 +180,51 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
   }
 }
 
+// per-channel sums over an image's chunks into LDS (sa, sb): threads = (channel, chunk-part) pairs so every
+// thread of the block loads, parts combined in a fixed order
+__device__ __forceinline__ void gn_chan_sums(const float* partial, int n, int chunks, int C, double* sa, double* sb,
+                                             double* scratch_a, double* scratch_b) {
+  const int parts = C >= 256 ? 1 : 256 / C;
+  for (int c0 = 0; c0 < C; c0 += 256) {
+    const int c = c0 + (int)threadIdx.x % (C >= 256 ? 256 : C), part = (int)threadIdx.x / (C >= 256 ? 256 : C);
+    double a = 0.0, b = 0.0;
+    if (c < C && part < parts)
+      for (int ch = part; ch < chunks; ch += parts) {
+        const float* p = partial + ((long)n * chunks + ch) * 2 * C;
+        a += p[c];
+        b += p[C + c];
+      }
+    scratch_a[threadIdx.x] = a;
+    scratch_b[threadIdx.x] = b;
+    __syncthreads();
+    if ((int)threadIdx.x < (C >= 256 ? 256 : C) && c < C) {
+      double ta = 0.0, tb = 0.0;
+      for (int q = 0; q < parts; ++q) {
+        ta += scratch_a[q * (C >= 256 ? 256 : C) + threadIdx.x];
+        tb += scratch_b[q * (C >= 256 ? 256 : C) + threadIdx.x];
+      }
+      sa[c] = ta;
+      sb[c] = tb;
+    }
+    __syncthreads();
+  }
+}
+
 // GroupNorm forward finalize: block per image; partial [n][chunks][2][C]
 __global__ void __launch_bounds__(256) gn_finalize_kernel(const float* __restrict__ partial, int chunks, int C, int G,
                                                           double count, const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float eps, float* scale,
                                                           float* shift, float* mean_out, float* rstd_out) {
-  int n = blockIdx.x;
+  const int n = blockIdx.x;
   __shared__ double gm[64], gr[64];
-  int cpg = C / G;
+  __shared__ double sa[1024], sb[1024], xa[256], xb[256];
+  gn_chan_sums(partial, n, chunks, C, sa, sb, xa, xb);
+  const int cpg = C / G;
   for (int g = threadIdx.x; g < G; g += 256) {
     double a = 0.0, b = 0.0;
-    for (int ch = 0; ch < chunks; ++ch) {
-      const float* p = partial + ((long)n * chunks + ch) * 2 * C;
-      for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
-        a += p[c];
-        b += p[C + c];
-      }
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      a += sa[c];
+      b += sb[c];
     }
     double mu = a / count, var = b / count - mu * mu;
     if (var < 0) var = 0;
@@ -221,17 +250,13 @@ __global__ void __launch_bounds__(256) gn_bwd_coef_kernel(const float* __restric
                                                           const float* __restrict__ gamma, float* A, float* B,
                                                           float* Cc) {
   const int n = blockIdx.x, cpg = C / G;
-  __shared__ double sa[1024], sg[1024];
+  __shared__ double sa[1024], sg[1024], xa[256], xb[256];
   __shared__ double s1[64], s2[64];
+  gn_chan_sums(partial, n, chunks, C, sa, sg, xa, xb);
   for (int c = threadIdx.x; c < C; c += 256) {
     const int g = c / cpg;
     const double mu = mean[n * G + g], rs = rstd[n * G + g];
-    double a = 0.0, b = 0.0;
-    for (int ch = 0; ch < chunks; ++ch) {
-      const float* p = partial + ((long)n * chunks + ch) * 2 * C;
-      a += p[c];
-      b += p[C + c];
-    }
+    const double a = sa[c], b = sg[c];
     const double gm = gamma ? gamma[c] : 1.0;
     sa[c] = gm * a;                  // sum dxhat
     sg[c] = gm * (b - mu * a) * rs;  // sum dxhat * xhat
@@ -464,7 +489,7 @@ extern "C" int adr_bn_bwd_finalize(const float* partial, int P, int C, double co
 extern "C" int adr_gn_finalize(const float* partial, int N, int chunks, int C, int G, double count, const float* gamma,
                                const float* beta, float eps, float* scale, float* shift, float* mean, float* rstd,
                                void* stream) {
-  ADR_REQUIRE(G <= 64 && C % G == 0, "gn_finalize: G=%d C=%d", G, C);
+  ADR_REQUIRE(G <= 64 && C <= 1024 && C % G == 0, "gn_finalize: G=%d C=%d", G, C);
   hipLaunchKernelGGL(gn_finalize_kernel, dim3(N), dim3(256), 0, (hipStream_t)stream, partial, chunks, C, G, count,
                      gamma, beta, eps, scale, shift, mean, rstd);
   return check_launch("adr_gn_finalize");
