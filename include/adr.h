@@ -135,6 +135,16 @@ int adr_pack_chunk_size(void);
 int adr_pack_weight2_batched(int dtype, const void* table, int nchunks, void* stream);
 int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, int RS, int transpose_kc,
                            int accumulate, void* stream);
+/* Stem: model.0 Conv(3, K, 3, 2) (nn/modules/conv.py:36-54, the first yaml row) straight from the fp32 NCHW
+ * image batch (detect/train.py:57-59), bf16 compute (adr_stem.hip). Forward writes y (N, H/2, W/2, K) NHWC bf16
+ * and, when stats != NULL, [adr_stem_fwd_tiles(N, Ho)][2][K] BatchNorm partial sums of the stored values.
+ * The weight gradient writes dw (K, 3, 3, 3) fp32 (+= if accumulate). K in {16, 32, 64}. */
+int adr_stem_fwd_tiles(int N, int Ho);
+int adr_stem_conv_fwd(const float* img, int N, int H, int W, const float* w, int K, void* y, int ycs, float* stats,
+                      void* stream);
+size_t adr_stem_wgrad_workspace(int N, int H, int W, int K);
+int adr_stem_conv_wgrad(const float* img, int N, int H, int W, const void* dy, int dcs, int K, float* dw,
+                        int accumulate, float* ws, size_t ws_bytes, void* stream);
 /* NCHW fp32 images (detect/train.py:57-59 preprocess output) -> NHWC compute dtype, channels padded to Cp. */
 int adr_image_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cp, void* stream);
 int adr_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long n, void* stream);

@@ -102,3 +102,27 @@ def test_conv_transpose_fixture(dtype):
     ref = dict(zip([str(k) for k in g["param_grad_norms_keys"]], g["param_grad_norms"]))
     assert abs(float(m.weight.grad.norm()) - ref["weight"]) <= tol["rtol"] * ref["weight"]
     assert abs(float(m.bias.grad.norm()) - ref["bias"]) <= tol["rtol"] * ref["bias"]
+
+
+@pytest.mark.parametrize("S,K", [(64, 16), (40, 32)])
+def test_stem_from_image(S, K):
+    """model.0 Conv(3, K, 3, 2) through the stem kernels (fp32 NCHW image in, bf16 compute) against the generic
+    path (image_to_nhwc + implicit GEMM): pre-BN output, BN statistics (via the BN'd output), weight gradient."""
+    from adrefine import kernels as Kn
+    from adrefine.nn.modules import Conv
+    torch.manual_seed(0)
+    m = Conv(3, K, 3, 2).cuda().train()
+    img = torch.rand(2, 3, S, S, device="cuda")
+    gout = torch.randn(2, K, S // 2, S // 2, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    ya = m.forward_image(img)
+    ya.backward(gout)
+    ga = m.conv.weight.grad.clone()
+    m.conv.weight.grad = None
+    yb = m(Kn.image_to_nhwc(img, torch.bfloat16, cpad=8))
+    yb.backward(gout)
+    gb = m.conv.weight.grad.clone()
+    d = (ya.float() - yb.float()).abs().max() / yb.float().abs().max()
+    assert float(d) < 2e-2, float(d)
+    dg = (ga - gb).norm() / gb.norm()
+    assert float(dg) < 1e-2, float(dg)

@@ -669,6 +669,50 @@ class GNActFn(torch.autograd.Function):
         return dy, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None
 
 
+class StemConvFn(torch.autograd.Function):
+    """model.0 Conv(3, K, 3, 2)'s convolution read straight from the fp32 NCHW image (bf16 compute): returns the
+    pre-BN output (NHWC bf16) and its BatchNorm partial statistics; backward = the weight gradient only (the
+    image needs none)."""
+
+    @staticmethod
+    def forward(ctx, img, w, want_stats):
+        _req_cuda(img)
+        img = img.float().contiguous()
+        N, _, H, W = img.shape
+        Kc = w.shape[0]
+        Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+        y = empty_act(N, Kc, Ho, Wo, torch.bfloat16, img.device)
+        stats = None
+        if want_stats:
+            stats = torch.empty(lib.adr_stem_fwd_tiles(N, Ho) * 2 * Kc, dtype=torch.float32, device=img.device)
+        wf = w.detach().float().contiguous()
+        lib.adr_stem_conv_fwd(fptr(img), N, H, W, fptr(wf), Kc, ctypes.c_void_p(y.data_ptr()), Kc, fptr(stats),
+                              stream())
+        ctx.save_for_backward(img)
+        ctx.pw = w
+        if stats is None:
+            stats = torch.empty(0, device=img.device)
+        ctx.mark_non_differentiable(stats)
+        return y, stats
+
+    @staticmethod
+    def backward(ctx, dy, _dstats):
+        (img,) = ctx.saved_tensors
+        N, _, H, W = img.shape
+        w = ctx.pw
+        Kc = w.shape[0]
+        dy, dyp, dycs = nhwc(dy.to(torch.bfloat16) if dy.dtype != torch.bfloat16 else dy)
+        dw, pdw, acc = grad_dst(w, w.numel(), img.device)
+        wsb = lib.adr_stem_wgrad_workspace(N, H, W, Kc)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=img.device)
+        lib.adr_stem_conv_wgrad(fptr(img), N, H, W, ctypes.c_void_p(dyp), dycs, Kc, pdw, acc, fptr(ws), wsb, stream())
+        return None, grad_ret(w, dw), None
+
+
+def stem_conv(img, w, want_stats):
+    return StemConvFn.apply(img, w, want_stats)
+
+
 def image_to_nhwc(img: torch.Tensor, dtype, cpad=8):
     """(B, 3, H, W) float images -> NHWC compute-dtype activation with channels padded to `cpad`."""
     _req_cuda(img)

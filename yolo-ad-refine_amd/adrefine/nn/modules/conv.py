@@ -75,3 +75,14 @@ class Conv(nn.Module):
         cv = self.conv
         y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight))
         return K.bn_act(y, st, self.bn, self.act_name, self.training)
+
+    def stem_ok(self):
+        """The adr_stem kernels cover Conv(3, K in {16, 32, 64}, 3, 2) with pad 1 (every yaml's model.0)."""
+        cv = self.conv
+        return (cv.in_channels == 3 and cv.out_channels in (16, 32, 64) and cv.kernel_size == (3, 3)
+                and cv.stride == (2, 2) and cv.padding == (1, 1) and cv.groups == 1 and cv.dilation == (1, 1))
+
+    def forward_image(self, img):
+        """The same Conv on the fp32 NCHW image batch, through the stem kernels (bf16 compute)."""
+        y, st = K.stem_conv(img, self.conv.weight, self.training)
+        return K.bn_act(y, st if st.numel() else None, self.bn, self.act_name, self.training)

@@ -175,10 +175,16 @@ class DetectionModel(nn.Module):
 
     def _predict_once(self, x):
         """tasks.py:141-168 layer routing by m.f with the save list."""
+        first = 0
         if x.dim() == 4 and x.shape[1] == 3:
-            x = K.image_to_nhwc(x, self.compute_dtype, cpad=8)
-        y = []
-        for m in self.model:
+            m0 = self.model[0]
+            if self.compute_dtype == torch.bfloat16 and m0.f == -1 and getattr(m0, "stem_ok", lambda: False)():
+                x = m0.forward_image(x)  # stem conv straight from the fp32 image (no NHWC copy of it)
+                first = 1
+            else:
+                x = K.image_to_nhwc(x, self.compute_dtype, cpad=8)
+        y = [x if self.model[0].i in self.save else None] if first else []
+        for m in list(self.model)[first:]:
             if m.f != -1:
                 x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
             x = m(x)

@@ -1,0 +1,318 @@
+// The network stem — model.0 Conv(3, c2, 3, 2) (reference nn/modules/conv.py:36-54, first row of the yaml
+// backbone) — read straight from the preprocessed fp32 NCHW image batch (detect/train.py:57-59), bf16 compute:
+//   * forward: y (16 pixels x 16 channels) = im2col (16 x 27->32) x W^T per v_mfma_f32_16x16x32_bf16 from the
+//     image rows staged in LDS (bf16), fp32 accumulation, bf16 NHWC output, plus the per-block BatchNorm
+//     partial statistics of the stored values (the same contract as the conv epilogue).
+//   * weight gradient: dw[k][j] = sum_pixels dy[p][k] * im2col(img)[p][j] (j = c*9 + ky*3 + kx) on MFMA
+//     v_mfma_f32_16x16x32_bf16: A = dy^T (16 output channels x 32 pixels), B = im2col (32 pixels x 2 x 16
+//     columns), accumulated per wave over a pixel range, block partials summed in a fixed order.
+// Both replace image_to_nhwc + the generic implicit GEMM on a channel-padded copy of the image (420 MB of
+// bf16 written and read twice per bs64 step) with one read of the fp32 image per pass.
+#include "adr_common.h"
+
+namespace adr {
+
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+constexpr int STEM_ROWS = 2;
+
+// stage image rows iy0 .. iy0+IR-1 of the 3 channels of image n into LDS as bf16 [3][IR][W+2] with zero
+// columns at -1 and W (and zero rows outside the image); 16-byte loads when W % 4 == 0
+template <int IR>
+__device__ __forceinline__ void stage_rows(const float* __restrict__ img, int n, int H, int W, int iy0, __bf16* xs) {
+  constexpr int NR = 3 * IR;
+  const int Wp = W + 2;
+  if ((W & 3) == 0) {
+    // every row's 16-byte load issued before any LDS store: NR loads in flight per thread
+    for (int q = threadIdx.x; q < W / 4; q += blockDim.x) {
+      f32x4 v[NR];
+#pragma unroll
+      for (int row = 0; row < NR; ++row) {
+        const int c = row / IR, iy = iy0 + row % IR;
+        const bool rok = iy >= 0 && iy < H;
+        v[row] = rok ? *reinterpret_cast<const f32x4*>(img + (((long)n * 3 + c) * H + iy) * W + 4 * q)
+                     : (f32x4){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+      for (int row = 0; row < NR; ++row)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xs[row * Wp + 1 + 4 * q + e] = (__bf16)v[row][e];
+    }
+  } else {
+    for (int row = 0; row < NR; ++row) {
+      const int c = row / IR, iy = iy0 + row % IR;
+      const bool rok = iy >= 0 && iy < H;
+      for (int q = threadIdx.x; q < W; q += blockDim.x)
+        xs[row * Wp + 1 + q] = (__bf16)(rok ? img[(((long)n * 3 + c) * H + iy) * W + q] : 0.f);
+    }
+  }
+  if (threadIdx.x < NR) {
+    xs[threadIdx.x * Wp] = (__bf16)0.f;
+    xs[threadIdx.x * Wp + W + 1] = (__bf16)0.f;
+  }
+}
+
+// weight gradient partials: block per (image, pair of output rows); the 5 input rows it needs (3 channels,
+// columns -1..W zero-padded) and its dy rows are staged in LDS as bf16, then 4 waves run the MFMA steps over
+// the block's 2*Wo pixels (32 per step). part[block][KT*16][32].
+template <int KT>
+__global__ void __launch_bounds__(256) stem_wgrad_kernel(const float* __restrict__ img, int H, int W,
+                                                         const __bf16* __restrict__ dy, int dcs, int Ho, int Wo,
+                                                         float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+  constexpr int IR = 2 * STEM_ROWS + 1;  // input rows
+  const int Wp = W + 2;
+  __bf16* xs = reinterpret_cast<__bf16*>(smraw);                 // [3][IR][Wp]
+  __bf16* ds = xs + ((3 * IR * Wp + 7) & ~7);                    // [STEM_ROWS * Wo][KT * 16]
+  float* red = reinterpret_cast<float*>(ds + (long)STEM_ROWS * Wo * KT * 16);  // [4][KT*16][32]
+  const int rb = blockIdx.x % ((Ho + STEM_ROWS - 1) / STEM_ROWS), n = blockIdx.x / ((Ho + STEM_ROWS - 1) / STEM_ROWS);
+  const int oy0 = rb * STEM_ROWS, nrow = min(STEM_ROWS, Ho - oy0), iy0 = 2 * oy0 - 1;
+  stage_rows<IR>(img, n, H, W, iy0, xs);
+  const int npx = nrow * Wo;
+  const __bf16* dyb = dy + ((long)n * Ho + oy0) * Wo * (long)dcs;
+  {  // 16-byte chunks of 8 channels, four loads in flight per thread
+    const int nch = npx * KT * 2;
+    for (int i0 = threadIdx.x; i0 < nch; i0 += 4 * 256) {
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        if (i < nch) v[u] = ld16(dyb + (long)(i / (KT * 2)) * dcs + (i % (KT * 2)) * 8);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * 256;
+        if (i < nch) *reinterpret_cast<u32x4*>(ds + (long)(i / (KT * 2)) * KT * 16 + (i % (KT * 2)) * 8) = v[u];
+      }
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  int cj[2], kyj[2], kxj[2];
+  bool jok[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const int j = jt * 16 + i;
+    jok[jt] = j < 27;
+    const int jj = jok[jt] ? j : 0;
+    cj[jt] = jj / 9;
+    kyj[jt] = (jj % 9) / 3;
+    kxj[jt] = jj % 3;
+  }
+  f32x4 acc[KT][2];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) acc[t][0] = acc[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  const int nsteps = (npx + 31) / 32;
+  for (int s = wave; s < nsteps; s += 4) {
+    const int pbase = s * 32 + 8 * g;
+    int r = pbase / Wo, ox = pbase - r * Wo;
+    s16x8 a[KT], b[2];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const bool pok = pbase + e < npx;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const __bf16 v = pok ? ds[(long)(pbase + e) * KT * 16 + t * 16 + i] : (__bf16)0.f;
+        a[t][e] = *reinterpret_cast<const short*>(&v);
+      }
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt) {
+        const __bf16 v = (pok && jok[jt]) ? xs[(cj[jt] * IR + 2 * r + kyj[jt]) * Wp + 2 * ox + kxj[jt]]
+                                          : (__bf16)0.f;
+        b[jt][e] = *reinterpret_cast<const short*>(&v);
+      }
+      if (++ox == Wo) {
+        ox = 0;
+        ++r;
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t)
+#pragma unroll
+      for (int jt = 0; jt < 2; ++jt)
+        acc[t][jt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&a[t]),
+                                                             *reinterpret_cast<bf16x8*>(&b[jt]), acc[t][jt], 0, 0, 0);
+  }
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) red[(wave * KT * 16 + t * 16 + 4 * g + rr) * 32 + jt * 16 + i] = acc[t][jt][rr];
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < KT * 16 * 32; idx += 256) {
+    const int M = KT * 16 * 32;
+    part[(long)blockIdx.x * M + idx] = (red[idx] + red[M + idx]) + (red[2 * M + idx] + red[3 * M + idx]);
+  }
+}
+
+static size_t stem_wgrad_smem(int W, int Wo, int KT) {
+  const int IR = 2 * STEM_ROWS + 1;
+  return (((size_t)3 * IR * (W + 2) + 7) & ~(size_t)7) * 2 + (size_t)STEM_ROWS * Wo * KT * 16 * 2 +
+         (size_t)4 * KT * 16 * 32 * 4;
+}
+
+// forward on MFMA: block per (image, pair of output rows), image rows staged in LDS exactly as for the weight
+// gradient; y[16 pixels][16 k] = im2col (16 x 32) * W^T (32 x 16) per v_mfma_f32_16x16x32_bf16. The W^T
+// fragment is the same for every step (preloaded); stats = per-block sums of the stored bf16 values.
+template <int KT>
+__global__ void __launch_bounds__(256) stem_fwd_kernel(const float* __restrict__ img, int H, int W,
+                                                       const float* __restrict__ w, __bf16* __restrict__ y, int ycs,
+                                                       int Ho, int Wo, float* __restrict__ stats) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+  constexpr int IR = 2 * STEM_ROWS + 1;
+  const int Wp = W + 2;
+  __bf16* xs = reinterpret_cast<__bf16*>(smraw);  // [3][IR][Wp]
+  __shared__ float red[4][2][KT * 16];
+  const int nrb = (Ho + STEM_ROWS - 1) / STEM_ROWS;
+  const int rb = blockIdx.x % nrb, n = blockIdx.x / nrb;
+  const int oy0 = rb * STEM_ROWS, nrow = min(STEM_ROWS, Ho - oy0), iy0 = 2 * oy0 - 1;
+  stage_rows<IR>(img, n, H, W, iy0, xs);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int g = lane >> 4, i = lane & 15;
+  // B = W^T: lane supplies B[j = 8g + e][k = t*16 + i] = w[k][j]
+  s16x8 bw[KT];
+  int jc[8], jky[8], jkx[8];
+  bool jok[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int j = 8 * g + e;
+    jok[e] = j < 27;
+    const int jj = jok[e] ? j : 0;
+    jc[e] = jj / 9;
+    jky[e] = (jj % 9) / 3;
+    jkx[e] = jj % 3;
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      const __bf16 v = (__bf16)(jok[e] ? w[(t * 16 + i) * 27 + j] : 0.f);
+      bw[t][e] = *reinterpret_cast<const short*>(&v);
+    }
+  }
+  __syncthreads();
+  float s1[KT], s2[KT];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) s1[t] = s2[t] = 0.f;
+  const int npx = nrow * Wo;
+  __bf16* yb = y + ((long)n * Ho + oy0) * Wo * (long)ycs;
+  for (int st = wave; st * 16 < npx; st += 4) {
+    // A = im2col: lane supplies A[pixel i][j = 8g + e]
+    const int p = st * 16 + i;
+    const bool pok = p < npx;
+    const int r = pok ? p / Wo : 0, ox = pok ? p - r * Wo : 0;
+    s16x8 a;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const __bf16 v = (pok && jok[e]) ? xs[(jc[e] * IR + 2 * r + jky[e]) * Wp + 2 * ox + jkx[e]] : (__bf16)0.f;
+      a[e] = *reinterpret_cast<const short*>(&v);
+    }
+#pragma unroll
+    for (int t = 0; t < KT; ++t) {
+      f32x4 d = {0.f, 0.f, 0.f, 0.f};
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&a), *reinterpret_cast<bf16x8*>(&bw[t]),
+                                                  d, 0, 0, 0);
+      // D[pixel 4g + rr][k = t*16 + i]
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        const int q = st * 16 + 4 * g + rr;
+        if (q < npx) {
+          const __bf16 v = (__bf16)d[rr];
+          yb[(long)q * ycs + t * 16 + i] = v;
+          const float f = (float)v;
+          s1[t] += f;
+          s2[t] += f * f;
+        }
+      }
+    }
+  }
+  if (!stats) return;
+#pragma unroll
+  for (int t = 0; t < KT; ++t) {  // combine the four lane groups (same k), then the waves
+    s1[t] += __shfl_xor(s1[t], 16, 64);
+    s1[t] += __shfl_xor(s1[t], 32, 64);
+    s2[t] += __shfl_xor(s2[t], 16, 64);
+    s2[t] += __shfl_xor(s2[t], 32, 64);
+    if (g == 0) {
+      red[wave][0][t * 16 + i] = s1[t];
+      red[wave][1][t * 16 + i] = s2[t];
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * KT * 16) {
+    const int q = threadIdx.x / (KT * 16), k = threadIdx.x % (KT * 16);
+    stats[(long)blockIdx.x * 2 * KT * 16 + threadIdx.x] = (red[0][q][k] + red[1][q][k]) + (red[2][q][k] + red[3][q][k]);
+  }
+}
+
+// dw[k][j] (+)= sum_blocks part[b][k][j], j < 27 (the (K, 3, 3, 3) parameter layout)
+__global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* __restrict__ part, int nblk, int K,
+                                                                float* dw, int accumulate) {
+  __shared__ float sh[256];
+  const int k = blockIdx.x / 27, j = blockIdx.x % 27;
+  float s = 0.f;
+  for (int b = threadIdx.x; b < nblk; b += 256) s += part[((long)b * K + k) * 32 + j];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) dw[k * 27 + j] = accumulate ? dw[k * 27 + j] + sh[0] : sh[0];
+}
+
+
+}  // namespace adr
+
+using namespace adr;
+
+// forward tiles = blocks (image, pair of output rows); npix = N * Ho * Wo with Ho, Wo of the stem
+extern "C" int adr_stem_fwd_tiles(int N, int Ho) { return N * ((Ho + STEM_ROWS - 1) / STEM_ROWS); }
+
+extern "C" int adr_stem_conv_fwd(const float* img, int N, int H, int W, const float* w, int K, void* y, int ycs,
+                                 float* stats, void* stream) {
+  ADR_REQUIRE(N > 0 && H > 1 && W > 1 && (K == 16 || K == 32 || K == 64) && ycs >= K,
+              "stem_conv_fwd: N=%d H=%d W=%d K=%d ycs=%d", N, H, W, K, ycs);
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  ADR_REQUIRE((long)N * Ho * Wo < (1l << 31), "stem_conv_fwd: too many pixels");
+  const size_t sm = (((size_t)3 * (2 * STEM_ROWS + 1) * (W + 2) + 7) & ~(size_t)7) * 2;
+  ADR_REQUIRE(sm <= 64 * 1024, "stem_conv_fwd: W=%d too wide for the LDS plan", W);
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid(adr_stem_fwd_tiles(N, Ho));
+  if (K == 16)
+    hipLaunchKernelGGL(stem_fwd_kernel<1>, grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
+  else if (K == 32)
+    hipLaunchKernelGGL(stem_fwd_kernel<2>, grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
+  else
+    hipLaunchKernelGGL(stem_fwd_kernel<4>, grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
+  return check_launch("adr_stem_conv_fwd");
+}
+
+extern "C" size_t adr_stem_wgrad_workspace(int N, int H, int W, int K) {
+  const int Ho = (H - 1) / 2 + 1;
+  const long blocks = (long)N * ((Ho + STEM_ROWS - 1) / STEM_ROWS);
+  return (size_t)blocks * K * 32 * sizeof(float);
+}
+
+extern "C" int adr_stem_conv_wgrad(const float* img, int N, int H, int W, const void* dy, int dcs, int K, float* dw,
+                                   int accumulate, float* ws, size_t ws_bytes, void* stream) {
+  ADR_REQUIRE(N > 0 && H > 1 && W > 1 && (K == 16 || K == 32 || K == 64) && dcs >= K,
+              "stem_conv_wgrad: N=%d H=%d W=%d K=%d", N, H, W, K);
+  ADR_REQUIRE(ws_bytes >= adr_stem_wgrad_workspace(N, H, W, K), "stem_conv_wgrad: workspace");
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  const int blocks = N * ((Ho + STEM_ROWS - 1) / STEM_ROWS);
+  const int KT = K / 16;
+  const size_t sm = stem_wgrad_smem(W, Wo, KT);
+  ADR_REQUIRE(sm <= 64 * 1024 && dcs % 8 == 0, "stem_conv_wgrad: W=%d too wide for the LDS plan", W);
+  hipStream_t st = (hipStream_t)stream;
+  if (K == 16)
+    hipLaunchKernelGGL(stem_wgrad_kernel<1>, dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs, Ho,
+                       Wo, ws);
+  else if (K == 32)
+    hipLaunchKernelGGL(stem_wgrad_kernel<2>, dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs, Ho,
+                       Wo, ws);
+  else
+    hipLaunchKernelGGL(stem_wgrad_kernel<4>, dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs, Ho,
+                       Wo, ws);
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(K * 27), dim3(256), 0, st, ws, blocks, K, dw, accumulate);
+  return check_launch("adr_stem_conv_wgrad");
+}
