@@ -758,7 +758,13 @@ __global__ void __launch_bounds__(256) edffn_dw_fin_kernel(const float* part, in
   for (int u = wave; u < nuv; u += 4) {
     const float* b = Bm + (long)u * 4096;
     float sacc = 0.f;
-    for (int e = lane; e < 4096; e += 64) sacc += b[e] * dM[e];
+    for (int e0 = lane; e0 < 4096; e0 += 64 * 8) {
+      float bv[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) bv[q] = b[e0 + 64 * q];  // eight loads in flight
+#pragma unroll
+      for (int q = 0; q < 8; ++q) sacc += bv[q] * dM[e0 + 64 * q];
+    }
     sacc = wave_sum(sacc);
     if (lane == 0) dw[c * nuv + u] = accumulate ? dw[c * nuv + u] + sacc : sacc;
   }

@@ -484,7 +484,7 @@ __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, 
   for (int it = 0; it < CLS_ANCHORS_PER_BLOCK / 16; ++it) {
     const long i = (long)blockIdx.x * CLS_ANCHORS_PER_BLOCK + it * 16 + sub;
     if (i >= nanch) break;
-    const int a = (int)(i % L.A), b = (int)(i / L.A);
+    const int b = (int)((unsigned)i / (unsigned)L.A), a = (int)i - b * L.A;  // B * A < 2^31
     int lvl;
     float ax, ay;
     const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
@@ -505,10 +505,13 @@ __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, 
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
           const float t = (c0 + k == lab) ? nrm : 0.f;
-          const float bce = fmaxf(x[k], 0.f) - x[k] * t + log1pf(expf(-fabsf(x[k])));
-          const float mod = (t <= mu - 0.1f) ? 1.f : ((t < mu) ? e21 : expf(-(t - 1.f)));
+          // one exponential per logit: e = exp(-|x|) gives both the stable softplus term and the sigmoid
+          const float e = __expf(-fabsf(x[k]));
+          const float bce = fmaxf(x[k], 0.f) - x[k] * t + log1pf(e);
+          const float mod = (t <= mu - 0.1f) ? 1.f : ((t < mu) ? e21 : __expf(-(t - 1.f)));
           acc += bce * mod;
-          const float sg = 1.f / (1.f + expf(-x[k]));
+          const float r1 = 1.f / (1.f + e);
+          const float sg = x[k] >= 0.f ? r1 : e * r1;
           g[k] = (sg - t) * mod * cscale;
         }
         store8<T>(gp + 4 * RM + c0, g);
