@@ -1,6 +1,6 @@
 """Which PyTorch-native ops still run inside the train step (copies, fills, adds): one eager bs64 step under
-torch.profiler with Python stacks, aggregated by (op, innermost adrefine frame).
-usage: python scripts/torch_ops.py   (GPU)"""
+torch.profiler (CPU ops only); every aten copy/fill/add event is attributed to its outermost autograd node or
+Python-level parent op. usage: python scripts/torch_ops.py   (GPU)"""
 import sys
 from collections import Counter
 from pathlib import Path
@@ -22,16 +22,24 @@ batch, _ = train_batch(64, 640, seed=0, device=dev)
 for _ in range(2):
     tr.step(batch)
 torch.cuda.synchronize()
-with profile(activities=[ProfilerActivity.CPU], with_stack=True) as prof:
+
+WATCH = ("aten::copy_", "aten::fill_", "aten::zero_", "aten::add", "aten::add_", "aten::to", "aten::clone",
+         "aten::contiguous", "aten::zeros", "aten::zeros_like", "aten::cat", "aten::sum", "aten::mul")
+with profile(activities=[ProfilerActivity.CPU], with_stack=False) as prof:
     tr.step(batch)
     torch.cuda.synchronize()
+
 cnt = Counter()
 for ev in prof.events():
-    if ev.name not in ("aten::copy_", "aten::fill_", "aten::add", "aten::add_", "aten::zero_", "aten::clone",
-                       "aten::contiguous", "aten::cat", "aten::mul", "aten::sum", "aten::to", "aten::_to_copy"):
+    if ev.name not in WATCH:
         continue
-    frames = [f for f in (ev.stack or []) if "adrefine" in f or "torch/autograd" in f]
-    site = frames[0] if frames else "(no adrefine frame)"
-    cnt[(ev.name, site)] += 1
-for (name, site), n in cnt.most_common(60):
-    print(f"{n:4d}  {name:18s} {site}")
+    chain = []
+    p = ev.cpu_parent
+    while p is not None:
+        chain.append(p.name)
+        p = p.cpu_parent
+    # nearest autograd node / Python op, then the outermost frame
+    near = next((c for c in chain if "autograd" in c or "Backward" in c or not c.startswith("aten::")), "(top)")
+    cnt[(ev.name, near[:90], chain[0][:40] if chain else "")] += 1
+for (name, near, par), n in cnt.most_common(70):
+    print(f"{n:4d}  {name:16s} {par:40s} {near}")

@@ -457,6 +457,7 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, want_stats, cpad):
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         dtype = x.dtype
         x, xp, xcs = nhwc(x)
         N, C, H, W = x.shape
@@ -484,6 +485,8 @@ class Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
+        if dy is None:
+            return None, None, None, None, None, None, None
         x, wp, wt = ctx.saved_tensors
         stride, pad, cpad, wshape, has_b = ctx.meta
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
@@ -676,6 +679,7 @@ class StemConvFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, img, w, want_stats):
+        ctx.set_materialize_grads(False)
         _req_cuda(img)
         img = img.float().contiguous()
         N, _, H, W = img.shape
@@ -697,6 +701,8 @@ class StemConvFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy, _dstats):
+        if dy is None:
+            return None, None, None
         (img,) = ctx.saved_tensors
         N, _, H, W = img.shape
         w = ctx.pw
