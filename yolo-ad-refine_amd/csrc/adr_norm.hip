@@ -45,26 +45,40 @@ __global__ void __launch_bounds__(256) nc_reduce_kernel(const T* __restrict__ x,
     }
   }
   if (r0 < rpp) {
-    for (int r = rbeg + r0; r < rend; r += rpp) {
-      long pix = (long)n * HW + r;
-      u32x4 xv = ld16(x + pix * xcs + xco + c0);
-      const T* xe = reinterpret_cast<const T*>(&xv);
-      if (MODE == RED_BWD) {
-        u32x4 dv = ld16(dz + pix * dcs + dco + c0);
-        const T* de = reinterpret_cast<const T*>(&dv);
+    // NU rows in flight per thread: all loads of a group are issued before any is consumed
+    constexpr int NU = 4;
+    const T* xb = x + ((long)n * HW) * xcs + xco + c0;
+    const T* db = MODE == RED_BWD ? dz + ((long)n * HW) * dcs + dco + c0 : nullptr;
+    for (int r = rbeg + r0; r < rend; r += NU * rpp) {
+      u32x4 xv[NU], dv[NU];
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          float xf = to_f(xe[e]);
-          float g = to_f(de[e]) * act_bwd(act, xf * sc[e] + sf[e]);
-          s1[e] += g;
-          s2[e] += g * xf;
+      for (int u = 0; u < NU; ++u) {
+        const int ru = r + u * rpp;
+        if (ru < rend) {
+          xv[u] = ld16(xb + (long)ru * xcs);
+          if (MODE == RED_BWD) dv[u] = ld16(db + (long)ru * dcs);
         }
-      } else {
+      }
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          float xf = to_f(xe[e]);
-          s1[e] += xf;
-          s2[e] += xf * xf;
+      for (int u = 0; u < NU; ++u) {
+        if (r + u * rpp >= rend) break;
+        const T* xe = reinterpret_cast<const T*>(&xv[u]);
+        if (MODE == RED_BWD) {
+          const T* de = reinterpret_cast<const T*>(&dv[u]);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            float xf = to_f(xe[e]);
+            float g = to_f(de[e]) * act_bwd(act, xf * sc[e] + sf[e]);
+            s1[e] += g;
+            s2[e] += g * xf;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            float xf = to_f(xe[e]);
+            s1[e] += xf;
+            s2[e] += xf * xf;
+          }
         }
       }
     }
