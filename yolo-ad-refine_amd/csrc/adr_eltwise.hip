@@ -162,15 +162,25 @@ __global__ void __launch_bounds__(256) dot_reduce_kernel(const T* __restrict__ x
   for (int e = 0; e < V; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
   const int rbeg = chunk * rows_per_chunk, rend = min(HW, rbeg + rows_per_chunk);
   if (r0 < rpp) {
-    for (int r = rbeg + r0; r < rend; r += rpp) {
-      long pix = (long)n * HW + r;
-      float fx[V], fd[V];
-      if (x) VecIO<T>::load(x + pix * xcs + cg * V, fx);
-      VecIO<T>::load(dz + pix * dcs + cg * V, fd);
+    constexpr int NU = 4;  // rows in flight per thread
+    for (int r = rbeg + r0; r < rend; r += NU * rpp) {
+      float fx[NU][V], fd[NU][V];
 #pragma unroll
-      for (int e = 0; e < V; ++e) {
-        s1[e] += x ? fx[e] * fd[e] : 0.f;
-        s2[e] += fd[e];
+      for (int u = 0; u < NU; ++u) {
+        const long pix = (long)n * HW + r + u * rpp;
+        if (r + u * rpp < rend) {
+          if (x) VecIO<T>::load(x + pix * xcs + cg * V, fx[u]);
+          VecIO<T>::load(dz + pix * dcs + cg * V, fd[u]);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        if (r + u * rpp >= rend) break;
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          s1[e] += x ? fx[u][e] * fd[u][e] : 0.f;
+          s2[e] += fd[u][e];
+        }
       }
     }
   }
