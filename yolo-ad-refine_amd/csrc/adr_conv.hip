@@ -41,14 +41,19 @@ struct ConvArgs {
 constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
 
 template <int BN, int MODE>
-__global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
+__global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvArgs a) {
   constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
   constexpr int WROWS = CBM / WAVES_M, WCOLS = BN / WAVES_N;
   constexpr int TM = WROWS / 16, TN = WCOLS / 16;
   constexpr int A_CH = CBM * (CBK / 8) / 256;                  // 4 chunks per thread
   constexpr int B_TOT = BN * (CBK / 8), B_CH = (B_TOT + 255) / 256;
   constexpr int OPITCH = BN + 8;                               // output image pitch (elements)
-  constexpr int SMEM_AB = (CBM + BN) * CLD;
+  // BN = 128 double-buffers the A/B tiles (one barrier per K-step): its VGPR budget already limits it to 2
+  // waves/SIMD, which the doubled LDS (73.7 KB, 2 blocks/CU) matches; narrower tiles keep one buffer and their
+  // higher occupancy
+  constexpr bool DB = BN == 128;
+  constexpr int STAGE = (CBM + BN) * CLD;
+  constexpr int SMEM_AB = (DB ? 2 : 1) * STAGE;
   constexpr int SMEM_O = CBM * OPITCH;
   constexpr int SMEM = SMEM_AB > SMEM_O ? SMEM_AB : SMEM_O;
   constexpr int RG = 256 / (BN / 8);                           // row groups of the stats epilogue
@@ -60,6 +65,10 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   float (*red)[RG][BN] = reinterpret_cast<float (*)[RG][BN]>(lds_raw);
   __bf16* As = smem;
   __bf16* Bs = smem + CBM * CLD;
+  auto set_stage = [&](int b) {
+    As = smem + b * STAGE;
+    Bs = As + CBM * CLD;
+  };
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
@@ -93,7 +102,13 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
 
   // per-thread A rows: chunk q = tid + 256 i -> row q / 8, reduction chunk q % 8
   const int kc = tid & 7;
-  int r_img[A_CH], r_y[A_CH], r_x[A_CH];
+  // FWD and stride-1 DGRAD gather linearly: source pixel = row base + SG * (kh * sw + kw) with SG = +1 (FWD) or
+  // -1 (DGRAD), so a row keeps only its base element offset and its (y, x) origin for the padding test, and a
+  // chunk's address is one 32-bit add per step (the host guarantees < 2^31 elements). Stride-2 DGRAD parity
+  // classes keep the general (image, y, x) form.
+  constexpr bool LIN = MODE != CV_DGRAD2;
+  constexpr int SG = MODE == CV_FWD ? 1 : -1;
+  int r_img[A_CH], r_y[A_CH], r_x[A_CH], r_off[A_CH];
   bool r_ok[A_CH];
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
@@ -104,6 +119,12 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     const int rem = (int)(mm - (long)r_img[i] * hw);
     r_y[i] = (rem / rows_w) * ystep + cy;
     r_x[i] = (rem % rows_w) * ystep + cx;
+    if constexpr (LIN) {
+      // origin of the gather window: FWD y*str - pad (+kh) ; DGRAD y + pad (-kh)
+      r_y[i] = MODE == CV_FWD ? r_y[i] * a.str - a.ph : r_y[i] + a.ph;
+      r_x[i] = MODE == CV_FWD ? r_x[i] * a.str - a.pw : r_x[i] + a.pw;
+      r_off[i] = ((r_img[i] * a.sh_ + r_y[i]) * a.sw_ + r_x[i]) * a.scs + a.sco;
+    }
   }
   const int RS = a.r * a.s;
   const int ksteps = (ktot + CBK - 1) / CBK;
@@ -123,7 +144,9 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     kh = ta / a.s;
     kw = ta - kh * a.s;
   }
+  int kpos = kc * 8;  // LIN: reduction position = element offset within a B row
   auto advance = [&]() {
+    kpos += CBK;
     ca += CBK;
     while (ca >= a.sc) {
       ca -= a.sc;
@@ -135,44 +158,40 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
       }
     }
   };
+  // B rows n0 + q/8 (reduction-contiguous rows of RS * sc elements)
+  // chunk i of this thread: row n0 + tid/8 + 32 i
+  const int b_row = LIN ? ktot : RS * a.sc;
+  const int b_n = n0 + (tid >> 3);
+  const int b_off0 = b_n * b_row;
+  auto b_ok = [&](int i) { return tid + 256 * i < B_TOT && b_n + 32 * i < a.N; };
   auto load = [&]() {
     const bool kok = ta < ntaps;
     const int c = ca;
+    if constexpr (LIN) {
+      const int dy = SG * kh, dx = SG * kw;
+      const int toff = (dy * a.sw_ + dx) * a.scs + c;
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      int sy, sx;
-      bool ok = kok && r_ok[i];
-      if constexpr (MODE == CV_FWD) {
-        sy = r_y[i] * a.str - a.ph + kh;
-        sx = r_x[i] * a.str - a.pw + kw;
-      } else if constexpr (MODE == CV_DGRAD2) {
+      for (int i = 0; i < A_CH; ++i) {
+        const bool ok = kok && r_ok[i] && (unsigned)(r_y[i] + dy) < (unsigned)a.sh_ &&
+                        (unsigned)(r_x[i] + dx) < (unsigned)a.sw_;
+        ra[i] = ok ? ld16(a.src + (unsigned)(r_off[i] + toff)) : zero;
+      }
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i)
+        rb[i] = (b_ok(i) && kok) ? ld16(a.wt + (unsigned)(b_off0 + 32 * i * b_row + kpos)) : zero;
+    } else {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
         // parity class: ny, nx are even by construction
         const int ny = r_y[i] + a.ph - kh, nx = r_x[i] + a.pw - kw;
-        sy = ny >> 1;
-        sx = nx >> 1;
-        ok = ok && ny >= 0 && nx >= 0;
-      } else {
-        const int ny = r_y[i] + a.ph - kh, nx = r_x[i] + a.pw - kw;
-        if (a.str == 1) {
-          sy = ny;
-          sx = nx;
-        } else {
-          sy = ny / a.str;
-          sx = nx / a.str;
-          ok = ok && ny >= 0 && nx >= 0 && sy * a.str == ny && sx * a.str == nx;
-        }
+        const int sy = ny >> 1, sx = nx >> 1;
+        const bool ok = kok && r_ok[i] && ny >= 0 && nx >= 0 && sy < a.sh_ && sx < a.sw_;
+        ra[i] = ok ? ld16(a.src + ((long)(r_img[i] * a.sh_ + sy) * a.sw_ + sx) * a.scs + a.sco + c) : zero;
       }
-      ok = ok && sy >= 0 && sy < a.sh_ && sx >= 0 && sx < a.sw_;
-      ra[i] = ok ? ld16(a.src + ((long)(r_img[i] * a.sh_ + sy) * a.sw_ + sx) * a.scs + a.sco + c) : zero;
-    }
-    // B rows n0 + q/8 (reduction-contiguous rows of RS * sc elements), at this thread's chunk position
-    const int tf = MODE == CV_DGRAD2 ? kh * a.s + kw : ta;
+      const int tf = kh * a.s + kw;
 #pragma unroll
-    for (int i = 0; i < B_CH; ++i) {
-      const int q = tid + 256 * i;
-      const int n = n0 + (q >> 3);
-      const bool ok = q < B_TOT && n < a.N && kok;
-      rb[i] = ok ? ld16(a.wt + ((long)n * RS + tf) * a.sc + c) : zero;
+      for (int i = 0; i < B_CH; ++i)
+        rb[i] = (b_ok(i) && kok) ? ld16(a.wt + (long)(b_off0 + 32 * i * b_row) + tf * a.sc + c) : zero;
     }
     advance();
   };
@@ -198,6 +217,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     __syncthreads();
   }
   for (int t = 0; t < ksteps; ++t) {
+    if constexpr (DB) set_stage(t & 1);
     if (t + 1 < ksteps) load();
 #pragma unroll
     for (int kk = 0; kk < CBK / 32; ++kk) {
@@ -214,10 +234,18 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    __syncthreads();
-    if (t + 1 < ksteps) {
-      store();
+    if constexpr (DB) {
+      if (t + 1 < ksteps) {
+        set_stage((t + 1) & 1);
+        store();  // the other stage: last read in step t-1, before the barrier that ended it
+      }
       __syncthreads();
+    } else {
+      __syncthreads();
+      if (t + 1 < ksteps) {
+        store();
+        __syncthreads();
+      }
     }
   }
 
@@ -306,7 +334,8 @@ static int conv_check(const adr_conv_desc* d) {
   ADR_REQUIRE(d->stride_h == d->stride_w && d->pad_h == d->pad_w, "conv: anisotropic stride/padding");
   const int ho = (d->h + 2 * d->pad_h - d->r) / d->stride_h + 1, wo = (d->w + 2 * d->pad_w - d->s) / d->stride_w + 1;
   ADR_REQUIRE(ho == d->ho && wo == d->wo, "conv: output size mismatch (%dx%d vs %dx%d)", d->ho, d->wo, ho, wo);
-  ADR_REQUIRE((long)d->n * d->h * d->w < (1l << 31) && (long)d->n * d->ho * d->wo < (1l << 31), "conv: too many pixels");
+  ADR_REQUIRE((long)d->n * d->h * d->w * d->x_cstride < (1l << 31) && (long)d->n * d->ho * d->wo * d->y_cstride < (1l << 31)
+              && (long)d->k * d->c * d->r * d->s < (1l << 31), "conv: tensor exceeds 2^31 elements (32-bit gather offsets)");
   return ADR_OK;
 }
 
@@ -344,6 +373,7 @@ extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, con
   const int bn = conv_pick_bn(g.N);
   g.ntiles = cdiv(g.N, bn);
   hipStream_t st = (hipStream_t)stream;
+  ADR_REQUIRE(d->stride_h == 1 || d->stride_h == 2, "conv dgrad (bf16 engine): stride %d", d->stride_h);
   if (d->stride_h == 2) {  // parity classes; the largest (even, even) class sizes the grid
     dim3 grid(cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM) * g.ntiles, 1, 4);
     launch_conv<CV_DGRAD2>(bn, grid, g, st);
