@@ -16,6 +16,8 @@
 // Epilogue: accumulators (+bias) are rounded to bf16 into an LDS image of the output tile, then written with
 // 16-byte row-contiguous stores; the optional train-mode BatchNorm partial sums (sum, sum of squares of the
 // stored values per column) are reduced from that image in a fixed order.
+#include <type_traits>
+
 #include "adr_common.h"
 
 namespace adr {
@@ -36,6 +38,7 @@ struct ConvArgs {
   int ktot;                    // reduction length = taps * sc
   int ntiles;
   int accumulate;
+  int src_bytes, wt_bytes;     // extents of src / wt (buffer-load range checks; < 2^31)
 };
 
 constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
@@ -129,7 +132,10 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
   const int RS = a.r * a.s;
   const int ksteps = (ktot + CBK - 1) / CBK;
 
-  u32x4 ra[A_CH], rb[B_CH];
+  // DB tiles keep two register stages: the global loads of step t+2 are issued while step t computes, so each
+  // load has two K-steps of MFMA work to land behind (one step for the single-buffered narrow tiles)
+  constexpr int NR = DB ? 2 : 1;
+  u32x4 ra_s[NR][A_CH], rb_s[NR][B_CH];
   const u32x4 zero = {0u, 0u, 0u, 0u};
   // Reduction-position decoder, advanced by CBK per k-step without integer division: this thread's chunk sits
   // at k = t*CBK + kc*8 = (tap ta, channel ca); (kh, kw) are the tap's kernel coordinates. The B rows use the
@@ -164,7 +170,14 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
   const int b_n = n0 + (tid >> 3);
   const int b_off0 = b_n * b_row;
   auto b_ok = [&](int i) { return tid + 256 * i < B_TOT && b_n + 32 * i < a.N; };
-  auto load = [&]() {
+  // LIN gathers go through buffer descriptors: a padding / out-of-range chunk gets an offset past the
+  // descriptor's range and the hardware returns zeros — no branch and no zero moves per chunk
+  constexpr unsigned OOR = 0x7FFFFFF0u;
+  const __amdgpu_buffer_rsrc_t src_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, a.src_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, a.wt_bytes, 0x00020000);
+  auto load = [&](auto S) {
+    u32x4(&ra)[A_CH] = ra_s[decltype(S)::value];
+    u32x4(&rb)[B_CH] = rb_s[decltype(S)::value];
     const bool kok = ta < ntaps;
     const int c = ca;
     if constexpr (LIN) {
@@ -174,11 +187,12 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
       for (int i = 0; i < A_CH; ++i) {
         const bool ok = kok && r_ok[i] && (unsigned)(r_y[i] + dy) < (unsigned)a.sh_ &&
                         (unsigned)(r_x[i] + dx) < (unsigned)a.sw_;
-        ra[i] = ok ? ld16(a.src + (unsigned)(r_off[i] + toff)) : zero;
+        ra[i] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, ok ? (unsigned)(r_off[i] + toff) * 2u : OOR, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i)
-        rb[i] = (b_ok(i) && kok) ? ld16(a.wt + (unsigned)(b_off0 + 32 * i * b_row + kpos)) : zero;
+        rb[i] = __builtin_amdgcn_raw_buffer_load_b128(
+            wt_rs, (b_ok(i) && kok) ? (unsigned)(b_off0 + 32 * i * b_row + kpos) * 2u : OOR, 0, 0);
     } else {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
@@ -195,7 +209,9 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
     }
     advance();
   };
-  auto store = [&]() {
+  auto store = [&](auto S) {
+    const u32x4(&ra)[A_CH] = ra_s[decltype(S)::value];
+    const u32x4(&rb)[B_CH] = rb_s[decltype(S)::value];
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) st16(&As[((tid >> 3) + 32 * i) * CLD + kc * 8], ra[i]);
 #pragma unroll
@@ -211,14 +227,9 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
-  if (ksteps > 0) {
-    load();
-    store();
-    __syncthreads();
-  }
-  for (int t = 0; t < ksteps; ++t) {
-    if constexpr (DB) set_stage(t & 1);
-    if (t + 1 < ksteps) load();
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, NR - 1>;
+  auto compute = [&]() {
 #pragma unroll
     for (int kk = 0; kk < CBK / 32; ++kk) {
       bf16x8 fa[TM], fb[TN];
@@ -234,16 +245,43 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if constexpr (DB) {
+  };
+  if constexpr (DB) {
+    // stage s (LDS) and register set s alternate; step t computes stage t&1 while set t&1 receives step t+2
+    if (ksteps > 0) {
+      load(S0{});
+      store(S0{});
+      if (ksteps > 1) load(S1{});
+      __syncthreads();
+    }
+    auto step = [&](int t, auto S) {
+      constexpr int cur = decltype(S)::value;
+      using SO = std::integral_constant<int, 1 - cur>;
+      set_stage(cur);
+      if (t + 2 < ksteps) load(S);  // set cur was stored into its stage one step ago
+      compute();
       if (t + 1 < ksteps) {
-        set_stage((t + 1) & 1);
-        store();  // the other stage: last read in step t-1, before the barrier that ended it
+        set_stage(1 - cur);
+        store(SO{});  // step t+1 (loaded two steps ago) into the other stage, last read in step t-1
       }
       __syncthreads();
-    } else {
+    };
+    for (int t = 0; t < ksteps; t += 2) {
+      step(t, S0{});
+      if (t + 1 < ksteps) step(t + 1, S1{});
+    }
+  } else {
+    if (ksteps > 0) {
+      load(S0{});
+      store(S0{});
+      __syncthreads();
+    }
+    for (int t = 0; t < ksteps; ++t) {
+      if (t + 1 < ksteps) load(S0{});
+      compute();
       __syncthreads();
       if (t + 1 < ksteps) {
-        store();
+        store(S0{});
         __syncthreads();
       }
     }
@@ -334,8 +372,8 @@ static int conv_check(const adr_conv_desc* d) {
   ADR_REQUIRE(d->stride_h == d->stride_w && d->pad_h == d->pad_w, "conv: anisotropic stride/padding");
   const int ho = (d->h + 2 * d->pad_h - d->r) / d->stride_h + 1, wo = (d->w + 2 * d->pad_w - d->s) / d->stride_w + 1;
   ADR_REQUIRE(ho == d->ho && wo == d->wo, "conv: output size mismatch (%dx%d vs %dx%d)", d->ho, d->wo, ho, wo);
-  ADR_REQUIRE((long)d->n * d->h * d->w * d->x_cstride < (1l << 31) && (long)d->n * d->ho * d->wo * d->y_cstride < (1l << 31)
-              && (long)d->k * d->c * d->r * d->s < (1l << 31), "conv: tensor exceeds 2^31 elements (32-bit gather offsets)");
+  ADR_REQUIRE((long)d->n * d->h * d->w * d->x_cstride < (1l << 30) && (long)d->n * d->ho * d->wo * d->y_cstride < (1l << 30)
+              && (long)d->k * d->c * d->r * d->s < (1l << 30), "conv: tensor exceeds 2^30 elements (32-bit buffer offsets)");
   return ADR_OK;
 }
 
@@ -353,6 +391,8 @@ extern "C" int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const 
   g.rh = d->ho; g.rw = d->wo; g.ocs = d->y_cstride; g.oco = d->y_coff;
   g.r = d->r; g.s = d->s; g.str = d->stride_h; g.ph = d->pad_h; g.pw = d->pad_w;
   g.N = d->k; g.ktot = d->r * d->s * d->c; g.accumulate = accumulate;
+  g.src_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
+  g.wt_bytes = (int)(2l * g.N * g.ktot);
   const int bn = conv_pick_bn(g.N);
   g.ntiles = cdiv(g.N, bn);
   dim3 grid(cdiv((long)d->n * d->ho * d->wo, CBM) * g.ntiles);
@@ -370,6 +410,8 @@ extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, con
   g.rh = d->h; g.rw = d->w; g.ocs = d->x_cstride; g.oco = d->x_coff;
   g.r = d->r; g.s = d->s; g.str = d->stride_h; g.ph = d->pad_h; g.pw = d->pad_w;
   g.N = d->c; g.ktot = d->r * d->s * d->k; g.accumulate = accumulate;
+  g.src_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
+  g.wt_bytes = (int)(2l * g.N * g.ktot);
   const int bn = conv_pick_bn(g.N);
   g.ntiles = cdiv(g.N, bn);
   hipStream_t st = (hipStream_t)stream;
