@@ -17,7 +17,11 @@ def _prefixed(P, pre="m"):
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("c1,c2,k,s,hw", [(16, 32, 3, 2, 24), (32, 64, 1, 1, 20), (64, 128, 3, 1, 13),
                                            (128, 256, 3, 2, 20), (48, 16, 1, 1, 9), (8, 16, 3, 1, 7),
-                                           (32, 32, 3, 2, 15), (16, 16, 1, 2, 9)])
+                                           (32, 32, 3, 2, 15), (16, 16, 1, 2, 9),
+                                           # 3x3 halo-tile path (adr_conv.hip conv3_kernel): 16- and 8-wide tiles,
+                                           # ragged last tile row band, one and several 32-channel chunks
+                                           (64, 64, 3, 1, 16), (64, 128, 3, 1, 24), (32, 64, 3, 1, 40),
+                                           (128, 64, 3, 1, 16)])
 def test_conv_bn_silu(dtype, c1, c2, k, s, hw):
     from adrefine.nn.modules import Conv
     m = Conv(c1, c2, k, s)

@@ -488,7 +488,8 @@ class Conv2dFn(torch.autograd.Function):
         y = empty_act(N, K, Ho, Wo, dtype, x.device)
         stats = None
         if want_stats:
-            tiles = lib.adr_conv2d_fwd_stat_tiles(ctypes.byref(d))
+            tiles = (lib.adr_conv2d_fwd_bf16_stat_tiles if _engine2(d, d.c) else lib.adr_conv2d_fwd_stat_tiles)(
+                ctypes.byref(d))
             stats = torch.empty(tiles * 2 * K, dtype=torch.float32, device=x.device)
         bf = b.detach().float().contiguous() if b is not None else None
         conv_fwd(d, xp, wp.data_ptr(), fptr(bf), y.data_ptr(), fptr(stats))

@@ -349,6 +349,193 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// 3x3 / stride 1 / pad 1 convolutions (FWD, and DGRAD which is the same contraction with the taps mirrored):
+// the implicit GEMM above gathers every input pixel once per tap, i.e. nine times through L2, and its K-steps
+// are too short to hide those loads. Here a block owns a TH x TW output tile (TH*TW = 128 rows) and 64 output
+// channels; per 32-channel chunk it stages the (TH+2) x (TW+2) input halo tile and the 9-tap weight slab in LDS
+// ONCE and runs all nine taps out of LDS (72 MFMAs per wave per chunk), while the next chunk's loads are in
+// flight in registers. A fragment row for tap (kh, kw) is the halo pixel (py + kh, px + kw) (mirrored for
+// DGRAD), so the gather costs one LDS address add per tap.
+constexpr int C3_CK = 32, C3_LD = C3_CK;  // chunk channels; unpadded 64-byte LDS rows, XOR-swizzled:
+// the 16-byte chunk kq of row r sits in slot kq ^ ((r >> 2) & 3), so any 16 consecutive rows a ds_read_b128 lane
+// group reads cover 16 disjoint bank quads (48 KB per block: 3 blocks per CU)
+__device__ __forceinline__ int c3_swz(int row, int kq) { return row * C3_LD + ((kq ^ ((row >> 2) & 3)) << 3); }
+
+template <int TW, bool DG>
+__global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
+  constexpr int BN = 64, TH = 128 / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
+  constexpr int A_TOT = NPIX * (C3_CK / 8), A_CH = (A_TOT + 255) / 256;
+  constexpr int B_CH = 9 * BN * (C3_CK / 8) / 256;  // = 9: chunk i of a thread is tap i
+  constexpr int TM = 2, TN = 4;                     // 4 waves along M (32 rows each) x all 64 columns
+  constexpr int OPITCH = BN + 8, CPR = BN / 8, RPP = 256 / CPR;
+  constexpr int SMEM_A = NPIX * C3_LD, SMEM_B = 9 * BN * C3_LD;
+  constexpr int SMEM_AB = 2 * (SMEM_A + SMEM_B), SMEM_O = 2 * 128 * OPITCH, SMEM_R = 2 * RPP * BN * 4;
+  constexpr int SMEM_BYTES = SMEM_AB > SMEM_O ? (SMEM_AB > SMEM_R ? SMEM_AB : SMEM_R) : (SMEM_O > SMEM_R ? SMEM_O : SMEM_R);
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[SMEM_BYTES];
+  __bf16* As = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* Bs = As + SMEM_A;
+  float (*red)[RPP][BN] = reinterpret_cast<float (*)[RPP][BN]>(lds_raw);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.rh, W = a.rw;
+  const int tx = W / TW, ty = (H + TH - 1) / TH;
+  const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x - (blockIdx.x / a.ntiles) * a.ntiles;
+  const int n0 = nt * BN;
+  const int img = mt / (tx * ty), trem = mt - img * (tx * ty);
+  const int y0 = (trem / tx) * TH, x0 = (trem - (trem / tx) * tx) * TW;
+
+  // halo chunks of this thread: e = tid + 256 i -> halo pixel e / 4, channel quad e % 4
+  constexpr unsigned OOR = 0x7FFFFFF0u;
+  const __amdgpu_buffer_rsrc_t src_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, a.src_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, a.wt_bytes, 0x00020000);
+  int a_off[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int e = tid + 256 * i, q = e >> 2, hy = q / HWW, hx = q - (q / HWW) * HWW;
+    const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
+    const bool ok = e < A_TOT && gy >= 0 && gy < a.sh_ && gx >= 0 && gx < a.sw_;
+    a_off[i] = ok ? ((img * a.sh_ + gy) * a.sw_ + gx) * a.scs + a.sco + (e & 3) * 8 : -1;
+  }
+  const bool b_ok = n0 + (tid >> 2) < a.N;
+  const int b_off = (n0 + (tid >> 2)) * 9 * a.sc + (tid & 3) * 8;  // + tap * sc + c0
+
+  u32x4 ra[A_CH], rb[B_CH];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i)
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, a_off[i] >= 0 ? (unsigned)(a_off[i] + c0) * 2u : OOR, 0, 0);
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i)
+      rb[i] = __builtin_amdgcn_raw_buffer_load_b128(wt_rs, b_ok ? (unsigned)(b_off + i * a.sc + c0) * 2u : OOR, 0, 0);
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int e = tid + 256 * i;
+      if (e < A_TOT) st16(&As[c3_swz(e >> 2, e & 3)], ra[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) st16(&Bs[c3_swz(i * BN + (tid >> 2), tid & 3)], rb[i]);
+  };
+
+  const int wr0 = wave * 32;
+  int fq[TM];  // halo pixel of this lane's fragment row, tap (0, 0)
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = wr0 + i * 16 + (lane & 15);
+    fq[i] = (p / TW) * HWW + (p % TW);
+  }
+  const int kq = lane >> 4;
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.sc / C3_CK;
+  load(0);
+  for (int ch = 0; ch < nch; ++ch) {
+    store();
+    __syncthreads();
+    if (ch + 1 < nch) load((ch + 1) * C3_CK);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int kh = t / 3, kw = t % 3;
+      const int dq = DG ? (2 - kh) * HWW + (2 - kw) : kh * HWW + kw;
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(&As[c3_swz(fq[i] + dq, kq)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[c3_swz(t * BN + j * 16 + (lane & 15), kq)]);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue (as conv_bf16_kernel): bf16 tile image in LDS, 16-byte row stores, optional BN partials ----
+  __bf16* Os = reinterpret_cast<__bf16*>(lds_raw);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = j * 16 + (lane & 15);
+    const float b = (a.bias && n0 + col < a.N) ? a.bias[n0 + col] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) Os[(wr0 + i * 16 + 4 * (lane >> 4) + e) * OPITCH + col] = (__bf16)(acc[i][j][e] + b);
+  }
+  __syncthreads();
+  const int oc = tid % CPR, orow = tid / CPR;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  const bool col_ok = n0 + oc * 8 < a.N;
+  for (int r = orow; r < 128; r += RPP) {
+    const int y = y0 + r / TW;
+    if (y >= H || !col_ok) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
+    __bf16* dst = a.out + ((long)(img * H + y) * W + x0 + r % TW) * a.ocs + a.oco + n0 + oc * 8;
+    if (a.accumulate) {
+      const u32x4 o = ld16(dst);
+      const __bf16* ov = reinterpret_cast<const __bf16*>(&o);
+      __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e]);
+    }
+    st16(dst, v);
+    if (a.stats) {
+      const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = (float)sv[e];
+        s1[e] += f;
+        s2[e] += f * f;
+      }
+    }
+  }
+  if (a.stats) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[0][orow][oc * 8 + e] = s1[e];
+      red[1][orow][oc * 8 + e] = s2[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      float x1 = 0.f, x2 = 0.f;
+      for (int g = 0; g < RPP; ++g) {
+        x1 += red[0][g][tid];
+        x2 += red[1][g][tid];
+      }
+      a.stats[(long)mt * 2 * a.N + n0 + tid] = x1;
+      a.stats[(long)mt * 2 * a.N + a.N + n0 + tid] = x2;
+    }
+  }
+}
+
+// tile width of the 3x3 path for this geometry, or 0 when it does not apply
+static int conv3_tw(const adr_conv_desc* d, int red_ch, int out_ch) {
+  if (d->r != 3 || d->s != 3 || d->stride_h != 1 || d->pad_h != 1 || red_ch % C3_CK || out_ch % 64) return 0;
+  if (d->w % 16 == 0 && d->h >= 8) return 16;
+  if (d->w % 8 == 0) return 8;
+  return 0;
+}
+static int conv3_tiles(const adr_conv_desc* d, int tw) {
+  return d->n * ((d->h + 128 / tw - 1) / (128 / tw)) * (d->w / tw);
+}
+template <bool DG>
+static void launch_conv3(int tw, const adr_conv_desc* d, ConvArgs& g, hipStream_t st) {
+  g.ntiles = g.N / 64;
+  dim3 grid(conv3_tiles(d, tw) * g.ntiles);
+  if (tw == 16) hipLaunchKernelGGL((conv3_kernel<16, DG>), grid, dim3(256), 0, st, g);
+  else hipLaunchKernelGGL((conv3_kernel<8, DG>), grid, dim3(256), 0, st, g);
+}
+
 template <int MODE>
 static void launch_conv(int bn, dim3 grid, const ConvArgs& g, hipStream_t st) {
   switch (bn) {
@@ -393,6 +580,10 @@ extern "C" int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const 
   g.N = d->k; g.ktot = d->r * d->s * d->c; g.accumulate = accumulate;
   g.src_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
   g.wt_bytes = (int)(2l * g.N * g.ktot);
+  if (const int tw = conv3_tw(d, d->c, d->k)) {
+    launch_conv3<false>(tw, d, g, (hipStream_t)stream);
+    return check_launch("adr_conv2d_fwd_bf16");
+  }
   const int bn = conv_pick_bn(g.N);
   g.ntiles = cdiv(g.N, bn);
   dim3 grid(cdiv((long)d->n * d->ho * d->wo, CBM) * g.ntiles);
@@ -419,6 +610,8 @@ extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, con
   if (d->stride_h == 2) {  // parity classes; the largest (even, even) class sizes the grid
     dim3 grid(cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM) * g.ntiles, 1, 4);
     launch_conv<CV_DGRAD2>(bn, grid, g, st);
+  } else if (const int tw = conv3_tw(d, d->k, d->c)) {
+    launch_conv3<true>(tw, d, g, st);
   } else {
     dim3 grid(cdiv((long)d->n * d->h * d->w, CBM) * g.ntiles);
     launch_conv<CV_DGRAD>(bn, grid, g, st);
@@ -426,4 +619,7 @@ extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, con
   return check_launch("adr_conv2d_dgrad_bf16");
 }
 
-extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) { return cdiv((long)d->n * d->ho * d->wo, CBM); }
+extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) {
+  if (const int tw = conv3_tw(d, d->c, d->k)) return conv3_tiles(d, tw);
+  return cdiv((long)d->n * d->ho * d->wo, CBM);
+}
