@@ -14,4 +14,9 @@ dgrad2 64 80 80 64 64 3 3 1
 dgrad2 64 40 40 128 128 3 3 1
 dgrad2 64 80 80 128 64 1 1 1
 dgrad2 64 160 160 32 64 3 3 2
+wgrad 64 80 80 64 64 3 3 1
+wgrad 64 80 80 128 128 3 3 2
+wgrad 64 320 320 16 32 3 3 2
+wgrad 64 40 40 128 128 1 1 1
+wgrad 64 80 80 64 32 3 3 1
 SHAPES

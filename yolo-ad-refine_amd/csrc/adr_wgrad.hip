@@ -32,6 +32,7 @@ struct WgArgs {
   long red_per_split;
   int ksteps;
   int ctiles;  // input-channel tiles per tap
+  int x_bytes, dy_bytes;  // buffer-descriptor extents (< 2^31): out-of-range offsets read as zero
   int accumulate;
 };
 
@@ -74,7 +75,9 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
   const int hw = a.ho * a.wo;
 
   u32x4 ra[A_CH], rb[B_CH];
-  const u32x4 zero = {0u, 0u, 0u, 0u};
+  constexpr unsigned OOR = 0x7FFFFFF0u;
+  const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dy_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
   // per B chunk: the output pixel (img, oy, ox) of its reduction row, advanced by R rows per k-step without
   // integer division (the row of a chunk is fixed across steps: pl = q / (BN / 8))
   int b_img[B_CH], b_oy[B_CH], b_ox[B_CH];
@@ -98,7 +101,7 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
       const long p = p0 + pl;
       const int co = m0 + cc * 8;
       const bool ok = q < A_CHT && p < pend && co < a.k;
-      ra[i] = ok ? ld16(a.dy + p * a.ycs + a.yco + co) : zero;
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(dy_rs, ok ? (unsigned)((int)p * a.ycs + a.yco + co) * 2u : OOR, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
@@ -109,7 +112,8 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
       bool ok = q < B_CHT && p < pend && ci < a.c;
       const int iy = b_oy[i] * a.sh - a.ph + kh, ix = b_ox[i] * a.sw - a.pw + kw;
       ok = ok && iy >= 0 && iy < a.h && ix >= 0 && ix < a.w;
-      rb[i] = ok ? ld16(a.x + ((long)(b_img[i] * a.h + iy) * a.w + ix) * a.xcs + a.xco + ci) : zero;
+      rb[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          x_rs, ok ? (unsigned)(((b_img[i] * a.h + iy) * a.w + ix) * a.xcs + a.xco + ci) * 2u : OOR, 0, 0);
       b_ox[i] += R;  // next k-step's row
       while (b_ox[i] >= a.wo) {
         b_ox[i] -= a.wo;
@@ -267,6 +271,8 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
 
 int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
                       const WgPlan& p, hipStream_t st) {
+  ADR_REQUIRE(2l * d->n * d->h * d->w * d->x_cstride < (1l << 31) && 2l * d->n * d->ho * d->wo * d->y_cstride < (1l << 31),
+              "conv wgrad (bf16): operand exceeds 2 GB (32-bit buffer offsets)");
   WgArgs g;
   g.x = (const __bf16*)x;
   g.dy = (const __bf16*)dy;
@@ -279,6 +285,8 @@ int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, flo
   g.ksteps = (int)(p.per / p.R);
   g.ctiles = cdiv(d->c, p.bn);
   g.accumulate = accumulate;
+  g.x_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
+  g.dy_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
   dim3 grid(p.tiles, p.splits);
   switch (p.bm) {
     case 16: launch_bm<16>(p.bn, grid, g, st); break;
