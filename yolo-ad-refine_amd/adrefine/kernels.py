@@ -445,7 +445,7 @@ def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device):
         RS_ *= v
     Cp = max(C_, cpad)
     out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
-    tok = _t0("void adr::wgrad_reduce_kernel<true>(float const*, long, float*, long, int, int, adr::Unpack)",
+    tok = _t0("adr::wgrad_reduce_kernel<true, OUT, SL> (split reduce + unpack)",
               4 * stride * (splits + 1), stride * splits, shp)
     lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, K_, C_, Cp, RS_, 0, acc, stream())
     _t1(tok)

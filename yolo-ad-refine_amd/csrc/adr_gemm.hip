@@ -419,32 +419,38 @@ __global__ void __launch_bounds__(256) gemm_kernel(GemmArgs a) {
 // outputs; its 8 slices of 32 threads each sum every 8th split (coalesced 128-byte rows, 4 loads in flight),
 // then the slices are combined in LDS in a fixed order — parallel over splits as well as outputs, so a
 // small-output / many-split reduction still fills the chip.
-constexpr int WR_OUT = 32, WR_SL = 8;
 struct Unpack {  // UNPACK: output i = (k*RS + t)*Cp + c of the KRSC partials lands at the (K,C,RS) parameter slot
   int K, C, Cp, RS, transpose_kc;
 };
-template <bool UNPACK>
+// OUT outputs x SL split slices per 256-thread block; many-split reductions use 16 x 16 so that each thread sums
+// fewer splits, with 8 loads in flight (fixed order per configuration: deterministic)
+template <bool UNPACK, int OUT, int SL>
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, long stride,
                                                            float* __restrict__ dw, long n, int splits, int accumulate,
                                                            Unpack u) {
-  __shared__ float sh[WR_SL][WR_OUT];
-  const int o = threadIdx.x % WR_OUT, sl = threadIdx.x / WR_OUT;
-  const long i = (long)blockIdx.x * WR_OUT + o;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  if (i < n) {
-    int k = sl, q = 0;
-    for (; k + 3 * WR_SL < splits; k += 4 * WR_SL) {
+  __shared__ float sh[SL][OUT];
+  const int o = threadIdx.x % OUT, sl = threadIdx.x / OUT;
+  const long i = (long)blockIdx.x * OUT + o;
+  constexpr int U = 8;
+  float acc[U];
 #pragma unroll
-      for (int v = 0; v < 4; ++v) acc[v] += part[(long)(k + v * WR_SL) * stride + i];
+  for (int v = 0; v < U; ++v) acc[v] = 0.f;
+  if (i < n) {
+    int k = sl;
+    for (; k + (U - 1) * SL < splits; k += U * SL) {
+#pragma unroll
+      for (int v = 0; v < U; ++v) acc[v] += part[(long)(k + v * SL) * stride + i];
     }
-    for (; k < splits; k += WR_SL, ++q) acc[q & 3] += part[(long)k * stride + i];
+#pragma unroll
+    for (int v = 0; v < U; ++v)
+      if (k + v * SL < splits) acc[v] += part[(long)(k + v * SL) * stride + i];
   }
-  sh[sl][o] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+  sh[sl][o] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
   __syncthreads();
   if (sl == 0 && i < n) {
     float s = 0.f;
 #pragma unroll
-    for (int q = 0; q < WR_SL; ++q) s += sh[q][o];
+    for (int q = 0; q < SL; ++q) s += sh[q][o];
     long di = i;
     if constexpr (UNPACK) {
       const int c = (int)(i % u.Cp);
@@ -613,8 +619,12 @@ extern "C" int adr_conv2d_wgrad_partials(const adr_conv_desc* d, const void* x, 
 
 extern "C" int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accumulate, void* stream) {
   ADR_REQUIRE(n > 0 && splits >= 1, "wgrad_reduce: n=%ld splits=%d", n, splits);
-  hipLaunchKernelGGL(wgrad_reduce_kernel<false>, dim3(cdiv(n, WR_OUT)), dim3(256), 0, (hipStream_t)stream, part, n, dw,
-                     n, splits, accumulate, Unpack{});
+  if (splits >= 256)
+    hipLaunchKernelGGL((wgrad_reduce_kernel<false, 16, 16>), dim3(cdiv(n, 16)), dim3(256), 0, (hipStream_t)stream, part,
+                       n, dw, n, splits, accumulate, Unpack{});
+  else
+    hipLaunchKernelGGL((wgrad_reduce_kernel<false, 32, 8>), dim3(cdiv(n, 32)), dim3(256), 0, (hipStream_t)stream, part,
+                       n, dw, n, splits, accumulate, Unpack{});
   return check_launch("adr_wgrad_reduce");
 }
 
@@ -623,8 +633,12 @@ extern "C" int adr_wgrad_reduce_unpack(const float* part, long split_stride, int
   const long n = (long)K * RS * Cp;
   ADR_REQUIRE(n > 0 && splits >= 1 && C <= Cp && split_stride >= n, "wgrad_reduce_unpack: K=%d C=%d Cp=%d RS=%d", K, C,
               Cp, RS);
-  hipLaunchKernelGGL(wgrad_reduce_kernel<true>, dim3(cdiv(n, WR_OUT)), dim3(256), 0, (hipStream_t)stream, part,
-                     split_stride, dst, n, splits, accumulate, Unpack{K, C, Cp, RS, transpose_kc});
+  if (splits >= 256)
+    hipLaunchKernelGGL((wgrad_reduce_kernel<true, 16, 16>), dim3(cdiv(n, 16)), dim3(256), 0, (hipStream_t)stream, part,
+                       split_stride, dst, n, splits, accumulate, Unpack{K, C, Cp, RS, transpose_kc});
+  else
+    hipLaunchKernelGGL((wgrad_reduce_kernel<true, 32, 8>), dim3(cdiv(n, 32)), dim3(256), 0, (hipStream_t)stream, part,
+                       split_stride, dst, n, splits, accumulate, Unpack{K, C, Cp, RS, transpose_kc});
   return check_launch("adr_wgrad_reduce_unpack");
 }
 
