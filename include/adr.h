@@ -65,6 +65,9 @@ int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w_krs
 int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
                           int accumulate, void* stream);
 int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d);
+/* Mangled name of the kernel the bf16 engine launches for this contraction (dgrad != 0: the data gradient),
+ * written to buf (len >= 64) — the label the bench's roofline and rocprofv3 share. */
+int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, char* buf, int len);
 /* dx = conv_transpose(dy, w) (+ bias[c]) (+ dx if accumulate).  Also ConvTranspose2d forward
  * (nn.ConvTranspose2d weight (Cin_T, Cout_T, R, S) channels_last == KRSC of the equivalent conv). */
 int adr_conv2d_dgrad(const adr_conv_desc* d, const void* dy, const void* w, const float* bias, void* dx,

@@ -3,7 +3,7 @@ set -e
 OLD=abtree/yolo-ad-refine_amd/adrefine/lib/libadr_hip.so
 while read -r m args; do
   echo -n "new "; timeout -k 5 60 python scripts/conv_micro.py $m $args 2>/dev/null
-  echo -n "old "; ADR_LIB=$OLD timeout -k 5 60 python scripts/conv_micro.py $m $args 2>/dev/null
+  echo -n "old "; ADR_LIB=$OLD ADR_HEADER=abtree/include/adr.h timeout -k 5 60 python scripts/conv_micro.py $m $args 2>/dev/null
 done <<'SHAPES'
 fwd2 64 80 80 64 64 3 3 1
 fwd2 64 40 40 128 128 3 3 1

@@ -284,14 +284,17 @@ def _engine2(d, red_channels):
     return d.dtype == BF16 and d.stride_h == d.stride_w and d.pad_h == d.pad_w
 
 
-def _conv2_symbol(bn, mode):
-    return f"_ZN3adr16conv_bf16_kernelILi{bn}ELi{mode}EEEvNS_8ConvArgsE"
+def _conv2_symbol(d, dgrad):
+    """The bf16 engine's kernel for this contraction, as the library dispatches it (roofline label)."""
+    buf = ctypes.create_string_buffer(128)
+    lib.adr_conv2d_bf16_kernel_symbol(ctypes.byref(d), int(dgrad), buf, 128)
+    return buf.value.decode()
 
 
 def conv_fwd(d, xp, wp, bias, yp, stats=None, accumulate=0):
     """y (+)= conv(x, w_krsc) (+bias); optional per-128-row-tile BN partial statistics of the stored values."""
     e2 = _engine2(d, d.c)
-    sym = _conv2_symbol(_bn_of(d.k), 0) if e2 else _gemm_symbol(d.dtype, _bn_of(d.k), 0)
+    sym = "" if _TIMING is None else _conv2_symbol(d, False) if e2 else _gemm_symbol(d.dtype, _bn_of(d.k), 0)
     rep = _reps(accumulate)
     tok = _t0(sym, *_conv_work(d), _shape(d, "fwd") if _TIMING is not None else "", rep)
     fn = lib.adr_conv2d_fwd_bf16 if e2 else lib.adr_conv2d_fwd
@@ -306,7 +309,8 @@ def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0):
     krsc, crsk = wpair
     e2 = crsk is not None and _engine2(d, d.k)
     mode = 2 if d.stride_h == 2 else 1
-    sym = _conv2_symbol(_bn_of(d.c), mode) if e2 else _gemm_symbol(d.dtype, _bn_of(d.c), 3 if mode == 2 else 1)
+    sym = "" if _TIMING is None else (_conv2_symbol(d, True) if e2 else
+                                      _gemm_symbol(d.dtype, _bn_of(d.c), 3 if mode == 2 else 1))
     rep = _reps(accumulate)
     tok = _t0(sym, *_conv_work(d), _shape(d, "dgrad") if _TIMING is not None else "", rep)
     for _ in range(rep):

@@ -16,6 +16,7 @@
 // Epilogue: accumulators (+bias) are rounded to bf16 into an LDS image of the output tile, then written with
 // 16-byte row-contiguous stores; the optional train-mode BatchNorm partial sums (sum, sum of squares of the
 // stored values per column) are reduced from that image in a fixed order.
+#include <cstdio>
 #include <type_traits>
 
 #include "adr_common.h"
@@ -564,6 +565,23 @@ static int conv_check(const adr_conv_desc* d) {
   return ADR_OK;
 }
 
+// The kernel a bf16 contraction runs on — shared by the launchers and adr_conv2d_bf16_kernel_symbol, so the
+// roofline labels cannot drift from the dispatch.
+struct ConvPlan {
+  int tw;    // > 0: conv3_kernel<tw, dgrad> (3x3 stride-1 halo tiles)
+  int bn;    // else conv_bf16_kernel<bn, mode>
+  int mode;  // CV_FWD / CV_DGRAD / CV_DGRAD2
+};
+static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad) {
+  ConvPlan p{0, 0, dgrad ? (d->stride_h == 2 ? CV_DGRAD2 : CV_DGRAD) : CV_FWD};
+  const int red = dgrad ? d->k : d->c, out = dgrad ? d->c : d->k;
+  if (p.mode != CV_DGRAD2) p.tw = conv3_tw(d, red, out);
+  // 1x1 contractions are two or three K-steps long: 64-wide column tiles (4 waves/SIMD) hide their load latency
+  // better than 128-wide ones (2 waves/SIMD), at the cost of reading the A rows once per column tile (L2 hits)
+  p.bn = (d->r * d->s == 1 && out > 64) ? 64 : conv_pick_bn(out);
+  return p;
+}
+
 }  // namespace adr
 
 using namespace adr;
@@ -580,11 +598,12 @@ extern "C" int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const 
   g.N = d->k; g.ktot = d->r * d->s * d->c; g.accumulate = accumulate;
   g.src_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
   g.wt_bytes = (int)(2l * g.N * g.ktot);
-  if (const int tw = conv3_tw(d, d->c, d->k)) {
-    launch_conv3<false>(tw, d, g, (hipStream_t)stream);
+  const ConvPlan pl = conv_plan(d, false);
+  if (pl.tw) {
+    launch_conv3<false>(pl.tw, d, g, (hipStream_t)stream);
     return check_launch("adr_conv2d_fwd_bf16");
   }
-  const int bn = conv_pick_bn(g.N);
+  const int bn = pl.bn;
   g.ntiles = cdiv(g.N, bn);
   dim3 grid(cdiv((long)d->n * d->ho * d->wo, CBM) * g.ntiles);
   launch_conv<CV_FWD>(bn, grid, g, (hipStream_t)stream);
@@ -603,15 +622,16 @@ extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, con
   g.N = d->c; g.ktot = d->r * d->s * d->k; g.accumulate = accumulate;
   g.src_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
   g.wt_bytes = (int)(2l * g.N * g.ktot);
-  const int bn = conv_pick_bn(g.N);
+  ADR_REQUIRE(d->stride_h == 1 || d->stride_h == 2, "conv dgrad (bf16 engine): stride %d", d->stride_h);
+  const ConvPlan pl = conv_plan(d, true);
+  const int bn = pl.bn;
   g.ntiles = cdiv(g.N, bn);
   hipStream_t st = (hipStream_t)stream;
-  ADR_REQUIRE(d->stride_h == 1 || d->stride_h == 2, "conv dgrad (bf16 engine): stride %d", d->stride_h);
-  if (d->stride_h == 2) {  // parity classes; the largest (even, even) class sizes the grid
+  if (pl.mode == CV_DGRAD2) {  // parity classes; the largest (even, even) class sizes the grid
     dim3 grid(cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM) * g.ntiles, 1, 4);
     launch_conv<CV_DGRAD2>(bn, grid, g, st);
-  } else if (const int tw = conv3_tw(d, d->k, d->c)) {
-    launch_conv3<true>(tw, d, g, st);
+  } else if (pl.tw) {
+    launch_conv3<true>(pl.tw, d, g, st);
   } else {
     dim3 grid(cdiv((long)d->n * d->h * d->w, CBM) * g.ntiles);
     launch_conv<CV_DGRAD>(bn, grid, g, st);
@@ -620,6 +640,17 @@ extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, con
 }
 
 extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) {
-  if (const int tw = conv3_tw(d, d->c, d->k)) return conv3_tiles(d, tw);
+  const ConvPlan pl = conv_plan(d, false);
+  if (pl.tw) return conv3_tiles(d, pl.tw);
   return cdiv((long)d->n * d->ho * d->wo, CBM);
+}
+
+extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, char* buf, int len) {
+  ADR_REQUIRE(d && buf && len >= 64, "conv kernel symbol: bad arguments");
+  const ConvPlan pl = conv_plan(d, dgrad != 0);
+  if (pl.tw)
+    snprintf(buf, len, "_ZN3adr12conv3_kernelILi%dELb%dEEEvNS_8ConvArgsE", pl.tw, dgrad ? 1 : 0);
+  else
+    snprintf(buf, len, "_ZN3adr16conv_bf16_kernelILi%dELi%dEEEvNS_8ConvArgsE", pl.bn, pl.mode);
+  return ADR_OK;
 }
