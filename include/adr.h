@@ -89,6 +89,17 @@ int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accum
  * (k, c, rs) (or (c, k, rs) with transpose_kc), padded channels c >= C dropped. */
 int adr_wgrad_reduce_unpack(const float* part, long split_stride, int splits, float* dst, int K, int C, int Cp,
                             int RS, int transpose_kc, int accumulate, void* stream);
+/* Deferred WGRAD reductions, many per launch (<= 56 entries each; more are split into several launches): each
+ * entry is reduced and unpacked in the split order adr_wgrad_reduce_unpack uses below 256 splits.
+ * `entries` is a host array (its contents travel in the kernel arguments). Two entries of one call must not
+ * share a destination. */
+typedef struct {
+  const float* part;   /* [splits][K*RS*Cp] partials */
+  float* dst;          /* (K, C, RS) parameter gradient (or (C, K, RS) with transpose_kc) */
+  long split_stride;   /* floats between consecutive splits' slabs */
+  int splits, K, C, Cp, RS, transpose_kc, accumulate, pad_;
+} adr_wgrad_reduce_entry;
+int adr_wgrad_reduce_batched(const adr_wgrad_reduce_entry* entries, int count, void* stream);
 
 
 /* ---------------------------------------------------------------------------------------------------------

@@ -131,7 +131,8 @@ class FusedTrainer:
         with K.pack_scope(self.packs):
             self.packs.pack_all()  # every conv weight's bf16 operand copies, one launch (no-op on the first step)
             loss, items = self.model(batch)
-            loss.backward()
+            with K.defer_wgrad():  # conv weight-gradient split reductions: a few batched launches at the end
+                loss.backward()
         return items
 
     def _set_hyper(self):

@@ -423,6 +423,56 @@ def pack_weight2(w: torch.Tensor, dtype, cpad: int = 0, transpose_kc: int = 0, k
     return krsc, crsk
 
 
+class WgradEntry(ctypes.Structure):
+    """adr_wgrad_reduce_entry (include/adr.h)."""
+    _fields_ = [("part", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("split_stride", ctypes.c_long)] + [
+        (n, ctypes.c_int) for n in ("splits", "K", "C", "Cp", "RS", "transpose_kc", "accumulate", "pad_")]
+
+
+class WgradDeferral:
+    """Collects the split-K reductions of every conv weight gradient that lands in the trainer's gradient arena
+    and runs them as a few batched launches (adr_wgrad_reduce_batched) when the backward pass ends, instead of
+    one launch per conv. The partial slabs stay alive until then. A second entry for the same destination (a
+    weight shared by several calls, e.g. the head's shared convs) flushes the pending batch first, so every
+    destination's contributions still accumulate in program order."""
+
+    def __init__(self):
+        self.entries, self.keep, self.dsts = [], [], set()
+
+    def add(self, ws, stride, splits, dst, K_, C_, Cp, RS_, transpose_kc, acc):
+        dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
+        if dst in self.dsts:
+            self.flush()
+        self.entries.append(WgradEntry(ws.data_ptr(), dst, stride, splits, K_, C_, Cp, RS_, transpose_kc, acc, 0))
+        self.keep.append(ws)
+        self.dsts.add(dst)
+
+    def flush(self):
+        if self.entries:
+            arr = (WgradEntry * len(self.entries))(*self.entries)
+            lib.adr_wgrad_reduce_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.entries), stream())
+        self.entries, self.keep, self.dsts = [], [], set()
+
+
+_DEFER = None  # the active WgradDeferral (set by the trainer around its backward pass)
+
+
+def defer_wgrad():
+    """Context manager: defer arena-bound WGRAD reductions to one batched flush at exit."""
+    import contextlib
+
+    @contextlib.contextmanager
+    def _cm():
+        global _DEFER
+        prev, _DEFER = _DEFER, WgradDeferral()
+        try:
+            yield _DEFER
+            _DEFER.flush()
+        finally:
+            _DEFER = prev
+    return _cm()
+
+
 def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device):
     """Weight gradient of a conv contraction straight into its parameter's gradient destination: the split-K
     WGRAD GEMM writes [split][K][RS][C] fp32 slabs, and one fused reduce+unpack kernel sums the splits in a
@@ -449,6 +499,9 @@ def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device):
         RS_ *= v
     Cp = max(C_, cpad)
     out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
+    if _DEFER is not None and acc and _TIMING is None:
+        _DEFER.add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
+        return grad_ret(param, out)
     tok = _t0("adr::wgrad_reduce_kernel<true, OUT, SL> (split reduce + unpack)",
               4 * stride * (splits + 1), stride * splits, shp)
     lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, K_, C_, Cp, RS_, 0, acc, stream())

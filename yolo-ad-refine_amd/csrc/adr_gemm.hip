@@ -463,6 +463,52 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// Many WGRAD reductions in one launch (the trainer defers them to the end of the backward pass): a block's
+// entry is found from the per-entry block offsets; each entry is reduced exactly as wgrad_reduce_kernel<true, 32,
+// 8> would (same split order), so deferring changes no result. The entries ride in the kernel arguments.
+constexpr int RB_MAX = 56;
+struct RedBatch {
+  adr_wgrad_reduce_entry e[RB_MAX];
+  int start[RB_MAX + 1];
+  int count;
+};
+__global__ void __launch_bounds__(256) wgrad_reduce_batched_kernel(RedBatch b) {
+  constexpr int OUT = 32, SL = 8, U = 8;
+  int j = 0;
+  while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  const adr_wgrad_reduce_entry& en = b.e[j];
+  __shared__ float sh[SL][OUT];
+  const int o = threadIdx.x % OUT, sl = threadIdx.x / OUT;
+  const long i = (long)(blockIdx.x - b.start[j]) * OUT + o;
+  const long n = (long)en.K * en.RS * en.Cp;
+  float acc[U];
+#pragma unroll
+  for (int v = 0; v < U; ++v) acc[v] = 0.f;
+  if (i < n) {
+    int k = sl;
+    for (; k + (U - 1) * SL < en.splits; k += U * SL) {
+#pragma unroll
+      for (int v = 0; v < U; ++v) acc[v] += en.part[(long)(k + v * SL) * en.split_stride + i];
+    }
+#pragma unroll
+    for (int v = 0; v < U; ++v)
+      if (k + v * SL < en.splits) acc[v] += en.part[(long)(k + v * SL) * en.split_stride + i];
+  }
+  sh[sl][o] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
+  __syncthreads();
+  if (sl == 0 && i < n) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < SL; ++q) s += sh[q][o];
+    const int c = (int)(i % en.Cp);
+    const long r = i / en.Cp;
+    const int t = (int)(r % en.RS), kk = (int)(r / en.RS);
+    if (c >= en.C) return;
+    const long di = en.transpose_kc ? ((long)c * en.K + kk) * en.RS + t : ((long)kk * en.C + c) * en.RS + t;
+    en.dst[di] = en.accumulate ? en.dst[di] + s : s;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------------------------
@@ -640,6 +686,31 @@ extern "C" int adr_wgrad_reduce_unpack(const float* part, long split_stride, int
     hipLaunchKernelGGL((wgrad_reduce_kernel<true, 32, 8>), dim3(cdiv(n, 32)), dim3(256), 0, (hipStream_t)stream, part,
                        split_stride, dst, n, splits, accumulate, Unpack{K, C, Cp, RS, transpose_kc});
   return check_launch("adr_wgrad_reduce_unpack");
+}
+
+extern "C" int adr_wgrad_reduce_batched(const adr_wgrad_reduce_entry* entries, int count, void* stream) {
+  ADR_REQUIRE(count >= 0 && (count == 0 || entries), "wgrad_reduce_batched: count=%d", count);
+  for (int b0 = 0; b0 < count; b0 += RB_MAX) {
+    RedBatch rb{};
+    rb.count = count - b0 < RB_MAX ? count - b0 : RB_MAX;
+    int blocks = 0;
+    for (int j = 0; j < rb.count; ++j) {
+      const adr_wgrad_reduce_entry& en = entries[b0 + j];
+      const long n = (long)en.K * en.RS * en.Cp;
+      ADR_REQUIRE(en.part && en.dst && n > 0 && en.splits >= 1 && en.C <= en.Cp && en.split_stride >= n,
+                  "wgrad_reduce_batched: entry %d (K=%d C=%d Cp=%d RS=%d splits=%d)", b0 + j, en.K, en.C, en.Cp,
+                  en.RS, en.splits);
+      for (int q = 0; q < j; ++q)  // same destination twice in one launch would race: the caller must split
+        ADR_REQUIRE(rb.e[q].dst != en.dst, "wgrad_reduce_batched: entries %d and %d share a destination", b0 + q,
+                    b0 + j);
+      rb.e[j] = en;
+      rb.start[j] = blocks;
+      blocks += (int)cdiv(n, 32);
+    }
+    rb.start[rb.count] = blocks;
+    hipLaunchKernelGGL(wgrad_reduce_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rb);
+  }
+  return check_launch("adr_wgrad_reduce_batched");
 }
 
 extern "C" int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const void* dy, float* dw, int accumulate,
