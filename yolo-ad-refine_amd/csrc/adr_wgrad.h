@@ -15,7 +15,8 @@ __host__ __device__ constexpr int wg_ku(int bm, int bn) {
 }
 struct WgPlan {
   int bm, bn, R, tiles, splits;
-  long per;  // reduction rows per split (multiple of R)
+  long per;  // reduction rows per split (multiple of R); for the 3x3 halo kernel: output tiles per split
+  int tw3;   // > 0: 3x3 stride-1 halo-tile kernel (wgrad3_kernel<tw3>) with `per` 128-pixel tiles per split
 };
 WgPlan wgrad_bf16_plan(const adr_conv_desc* d);
 int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,

@@ -232,6 +232,126 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// 3x3 / stride-1 / pad-1 weight gradient on 2-D output tiles (the WGRAD counterpart of adr_conv.hip's
+// conv3_kernel): per 128-pixel TH x TW tile, the dy tile (64 output channels) and the (TH+2) x (TW+2) input
+// halo (32 input channels) are staged in LDS ONCE and all nine taps accumulate from them — the per-tap kernel
+// above re-gathers x and re-reads dy for every tap. Wave w owns output channels k0 + 16w .. +15 for all nine
+// taps and both 16-channel input halves (18 accumulators); the MFMA reduction runs over pixels, 32 per step,
+// fragments read with the transposing ds_read_b64_tr_b16 (a B row is the lane's pixel shifted by the tap in the
+// halo image). Split over tiles; partials [split][K][9][C] as the general kernel writes them.
+template <int TW>
+__global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
+  constexpr int TH = 128 / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
+  constexpr int KB = 64, CK = 32;
+  constexpr int PD = KB + 16, PX = CK + 16;  // LDS pitches (elements): odd multiples of 32 bytes
+  constexpr int D_CH = 128 * KB / 8 / 256;   // 4 dy chunks per thread
+  constexpr int X_TOT = NPIX * CK / 8, X_CH = (X_TOT + 255) / 256;
+  __shared__ __attribute__((aligned(16))) __bf16 Ds[128 * PD];
+  __shared__ __attribute__((aligned(16))) __bf16 Xs[NPIX * PX];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ctiles = a.c / CK;
+  const int kt = blockIdx.x / ctiles, ct = blockIdx.x - (blockIdx.x / ctiles) * ctiles;
+  const int k0 = kt * KB, c0 = ct * CK;
+  const int H = a.ho, W = a.wo;
+  const int tx = W / TW, ty = (H + TH - 1) / TH, ntile = a.n * tx * ty;
+  const int t_beg = blockIdx.y * (int)a.red_per_split;
+  const int t_end = min(ntile, t_beg + (int)a.red_per_split);
+
+  constexpr unsigned OOR = 0x7FFFFFF0u;
+  const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dy_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
+  u32x4 rd[D_CH], rx[X_CH];
+  auto load = [&](int tile) {
+    const int img = tile / (tx * ty), trem = tile - img * (tx * ty);
+    const int y0 = (trem / tx) * TH, x0 = (trem - (trem / tx) * tx) * TW;
+#pragma unroll
+    for (int i = 0; i < D_CH; ++i) {
+      const int e = tid + 256 * i, p = e >> 3, kq = e & 7;
+      const int y = y0 + p / TW, xx = x0 + p % TW;
+      const bool ok = y < H;
+      rd[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          dy_rs, ok ? (unsigned)(((img * H + y) * W + xx) * a.ycs + a.yco + k0 + kq * 8) * 2u : OOR, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < X_CH; ++i) {
+      const int e = tid + 256 * i, q = e >> 2, cq = e & 3;
+      const int hy = q / HWW, hx = q - (q / HWW) * HWW;
+      const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
+      const bool ok = e < X_TOT && gy >= 0 && gy < a.h && gx >= 0 && gx < a.w;
+      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          x_rs, ok ? (unsigned)(((img * a.h + gy) * a.w + gx) * a.xcs + a.xco + c0 + cq * 8) * 2u : OOR, 0, 0);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < D_CH; ++i) {
+      const int e = tid + 256 * i;
+      st16(&Ds[(e >> 3) * PD + (e & 7) * 8], rd[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < X_CH; ++i) {
+      const int e = tid + 256 * i;
+      if (e < X_TOT) st16(&Xs[(e >> 2) * PX + (e & 3) * 8], rx[i]);
+    }
+  };
+
+  // transposed-read lane roles (see the header comment of this file): row 4g + q4 (+16), column 4 p4
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  f32x4 acc[9][2];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (t_beg < t_end) load(t_beg);
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    store();
+    __syncthreads();
+    if (tile + 1 < t_end) load(tile + 1);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int plo = ks * 32 + 4 * g + q4, phi = plo + 16;
+      const __bf16* da = Ds + wave * 16 + 4 * p4;
+      v4s lo = tr_read(da + plo * PD), hi = tr_read(da + phi * PD);
+      v4s both[2] = {lo, hi};
+      const bf16x8 fa = *reinterpret_cast<bf16x8*>(both);
+      const int qlo = (plo / TW) * HWW + plo % TW, qhi = (phi / TW) * HWW + phi % TW;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int dq = (t / 3) * HWW + (t % 3);
+#pragma unroll
+        for (int cf = 0; cf < 2; ++cf) {
+          const __bf16* xb = Xs + cf * 16 + 4 * p4;
+          v4s blo = tr_read(xb + (qlo + dq) * PX), bhi = tr_read(xb + (qhi + dq) * PX);
+          v4s bb[2] = {blo, bhi};
+          acc[t][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, *reinterpret_cast<bf16x8*>(bb), acc[t][cf], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  float* part = a.out + (long)blockIdx.y * a.k * (9L * a.c);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int cf = 0; cf < 2; ++cf)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = k0 + wave * 16 + 4 * (lane >> 4) + e, ci = c0 + cf * 16 + (lane & 15);
+        float* o = part + ((long)co * 9 + t) * a.c + ci;
+        *o = a.accumulate ? *o + acc[t][cf][e] : acc[t][cf][e];
+      }
+}
+
+static int wg3_tw(const adr_conv_desc* d) {
+  if (d->r != 3 || d->s != 3 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 1 || d->pad_w != 1) return 0;
+  if (d->c % 32 || d->k % 64) return 0;
+  if (d->wo % 16 == 0 && d->ho >= 8) return 16;
+  if (d->wo % 8 == 0) return 8;
+  return 0;
+}
+
 static int wg_pick16(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128; }
 
 template <int BM>
@@ -248,6 +368,25 @@ static void launch_bm(int bn, dim3 grid, const WgArgs& g, hipStream_t st) {
 
 WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   WgPlan p;
+  p.tw3 = wg3_tw(d);
+  if (p.tw3) {
+    const int th = 128 / p.tw3;
+    const long ntile = (long)d->n * ((d->ho + th - 1) / th) * (d->wo / p.tw3);
+    p.bm = 64;
+    p.bn = 32;
+    p.R = 128;
+    p.tiles = (d->k / 64) * (d->c / 32);
+    long s = (768 + p.tiles - 1) / p.tiles;                      // ~3 workgroups per CU
+    const long by_work = ntile / 4;                              // >= 4 tiles per split
+    const long by_bytes = (64l << 20) / ((long)d->k * 9 * d->c * 4);
+    if (s > by_work) s = by_work;
+    if (s > by_bytes) s = by_bytes;
+    if (s < 1) s = 1;
+    const long per = (ntile + s - 1) / s;
+    p.splits = (int)((ntile + per - 1) / per);
+    p.per = per;
+    return p;
+  }
   p.bm = wg_pick16(d->k);
   p.bn = wg_pick16(d->c);
   const int wm = p.bm / 16 < 2 ? p.bm / 16 : 2, wn = p.bn / 16 < 2 ? p.bn / 16 : 2;
@@ -288,6 +427,11 @@ int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, flo
   g.x_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
   g.dy_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
   dim3 grid(p.tiles, p.splits);
+  if (p.tw3) {
+    if (p.tw3 == 16) hipLaunchKernelGGL(wgrad3_kernel<16>, grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL(wgrad3_kernel<8>, grid, dim3(256), 0, st, g);
+    return check_launch("adr_conv2d_wgrad(bf16, 3x3 halo)");
+  }
   switch (p.bm) {
     case 16: launch_bm<16>(p.bn, grid, g, st); break;
     case 32: launch_bm<32>(p.bn, grid, g, st); break;
