@@ -21,7 +21,7 @@ def _prefixed(P, pre="m"):
                                            # 3x3 halo-tile path (adr_conv.hip conv3_kernel): 16- and 8-wide tiles,
                                            # ragged last tile row band, one and several 32-channel chunks
                                            (64, 64, 3, 1, 16), (64, 128, 3, 1, 24), (32, 64, 3, 1, 40),
-                                           (128, 64, 3, 1, 16)])
+                                           (128, 64, 3, 1, 16), (64, 32, 3, 1, 16), (32, 32, 3, 1, 24)])
 def test_conv_bn_silu(dtype, c1, c2, k, s, hw):
     from adrefine.nn.modules import Conv
     m = Conv(c1, c2, k, s)

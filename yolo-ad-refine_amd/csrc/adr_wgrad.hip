@@ -240,18 +240,21 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
 // taps and both 16-channel input halves (18 accumulators); the MFMA reduction runs over pixels, 32 per step,
 // fragments read with the transposing ds_read_b64_tr_b16 (a B row is the lane's pixel shifted by the tap in the
 // halo image). Split over tiles; partials [split][K][9][C] as the general kernel writes them.
-template <int TW>
+template <int TW, int KF>
 __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
   constexpr int TH = 128 / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
-  constexpr int KB = 64, CK = 32;
+  constexpr int KB = 16 * KF, CK = 32;       // KF = 4: wave w = k fragment w, both c halves; KF = 2: wave w =
+  constexpr int NCF = KF == 4 ? 2 : 1;       // (k fragment w % 2, c half w / 2)
   constexpr int PD = KB + 16, PX = CK + 16;  // LDS pitches (elements): odd multiples of 32 bytes
-  constexpr int D_CH = 128 * KB / 8 / 256;   // 4 dy chunks per thread
+  constexpr int D_CH = 128 * KB / 8 / 256;   // dy chunks per thread
+  constexpr int KQ = KB / 8;                 // 16-byte chunks per dy pixel row
   constexpr int X_TOT = NPIX * CK / 8, X_CH = (X_TOT + 255) / 256;
   __shared__ __attribute__((aligned(16))) __bf16 Ds[128 * PD];
   __shared__ __attribute__((aligned(16))) __bf16 Xs[NPIX * PX];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ctiles = a.c / CK;
+  const int wkf = wave % KF, wcf = KF == 4 ? 0 : wave / KF;
   const int kt = blockIdx.x / ctiles, ct = blockIdx.x - (blockIdx.x / ctiles) * ctiles;
   const int k0 = kt * KB, c0 = ct * CK;
   const int H = a.ho, W = a.wo;
@@ -268,7 +271,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
     const int y0 = (trem / tx) * TH, x0 = (trem - (trem / tx) * tx) * TW;
 #pragma unroll
     for (int i = 0; i < D_CH; ++i) {
-      const int e = tid + 256 * i, p = e >> 3, kq = e & 7;
+      const int e = tid + 256 * i, p = e / KQ, kq = e % KQ;
       const int y = y0 + p / TW, xx = x0 + p % TW;
       const bool ok = y < H;
       rd[i] = __builtin_amdgcn_raw_buffer_load_b128(
@@ -288,7 +291,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
 #pragma unroll
     for (int i = 0; i < D_CH; ++i) {
       const int e = tid + 256 * i;
-      st16(&Ds[(e >> 3) * PD + (e & 7) * 8], rd[i]);
+      st16(&Ds[(e / KQ) * PD + (e % KQ) * 8], rd[i]);
     }
 #pragma unroll
     for (int i = 0; i < X_CH; ++i) {
@@ -299,9 +302,11 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
 
   // transposed-read lane roles (see the header comment of this file): row 4g + q4 (+16), column 4 p4
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
-  f32x4 acc[9][2];
+  f32x4 acc[9][NCF];
 #pragma unroll
-  for (int t = 0; t < 9; ++t) acc[t][0] = acc[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int cf = 0; cf < NCF; ++cf) acc[t][cf] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   if (t_beg < t_end) load(t_beg);
   for (int tile = t_beg; tile < t_end; ++tile) {
@@ -311,7 +316,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       const int plo = ks * 32 + 4 * g + q4, phi = plo + 16;
-      const __bf16* da = Ds + wave * 16 + 4 * p4;
+      const __bf16* da = Ds + wkf * 16 + 4 * p4;
       v4s lo = tr_read(da + plo * PD), hi = tr_read(da + phi * PD);
       v4s both[2] = {lo, hi};
       const bf16x8 fa = *reinterpret_cast<bf16x8*>(both);
@@ -320,8 +325,8 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
       for (int t = 0; t < 9; ++t) {
         const int dq = (t / 3) * HWW + (t % 3);
 #pragma unroll
-        for (int cf = 0; cf < 2; ++cf) {
-          const __bf16* xb = Xs + cf * 16 + 4 * p4;
+        for (int cf = 0; cf < NCF; ++cf) {
+          const __bf16* xb = Xs + (wcf + cf) * 16 + 4 * p4;
           v4s blo = tr_read(xb + (qlo + dq) * PX), bhi = tr_read(xb + (qhi + dq) * PX);
           v4s bb[2] = {blo, bhi};
           acc[t][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, *reinterpret_cast<bf16x8*>(bb), acc[t][cf], 0, 0, 0);
@@ -335,10 +340,10 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
-    for (int cf = 0; cf < 2; ++cf)
+    for (int cf = 0; cf < NCF; ++cf)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int co = k0 + wave * 16 + 4 * (lane >> 4) + e, ci = c0 + cf * 16 + (lane & 15);
+        const int co = k0 + wkf * 16 + 4 * (lane >> 4) + e, ci = c0 + (wcf + cf) * 16 + (lane & 15);
         float* o = part + ((long)co * 9 + t) * a.c + ci;
         *o = a.accumulate ? *o + acc[t][cf][e] : acc[t][cf][e];
       }
@@ -346,7 +351,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
 
 static int wg3_tw(const adr_conv_desc* d) {
   if (d->r != 3 || d->s != 3 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 1 || d->pad_w != 1) return 0;
-  if (d->c % 32 || d->k % 64) return 0;
+  if (d->c % 32 || d->k % 32) return 0;
   if (d->wo % 16 == 0 && d->ho >= 8) return 16;
   if (d->wo % 8 == 0) return 8;
   return 0;
@@ -372,10 +377,10 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   if (p.tw3) {
     const int th = 128 / p.tw3;
     const long ntile = (long)d->n * ((d->ho + th - 1) / th) * (d->wo / p.tw3);
-    p.bm = 64;
+    p.bm = d->k % 64 == 0 ? 64 : 32;  // k rows per block (KF = bm / 16)
     p.bn = 32;
     p.R = 128;
-    p.tiles = (d->k / 64) * (d->c / 32);
+    p.tiles = (d->k / p.bm) * (d->c / 32);
     long s = (768 + p.tiles - 1) / p.tiles;                      // ~3 workgroups per CU
     const long by_work = ntile / 4;                              // >= 4 tiles per split
     const long by_bytes = (64l << 20) / ((long)d->k * 9 * d->c * 4);
@@ -428,8 +433,13 @@ int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, flo
   g.dy_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
   dim3 grid(p.tiles, p.splits);
   if (p.tw3) {
-    if (p.tw3 == 16) hipLaunchKernelGGL(wgrad3_kernel<16>, grid, dim3(256), 0, st, g);
-    else hipLaunchKernelGGL(wgrad3_kernel<8>, grid, dim3(256), 0, st, g);
+    if (p.bm == 64) {
+      if (p.tw3 == 16) hipLaunchKernelGGL((wgrad3_kernel<16, 4>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((wgrad3_kernel<8, 4>), grid, dim3(256), 0, st, g);
+    } else {
+      if (p.tw3 == 16) hipLaunchKernelGGL((wgrad3_kernel<16, 2>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((wgrad3_kernel<8, 2>), grid, dim3(256), 0, st, g);
+    }
     return check_launch("adr_conv2d_wgrad(bf16, 3x3 halo)");
   }
   switch (p.bm) {
