@@ -44,6 +44,14 @@ struct ConvArgs {
 
 constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
 
+// XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin over the 8 XCDs (each with
+// its own L2), so the column tiles of one row tile — which read the same A rows — would land on different XCDs
+// and each fetch those rows from HBM. Renumbering so that consecutive logical ids share an XCD keeps them in one
+// L2 (grids that are not a multiple of 8 keep the identity order).
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+  return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
+}
+
 template <int BN, int MODE>
 __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvArgs a) {
   constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
@@ -76,7 +84,8 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WAVES_N, wn = wave % WAVES_N;
-  const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x % a.ntiles;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int mt = bid / a.ntiles, nt = bid % a.ntiles;
   const int m0 = mt * CBM, n0 = nt * BN;
 
   // ---- row space (and the parity class for stride-2 DGRAD) ----
@@ -381,7 +390,8 @@ __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int H = a.rh, W = a.rw;
   const int tx = W / TW, ty = (H + TH - 1) / TH;
-  const int mt = blockIdx.x / a.ntiles, nt = blockIdx.x - (blockIdx.x / a.ntiles) * a.ntiles;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int mt = bid / a.ntiles, nt = bid - (bid / a.ntiles) * a.ntiles;
   const int n0 = nt * BN;
   const int img = mt / (tx * ty), trem = mt - img * (tx * ty);
   const int y0 = (trem / tx) * TH, x0 = (trem - (trem / tx) * tx) * TW;
