@@ -40,6 +40,16 @@ __device__ __forceinline__ v4s tr_read(const __bf16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p));
 }
 
+// XCD-aware (tile, split) order: workgroups of one split read the same pixel rows of dy / x, so consecutive
+// logical ids — which walk the tiles of one split — are kept on one XCD (one L2). Returns (bx, by).
+__device__ __forceinline__ void wg_xcd_block(int& bx, int& by) {
+  const int gx = gridDim.x, nb = gx * gridDim.y;
+  int b = blockIdx.x + blockIdx.y * gx;
+  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
+  by = b / gx;
+  bx = b - by * gx;
+}
+
 template <int BM, int BN>
 __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
   constexpr int WM = BM / 16 < 2 ? BM / 16 : 2;
@@ -62,15 +72,16 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN), wm = wmn / WN, wn = wmn % WN;
   const int RS = a.r * a.s;
-  // blockIdx.x -> (co tile, tap, ci tile); blockIdx.y = split
-  int bid = blockIdx.x;
+  // block x -> (co tile, tap, ci tile); block y = split
+  int bid, split;
+  wg_xcd_block(bid, split);
   const int ct = bid % a.ctiles;
   bid /= a.ctiles;
   const int tap = bid % RS;
   const int mt = bid / RS;
   const int m0 = mt * BM, c0 = ct * BN;
   const int kh = tap / a.s, kw = tap % a.s;
-  const long pbeg = (long)blockIdx.y * a.red_per_split;
+  const long pbeg = (long)split * a.red_per_split;
   const long pend = min(a.red_total, pbeg + a.red_per_split);
   const int hw = a.ho * a.wo;
 
@@ -215,7 +226,7 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
           for (int s2 = 0; s2 < WK - 1; ++s2) acc[i][j][e] += red[s2 * BM * BN + rr * BN + cc];
         }
   }
-  float* part = a.out + (long)blockIdx.y * a.k * ((long)RS * a.c);
+  float* part = a.out + (long)split * a.k * ((long)RS * a.c);
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -255,11 +266,13 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ctiles = a.c / CK;
   const int wkf = wave % KF, wcf = KF == 4 ? 0 : wave / KF;
-  const int kt = blockIdx.x / ctiles, ct = blockIdx.x - (blockIdx.x / ctiles) * ctiles;
+  int bx, split;
+  wg_xcd_block(bx, split);
+  const int kt = bx / ctiles, ct = bx - (bx / ctiles) * ctiles;
   const int k0 = kt * KB, c0 = ct * CK;
   const int H = a.ho, W = a.wo;
   const int tx = W / TW, ty = (H + TH - 1) / TH, ntile = a.n * tx * ty;
-  const int t_beg = blockIdx.y * (int)a.red_per_split;
+  const int t_beg = split * (int)a.red_per_split;
   const int t_end = min(ntile, t_beg + (int)a.red_per_split);
 
   constexpr unsigned OOR = 0x7FFFFFF0u;
@@ -336,7 +349,7 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
     __syncthreads();
   }
 
-  float* part = a.out + (long)blockIdx.y * a.k * (9L * a.c);
+  float* part = a.out + (long)split * a.k * (9L * a.c);
 #pragma unroll
   for (int t = 0; t < 9; ++t)
 #pragma unroll
