@@ -96,7 +96,10 @@ constexpr int DCN_WPB = 4;             // waves per block
 template <typename T>
 __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, const T* om, int omcs, const T* dcols,
                                                          float* dx32, T* dom, int domcs, int N, int H, int W, int C) {
-  __shared__ float winbuf[DCN_WPB][DCN_WIN * DCN_WIN * DCN_CC];
+  // window cells 0..48 (ring row slot * 7 + column) plus one scratch cell (49) that absorbs the adds of corners
+  // outside the window or out of the image, so every corner update is the same unconditional LDS read-add-write
+  constexpr int NCELL = DCN_WIN * DCN_WIN, SCRATCH = NCELL;
+  __shared__ float winbuf[DCN_WPB][(NCELL + 1) * DCN_CC];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float* win = winbuf[wave];
   const int nstrip = (H + DCN_SL - 1) / DCN_SL;
@@ -106,28 +109,34 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
   const long r = sid / W;
   const int strip = (int)(r % nstrip), n = (int)(r / nstrip);
   const int hb = strip * DCN_SL, he = min(H, hb + DCN_SL);
-  const T* xb = x + (long)n * H * W * xcs;
+  const T* xb = x + (long)n * H * W * xcs;  // per-image bases; offsets inside an image are 32-bit
   float* dxb = dx32 + (long)n * H * W * C;
   const int wx0 = w - DCN_WIN / 2;  // window column 0
-  auto flush_row = [&](int y, int c) {  // add window row y to dx32 and clear it
-    float* row = win + (y % DCN_WIN + DCN_WIN) % DCN_WIN * DCN_WIN * DCN_CC;
+  auto flush_row = [&](int y, int slot, int c) {  // add window row y (ring slot) to dx32 and clear it
+    float* row = win + slot * DCN_WIN * DCN_CC;
+    const bool yok = y >= 0 && y < H && c < C;
 #pragma unroll
     for (int j = 0; j < DCN_WIN; ++j) {
       const float v = row[j * DCN_CC + lane];
       const int xx = wx0 + j;
-      if (y >= 0 && y < H && xx >= 0 && xx < W && c < C && v != 0.f) unsafeAtomicAdd(dxb + ((long)y * W + xx) * C + c, v);
+      if (yok && xx >= 0 && xx < W && v != 0.f) unsafeAtomicAdd(dxb + (y * W + xx) * C + c, v);
       row[j * DCN_CC + lane] = 0.f;
     }
   };
   for (int c0 = 0; c0 < C; c0 += DCN_CC) {
     const int c = c0 + lane;
     const int cc = min(c, C - 1);
-    for (int i = 0; i < DCN_WIN * DCN_WIN; ++i) win[i * DCN_CC + lane] = 0.f;
-    for (int h = hb; h < he; ++h) {
-      if (h > hb) flush_row(h - 1 - DCN_WIN / 2, c);  // row h-4 leaves the window (its slot becomes row h+3)
-      const long pix = ((long)n * H + h) * W + w;
-      const float omv = lane < 27 ? to_f(om[pix * omcs + lane]) : 0.f;
-      T* d = dom + pix * domcs;
+    for (int i = 0; i <= NCELL; ++i) win[i * DCN_CC + lane] = 0.f;
+    int hs = hb % DCN_WIN;  // ring slot of row h
+    for (int h = hb; h < he; ++h, hs = hs + 1 == DCN_WIN ? 0 : hs + 1) {
+      if (h > hb) {  // row h-4 leaves the window (its slot becomes row h+3)
+        const int fs = hs - 1 - DCN_WIN / 2;
+        flush_row(h - 1 - DCN_WIN / 2, fs < 0 ? fs + DCN_WIN : fs, c);
+      }
+      const int pix = (n * H + h) * W + w;
+      const float omv = lane < 27 ? to_f(om[(long)pix * omcs + lane]) : 0.f;
+      T* d = dom + (long)pix * domcs;
+      const T* gcol = dcols + (long)pix * 9 * C + cc;
 #pragma unroll 1
       for (int tg = 0; tg < 3; ++tg) {
         int y0[3], x0[3];
@@ -145,11 +154,11 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
         }
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
-          g[u] = to_f(dcols[(pix * 9 + tg * 3 + u) * C + cc]);
+          g[u] = to_f(gcol[(tg * 3 + u) * C]);
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const int yy = min(max(y0[u] + (q >> 1), 0), H - 1), xx = min(max(x0[u] + (q & 1), 0), W - 1);
-            const float v = to_f(xb[((long)yy * W + xx) * xcs + cc]);
+            const float v = to_f(xb[(yy * W + xx) * xcs + cc]);
             xv[u][q] = ok[u][q] ? v : 0.f;
           }
         }
@@ -170,15 +179,15 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
           const float gm = g[u] * m[u];
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            if (!ok[u][q]) continue;  // wave-uniform (depends on the pixel and tap only)
+            // wt is 0 for an invalid corner; the cell choice is wave-uniform (pixel and tap only)
             const int yy = y0[u] + (q >> 1), xx = x0[u] + (q & 1);
             const int dyw = yy - h, dxw = xx - wx0;
-            if (dyw >= -(DCN_WIN / 2) && dyw <= DCN_WIN / 2 && dxw >= 0 && dxw < DCN_WIN) {
-              float* cell = win + ((yy % DCN_WIN) * DCN_WIN + dxw) * DCN_CC + lane;
-              *cell += gm * wt[u][q];
-            } else if (c < C) {
-              unsafeAtomicAdd(dxb + ((long)yy * W + xx) * C + c, gm * wt[u][q]);
-            }
+            const bool inwin = dyw >= -(DCN_WIN / 2) && dyw <= DCN_WIN / 2 && dxw >= 0 && dxw < DCN_WIN;
+            int slot = hs + dyw;
+            slot = slot < 0 ? slot + DCN_WIN : (slot >= DCN_WIN ? slot - DCN_WIN : slot);
+            const int cell = (ok[u][q] && inwin) ? slot * DCN_WIN + dxw : SCRATCH;
+            win[cell * DCN_CC + lane] += gm * wt[u][q];
+            if (ok[u][q] && !inwin && c < C) unsafeAtomicAdd(dxb + (yy * W + xx) * C + c, gm * wt[u][q]);
           }
           const float spy = wave_sum_dpp(gm * sy), spx = wave_sum_dpp(gm * sx), smk = wave_sum_dpp(g[u] * val);
           if (lane == 0) {
@@ -193,7 +202,14 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
         }
       }
     }
-    for (int y = he - 1 - DCN_WIN / 2; y <= he - 1 + DCN_WIN / 2; ++y) flush_row(y, c);
+    {  // flush the rows still in the window: he-1-3 .. he-1+3, slots relative to the last row's slot
+      const int ls = (he - 1) % DCN_WIN;
+      for (int dy = -(DCN_WIN / 2); dy <= DCN_WIN / 2; ++dy) {
+        int sl = ls + dy;
+        sl = sl < 0 ? sl + DCN_WIN : (sl >= DCN_WIN ? sl - DCN_WIN : sl);
+        flush_row(he - 1 + dy, sl, c);
+      }
+    }
   }
 }
 
