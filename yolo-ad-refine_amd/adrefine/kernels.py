@@ -891,7 +891,9 @@ class CatFn(torch.autograd.Function):
         dy, _, _ = _v(dy)
         outs, off = [], 0
         for s in ctx.sizes:
-            outs.append(dy[:, off:off + s])
+            piece = dy[:, off:off + s]
+            piece._adr_excl = True  # a disjoint slice handed to exactly one consumer: FanOutFn may add into it
+            outs.append(piece)
             off += s
         return tuple(outs)
 
@@ -924,6 +926,9 @@ class SplitFn(torch.autograd.Function):
     def backward(ctx, *grads):
         sizes, shape, dtype = ctx.meta
         N, C, H, W = shape
+        joined = _adjacent_slices(grads, sizes, dtype)
+        if joined is not None:  # the pieces are consecutive channel slices of one buffer (a concat gradient)
+            return joined, None
         dev = next(g for g in grads if g is not None).device
         dx = empty_act(N, C, H, W, dtype, dev)
         off = 0
@@ -941,6 +946,56 @@ class SplitFn(torch.autograd.Function):
 
 def split(x, sizes):
     return SplitFn.apply(x, list(sizes))
+
+
+def _adjacent_slices(grads, sizes, dtype):
+    """One NHWC view spanning `grads` when they are consecutive channel slices of one buffer, else None."""
+    if any(g is None or g.dtype != dtype for g in grads):
+        return None
+    g0 = grads[0]
+    cs, es, st = g0.stride(3), g0.element_size(), g0.untyped_storage().data_ptr()
+    off = 0
+    for g, sz in zip(grads, sizes):
+        if g.shape[1] != sz or g.stride() != g0.stride() or g.untyped_storage().data_ptr() != st or \
+                g.data_ptr() != g0.data_ptr() + off * es or (g.stride(1) != 1 and sz > 1):
+            return None
+        off += sz
+    if off > cs:
+        return None
+    n, _, h, w = g0.shape
+    return torch.as_strided(g0, (n, off, h, w), g0.stride(), g0.storage_offset())
+
+
+class FanOutFn(torch.autograd.Function):
+    """x used by two consumers, as two views. Backward sums the two gradients with one adr_ew launch — into
+    the one that is an exclusive concat-gradient slice when there is one (no new buffer, and the split that
+    produced x can then hand its gradient back as a view) — instead of autograd's own accumulation, which is a
+    PyTorch add (a slow strided kernel on channel slices)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.set_materialize_grads(False)
+        return x[:, :], x[:, :]
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        if ga is None or gb is None:
+            return gb if ga is None else ga
+        if gb.dtype != ga.dtype:
+            gb = gb.to(ga.dtype)
+        if not getattr(ga, "_adr_excl", False) and getattr(gb, "_adr_excl", False):
+            ga, gb = gb, ga
+        va, vb = _v(ga), _v(gb)
+        if getattr(ga, "_adr_excl", False) and va[0] is ga:
+            _ew(EW_COPY, va, vb, accumulate=1)  # ga += gb in place
+            return ga
+        out = _new_like(va[0])
+        _ew(EW_AXPBY, (out, out.data_ptr(), out.shape[1]), va, vb)
+        return out
+
+
+def fanout(x):
+    return FanOutFn.apply(x)
 
 
 class AddFn(torch.autograd.Function):

@@ -48,7 +48,8 @@ class C2f(nn.Module):
     def forward(self, x):
         ys = list(K.split(self.cv1(x), (self.c, self.c)))  # chunk(2, 1): NHWC views, no copy
         for m in self.m:
-            ys.append(m(ys[-1]))
+            ys[-1], feed = K.fanout(ys[-1])  # used by the concat and by m: one gradient sum, in the concat slice
+            ys.append(m(feed))
         return self.cv2(K.cat(ys))
 
 
@@ -98,7 +99,8 @@ class SPPF(nn.Module):
     def forward(self, x):
         y = [self.cv1(x)]
         for _ in range(3):
-            y.append(K.maxpool(y[-1], self.k))
+            y[-1], feed = K.fanout(y[-1])
+            y.append(K.maxpool(feed, self.k))
         return self.cv2(K.cat(y))
 
 
