@@ -631,7 +631,7 @@ class BNActFn(torch.autograd.Function):
     """act(BatchNorm2d(y)) — train mode uses batch statistics (from the conv epilogue when given)."""
 
     @staticmethod
-    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps):
+    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None):
         dtype = y.dtype
         y, yp, ycs = nhwc(y)
         N, C, H, W = y.shape
@@ -651,8 +651,8 @@ class BNActFn(torch.autograd.Function):
         lib.adr_bn_finalize(fptr(stats) if training else None, P, C, float(N * HW), fptr(gamma.detach()),
                             fptr(beta.detach()), fptr(rm), fptr(rv), float(momentum), float(eps), int(training),
                             fptr(scale), fptr(shift), fptr(mean), fptr(rstd), stream())
-        z = empty_act(N, C, H, W, dtype, dev)
-        lib.adr_affine_act(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(z.data_ptr()), C, 0,
+        z, zp, zcs = _out_view(box, N, C, H, W, dtype, dev)
+        lib.adr_affine_act(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(zp), zcs, 0,
                            fptr(scale), fptr(shift), 0, ACT[act], N, HW, C, stream())
         ctx.save_for_backward(y, scale, shift, mean, rstd, gamma)
         ctx.meta = (act, training)
@@ -685,7 +685,7 @@ class BNActFn(torch.autograd.Function):
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
                                fptr(Cc), 0, 0, ACT[act], N, HW, C, 0, stream())
-        return dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None, None
+        return dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None, None, None
 
 
 class GNActFn(torch.autograd.Function):
@@ -821,9 +821,32 @@ def conv_transpose2d(x, w, b, stride, pad, out_pad):
     return ConvT2dFn.apply(x, w, b, stride, pad, out_pad)
 
 
-def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool):
+class OutBox:
+    """A caller-provided output view (a channel slice of a concat buffer) passed to a Function as a non-tensor
+    argument, so autograd does not treat the destination as an input being modified in place."""
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+
+def _out_view(box, N, C, H, W, dtype, dev):
+    """(tensor, ptr, channel stride) of the output: the boxed view, or a fresh NHWC activation."""
+    if box is None:
+        z = empty_act(N, C, H, W, dtype, dev)
+        return z, z.data_ptr(), C
+    z = box.t
+    if tuple(z.shape) != (N, C, H, W) or z.dtype != dtype:
+        raise RuntimeError(f"out view {tuple(z.shape)} {z.dtype} != {(N, C, H, W)} {dtype}")
+    z, ptr, cs = nhwc(z)
+    if z is not box.t:
+        raise RuntimeError("out view is not an NHWC channel slice")
+    return z, ptr, cs
+
+
+def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None):
     return BNActFn.apply(y, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, act, training, bn.momentum,
-                         bn.eps)
+                         bn.eps, None if out is None else OutBox(out))
 
 
 def gn_act(y, gn: torch.nn.Module, act: str):
@@ -870,21 +893,24 @@ class CatFn(torch.autograd.Function):
     """torch.cat(xs, dim=1) on NHWC: one copy per piece into the concat buffer; backward = zero-copy slices."""
 
     @staticmethod
-    def forward(ctx, *xs):
+    def forward(ctx, box, *xs):
         t0 = xs[0]
         N, _, H, W = t0.shape
         Ctot = sum(x.shape[1] for x in xs)
-        out = empty_act(N, Ctot, H, W, t0.dtype, t0.device)
+        out = empty_act(N, Ctot, H, W, t0.dtype, t0.device) if box is None else box.t
+        if tuple(out.shape) != (N, Ctot, H, W) or out.stride(1) != 1 or out.stride(3) != Ctot:
+            raise RuntimeError("cat: out buffer must be a whole NHWC activation of the concat shape")
         off = 0
         sizes = []
         for x in xs:
             v = _v(x)
             o = out[:, off:off + x.shape[1]]
-            _ew(EW_COPY, (o, o.data_ptr(), Ctot), v)
+            if not (v[1] == o.data_ptr() and v[2] == Ctot):  # producers that wrote in place need no copy
+                _ew(EW_COPY, (o, o.data_ptr(), Ctot), v)
             sizes.append(x.shape[1])
             off += x.shape[1]
         ctx.sizes = sizes
-        return out
+        return out if box is None else out[:, :]
 
     @staticmethod
     def backward(ctx, dy):
@@ -895,11 +921,13 @@ class CatFn(torch.autograd.Function):
             piece._adr_excl = True  # a disjoint slice handed to exactly one consumer: FanOutFn may add into it
             outs.append(piece)
             off += s
-        return tuple(outs)
+        return (None,) + tuple(outs)
 
 
-def cat(xs):
-    return CatFn.apply(*xs)
+def cat(xs, out=None):
+    """torch.cat(xs, 1). With `out` (an NHWC concat buffer whose slices some producers already wrote through
+    their own `out=` views), only the pieces that are not in place are copied."""
+    return CatFn.apply(None if out is None else OutBox(out), *xs)
 
 
 def zero_(t):
@@ -1002,23 +1030,24 @@ class AddFn(torch.autograd.Function):
     """a + b (+ c)."""
 
     @staticmethod
-    def forward(ctx, a, b, c=None):
+    def forward(ctx, a, b, c=None, box=None):
         va, vb = _v(a), _v(b)
-        out = _new_like(va[0])
+        N, C, H, W = va[0].shape
+        o = _out_view(box, N, C, H, W, va[0].dtype, va[0].device)
         if c is None:
-            _ew(EW_AXPBY, (out, out.data_ptr(), out.shape[1]), va, vb)
+            _ew(EW_AXPBY, o, va, vb)
         else:
-            _ew(EW_ADD3, (out, out.data_ptr(), out.shape[1]), va, vb, _v(c))
+            _ew(EW_ADD3, o, va, vb, _v(c))
         ctx.three = c is not None
-        return out
+        return o[0]
 
     @staticmethod
     def backward(ctx, dy):
-        return (dy, dy, dy) if ctx.three else (dy, dy, None)
+        return (dy, dy, dy, None) if ctx.three else (dy, dy, None, None)
 
 
-def add(a, b, c=None):
-    return AddFn.apply(a, b, c)
+def add(a, b, c=None, out=None):
+    return AddFn.apply(a, b, c, None if out is None else OutBox(out))
 
 
 class MulFn(torch.autograd.Function):

@@ -30,9 +30,12 @@ class Bottleneck(nn.Module):
         self.cv2 = Conv(c_, c2, k[1], 1, g=g)
         self.add = shortcut and c1 == c2
 
-    def forward(self, x):
-        y = self.cv2(self.cv1(x))
-        return K.add(x, y) if self.add else y
+    accepts_out = True
+
+    def forward(self, x, out=None):
+        if self.add:
+            return K.add(x, self.cv2(self.cv1(x)), out=out)
+        return self.cv2(self.cv1(x), out=out)
 
 
 class C2f(nn.Module):
@@ -46,11 +49,17 @@ class C2f(nn.Module):
         self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut, g, k=((3, 3), (3, 3)), e=1.0) for _ in range(n))
 
     def forward(self, x):
-        ys = list(K.split(self.cv1(x), (self.c, self.c)))  # chunk(2, 1): NHWC views, no copy
-        for m in self.m:
+        # cv1 and every block that can write its output through an `out=` view write straight into their slice
+        # of the concat buffer, so the concat copies only the pieces of blocks that cannot (e.g. MLCA bottlenecks)
+        N, _, H, W = x.shape
+        c, n = self.c, len(self.m)
+        buf = K.empty_act(N, (2 + n) * c, H, W, x.dtype, x.device)
+        ys = list(K.split(self.cv1(x, out=buf[:, :2 * c]), (c, c)))  # chunk(2, 1): NHWC views, no copy
+        for i, m in enumerate(self.m):
             ys[-1], feed = K.fanout(ys[-1])  # used by the concat and by m: one gradient sum, in the concat slice
-            ys.append(m(feed))
-        return self.cv2(K.cat(ys))
+            slot = buf[:, (2 + i) * c:(3 + i) * c]
+            ys.append(m(feed, out=slot) if getattr(m, "accepts_out", False) else m(feed))
+        return self.cv2(K.cat(ys, out=buf))
 
 
 class C3(nn.Module):
@@ -64,8 +73,10 @@ class C3(nn.Module):
         self.cv3 = Conv(2 * c_, c2, 1)
         self.m = nn.Sequential(*(Bottleneck(c_, c_, shortcut, g, k=((1, 1), (3, 3)), e=1.0) for _ in range(n)))
 
-    def forward(self, x):
-        return self.cv3(K.cat([self.m(self.cv1(x)), self.cv2(x)]))
+    accepts_out = True
+
+    def forward(self, x, out=None):
+        return self.cv3(K.cat([self.m(self.cv1(x)), self.cv2(x)]), out=out)
 
 
 class C3k(C3):
@@ -124,6 +135,8 @@ class MLCA(nn.Module):
 
 class Bottleneck_MLCA(Bottleneck):
     """Bottleneck with MLCA on the residual branch (reference block.py:1586-1594); residual add fused."""
+
+    accepts_out = False  # the fused MLCA kernel allocates its own output
 
     def __init__(self, c1, c2, shortcut=True, g=1, k=(3, 3), e=0.5):
         super().__init__(c1, c2, shortcut, g, k, e)

@@ -71,10 +71,12 @@ class Conv(nn.Module):
         self.bn = nn.BatchNorm2d(c2, eps=1e-3, momentum=0.03)  # initialize_weights (torch_utils.py:430-432)
         self.act_name = _act_name(act)
 
-    def forward(self, x):
+    accepts_out = True  # forward(x, out=view) writes the activation into a caller's concat slice
+
+    def forward(self, x, out=None):
         cv = self.conv
         y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight))
-        return K.bn_act(y, st, self.bn, self.act_name, self.training)
+        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out)
 
     def stem_ok(self):
         """The adr_stem kernels cover Conv(3, K in {16, 32, 64}, 3, 2) with pad 1 (every yaml's model.0)."""
