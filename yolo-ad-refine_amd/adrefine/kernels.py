@@ -455,6 +455,9 @@ class WgradDeferral:
 
 
 _DEFER = None  # the active WgradDeferral (set by the trainer around its backward pass)
+# Partial sets above this size are reduced right away (while still in L2) instead of deferred. Measured
+# (scripts/ab_env.sh): deferring all of them is fastest — 32.39 ms vs 32.49 / 32.64 / 32.70 ms for 16 / 4 / 1 MB.
+DEFER_MAX_BYTES = int(__import__("os").environ.get("ADR_DEFER_MAX_BYTES", 1 << 62))
 
 
 def defer_wgrad():
@@ -499,7 +502,7 @@ def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device):
         RS_ *= v
     Cp = max(C_, cpad)
     out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
-    if _DEFER is not None and acc and _TIMING is None:
+    if _DEFER is not None and acc and _TIMING is None and splits * stride * 4 <= DEFER_MAX_BYTES:
         _DEFER.add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
         return grad_ret(param, out)
     tok = _t0("adr::wgrad_reduce_kernel<true, OUT, SL> (split reduce + unpack)",
