@@ -254,14 +254,28 @@ __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, 
   }
 }
 
-// dw[c][t] = sum_chunks partial[chunk][t][c]
+// dw[c][t] = sum_chunks partial[chunk][t][c]; threads walk c fastest (coalesced partial rows), 8 chunks in flight
 __global__ void dw_w_reduce_kernel(const float* partial, int chunks, int C, int kk, float* dw, int accumulate) {
-  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= C * kk) return;
-  int c = i / kk, t = i % kk;
-  float s = 0.f;
-  for (int ch = 0; ch < chunks; ++ch) s += partial[((long)ch * kk + t) * C + c];
-  dw[i] = accumulate ? dw[i] + s : s;
+  const int t = i / C, c = i - (i / C) * C;
+  const float* p = partial + (long)t * C + c;
+  const long stride = (long)kk * C;
+  constexpr int U = 8;
+  float s[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) s[u] = 0.f;
+  int ch = 0;
+  for (; ch + U <= chunks; ch += U) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) s[u] += p[(long)(ch + u) * stride];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (ch + u < chunks) s[u] += p[(long)(ch + u) * stride];
+  const float r = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  const int o = c * kk + t;
+  dw[o] = accumulate ? dw[o] + r : r;
 }
 
 // ---------------- AdaptiveDynamicTanh ----------------
