@@ -271,7 +271,8 @@ __global__ void __launch_bounds__(256) gate_mlp_kernel(const float* in, float in
 }
 
 // backward: given dout (N,H2) -> din (N,Cin) (times in_scale) and dW1/db1/dW2/db2 summed over images.
-// One block, every phase thread-parallel over its outputs; the image sums run in a fixed order (deterministic).
+// Every block recomputes the small dz2 / dh stages in LDS; the output phases (din, dW1, dW2, db1, db2) are spread
+// over the grid, one thread per output, image sums in a fixed order (deterministic).
 // accumulate: weight/bias gradients are added to the destination (the trainer's gradient arena).
 __global__ void __launch_bounds__(256) gate_mlp_bwd_kernel(const float* in, float in_scale, int Cin, const float* W1,
                                                            int H1, int act1, const float* W2, int H2, int act2,
@@ -300,33 +301,35 @@ __global__ void __launch_bounds__(256) gate_mlp_bwd_kernel(const float* in, floa
     dh[i] = (act1 == 3) ? (hv > 0.f ? s : 0.f) : (act1 == 4 ? s * hv * (1.f - hv) : s);
   }
   __syncthreads();
-  for (int i = tid; i < N * Cin; i += 256) {
+  // the output phases are spread over the grid (every block recomputed dz2 / dh above, a few k MACs)
+  const int gt = blockIdx.x * 256 + tid, gs = gridDim.x * 256;
+  for (int i = gt; i < N * Cin; i += gs) {
     const int n = i / Cin, c = i % Cin;
     float s = 0.f;
     for (int j = 0; j < H1; ++j) s += W1[(long)j * Cin + c] * dh[n * H1 + j];
     din[i] = s * in_scale;
   }
-  for (int i = tid; i < H1 * Cin; i += 256) {
+  for (int i = gt; i < H1 * Cin; i += gs) {
     const int j = i / Cin, c = i % Cin;
     float s = 0.f;
     for (int n = 0; n < N; ++n) s += dh[n * H1 + j] * in[(long)n * Cin + c];
     s *= in_scale;
     dW1[i] = accumulate ? dW1[i] + s : s;
   }
-  for (int i = tid; i < H2 * H1; i += 256) {
+  for (int i = gt; i < H2 * H1; i += gs) {
     const int j = i / H1, c = i % H1;
     float s = 0.f;
     for (int n = 0; n < N; ++n) s += dz2[n * H2 + j] * hidden[(long)n * H1 + c];
     dW2[i] = accumulate ? dW2[i] + s : s;
   }
   if (db1)
-    for (int j = tid; j < H1; j += 256) {
+    for (int j = gt; j < H1; j += gs) {
       float s = 0.f;
       for (int n = 0; n < N; ++n) s += dh[n * H1 + j];
       db1[j] = accumulate ? db1[j] + s : s;
     }
   if (db2)
-    for (int j = tid; j < H2; j += 256) {
+    for (int j = gt; j < H2; j += gs) {
       float s = 0.f;
       for (int n = 0; n < N; ++n) s += dz2[n * H2 + j];
       db2[j] = accumulate ? db2[j] + s : s;
@@ -479,7 +482,7 @@ extern "C" int adr_gate_mlp_bwd(const float* in, float in_scale, int N, int Cin,
                                 int accumulate, void* stream) {
   size_t sm = (size_t)N * (H1 + H2) * sizeof(float);
   ADR_REQUIRE(sm <= 64 * 1024, "gate_mlp_bwd: N=%d H1=%d H2=%d exceed the LDS budget", N, H1, H2);
-  hipLaunchKernelGGL(gate_mlp_bwd_kernel, dim3(1), dim3(256), sm, (hipStream_t)stream, in, in_scale, Cin, W1, H1, act1,
+  hipLaunchKernelGGL(gate_mlp_bwd_kernel, dim3(16), dim3(256), sm, (hipStream_t)stream, in, in_scale, Cin, W1, H1, act1,
                      W2, H2, act2, hidden, out, dout, N, din, dW1, db1, dW2, db2, accumulate);
   return check_launch("adr_gate_mlp_bwd");
 }
