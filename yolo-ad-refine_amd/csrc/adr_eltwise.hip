@@ -109,7 +109,7 @@ __global__ void __launch_bounds__(256) bcast_mul_kernel(const T* x, int xcs, con
 
 // out[n][c] = sum over chunks of partial[n][chunk][which][c], then optionally summed over n and/or c.
 // One workgroup per output element (NT threads: 1024 when everything collapses to a scalar), fixed-order
-// per-thread strides + tree combine (deterministic); four loads in flight per thread.
+// per-thread strides + tree combine (deterministic); the full collapse walks rows division-free, 8 loads in flight.
 template <int NT>
 __global__ void __launch_bounds__(NT) nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which,
                                                          float* out, int sum_n, int sum_c, int accumulate) {
@@ -126,15 +126,30 @@ __global__ void __launch_bounds__(NT) nc_collapse_kernel(const float* partial, i
     return partial[((long)n * chunks + ch) * 2 * C + (long)which * C + c];
   };
   double s = 0.0;
-  int it = threadIdx.x;
-  for (; it + 3 * NT < items; it += 4 * NT) {
-    const float a = at(it), b = at(it + NT), c = at(it + 2 * NT), d = at(it + 3 * NT);
-    s += (double)a;
-    s += (double)b;
-    s += (double)c;
-    s += (double)d;
+  if (sum_n && sum_c && C <= NT && NT % C == 0) {
+    // full collapse: thread = (channel, row lane), rows walked without index division, 8 loads in flight
+    const int c = threadIdx.x % C, rstep = NT / C, R = N * chunks;
+    const float* p = partial + (long)which * C + c;
+    int r = threadIdx.x / C;
+    for (; r + 7 * rstep < R; r += 8 * rstep) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = p[(long)(r + u * rstep) * 2 * C];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += (double)v[u];
+    }
+    for (; r < R; r += rstep) s += (double)p[(long)r * 2 * C];
+  } else {
+    int it = threadIdx.x;
+    for (; it + 3 * NT < items; it += 4 * NT) {
+      const float a = at(it), b = at(it + NT), c = at(it + 2 * NT), d = at(it + 3 * NT);
+      s += (double)a;
+      s += (double)b;
+      s += (double)c;
+      s += (double)d;
+    }
+    for (; it < items; it += NT) s += (double)at(it);
   }
-  for (; it < items; it += NT) s += (double)at(it);
   __shared__ double sh[NT];
   sh[threadIdx.x] = s;
   __syncthreads();
