@@ -135,6 +135,14 @@ int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, const void* d
                        int accumulate, void* stream);
 /* out[c] (+)= sum_p partial[p][which][c] */
 int adr_partial_sum(const float* partial, int P, int C, int which, float* out, int accumulate, void* stream);
+/* Many adr_partial_sum reductions in one launch (<= 80 entries each; more are split), each reduced in the same
+ * order as adr_partial_sum. `entries` is a host array (kernel arguments); destinations must be distinct. */
+typedef struct {
+  const float* partial;
+  float* out;
+  int P, C, which, accumulate;
+} adr_psum_entry;
+int adr_partial_sum_batched(const adr_psum_entry* entries, int count, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Parameter plumbing: (K, C, R*S) fp32 <-> KRSC operand (compute dtype); transpose_kc=1 reads a

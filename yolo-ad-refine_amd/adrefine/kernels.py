@@ -437,6 +437,12 @@ class WgradEntry(ctypes.Structure):
         (n, ctypes.c_int) for n in ("splits", "K", "C", "Cp", "RS", "transpose_kc", "accumulate", "pad_")]
 
 
+class PsumEntry(ctypes.Structure):
+    """adr_psum_entry (include/adr.h)."""
+    _fields_ = [("partial", ctypes.c_void_p), ("out", ctypes.c_void_p)] + [
+        (n, ctypes.c_int) for n in ("P", "C", "which", "accumulate")]
+
+
 class WgradDeferral:
     """Collects the split-K reductions of every conv weight gradient that lands in the trainer's gradient arena
     and runs them as a few batched launches (adr_wgrad_reduce_batched) when the backward pass ends, instead of
@@ -446,6 +452,16 @@ class WgradDeferral:
 
     def __init__(self):
         self.entries, self.keep, self.dsts = [], [], set()
+        self.psums, self.pkeep, self.pdsts = [], [], set()
+
+    def add_psum(self, part, P, C, which, dst, acc):
+        """A bias gradient (adr_partial_sum into the arena), batched the same way."""
+        dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
+        if dst in self.pdsts:
+            self.flush()
+        self.psums.append(PsumEntry(part.data_ptr(), dst, P, C, which, acc))
+        self.pkeep.append(part)
+        self.pdsts.add(dst)
 
     def add(self, ws, stride, splits, dst, K_, C_, Cp, RS_, transpose_kc, acc):
         dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
@@ -459,7 +475,11 @@ class WgradDeferral:
         if self.entries:
             arr = (WgradEntry * len(self.entries))(*self.entries)
             lib.adr_wgrad_reduce_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.entries), stream())
+        if self.psums:
+            arr = (PsumEntry * len(self.psums))(*self.psums)
+            lib.adr_partial_sum_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.psums), stream())
         self.entries, self.keep, self.dsts = [], [], set()
+        self.psums, self.pkeep, self.pdsts = [], [], set()
 
 
 _DEFER = None  # the active WgradDeferral (set by the trainer around its backward pass)
@@ -530,7 +550,10 @@ def _bias_grad(dy, K, N, HW, cs, param=None):
                       _stats_rows(N, HW), fptr(part), stream())
     if param is not None:
         db, p, acc = grad_dst(param, K, dy.device)
-        lib.adr_partial_sum(fptr(part), N * chunks, K, 0, p, acc, stream())
+        if _DEFER is not None and acc and _TIMING is None:
+            _DEFER.add_psum(part, N * chunks, K, 0, p, acc)
+        else:
+            lib.adr_partial_sum(fptr(part), N * chunks, K, 0, p, acc, stream())
         return grad_ret(param, db)
     db = torch.empty(K, dtype=torch.float32, device=dy.device)
     lib.adr_partial_sum(fptr(part), N * chunks, K, 0, fptr(db), 0, stream())

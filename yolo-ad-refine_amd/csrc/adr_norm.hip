@@ -437,6 +437,25 @@ __global__ void __launch_bounds__(256) partial_sum_kernel(const float* __restric
   if (threadIdx.x == 0) out[c] = accumulate ? out[c] + (float)a : (float)a;
 }
 
+// Many partial sums per launch (the trainer defers the bias gradients to the end of backward): block j of the
+// grid reduces channel j - start[e] of entry e exactly as partial_sum_kernel does (same order).
+constexpr int PSB_MAX = 80;
+struct PsumBatch {
+  adr_psum_entry e[PSB_MAX];
+  int start[PSB_MAX + 1];
+  int count;
+};
+__global__ void __launch_bounds__(256) partial_sum_batched_kernel(PsumBatch b) {
+  int j = 0;
+  while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  const adr_psum_entry& en = b.e[j];
+  const int c = blockIdx.x - b.start[j];
+  double a = 0.0, z = 0.0;
+  for (int p = threadIdx.x; p < en.P; p += 256) a += en.partial[(long)p * 2 * en.C + en.which * en.C + c];
+  block_sum2(a, z);
+  if (threadIdx.x == 0) en.out[c] = en.accumulate ? en.out[c] + (float)a : (float)a;
+}
+
 static int grid_for(long npix, int G) {
   const long rpb = 256 / G;  // pixels per block pass (PixLanes)
   long b = (npix + rpb - 1) / rpb;
@@ -562,6 +581,27 @@ extern "C" int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, co
                        (const float*)dz, dcs, dco, (float*)dx, ocs, oco, scale, shift, A, B, Cc, per_sample,
                        coef_per_sample, act, npix, HW, C, accumulate);
   return check_launch("adr_affine_act_bwd");
+}
+
+extern "C" int adr_partial_sum_batched(const adr_psum_entry* entries, int count, void* stream) {
+  ADR_REQUIRE(count >= 0 && (count == 0 || entries), "partial_sum_batched: count=%d", count);
+  for (int b0 = 0; b0 < count; b0 += PSB_MAX) {
+    PsumBatch pb{};
+    pb.count = count - b0 < PSB_MAX ? count - b0 : PSB_MAX;
+    int blocks = 0;
+    for (int j = 0; j < pb.count; ++j) {
+      const adr_psum_entry& en = entries[b0 + j];
+      ADR_REQUIRE(en.partial && en.out && en.P > 0 && en.C > 0, "partial_sum_batched: entry %d", b0 + j);
+      for (int q = 0; q < j; ++q)
+        ADR_REQUIRE(pb.e[q].out != en.out, "partial_sum_batched: entries %d and %d share a destination", b0 + q, b0 + j);
+      pb.e[j] = en;
+      pb.start[j] = blocks;
+      blocks += en.C;
+    }
+    pb.start[pb.count] = blocks;
+    hipLaunchKernelGGL(partial_sum_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, pb);
+  }
+  return check_launch("adr_partial_sum_batched");
 }
 
 extern "C" int adr_partial_sum(const float* partial, int P, int C, int which, float* out, int accumulate,
