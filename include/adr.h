@@ -193,6 +193,14 @@ int adr_nc_collapse(const float* partial, int N, int chunks, int C, int which, f
                     int accumulate, void* stream);
 /* y += a*x over n fp32 values (gradient accumulation into the trainer's flat gradient arena). */
 int adr_axpy(long n, float a, const float* x, float* y, void* stream);
+/* y_i += x_i for many (x, y, n) in one launch (<= 96 entries each; more are split); destinations distinct.
+ * `entries` is a host array (kernel arguments). */
+typedef struct {
+  const float* x;
+  float* y;
+  long n;
+} adr_axpy_entry;
+int adr_axpy_batched(const adr_axpy_entry* entries, int count, void* stream);
 /* BiFPN weights w = relu(fw)/(sum relu(fw)+eps) and backward (block.py:1532-1535). */
 int adr_fusion_weights(const float* fw, int n, float eps, float* w, void* stream);
 int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream);

@@ -192,7 +192,10 @@ def sink(t, g):
         gc = gc.contiguous()
     if gc.numel() != tgt.numel():
         raise RuntimeError("sink: gradient size mismatch")
-    lib.adr_axpy(gc.numel(), 1.0, fptr(gc), fptr(tgt._adr_grad), stream())
+    if _DEFER is not None and _TIMING is None:
+        _DEFER.add_axpy(gc, tgt._adr_grad.data_ptr(), gc.numel())
+    else:
+        lib.adr_axpy(gc.numel(), 1.0, fptr(gc), fptr(tgt._adr_grad), stream())
     tgt._adr_used = True
     return None
 
@@ -443,6 +446,11 @@ class PsumEntry(ctypes.Structure):
         (n, ctypes.c_int) for n in ("P", "C", "which", "accumulate")]
 
 
+class AxpyEntry(ctypes.Structure):
+    """adr_axpy_entry (include/adr.h)."""
+    _fields_ = [("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("n", ctypes.c_long)]
+
+
 class WgradDeferral:
     """Collects the split-K reductions of every conv weight gradient that lands in the trainer's gradient arena
     and runs them as a few batched launches (adr_wgrad_reduce_batched) when the backward pass ends, instead of
@@ -453,6 +461,16 @@ class WgradDeferral:
     def __init__(self):
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
+        self.axpys, self.akeep, self.adsts = [], [], set()
+
+    def add_axpy(self, src, dst, n):
+        """A parameter gradient computed into a temporary, to be added into the arena (sink)."""
+        dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
+        if dst in self.adsts:
+            self.flush()
+        self.axpys.append(AxpyEntry(src.data_ptr(), dst, n))
+        self.akeep.append(src)
+        self.adsts.add(dst)
 
     def add_psum(self, part, P, C, which, dst, acc):
         """A bias gradient (adr_partial_sum into the arena), batched the same way."""
@@ -478,8 +496,12 @@ class WgradDeferral:
         if self.psums:
             arr = (PsumEntry * len(self.psums))(*self.psums)
             lib.adr_partial_sum_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.psums), stream())
+        if self.axpys:
+            arr = (AxpyEntry * len(self.axpys))(*self.axpys)
+            lib.adr_axpy_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.axpys), stream())
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
+        self.axpys, self.akeep, self.adsts = [], [], set()
 
 
 _DEFER = None  # the active WgradDeferral (set by the trainer around its backward pass)

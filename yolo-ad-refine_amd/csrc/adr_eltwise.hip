@@ -243,6 +243,26 @@ __global__ void axpy_kernel(long n, float a, const float* x, float* y) {
   if (i < n) y[i] += a * x[i];
 }
 
+// Many y += x over distinct destinations in one launch (the trainer's deferred parameter-gradient adds): 1024
+// elements per workgroup, the entry found from the per-entry block offsets.
+constexpr int AXB_MAX = 96;
+struct AxpyBatch {
+  adr_axpy_entry e[AXB_MAX];
+  int start[AXB_MAX + 1];
+  int count;
+};
+__global__ void __launch_bounds__(256) axpy_batched_kernel(AxpyBatch b) {
+  int j = 0;
+  while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  const adr_axpy_entry& en = b.e[j];
+  const long base = (long)(blockIdx.x - b.start[j]) * 1024 + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long i = base + u * 256;
+    if (i < en.n) en.y[i] += en.x[i];
+  }
+}
+
 static int ew_grid(long npix, int G) {
   const long rpb = 256 / G;  // pixels per block pass (PixLanes)
   long b = (npix + rpb - 1) / rpb;
@@ -327,6 +347,28 @@ extern "C" int adr_fusion_weights(const float* fw, int n, float eps, float* w, v
 extern "C" int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream) {
   hipLaunchKernelGGL(fusion_weights_bwd_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, fw, n, eps, dw, dfw);
   return check_launch("adr_fusion_weights_bwd");
+}
+
+extern "C" int adr_axpy_batched(const adr_axpy_entry* entries, int count, void* stream) {
+  ADR_REQUIRE(count >= 0 && (count == 0 || entries), "axpy_batched: count=%d", count);
+  for (int b0 = 0; b0 < count; b0 += AXB_MAX) {
+    AxpyBatch ab{};
+    ab.count = count - b0 < AXB_MAX ? count - b0 : AXB_MAX;
+    long blocks = 0;
+    for (int j = 0; j < ab.count; ++j) {
+      const adr_axpy_entry& en = entries[b0 + j];
+      ADR_REQUIRE(en.x && en.y && en.n > 0, "axpy_batched: entry %d", b0 + j);
+      for (int q = 0; q < j; ++q)
+        ADR_REQUIRE(ab.e[q].y != en.y, "axpy_batched: entries %d and %d share a destination", b0 + q, b0 + j);
+      ab.e[j] = en;
+      ab.start[j] = (int)blocks;
+      blocks += cdiv(en.n, 1024);
+    }
+    ADR_REQUIRE(blocks < (1l << 31), "axpy_batched: too many elements");
+    ab.start[ab.count] = (int)blocks;
+    hipLaunchKernelGGL(axpy_batched_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ab);
+  }
+  return check_launch("adr_axpy_batched");
 }
 
 extern "C" int adr_axpy(long n, float a, const float* x, float* y, void* stream) {
