@@ -57,7 +57,7 @@ int adr_conv2d_fwd_stat_tiles(const adr_conv_desc* d);
 /* bf16 engine (adr_conv.hip): the same contractions with BK = 64 steps, tap-packed reductions for channel
  * counts below 64, LDS-staged 16-byte output rows and stride-2 DGRAD by output parity class. The forward takes
  * the KRSC weight; the data gradient takes the CRSK weight (adr_pack_weight2). 3x3 / stride-1 / pad-1 shapes with
- * reduction channels % 32 == 0, output channels % 64 == 0 and W % 8 == 0 run on 2-D output tiles with an LDS
+ * reduction channels % 32 == 0, output channels % 32 == 0 and W % 8 == 0 run on 2-D output tiles with an LDS
  * halo tile (all nine taps from one staging). Stats tiles: adr_conv2d_fwd_bf16_stat_tiles(d) (tile geometry
  * depends on the path). */
 int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w_krsc, const float* bias, void* y,

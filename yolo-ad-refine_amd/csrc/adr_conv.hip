@@ -372,12 +372,13 @@ constexpr int C3_CK = 32, C3_LD = C3_CK;  // chunk channels; unpadded 64-byte LD
 // group reads cover 16 disjoint bank quads (48 KB per block: 3 blocks per CU)
 __device__ __forceinline__ int c3_swz(int row, int kq) { return row * C3_LD + ((kq ^ ((row >> 2) & 3)) << 3); }
 
-template <int TW, bool DG>
+template <int TW, bool DG, int BN>
 __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
-  constexpr int BN = 64, TH = 128 / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
+  constexpr int TH = 128 / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
   constexpr int A_TOT = NPIX * (C3_CK / 8), A_CH = (A_TOT + 255) / 256;
-  constexpr int B_CH = 9 * BN * (C3_CK / 8) / 256;  // = 9: chunk i of a thread is tap i
-  constexpr int TM = 2, TN = 4;                     // 4 waves along M (32 rows each) x all 64 columns
+  constexpr int TPP = 256 / (BN * (C3_CK / 8));      // taps per pass of the 256 threads over the weight slab
+  constexpr int B_CH = (9 + TPP - 1) / TPP;          // chunk i of a thread is tap i * TPP + tid / (4 BN)
+  constexpr int TM = 2, TN = BN / 16;                // 4 waves along M (32 rows each) x all BN columns
   constexpr int OPITCH = BN + 8, CPR = BN / 8, RPP = 256 / CPR;
   constexpr int SMEM_A = NPIX * C3_LD, SMEM_B = 9 * BN * C3_LD;
   constexpr int SMEM_AB = 2 * (SMEM_A + SMEM_B), SMEM_O = 2 * 128 * OPITCH, SMEM_R = 2 * RPP * BN * 4;
@@ -408,8 +409,9 @@ __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
     const bool ok = e < A_TOT && gy >= 0 && gy < a.sh_ && gx >= 0 && gx < a.sw_;
     a_off[i] = ok ? ((img * a.sh_ + gy) * a.sw_ + gx) * a.scs + a.sco + (e & 3) * 8 : -1;
   }
-  const bool b_ok = n0 + (tid >> 2) < a.N;
-  const int b_off = (n0 + (tid >> 2)) * 9 * a.sc + (tid & 3) * 8;  // + tap * sc + c0
+  const int b_row = (tid >> 2) % BN, b_tap0 = tid / (4 * BN);
+  const bool b_ok = n0 + b_row < a.N;
+  const int b_off = (n0 + b_row) * 9 * a.sc + (tid & 3) * 8;  // + tap * sc + c0
 
   u32x4 ra[A_CH], rb[B_CH];
   auto load = [&](int c0) {
@@ -417,8 +419,11 @@ __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
     for (int i = 0; i < A_CH; ++i)
       ra[i] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, a_off[i] >= 0 ? (unsigned)(a_off[i] + c0) * 2u : OOR, 0, 0);
 #pragma unroll
-    for (int i = 0; i < B_CH; ++i)
-      rb[i] = __builtin_amdgcn_raw_buffer_load_b128(wt_rs, b_ok ? (unsigned)(b_off + i * a.sc + c0) * 2u : OOR, 0, 0);
+    for (int i = 0; i < B_CH; ++i) {
+      const int tap = i * TPP + b_tap0;
+      rb[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          wt_rs, (b_ok && tap < 9) ? (unsigned)(b_off + tap * a.sc + c0) * 2u : OOR, 0, 0);
+    }
   };
   auto store = [&]() {
 #pragma unroll
@@ -427,7 +432,10 @@ __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
       if (e < A_TOT) st16(&As[c3_swz(e >> 2, e & 3)], ra[i]);
     }
 #pragma unroll
-    for (int i = 0; i < B_CH; ++i) st16(&Bs[c3_swz(i * BN + (tid >> 2), tid & 3)], rb[i]);
+    for (int i = 0; i < B_CH; ++i) {
+      const int tap = i * TPP + b_tap0;
+      if (tap < 9) st16(&Bs[c3_swz(tap * BN + b_row, tid & 3)], rb[i]);
+    }
   };
 
   const int wr0 = wave * 32;
@@ -531,20 +539,26 @@ __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
 
 // tile width of the 3x3 path for this geometry, or 0 when it does not apply
 static int conv3_tw(const adr_conv_desc* d, int red_ch, int out_ch) {
-  if (d->r != 3 || d->s != 3 || d->stride_h != 1 || d->pad_h != 1 || red_ch % C3_CK || out_ch % 64) return 0;
+  if (d->r != 3 || d->s != 3 || d->stride_h != 1 || d->pad_h != 1 || red_ch % C3_CK || out_ch % 32) return 0;
   if (d->w % 16 == 0 && d->h >= 8) return 16;
   if (d->w % 8 == 0) return 8;
   return 0;
 }
+static int conv3_bn(int out_ch) { return out_ch % 64 == 0 ? 64 : 32; }
 static int conv3_tiles(const adr_conv_desc* d, int tw) {
   return d->n * ((d->h + 128 / tw - 1) / (128 / tw)) * (d->w / tw);
 }
 template <bool DG>
-static void launch_conv3(int tw, const adr_conv_desc* d, ConvArgs& g, hipStream_t st) {
-  g.ntiles = g.N / 64;
+static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hipStream_t st) {
+  g.ntiles = g.N / bn;
   dim3 grid(conv3_tiles(d, tw) * g.ntiles);
-  if (tw == 16) hipLaunchKernelGGL((conv3_kernel<16, DG>), grid, dim3(256), 0, st, g);
-  else hipLaunchKernelGGL((conv3_kernel<8, DG>), grid, dim3(256), 0, st, g);
+  if (bn == 64) {
+    if (tw == 16) hipLaunchKernelGGL((conv3_kernel<16, DG, 64>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((conv3_kernel<8, DG, 64>), grid, dim3(256), 0, st, g);
+  } else {
+    if (tw == 16) hipLaunchKernelGGL((conv3_kernel<16, DG, 32>), grid, dim3(256), 0, st, g);
+    else hipLaunchKernelGGL((conv3_kernel<8, DG, 32>), grid, dim3(256), 0, st, g);
+  }
 }
 
 template <int MODE>
@@ -588,7 +602,7 @@ static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad) {
   if (p.mode != CV_DGRAD2) p.tw = conv3_tw(d, red, out);
   // 1x1 contractions are two or three K-steps long: 64-wide column tiles (4 waves/SIMD) hide their load latency
   // better than 128-wide ones (2 waves/SIMD), at the cost of reading the A rows once per column tile (L2 hits)
-  p.bn = (d->r * d->s == 1 && out > 64) ? 64 : conv_pick_bn(out);
+  p.bn = p.tw ? conv3_bn(out) : (d->r * d->s == 1 && out > 64) ? 64 : conv_pick_bn(out);
   return p;
 }
 
@@ -610,7 +624,7 @@ extern "C" int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const 
   g.wt_bytes = (int)(2l * g.N * g.ktot);
   const ConvPlan pl = conv_plan(d, false);
   if (pl.tw) {
-    launch_conv3<false>(pl.tw, d, g, (hipStream_t)stream);
+    launch_conv3<false>(pl.tw, pl.bn, d, g, (hipStream_t)stream);
     return check_launch("adr_conv2d_fwd_bf16");
   }
   const int bn = pl.bn;
@@ -641,7 +655,7 @@ extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, con
     dim3 grid(cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM) * g.ntiles, 1, 4);
     launch_conv<CV_DGRAD2>(bn, grid, g, st);
   } else if (pl.tw) {
-    launch_conv3<true>(pl.tw, d, g, st);
+    launch_conv3<true>(pl.tw, pl.bn, d, g, st);
   } else {
     dim3 grid(cdiv((long)d->n * d->h * d->w, CBM) * g.ntiles);
     launch_conv<CV_DGRAD>(bn, grid, g, st);
@@ -659,7 +673,7 @@ extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, 
   ADR_REQUIRE(d && buf && len >= 64, "conv kernel symbol: bad arguments");
   const ConvPlan pl = conv_plan(d, dgrad != 0);
   if (pl.tw)
-    snprintf(buf, len, "_ZN3adr12conv3_kernelILi%dELb%dEEEvNS_8ConvArgsE", pl.tw, dgrad ? 1 : 0);
+    snprintf(buf, len, "_ZN3adr12conv3_kernelILi%dELb%dELi%dEEEvNS_8ConvArgsE", pl.tw, dgrad ? 1 : 0, pl.bn);
   else
     snprintf(buf, len, "_ZN3adr16conv_bf16_kernelILi%dELi%dEEEvNS_8ConvArgsE", pl.bn, pl.mode);
   return ADR_OK;
