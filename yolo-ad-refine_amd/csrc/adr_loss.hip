@@ -654,6 +654,7 @@ extern "C" int adr_det_loss(int dtype, const void* f0, const void* f1, const voi
     if (dtype == ADR_BF16) hipLaunchKernelGGL(KERN<__bf16>, grid, block, 0, st, __VA_ARGS__); \
     else hipLaunchKernelGGL(KERN<float>, grid, block, 0, st, __VA_ARGS__);                \
   } while (0)
+  ADR_REQUIRE(nc % 8 == 0 && nc <= 96, "det_loss: nc=%d (needs a multiple of 8, at most 96)", nc);
   LDISPATCH(loss_decode_kernel, dim3(cdiv((long)n, 256)), dim3(256), L, B, pbox);
   if (nmax > 0) {
     long tot = (long)rows * A;
@@ -662,12 +663,13 @@ extern "C" int adr_det_loss(int dtype, const void* f0, const void* f1, const voi
     hipLaunchKernelGGL(tal_assign_kernel, dim3(cdiv((long)n, 256)), dim3(256), 0, st, flags, ovl, B, nmax, A, tgi, fg);
     hipLaunchKernelGGL(tal_norm_kernel, dim3((unsigned)rows), dim3(256), 0, st, align, ovl, tgi, fg, B, nmax, A, pos);
   } else {
-    hipMemsetAsync(fg, 0, n, st);
-    hipMemsetAsync(tgi, 0, n * 4, st);
+    hipError_t e1 = hipMemsetAsync(fg, 0, n, st);
+    hipError_t e2 = hipMemsetAsync(tgi, 0, n * 4, st);
+    ADR_REQUIRE(e1 == hipSuccess && e2 == hipSuccess, "det_loss: hipMemsetAsync failed (%s)",
+                hipGetErrorString(e1 != hipSuccess ? e1 : e2));
   }
   LDISPATCH(loss_fg_kernel, dim3(nblk), dim3(256), L, B, nmax, gt, pbox, align, tgi, fg, pos, tnorm, part);
   hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(256), 0, st, part, nblk, scal);
-  ADR_REQUIRE(nc % 8 == 0 && nc <= 96, "det_loss: nc=%d (needs a multiple of 8, at most 96)", nc);
   LDISPATCH(loss_cls_grad_kernel, dim3(cdiv((long)n, CLS_ANCHORS_PER_BLOCK)), dim3(256), L, G, B, nmax, nc, grad_scale, gt, pbox, tgi, fg, tnorm, scal,
             part2, box_gain, cls_gain, dfl_gain);
   hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, part2, (int)cdiv((long)n, CLS_ANCHORS_PER_BLOCK), scal, B, box_gain, cls_gain, dfl_gain,
