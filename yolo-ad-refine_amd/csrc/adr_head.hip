@@ -88,7 +88,7 @@ __global__ void __launch_bounds__(256) dcn_im2col_kernel(const T* x, int xcs, co
 // window go straight to dx32. The same pass computes d_offset / d_mask_logit from the corner values (DPP wave
 // sums). All loads of a tap group are unconditional at clamped addresses (masked afterwards), so they are in
 // flight together instead of each waiting behind a branch.
-constexpr int DCN_SL = 40;             // strip length (rows per wave)
+constexpr int DCN_SL = 10;             // strip length (rows per wave; 10 beat 20 and 40 by 0.1 / 0.2 ms per step)
 constexpr int DCN_WIN = 7;             // window rows / columns (pixel +-3)
 constexpr int DCN_CC = 64;             // channels per pass (= lanes)
 constexpr int DCN_WPB = 4;             // waves per block
