@@ -117,7 +117,8 @@ def main():
     if world > 1:  # same initial weights on every rank (DDP broadcasts rank 0's parameters at construction)
         for p in model.parameters():
             dist.broadcast(p.data, 0)
-    tr = FusedTrainer(model, batch_size=args.bs, world_size=world)
+    # the reference's batch_size is the GLOBAL batch (trainer.py:290, 305-306): accumulate and weight decay
+    tr = FusedTrainer(model, batch_size=world * args.bs, world_size=world)
     batch, _ = train_batch(args.bs, args.img, seed=1000 * rank, device=dev)  # rank's shard of the stream
 
     for _ in range(args.warmup):

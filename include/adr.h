@@ -339,11 +339,12 @@ int adr_det_loss(int dtype, const void* f0, const void* f1, const void* f2, int 
 
 /* ---------------------------------------------------------------------------------------------------------
  * Trainer tail (engine/trainer.py:580-588, 753-813; utils/torch_utils.py:521-546) over a chunk table:
- * entry = {float* p; const float* g; float* momentum_buf; float* ema; int64 n; int group; int pad}
+ * entry = {float* p; float* g; float* momentum_buf; float* ema; int64 n; int group; int pad}
  * (group 0 decayed weights, 1 norm weights, 2 biases, 3 buffers / frozen: EMA only);
  * chunk = {int entry; int pad; int64 start; int64 len}. Both tables live in device memory.
  * adr_opt_step: clip_grad_norm_(10) + SGD(momentum, nesterov, per-group lr / weight decay) + EMA
- * (ema = d*ema + (1-d)*p after the update); norm_out (optional) receives the pre-clip total norm.
+ * (ema = d*ema + (1-d)*p after the update) + optimizer.zero_grad() (trainer.py:586: each updated entry's
+ * gradient is zeroed after it is consumed); norm_out (optional) receives the pre-clip total norm.
  * hyper is DEVICE memory: [lr0, lr1, lr2, wd0, wd1, wd2, momentum, nesterov, first, ema_decay] (first != 0:
  * momentum buffer initialised to the gradient), so a captured hipGraph of the step follows the schedule. */
 int adr_opt_entry_size(void);

@@ -1,0 +1,130 @@
+"""Multi-process data parallelism on the GPU: two ranks (one process each, both on cuda:0 —
+the box has one GPU — with the gloo backend, which reduces device tensors through the host) run
+FusedTrainer(world_size=2): the staged backward with bucketed async all-reduce, first eagerly, then through
+the captured per-stage hipGraphs with the collectives launched between replays.
+
+Oracle: the CPU restatement runs each rank's shard as its own forward + loss + backward (BatchNorm and MLCA's
+batch-axis pooling are per rank, as in the reference's DDP), the two gradients are summed (== the reference's
+loss * world_size + DDP averaging, trainer.py:387/273), then clip_grad_norm_(10) + SGD-nesterov with the
+reference's three groups and the weight decay of the GLOBAL batch (trainer.py:305-306). Two such steps; the
+post-step parameters and EMA of both ranks are compared with it."""
+import math
+import os
+import socket
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+import yaml
+
+import adr_oracle as O
+from conftest import ROOT, state_dict_spec
+from recipe import recipe_state_dict, synthetic_images, synthetic_labels
+
+pytestmark = pytest.mark.gpu
+CFG = ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml"
+WORLD, BS = 2, 2
+
+
+def _shard(step, rank):
+    return synthetic_images(BS, 320, seed=50 + 10 * step + rank), synthetic_labels(BS, 80, seed=60 + 10 * step + rank)
+
+
+def _worker(rank, port, out_dir, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        from adrefine.engine.trainer import FusedTrainer
+        from adrefine.nn.tasks import DetectionModel
+        from gpu_util import load_recipe_into
+        torch.cuda.set_device(0)
+        m = DetectionModel(str(CFG))
+        load_recipe_into(m)
+        m = m.cuda()
+        tr = FusedTrainer(m, nbs=WORLD * BS, batch_size=WORLD * BS, world_size=WORLD)
+        assert tr.cuts == (6, 10) and tr.accumulate == 1
+        x, lab = _shard(0, rank)
+        tr.step({"img": x.cuda(), **lab})  # eager: bucket all-reduces launched between backward stages
+        x, lab = _shard(1, rank)
+        b = {"img": x.cuda(), **lab}
+        # capture on a copy of the state, then restore: the graphs replay the second step
+        tr.capture(b, max_targets=64)
+        tr.step(b)
+        torch.cuda.synchronize()
+        sd = {k: v.detach().cpu() for k, v in m.state_dict().items()}
+        ema = {k: v.detach().cpu().clone() for k, v in tr.ema_state_dict().items()}
+        torch.save({"sd": sd, "ema": ema, "norm": float(tr.norm), "wd": tr.wd, "buckets": tr.buckets},
+                   os.path.join(out_dir, f"rank{rank}.pt"))
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, None))
+    except Exception as e:  # noqa: BLE001
+        import traceback
+        q.put((rank, traceback.format_exc() + repr(e)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_ddp_world2_matches_oracle(tmp_path):
+    from adrefine.engine.trainer import param_groups
+    from adrefine.nn.tasks import DetectionModel
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, str(tmp_path), q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=240) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, err in res:
+        assert err is None, f"rank {rank}: {err}"
+    outs = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(WORLD)]
+    assert abs(outs[0]["wd"] - 5e-4 * WORLD * BS / (WORLD * BS)) < 1e-12
+    # oracle: two DDP steps
+    groups = [[n for n, _ in g] for g in param_groups(DetectionModel(str(CFG)))]
+    P = recipe_state_dict([(k, s) for k, s, _ in state_dict_spec("701")])
+    layers, save = O.parse(yaml.safe_load(CFG.read_text()), 3, None)
+    for k, v in P.items():
+        if v.dtype.is_floating_point and "running" not in k and not k.endswith("dfl.conv.weight"):
+            v.requires_grad_(True)
+    init = {k: v.detach().clone() for k, v in P.items()}
+    ema = {k: v.detach().clone().float() for k, v in P.items() if v.dtype.is_floating_point}
+    opt, used, norms = None, None, []
+    for step in range(2):
+        for r in range(WORLD):  # per-rank passes; BN running stats: rank 0's chain is the one compared
+            x, lab = _shard(step, r)
+            Pr = P if r == 0 else {k: (v.detach().clone() if "running" in k else v) for k, v in P.items()}
+            preds = O.forward(Pr, layers, save, x, train=True)
+            loss, _ = O.detection_loss(preds, lab["batch_idx"], lab["cls"], lab["bboxes"])
+            loss.backward()  # .grad accumulates the sum over ranks
+        if opt is None:
+            used = [k for k in P if P[k].requires_grad and P[k].grad is not None]
+            opt = torch.optim.SGD([P[k] for k in groups[2] if k in used], lr=0.01, momentum=0.937, nesterov=True)
+            opt.add_param_group({"params": [P[k] for k in groups[0] if k in used], "weight_decay": 5e-4})
+            opt.add_param_group({"params": [P[k] for k in groups[1] if k in used], "weight_decay": 0.0})
+        norms.append(float(torch.nn.utils.clip_grad_norm_([P[k] for k in used], max_norm=10.0)))
+        opt.step()
+        opt.zero_grad()
+        d = 0.9999 * (1 - math.exp(-(step + 1) / 2000))
+        for k in ema:
+            ema[k] = d * ema[k] + (1 - d) * P[k].detach().float()
+    for r, o in enumerate(outs):
+        assert abs(o["norm"] - norms[1]) <= 2e-3 * norms[1], (r, o["norm"], norms[1])
+        worst = 0.0
+        for k in used:
+            a, b = o["sd"][k].float(), P[k].detach()
+            delta = float((b - init[k]).abs().max())
+            worst = max(worst, float((a - b).abs().max()) / (delta + 1e-12))
+        assert worst < 3e-2, (r, worst)
+        k = "model.33.cv3.0.weight" if "model.33.cv3.0.weight" in ema else used[0]
+        e = o["ema"][k]
+        assert float((e - ema[k]).abs().max()) <= 3e-2 * float((ema[k] - init[k]).abs().max()) + 1e-7, k
+    # both ranks hold the same model after the reduced steps
+    for k in used:
+        assert torch.allclose(outs[0]["sd"][k], outs[1]["sd"][k], rtol=0, atol=1e-6), k

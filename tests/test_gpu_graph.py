@@ -12,16 +12,16 @@ pytestmark = pytest.mark.gpu
 CFG = ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml"
 
 
-def _trainer():
+def _trainer(stages=None):
     from adrefine.engine.trainer import FusedTrainer
     from adrefine.nn.tasks import DetectionModel
     m = DetectionModel(str(CFG))
     load_recipe_into(m)
-    return FusedTrainer(m.cuda(), batch_size=2)
+    return FusedTrainer(m.cuda(), nbs=2, batch_size=2, stages=stages)
 
 
-def _run(seq, graph):
-    tr = _trainer()
+def _run(seq, graph, stages=None):
+    tr = _trainer(stages)
     out = [tr.step(seq[0]).clone()]
     if graph:
         tr.capture(seq[1], max_targets=100)
@@ -53,6 +53,27 @@ def test_graph_step_matches_eager():
     assert max(float((ee[k] - eg[k]).abs().max()) for k in ee) <= 10 * spread + 2e-4
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_staged_step_matches_unstaged(graph):
+    """The DDP stage split (backward in three stages L0-L6 | L7-L10 | L11-L33, one graph per stage when
+    captured, engine/ddp.py) reproduces the single-stage step."""
+    b1 = {"img": synthetic_images(2, 320, seed=0).cuda(), **synthetic_labels(2, 80, seed=1)}
+    b2 = {"img": synthetic_images(2, 320, seed=5).cuda(), **synthetic_labels(2, 80, seed=6)}
+    seq = [b1, b1, b2]
+    e1, o1 = _run(seq, False)
+    e2, o2 = _run(seq, False)
+    st, os_ = _run(seq, graph, stages=(6, 10))
+    assert st.cuts == (6, 10) and len(st.buckets) == 3
+    if graph:
+        assert len(st.graphs[0]) == 3
+    spread = _pdiff(e1, e2)
+    d = _pdiff(e1, st)
+    print(f"eager-eager max |dparam| {spread:.3e}, unstaged-staged {d:.3e}")
+    assert d <= 10 * spread + 2e-4, (d, spread)
+    for a, b, c in zip(o1, os_, o2):
+        assert float((a - b).abs().max()) <= 10 * float((a - c).abs().max()) + 2e-4 * float(a.abs().max())
+
+
 def test_pack_cache_matches_direct_packing():
     """The trainer's batched once-per-step weight packing (PackCache.pack_all) produces exactly the operands a
     per-call adr_pack_weight2 would, for every recorded conv weight, after an optimizer update."""
@@ -61,7 +82,7 @@ def test_pack_cache_matches_direct_packing():
     from adrefine.nn.tasks import DetectionModel
     m = DetectionModel(str(CFG), compute_dtype=torch.bfloat16)
     load_recipe_into(m)
-    tr = FusedTrainer(m.cuda(), batch_size=2)
+    tr = FusedTrainer(m.cuda(), nbs=2, batch_size=2)
     b = {"img": synthetic_images(2, 320, seed=0).cuda(), **synthetic_labels(2, 80, seed=1)}
     tr.step(b)
     tr.step(b)  # second step runs on pack_all's buffers; the weights have moved since

@@ -1,0 +1,135 @@
+"""Data-parallel plumbing of the training step: staged backward + bucketed gradient all-reduce.
+
+The reference wraps the model in DistributedDataParallel (engine/trainer.py:273) whose autograd hooks all-reduce
+gradient buckets while `scaler.scale(loss).backward()` (:393) is still running, so communication of the late
+layers' gradients overlaps the backward of the early layers. This build keeps every parameter gradient in ONE
+flat fp32 arena written by the kernels themselves (no per-parameter hooks), so it gets the same overlap a
+different way:
+
+* the layer list is cut into stages (`cuts` = layer indices after which a stage ends; default after L6 and L10,
+  SURVEY.md §8e) and the tensors that cross a cut are detached into fresh leaves during the forward
+  (`cut_live`), so the backward runs stage by stage, last stage first (`staged_backward`);
+* the arena is laid out stage-major, last stage first (`stage_of`, FusedTrainer), so when a stage's backward
+  (and its batched WGRAD reductions) is done, its parameters' gradients form one contiguous bucket;
+* `BucketReducer.launch(k)` starts an async all-reduce(SUM) of that bucket (RCCL over xGMI with backend "nccl",
+  or gloo) while the next stage's backward is enqueued behind it on the compute stream.
+
+With hipGraph replay (FusedTrainer.capture) every stage's backward is its own graph, and the collectives are
+launched eagerly between the replays — the graphs themselves hold no collective.
+
+Summing the per-rank gradients equals the reference's `loss *= world_size` (trainer.py:387) followed by DDP's
+gradient average. BatchNorm statistics stay per rank as in the reference (no SyncBatchNorm). DDP also
+broadcasts rank 0's buffers every forward (broadcast_buffers=True); batch-statistics BN never reads them in
+training, rank 0's running statistics are rank 0's own update chain either way, and only rank 0's model/EMA is
+saved or validated (trainer.py:436-444) — so skipping that broadcast changes nothing observable.
+"""
+from __future__ import annotations
+
+import re
+
+import torch
+
+_LAYER = re.compile(r"^model\.(\d+)\.")
+
+
+def layer_of(name: str) -> int:
+    """Layer index of a DetectionModel parameter / buffer name ('model.<i>.…'); -1 when it has none."""
+    m = _LAYER.match(name)
+    return int(m.group(1)) if m else -1
+
+
+def stage_of(layer: int, cuts) -> int:
+    """Stage index of a layer: stage s holds the layers after cuts[s-1] up to and including cuts[s]."""
+    s = 0
+    for c in sorted(cuts):
+        if layer > c:
+            s += 1
+    return s
+
+
+def detach_leaf(t):
+    """A leaf view of t (same storage and strides) that collects the gradient flowing back to t."""
+    if not torch.is_tensor(t) or not t.requires_grad:
+        return t
+    leaf = t.detach()
+    leaf.requires_grad_(True)
+    return leaf
+
+
+def cut_live(x, y, layers, i, bounds):
+    """At the end of layer i: replace every tensor that a later layer reads (y[j] for j <= i in a later `f`, and
+    x when layer i+1 reads -1) by a detached leaf, and record (tensor, leaf) pairs in `bounds`. Returns x."""
+    later = layers[i + 1:]
+    need = set()
+    for m in later:
+        for j in ([m.f] if isinstance(m.f, int) else m.f):
+            if j != -1 and j <= i:
+                need.add(j)
+    pairs = []
+    seen = {}
+    for j in sorted(need):
+        t = y[j]
+        if t is None:
+            raise RuntimeError(f"stage cut after layer {i}: layer {j}'s output is read later but not saved")
+        if id(t) not in seen:
+            seen[id(t)] = detach_leaf(t)
+            pairs.append((t, seen[id(t)]))
+        y[j] = seen[id(t)]
+    if later and (later[0].f == -1 or (not isinstance(later[0].f, int) and -1 in later[0].f)):
+        if id(x) not in seen:
+            seen[id(x)] = detach_leaf(x)
+            pairs.append((x, seen[id(x)]))
+        x = seen[id(x)]
+    bounds.append([(t, leaf) for t, leaf in pairs if leaf is not t])
+    return x
+
+
+def staged_backward(loss, bounds, run, after_stage):
+    """Backward of a forward that was cut into len(bounds)+1 stages: the last stage from `loss`, then every
+    earlier stage from the gradients its leaves collected. `run(fn)` wraps each stage's backward (the trainer
+    passes its WGRAD deferral scope, so a stage's gradients are complete when it returns); `after_stage(s)` is
+    called once stage s's parameter gradients are final."""
+    S = len(bounds) + 1
+    run(lambda: loss.backward())
+    after_stage(S - 1)
+    for k in range(S - 2, -1, -1):
+        ts, gs = [], []
+        for t, leaf in bounds[k]:
+            if leaf.grad is not None:
+                ts.append(t)
+                gs.append(leaf.grad)
+        if ts:
+            run(lambda: torch.autograd.backward(ts, gs))
+        for _, leaf in bounds[k]:
+            leaf.grad = None
+        after_stage(k)
+
+
+class BucketReducer:
+    """Async all-reduce(SUM) of contiguous gradient-arena buckets over a process group. `launch(k)` enqueues
+    bucket k behind the work already on the current stream (ProcessGroupNCCL waits on it; gloo copies through
+    the host); `wait()` makes the current stream wait for every launched bucket."""
+
+    def __init__(self, arena, ranges, world_size, group=None):
+        self.arena = arena
+        self.ranges = list(ranges)
+        self.world_size = world_size
+        self.group = group
+        self.works = []
+        self.launched = []
+
+    def launch(self, k):
+        lo, hi = self.ranges[k]
+        self.launched.append(k)
+        if self.world_size <= 1 or hi <= lo:
+            return
+        import torch.distributed as dist
+        self.works.append(dist.all_reduce(self.arena[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                          async_op=True))
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+        self.works = []
+        done, self.launched = self.launched, []
+        return done

@@ -141,6 +141,24 @@ def initialize_weights(model):
             m.eps, m.momentum = 1e-3, 0.03
 
 
+def route_layers(layers, save, x, y, start=0, cuts=()):
+    """The layer loop of _predict_once (tasks.py:155-167): each layer reads x (f == -1) or saved outputs y[f],
+    and its output is kept in y when a later layer reads it. With `cuts`, the tensors crossing the end of each
+    listed layer are replaced by detached leaves (engine/ddp.cut_live) and returned as per-cut (tensor, leaf)
+    lists, so the backward can run stage by stage."""
+    bounds = []
+    if cuts:
+        from ..engine.ddp import cut_live
+    for m in layers[start:]:
+        if m.f != -1:
+            x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+        x = m(x)
+        y.append(x if m.i in save else None)
+        if m.i in cuts:
+            x = cut_live(x, y, layers, m.i, bounds)  # y[i] and x stay one leaf when they are one tensor
+    return x, bounds
+
+
 class DetectionModel(nn.Module):
     """YOLO detection model (tasks.py:309-398). Compute dtype: float32 (parity) or bfloat16 (performance);
     parameters stay fp32. Input: float images (B, 3, H, W) in [0, 1] on a ROCm device."""
@@ -170,12 +188,15 @@ class DetectionModel(nn.Module):
             return self.loss(x, *args, **kwargs)
         return self.predict(x, *args, **kwargs)
 
-    def predict(self, x, profile=False, visualize=False, augment=False, embed=None):
-        return self._predict_once(x)
+    def predict(self, x, profile=False, visualize=False, augment=False, embed=None, cuts=()):
+        return self._predict_once(x, cuts)
 
-    def _predict_once(self, x):
-        """tasks.py:141-168 layer routing by m.f with the save list."""
+    def _predict_once(self, x, cuts=()):
+        """tasks.py:141-168 layer routing by m.f with the save list. `cuts` (layer indices) splits the autograd
+        graph into backward stages for the DDP bucket overlap (engine/ddp.py): the tensors crossing each cut are
+        replaced by detached leaves, recorded in self.stage_bounds."""
         first = 0
+        layers = list(self.model)
         if x.dim() == 4 and x.shape[1] == 3:
             m0 = self.model[0]
             if self.compute_dtype == torch.bfloat16 and m0.f == -1 and getattr(m0, "stem_ok", lambda: False)():
@@ -184,17 +205,17 @@ class DetectionModel(nn.Module):
             else:
                 x = K.image_to_nhwc(x, self.compute_dtype, cpad=8)
         y = [x if self.model[0].i in self.save else None] if first else []
-        for m in list(self.model)[first:]:
-            if m.f != -1:
-                x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
-            x = m(x)
-            y.append(x if m.i in self.save else None)
+        if cuts and first and 0 in cuts:
+            raise RuntimeError("stage cut after the fused stem layer is not supported")
+        x, bounds = route_layers(layers, self.save, x, y, first, cuts)
+        if cuts:
+            self.stage_bounds = bounds
         return x
 
-    def loss(self, batch, preds=None):
+    def loss(self, batch, preds=None, cuts=()):
         if getattr(self, "criterion", None) is None:
             self.criterion = self.init_criterion()
-        preds = self.forward(batch["img"]) if preds is None else preds
+        preds = self.predict(batch["img"], cuts=cuts) if preds is None else preds
         return self.criterion(preds, batch)
 
     def init_criterion(self):

@@ -25,16 +25,18 @@ def preprocess_targets(batch_idx, cls, bboxes, bs, imgsz_hw):
     counts = np.bincount(idx, minlength=bs)
     nmax = int(counts.max())
     out = np.zeros((bs, nmax, 5), dtype=np.float32)
-    fill = np.zeros(bs, dtype=np.int64)
     h, w = float(imgsz_hw[0]), float(imgsz_hw[1])
     scale = np.array([w, h, w, h], dtype=np.float32)
-    for k in range(n):  # keeps the per-image label order of the reference's boolean-mask gather
-        j = idx[k]
-        xywh = bx[k] * scale
-        out[j, fill[j], 0] = cl[k]
-        out[j, fill[j], 1:3] = xywh[:2] - xywh[2:] / 2
-        out[j, fill[j], 3:5] = xywh[:2] + xywh[2:] / 2
-        fill[j] += 1
+    # slot of every label inside its image: a stable sort by image keeps the per-image label order of the
+    # reference's boolean-mask gather (loss.py:402-406), vectorised (no per-label Python loop)
+    order = np.argsort(idx, kind="stable")
+    starts = np.concatenate(([0], np.cumsum(counts)[:-1]))
+    slot = np.empty(n, dtype=np.int64)
+    slot[order] = np.arange(n) - starts[idx[order]]
+    xywh = bx * scale
+    out[idx, slot, 0] = cl
+    out[idx, slot, 1:3] = xywh[:, :2] - xywh[:, 2:] / 2
+    out[idx, slot, 3:5] = xywh[:, :2] + xywh[:, 2:] / 2
     t = torch.from_numpy(out)
     return t.pin_memory() if torch.cuda.is_available() else t
 

@@ -9,7 +9,7 @@ namespace adr {
 
 struct OptEntry {
   float* p;          // parameter or buffer (fp32)
-  const float* g;    // gradient (null: no update, e.g. buffers / frozen params)
+  float* g;          // gradient (null: no update, e.g. buffers / frozen params); zeroed after use
   float* buf;        // momentum buffer
   float* ema;        // EMA copy (null: none)
   long n;
@@ -103,6 +103,7 @@ __global__ void __launch_bounds__(256) sgd_ema_kernel(const OptEntry* tab, const
         if (wd != 0.f) gv += wd * pv;
         const float bv = first ? gv : momentum * b[u] + gv;
         e.buf[i] = bv;
+        e.g[i] = 0.f;  // optimizer.zero_grad() (trainer.py:586): the arena starts the next accumulation at 0
         const float step = nesterov ? gv + momentum * bv : bv;
         pv -= lr * step;
         e.p[i] = pv;
