@@ -116,15 +116,41 @@ def test_ddp_world2_matches_oracle(tmp_path):
             ema[k] = d * ema[k] + (1 - d) * P[k].detach().float()
     for r, o in enumerate(outs):
         assert abs(o["norm"] - norms[1]) <= 2e-3 * norms[1], (r, o["norm"], norms[1])
-        worst = 0.0
-        for k in used:
+        errs = []
+        num = den = 0.0
+        for k in used:  # per tensor: ||trainer - oracle|| relative to the size of the two-step update itself
             a, b = o["sd"][k].float(), P[k].detach()
-            delta = float((b - init[k]).abs().max())
-            worst = max(worst, float((a - b).abs().max()) / (delta + 1e-12))
-        assert worst < 3e-2, (r, worst)
+            e2, u2 = float((a - b).norm()) ** 2, float((b - init[k]).norm()) ** 2
+            num, den = num + e2, den + u2
+            errs.append(((e2 / (u2 + 1e-30)) ** 0.5, k, u2 ** 0.5))
+        errs.sort(reverse=True)
+        glob = (num / den) ** 0.5
+        print(f"rank {r}: global relative update error {glob:.2e}; worst tensors {errs[:4]}")
+        assert glob < 1e-2, (r, glob)
+        assert errs[0][0] < 0.2, (r, errs[:4])
         k = "model.33.cv3.0.weight" if "model.33.cv3.0.weight" in ema else used[0]
         e = o["ema"][k]
         assert float((e - ema[k]).abs().max()) <= 3e-2 * float((ema[k] - init[k]).abs().max()) + 1e-7, k
     # both ranks hold the same model after the reduced steps
     for k in used:
         assert torch.allclose(outs[0]["sd"][k], outs[1]["sd"][k], rtol=0, atol=1e-6), k
+    # and the same model as ONE process accumulating both shards (accumulate 2, same global-batch decay):
+    # the same kernels, so this is tight — only the summation order and DCN atomics differ
+    from adrefine.engine.trainer import FusedTrainer
+    from gpu_util import load_recipe_into
+    m = DetectionModel(str(CFG))
+    load_recipe_into(m)
+    m = m.cuda()
+    tr = FusedTrainer(m, nbs=WORLD * BS, batch_size=BS)
+    assert tr.accumulate == WORLD and abs(tr.wd - outs[0]["wd"]) < 1e-12
+    for step in range(2):
+        for r in range(WORLD):
+            x, lab = _shard(step, r)
+            tr.step({"img": x.cuda(), **lab})
+    sd1 = m.state_dict()
+    num = den = 0.0
+    for k in used:
+        num += float((outs[0]["sd"][k] - sd1[k].cpu()).norm()) ** 2
+        den += float((sd1[k].cpu() - init[k]).norm()) ** 2
+    print(f"DDP vs single-process accumulation: global relative update difference {(num / den) ** 0.5:.2e}")
+    assert (num / den) ** 0.5 < 2e-3
