@@ -249,11 +249,29 @@ int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout, int dcs, v
  * DyDCNv2 / mmcv ModulatedDeformConv2d (head.py:751-782), 3x3, stride 1, pad 1, deform_groups 1. `om` holds
  * the spatial_conv_offset output: channels [0,18) offsets (2k = dy, 2k+1 = dx), [18,27) mask LOGITS (the
  * sigmoid of head.py:1156 is applied inside). cols: [N*H*W][9][C]. dx32: fp32 NHWC accumulation buffer
- * (zeroed by the caller; float atomics). dom receives d(offset) and d(mask logit) in the om layout. */
+ * (zeroed by the caller). dom receives d(offset) and d(mask logit) in the om layout.
+ * adr_dcn_col2im: deterministic = 0 accumulates dx32 with float atomics (mmcv's own col2im order-freedom);
+ * deterministic != 0 (fp32 parity mode) accumulates it with one thread per (image, channel) in a fixed order:
+ * bitwise repeatable. */
 int adr_dcn_im2col(int dtype, const void* x, int xcs, const void* om, int omcs, void* cols, int N, int H, int W,
                    int C, void* stream);
 int adr_dcn_col2im(int dtype, const void* x, int xcs, const void* om, int omcs, const void* dcols, float* dx32,
-                   void* dom, int domcs, int N, int H, int W, int C, void* stream);
+                   void* dom, int domcs, int N, int H, int W, int C, int deterministic, void* stream);
+/* Fused bf16 DCNv2 (adr_dcn.hip; replaces im2col + GEMMs + col2im on the performance path; no column matrix in
+ * HBM). C % 64 == 0, Cout % 64 == 0 (<= 256), omcs % 8 == 0 and >= 32.
+ * adr_dcn_fwd_bf16: y[p][co] = sum W_krsc[co][t][c] * m * bilinear(x)  (w_krsc: bf16 [Cout][9][C]).
+ * adr_dcn_wgrad_bf16: split-K partials part[split][Cout][9][C] (fp32) of dW, `splits` from
+ *   adr_dcn_wgrad_bf16_splits; reduce with adr_wgrad_reduce_unpack(K=Cout, C=C, RS=9).
+ * adr_dcn_bwd_bf16 (C == Cout == 64): dx32 (+)= input gradient (fp32, zeroed by the caller, float atomics), dom =
+ *   offset / mask-logit gradient (channels [0,27); the caller zeroes the rest); w_t: bf16 [9][C][Cout]
+ *   (adr_dcn_weight_t). */
+int adr_dcn_fwd_bf16(const void* x, int xcs, const void* om, int omcs, const void* w_krsc, void* y, int ycs, int N,
+                     int H, int W, int C, int Cout, void* stream);
+int adr_dcn_wgrad_bf16_splits(int N, int H, int W, int C, int Cout);
+int adr_dcn_wgrad_bf16(const void* x, int xcs, const void* om, int omcs, const void* dy, int dycs, float* part,
+                       int splits, int N, int H, int W, int C, int Cout, void* stream);
+int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs, const void* dy, int dycs, const void* w_t,
+                     float* dx32, void* dom, int domcs, int N, int H, int W, int C, int Cout, void* stream);
 /* W (Cout, C, 3, 3) fp32 -> [(tap*C + c)][Cout] operand for dcols = dy x W. */
 int adr_dcn_weight_t(int dtype, const float* w, void* out, int Cout, int C, void* stream);
 /* Per-image 2-layer gate MLP on pooled vectors: out = act2(W2 act1(W1 (in*in_scale) + b1) + b2);

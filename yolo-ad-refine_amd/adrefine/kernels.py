@@ -1644,8 +1644,26 @@ class PaddedConvFn(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+def _dcn_fused(dtype, C, Cout, omcs):
+    """The bf16 fused DCN kernels (adr_dcn.hip) cover the head's shapes; fp32 parity mode and other shapes take
+    im2col + GEMM + the deterministic col2im."""
+    return _DCN_FUSED and dtype == torch.bfloat16 and C % 64 == 0 and Cout % 64 == 0 and Cout <= 256 and \
+        omcs % 8 == 0 and omcs >= 32
+
+
+_DCN_FUSED = bool(int(__import__("os").environ.get("ADR_DCN_FUSED", "1")))  # 0: im2col path (A/B only)
+
+
+def _dcn_work(N, H, W, C, Cout, es=2):
+    """Algorithmic (bytes, flops) of one DCN pass: x, the 27 offset/mask channels, the weight and y (or dy) once."""
+    pix = N * H * W
+    return es * (pix * (C + 27 + Cout) + 9 * C * Cout), 2 * pix * 9 * C * Cout
+
+
 class DCNFn(torch.autograd.Function):
-    """mmcv ModulatedDeformConv2d(C, Cout, 3, 1, 1, bias=False) with offsets / mask logits from `om`."""
+    """mmcv ModulatedDeformConv2d(C, Cout, 3, 1, 1, bias=False) with offsets / mask logits from `om`
+    (head.py:751-782). bf16: fused sampling + MFMA kernels, no column matrix in HBM (adr_dcn.hip). fp32 parity
+    mode: im2col -> GEMM, and a deterministic col2im (bitwise repeatable)."""
 
     @staticmethod
     def forward(ctx, x, om, w):
@@ -1654,20 +1672,36 @@ class DCNFn(torch.autograd.Function):
         om, omp, omcs = nhwc(om)
         N, C, H, W = x.shape
         Cout = w.shape[0]
-        cols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=x.device)
-        lib.adr_dcn_im2col(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(cols), N, H, W, C,
-                           stream())
-        wp = pack_weight(w, dtype)  # KRSC [co][tap][c] == 1x1 weight over the [tap][c] columns
-        d, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, Cout, dtype)
         y = empty_act(N, Cout, H, W, dtype, x.device)
-        conv_fwd(d, cols.data_ptr(), wp.data_ptr(), None, y.data_ptr())
-        ctx.save_for_backward(x, om, cols, w)
+        ctx.fused = _dcn_fused(dtype, C, Cout, omcs)
+        ctx.fused_bwd = ctx.fused and C == 64 and Cout == 64
+        if ctx.fused:
+            wp = pack_weight2(w, dtype)[0]  # KRSC [co][tap][c]
+            tok = _t0("adr::dcn_fwd_kernel(adr::DcnArgs)", *_dcn_work(N, H, W, C, Cout),
+                      f"dcn fwd n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "", _reps())
+            for _ in range(_reps()):
+                lib.adr_dcn_fwd_bf16(ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(wp),
+                                     ctypes.c_void_p(y.data_ptr()), Cout, N, H, W, C, Cout, stream())
+            _t1(tok)
+            ctx.save_for_backward(x, om, w)
+        else:
+            cols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=x.device)
+            lib.adr_dcn_im2col(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(cols), N, H, W,
+                               C, stream())
+            wp = pack_weight(w, dtype)  # KRSC [co][tap][c] == 1x1 weight over the [tap][c] columns
+            d, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, Cout, dtype)
+            conv_fwd(d, cols.data_ptr(), wp.data_ptr(), None, y.data_ptr())
+            ctx.save_for_backward(x, om, cols, w)
         ctx.pw = w
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, om, cols, w = ctx.saved_tensors
+        cols = None
+        if ctx.fused:
+            x, om, w = ctx.saved_tensors
+        else:
+            x, om, cols, w = ctx.saved_tensors
         dtype = x.dtype
         _, xp, xcs = nhwc(x)
         _, omp, omcs = nhwc(om)
@@ -1675,20 +1709,51 @@ class DCNFn(torch.autograd.Function):
         N, C, H, W = x.shape
         Cout = w.shape[0]
         dev = x.device
-        # dcols = dy x W^T  (1x1 GEMM: Cin = Cout, K = 9C)
-        wt = torch.empty(9 * C * Cout, dtype=dtype, device=dev)
+        wt = torch.empty(9 * C * Cout, dtype=dtype, device=dev)  # W^T [(tap*C + c)][co]
         lib.adr_dcn_weight_t(dcode(dtype), fptr(w.detach().float().contiguous()), fptr(wt), Cout, C, stream())
-        dcols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=dev)
-        d, _, _ = conv_desc(N, H, W, Cout, dycs, 9 * C, 1, 1, 1, 1, 0, 0, 9 * C, dtype)
-        conv_fwd(d, dyp, wt.data_ptr(), None, dcols.data_ptr())
-        dw = None
-        if ctx.needs_input_grad[2]:
-            dwd, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, dycs, dtype)
-            dw = wgrad_param(ctx.pw, dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, w.shape, 0, dev)
         dx32 = zero_(torch.empty(N * H * W * C, dtype=torch.float32, device=dev))
         dom = zero_(empty_act(N, om.shape[1], H, W, dtype, dev))
-        lib.adr_dcn_col2im(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(dcols), fptr(dx32),
-                           ctypes.c_void_p(dom.data_ptr()), om.shape[1], N, H, W, C, stream())
+        dw = None
+        if ctx.fused and not ctx.fused_bwd:  # fused forward, other shapes: rebuild the columns for the GEMMs
+            cols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=dev)
+            lib.adr_dcn_im2col(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(cols), N, H,
+                               W, C, stream())
+        if ctx.fused_bwd:
+            nb, fl = _dcn_work(N, H, W, C, Cout)
+            tok = _t0("adr::dcn_bwd_kernel(adr::DcnArgs)", nb + 2 * N * H * W * C, 2 * fl,
+                      f"dcn bwd n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "")
+            lib.adr_dcn_bwd_bf16(ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, ctypes.c_void_p(dyp), dycs,
+                                 fptr(wt), fptr(dx32), ctypes.c_void_p(dom.data_ptr()), om.shape[1], N, H, W, C, Cout,
+                                 stream())
+            _t1(tok)
+            if ctx.needs_input_grad[2]:
+                splits = lib.adr_dcn_wgrad_bf16_splits(N, H, W, C, Cout)
+                stride = Cout * 9 * C
+                ws = torch.empty(splits * stride, dtype=torch.float32, device=dev)
+                rep = _reps()
+                tok = _t0("adr::dcn_wgrad_kernel(adr::DcnArgs)", nb + 4 * splits * stride, fl,
+                          f"dcn wgrad/{splits} n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "", rep)
+                for _ in range(rep):
+                    lib.adr_dcn_wgrad_bf16(ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, ctypes.c_void_p(dyp),
+                                           dycs, fptr(ws), splits, N, H, W, C, Cout, stream())
+                _t1(tok)
+                out, ptr, acc = grad_dst(ctx.pw, stride, dev)
+                if _DEFER is not None and acc and _TIMING is None:
+                    _DEFER.add(ws, stride, splits, ptr, Cout, C, C, 9, 0, acc)
+                else:
+                    lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, Cout, C, C, 9, 0, acc, stream())
+                dw = grad_ret(ctx.pw, out)
+        else:
+            # dcols = dy x W^T  (1x1 GEMM: Cin = Cout, K = 9C)
+            dcols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=dev)
+            d, _, _ = conv_desc(N, H, W, Cout, dycs, 9 * C, 1, 1, 1, 1, 0, 0, 9 * C, dtype)
+            conv_fwd(d, dyp, wt.data_ptr(), None, dcols.data_ptr())
+            if ctx.needs_input_grad[2]:
+                dwd, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, dycs, dtype)
+                dw = wgrad_param(ctx.pw, dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, w.shape, 0, dev)
+            lib.adr_dcn_col2im(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(dcols),
+                               fptr(dx32), ctypes.c_void_p(dom.data_ptr()), om.shape[1], N, H, W, C,
+                               int(dtype == torch.float32), stream())
         dx = empty_act(N, C, H, W, dtype, dev)
         lib.adr_cast(F32, fptr(dx32), dcode(dtype), ctypes.c_void_p(dx.data_ptr()), N * H * W * C, stream())
         return dx, dom, dw

@@ -110,7 +110,7 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
   const int strip = (int)(r % nstrip), n = (int)(r / nstrip);
   const int hb = strip * DCN_SL, he = min(H, hb + DCN_SL);
   const T* xb = x + (long)n * H * W * xcs;  // per-image bases; offsets inside an image are 32-bit
-  float* dxb = dx32 + (long)n * H * W * C;
+  float* dxb = dx32 ? dx32 + (long)n * H * W * C : nullptr;  // null: offsets / mask only (deterministic dx below)
   const int wx0 = w - DCN_WIN / 2;  // window column 0
   auto flush_row = [&](int y, int slot, int c) {  // add window row y (ring slot) to dx32 and clear it
     float* row = win + slot * DCN_WIN * DCN_CC;
@@ -119,7 +119,7 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
     for (int j = 0; j < DCN_WIN; ++j) {
       const float v = row[j * DCN_CC + lane];
       const int xx = wx0 + j;
-      if (yok && xx >= 0 && xx < W && v != 0.f) unsafeAtomicAdd(dxb + (y * W + xx) * C + c, v);
+      if (dxb && yok && xx >= 0 && xx < W && v != 0.f) unsafeAtomicAdd(dxb + (y * W + xx) * C + c, v);
       row[j * DCN_CC + lane] = 0.f;
     }
   };
@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
             slot = slot < 0 ? slot + DCN_WIN : (slot >= DCN_WIN ? slot - DCN_WIN : slot);
             const int cell = (ok[u][q] && inwin) ? slot * DCN_WIN + dxw : SCRATCH;
             win[cell * DCN_CC + lane] += gm * wt[u][q];
-            if (ok[u][q] && !inwin && c < C) unsafeAtomicAdd(dxb + (yy * W + xx) * C + c, gm * wt[u][q]);
+            if (dxb && ok[u][q] && !inwin && c < C) unsafeAtomicAdd(dxb + (yy * W + xx) * C + c, gm * wt[u][q]);
           }
           const float spy = wave_sum_dpp(gm * sy), spx = wave_sum_dpp(gm * sx), smk = wave_sum_dpp(g[u] * val);
           if (lane == 0) {
@@ -211,6 +211,36 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
       }
     }
   }
+}
+
+// Deterministic input gradient (parity mode): one thread per (image, channel) walks every (pixel, tap, corner)
+// of its image in a fixed order and accumulates into its own (n, :, :, c) plane — plain read-modify-writes, no
+// atomics, so the fp32 result is bitwise repeatable. The summation order equals the reference
+// CPU loop's for one channel (pixel-major, taps in order, corners in mmcv's order).
+template <typename T>
+__global__ void __launch_bounds__(64) dcn_dx_serial_kernel(const T* om, int omcs, const T* dcols, float* dx32, int N,
+                                                           int H, int W, int C) {
+  const long id = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= (long)N * C) return;
+  const int n = (int)(id / C), c = (int)(id % C);
+  float* d = dx32 + (long)n * H * W * C + c;
+  for (int h = 0; h < H; ++h)
+    for (int w = 0; w < W; ++w) {
+      const long pix = ((long)n * H + h) * W + w;
+      const T* o = om + pix * omcs;
+      for (int t = 0; t < 9; ++t) {
+        const float m = 1.f / (1.f + __expf(-to_f(o[18 + t])));
+        const float py = (float)(h - 1 + t / 3) + to_f(o[2 * t]), px = (float)(w - 1 + t % 3) + to_f(o[2 * t + 1]);
+        int y0, x0;
+        float wt[4];
+        bool ok[4];
+        dcn_sample(py, px, H, W, y0, x0, wt, ok);
+        const float gm = to_f(dcols[(pix * 9 + t) * C + c]) * m;
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (ok[q]) d[((long)(y0 + (q >> 1)) * W + x0 + (q & 1)) * C] += gm * wt[q];
+      }
+    }
 }
 
 // W (Cout, C, 3, 3) fp32 -> W^T as a 1x1-conv weight [(t*C + c)][co] in dtype
@@ -441,19 +471,30 @@ extern "C" int adr_dcn_im2col(int dtype, const void* x, int xcs, const void* om,
 }
 
 extern "C" int adr_dcn_col2im(int dtype, const void* x, int xcs, const void* om, int omcs, const void* dcols,
-                              float* dx32, void* dom, int domcs, int N, int H, int W, int C, void* stream) {
+                              float* dx32, void* dom, int domcs, int N, int H, int W, int C, int deterministic,
+                              void* stream) {
   ADR_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && omcs >= 27 && domcs >= 27, "dcn_col2im: bad geometry");
   const long waves = (long)N * cdiv(H, DCN_SL) * W;
   ADR_REQUIRE(waves / DCN_WPB < (1l << 31), "dcn_col2im: grid too large");
   hipStream_t st = (hipStream_t)stream;
+  float* dxa = deterministic ? nullptr : dx32;
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(dcn_col2im_kernel<__bf16>, dim3(cdiv(waves, DCN_WPB)), dim3(64 * DCN_WPB), 0, st,
-                       (const __bf16*)x, xcs, (const __bf16*)om, omcs, (const __bf16*)dcols, dx32, (__bf16*)dom, domcs,
+                       (const __bf16*)x, xcs, (const __bf16*)om, omcs, (const __bf16*)dcols, dxa, (__bf16*)dom, domcs,
                        N, H, W, C);
   else
     hipLaunchKernelGGL(dcn_col2im_kernel<float>, dim3(cdiv(waves, DCN_WPB)), dim3(64 * DCN_WPB), 0, st,
-                       (const float*)x, xcs, (const float*)om, omcs, (const float*)dcols, dx32, (float*)dom, domcs, N,
+                       (const float*)x, xcs, (const float*)om, omcs, (const float*)dcols, dxa, (float*)dom, domcs, N,
                        H, W, C);
+  if (deterministic) {
+    const long nc = (long)N * C;
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL(dcn_dx_serial_kernel<__bf16>, dim3(cdiv(nc, 64)), dim3(64), 0, st, (const __bf16*)om, omcs,
+                         (const __bf16*)dcols, dx32, N, H, W, C);
+    else
+      hipLaunchKernelGGL(dcn_dx_serial_kernel<float>, dim3(cdiv(nc, 64)), dim3(64), 0, st, (const float*)om, omcs,
+                         (const float*)dcols, dx32, N, H, W, C);
+  }
   return check_launch("adr_dcn_col2im");
 }
 
