@@ -21,6 +21,8 @@
 // Sampling follows mmcv dmcn_im2col_bilinear / dmcn_get_coordinate_weight: point (h - 1 + i + dy, w - 1 + j + dx),
 // zero unless -1 < py < H and -1 < px < W, every bilinear corner bounds-checked.
 // Shapes: C % 64 == 0, Cout % 64 == 0, omcs % 8 == 0 and >= 32 (the head pads the 27 channels to 32).
+#include <type_traits>
+
 #include "adr_common.h"
 
 namespace adr {
@@ -383,6 +385,7 @@ __global__ void __launch_bounds__(256, 2) dcn_bwd_kernel(DcnArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 S[BROWS * SPITCH];   // [cell][pixel]
   __shared__ __attribute__((aligned(16))) __bf16 D[64 * DPITCH];      // dcols [pixel][channel]
   __shared__ __attribute__((aligned(16))) __bf16 oms[64 * 32];
+  __shared__ __attribute__((aligned(16))) __bf16 WT[2][64 * 72];     // W_t^T [c][co], two taps
   __shared__ int ovf[BOVF];                                            // pixel * 4 + corner
   __shared__ int novf[2];                                              // per-tap queue length (alternating)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -422,14 +425,38 @@ __global__ void __launch_bounds__(256, 2) dcn_bwd_kernel(DcnArgs a) {
     if (pok) v = ld16(a.dy + ppix * a.dycs + 32 * k + 8 * g);
     fb[k] = *reinterpret_cast<bf16x8*>(&v);
   }
-  u32x4 wf[4][2];  // W_t^T fragments (A operand: row = input channel 16 i + (lane & 15), k = output channel)
-  auto wload = [&](int t) {
+  // the tap's W^T slab (LDS, loaded cooperatively) and this lane's bilinear-corner loads, both issued one tap
+  // ahead: the corners into the other of two register sets, the slab through registers into the other LDS buffer
+  u32x2 xv[2][4][4];
+  Corners cs[2];
+  float mks[2];
+  u32x4 wreg[2];
+  auto issue = [&](int t, auto SB) {
+    constexpr int b = decltype(SB)::value;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + 256 * i;
+      wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, (unsigned)((t * 64 + (q >> 3)) * 64 + (q & 7) * 8) * 2u, 0, 0);
+    }
+    const float oy = (float)oms[pl * 32 + 2 * t], ox = (float)oms[pl * 32 + 2 * t + 1];
+    mks[b] = sigm((float)oms[pl * 32 + 18 + t]);
+    sample((float)(ph - 1 + t / 3) + oy, (float)(pw - 1 + t % 3) + ox, a.H, a.W, cs[b]);
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-        wf[i][k] = __builtin_amdgcn_raw_buffer_load_b128(
-            wr, (unsigned)(((t * 64 + 16 * i + (lane & 15)) * 64) + 32 * k + 8 * g) * 2u, 0, 0);
+    for (int q = 0; q < 4; ++q) {
+      const bool ok = pok && cs[b].ok[q];
+      const int pix = ibase + (cs[b].y0 + (q >> 1)) * a.W + cs[b].x0 + (q & 1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        xv[b][q][i] =
+            __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? (unsigned)(pix * a.xcs + 16 * i + 4 * g) * 2u : OOR, 0, 0);
+    }
+  };
+  auto wstore = [&](int b) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + 256 * i;
+      st16(&WT[b][(q >> 3) * 72 + (q & 7) * 8], wreg[i]);
+    }
   };
   // window accumulators: wave w owns channels 16 w .. +15, all 13 cell blocks
   f32x4 win[13];
@@ -441,24 +468,18 @@ __global__ void __launch_bounds__(256, 2) dcn_bwd_kernel(DcnArgs a) {
   const __bf16* dtr = D + (4 * g + q4) * DPITCH + 16 * wave + 4 * p4;
   int prev[4] = {-1, -1, -1, -1};  // S cells written in the previous tap (g == 0 lanes)
   __syncthreads();  // oms / S ready
+  using B0 = std::integral_constant<int, 0>;
+  using B1 = std::integral_constant<int, 1>;
+  issue(0, B0{});
+  wstore(0);
+  __syncthreads();
 
-#pragma unroll 1
-  for (int t = 0; t < 9; ++t) {
-    wload(t);
-    // sampling point of (pixel, tap) and this lane's corner loads (channels 16 i + 4 g .. +3)
-    const float oy = (float)oms[pl * 32 + 2 * t], ox = (float)oms[pl * 32 + 2 * t + 1];
-    const float mk = sigm((float)oms[pl * 32 + 18 + t]);
-    Corners cs;
-    sample((float)(ph - 1 + t / 3) + oy, (float)(pw - 1 + t % 3) + ox, a.H, a.W, cs);
-    u32x2 xv[4][4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool ok = pok && cs.ok[q];
-      const int pix = ibase + (cs.y0 + (q >> 1)) * a.W + cs.x0 + (q & 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        xv[q][i] = __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? (unsigned)(pix * a.xcs + 16 * i + 4 * g) * 2u : OOR, 0, 0);
-    }
+  auto tap = [&](int t, auto SB) {
+    constexpr int cur = decltype(SB)::value;
+    using NB = std::integral_constant<int, 1 - cur>;
+    if (t + 1 < 9) issue(t + 1, NB{});  // WT[1 - cur] was last read before the previous tap's first barrier
+    const Corners& c0 = cs[cur];
+    const float mk = mks[cur];
     // the sampling-matrix column of this pixel: clear the previous tap's entries, write this tap's
     if (g == 0) {
 #pragma unroll
@@ -466,14 +487,14 @@ __global__ void __launch_bounds__(256, 2) dcn_bwd_kernel(DcnArgs a) {
         if (prev[q] >= 0) S[prev[q] * SPITCH + pl] = (__bf16)0.f;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const int yy = cs.y0 + (q >> 1), xx = cs.x0 + (q & 1);
+        const int yy = c0.y0 + (q >> 1), xx = c0.x0 + (q & 1);
         const int cy = yy - wy0, cx = xx - wx0;
-        const bool valid = pok && cs.ok[q];
+        const bool valid = pok && c0.ok[q];
         const bool inwin = cy >= 0 && cy < BWIN && cx >= 0 && cx < BWIN;
         prev[q] = -1;
         if (valid && inwin) {
           prev[q] = cy * BWIN + cx;
-          S[prev[q] * SPITCH + pl] = (__bf16)(mk * cs.w[q]);
+          S[prev[q] * SPITCH + pl] = (__bf16)(mk * c0.w[q]);
         } else if (valid) {
           const int k = atomicAdd(&novf[t & 1], 1);  // at most 64 x 4 = BOVF entries
           ovf[k] = pl * 4 + q;
@@ -487,9 +508,11 @@ __global__ void __launch_bounds__(256, 2) dcn_bwd_kernel(DcnArgs a) {
       acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k = 0; k < 2; ++k)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&wf[i][k]), fb[k], acc[i], 0, 0,
-                                                         0);
+        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            *reinterpret_cast<const bf16x8*>(&WT[cur][(16 * i + (lane & 15)) * 72 + 32 * k + 8 * g]), fb[k], acc[i], 0,
+            0, 0);
     }
+    if (t + 1 < 9) wstore(1 - cur);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       __bf16 v4[4];
@@ -505,17 +528,17 @@ __global__ void __launch_bounds__(256, 2) dcn_bwd_kernel(DcnArgs a) {
       float xf[4][4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const __bf16* e = reinterpret_cast<const __bf16*>(&xv[q][i]);
+        const __bf16* e = reinterpret_cast<const __bf16*>(&xv[cur][q][i]);
 #pragma unroll
         for (int k = 0; k < 4; ++k) xf[q][k] = (float)e[k];
       }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const float top = xf[0][e] + cs.lx * (xf[1][e] - xf[0][e]);
-        const float bot = xf[2][e] + cs.lx * (xf[3][e] - xf[2][e]);
+        const float top = xf[0][e] + c0.lx * (xf[1][e] - xf[0][e]);
+        const float bot = xf[2][e] + c0.lx * (xf[3][e] - xf[2][e]);
         const float d01 = xf[1][e] - xf[0][e], d23 = xf[3][e] - xf[2][e];
-        const float val = top + cs.ly * (bot - top);
-        const float sy = bot - top, sx = d01 + cs.ly * (d23 - d01);
+        const float val = top + c0.ly * (bot - top);
+        const float sy = bot - top, sx = d01 + c0.ly * (d23 - d01);
         const float gv = acc[i][e];
         smk += gv * val;
         spy += gv * sy;
@@ -563,6 +586,11 @@ __global__ void __launch_bounds__(256, 2) dcn_bwd_kernel(DcnArgs a) {
       unsafeAtomicAdd(a.dx32 + (long)(ibase + yy * a.W + xx) * 64 + lane, (float)D[p * DPITCH + lane] * mk2 * c2.w[qq]);
     }
     __syncthreads();  // before the next tap rewrites S / dcols
+  };
+#pragma unroll 1
+  for (int t = 0; t < 9; t += 2) {
+    tap(t, B0{});
+    if (t + 1 < 9) tap(t + 1, B1{});
   }
   // flush the window: one global atomic per (cell, channel) that received anything
 #pragma unroll
