@@ -64,7 +64,7 @@ def cpu_baseline(bs=2, img=640, budget_s=20.0):
 def pmc_traffic(symbol):
     """HBM bytes per launch of `symbol` from the committed PMC passes (profiles/pmc_traffic.json, written by
     scripts/pmc_traffic.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this same bench); (None, None)
-    when the kernel was not covered."""
+    when the kernel was not covered. Matches the demangled name, or the unique entry the label is a prefix of."""
     import subprocess
     f = ROOT / "profiles" / "pmc_traffic.json"
     if not f.exists():
@@ -78,8 +78,31 @@ def pmc_traffic(symbol):
             return None, None
     rec = doc["kernels"].get(name)
     if rec is None:
-        return None, None
+        hits = [k for k in doc["kernels"] if k.replace("void ", "").startswith(name + "(")]
+        if len(hits) != 1:
+            return None, None
+        rec = doc["kernels"][hits[0]]
     return rec["hbm_bytes_per_launch"], f"profiles/pmc_traffic.json ({rec['launches']} launches)"
+
+
+# SURVEY.md §8d / BASELINE.md §3: per-image algorithmic work of the fwd+bwd step at n/640 (layer granularity)
+NET_BYTES_PER_IMG = 210e6
+NET_FLOPS_PER_IMG = 34.6e9
+
+
+def conv_attainable(detail, hbm_gbs, mfma_tf):
+    """Attainable-roofline fraction of the conv family (north_star: '>= 70 % CDNA4 bf16 MFMA roofline on the fused
+    Conv-BN-SiLU backbone'): sum over conv fwd/dgrad launches of max(bytes / HBM peak, flops / MFMA peak)
+    divided by their measured time."""
+    ideal = meas = 0.0
+    for tag, shape, nb, fl, t in detail:
+        if not (tag.startswith("_ZN3adr16conv_bf16") or tag.startswith("_ZN3adr12conv3") or "stem" in tag):
+            continue
+        ideal += max(nb / (hbm_gbs * 1e9), fl / (mfma_tf * 1e12))
+        meas += t
+    return None if meas == 0 else {"launches_timed": sum(1 for d in detail if d[0].startswith(("_ZN3adr16conv_bf16",
+                                                                                                "_ZN3adr12conv3"))),
+                                   "attainable_frac": round(ideal / meas, 4), "ms_total": round(1e3 * meas, 3)}
 
 
 def main():
@@ -154,9 +177,14 @@ def main():
     ips = world * args.bs * args.steps / dt
     if rank == 0:
         finite = bool(torch.isfinite(items).all())
-        roof = K.roofline_report(ktimes, dtype, HBM_PEAK_GBS, BF16_MFMA_PEAK_TF if dtype == torch.bfloat16 else F32_MFMA_PEAK_TF)
+        mfma_peak = BF16_MFMA_PEAK_TF if dtype == torch.bfloat16 else F32_MFMA_PEAK_TF
+        roof = K.roofline_report(ktimes, dtype, HBM_PEAK_GBS, mfma_peak)
         if roof is not None:
             roof["traffic"], roof["traffic_source"] = pmc_traffic(roof["kernel"])
+            roof["network"] = {"bytes_per_img": NET_BYTES_PER_IMG, "flops_per_img": NET_FLOPS_PER_IMG,
+                               "hbm_frac": round(ips * NET_BYTES_PER_IMG / (HBM_PEAK_GBS * 1e9), 4),
+                               "mfma_frac": round(ips * NET_FLOPS_PER_IMG / (mfma_peak * 1e12), 4)}
+            roof["conv_family"] = conv_attainable(K.timing_detail(), HBM_PEAK_GBS, mfma_peak)
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(budget_s=args.cpu_budget)
         out = {
             "metric": "images/sec whole-node (640x640) fwd+bwd, YOLO-AD-Refine-n at 1/2/4/8 GPU",

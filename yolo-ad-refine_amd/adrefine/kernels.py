@@ -40,16 +40,24 @@ _TRACE_RELAYOUT = bool(int(__import__("os").environ.get("ADR_TRACE_RELAYOUT", "0
 # live per-kernel timing with HIP events on the launch stream (bench.py roofline); off unless timing_begin()
 # ---------------------------------------------------------------------------------------------------------
 _TIMING = None
+_ANNOT = [0]  # > 0 inside an annotated _t0/_t1 region (its own bytes / flops; the generic hook stays out)
 
 
 def timing_begin():
+    """Time every libadr launch of the following eager work with HIP events on the launch stream: the conv / DCN
+    paths annotate their launches with algorithmic bytes and flops (_t0/_t1); every other entry point is caught
+    by the generic hook below, with bytes from _ALG_BYTES where the entry point has an estimator."""
     global _TIMING
     _TIMING = []
+    from . import native
+    native.CALL_HOOK = _hook_call
 
 
 def timing_end():
     global _TIMING
     global _DETAIL
+    from . import native
+    native.CALL_HOOK = None
     recs, _TIMING = _TIMING, None
     if not recs:
         return []
@@ -79,6 +87,7 @@ def _reps(accumulate=0):
 def _t0(tag, nbytes, flops, shape="", rep=1):
     if _TIMING is None:
         return None
+    _ANNOT[0] += 1
     e0 = torch.cuda.Event(enable_timing=True)
     e0.record()
     return (tag, nbytes, flops, e0, shape, rep)
@@ -86,10 +95,57 @@ def _t0(tag, nbytes, flops, shape="", rep=1):
 
 def _t1(tok):
     if tok is not None:
+        _ANNOT[0] -= 1
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record()
         tag, nb, fl, e0, shape, rep = tok
         _TIMING.append((tag, nb, fl, e0, e1, shape, rep))
+
+
+def _es(dtype_code):
+    return 2 if dtype_code == BF16 else 4
+
+
+# entry point -> (kernel label as rocprofv3 names it, algorithmic bytes from the call's arguments, idempotent?)
+# Algorithmic bytes: every tensor the launch must touch, read or written once (NHWC activations, compute dtype).
+_ALG_BYTES = {
+    "adr_affine_act_bwd": ("adr::affine_act_bwd_kernel<__bf16>",
+                           lambda a: _es(a[0]) * a[18] * a[19] * a[20] * (3 + a[21]), lambda a: a[21] == 0),
+    "adr_affine_act": ("adr::affine_act_kernel<__bf16>", lambda a: _es(a[0]) * a[11] * a[12] * a[13] * 2,
+                       lambda a: True),
+    "adr_nc_reduce": (lambda a: f"adr::nc_reduce_kernel<__bf16, {1 if a[1] == 1 else 0}>",
+                      lambda a: _es(a[0]) * a[12] * a[13] * a[14] * (2 if a[1] == 1 else 1), lambda a: True),
+    "adr_ew": ("adr::ew_kernel<__bf16>",
+               lambda a: _es(a[0]) * a[11] * a[12] * (2 + (a[5] is not None) + (a[7] is not None) + a[15]),
+               lambda a: False),
+}
+
+
+def _hook_call(name, fn, args):
+    """Generic timing of one libadr call (outside annotated regions)."""
+    if _TIMING is None or _ANNOT[0] > 0:
+        rc = fn(*args)
+    else:
+        spec = _ALG_BYTES.get(name)
+        label, nbytes, rep = name, None, 1
+        if spec is not None:
+            label = spec[0](args) if callable(spec[0]) else spec[0]
+            if args[0] != BF16:
+                label = label.replace("__bf16", "float")
+            nbytes = int(spec[1](args))
+            rep = TIMING_REPEAT if spec[2](args) else 1
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        rc = 0
+        for _ in range(rep):
+            rc = fn(*args)
+            if rc != 0:
+                break
+        e1.record()
+        _TIMING.append((label, nbytes, 0, e0, e1, "", rep))
+    if rc != 0:
+        raise RuntimeError(f"{name}: {lib.lib.adr_last_error().decode()}")
+    return rc
 
 
 def _bn_of(n):
@@ -97,31 +153,34 @@ def _bn_of(n):
 
 
 def roofline_report(recs, dtype, hbm_gbs, mfma_tf):
-    """Dominant kernel family by total measured time -> achieved algorithmic GB/s and TF/s vs peaks."""
+    """The dominant kernel of the measured step (largest total time over every timed launch) -> achieved
+    algorithmic GB/s or TF/s against the bound that applies to it (HBM below the ridge, MFMA above)."""
     if not recs:
         return None
     agg = {}
     for tag, nb, fl, t in recs:
-        a = agg.setdefault(tag, [0, 0.0, 0.0, 0.0])
+        a = agg.setdefault(tag, [0, 0.0, 0.0, 0.0, True])
         a[0] += 1
-        a[1] += nb
-        a[2] += fl
+        a[1] += nb or 0
+        a[2] += fl or 0
         a[3] += t
-    tag, (cnt, nb, fl, t) = max(agg.items(), key=lambda kv: kv[1][3])
-    gbs = nb / t / 1e9
+        a[4] = a[4] and nb is not None
+    total_t = sum(v[3] for v in agg.values())
+    tag, (cnt, nb, fl, t, known) = max(agg.items(), key=lambda kv: kv[1][3])
+    gbs = nb / t / 1e9 if known else None
     tfs = fl / t / 1e12
     ridge = mfma_tf * 1e12 / (hbm_gbs * 1e9)
     ai = fl / max(nb, 1)
     bound = "mfma" if ai > ridge else "hbm"
     achieved, peak, unit = (tfs, mfma_tf, "TFLOP/s") if bound == "mfma" else (gbs, hbm_gbs, "GB/s")
-    total_t = sum(v[3] for v in agg.values())
-    return {"bound": bound, "achieved": round(achieved, 2), "peak": peak, "unit": unit,
-            "frac": round(achieved / peak, 4), "traffic": None, "kernel": tag, "launches": cnt,
-            "avg_us": round(1e6 * t / cnt, 2), "alg_bytes_per_launch": int(nb / cnt),
-            "alg_flops_per_launch": int(fl / cnt), "achieved_gbs": round(gbs, 1), "achieved_tfs": round(tfs, 2),
-            "share_of_timed_conv_time": round(t / total_t, 3),
-            "kernels": {k: {"launches": v[0], "ms_total": round(1e3 * v[3], 3), "avg_us": round(1e6 * v[3] / v[0], 2)}
-                        for k, v in sorted(agg.items(), key=lambda kv: -kv[1][3])}}
+    return {"bound": bound, "achieved": None if achieved is None else round(achieved, 2), "peak": peak, "unit": unit,
+            "frac": None if achieved is None else round(achieved / peak, 4), "traffic": None, "kernel": tag,
+            "launches": cnt, "avg_us": round(1e6 * t / cnt, 2), "alg_bytes_per_launch": int(nb / cnt),
+            "alg_flops_per_launch": int(fl / cnt), "achieved_gbs": None if gbs is None else round(gbs, 1),
+            "achieved_tfs": round(tfs, 2), "share_of_timed_time": round(t / total_t, 3),
+            "kernels": {k: {"launches": v[0], "ms_total": round(1e3 * v[3], 3), "avg_us": round(1e6 * v[3] / v[0], 2),
+                            "gbs": round(v[1] / v[3] / 1e9, 1) if v[4] and v[1] else None}
+                        for k, v in sorted(agg.items(), key=lambda kv: -kv[1][3])[:25]}}
 
 
 def dcode(dtype) -> int:

@@ -74,6 +74,8 @@ class _Lib:
             def call(*a):
                 if OP_TRACE is not None:
                     return _traced(name, fn, a)
+                if CALL_HOOK is not None:
+                    return CALL_HOOK(name, fn, a)
                 rc = fn(*a)
                 if rc != 0:
                     raise RuntimeError(f"{name}: {self.lib.adr_last_error().decode()}")
@@ -83,6 +85,10 @@ class _Lib:
         setattr(self, name, fn)
         return fn
 
+
+# Measurement hook (kernels.timing_begin for bench.py's roofline): when set, status-returning entry points are
+# called as CALL_HOOK(name, fn, args) -> status.
+CALL_HOOK = None
 
 # Development op tracer (scripts/op_table.py): when OP_TRACE is a list, every status-returning entry point is
 # bracketed by HIP events on the current stream and recorded as (name, caller, int args, event0, event1).
