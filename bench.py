@@ -79,6 +79,9 @@ def pmc_traffic(symbol):
     rec = doc["kernels"].get(name)
     if rec is None:
         hits = [k for k in doc["kernels"] if k.replace("void ", "").startswith(name + "(")]
+        if not hits and name.startswith("adr::") and name.endswith("<__bf16>"):
+            base = name[5:-8]  # rocprofv3 leaves these templates mangled: _ZN3adr<len><name>IDF16b...
+            hits = [k for k in doc["kernels"] if k.startswith(f"_ZN3adr{len(base)}{base}IDF16b")]
         if len(hits) != 1:
             return None, None
         rec = doc["kernels"][hits[0]]
@@ -96,7 +99,7 @@ def conv_attainable(detail, hbm_gbs, mfma_tf):
     divided by their measured time."""
     ideal = meas = 0.0
     for tag, shape, nb, fl, t in detail:
-        if not (tag.startswith("_ZN3adr16conv_bf16") or tag.startswith("_ZN3adr12conv3") or "stem" in tag):
+        if nb is None or not (tag.startswith("_ZN3adr16conv_bf16") or tag.startswith("_ZN3adr12conv3")):
             continue
         ideal += max(nb / (hbm_gbs * 1e9), fl / (mfma_tf * 1e12))
         meas += t

@@ -117,13 +117,20 @@ _ALG_BYTES = {
                       lambda a: _es(a[0]) * a[12] * a[13] * a[14] * (2 if a[1] == 1 else 1), lambda a: True),
     "adr_ew": ("adr::ew_kernel<__bf16>",
                lambda a: _es(a[0]) * a[11] * a[12] * (2 + (a[5] is not None) + (a[7] is not None) + a[15]),
-               lambda a: False),
+               lambda a: a[15] == 0 and _ptr(a[9]) not in (_ptr(a[3]), _ptr(a[5]), _ptr(a[7]))),
 }
 
 
+def _ptr(v):
+    return v.value if isinstance(v, ctypes.c_void_p) else v
+
+
+_UNTIMED = ("_symbol", "_workspace", "_splits", "_tiles", "_chunks", "_size", "_floats", "adr_set_f32")
+
+
 def _hook_call(name, fn, args):
-    """Generic timing of one libadr call (outside annotated regions)."""
-    if _TIMING is None or _ANNOT[0] > 0:
+    """Generic timing of one libadr call (outside annotated regions; host-side queries are not timed)."""
+    if _TIMING is None or _ANNOT[0] > 0 or name.endswith(_UNTIMED):
         rc = fn(*args)
     else:
         spec = _ALG_BYTES.get(name)
