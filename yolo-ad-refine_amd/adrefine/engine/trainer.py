@@ -154,6 +154,8 @@ class FusedTrainer:
         # EMA over every floating state entry (params + BN running stats), buffers as group 3
         self.use_ema = ema
         pset = {id(p) for _, p, _, _ in self.entries}
+        # integer buffers (BN num_batches_tracked) as the reference's EMA copy holds them: never updated
+        self.ema_int = {k: v.detach().clone() for k, v in model.state_dict().items() if not v.dtype.is_floating_point}
         for k, v in model.state_dict(keep_vars=True).items():
             if v.dtype.is_floating_point and id(v) not in pset:
                 self.entries.append((k, v, 3, False))
