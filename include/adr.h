@@ -421,6 +421,9 @@ int adr_seed_advance(int64_t* seed, void* stream);
  * agnostic: one NMS over all classes (single-label only); class_mask[nc] (nullable): the `classes` filter.
  * out (B, max_det, 6) rows x1 y1 x2 y2 conf cls in the reference's output order; nout[B] valid rows per image.
  * Requires A <= 16384, nc <= 1024, max_det <= 300. */
+/* Pairwise IoU of xyxy boxes a (N,4) and b (M,4) -> out (N,M), eps added to the union (utils/metrics.py:52-72);
+ * the validator's TP matching (models/yolo/detect/val.py:213-214). */
+int adr_box_iou(const float* a, int N, const float* b, int M, float eps, float* out, void* stream);
 size_t adr_nms_workspace(int B, int nc, int A, int multi, int max_det);
 int adr_nms(const float* y, int B, int nc, int A, float conf, float iou, int multi, int agnostic,
             const unsigned char* class_mask, int max_det, int max_nms, float max_wh, float* out, int* nout, void* ws,

@@ -89,6 +89,16 @@ def main():
     OUT.mkdir(parents=True, exist_ok=True)
     torch.set_num_threads(8)
     only_nms = "--only-nms" in sys.argv
+    only = [a.split("=", 1)[1] for a in sys.argv if a.startswith("--only=")]
+    if only:
+        manifest = json.loads((OUT / "MANIFEST.json").read_text())
+
+        def note(name, what, cites, unpinned=False):
+            manifest["fixtures"][name] = {"what": what, "reference": cites, "unpinned_3rdparty": unpinned}
+        for what in only[0].split(","):
+            globals()[f"{what}_fixtures"](tasks, block, conv, head, uloss, uops, note)
+        (OUT / "MANIFEST.json").write_text(json.dumps(manifest, indent=1))
+        return
     if only_nms:
         manifest = json.loads((OUT / "MANIFEST.json").read_text())
     else:
@@ -233,6 +243,62 @@ def main():
 
     (OUT / "MANIFEST.json").write_text(json.dumps(manifest, indent=1))
     print("wrote", len(list(OUT.glob("*.npz"))), "fixtures to", OUT)
+
+
+def metrics_fixtures(tasks, block, conv, head, uloss, uops, note):
+    """Validator metrics tail on synthetic detections: per-image box_iou (utils/metrics.py:52) + greedy
+    match_predictions (engine/validator.py:221) -> tp (N, 10); ap_per_class (metrics.py:1144) + Metric
+    mean_results / fitness (metrics.py:1340-1358). Inputs are stored in the fixture."""
+    from ultralytics.engine.validator import BaseValidator
+    from ultralytics.utils import metrics as M
+    rng = np.random.default_rng(123)
+    preds, labels = [], []
+    for img in range(6):
+        n = int(rng.integers(0 if img == 5 else 2, 14))
+        xy = rng.uniform(20, 560, (n, 2))
+        wh = rng.uniform(8, 200, (n, 2))
+        gt = np.concatenate([xy, np.minimum(xy + wh, 639)], 1)
+        gcls = rng.integers(0, 12, n).astype(np.float32)
+        rows = []
+        for k in range(n):
+            if rng.random() < 0.8:  # a detection of this object, jittered
+                j = gt[k] + rng.normal(0, 0.08, 4) * np.r_[wh[k], wh[k]]
+                c = gcls[k] if rng.random() < 0.9 else float(rng.integers(0, 12))
+                rows.append([*j, rng.uniform(0.2, 1.0), c])
+        for _ in range(int(rng.integers(0, 20))):  # false positives
+            xy0 = rng.uniform(0, 600, 2)
+            rows.append([*xy0, *(xy0 + rng.uniform(5, 150, 2)), rng.uniform(0.001, 0.7), float(rng.integers(0, 12))])
+        if img == 4:
+            rows = []  # an image with labels and no detections
+        pr = np.array(rows, dtype=np.float32).reshape(-1, 6)
+        preds.append(pr)
+        labels.append(np.concatenate([np.full((n, 1), img, np.float32), gcls[:, None], gt.astype(np.float32)], 1))
+    v = BaseValidator.__new__(BaseValidator)
+    v.iouv = torch.linspace(0.5, 0.95, 10)
+    tps, confs, pcls, tcls = [], [], [], []
+    for img, (pr, lb) in enumerate(zip(preds, labels)):
+        p = torch.from_numpy(pr)
+        if len(lb) and len(pr):
+            iou = M.box_iou(torch.from_numpy(lb[:, 2:6]), p[:, :4])
+            tp = v.match_predictions(p[:, 5], torch.from_numpy(lb[:, 1]), iou).numpy()
+        else:
+            tp = np.zeros((len(pr), 10), dtype=bool)
+        tps.append(tp)
+        confs.append(pr[:, 4])
+        pcls.append(pr[:, 5])
+        tcls.append(lb[:, 1])
+    tp, conf, pc, tc = (np.concatenate(a, 0) for a in (tps, confs, pcls, tcls))
+    res = M.ap_per_class(tp, conf, pc, tc)
+    met = M.Metric()
+    met.update(res[2:])
+    d = {"preds": np.concatenate([np.concatenate([np.full((len(p), 1), i, np.float32), p], 1)
+                                  for i, p in enumerate(preds)], 0),
+         "labels": np.concatenate(labels, 0), "tp": tp, "p": res[2], "r": res[3], "ap": res[5],
+         "ap_class_index": res[6], "mean_results": np.array(met.mean_results(), dtype=np.float64),
+         "fitness": np.array(met.fitness(), dtype=np.float64)}
+    np.savez_compressed(OUT / "metrics_val.npz", **d)
+    note("metrics_val", "validator TP matching + ap_per_class + Metric on synthetic detections (6 images)",
+         "models/yolo/detect/val.py:125-229, engine/validator.py:221-261, utils/metrics.py:52,1112-1360")
 
 
 def nms_fixtures(uops, note):

@@ -392,3 +392,28 @@ extern "C" int adr_nms(const float* y, int B, int nc, int A, float conf, float i
   hipLaunchKernelGGL(nms_merge_kernel, dim3(B), dim3(64), 0, st, a);
   return check_launch("adr_nms");
 }
+
+// ---------------- box IoU matrix for the validator's TP matching (models/yolo/detect/val.py:213-214) ----------------
+// out[i][j] = inter / (area_a + area_b - inter + eps), xyxy boxes, the reference's utils/metrics.py:52-72 arithmetic
+// order (compiled without FMA contraction, like the rest of this file).
+__global__ void __launch_bounds__(256) box_iou_kernel(const float* __restrict__ a, int N, const float* __restrict__ b,
+                                                      int M, float eps, float* __restrict__ out) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long)N * M) return;
+  const int r = (int)(i / M), c = (int)(i % M);
+  const float ax1 = a[4 * r], ay1 = a[4 * r + 1], ax2 = a[4 * r + 2], ay2 = a[4 * r + 3];
+  const float bx1 = b[4 * c], by1 = b[4 * c + 1], bx2 = b[4 * c + 2], by2 = b[4 * c + 3];
+  const float iw = fmaxf(fminf(ax2, bx2) - fmaxf(ax1, bx1), 0.f);
+  const float ih = fmaxf(fminf(ay2, by2) - fmaxf(ay1, by1), 0.f);
+  const float inter = iw * ih;
+  const float area_a = (ax2 - ax1) * (ay2 - ay1), area_b = (bx2 - bx1) * (by2 - by1);
+  out[i] = inter / (area_a + area_b - inter + eps);
+}
+
+extern "C" int adr_box_iou(const float* a, int N, const float* b, int M, float eps, float* out, void* stream) {
+  ADR_REQUIRE(N >= 0 && M >= 0, "box_iou: N=%d M=%d", N, M);
+  if ((long)N * M == 0) return 0;
+  hipLaunchKernelGGL(box_iou_kernel, dim3(cdiv((long)N * M, 256)), dim3(256), 0, (hipStream_t)stream, a, N, b, M, eps,
+                     out);
+  return check_launch("adr_box_iou");
+}
