@@ -120,6 +120,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel from Python (no hipGraph replay)")
     ap.add_argument("--roofline-steps", type=int, default=2)
+    ap.add_argument("--float-images", action="store_true", help="feed pre-normalised fp32 images instead of uint8")
     args = ap.parse_args()
 
     import torch
@@ -145,7 +146,9 @@ def main():
             dist.broadcast(p.data, 0)
     # the reference's batch_size is the GLOBAL batch (trainer.py:290, 305-306): accumulate and weight decay
     tr = FusedTrainer(model, batch_size=world * args.bs, world_size=world)
-    batch, _ = train_batch(args.bs, args.img, seed=1000 * rank, device=dev)  # rank's shard of the stream
+    # rank's shard of the stream, as the dataloader yields it: uint8 images (preprocess_batch's /255 runs inside the
+    # step, fused into the stem kernels) + COCO-shape labels
+    batch, _ = train_batch(args.bs, args.img, seed=1000 * rank, device=dev, u8=not args.float_images)
 
     for _ in range(args.warmup):
         tr.step(batch)
@@ -193,7 +196,8 @@ def main():
             "metric": "images/sec whole-node (640x640) fwd+bwd, YOLO-AD-Refine-n at 1/2/4/8 GPU",
             "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype, "data": "synthetic",
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "data": "synthetic (uint8 images + COCO-shape labels)" if not args.float_images else "synthetic (fp32 images)",
             "config": {"workload": f"yolo11-701-YOLO-AD-Refine.yaml (n) train step bs={args.bs}/GPU "
                                    f"{args.img}x{args.img}, synthetic COCO-shape labels, TAL+DFL+CIoU/NWD loss, "
                                    f"SGD+EMA", "global_batch": world * args.bs, "img": args.img,

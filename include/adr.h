@@ -170,8 +170,16 @@ int adr_stem_conv_fwd(const float* img, int N, int H, int W, const float* w, int
 size_t adr_stem_wgrad_workspace(int N, int H, int W, int K);
 int adr_stem_conv_wgrad(const float* img, int N, int H, int W, const void* dy, int dcs, int K, float* dw,
                         int accumulate, float* ws, size_t ws_bytes, void* stream);
+/* The same on the dataloader's uint8 NCHW batch: preprocess_batch's .float() / 255 (detect/train.py:57-59) is
+ * applied while the rows are staged, so the float image never exists in HBM. */
+int adr_stem_conv_fwd_u8(const uint8_t* img, int N, int H, int W, const float* w, int K, void* y, int ycs,
+                         float* stats, void* stream);
+int adr_stem_conv_wgrad_u8(const uint8_t* img, int N, int H, int W, const void* dy, int dcs, int K, float* dw,
+                           int accumulate, float* ws, size_t ws_bytes, void* stream);
 /* NCHW fp32 images (detect/train.py:57-59 preprocess output) -> NHWC compute dtype, channels padded to Cp. */
 int adr_image_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cp, void* stream);
+/* uint8 NCHW images -> NHWC compute dtype, value / 255 (preprocess_batch), channels padded to Cp. */
+int adr_image_u8_to_nhwc(int dtype, const uint8_t* src, void* dst, int N, int C, int H, int W, int Cp, void* stream);
 int adr_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long n, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------

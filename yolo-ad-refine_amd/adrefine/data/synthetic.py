@@ -15,6 +15,13 @@ def images(bs: int, size: int, seed: int = 0) -> torch.Tensor:
     return torch.rand(bs, 3, size, size, generator=g)
 
 
+def images_u8(bs: int, size: int, seed: int = 0) -> torch.Tensor:
+    """The dataloader's form of a batch: uint8 NCHW (YOLODataset.collate_fn stacks uint8 images; the trainer's
+    preprocess_batch divides by 255 on the device, detect/train.py:57-59)."""
+    g = torch.Generator().manual_seed(seed)
+    return torch.randint(0, 256, (bs, 3, size, size), generator=g, dtype=torch.uint8)
+
+
 def labels(bs: int, nc: int = 80, seed: int = 1, mean_n: float = 7.3, max_n: int = 93):
     """Per image n ~ Poisson(mean_n) clipped to [1, max_n]; cls ~ U{0..nc-1}; centre ~ U(0.05, 0.95)^2;
     w, h = exp(U(ln 0.02, ln 0.6)) shrunk to stay inside the image."""
@@ -34,9 +41,11 @@ def labels(bs: int, nc: int = 80, seed: int = 1, mean_n: float = 7.3, max_n: int
     return {"batch_idx": torch.cat(bi), "cls": torch.cat(cl), "bboxes": torch.cat(bx)}
 
 
-def train_batch(bs: int, img: int, seed: int, device, nc: int = 80):
-    """Device-resident batch for FusedTrainer.step: {'img': (bs,3,img,img) fp32, 'gt': (bs, nmax, 5)}."""
+def train_batch(bs: int, img: int, seed: int, device, nc: int = 80, u8: bool = False):
+    """Device-resident batch for FusedTrainer.step: {'img': (bs,3,img,img) fp32 in [0, 1] (or the uint8 batch the
+    dataloader yields, u8=True), 'gt': (bs, nmax, 5)}."""
     from ..utils.loss import preprocess_targets
     lab = labels(bs, nc, seed=seed + 1)
     gt = preprocess_targets(lab["batch_idx"], lab["cls"], lab["bboxes"], bs, (img, img)).to(device)
-    return {"img": images(bs, img, seed=seed).to(device), "gt": gt}, lab
+    im = images_u8(bs, img, seed=seed) if u8 else images(bs, img, seed=seed)
+    return {"img": im.to(device), "gt": gt}, lab

@@ -870,15 +870,17 @@ class GNActFn(torch.autograd.Function):
 
 
 class StemConvFn(torch.autograd.Function):
-    """model.0 Conv(3, K, 3, 2)'s convolution read straight from the fp32 NCHW image (bf16 compute): returns the
-    pre-BN output (NHWC bf16) and its BatchNorm partial statistics; backward = the weight gradient only (the
-    image needs none)."""
+    """model.0 Conv(3, K, 3, 2)'s convolution read straight from the NCHW image batch (bf16 compute): fp32 images
+    (already preprocessed), or the dataloader's uint8 batch with preprocess_batch's /255 (detect/train.py:57-59)
+    applied inside the kernel. Returns the pre-BN output (NHWC bf16) and its BatchNorm partial statistics;
+    backward = the weight gradient only (the image needs none)."""
 
     @staticmethod
     def forward(ctx, img, w, want_stats):
         ctx.set_materialize_grads(False)
         _req_cuda(img)
-        img = img.float().contiguous()
+        u8 = img.dtype == torch.uint8
+        img = img.contiguous() if u8 else img.float().contiguous()
         N, _, H, W = img.shape
         Kc = w.shape[0]
         Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
@@ -887,8 +889,8 @@ class StemConvFn(torch.autograd.Function):
         if want_stats:
             stats = torch.empty(lib.adr_stem_fwd_tiles(N, Ho) * 2 * Kc, dtype=torch.float32, device=img.device)
         wf = w.detach().float().contiguous()
-        lib.adr_stem_conv_fwd(fptr(img), N, H, W, fptr(wf), Kc, ctypes.c_void_p(y.data_ptr()), Kc, fptr(stats),
-                              stream())
+        (lib.adr_stem_conv_fwd_u8 if u8 else lib.adr_stem_conv_fwd)(
+            fptr(img), N, H, W, fptr(wf), Kc, ctypes.c_void_p(y.data_ptr()), Kc, fptr(stats), stream())
         ctx.save_for_backward(img)
         ctx.pw = w
         if stats is None:
@@ -908,7 +910,8 @@ class StemConvFn(torch.autograd.Function):
         dw, pdw, acc = grad_dst(w, w.numel(), img.device)
         wsb = lib.adr_stem_wgrad_workspace(N, H, W, Kc)
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=img.device)
-        lib.adr_stem_conv_wgrad(fptr(img), N, H, W, ctypes.c_void_p(dyp), dycs, Kc, pdw, acc, fptr(ws), wsb, stream())
+        (lib.adr_stem_conv_wgrad_u8 if img.dtype == torch.uint8 else lib.adr_stem_conv_wgrad)(
+            fptr(img), N, H, W, ctypes.c_void_p(dyp), dycs, Kc, pdw, acc, fptr(ws), wsb, stream())
         return None, grad_ret(w, dw), None
 
 
@@ -917,15 +920,20 @@ def stem_conv(img, w, want_stats):
 
 
 def image_to_nhwc(img: torch.Tensor, dtype, cpad=8):
-    """(B, 3, H, W) float images -> NHWC compute-dtype activation with channels padded to `cpad`."""
+    """(B, 3, H, W) float images, or uint8 images (divided by 255 on the way, preprocess_batch) -> NHWC
+    compute-dtype activation with channels padded to `cpad`."""
     _req_cuda(img)
-    img = img.float()
+    u8 = img.dtype == torch.uint8
+    if not u8:
+        img = img.float()
     if not img.is_contiguous():
         relayout_count[0] += 1
         img = img.contiguous()
     N, C, H, W = img.shape
     out = empty_act(N, cpad, H, W, dtype, img.device)
-    lib.adr_image_to_nhwc(dcode(dtype), fptr(img), ctypes.c_void_p(out.data_ptr()), N, C, H, W, cpad, stream())
+    (lib.adr_image_u8_to_nhwc if u8 else lib.adr_image_to_nhwc)(dcode(dtype), fptr(img),
+                                                                ctypes.c_void_p(out.data_ptr()), N, C, H, W, cpad,
+                                                                stream())
     return out
 
 

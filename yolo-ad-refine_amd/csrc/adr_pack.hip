@@ -209,6 +209,37 @@ __global__ void __launch_bounds__(256) image_to_nhwc8_kernel(const float* __rest
   }
 }
 
+// uint8 NCHW batch -> NHWC compute-dtype activation with channels zero-padded to Cp, value / 255 (preprocess_batch)
+template <typename T>
+__global__ void image_u8_to_nhwc_kernel(const uint8_t* __restrict__ src, T* __restrict__ dst, int N, int C, int H,
+                                        int W, int Cp) {
+  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long n = (long)N * H * W * Cp;
+  if (i >= n) return;
+  int c = (int)(i % Cp);
+  long pix = i / Cp;
+  int w = (int)(pix % W);
+  long r = pix / W;
+  int h = (int)(r % H);
+  int b = (int)(r / H);
+  float v = c < C ? (float)src[(((long)b * C + c) * H + h) * W + w] / 255.f : 0.f;
+  dst[i] = from_f<T>(v);
+}
+
+extern "C" int adr_image_u8_to_nhwc(int dtype, const uint8_t* src, void* dst, int N, int C, int H, int W, int Cp,
+                                    void* stream) {
+  ADR_REQUIRE(Cp >= C && C > 0, "image_u8_to_nhwc: C=%d Cp=%d", C, Cp);
+  long n = (long)N * H * W * Cp;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16)
+    hipLaunchKernelGGL(image_u8_to_nhwc_kernel<__bf16>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (__bf16*)dst, N, C, H,
+                       W, Cp);
+  else
+    hipLaunchKernelGGL(image_u8_to_nhwc_kernel<float>, dim3(cdiv(n, 256)), dim3(256), 0, st, src, (float*)dst, N, C, H,
+                       W, Cp);
+  return check_launch("adr_image_u8_to_nhwc");
+}
+
 extern "C" int adr_image_to_nhwc(int dtype, const float* src, void* dst, int N, int C, int H, int W, int Cp,
                                  void* stream) {
   long n = (long)N * H * W * Cp;

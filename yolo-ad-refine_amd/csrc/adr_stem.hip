@@ -7,7 +7,9 @@
 //     v_mfma_f32_16x16x32_bf16: A = dy^T (16 output channels x 32 pixels), B = im2col (32 pixels x 2 x 16
 //     columns), accumulated per wave over a pixel range, block partials summed in a fixed order.
 // Both replace image_to_nhwc + the generic implicit GEMM on a channel-padded copy of the image (420 MB of
-// bf16 written and read twice per bs64 step) with one read of the fp32 image per pass.
+// bf16 written and read twice per bs64 step) with one read of the image per pass. The _u8 entry points read the
+// dataloader's uint8 batch and apply preprocess_batch's /255 (detect/train.py:57-59) while staging: the
+// float image never exists (79 MB read per pass at bs 64 instead of 315 MB).
 #include "adr_common.h"
 
 namespace adr {
@@ -16,8 +18,45 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 
 constexpr int STEM_ROWS = 2;
 
+// image element -> the reference's preprocessed value: fp32 as is; uint8 as .float() / 255 (detect/train.py:57-59,
+// the dataloader's uint8 batch normalised on the device), an IEEE division like torch's
+__device__ __forceinline__ float img_val(float v) { return v; }
+__device__ __forceinline__ float img_val(uint8_t v) { return (float)v / 255.f; }
+
 // stage image rows iy0 .. iy0+IR-1 of the 3 channels of image n into LDS as bf16 [3][IR][W+2] with zero
-// columns at -1 and W (and zero rows outside the image); 16-byte loads when W % 4 == 0
+// columns at -1 and W (and zero rows outside the image); 16-byte (fp32) / 4-byte (uint8) loads when W % 4 == 0
+template <int IR>
+__device__ __forceinline__ void stage_rows(const uint8_t* __restrict__ img, int n, int H, int W, int iy0, __bf16* xs) {
+  constexpr int NR = 3 * IR;
+  const int Wp = W + 2;
+  if ((W & 3) == 0) {
+    for (int q = threadIdx.x; q < W / 4; q += blockDim.x) {
+      unsigned v[NR];
+#pragma unroll
+      for (int row = 0; row < NR; ++row) {
+        const int c = row / IR, iy = iy0 + row % IR;
+        const bool rok = iy >= 0 && iy < H;
+        v[row] = rok ? *reinterpret_cast<const unsigned*>(img + (((long)n * 3 + c) * H + iy) * W + 4 * q) : 0u;
+      }
+#pragma unroll
+      for (int row = 0; row < NR; ++row)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) xs[row * Wp + 1 + 4 * q + e] = (__bf16)img_val((uint8_t)(v[row] >> (8 * e)));
+    }
+  } else {
+    for (int row = 0; row < NR; ++row) {
+      const int c = row / IR, iy = iy0 + row % IR;
+      const bool rok = iy >= 0 && iy < H;
+      for (int q = threadIdx.x; q < W; q += blockDim.x)
+        xs[row * Wp + 1 + q] = (__bf16)(rok ? img_val(img[(((long)n * 3 + c) * H + iy) * W + q]) : 0.f);
+    }
+  }
+  if (threadIdx.x < NR) {
+    xs[threadIdx.x * Wp] = (__bf16)0.f;
+    xs[threadIdx.x * Wp + W + 1] = (__bf16)0.f;
+  }
+}
+
 template <int IR>
 __device__ __forceinline__ void stage_rows(const float* __restrict__ img, int n, int H, int W, int iy0, __bf16* xs) {
   constexpr int NR = 3 * IR;
@@ -55,8 +94,8 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ img, int n,
 // weight gradient partials: block per (image, pair of output rows); the 5 input rows it needs (3 channels,
 // columns -1..W zero-padded) and its dy rows are staged in LDS as bf16, then 4 waves run the MFMA steps over
 // the block's 2*Wo pixels (32 per step). part[block][KT*16][32].
-template <int KT>
-__global__ void __launch_bounds__(256) stem_wgrad_kernel(const float* __restrict__ img, int H, int W,
+template <int KT, typename TI>
+__global__ void __launch_bounds__(256) stem_wgrad_kernel(const TI* __restrict__ img, int H, int W,
                                                          const __bf16* __restrict__ dy, int dcs, int Ho, int Wo,
                                                          float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
@@ -156,8 +195,8 @@ static size_t stem_wgrad_smem(int W, int Wo, int KT) {
 // forward on MFMA: block per (image, pair of output rows), image rows staged in LDS exactly as for the weight
 // gradient; y[16 pixels][16 k] = im2col (16 x 32) * W^T (32 x 16) per v_mfma_f32_16x16x32_bf16. The W^T
 // fragment is the same for every step (preloaded); stats = per-block sums of the stored bf16 values.
-template <int KT>
-__global__ void __launch_bounds__(256) stem_fwd_kernel(const float* __restrict__ img, int H, int W,
+template <int KT, typename TI>
+__global__ void __launch_bounds__(256) stem_fwd_kernel(const TI* __restrict__ img, int H, int W,
                                                        const float* __restrict__ w, __bf16* __restrict__ y, int ycs,
                                                        int Ho, int Wo, float* __restrict__ stats) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
@@ -268,8 +307,9 @@ using namespace adr;
 // forward tiles = blocks (image, pair of output rows); npix = N * Ho * Wo with Ho, Wo of the stem
 extern "C" int adr_stem_fwd_tiles(int N, int Ho) { return N * ((Ho + STEM_ROWS - 1) / STEM_ROWS); }
 
-extern "C" int adr_stem_conv_fwd(const float* img, int N, int H, int W, const float* w, int K, void* y, int ycs,
-                                 float* stats, void* stream) {
+template <typename TI>
+static int stem_fwd(const TI* img, int N, int H, int W, const float* w, int K, void* y, int ycs, float* stats,
+                    void* stream) {
   ADR_REQUIRE(N > 0 && H > 1 && W > 1 && (K == 16 || K == 32 || K == 64) && ycs >= K,
               "stem_conv_fwd: N=%d H=%d W=%d K=%d ycs=%d", N, H, W, K, ycs);
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
@@ -279,12 +319,22 @@ extern "C" int adr_stem_conv_fwd(const float* img, int N, int H, int W, const fl
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid(adr_stem_fwd_tiles(N, Ho));
   if (K == 16)
-    hipLaunchKernelGGL(stem_fwd_kernel<1>, grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
+    hipLaunchKernelGGL((stem_fwd_kernel<1, TI>), grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
   else if (K == 32)
-    hipLaunchKernelGGL(stem_fwd_kernel<2>, grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
+    hipLaunchKernelGGL((stem_fwd_kernel<2, TI>), grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
   else
-    hipLaunchKernelGGL(stem_fwd_kernel<4>, grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
+    hipLaunchKernelGGL((stem_fwd_kernel<4, TI>), grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
   return check_launch("adr_stem_conv_fwd");
+}
+
+extern "C" int adr_stem_conv_fwd(const float* img, int N, int H, int W, const float* w, int K, void* y, int ycs,
+                                 float* stats, void* stream) {
+  return stem_fwd(img, N, H, W, w, K, y, ycs, stats, stream);
+}
+
+extern "C" int adr_stem_conv_fwd_u8(const uint8_t* img, int N, int H, int W, const float* w, int K, void* y, int ycs,
+                                    float* stats, void* stream) {
+  return stem_fwd(img, N, H, W, w, K, y, ycs, stats, stream);
 }
 
 extern "C" size_t adr_stem_wgrad_workspace(int N, int H, int W, int K) {
@@ -293,8 +343,9 @@ extern "C" size_t adr_stem_wgrad_workspace(int N, int H, int W, int K) {
   return (size_t)blocks * K * 32 * sizeof(float);
 }
 
-extern "C" int adr_stem_conv_wgrad(const float* img, int N, int H, int W, const void* dy, int dcs, int K, float* dw,
-                                   int accumulate, float* ws, size_t ws_bytes, void* stream) {
+template <typename TI>
+static int stem_wgrad(const TI* img, int N, int H, int W, const void* dy, int dcs, int K, float* dw, int accumulate,
+                      float* ws, size_t ws_bytes, void* stream) {
   ADR_REQUIRE(N > 0 && H > 1 && W > 1 && (K == 16 || K == 32 || K == 64) && dcs >= K,
               "stem_conv_wgrad: N=%d H=%d W=%d K=%d", N, H, W, K);
   ADR_REQUIRE(ws_bytes >= adr_stem_wgrad_workspace(N, H, W, K), "stem_conv_wgrad: workspace");
@@ -305,14 +356,24 @@ extern "C" int adr_stem_conv_wgrad(const float* img, int N, int H, int W, const 
   ADR_REQUIRE(sm <= 64 * 1024 && dcs % 8 == 0, "stem_conv_wgrad: W=%d too wide for the LDS plan", W);
   hipStream_t st = (hipStream_t)stream;
   if (K == 16)
-    hipLaunchKernelGGL(stem_wgrad_kernel<1>, dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs, Ho,
-                       Wo, ws);
+    hipLaunchKernelGGL((stem_wgrad_kernel<1, TI>), dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs,
+                       Ho, Wo, ws);
   else if (K == 32)
-    hipLaunchKernelGGL(stem_wgrad_kernel<2>, dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs, Ho,
-                       Wo, ws);
+    hipLaunchKernelGGL((stem_wgrad_kernel<2, TI>), dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs,
+                       Ho, Wo, ws);
   else
-    hipLaunchKernelGGL(stem_wgrad_kernel<4>, dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs, Ho,
-                       Wo, ws);
+    hipLaunchKernelGGL((stem_wgrad_kernel<4, TI>), dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs,
+                       Ho, Wo, ws);
   hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(K * 27), dim3(256), 0, st, ws, blocks, K, dw, accumulate);
   return check_launch("adr_stem_conv_wgrad");
+}
+
+extern "C" int adr_stem_conv_wgrad(const float* img, int N, int H, int W, const void* dy, int dcs, int K, float* dw,
+                                   int accumulate, float* ws, size_t ws_bytes, void* stream) {
+  return stem_wgrad(img, N, H, W, dy, dcs, K, dw, accumulate, ws, ws_bytes, stream);
+}
+
+extern "C" int adr_stem_conv_wgrad_u8(const uint8_t* img, int N, int H, int W, const void* dy, int dcs, int K,
+                                      float* dw, int accumulate, float* ws, size_t ws_bytes, void* stream) {
+  return stem_wgrad(img, N, H, W, dy, dcs, K, dw, accumulate, ws, ws_bytes, stream);
 }
