@@ -222,7 +222,8 @@ __global__ void image_u8_to_nhwc_kernel(const uint8_t* __restrict__ src, T* __re
   long r = pix / W;
   int h = (int)(r % H);
   int b = (int)(r / H);
-  float v = c < C ? (float)src[(((long)b * C + c) * H + h) * W + w] / 255.f : 0.f;
+  // x * fp32(1/255): torch's device division by a scalar (a multiplication by the reciprocal), bitwise
+  float v = c < C ? (float)src[(((long)b * C + c) * H + h) * W + w] * (1.f / 255.f) : 0.f;
   dst[i] = from_f<T>(v);
 }
 

@@ -19,9 +19,10 @@ typedef __attribute__((ext_vector_type(8))) short s16x8;
 constexpr int STEM_ROWS = 2;
 
 // image element -> the reference's preprocessed value: fp32 as is; uint8 as .float() / 255 (detect/train.py:57-59,
-// the dataloader's uint8 batch normalised on the device), an IEEE division like torch's
+// the dataloader's uint8 batch normalised on the device). torch evaluates a division by a scalar on the device as
+// a multiplication by the fp32 reciprocal (BinaryDivTrueKernel), so this does too — bitwise the reference's input
 __device__ __forceinline__ float img_val(float v) { return v; }
-__device__ __forceinline__ float img_val(uint8_t v) { return (float)v / 255.f; }
+__device__ __forceinline__ float img_val(uint8_t v) { return (float)v * (1.f / 255.f); }
 
 // stage image rows iy0 .. iy0+IR-1 of the 3 channels of image n into LDS as bf16 [3][IR][W+2] with zero
 // columns at -1 and W (and zero rows outside the image); 16-byte (fp32) / 4-byte (uint8) loads when W % 4 == 0
