@@ -239,6 +239,13 @@ int adr_bilinear(int dtype, const void* x, int xcs, int N, int H, int W, int C, 
                  void* stream);
 int adr_bilinear_bwd(int dtype, const void* dy, int dcs, int N, int H, int W, int C, void* dx, int ocs, int OH,
                      int OW, int accumulate, void* stream);
+/* nn.Upsample(scale_factor=s, mode='nearest') (yolo11.yaml head rows; torch upsample_nearest2d with an
+ * integer factor: out[oh][ow] = x[oh/s][ow/s]). y may be a channel slice of a concat buffer (ycs). Backward
+ * gathers the s x s block of dy per input pixel (no atomics). */
+int adr_upsample_nearest(int dtype, const void* x, int xcs, int N, int H, int W, int C, void* y, int ycs, int s,
+                         void* stream);
+int adr_upsample_nearest_bwd(int dtype, const void* dy, int dcs, int N, int H, int W, int C, void* dx, int ocs, int s,
+                             int accumulate, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------
  * MLCA (block.py:1540-1584) fused: out = res + y * up(att(y)).  Saved tensors (fp32, caller-owned):
@@ -340,14 +347,19 @@ size_t adr_edffn_bwd_workspace(int N, int H, int W, int C);
 int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* M, const float* basis,
                   int nuv, void* dx, int ocs, float* dw, int N, int H, int W, int C, int dw_accumulate, float* ws,
                   size_t ws_bytes, void* stream);
-/* Flash attention, head_dim 64 (nn.MultiheadAttention core in CrossScaleAttentionTSSA, :2432/:2484):
- * o = softmax(q k^T * scale) v per (image, head); rows [b*L + l], channel strides cs / ocs, q/k/v channel
- * offsets qo/ko/vo (+ h*64). lse [B][heads][L] (natural log) is saved for the backward. */
-int adr_attn_fwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo, void* o,
-                 int ocs, int B, int L, int heads, int head_dim, float scale, float* lse, void* stream);
-int adr_attn_bwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo,
+/* Flash attention (no mask): o = softmax(q k^T * scale) v per (image, head); token rows [b*L + l], channel
+ * strides cs / ocs. Head h's q / k / v start at channel qo / ko / vo + h*hs (hs = head stride); q/k width
+ * qk_dim in {32, 64}, v / o width v_dim = 64 (o and dO hold head h at [h*64, h*64+64)).
+ * Replaces: nn.MultiheadAttention core in CrossScaleAttentionTSSA (block.py:2432/:2484; qk 64, hs 64) and
+ * Attention.forward of C2PSA/PSABlock (block.py:906-927, `(q^T k) * key_dim^-0.5`, softmax, `v @ attn^T`;
+ * qk 32, hs 128). lse [B][heads][L] (natural log) is saved for the backward; dq/dk/dv use the same head
+ * stride at offsets gqo/gko/gvo of a gcs-strided gradient buffer. */
+int adr_attn_fwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo, int hs,
+                 void* o, int ocs, int B, int L, int heads, int qk_dim, int v_dim, float scale, float* lse,
+                 void* stream);
+int adr_attn_bwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo, int hs,
                  const void* o, int ocs, const void* dout, int dcs, const float* lse, void* dq, void* dk, void* dv,
-                 int gcs, int gqo, int gko, int gvo, int B, int L, int heads, int head_dim, float scale,
+                 int gcs, int gqo, int gko, int gvo, int B, int L, int heads, int qk_dim, int v_dim, float scale,
                  float* dvec_ws, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------

@@ -66,7 +66,7 @@ def module_fixture(name, mod, specs, seed, extra=None):
     specs = [sp if isinstance(sp, tuple) and isinstance(sp[0], tuple) else (tuple(sp), 11) for sp in specs]
     inputs = [seeded_randn(*shp, seed=sd) for shp, sd in specs]
     ins = [x.clone().requires_grad_(True) for x in inputs]
-    out = mod(ins) if getattr(mod, "_list_input", False) else mod(ins[0])
+    out = mod(list(ins)) if getattr(mod, "_list_input", False) else mod(ins[0])  # Detect writes into its list
     outs = out if isinstance(out, (list, tuple)) else [out]
     g = torch.Generator().manual_seed(seed + 1)
     gouts = [torch.randn(o.shape, generator=g) for o in outs]
@@ -97,6 +97,7 @@ def main():
             manifest["fixtures"][name] = {"what": what, "reference": cites, "unpinned_3rdparty": unpinned}
         for what in only[0].split(","):
             globals()[f"{what}_fixtures"](tasks, block, conv, head, uloss, uops, note)
+        manifest.update(manifest_extra)
         (OUT / "MANIFEST.json").write_text(json.dumps(manifest, indent=1))
         return
     if only_nms:
@@ -243,6 +244,116 @@ def main():
 
     (OUT / "MANIFEST.json").write_text(json.dumps(manifest, indent=1))
     print("wrote", len(list(OUT.glob("*.npz"))), "fixtures to", OUT)
+
+
+def _hyp():
+    return type("H", (), {"box": 7.5, "cls": 0.5, "dfl": 1.5})()
+
+
+def _eval_fixture(model, S, name):
+    model.eval()
+    x = synthetic_images(1, S, seed=0)
+    with torch.no_grad():
+        y, _ = model(x)
+    np.savez_compressed(OUT / f"{name}.npz", img_seed=np.array(0), y=_np(y))
+
+
+def _train_fixture(model, uloss, S, bs, name, rec):
+    """Train-mode forward + v8DetectionLoss + backward at S^2, batch bs (recipe weights reloaded first)."""
+    model.load_state_dict(rec, strict=True)
+    model.train()
+    x = synthetic_images(bs, S, seed=0)
+    batch = synthetic_labels(bs, 80, seed=1)
+    preds = model(x)
+    crit = uloss.v8DetectionLoss(model)
+    loss, items = crit(preds, batch)
+    for p in preds:
+        p.retain_grad()
+    loss.backward()
+    gn = {k: float(p.grad.norm()) if p.grad is not None else 0.0 for k, p in model.named_parameters()}
+    d = {"img_seed": np.array(0), "img_size": np.array(S), "batch_idx": _np(batch["batch_idx"]),
+         "cls": _np(batch["cls"]), "bboxes": _np(batch["bboxes"]), "loss": _np(loss), "items": _np(items),
+         "gn_keys": np.array(list(gn.keys())), "gn": np.array(list(gn.values()), dtype=np.float64)}
+    for i, p in enumerate(preds):
+        d[f"pred{i}"] = _np(p)
+        d[f"gpred{i}_norm"] = np.array(float(p.grad.norm()))
+        d[f"gpred{i}_sum"] = np.array(float(p.grad.sum()))
+    sd = model.state_dict()
+    d["post_model.0.bn.running_mean"] = _np(sd["model.0.bn.running_mean"])
+    d["post_model.0.bn.running_var"] = _np(sd["model.0.bn.running_var"])
+    np.savez_compressed(OUT / f"{name}.npz", **d)
+
+
+def yolo11_fixtures(tasks, block, conv, head, uloss, uops, note):
+    """Config 1: the stock yolo11n (tests/configs/yolo11.yaml, scale n) — construction facts of the reference's
+    DetectionModel (probe strides, bias_init, the probe's BatchNorm side effects), eval 320/640, a train step at
+    320 bs2, and module fixtures for C2PSA and Detect."""
+    global manifest_extra
+    torch.manual_seed(0)
+    model = tasks.DetectionModel(str(REPO / "tests" / "configs" / "yolo11n.yaml"), verbose=False)
+    m = model.model[-1]
+    sd = model.state_dict()
+    manifest_extra["state_dict_y11n"] = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()]
+    init = {"stride": _np(m.stride), "cv2_bias": np.stack([_np(a[-1].bias) for a in m.cv2]),
+            "cv3_bias": np.stack([_np(b[-1].bias) for b in m.cv3]),
+            "bn_running_var": np.concatenate([_np(v).ravel() for k, v in sd.items() if k.endswith("running_var")]),
+            "bn_running_mean": np.concatenate([_np(v).ravel() for k, v in sd.items() if k.endswith("running_mean")]),
+            "bn_nbt": np.array([int(v) for k, v in sd.items() if k.endswith("num_batches_tracked")]),
+            "bn_eps": np.array([mm.eps for mm in model.modules() if isinstance(mm, torch.nn.BatchNorm2d)]),
+            "bn_momentum": np.array([mm.momentum for mm in model.modules() if isinstance(mm, torch.nn.BatchNorm2d)]),
+            "n_params": np.array(sum(p.numel() for p in model.parameters()))}
+    np.savez_compressed(OUT / "y11n_init.npz", **init)
+    note("y11n_init", "yolo11n DetectionModel construction: probe strides, Detect.bias_init, BN state after the "
+         "zero-image probe, BN eps/momentum after initialize_weights", "nn/tasks.py:309-350, head.py:137-147")
+    rec = load_recipe(model)
+    model.args = _hyp()
+    for S in (320, 640):
+        _eval_fixture(model, S, f"y11n_eval_{S}")
+        note(f"y11n_eval_{S}", f"yolo11n eval forward bs1 {S}^2 (recipe weights)", "nn/tasks.py:141-168, head.py:55-115")
+    _train_fixture(model, uloss, 320, 2, "y11n_train_320", rec)
+    note("y11n_train_320", "yolo11n train fwd + v8DetectionLoss + bwd, bs2 320^2",
+         "engine/trainer.py:383-393, utils/loss.py:419-520, utils/tal.py:39-265")
+
+    def bnfix(mod):
+        for mm in mod.modules():
+            if isinstance(mm, torch.nn.BatchNorm2d):
+                mm.eps, mm.momentum = 1e-3, 0.03
+        return mod
+    module_fixture("c2psa", bnfix(block.C2PSA(256, 256, 1)), [((2, 256, 20, 20), 11)], 33)
+    note("mod_c2psa", "C2PSA(256,256,1) @20x20 (2 heads, key_dim 32)", "block.py:874-1045")
+    module_fixture("c2psa_l", bnfix(block.C2PSA(512, 512, 2)), [((2, 512, 10, 10), 12)], 34)
+    note("mod_c2psa_l", "C2PSA(512,512,2) @10x10 (4 heads, 2 blocks)", "block.py:874-1045")
+    dt = bnfix(head.Detect(80, [64, 128, 256]))
+    dt.stride = torch.tensor([8.0, 16.0, 32.0])
+    dt._list_input = True
+    module_fixture("detect", dt, [((2, 64, 16, 16), 3), ((2, 128, 8, 8), 4), ((2, 256, 4, 4), 5)], 35)
+    note("mod_detect", "Detect(80,[64,128,256]) train fwd/bwd", "head.py:21-70")
+
+
+def lscale_fixtures(tasks, block, conv, head, uloss, uops, note):
+    """Config 5 groundwork: the 701 yaml at scale 'l' (C3k2 c3k=True per tasks.py:1050-1051, C2PTSSA c=256 with 4
+    heads, AYHead hidc 512), eval 256^2 bs1 and a train step at 256^2 bs2 (CPU-sized stand-ins for 1280^2)."""
+    import yaml as _yaml
+    global manifest_extra
+    d = _yaml.safe_load((REF / "z-yaml" / "yolo11-701-YOLO-AD-Refine.yaml").read_text())
+    d["scale"] = "l"
+    model = tasks.DetectionModel(d, verbose=False)
+    for mm in model.modules():
+        if isinstance(mm, torch.nn.Dropout):
+            mm.p = 0.0
+    sd = model.state_dict()
+    manifest_extra["state_dict_701l"] = [[k, list(v.shape), str(v.dtype).replace("torch.", "")] for k, v in sd.items()]
+    rec = load_recipe(model)
+    model.args = _hyp()
+    _eval_fixture(model, 256, "net701l_eval_256")
+    note("net701l_eval_256", "701 yaml scale l eval forward bs1 256^2 (recipe weights)",
+         "nn/tasks.py:141-168,1050-1051, head.py:1181-1204", True)
+    _train_fixture(model, uloss, 256, 2, "net701l_train_256", rec)
+    note("net701l_train_256", "701 yaml scale l train fwd + v8DetectionLoss + bwd, bs2 256^2",
+         "engine/trainer.py:383-393, utils/loss.py:419-520", True)
+
+
+manifest_extra = {}
 
 
 def metrics_fixtures(tasks, block, conv, head, uloss, uops, note):

@@ -9,7 +9,8 @@ from recipe import seeded_randn
 pytestmark = pytest.mark.gpu
 
 SEEDS = {"conv_k3s2": 21, "c3k2": 22, "c3k2_mlca_c3k": 23, "c3k2_mlca": 24, "sppf": 25, "ela": 26,
-         "ela_noflag": 27, "convT": 28, "fusion": 29, "c2ptssa": 30, "c2tssa_mona": 31, "ayhead": 32}
+         "ela_noflag": 27, "convT": 28, "fusion": 29, "c2ptssa": 30, "c2tssa_mona": 31, "ayhead": 32,
+         "c2psa": 33, "c2psa_l": 34, "detect": 35}
 
 
 def run_fixture(name, module, dtype, list_input=False, tol=None):
@@ -140,3 +141,27 @@ def test_mona_dropout_mask():
     assert not torch.equal(y1, y2)
     y1.backward(torch.ones_like(y1))
     assert torch.equal((x.grad != 0), (y1 != 0))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c2psa(dtype):
+    """yolo11 C2PSA (block.py:874-1045): 2 heads, key_dim 32 / head_dim 64 interleaved in the qkv activation,
+    depthwise pe, FFN; flash kernel with qk width 32 and head stride 128."""
+    from adrefine.nn.modules.block import C2PSA
+    run_fixture("c2psa", C2PSA(256, 256, 1), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c2psa_l(dtype):
+    """C2PSA at the l/x channel count: 4 heads, two stacked PSABlocks, 100 tokens (ragged 64-token blocks)."""
+    from adrefine.nn.modules.block import C2PSA
+    run_fixture("c2psa_l", C2PSA(512, 512, 2), dtype)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_detect_train(dtype):
+    """Stock Detect head (head.py:21-70): box branch 3x3 Convs + 1x1, class branch DWConv + Conv twice + 1x1."""
+    from adrefine.nn.modules.head import Detect
+    m = Detect(80, [64, 128, 256])
+    m.stride = torch.tensor([8.0, 16.0, 32.0])
+    run_fixture("detect", m, dtype, list_input=True)

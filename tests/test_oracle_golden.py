@@ -12,7 +12,10 @@ from conftest import ROOT, golden, state_dict_spec
 from recipe import recipe_state_dict, seeded_randn, synthetic_images, synthetic_labels, synthetic_predictions
 
 YAMLS = {"701": ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml",
-         "697": ROOT / "tests" / "configs" / "yolo11-697-newfpn+mona+AYHead+mlca3.yaml"}
+         "697": ROOT / "tests" / "configs" / "yolo11-697-newfpn+mona+AYHead+mlca3.yaml",
+         "y11n": ROOT / "tests" / "configs" / "yolo11.yaml",
+         "701l": ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml"}
+SCALES = {"y11n": "n", "701l": "l"}
 
 
 def _close(a, b, rtol=1e-4, atol=1e-5):
@@ -57,7 +60,8 @@ def _mod_run(name, keys, fn):
 
 
 name_seed = {"conv_k3s2": 21, "c3k2": 22, "c3k2_mlca_c3k": 23, "c3k2_mlca": 24, "sppf": 25, "ela": 26,
-             "ela_noflag": 27, "convT": 28, "fusion": 29, "c2ptssa": 30, "c2tssa_mona": 31, "ayhead": 32}
+             "ela_noflag": 27, "convT": 28, "fusion": 29, "c2ptssa": 30, "c2tssa_mona": 31, "ayhead": 32,
+             "c2psa": 33, "c2psa_l": 34, "detect": 35}
 
 
 def _keys_for(prefix, tag="701", strip=True):
@@ -126,16 +130,33 @@ def test_ayhead_module():
     _mod_run("ayhead", _keys_for("model.33"), lambda P, x: O.ayhead(_prefixed(P), "m", x, 80, True))
 
 
+def test_c2psa_modules():
+    _mod_run("c2psa", _keys_for("model.10", "y11n"), lambda P, x: O.c2psa(_prefixed(P), "m", x[0], 256, 256, 1))
+    from adrefine.nn.modules.block import C2PSA  # key order of the same module at 512 channels, 2 blocks
+    keys = [(k, tuple(v.shape)) for k, v in C2PSA(512, 512, 2).state_dict().items()]
+    _mod_run("c2psa_l", keys, lambda P, x: O.c2psa(_prefixed(P), "m", x[0], 512, 512, 2))
+
+
+def test_detect_module():
+    _mod_run("detect", _keys_for("model.23", "y11n"),
+             lambda P, x: O.detect(_prefixed(P), "m", x, 80, True, (8, 16, 32)))
+
+
 def _net(tag):
     P = recipe_state_dict([(k, s) for k, s, _ in state_dict_spec(tag)])
     d = yaml.safe_load(YAMLS[tag].read_text())
-    layers, save = O.parse(d, 3, O.guess_scale(YAMLS[tag].name) or None)
+    layers, save = O.parse(d, 3, SCALES.get(tag) or O.guess_scale(YAMLS[tag].name) or None)
     return P, layers, save
 
 
-@pytest.mark.parametrize("tag,S", [("701", 320), ("701", 640), ("697", 320)])
+def _fixture_name(tag, kind, S):
+    return f"y11n_{kind}_{S}" if tag == "y11n" else f"net{tag}_{kind}_{S}"
+
+
+@pytest.mark.parametrize("tag,S", [("701", 320), ("701", 640), ("697", 320), ("y11n", 320), ("y11n", 640),
+                                   ("701l", 256)])
 def test_net_eval(tag, S):
-    g = golden(f"net{tag}_eval_{S}")
+    g = golden(_fixture_name(tag, "eval", S))
     P, layers, save = _net(tag)
     x = synthetic_images(1, S, seed=int(g["img_seed"]))
     with torch.no_grad():
@@ -143,14 +164,14 @@ def test_net_eval(tag, S):
     _close(y, g["y"], rtol=2e-5, atol=1e-4)
 
 
-@pytest.mark.parametrize("tag", ["701", "697"])
-def test_net_train_step(tag):
-    g = golden(f"net{tag}_train_320")
+@pytest.mark.parametrize("tag,S", [("701", 320), ("697", 320), ("y11n", 320), ("701l", 256)])
+def test_net_train_step(tag, S):
+    g = golden(_fixture_name(tag, "train", S))
     P, layers, save = _net(tag)
     for k, v in P.items():
         if v.dtype.is_floating_point and "running" not in k:
             v.requires_grad_(True)
-    x = synthetic_images(2, 320, seed=int(g["img_seed"]))
+    x = synthetic_images(2, S, seed=int(g["img_seed"]))
     preds = O.forward(P, layers, save, x, train=True)
     for i, p in enumerate(preds):
         _close(p.detach(), g[f"pred{i}"], rtol=1e-4, atol=1e-4)

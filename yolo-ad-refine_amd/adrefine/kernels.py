@@ -2057,7 +2057,8 @@ class AttnFn(torch.autograd.Function):
         o = empty_act(B, E, L, 1, qkv.dtype, qkv.device)
         lse = torch.empty(B * heads * L, dtype=torch.float32, device=qkv.device)
         lib.adr_attn_fwd(dcode(qkv.dtype), ctypes.c_void_p(p), ctypes.c_void_p(p), ctypes.c_void_p(p), cs, 0, E, 2 * E,
-                         ctypes.c_void_p(o.data_ptr()), E, B, L, heads, hd, float(hd ** -0.5), fptr(lse), stream())
+                         hd, ctypes.c_void_p(o.data_ptr()), E, B, L, heads, hd, hd, float(hd ** -0.5), fptr(lse),
+                         stream())
         ctx.save_for_backward(t, o, lse)
         ctx.heads = heads
         return o
@@ -2075,14 +2076,72 @@ class AttnFn(torch.autograd.Function):
         dvec = torch.empty(B * heads * L, dtype=torch.float32, device=t.device)
         gp = g.data_ptr()
         lib.adr_attn_bwd(dcode(t.dtype), ctypes.c_void_p(p), ctypes.c_void_p(p), ctypes.c_void_p(p), cs, 0, E, 2 * E,
-                         ctypes.c_void_p(o.data_ptr()), E, ctypes.c_void_p(ddp), dcs, fptr(lse), ctypes.c_void_p(gp),
-                         ctypes.c_void_p(gp), ctypes.c_void_p(gp), C3, 0, E, 2 * E, B, L, heads, hd, float(hd ** -0.5),
-                         fptr(dvec), stream())
+                         hd, ctypes.c_void_p(o.data_ptr()), E, ctypes.c_void_p(ddp), dcs, fptr(lse),
+                         ctypes.c_void_p(gp), ctypes.c_void_p(gp), ctypes.c_void_p(gp), C3, 0, E, 2 * E, B, L, heads,
+                         hd, hd, float(hd ** -0.5), fptr(dvec), stream())
         return g, None
 
 
 def attention(qkv, heads):
     return AttnFn.apply(qkv, heads)
+
+
+class PSAAttnFn(torch.autograd.Function):
+    """The core of C2PSA's Attention (block.py:906-927) on the NHWC qkv activation (B, heads*(2kd+hd), H, W)
+    whose channels are per head [q(kd) k(kd) v(hd)] — `qkv.view(B, heads, 2kd+hd, N).split(...)`. Returns
+    o = (v @ softmax(q^T k * kd^-0.5)^T).view(B, C, H, W) and v.reshape(B, C, H, W) (the input of `pe`) as NHWC
+    activations; backward writes dq/dk/dv straight into one qkv-shaped gradient and adds pe's v-gradient."""
+
+    @staticmethod
+    def forward(ctx, qkv, heads, kd, hd):
+        ctx.set_materialize_grads(False)
+        t, p, cs = _v(qkv)
+        B, Ctot, H, W = qkv.shape
+        hs = 2 * kd + hd
+        if Ctot != heads * hs:
+            raise RuntimeError(f"psa_attention: {Ctot} channels != heads {heads} x (2*{kd}+{hd})")
+        L, C = H * W, heads * hd
+        o = empty_act(B, C, H, W, qkv.dtype, qkv.device)
+        lse = torch.empty(B * heads * L, dtype=torch.float32, device=qkv.device)
+        lib.adr_attn_fwd(dcode(qkv.dtype), ctypes.c_void_p(p), ctypes.c_void_p(p), ctypes.c_void_p(p), cs, 0, kd,
+                         2 * kd, hs, ctypes.c_void_p(o.data_ptr()), C, B, L, heads, kd, hd, float(kd ** -0.5),
+                         fptr(lse), stream())
+        v = empty_act(B, C, H, W, qkv.dtype, qkv.device)
+        for h in range(heads):
+            dst = v[:, h * hd:(h + 1) * hd]
+            _ew(EW_COPY, (dst, dst.data_ptr(), C), _v(t[:, h * hs + 2 * kd:h * hs + 2 * kd + hd]))
+        ctx.save_for_backward(t, o, lse)
+        ctx.meta = (heads, kd, hd)
+        return o, v
+
+    @staticmethod
+    def backward(ctx, do, dv_pe):
+        t, o, lse = ctx.saved_tensors
+        heads, kd, hd = ctx.meta
+        _, p, cs = _v(t)
+        B, Ctot, H, W = t.shape
+        L, C, hs = H * W, heads * hd, 2 * kd + hd
+        g = empty_act(B, Ctot, H, W, t.dtype, t.device)
+        gp = g.data_ptr()
+        if do is None:
+            zero_(g)
+        else:
+            dd, ddp, dcs = _v(do.to(t.dtype) if do.dtype != t.dtype else do)
+            dvec = torch.empty(B * heads * L, dtype=torch.float32, device=t.device)
+            lib.adr_attn_bwd(dcode(t.dtype), ctypes.c_void_p(p), ctypes.c_void_p(p), ctypes.c_void_p(p), cs, 0, kd,
+                             2 * kd, hs, ctypes.c_void_p(o.data_ptr()), C, ctypes.c_void_p(ddp), dcs, fptr(lse),
+                             ctypes.c_void_p(gp), ctypes.c_void_p(gp), ctypes.c_void_p(gp), Ctot, 0, kd, 2 * kd, B, L,
+                             heads, kd, hd, float(kd ** -0.5), fptr(dvec), stream())
+        if dv_pe is not None:
+            dv_pe = _v(dv_pe.to(t.dtype) if dv_pe.dtype != t.dtype else dv_pe)[0]
+            for h in range(heads):
+                dst = g[:, h * hs + 2 * kd:h * hs + 2 * kd + hd]
+                _ew(EW_COPY, (dst, dst.data_ptr(), Ctot), _v(dv_pe[:, h * hd:(h + 1) * hd]), accumulate=1)
+        return g, None, None, None
+
+
+def psa_attention(qkv, heads, kd, hd):
+    return PSAAttnFn.apply(qkv, heads, kd, hd)
 
 
 class GroupMeanFn(torch.autograd.Function):
@@ -2162,6 +2221,33 @@ class BilinearFn(torch.autograd.Function):
 
 def bilinear(x, oh, ow):
     return BilinearFn.apply(x, oh, ow)
+
+
+class UpsampleNearestFn(torch.autograd.Function):
+    """nn.Upsample(scale_factor=s, mode='nearest') on NHWC; the output may be a caller's concat slice."""
+
+    @staticmethod
+    def forward(ctx, x, s, box=None):
+        t, p, cs = _v(x)
+        N, C, H, W = x.shape
+        y, yp, ycs = _out_view(box, N, C, H * s, W * s, x.dtype, x.device)
+        lib.adr_upsample_nearest(dcode(x.dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(yp), ycs, s,
+                                 stream())
+        ctx.meta = (x.shape, x.dtype, s)
+        return y if box is None else y[:, :]
+
+    @staticmethod
+    def backward(ctx, dy):
+        (N, C, H, W), dtype, s = ctx.meta
+        t, p, cs = _v(dy.to(dtype) if dy.dtype != dtype else dy)
+        dx = empty_act(N, C, H, W, dtype, dy.device)
+        lib.adr_upsample_nearest_bwd(dcode(dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(dx.data_ptr()),
+                                     C, s, 0, stream())
+        return dx, None, None
+
+
+def upsample_nearest(x, s, out=None):
+    return UpsampleNearestFn.apply(x, int(s), None if out is None else OutBox(out))
 
 
 _EDFFN_BASIS = {}

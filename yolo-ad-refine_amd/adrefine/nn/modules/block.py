@@ -16,7 +16,7 @@ from .conv import Conv, Conv2d
 from .mona import Mona
 
 __all__ = ("Bottleneck", "C2f", "C3", "C3k", "C3k2", "SPPF", "MLCA", "Bottleneck_MLCA", "C3k_MLCA", "C3k2_MLCA",
-           "ELA_HSFPN", "Multiply", "Add", "Fusion", "DFL", "C2PTSSA", "DynamicTanh", "AttentionTSSA",
+           "ELA_HSFPN", "Multiply", "Add", "Fusion", "DFL", "Attention", "PSABlock", "C2PSA", "C2PTSSA", "DynamicTanh", "AttentionTSSA",
            "TSSAlock_DYT_Mona_EDFFN", "C2TSSA_DYT_Mona_EDFFN")
 
 
@@ -380,8 +380,50 @@ class ProgressiveTSSA_Fusion(nn.Module):  # noqa: N801
         return K.scale(f, self.residual_weight2, "scalar", res=x) if self.add else f
 
 
+class Attention(nn.Module):
+    """Multi-head self-attention over the H*W pixels (reference block.py:874-927): qkv 1x1 Conv+BN, per head
+    q/k of key_dim = head_dim * attn_ratio and v of head_dim, softmax(q^T k * key_dim^-0.5), plus a depthwise
+    3x3 positional encoding of v, then a 1x1 Conv+BN projection. The attention runs in the flash kernel
+    (adr_attn_*, qk width 32, interleaved heads) straight on the NHWC qkv activation."""
+
+    def __init__(self, dim, num_heads=8, attn_ratio=0.5):
+        super().__init__()
+        self.num_heads = num_heads
+        self.head_dim = dim // num_heads
+        self.key_dim = int(self.head_dim * attn_ratio)
+        self.scale = self.key_dim ** -0.5
+        nh_kd = self.key_dim * num_heads
+        h = dim + nh_kd * 2
+        self.qkv = Conv(dim, h, 1, act=False)
+        self.proj = Conv(dim, dim, 1, act=False)
+        self.pe = Conv(dim, dim, 3, 1, g=dim, act=False)
+
+    def forward(self, x):
+        o, v = K.psa_attention(self.qkv(x), self.num_heads, self.key_dim, self.head_dim)
+        return self.proj(K.add(o, self.pe(v)))
+
+
+class PSABlock(nn.Module):
+    """Attention + FFN with shortcuts (reference block.py:930-967)."""
+
+    def __init__(self, c, attn_ratio=0.5, num_heads=4, shortcut=True) -> None:
+        super().__init__()
+        self.attn = Attention(c, attn_ratio=attn_ratio, num_heads=num_heads)
+        self.ffn = nn.Sequential(Conv(c, c * 2, 1), Conv(c * 2, c, 1, act=False))
+        self.add = shortcut
+
+    def forward(self, x):
+        if not self.add:
+            return self.ffn(self.attn(x))
+        xa, xb = K.fanout(x)  # x feeds the residual and the branch: one HIP gradient sum
+        x = K.add(xa, self.attn(xb))
+        xa, xb = K.fanout(x)
+        return K.add(xa, self.ffn(xb))
+
+
 class C2PSA(nn.Module):
-    """Split / concat frame of C2PSA (reference block.py:1010-1045) with the attention blocks in self.m."""
+    """C2PSA (reference block.py:1010-1045): cv1 split, n PSABlocks on one half, concat, cv2. Subclasses
+    (C2PTSSA, C2TSSA_DYT_Mona_EDFFN) replace self.m, as the reference's do."""
 
     def __init__(self, c1, c2, n=1, e=0.5):
         super().__init__()
@@ -389,7 +431,7 @@ class C2PSA(nn.Module):
         self.c = int(c1 * e)
         self.cv1 = Conv(c1, 2 * self.c, 1, 1)
         self.cv2 = Conv(2 * self.c, c1, 1)
-        self.m = nn.Sequential()
+        self.m = nn.Sequential(*(PSABlock(self.c, attn_ratio=0.5, num_heads=self.c // 64) for _ in range(n)))
 
     def forward(self, x):
         a, b = K.split(self.cv1(x), (self.c, self.c))

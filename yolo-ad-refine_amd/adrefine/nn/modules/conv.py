@@ -5,12 +5,14 @@ state_dicts load unchanged; forward passes run libadr_hip kernels on NHWC (chann
 """
 from __future__ import annotations
 
+import math
+
 import torch
 import torch.nn as nn
 
 from ... import kernels as K
 
-__all__ = ("Conv", "Conv2d", "ConvTranspose2d", "autopad")
+__all__ = ("Conv", "DWConv", "Conv2d", "ConvTranspose2d", "Concat", "Upsample", "autopad")
 
 
 def autopad(k, p=None, d=1):
@@ -61,7 +63,8 @@ class ConvTranspose2d(nn.ConvTranspose2d):
 
 class Conv(nn.Module):
     """Conv2d(no bias) -> BatchNorm2d -> SiLU (reference conv.py:36-54), fused on the GPU:
-    implicit-GEMM conv with BN partial statistics in the epilogue, then normalise + activation."""
+    implicit-GEMM conv with BN partial statistics in the epilogue, then normalise + activation. Depthwise
+    instances (g == c1 == c2: DWConv, Attention.pe) run the depthwise kernel instead of the GEMM."""
 
     default_act = "silu"
 
@@ -75,6 +78,12 @@ class Conv(nn.Module):
 
     def forward(self, x, out=None):
         cv = self.conv
+        if cv.groups != 1:
+            k = cv.kernel_size[0]
+            if not (cv.groups == cv.in_channels == cv.out_channels and cv.stride == (1, 1) and cv.dilation == (1, 1)
+                    and cv.kernel_size == (k, k) and cv.padding == (k // 2, k // 2)):
+                raise NotImplementedError("adrefine Conv: grouped convs are depthwise, stride 1, 'same' padding")
+            return K.bn_act(K.dwconv(x, cv.weight, None, k), None, self.bn, self.act_name, self.training, out=out)
         y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight))
         return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out)
 
@@ -88,3 +97,34 @@ class Conv(nn.Module):
         """The same Conv on the fp32 NCHW image batch, through the stem kernels (bf16 compute)."""
         y, st = K.stem_conv(img, self.conv.weight, self.training)
         return K.bn_act(y, st if st.numel() else None, self.bn, self.act_name, self.training)
+
+
+class DWConv(Conv):
+    """Depth-wise convolution (reference conv.py:101-106): Conv with g = gcd(c1, c2)."""
+
+    def __init__(self, c1, c2, k=1, s=1, d=1, act=True):
+        super().__init__(c1, c2, k, s, g=math.gcd(c1, c2), d=d, act=act)
+
+
+class Concat(nn.Module):
+    """torch.cat(x, dim) (reference conv.py:322-335); channel concatenation of NHWC activations."""
+
+    def __init__(self, dimension=1):
+        super().__init__()
+        self.d = dimension
+
+    def forward(self, x):
+        if self.d != 1:
+            raise NotImplementedError("adrefine Concat: channel (dim 1) concatenation only")
+        return K.cat(list(x))
+
+
+class Upsample(nn.Upsample):
+    """nn.Upsample drop-in for the yaml `nn.Upsample, [None, s, 'nearest']` rows (integer factor)."""
+
+    def forward(self, x):
+        sf = self.scale_factor
+        sf = sf[0] if isinstance(sf, tuple) else sf
+        if self.mode != "nearest" or self.size is not None or sf is None or float(sf) != int(sf):
+            raise NotImplementedError("adrefine Upsample: nearest mode with an integer scale_factor")
+        return K.upsample_nearest(x, int(sf))

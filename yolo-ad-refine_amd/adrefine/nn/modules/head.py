@@ -1,7 +1,7 @@
-"""AYHead (alias of AYHead1) and its parts — HIP-backed drop-ins for the reference's
-ultralytics/nn/modules/head.py:600-1252 with identical class names, constructor signatures and parameter
-names (state_dict keys). Output contract (head.py:1178-1204, WENTI:71-88): train -> list of (B, no, H, W);
-eval -> (y (B, 4+nc, A) fp32, list) or y when `export`.
+"""Detection heads — HIP-backed drop-ins for the reference's ultralytics/nn/modules/head.py with identical
+class names, constructor signatures and parameter names (state_dict keys): the stock YOLOv8/11 Detect
+(head.py:21-161) and AYHead (alias of AYHead1) with its parts (head.py:600-1252). Output contract (head.py:61-70,
+1178-1204): train -> list of (B, no, H, W); eval -> (y (B, 4+nc, A) fp32, list) or y when `export`.
 """
 from __future__ import annotations
 
@@ -12,10 +12,60 @@ import torch.nn as nn
 
 from ... import kernels as K
 from .block import DFL
-from .conv import Conv2d, autopad
+from .conv import Conv, Conv2d, DWConv, autopad
 
-__all__ = ("Conv_GN", "TaskDecomposition", "CoordAtt", "CrossTaskInteraction", "DyDCNv2", "Scale", "ResidualBlockGN",
+__all__ = ("Detect", "Conv_GN", "TaskDecomposition", "CoordAtt", "CrossTaskInteraction", "DyDCNv2", "Scale", "ResidualBlockGN",
            "AYHead1", "AYHead")
+
+
+class Detect(nn.Module):
+    """YOLOv8/11 Detect head (head.py:21-161): per level a box branch (two 3x3 Conv, a 1x1 nn.Conv2d to
+    4*reg_max) and a class branch (DWConv 3x3 + Conv 1x1, twice, then a 1x1 nn.Conv2d to nc), concatenated
+    channel-wise. Eval decodes with the fused DFL + dist2bbox + sigmoid kernel (_inference, head.py:86-115).
+    end2end (YOLOv10) is not part of this build."""
+
+    dynamic = False
+    export = False
+    end2end = False
+    max_det = 300
+    shape = None
+    anchors = torch.empty(0)
+    strides = torch.empty(0)
+    format = None
+
+    def __init__(self, nc=80, ch=()):
+        super().__init__()
+        self.nc = nc
+        self.nl = len(ch)
+        self.reg_max = 16
+        self.no = nc + self.reg_max * 4
+        self.stride = torch.zeros(self.nl)
+        c2, c3 = max((16, ch[0] // 4, self.reg_max * 4)), max(ch[0], min(self.nc, 100))
+        self.cv2 = nn.ModuleList(
+            nn.Sequential(Conv(x, c2, 3), Conv(c2, c2, 3), Conv2d(c2, 4 * self.reg_max, 1)) for x in ch)
+        self.cv3 = nn.ModuleList(
+            nn.Sequential(nn.Sequential(DWConv(x, x, 3), Conv(x, c3, 1)),
+                          nn.Sequential(DWConv(c3, c3, 3), Conv(c3, c3, 1)),
+                          Conv2d(c3, self.nc, 1)) for x in ch)
+        self.dfl = DFL(self.reg_max) if self.reg_max > 1 else nn.Identity()
+
+    def forward(self, x):
+        out = []
+        for i in range(self.nl):
+            xa, xb = K.fanout(x[i])  # the level feature feeds both branches: one HIP gradient sum
+            out.append(K.cat([self.cv2[i](xa), self.cv3[i](xb)]))
+        if self.training:
+            return out
+        if self.nl != 3:
+            raise NotImplementedError("adrefine Detect: the fused decode handles 3 levels (P3-P5)")
+        y = K.detect_decode(out, [float(s) for s in self.stride], self.nc, self.reg_max)
+        return y if self.export else (y, out)
+
+    def bias_init(self):
+        """head.py:137-147: box bias 1.0, class bias log(5 / nc / (640 / s)^2) (0.01 objects per 640 image)."""
+        for a, b, s in zip(self.cv2, self.cv3, self.stride):
+            a[-1].bias.data[:] = 1.0
+            b[-1].bias.data[: self.nc] = math.log(5 / self.nc / (640 / float(s)) ** 2)
 
 
 class Conv_GN(nn.Module):  # noqa: N801

@@ -28,10 +28,11 @@ _REGISTRY = {
     "SPPF": block.SPPF, "C3k2_MLCA": block.C3k2_MLCA, "C2PTSSA": block.C2PTSSA, "C2PSA": block.C2PSA,
     "ELA_HSFPN": block.ELA_HSFPN, "Multiply": block.Multiply, "Add": block.Add, "Fusion": block.Fusion,
     "AYHead": head.AYHead, "AYHead1": head.AYHead1, "C2TSSA_DYT_Mona_EDFFN": block.C2TSSA_DYT_Mona_EDFFN,
+    "Detect": head.Detect, "DWConv": conv.DWConv, "Concat": conv.Concat,
 }
-_NN = {"Conv2d": conv.Conv2d, "ConvTranspose2d": conv.ConvTranspose2d}
+_NN = {"Conv2d": conv.Conv2d, "ConvTranspose2d": conv.ConvTranspose2d, "Upsample": conv.Upsample}
 
-_CH_MODULES = {"Conv", "Bottleneck", "SPPF", "C2f", "C3", "C3k2", "C3k2_MLCA", "C2PTSSA", "C2PSA",
+_CH_MODULES = {"Conv", "DWConv", "Bottleneck", "SPPF", "C2f", "C3", "C3k2", "C3k2_MLCA", "C2PTSSA", "C2PSA",
                "C2TSSA_DYT_Mona_EDFFN", "nn.Conv2d", "nn.ConvTranspose2d"}
 _REPEAT_MODULES = {"C2f", "C3", "C3k2", "C3k2_MLCA", "C2PTSSA", "C2PSA", "C2TSSA_DYT_Mona_EDFFN"}
 
@@ -55,9 +56,11 @@ def guess_model_scale(model_path):
 
 
 def yaml_model_load(path):
-    """tasks.py:1110-1124 (without the hub download / -p6 renames): dict + scale guessed from the file name."""
+    """tasks.py:1110-1124 (without the hub download / -p6 renames): dict + scale guessed from the file name;
+    a scaled name resolves to its unified file (yolo11n.yaml -> yolo11.yaml, scale 'n')."""
     path = Path(path)
-    d = yaml.safe_load(path.read_text())
+    unified = Path(re.sub(r"(\d+)([nslmx])(.+)?$", r"\1\3", str(path)))
+    d = yaml.safe_load((unified if unified.is_file() else path).read_text())
     d["scale"] = guess_model_scale(path)
     d["yaml_file"] = str(path)
     return d
@@ -116,7 +119,9 @@ def parse_model(d, ch, verbose=False):
             args.insert(0, inc)
             mode = args[1] if len(args) > 1 else "bifpn"
             c2 = sum(inc) if mode == "concat" else inc[0]
-        elif m in ("AYHead", "AYHead1"):
+        elif m == "Concat":
+            c2 = sum(ch[x] for x in f)
+        elif m in ("AYHead", "AYHead1", "Detect"):
             args.append([ch[x] for x in f])
         else:
             c2 = ch[f]
@@ -132,6 +137,38 @@ def parse_model(d, ch, verbose=False):
             ch = []
         ch.append(c2)
     return nn.Sequential(*layers), sorted(save)
+
+
+def layer_strides(layers, ch_stride=1.0):
+    """Output stride of every layer of a parsed model, from the convolution / upsample strides along its inputs —
+    what the reference measures with a zero-image probe forward (tasks.py:333-346)."""
+    out = []
+    for m in layers:
+        f = m.f
+        s_in = (out[f] if f != -1 else (out[-1] if out else ch_stride)) if isinstance(f, int) else \
+            (out[f[0]] if f[0] != -1 else out[-1])
+        if isinstance(m, (conv.Conv, conv.Conv2d)):
+            cv = m.conv if isinstance(m, conv.Conv) else m
+            s_in = s_in * cv.stride[0]
+        elif isinstance(m, conv.ConvTranspose2d):
+            s_in = s_in / m.stride[0]
+        elif isinstance(m, conv.Upsample):
+            sf = m.scale_factor[0] if isinstance(m.scale_factor, tuple) else m.scale_factor
+            s_in = s_in / float(sf)
+        out.append(s_in)
+    return out
+
+
+def emulate_stride_probe(model):
+    """The reference's stride probe (tasks.py:345) is a train-mode forward of a zero image BEFORE
+    initialize_weights: every BatchNorm sees an all-zero batch (each conv has no bias and every block maps 0 to 0),
+    so with torch's default momentum 0.1 it leaves running_mean 0, running_var 0.9 * running_var and
+    num_batches_tracked 1. Reproduced here without running a forward."""
+    for mm in model.modules():
+        if isinstance(mm, nn.BatchNorm2d):
+            mm.running_mean.mul_(0.9)
+            mm.running_var.mul_(0.9)
+            mm.num_batches_tracked += 1
 
 
 def initialize_weights(model):
@@ -177,6 +214,12 @@ class DetectionModel(nn.Module):
             # AYHead is not a Detect subclass: the reference skips the stride probe (tasks.py:335) and the head
             # sets [8, 16, 32] itself (head.py:1209-1211)
             self.stride = m.stride
+        elif isinstance(m, head.Detect):
+            st = layer_strides(self.model)
+            m.stride = torch.tensor([st[j] for j in m.f], dtype=torch.float32)
+            self.stride = m.stride
+            emulate_stride_probe(self)
+            m.bias_init()
         else:
             self.stride = torch.Tensor([32])
         initialize_weights(self)

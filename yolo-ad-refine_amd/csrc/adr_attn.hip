@@ -1,9 +1,13 @@
-// Flash attention (forward + backward) for the cross-scale nn.MultiheadAttention of C2PTSSA
-// (reference nn/modules/block.py:2432 and :2484: self-attention over the 3*H*W stacked scale tokens,
-// head_dim 64, softmax(q k^T / sqrt(64)) v, no masking, no dropout).
+// Flash attention (forward + backward), no masking, no dropout, for two reference modules:
+//   * the cross-scale nn.MultiheadAttention of C2PTSSA (reference nn/modules/block.py:2432 and :2484:
+//     self-attention over the 3*H*W stacked scale tokens, q/k/v head_dim 64);
+//   * Attention of C2PSA / PSABlock (block.py:874-927, yolo11): per head q and k of key_dim 32, v of
+//     head_dim 64, interleaved per head as [q(32) k(32) v(64)] in the qkv conv output.
 //
 // Layout: q, k, v, o are token rows [b*L + l] with a channel stride (cs) — e.g. the packed in_proj output
-// (B*L, 3E) — and head h occupies channels [h*64, h*64+64). One workgroup = 4 waves = 64 queries (forward,
+// (B*L, 3E) or the NHWC qkv activation — and head h's q / k / v start at channel qo / ko / vo + h*hs (hs =
+// the head stride: 64 for MHA's planar [q|k|v], 128 for PSA's interleaved heads). o and dO hold head h at
+// channels [h*64, h*64+64). DQK (32 or 64) is the q/k width. One workgroup = 4 waves = 64 queries (forward,
 // dQ) or 64 keys (dK/dV) of one (image, head); each wave owns 16 of them.
 //
 // MFMA mapping (16x16 tiles, bf16 v_mfma_f32_16x16x32_bf16 or exact-fp32 v_mfma_f32_16x16x4_f32):
@@ -15,6 +19,7 @@
 // The forward stores the per-query log-sum-exp; the backward recomputes P (two kernels: dK/dV keyed by
 // key block, dQ keyed by query block), so there are no atomics and results are deterministic.
 #include "adr_common.h"
+#include <initializer_list>
 
 namespace adr {
 
@@ -22,12 +27,12 @@ static constexpr int HD = 64;      // head dim
 static constexpr int BLK = 64;     // queries or keys per workgroup
 static constexpr int LDT = HD + 8; // LDS row stride (elements)
 
-template <typename T>
+template <typename T, int D = HD>
 __device__ __forceinline__ void load_rows(T* dst, const T* src, long row0, int L, int cs, int coff) {
-  // 64 rows x 64 elems -> LDS [64][LDT]; rows >= L zero-filled
+  // 64 rows x D elems -> LDS [64][LDT]; rows >= L zero-filled
   constexpr int V = 16 / sizeof(T);
-  for (int i = threadIdx.x; i < BLK * (HD / V); i += 256) {
-    int r = i / (HD / V), c = (i % (HD / V)) * V;
+  for (int i = threadIdx.x; i < BLK * (D / V); i += 256) {
+    int r = i / (D / V), c = (i % (D / V)) * V;
     long row = row0 + r;
     u32x4 v = {0u, 0u, 0u, 0u};
     if (r < L) v = ld16(src + row * cs + coff + c);
@@ -35,20 +40,20 @@ __device__ __forceinline__ void load_rows(T* dst, const T* src, long row0, int L
   }
 }
 
-// C[i][j] += sum_d A[i][d] * B[j][d] for i in [ai, ai+16), j in [bj, bj+16)
-template <typename T>
+// C[i][j] += sum_{d<D} A[i][d] * B[j][d] for i in [ai, ai+16), j in [bj, bj+16)
+template <typename T, int D>
 __device__ __forceinline__ f32x4 nt_tile(const T* As, int ai, const T* Bs, int bj, f32x4 acc) {
   const int lane = threadIdx.x & 63;
   if constexpr (sizeof(T) == 2) {
 #pragma unroll
-    for (int ds = 0; ds < HD / 32; ++ds) {
+    for (int ds = 0; ds < D / 32; ++ds) {
       bf16x8 a = *reinterpret_cast<const bf16x8*>(As + (ai + (lane & 15)) * LDT + ds * 32 + 8 * (lane >> 4));
       bf16x8 b = *reinterpret_cast<const bf16x8*>(Bs + (bj + (lane & 15)) * LDT + ds * 32 + 8 * (lane >> 4));
       acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc, 0, 0, 0);
     }
   } else {
 #pragma unroll
-    for (int s = 0; s < HD / 4; ++s) {
+    for (int s = 0; s < D / 4; ++s) {
       float a = As[(ai + (lane & 15)) * LDT + 4 * s + (lane >> 4)];
       float b = Bs[(bj + (lane & 15)) * LDT + 4 * s + (lane >> 4)];
       acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
@@ -58,9 +63,9 @@ __device__ __forceinline__ f32x4 nt_tile(const T* As, int ai, const T* Bs, int b
 }
 
 // acc[dt] (C rows d = dt*16 + 4g + r, cols j) += sum_k X[k][d] * Pt[k][j], where Pt (64 x 16) lives in the
-// C-layout registers p[kt][r] (row k = kt*16 + 4g + r, col j = lane&15) and X is an LDS [k][d] tile.
-template <typename T>
-__device__ __forceinline__ void tn_reg(const T* Xs, const float (&p)[4][4], f32x4 (&acc)[4]) {
+// C-layout registers p[kt][r] (row k = kt*16 + 4g + r, col j = lane&15) and X is an LDS [k][d] tile, d < 16*DT.
+template <typename T, int DT>
+__device__ __forceinline__ void tn_reg(const T* Xs, const float (&p)[4][4], f32x4 (&acc)[DT]) {
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   if constexpr (sizeof(T) == 2) {
 #pragma unroll
@@ -72,7 +77,7 @@ __device__ __forceinline__ void tn_reg(const T* Xs, const float (&p)[4][4], f32x
         b[4 + j] = (__bf16)p[2 * ks + 1][j];
       }
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
+      for (int dt = 0; dt < DT; ++dt) {
         bf16x8 a;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -89,7 +94,7 @@ __device__ __forceinline__ void tn_reg(const T* Xs, const float (&p)[4][4], f32x
       for (int s = 0; s < 4; ++s) {
         float b = p[kt][s];
 #pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
+        for (int dt = 0; dt < DT; ++dt) {
           float a = Xs[(kt * 16 + 4 * g + s) * LDT + dt * 16 + c];
           acc[dt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[dt], 0, 0, 0);
         }
@@ -98,9 +103,9 @@ __device__ __forceinline__ void tn_reg(const T* Xs, const float (&p)[4][4], f32x
 }
 
 // ---------------- forward ----------------
-template <typename T>
+template <typename T, int DQK>
 __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* q, const T* k, const T* v, int cs, int qo, int ko,
-                                                       int vo, T* o, int ocs, int L, int heads, float scale,
+                                                       int vo, int hs, T* o, int ocs, int L, int heads, float scale,
                                                        float* lse) {
   __shared__ __attribute__((aligned(16))) T Qs[BLK * LDT];
   __shared__ __attribute__((aligned(16))) T Ks[BLK * LDT];
@@ -112,7 +117,7 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* q, const T* k, c
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const long rowb = (long)b * L;
   const int q0 = qb * BLK;
-  load_rows(Qs, q, rowb + q0, L - q0, cs, qo + h * HD);
+  load_rows<T, DQK>(Qs, q, rowb + q0, L - q0, cs, qo + h * hs);
   float m = -INFINITY, lsum = 0.f;
   f32x4 oacc[4];
 #pragma unroll
@@ -120,14 +125,14 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* q, const T* k, c
   const float sl2 = scale * 1.44269504088896341f;  // exp2 domain
   for (int k0 = 0; k0 < L; k0 += BLK) {
     __syncthreads();
-    load_rows(Ks, k, rowb + k0, L - k0, cs, ko + h * HD);
-    load_rows(Vs, v, rowb + k0, L - k0, cs, vo + h * HD);
+    load_rows<T, DQK>(Ks, k, rowb + k0, L - k0, cs, ko + h * hs);
+    load_rows(Vs, v, rowb + k0, L - k0, cs, vo + h * hs);
     __syncthreads();
     float p[4][4];
     float mx = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
-      f32x4 s = nt_tile(Ks, kt * 16, Qs, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
+      f32x4 s = nt_tile<T, DQK>(Ks, kt * 16, Qs, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int key = k0 + kt * 16 + 4 * g + r;
@@ -189,9 +194,9 @@ __global__ void __launch_bounds__(256) attn_dvec_kernel(const T* o, int ocs, con
 }
 
 // ---------------- backward: dK, dV (one workgroup per 64 keys) ----------------
-template <typename T>
+template <typename T, int DQK>
 __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(const T* q, const T* k, const T* v, int cs, int qo, int ko,
-                                                          int vo, const T* dout, int dcs, const float* lse,
+                                                          int vo, int hs, const T* dout, int dcs, const float* lse,
                                                           const float* dvec, int L, int heads, float scale, T* dq_unused,
                                                           T* dk, T* dv, int gcs, int gko, int gvo) {
   __shared__ __attribute__((aligned(16))) T Ks[BLK * LDT];
@@ -206,17 +211,17 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(const T* q, const T* k
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const long rowb = (long)b * L;
   const int k0 = kb * BLK;
-  load_rows(Ks, k, rowb + k0, L - k0, cs, ko + h * HD);
-  load_rows(Vs, v, rowb + k0, L - k0, cs, vo + h * HD);
-  f32x4 dka[4], dva[4];
+  constexpr int KT = DQK / 16;
+  load_rows<T, DQK>(Ks, k, rowb + k0, L - k0, cs, ko + h * hs);
+  load_rows(Vs, v, rowb + k0, L - k0, cs, vo + h * hs);
+  f32x4 dka[KT], dva[4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    dka[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    dva[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  }
+  for (int i = 0; i < 4; ++i) dva[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < KT; ++i) dka[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (int q0 = 0; q0 < L; q0 += BLK) {
     __syncthreads();
-    load_rows(Qs, q, rowb + q0, L - q0, cs, qo + h * HD);
+    load_rows<T, DQK>(Qs, q, rowb + q0, L - q0, cs, qo + h * hs);
     load_rows(Ds, dout, rowb + q0, L - q0, dcs, h * HD);
     for (int i = threadIdx.x; i < BLK; i += 256) {
       int qq = q0 + i;
@@ -228,8 +233,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(const T* q, const T* k
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
       // S[q][key], rows q = qt*16 + 4g + r, cols key = wave*16 + c
-      f32x4 s = nt_tile(Qs, qt * 16, Ks, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
-      f32x4 dp = nt_tile(Ds, qt * 16, Vs, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
+      f32x4 s = nt_tile<T, DQK>(Qs, qt * 16, Ks, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
+      f32x4 dp = nt_tile<T, HD>(Ds, qt * 16, Vs, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int qi = qt * 16 + 4 * g + r;
@@ -238,8 +243,8 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(const T* q, const T* k
         ds[qt][r] = pv * (dp[r] - dd[qi]);
       }
     }
-    tn_reg(Ds, p, dva);   // dV^T[d][key] += dO^T P
-    tn_reg(Qs, ds, dka);  // dK^T[d][key] += Q^T dS
+    tn_reg<T, 4>(Ds, p, dva);    // dV^T[d][key] += dO^T P
+    tn_reg<T, KT>(Qs, ds, dka);  // dK^T[d][key] += Q^T dS
   }
   const int kk = k0 + wave * 16 + c;
   if (kk < L) {
@@ -248,16 +253,22 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(const T* q, const T* k
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int d = dt * 16 + 4 * g + r;
-        dk[(rowb + kk) * gcs + gko + h * HD + d] = from_f<T>(dka[dt][r] * scale);
-        dv[(rowb + kk) * gcs + gvo + h * HD + d] = from_f<T>(dva[dt][r]);
+        dv[(rowb + kk) * gcs + gvo + h * hs + d] = from_f<T>(dva[dt][r]);
+      }
+#pragma unroll
+    for (int dt = 0; dt < KT; ++dt)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int d = dt * 16 + 4 * g + r;
+        dk[(rowb + kk) * gcs + gko + h * hs + d] = from_f<T>(dka[dt][r] * scale);
       }
   }
 }
 
 // ---------------- backward: dQ (one workgroup per 64 queries) ----------------
-template <typename T>
+template <typename T, int DQK>
 __global__ void __launch_bounds__(256) attn_bwd_q_kernel(const T* q, const T* k, const T* v, int cs, int qo, int ko,
-                                                         int vo, const T* dout, int dcs, const float* lse,
+                                                         int vo, int hs, const T* dout, int dcs, const float* lse,
                                                          const float* dvec, int L, int heads, float scale, T* dq,
                                                          int gcs, int gqo) {
   __shared__ __attribute__((aligned(16))) T Qs[BLK * LDT];
@@ -271,25 +282,26 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(const T* q, const T* k,
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const long rowb = (long)b * L;
   const int q0 = qb * BLK;
-  load_rows(Qs, q, rowb + q0, L - q0, cs, qo + h * HD);
+  constexpr int KT = DQK / 16;
+  load_rows<T, DQK>(Qs, q, rowb + q0, L - q0, cs, qo + h * hs);
   load_rows(Ds, dout, rowb + q0, L - q0, dcs, h * HD);
   const int qq = q0 + wave * 16 + c;
   const float lq = qq < L ? lse[(long)bh * L + qq] : INFINITY;
   const float dq_d = qq < L ? dvec[(long)bh * L + qq] : 0.f;
-  f32x4 dqa[4];
+  f32x4 dqa[KT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < KT; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   for (int k0 = 0; k0 < L; k0 += BLK) {
     __syncthreads();
-    load_rows(Ks, k, rowb + k0, L - k0, cs, ko + h * HD);
-    load_rows(Vs, v, rowb + k0, L - k0, cs, vo + h * HD);
+    load_rows<T, DQK>(Ks, k, rowb + k0, L - k0, cs, ko + h * hs);
+    load_rows(Vs, v, rowb + k0, L - k0, cs, vo + h * hs);
     __syncthreads();
     float ds[4][4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
       // S^T[key][q], rows key = kt*16 + 4g + r, cols q = wave*16 + c
-      f32x4 s = nt_tile(Ks, kt * 16, Qs, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
-      f32x4 dp = nt_tile(Vs, kt * 16, Ds, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
+      f32x4 s = nt_tile<T, DQK>(Ks, kt * 16, Qs, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
+      f32x4 dp = nt_tile<T, HD>(Vs, kt * 16, Ds, wave * 16, (f32x4){0.f, 0.f, 0.f, 0.f});
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int key = k0 + kt * 16 + 4 * g + r;
@@ -297,15 +309,15 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(const T* q, const T* k,
         ds[kt][r] = pv * (dp[r] - dq_d);
       }
     }
-    tn_reg(Ks, ds, dqa);  // dQ^T[d][q] += K^T dS^T
+    tn_reg<T, KT>(Ks, ds, dqa);  // dQ^T[d][q] += K^T dS^T
   }
   if (qq < L) {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
+    for (int dt = 0; dt < KT; ++dt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int d = dt * 16 + 4 * g + r;
-        dq[(rowb + qq) * gcs + gqo + h * HD + d] = from_f<T>(dqa[dt][r] * scale);
+        dq[(rowb + qq) * gcs + gqo + h * hs + d] = from_f<T>(dqa[dt][r] * scale);
       }
   }
 }
@@ -314,50 +326,70 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(const T* q, const T* k,
 
 using namespace adr;
 
-extern "C" int adr_attn_fwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo,
-                            void* o, int ocs, int B, int L, int heads, int head_dim, float scale, float* lse,
-                            void* stream) {
-  ADR_REQUIRE(head_dim == HD, "attn: head_dim must be 64 (got %d)", head_dim);
-  int vec = dtype == ADR_BF16 ? 8 : 4;
-  ADR_REQUIRE(cs % vec == 0 && ocs % vec == 0 && qo % vec == 0 && ko % vec == 0 && vo % vec == 0, "attn: views");
-  hipStream_t st = (hipStream_t)stream;
+template <typename T, int DQK>
+static void attn_fwd_launch(const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo, int hs, void* o,
+                            int ocs, int B, int L, int heads, float scale, float* lse, hipStream_t st) {
   dim3 grid(B * heads * cdiv(L, BLK));
-  if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(attn_fwd_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, cs, qo, ko, vo, (__bf16*)o, ocs, L, heads, scale, lse);
-  else
-    hipLaunchKernelGGL(attn_fwd_kernel<float>, grid, dim3(256), 0, st, (const float*)q, (const float*)k,
-                       (const float*)v, cs, qo, ko, vo, (float*)o, ocs, L, heads, scale, lse);
+  hipLaunchKernelGGL((attn_fwd_kernel<T, DQK>), grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, cs, qo,
+                     ko, vo, hs, (T*)o, ocs, L, heads, scale, lse);
+}
+
+template <typename T, int DQK>
+static void attn_bwd_launch(const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo, int hs,
+                            const void* o, int ocs, const void* dout, int dcs, const float* lse, void* dq, void* dk,
+                            void* dv, int gcs, int gqo, int gko, int gvo, int B, int L, int heads, float scale,
+                            float* dvec, hipStream_t st) {
+  long total = (long)B * heads * L;
+  dim3 grid(B * heads * cdiv(L, BLK));
+  hipLaunchKernelGGL((attn_dvec_kernel<T>), dim3(cdiv(total, 4)), dim3(256), 0, st, (const T*)o, ocs, (const T*)dout,
+                     dcs, L, heads, total, dvec);
+  hipLaunchKernelGGL((attn_bwd_kv_kernel<T, DQK>), grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, cs,
+                     qo, ko, vo, hs, (const T*)dout, dcs, lse, dvec, L, heads, scale, (T*)nullptr, (T*)dk, (T*)dv, gcs,
+                     gko, gvo);
+  hipLaunchKernelGGL((attn_bwd_q_kernel<T, DQK>), grid, dim3(256), 0, st, (const T*)q, (const T*)k, (const T*)v, cs,
+                     qo, ko, vo, hs, (const T*)dout, dcs, lse, dvec, L, heads, scale, (T*)dq, gcs, gqo);
+}
+
+static bool attn_views_ok(int dtype, std::initializer_list<int> offs) {
+  const int vec = dtype == ADR_BF16 ? 8 : 4;
+  for (int x : offs)
+    if (x % vec) return false;
+  return true;
+}
+
+extern "C" int adr_attn_fwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo,
+                            int hs, void* o, int ocs, int B, int L, int heads, int qk_dim, int v_dim, float scale,
+                            float* lse, void* stream) {
+  ADR_REQUIRE(v_dim == HD && (qk_dim == 32 || qk_dim == 64), "attn: v_dim must be 64 and qk_dim 32 or 64 (got %d/%d)",
+              v_dim, qk_dim);
+  ADR_REQUIRE(attn_views_ok(dtype, {cs, ocs, qo, ko, vo, hs}), "attn: views");
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16) {
+    if (qk_dim == 32) attn_fwd_launch<__bf16, 32>(q, k, v, cs, qo, ko, vo, hs, o, ocs, B, L, heads, scale, lse, st);
+    else attn_fwd_launch<__bf16, 64>(q, k, v, cs, qo, ko, vo, hs, o, ocs, B, L, heads, scale, lse, st);
+  } else {
+    if (qk_dim == 32) attn_fwd_launch<float, 32>(q, k, v, cs, qo, ko, vo, hs, o, ocs, B, L, heads, scale, lse, st);
+    else attn_fwd_launch<float, 64>(q, k, v, cs, qo, ko, vo, hs, o, ocs, B, L, heads, scale, lse, st);
+  }
   return check_launch("adr_attn_fwd");
 }
 
 extern "C" int adr_attn_bwd(int dtype, const void* q, const void* k, const void* v, int cs, int qo, int ko, int vo,
-                            const void* o, int ocs, const void* dout, int dcs, const float* lse, void* dq, void* dk,
-                            void* dv, int gcs, int gqo, int gko, int gvo, int B, int L, int heads, int head_dim,
-                            float scale, float* dvec_ws, void* stream) {
-  ADR_REQUIRE(head_dim == HD, "attn: head_dim must be 64");
+                            int hs, const void* o, int ocs, const void* dout, int dcs, const float* lse, void* dq,
+                            void* dk, void* dv, int gcs, int gqo, int gko, int gvo, int B, int L, int heads,
+                            int qk_dim, int v_dim, float scale, float* dvec_ws, void* stream) {
+  ADR_REQUIRE(v_dim == HD && (qk_dim == 32 || qk_dim == 64), "attn: v_dim must be 64 and qk_dim 32 or 64");
   hipStream_t st = (hipStream_t)stream;
-  long total = (long)B * heads * L;
-  dim3 g1(cdiv(total, 4));
-  dim3 grid(B * heads * cdiv(L, BLK));
+#define ADR_ATTN_BWD(T, D)                                                                                              \
+  attn_bwd_launch<T, D>(q, k, v, cs, qo, ko, vo, hs, o, ocs, dout, dcs, lse, dq, dk, dv, gcs, gqo, gko, gvo, B, L, heads, \
+                        scale, dvec_ws, st)
   if (dtype == ADR_BF16) {
-    hipLaunchKernelGGL(attn_dvec_kernel<__bf16>, g1, dim3(256), 0, st, (const __bf16*)o, ocs, (const __bf16*)dout, dcs,
-                       L, heads, total, dvec_ws);
-    hipLaunchKernelGGL(attn_bwd_kv_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, cs, qo, ko, vo, (const __bf16*)dout, dcs, lse, dvec_ws, L, heads, scale,
-                       (__bf16*)nullptr, (__bf16*)dk, (__bf16*)dv, gcs, gko, gvo);
-    hipLaunchKernelGGL(attn_bwd_q_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)q, (const __bf16*)k,
-                       (const __bf16*)v, cs, qo, ko, vo, (const __bf16*)dout, dcs, lse, dvec_ws, L, heads, scale,
-                       (__bf16*)dq, gcs, gqo);
+    if (qk_dim == 32) ADR_ATTN_BWD(__bf16, 32);
+    else ADR_ATTN_BWD(__bf16, 64);
   } else {
-    hipLaunchKernelGGL(attn_dvec_kernel<float>, g1, dim3(256), 0, st, (const float*)o, ocs, (const float*)dout, dcs, L,
-                       heads, total, dvec_ws);
-    hipLaunchKernelGGL(attn_bwd_kv_kernel<float>, grid, dim3(256), 0, st, (const float*)q, (const float*)k,
-                       (const float*)v, cs, qo, ko, vo, (const float*)dout, dcs, lse, dvec_ws, L, heads, scale,
-                       (float*)nullptr, (float*)dk, (float*)dv, gcs, gko, gvo);
-    hipLaunchKernelGGL(attn_bwd_q_kernel<float>, grid, dim3(256), 0, st, (const float*)q, (const float*)k,
-                       (const float*)v, cs, qo, ko, vo, (const float*)dout, dcs, lse, dvec_ws, L, heads, scale,
-                       (float*)dq, gcs, gqo);
+    if (qk_dim == 32) ADR_ATTN_BWD(float, 32);
+    else ADR_ATTN_BWD(float, 64);
   }
+#undef ADR_ATTN_BWD
   return check_launch("adr_attn_bwd");
 }

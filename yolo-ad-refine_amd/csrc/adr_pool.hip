@@ -5,6 +5,7 @@
 //     out = x * a_h[n,h,c] * a_w[n,w,c]  (ELA_HSFPN block.py:1418-1424; CoordAtt head.py:689-707).
 //   * adaptive average pooling, any in/out size (MLCA block.py:1558-1581; CrossScaleAttentionTSSA :2455).
 //   * bilinear resize, align_corners=False (CrossScaleAttentionTSSA block.py:2459-2462).
+//   * nearest upsample by an integer factor (nn.Upsample(None, 2, 'nearest') rows of yolo11.yaml).
 #include "adr_common.h"
 #include <initializer_list>
 
@@ -401,6 +402,51 @@ __global__ void __launch_bounds__(256) bilinear_bwd_kernel(const T* dy, int dcs,
   }
 }
 
+// ---- nearest upsample, integer factor s ----
+template <typename T, int VW>
+__global__ void __launch_bounds__(256) upsample_nearest_kernel(const T* x, int xcs, int N, int H, int W, int C, T* y,
+                                                               int ycs, int s) {
+  const int G = C / VW;
+  const PoolLanes L(G);
+  if (!L.active) return;
+  const int OH = H * s, OW = W * s;
+  const long npix = (long)N * OH * OW;
+  POOL_LOOP(L, npix, G) {
+    int n, oh, ow;
+    pix_nhw(pix, OH, OW, n, oh, ow);
+    const int c0 = cg * VW;
+    float v[VW];
+    vload<T, VW>(x + (((long)n * H + oh / s) * W + ow / s) * xcs + c0, v);
+    vstore<T, VW>(y + pix * ycs + c0, v);
+  }
+}
+
+template <typename T, int VW>
+__global__ void __launch_bounds__(256) upsample_nearest_bwd_kernel(const T* dy, int dcs, int N, int H, int W, int C,
+                                                                   T* dx, int ocs, int s, int accumulate) {
+  const int G = C / VW;
+  const PoolLanes L(G);
+  if (!L.active) return;
+  const int OH = H * s, OW = W * s;
+  const long npix = (long)N * H * W;
+  POOL_LOOP(L, npix, G) {
+    int n, h, w;
+    pix_nhw(pix, H, W, n, h, w);
+    const int c0 = cg * VW;
+    float acc[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) acc[e] = 0.f;
+    for (int a = 0; a < s; ++a)
+      for (int b = 0; b < s; ++b) {
+        float g[VW];
+        vload<T, VW>(dy + (((long)n * OH + h * s + a) * OW + w * s + b) * dcs + c0, g);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) acc[e] += g[e];
+      }
+    vstore_acc<T, VW>(dx + pix * ocs + c0, acc, accumulate);
+  }
+}
+
 }  // namespace adr
 
 using namespace adr;
@@ -588,4 +634,36 @@ extern "C" int adr_bilinear_bwd(int dtype, const void* dy, int dcs, int N, int H
     else hipLaunchKernelGGL((bilinear_bwd_kernel<float, 1>), g, dim3(256), 0, st, P(const float, dy), dcs, N, H, W, C, P(float, dx), ocs, OH, OW, accumulate);
   }
   return check_launch("adr_bilinear_bwd");
+}
+
+extern "C" int adr_upsample_nearest(int dtype, const void* x, int xcs, int N, int H, int W, int C, void* y, int ycs,
+                                    int s, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  ADR_REQUIRE(s >= 1 && s <= 8, "upsample_nearest: factor %d", s);
+  const bool v = vec_ok(C, VW_OF(dtype), {xcs, ycs}, {x, y});
+  const dim3 g = pool_grid((long)N * H * W * s * s, GOF(dtype, v, C));
+  if (dtype == ADR_BF16) {
+    if (v) hipLaunchKernelGGL((upsample_nearest_kernel<__bf16, 8>), g, dim3(256), 0, st, P(const __bf16, x), xcs, N, H, W, C, P(__bf16, y), ycs, s);
+    else hipLaunchKernelGGL((upsample_nearest_kernel<__bf16, 1>), g, dim3(256), 0, st, P(const __bf16, x), xcs, N, H, W, C, P(__bf16, y), ycs, s);
+  } else {
+    if (v) hipLaunchKernelGGL((upsample_nearest_kernel<float, 4>), g, dim3(256), 0, st, P(const float, x), xcs, N, H, W, C, P(float, y), ycs, s);
+    else hipLaunchKernelGGL((upsample_nearest_kernel<float, 1>), g, dim3(256), 0, st, P(const float, x), xcs, N, H, W, C, P(float, y), ycs, s);
+  }
+  return check_launch("adr_upsample_nearest");
+}
+
+extern "C" int adr_upsample_nearest_bwd(int dtype, const void* dy, int dcs, int N, int H, int W, int C, void* dx,
+                                        int ocs, int s, int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  ADR_REQUIRE(s >= 1 && s <= 8, "upsample_nearest_bwd: factor %d", s);
+  const bool v = vec_ok(C, VW_OF(dtype), {dcs, ocs}, {dy, dx});
+  const dim3 g = pool_grid((long)N * H * W, GOF(dtype, v, C));
+  if (dtype == ADR_BF16) {
+    if (v) hipLaunchKernelGGL((upsample_nearest_bwd_kernel<__bf16, 8>), g, dim3(256), 0, st, P(const __bf16, dy), dcs, N, H, W, C, P(__bf16, dx), ocs, s, accumulate);
+    else hipLaunchKernelGGL((upsample_nearest_bwd_kernel<__bf16, 1>), g, dim3(256), 0, st, P(const __bf16, dy), dcs, N, H, W, C, P(__bf16, dx), ocs, s, accumulate);
+  } else {
+    if (v) hipLaunchKernelGGL((upsample_nearest_bwd_kernel<float, 4>), g, dim3(256), 0, st, P(const float, dy), dcs, N, H, W, C, P(float, dx), ocs, s, accumulate);
+    else hipLaunchKernelGGL((upsample_nearest_bwd_kernel<float, 1>), g, dim3(256), 0, st, P(const float, dy), dcs, N, H, W, C, P(float, dx), ocs, s, accumulate);
+  }
+  return check_launch("adr_upsample_nearest_bwd");
 }
