@@ -3,8 +3,11 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--bs 64] [--img 640] [--dtype bf16|fp32]
   N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  python bench.py --infer [--infer-bs 32]   BASELINE.json configs[1]: batched inference (uint8 -> eval forward
+                                            -> decode -> NMS) as its own JSON line
 
-Prints ONE JSON line on rank 0 (value = images/s summed over all ranks; max-over-ranks timing).
+Prints ONE JSON line on rank 0 (value = images/s summed over all ranks; max-over-ranks timing). The training line
+also carries a short configs[1] inference measurement under "inference" (rank 0, N=1 only).
 """
 from __future__ import annotations
 
@@ -59,6 +62,68 @@ def cpu_baseline(bs=2, img=640, budget_s=20.0):
     dt = time.perf_counter() - t0
     return {"value": round(n * bs / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{n} steps x {bs} images @{img}^2 (fwd+loss+bwd, fp32, torch CPU {threads} threads)"}
+
+
+def cpu_baseline_infer(bs=1, img=640, budget_s=8.0):
+    """The CPU oracle's eval forward + decode (fp32, host cores) — the inference leg's baseline."""
+    import torch
+    import yaml
+    sys.path.insert(1, str(ROOT / "oracle"))
+    import adr_oracle as O
+    from recipe import recipe_state_dict, synthetic_images
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    d = yaml.safe_load(CFG.read_text())
+    layers, save = O.parse(d, 3, None)
+    import adrefine.nn.tasks as T
+    P = recipe_state_dict([(k, tuple(v.shape)) for k, v in T.DetectionModel(str(CFG)).state_dict().items()])
+    x = synthetic_images(bs, img, seed=0)
+    n, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            y, _ = O.forward(P, layers, save, x, train=False)
+            O.non_max_suppression(y, 0.25, 0.7)
+            n += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": round(n * bs / dt, 3), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} batches x {bs} images @{img}^2 (eval fwd + decode + NMS, fp32, torch CPU {threads} threads)"}
+
+
+def infer_bench(model, bs, img, steps, warmup, dev, graph=True, roofline=False):
+    """BASELINE.json configs[1]: uint8 batch -> /255 in the stem -> eval forward (bf16) -> decode -> NMS
+    (conf 0.25, iou 0.7, max_det 300), one hipGraph per batch. Inputs resident in HBM; the timed region is
+    `steps` graph replays between two synchronisations. Returns (images/s, ms/batch, roofline or None)."""
+    import torch
+    import adrefine.kernels as K
+    from adrefine.data.synthetic import images_u8
+    from adrefine.engine.predictor import FusedPredictor
+    was_training = model.training
+    model.eval()
+    x = images_u8(bs, img, seed=7).to(dev)
+    pred = FusedPredictor(model, conf=0.25, iou=0.7, max_det=300)
+    for _ in range(warmup):
+        pred.run_padded(x)
+    if graph:
+        pred.capture(x)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out, n = pred.run_padded(x)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    roof = None
+    if roofline:
+        g, pred.graph = pred.graph, None
+        K.timing_begin()
+        pred.run_padded(x)
+        roof = K.roofline_report(K.timing_end(), model.compute_dtype, HBM_PEAK_GBS,
+                                 BF16_MFMA_PEAK_TF if model.compute_dtype == torch.bfloat16 else F32_MFMA_PEAK_TF)
+        pred.graph = g
+    dets = int(n.sum())
+    model.train(was_training)
+    return bs * steps / dt, 1000 * dt / steps, roof, dets
 
 
 def pmc_traffic(symbol):
@@ -121,6 +186,9 @@ def main():
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel from Python (no hipGraph replay)")
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--float-images", action="store_true", help="feed pre-normalised fp32 images instead of uint8")
+    ap.add_argument("--infer", action="store_true", help="measure BASELINE.json configs[1] (batched inference) only")
+    ap.add_argument("--infer-bs", type=int, default=32)
+    ap.add_argument("--infer-steps", type=int, default=20)
     args = ap.parse_args()
 
     import torch
@@ -141,6 +209,27 @@ def main():
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
     model = DetectionModel(str(CFG), compute_dtype=dtype).to(dev)
+    if args.infer:
+        ips, ms, roof, dets = infer_bench(model, args.infer_bs, args.img, args.steps, args.warmup, dev,
+                                          graph=not args.no_graph, roofline=True)
+        if roof is not None:
+            roof["traffic"], roof["traffic_source"] = None, None
+        if rank == 0:
+            cpu = None if args.no_cpu_baseline else cpu_baseline_infer()
+            print(json.dumps({
+                "metric": "images/sec inference (640x640) bs32, YOLO-AD-Refine-n, 1 GPU",
+                "value": round(world * ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak",
+                "vs_baseline": None, "dtype": args.dtype, "data": "synthetic (uint8 images)",
+                "config": {"workload": f"yolo11-701-YOLO-AD-Refine.yaml (n) inference bs={args.infer_bs} "
+                                       f"{args.img}x{args.img}: uint8 -> eval fwd -> DFL decode -> NMS(conf 0.25, "
+                                       f"iou 0.7, max_det 300)", "global_batch": world * args.infer_bs,
+                           "img": args.img, "parallelism": f"replicas{world}"},
+                "roofline": roof, "cpu_baseline": cpu, "detections_per_batch": dets,
+                "hipgraph": not args.no_graph}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     if world > 1:  # same initial weights on every rank (DDP broadcasts rank 0's parameters at construction)
         for p in model.parameters():
             dist.broadcast(p.data, 0)
@@ -192,6 +281,14 @@ def main():
                                "mfma_frac": round(ips * NET_FLOPS_PER_IMG / (mfma_peak * 1e12), 4)}
             roof["conv_family"] = conv_attainable(K.timing_detail(), HBM_PEAK_GBS, mfma_peak)
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(budget_s=args.cpu_budget)
+        infer = None
+        if world == 1 and args.infer_steps > 0:  # configs[1] alongside the headline line
+            i_ips, i_ms, _, dets = infer_bench(model, args.infer_bs, args.img, args.infer_steps, 2, dev,
+                                               graph=not args.no_graph)
+            infer = {"metric": "images/sec inference (640x640) bs32, 1 GPU", "value": round(i_ips, 2),
+                     "ms_per_batch": round(i_ms, 3), "bs": args.infer_bs, "steps": args.infer_steps,
+                     "pipeline": "uint8 -> eval fwd (bf16) -> DFL decode -> NMS(0.25, 0.7, 300), one hipGraph",
+                     "detections_per_batch": dets}
         out = {
             "metric": "images/sec whole-node (640x640) fwd+bwd, YOLO-AD-Refine-n at 1/2/4/8 GPU",
             "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
@@ -204,6 +301,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "loss_finite": finite,
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3), "hipgraph": not args.no_graph,
+            "inference": infer,
         }
         print(json.dumps(out), flush=True)
     if world > 1:
