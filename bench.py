@@ -259,6 +259,7 @@ def main():
     dt = time.perf_counter() - t0
     # per-kernel durations for the roofline: HIP events on the launch stream around every conv-GEMM launch of
     # the same step, run eagerly right after the timed replays (a graph replay cannot be split per kernel)
+    peak_gib = torch.cuda.max_memory_allocated(dev) / 2 ** 30  # caching-allocator peak over warmup + capture + steps
     graphs, tr.graphs = tr.graphs, None
     K.timing_begin()
     for _ in range(args.roofline_steps):
@@ -301,7 +302,7 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": roof, "cpu_baseline": cpu, "loss_finite": finite,
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3), "hipgraph": not args.no_graph,
-            "inference": infer,
+            "inference": infer, "peak_hbm_gib": round(peak_gib, 2),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

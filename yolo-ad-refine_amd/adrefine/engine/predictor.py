@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import torch
 
+from .. import kernels as K
 from ..utils.ops import non_max_suppression_padded
 
 
@@ -29,10 +30,18 @@ class FusedPredictor:
         self.graph = None
         self.static_in = None
         self.static_out = None
+        self.packs = K.PackCache()  # bf16 conv operands packed once, not per batch (weights are fixed here)
+
+    def sync_weights(self):
+        """Repack the bf16 conv operands after the model's weights changed (e.g. between training epochs)."""
+        self.packs.pack_all()
 
     def _run(self, img):
-        with torch.no_grad():
+        with torch.no_grad(), K.pack_scope(self.packs):
+            first = not self.packs.valid
             y = self.model(img)
+            if first and self.packs.specs:
+                self.packs.valid = True  # the recording forward packed every operand into the cache
             y = y[0] if isinstance(y, (list, tuple)) else y
             return non_max_suppression_padded(y, self.conf, self.iou, self.classes, self.agnostic,
                                               self.multi_label, self.max_det)

@@ -411,43 +411,70 @@ __global__ void __launch_bounds__(256) mul_pixel_bwd_kernel(const T* x, int xcs,
 
 // ---------------- eval decode ----------------
 // feats: nl NHWC tensors (B, no, H_i, W_i) of dtype T; y (B, 4+nc, A) fp32
+// One block per 64 (image, anchor) rows: the rows (4*reg_max + nc channels each, NHWC) are staged into LDS with
+// coalesced reads (consecutive threads read consecutive channels of a row); then 4 threads per anchor (one per box
+// side) take the DFL expectation, and the box / class outputs are written channel-major with 64 consecutive anchors
+// per store instruction.
+constexpr int DEC_ROWS = 64;
+constexpr int DEC_MAXCH = 4 * 16 + 128;  // reg_max 16, up to 128 classes
+
 template <typename T>
 __global__ void __launch_bounds__(256) detect_decode_kernel(const T* f0, const T* f1, const T* f2, int cs0, int cs1,
                                                             int cs2, int H0, int W0, int H1, int W1, int H2, int W2,
                                                             float s0, float s1, float s2, int B, int nc, int reg_max,
                                                             float* y) {
-  int A = H0 * W0 + H1 * W1 + H2 * W2;
-  long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= (long)B * A) return;
-  int a = (int)(i % A);
-  int b = (int)(i / A);
-  const T* f;
-  int cs, W, HW, loc;
-  float st;
-  if (a < H0 * W0) { f = f0; cs = cs0; W = W0; HW = H0 * W0; loc = a; st = s0; }
-  else if (a < H0 * W0 + H1 * W1) { f = f1; cs = cs1; W = W1; HW = H1 * W1; loc = a - H0 * W0; st = s1; }
-  else { f = f2; cs = cs2; W = W2; HW = H2 * W2; loc = a - H0 * W0 - H1 * W1; st = s2; }
-  const T* p = f + ((long)b * HW + loc) * cs;
-  float ax = (float)(loc % W) + 0.5f, ay = (float)(loc / W) + 0.5f;
-  float d[4];
-  for (int k = 0; k < 4; ++k) {
-    float mx = -INFINITY;
-    for (int j = 0; j < reg_max; ++j) mx = fmaxf(mx, to_f(p[k * reg_max + j]));
-    float z = 0.f, e = 0.f;
-    for (int j = 0; j < reg_max; ++j) {
-      float ex = __expf(to_f(p[k * reg_max + j]) - mx);
-      z += ex;
-      e += ex * (float)j;
+  __shared__ float rows[DEC_ROWS][DEC_MAXCH + 1];
+  __shared__ float dist[4][DEC_ROWS];
+  const int A = H0 * W0 + H1 * W1 + H2 * W2;
+  const int no = 4 * reg_max + nc;
+  const long i0 = (long)blockIdx.x * DEC_ROWS;
+  const long total = (long)B * A;
+  auto src = [&](long i, int& loc, int& W, float& st) -> const T* {
+    const int a = (int)(i % A), b = (int)(i / A);
+    const T* f;
+    int cs, HW;
+    if (a < H0 * W0) { f = f0; cs = cs0; W = W0; HW = H0 * W0; loc = a; st = s0; }
+    else if (a < H0 * W0 + H1 * W1) { f = f1; cs = cs1; W = W1; HW = H1 * W1; loc = a - H0 * W0; st = s1; }
+    else { f = f2; cs = cs2; W = W2; HW = H2 * W2; loc = a - H0 * W0 - H1 * W1; st = s2; }
+    return f + ((long)b * HW + loc) * cs;
+  };
+  for (int e = threadIdx.x; e < DEC_ROWS * no; e += 256) {
+    const int r = e / no, c = e - r * no;
+    const long i = i0 + r;
+    if (i < total) {
+      int loc, W;
+      float st;
+      rows[r][c] = to_f(src(i, loc, W, st)[c]);
     }
-    d[k] = e / z;
   }
-  float x1 = ax - d[0], y1 = ay - d[1], x2 = ax + d[2], y2 = ay + d[3];
-  long base = (long)b * (4 + nc) * A + a;
-  y[base] = (x1 + x2) * 0.5f * st;
-  y[base + A] = (y1 + y2) * 0.5f * st;
-  y[base + 2L * A] = (x2 - x1) * st;
-  y[base + 3L * A] = (y2 - y1) * st;
-  for (int c = 0; c < nc; ++c) y[base + (long)(4 + c) * A] = 1.f / (1.f + __expf(-to_f(p[4 * reg_max + c])));
+  __syncthreads();
+  const int r = threadIdx.x & (DEC_ROWS - 1), k = threadIdx.x >> 6;  // anchor row, box side
+  const long i = i0 + r;
+  const bool live = i < total;
+  if (live) {
+    float mx = -INFINITY;
+    for (int j = 0; j < reg_max; ++j) mx = fmaxf(mx, rows[r][k * reg_max + j]);
+    float z = 0.f, ev = 0.f;
+    for (int j = 0; j < reg_max; ++j) {
+      const float ex = __expf(rows[r][k * reg_max + j] - mx);
+      z += ex;
+      ev += ex * (float)j;
+    }
+    dist[k][r] = ev / z;
+  }
+  __syncthreads();
+  if (!live) return;
+  const int a = (int)(i % A), b = (int)(i / A);
+  int loc, W;
+  float st;
+  src(i, loc, W, st);
+  const float ax = (float)(loc % W) + 0.5f, ay = (float)(loc / W) + 0.5f;
+  const float x1 = ax - dist[0][r], y1 = ay - dist[1][r], x2 = ax + dist[2][r], y2 = ay + dist[3][r];
+  const long base = (long)b * (4 + nc) * A + a;
+  const float box = k == 0 ? (x1 + x2) * 0.5f * st : k == 1 ? (y1 + y2) * 0.5f * st : k == 2 ? (x2 - x1) * st
+                                                                                             : (y2 - y1) * st;
+  y[base + (long)k * A] = box;
+  for (int c = k; c < nc; c += 4) y[base + (long)(4 + c) * A] = 1.f / (1.f + __expf(-rows[r][4 * reg_max + c]));
 }
 
 }  // namespace adr
@@ -570,13 +597,15 @@ extern "C" int adr_detect_decode(int dtype, const void* f0, const void* f1, cons
                                  int H0, int W0, int H1, int W1, int H2, int W2, float s0, float s1, float s2, int B,
                                  int nc, int reg_max, float* y, void* stream) {
   long total = (long)B * (H0 * W0 + H1 * W1 + H2 * W2);
+  ADR_REQUIRE(reg_max >= 1 && 4 * reg_max + nc <= DEC_MAXCH, "detect_decode: 4*reg_max + nc = %d > %d",
+              4 * reg_max + nc, DEC_MAXCH);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(detect_decode_kernel<__bf16>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const __bf16*)f0,
+    hipLaunchKernelGGL(detect_decode_kernel<__bf16>, dim3(cdiv(total, DEC_ROWS)), dim3(256), 0, st, (const __bf16*)f0,
                        (const __bf16*)f1, (const __bf16*)f2, cs0, cs1, cs2, H0, W0, H1, W1, H2, W2, s0, s1, s2, B, nc,
                        reg_max, y);
   else
-    hipLaunchKernelGGL(detect_decode_kernel<float>, dim3(cdiv(total, 256)), dim3(256), 0, st, (const float*)f0,
+    hipLaunchKernelGGL(detect_decode_kernel<float>, dim3(cdiv(total, DEC_ROWS)), dim3(256), 0, st, (const float*)f0,
                        (const float*)f1, (const float*)f2, cs0, cs1, cs2, H0, W0, H1, W1, H2, W2, s0, s1, s2, B, nc,
                        reg_max, y);
   return check_launch("adr_detect_decode");

@@ -26,6 +26,7 @@ struct NmsArgs {
   // workspace
   int* counts;      // [B][ng]
   int* offs;        // [B][ng]
+  int* ccnt;        // [B][chunks][ng] per-chunk counts, then start slots
   float* cscore;    // [B][cap]   candidate scores
   int* ckey;        // [B][cap]   candidate order key (anchor*nc + class for multi, anchor for single)
   int* ccls;        // [B][cap]   candidate class
@@ -41,71 +42,110 @@ __device__ __forceinline__ float ycoord(const NmsArgs& a, int b, int ch, int an)
   return a.y[((long)b * (4 + a.nc) + ch) * a.A + an];
 }
 
-// pass 1/2: one block per image; candidates appended per group in anchor order (deterministic)
-__global__ void __launch_bounds__(256) nms_collect_kernel(NmsArgs a, int fill) {
-  int b = blockIdx.x;
-  __shared__ int cnt[1024];
-  __shared__ int wsum[4];
-  const int nc = a.nc, ng = a.ng;
-  for (int g = threadIdx.x; g < ng; g += 256) cnt[g] = fill ? a.offs[b * ng + g] : 0;
-  __syncthreads();
+// Candidate collection, per image in anchor order within each group (deterministic), over a (chunk, image) grid
+// of 256-anchor chunks so the class-score reads of the whole batch are in flight at once:
+//   count: every wave records one ballot mask per group in LDS; the block writes its per-group counts;
+//   scan:  per image, group totals -> group offsets (counts/offs) and each (chunk, group)'s start slot;
+//   fill:  the same ballots again; a candidate's slot = its chunk's start + earlier waves' popcounts + lane rank.
+__device__ __forceinline__ void nms_chunk_masks(const NmsArgs& a, int b, int an, unsigned long long (*wm)[1024],
+                                                float& bs, int& best) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  // one ballot step: `take` candidates of group g, appended in lane (anchor) order
-  auto append = [&](int g, bool take, float s, int key, int cls) {
-    unsigned long long m = __ballot(take);
-    int before = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) wsum[wave] = __popcll(m);
-    __syncthreads();
-    int base = cnt[g];
-    for (int w = 0; w < wave; ++w) base += wsum[w];
-    if (fill && take) {
-      long pos = (long)b * a.cap + base + before;
-      a.cscore[pos] = s;
-      a.ckey[pos] = key;
-      a.ccls[pos] = cls;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) cnt[g] += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-    __syncthreads();
-  };
-  for (int a0 = 0; a0 < a.A; a0 += 256) {
-    const int an = a0 + threadIdx.x;
-    const bool valid = an < a.A;
-    if (a.multi) {
-      for (int c = 0; c < nc; ++c) {
-        float s = valid ? ycoord(a, b, 4 + c, an) : 0.f;
-        bool take = valid && s > a.conf && (!a.cmask || a.cmask[c]);
-        append(c, take, s, an * nc + c, c);
-      }
-    } else {
-      int best = 0;
-      float bs = -INFINITY;
-      if (valid)
-        for (int c = 0; c < nc; ++c) {
-          float s = ycoord(a, b, 4 + c, an);
-          if (s > bs) {  // first maximum, as torch.max(1)
-            bs = s;
-            best = c;
+  const bool valid = an < a.A;
+  const int nc = a.nc, ng = a.ng;
+  best = 0;
+  bs = -INFINITY;
+  bool ok = false;
+  if (!a.multi) {
+    if (valid) {
+      float s[8];
+      for (int c0 = 0; c0 < nc; c0 += 8) {  // 8 class rows in flight per thread
+#pragma unroll
+        for (int j = 0; j < 8; ++j) s[j] = c0 + j < nc ? ycoord(a, b, 4 + c0 + j, an) : -INFINITY;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          if (s[j] > bs) {  // first maximum, as torch.max(1)
+            bs = s[j];
+            best = c0 + j;
           }
-        }
-      bool ok = valid && bs > a.conf && (!a.cmask || a.cmask[best]);
-      if (a.agnostic) {
-        append(0, ok, bs, an, best);
-      } else {
-        for (int c = 0; c < nc; ++c) append(c, ok && best == c, bs, an, best);
       }
+    }
+    ok = valid && bs > a.conf && (!a.cmask || a.cmask[best]);
+  }
+#pragma unroll 8
+  for (int g = 0; g < ng; ++g) {
+    bool take;
+    if (a.multi) {
+      const float sc = valid ? ycoord(a, b, 4 + g, an) : 0.f;
+      take = valid && sc > a.conf && (!a.cmask || a.cmask[g]);
+    } else {
+      take = ok && (a.agnostic || best == g);
+    }
+    const unsigned long long m = __ballot(take);
+    if (lane == 0) wm[wave][g] = m;
+  }
+}
+
+__global__ void __launch_bounds__(256) nms_count_kernel(NmsArgs a) {
+  const int chunk = blockIdx.x, b = blockIdx.y, nch = gridDim.x;
+  __shared__ unsigned long long wm[4][1024];
+  float bs;
+  int best;
+  nms_chunk_masks(a, b, chunk * 256 + threadIdx.x, wm, bs, best);
+  __syncthreads();
+  for (int g = threadIdx.x; g < a.ng; g += 256)
+    a.ccnt[((long)b * nch + chunk) * a.ng + g] =
+        __popcll(wm[0][g]) + __popcll(wm[1][g]) + __popcll(wm[2][g]) + __popcll(wm[3][g]);
+}
+
+__global__ void __launch_bounds__(256) nms_scan_kernel(NmsArgs a, int nch) {
+  const int b = blockIdx.x, ng = a.ng;
+  __shared__ int tot[1024];
+  for (int g = threadIdx.x; g < ng; g += 256) {
+    int t = 0;
+    for (int ch = 0; ch < nch; ++ch) t += a.ccnt[((long)b * nch + ch) * ng + g];
+    tot[g] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int g = 0; g < ng; ++g) {
+      a.counts[b * ng + g] = tot[g];
+      a.offs[b * ng + g] = run;
+      run += tot[g];
     }
   }
-  if (!fill) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      int run = 0;
-      for (int g = 0; g < ng; ++g) {
-        a.counts[b * ng + g] = cnt[g];
-        a.offs[b * ng + g] = run;
-        run += cnt[g];
-      }
+  __syncthreads();
+  for (int g = threadIdx.x; g < ng; g += 256) {
+    int run = a.offs[b * ng + g];
+    for (int ch = 0; ch < nch; ++ch) {
+      const long i = ((long)b * nch + ch) * ng + g;
+      const int c = a.ccnt[i];
+      a.ccnt[i] = run;  // count -> start slot of (chunk, group)
+      run += c;
     }
+  }
+}
+
+__global__ void __launch_bounds__(256) nms_fill_kernel(NmsArgs a) {
+  const int chunk = blockIdx.x, b = blockIdx.y, nch = gridDim.x;
+  __shared__ unsigned long long wm[4][1024];
+  const int an = chunk * 256 + threadIdx.x;
+  float bs;
+  int best;
+  nms_chunk_masks(a, b, an, wm, bs, best);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  const int nc = a.nc;
+  for (int g = 0; g < a.ng; ++g) {
+    const unsigned long long m = wm[wave][g];
+    if (!((m >> lane) & 1ull)) continue;
+    int base = a.ccnt[((long)b * nch + chunk) * a.ng + g];
+    for (int w = 0; w < wave; ++w) base += __popcll(wm[w][g]);
+    const long pos = (long)b * a.cap + base + __popcll(m & below);
+    a.cscore[pos] = a.multi ? ycoord(a, b, 4 + g, an) : bs;
+    a.ckey[pos] = a.multi ? an * nc + g : an;
+    a.ccls[pos] = a.multi ? g : best;
   }
 }
 
@@ -357,7 +397,7 @@ using namespace adr;
 extern "C" size_t adr_nms_workspace(int B, int nc, int A, int multi, int max_det) {
   size_t cap = (size_t)A * (multi ? nc : 1);
   return (size_t)B * nc * 4 * 2 + (size_t)B * cap * 12 + (size_t)B * 8 + (size_t)B * nc * max_det * 4 +
-         (size_t)B * nc * 4 + 256;
+         (size_t)B * nc * 4 + (size_t)B * cdiv(A, 256) * nc * 4 + 256;
 }
 
 extern "C" int adr_nms(const float* y, int B, int nc, int A, float conf, float iou, int multi, int agnostic,
@@ -381,12 +421,15 @@ extern "C" int adr_nms(const float* y, int B, int nc, int A, float conf, float i
   a.ccls = (int*)w; w += (size_t)B * a.cap * 4;
   a.thr = (unsigned*)w; w += (size_t)B * 8;
   a.kept = (int*)w; w += (size_t)B * nc * max_det * 4;
-  a.nkept = (int*)w;
+  a.nkept = (int*)w; w += (size_t)B * nc * 4;
+  a.ccnt = (int*)w;
+  const int nch = cdiv(A, 256);
   a.out = out;
   a.nout = nout;
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(nms_collect_kernel, dim3(B), dim3(256), 0, st, a, 0);
-  hipLaunchKernelGGL(nms_collect_kernel, dim3(B), dim3(256), 0, st, a, 1);
+  hipLaunchKernelGGL(nms_count_kernel, dim3(nch, B), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(nms_scan_kernel, dim3(B), dim3(256), 0, st, a, nch);
+  hipLaunchKernelGGL(nms_fill_kernel, dim3(nch, B), dim3(256), 0, st, a);
   hipLaunchKernelGGL(nms_select_kernel, dim3(B), dim3(256), 0, st, a);
   hipLaunchKernelGGL(nms_class_kernel, dim3(B * a.ng), dim3(256), 0, st, a);
   hipLaunchKernelGGL(nms_merge_kernel, dim3(B), dim3(64), 0, st, a);
