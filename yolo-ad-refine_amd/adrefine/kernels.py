@@ -1127,35 +1127,59 @@ def _adjacent_slices(grads, sizes, dtype):
 
 
 class FanOutFn(torch.autograd.Function):
-    """x used by two consumers, as two views. Backward sums the two gradients with one adr_ew launch — into
-    the one that is an exclusive concat-gradient slice when there is one (no new buffer, and the split that
-    produced x can then hand its gradient back as a view) — instead of autograd's own accumulation, which is a
-    PyTorch add (a slow strided kernel on channel slices)."""
+    """x used by n consumers, as n views. Backward sums the n gradients with HIP launches (one for 2 or 3 of
+    them) — into one that is an exclusive concat-gradient slice when there is one (no new buffer, and the split
+    that produced x can then hand its gradient back as a view) — instead of autograd's own accumulation, which
+    is one PyTorch add per extra consumer (a slow strided kernel on channel slices)."""
 
     @staticmethod
-    def forward(ctx, x):
+    def forward(ctx, x, n):
         ctx.set_materialize_grads(False)
-        return x[:, :], x[:, :]
+        return tuple(x[:, :] for _ in range(n))
 
     @staticmethod
-    def backward(ctx, ga, gb):
-        if ga is None or gb is None:
-            return gb if ga is None else ga
-        if gb.dtype != ga.dtype:
-            gb = gb.to(ga.dtype)
-        if not getattr(ga, "_adr_excl", False) and getattr(gb, "_adr_excl", False):
-            ga, gb = gb, ga
-        va, vb = _v(ga), _v(gb)
-        if getattr(ga, "_adr_excl", False) and va[0] is ga:
-            _ew(EW_COPY, va, vb, accumulate=1)  # ga += gb in place
-            return ga
-        out = _new_like(va[0])
-        _ew(EW_AXPBY, (out, out.data_ptr(), out.shape[1]), va, vb)
-        return out
+    def backward(ctx, *grads):
+        gs = [g for g in grads if g is not None]
+        if not gs:
+            return None, None
+        if len(gs) == 1:
+            return gs[0], None
+        dt = gs[0].dtype
+        gs = [g if g.dtype == dt else g.to(dt) for g in gs]
+        excl = [g for g in gs if getattr(g, "_adr_excl", False) and _v(g)[0] is g]
+        if excl:  # accumulate the others into the exclusive slice in place
+            acc = excl[0]
+            rest = [g for g in gs if g is not acc]
+            va = _v(acc)
+            while rest:
+                if len(rest) >= 2:
+                    _ew(EW_AXPBY, va, _v(rest[0]), _v(rest[1]), accumulate=1)  # acc += r0 + r1
+                    rest = rest[2:]
+                else:
+                    _ew(EW_COPY, va, _v(rest[0]), accumulate=1)
+                    rest = rest[1:]
+            return acc, None
+        out = _new_like(_v(gs[0])[0])
+        vo = (out, out.data_ptr(), out.shape[1])
+        if len(gs) >= 3:
+            _ew(EW_ADD3, vo, _v(gs[0]), _v(gs[1]), _v(gs[2]))
+            rest = gs[3:]
+        else:
+            _ew(EW_AXPBY, vo, _v(gs[0]), _v(gs[1]))
+            rest = []
+        while rest:
+            if len(rest) >= 2:
+                _ew(EW_AXPBY, vo, _v(rest[0]), _v(rest[1]), accumulate=1)
+                rest = rest[2:]
+            else:
+                _ew(EW_COPY, vo, _v(rest[0]), accumulate=1)
+                rest = rest[1:]
+        return out, None
 
 
-def fanout(x):
-    return FanOutFn.apply(x)
+def fanout(x, n=2):
+    """n views of x whose gradients are summed by libadr (see FanOutFn)."""
+    return FanOutFn.apply(x, n)
 
 
 class AddFn(torch.autograd.Function):

@@ -34,7 +34,8 @@ class Bottleneck(nn.Module):
 
     def forward(self, x, out=None):
         if self.add:
-            return K.add(x, self.cv2(self.cv1(x)), out=out)
+            xa, xb = K.fanout(x)  # residual + branch: one HIP gradient sum instead of an autograd add
+            return K.add(xa, self.cv2(self.cv1(xb)), out=out)
         return self.cv2(self.cv1(x), out=out)
 
 
@@ -76,7 +77,8 @@ class C3(nn.Module):
     accepts_out = True
 
     def forward(self, x, out=None):
-        return self.cv3(K.cat([self.m(self.cv1(x)), self.cv2(x)]), out=out)
+        xa, xb = K.fanout(x)
+        return self.cv3(K.cat([self.m(self.cv1(xa)), self.cv2(xb)]), out=out)
 
 
 class C3k(C3):
@@ -143,8 +145,10 @@ class Bottleneck_MLCA(Bottleneck):
         self.attention = MLCA(c2)
 
     def forward(self, x):
-        y = self.cv2(self.cv1(x))
-        return self.attention(y, x if self.add else None)
+        if not self.add:
+            return self.attention(self.cv2(self.cv1(x)), None)
+        xa, xb = K.fanout(x)
+        return self.attention(self.cv2(self.cv1(xa)), xb)
 
 
 class C3k_MLCA(C3k):
@@ -178,11 +182,13 @@ class ELA_HSFPN(nn.Module):  # noqa: N801 (reference name)
     def forward(self, x):
         N, C, H, W = x.shape
         conv, gn = self.conv1x1[0], self.conv1x1[1]
+        if self.flag:
+            x, xg = K.fanout(x)
         p = K.axis_mean(x, "ela")  # (2N, C, L, 1): both branches as separate "images" (GN per branch)
         w4 = conv.weight.unsqueeze(-1)  # (C, C, 7) -> (C, C, 7, 1): a 7x1 conv over the pooled axis
         y, _ = K.conv2d(p, w4, conv.bias, (1, 1), (3, 0))
         a = K.gn_act(y, gn, "sigmoid")
-        return K.gate(x if self.flag else None, a, a, "ela", x.shape)
+        return K.gate(xg if self.flag else None, a, a, "ela", x.shape)
 
 
 class Multiply(nn.Module):
@@ -284,7 +290,9 @@ class CrossScaleAttentionTSSA(nn.Module):
     def forward(self, x):
         B, C, H, W = x.shape
         qkvs = []
+        xv = list(K.fanout(x, len(self.scales)))
         for s, proj in zip(self.scales, self.qkv_projections):
+            x = xv.pop()
             xs = x if s == 1 else K.bilinear(K.adaptive_avg_pool(x, H // s, W // s), H, W)
             qkvs.append(_linear(K.tokens(xs), proj.weight, proj.bias))
         st = K.tssa_stack(self.temps, self.heads, qkvs)  # (B, C, S*HW, 1)
@@ -315,8 +323,9 @@ class AdaptiveDynamicTanh(nn.Module):
 
     def forward(self, x):
         g1, g3 = self.importance_gate[1], self.importance_gate[3]
-        imp = K.gate_mlp(K.gap(x), g1.weight, g1.bias, g3.weight, g3.bias, "relu", "softmax")  # (N, 3)
-        return K.adyt(x, self.alphas, imp, self.weight, self.bias)
+        xa, xb = K.fanout(x)
+        imp = K.gate_mlp(K.gap(xa), g1.weight, g1.bias, g3.weight, g3.bias, "relu", "softmax")  # (N, 3)
+        return K.adyt(xb, self.alphas, imp, self.weight, self.bias)
 
 
 class ProgressiveFeatureFusion(nn.Module):
@@ -338,18 +347,23 @@ class ProgressiveFeatureFusion(nn.Module):
         self.stage_attention = nn.Parameter(torch.ones(num_stages) / num_stages)
 
     def forward(self, x):
+        # every multiply-read tensor is fanned out so its gradient is summed by one HIP launch, not autograd adds
         outs = []
-        cur = x
+        x, cur = K.fanout(x)  # base of the weighted sum / stage-0 input
         for i, st in enumerate(self.stages):
-            t = K.dwconv(cur, st["conv"].weight, st["conv"].bias, 3)
+            last = i == self.num_stages - 1
+            cv = list(K.fanout(cur, 2 if last else 3))
+            t = K.dwconv(cv[0], st["conv"].weight, st["conv"].bias, 3)
             t = K.bn_act(t, None, st["norm"], "gelu", self.training)
-            cm, _ = K.conv2d(t, st["channel_mix"].weight, st["channel_mix"].bias, 1, 0)
-            sm = K.dwconv(t, st["spatial_mix"].weight, st["spatial_mix"].bias, 7)
-            out = K.add(cm, sm, cur)
-            outs.append(out)
-            if i < self.num_stages - 1:
+            ta, tb = K.fanout(t)
+            cm, _ = K.conv2d(ta, st["channel_mix"].weight, st["channel_mix"].bias, 1, 0)
+            sm = K.dwconv(tb, st["spatial_mix"].weight, st["spatial_mix"].bias, 7)
+            out = K.add(cm, sm, cv[1])
+            if not last:
+                out, ob = K.fanout(out)
                 sf = self.stage_fusion[i]
-                cur, _ = K.conv2d(K.cat([cur, out]), sf.weight, sf.bias, 1, 0)
+                cur, _ = K.conv2d(K.cat([cv[2], ob]), sf.weight, sf.bias, 1, 0)
+            outs.append(out)
         return K.weighted_sum(self.stage_attention, outs, base=x)
 
 
@@ -371,13 +385,16 @@ class ProgressiveTSSA_Fusion(nn.Module):  # noqa: N801
 
     def forward(self, x):
         B, C, H, W = x.shape
-        identity = x
+        if self.add:
+            identity, x = K.fanout(x)
         x = self.progressive_fusion1(x)
         a = K.untokens(self.attn(self.dyt1(x)), H, W)
         x = K.scale(a, self.residual_weight1, "scalar", res=identity) if self.add else a
         x = self.progressive_fusion2(x)
+        if self.add:
+            x, xr = K.fanout(x)
         f = self.ffn(self.dyt2(x))
-        return K.scale(f, self.residual_weight2, "scalar", res=x) if self.add else f
+        return K.scale(f, self.residual_weight2, "scalar", res=xr) if self.add else f
 
 
 class Attention(nn.Module):

@@ -128,12 +128,13 @@ class CoordAtt(nn.Module):
         self.conv_w = Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
 
     def forward(self, x):
+        x, xg = K.fanout(x)
         y = K.axis_mean(x, "coord")  # (N, C, H+W, 1): [row means ; column means]
         y, _ = K.conv2d(y, self.conv1.weight, self.conv1.bias, 1, 0)
         y = K.bn_act(y, None, self.bn1, "hswish", self.training)
         a_h = K.act(K.conv2d(y, self.conv_h.weight, self.conv_h.bias, 1, 0)[0], "sigmoid")
         a_w = K.act(K.conv2d(y, self.conv_w.weight, self.conv_w.bias, 1, 0)[0], "sigmoid")
-        return K.gate(x, a_h, a_w, "coord", x.shape)
+        return K.gate(xg, a_h, a_w, "coord", x.shape)
 
 
 class CrossTaskInteraction(nn.Module):
@@ -147,11 +148,13 @@ class CrossTaskInteraction(nn.Module):
         self.reg_gate = nn.Sequential(Conv2d(channels * 2, channels, 1), nn.Sigmoid())
 
     def forward(self, cls_feat, reg_feat):
-        c2r = self.cls_to_reg(cls_feat)
-        r2c = self.reg_to_cls(reg_feat)
-        cg = K.act(self.cls_gate[0](K.cat([cls_feat, r2c])), "sigmoid")
-        rg = K.act(self.reg_gate[0](K.cat([reg_feat, c2r])), "sigmoid")
-        return K.fma(cls_feat, r2c, cg), K.fma(reg_feat, c2r, rg)
+        cf = list(K.fanout(cls_feat, 3))
+        rf = list(K.fanout(reg_feat, 3))
+        c2r = list(K.fanout(self.cls_to_reg(cf[0])))
+        r2c = list(K.fanout(self.reg_to_cls(rf[0])))
+        cg = K.act(self.cls_gate[0](K.cat([cf[1], r2c[0]])), "sigmoid")
+        rg = K.act(self.reg_gate[0](K.cat([rf[1], c2r[0]])), "sigmoid")
+        return K.fma(cf[2], r2c[1], cg), K.fma(rf[2], c2r[1], rg)
 
 
 class _DCNWeight(nn.Module):
@@ -202,7 +205,8 @@ class ResidualBlockGN(nn.Module):
         self.shortcut = nn.Identity() if c1 == c2 and s == 1 else Conv_GN(c1, c2, 1, s, act=False)
 
     def forward(self, x):
-        res = x if isinstance(self.shortcut, nn.Identity) else self.shortcut(x)
+        x, xs = K.fanout(x)
+        res = xs if isinstance(self.shortcut, nn.Identity) else self.shortcut(xs)
         return K.add(self.conv2(self.conv1(x)), res)
 
 
@@ -246,18 +250,19 @@ class AYHead1(nn.Module):
 
     def _level(self, x, i):
         ax = self.stems[i](x)
-        feat = self.share_conv(ax)
-        avg = K.gap(feat)
-        cls_f = self.cls_decomp(feat, avg)
-        reg_f = self.reg_decomp(feat, avg)
+        # feat feeds five consumers: its gradient is summed by libadr (K.fanout), not by autograd adds
+        fv = list(K.fanout(self.share_conv(ax), 5))
+        avg = K.gap(fv[0])
+        cls_f = self.cls_decomp(fv[1], avg)
+        reg_f = self.reg_decomp(fv[2], avg)
         cls_f, reg_f = self.cross_task(cls_f, reg_f)
         cls_e = self.rep_block_cls(cls_f)
         so = self.spatial_conv_offset
-        om = K.padded_conv2d(feat, so.weight, so.bias, 1, 1, 32)  # 27 channels padded to 32
+        om = K.padded_conv2d(fv[3], so.weight, so.bias, 1, 1, 32)  # 27 channels padded to 32
         r = self.DyDCNV2(reg_f, om)
         r = self.coord_attention_reg(r)
         c0, c2 = self.cls_prob_conv[0], self.cls_prob_conv[2]
-        cp = K.act(K.conv2d(feat, c0.weight, c0.bias, 1, 0)[0], "relu")
+        cp = K.act(K.conv2d(fv[4], c0.weight, c0.bias, 1, 0)[0], "relu")
         cp = K.act(K.padded_conv2d(cp, c2.weight, c2.bias, 1, 1, 8), "sigmoid")  # channel 0 valid
         reg_out = self.scale[i](self.cv2(r))
         cls_out = self.cv3(K.mul_pixel(cls_e, cp))

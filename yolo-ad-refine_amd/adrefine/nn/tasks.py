@@ -178,21 +178,53 @@ def initialize_weights(model):
             m.eps, m.momentum = 1e-3, 0.03
 
 
-def route_layers(layers, save, x, y, start=0, cuts=()):
+def consumer_counts(layers):
+    """How many later layers read each layer's output (its `f` references, -1 = the previous layer)."""
+    uses = {}
+    for m in layers:
+        for j in ([m.f] if isinstance(m.f, int) else m.f):
+            src = m.i - 1 if j == -1 else (j if j >= 0 else m.i + j)
+            uses[src] = uses.get(src, 0) + 1
+    return uses
+
+
+def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
     """The layer loop of _predict_once (tasks.py:155-167): each layer reads x (f == -1) or saved outputs y[f],
-    and its output is kept in y when a later layer reads it. With `cuts`, the tensors crossing the end of each
-    listed layer are replaced by detached leaves (engine/ddp.cut_live) and returned as per-cut (tensor, leaf)
-    lists, so the backward can run stage by stage."""
+    and its output is kept in y when a later layer reads it. An output read by several layers is handed to each
+    reader as its own view (K.fanout), so its gradient is summed by one libadr launch instead of autograd adds.
+    With `cuts`, the tensors crossing the end of each listed layer are replaced by detached leaves
+    (engine/ddp.cut_live) and returned as per-cut (tensor, leaf) lists, so the backward can run stage by stage."""
     bounds = []
+    views = {}
     if cuts:
         from ..engine.ddp import cut_live
+
+    def fan(j, t):
+        n = uses.get(j, 1) if uses else 1
+        if n > 1 and torch.is_tensor(t) and t.dim() == 4 and t.requires_grad:
+            views[j] = list(K.fanout(t, n))
+
+    def take(j, t):
+        v = views.get(j)
+        return v.pop() if v else t
+
+    if start > 0:
+        fan(start - 1, x)
     for m in layers[start:]:
-        if m.f != -1:
-            x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
+        if m.f == -1:
+            x = take(m.i - 1, x)
+        elif isinstance(m.f, int):
+            x = take(m.f, y[m.f])
+        else:
+            x = [take(m.i - 1, x) if j == -1 else take(j, y[j]) for j in m.f]
         x = m(x)
         y.append(x if m.i in save else None)
         if m.i in cuts:
             x = cut_live(x, y, layers, m.i, bounds)  # y[i] and x stay one leaf when they are one tensor
+            for j, vs in views.items():  # readers after the cut take views of the new leaves
+                if vs:
+                    views[j] = list(K.fanout(y[j], len(vs))) if len(vs) > 1 else [y[j]]
+        fan(m.i, x)
     return x, bounds
 
 
@@ -250,7 +282,9 @@ class DetectionModel(nn.Module):
         y = [x if self.model[0].i in self.save else None] if first else []
         if cuts and first and 0 in cuts:
             raise RuntimeError("stage cut after the fused stem layer is not supported")
-        x, bounds = route_layers(layers, self.save, x, y, first, cuts)
+        if getattr(self, "_uses", None) is None:
+            self._uses = consumer_counts(self.model)
+        x, bounds = route_layers(layers, self.save, x, y, first, cuts, self._uses)
         if cuts:
             self.stage_bounds = bounds
         return x
