@@ -21,7 +21,11 @@ def _prefixed(P, pre="m"):
                                            # 3x3 halo-tile path (adr_conv.hip conv3_kernel): 16- and 8-wide tiles,
                                            # ragged last tile row band, one and several 32-channel chunks
                                            (64, 64, 3, 1, 16), (64, 128, 3, 1, 24), (32, 64, 3, 1, 40),
-                                           (128, 64, 3, 1, 16), (64, 32, 3, 1, 16), (32, 32, 3, 1, 24)])
+                                           (128, 64, 3, 1, 16), (64, 32, 3, 1, 16), (32, 32, 3, 1, 24),
+                                           # thin-channel 3x3 halo WGRAD (adr_wgrad.hip wgrad3t_kernel): C <= 16,
+                                           # K <= 32, stride 1 and 2, padded channel blocks
+                                           (16, 8, 3, 1, 32), (8, 16, 3, 1, 32), (16, 32, 3, 2, 64),
+                                           (8, 32, 3, 2, 32)])
 def test_conv_bn_silu(dtype, c1, c2, k, s, hw):
     from adrefine.nn.modules import Conv
     m = Conv(c1, c2, k, s)
@@ -46,6 +50,30 @@ def test_conv_bn_silu(dtype, c1, c2, k, s, hw):
                  what="running_mean")
     assert_close(m.bn.running_var, P["bn.running_var"], rtol=1e-4, atol=1e-4 if dtype == torch.float32 else 2e-2,
                  what="running_var")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_c3k2_bottleneck_thin_sliced(dtype):
+    """The C3k2 bottleneck of model.2 at a tile-aligned size: its 16 -> 8 3x3 conv reads a 16-channel slice of the
+    48-channel concat buffer (x channel stride 48) and runs the thin-channel WGRAD kernel."""
+    from adrefine.nn.modules.block import C3k2
+    m = C3k2(32, 64, 1, False, 0.25)
+    rec = load_recipe_into(m)
+    m = m.cuda().train()
+    x = seeded_randn(2, 32, 32, 32, seed=7)
+    xd = to_dev(x, dtype)
+    y = m(xd)
+    g = seeded_randn(*y.shape, seed=8)
+    y.backward(g.to("cuda", dtype))
+    P = param_dict_requires_grad({k2: v.clone() for k2, v in rec.items()})
+    xr = x.clone().requires_grad_(True)
+    yr = O.c2f_family(_prefixed(P), "m", xr, 32, 64, 1, False, 0.25, True, True, False)
+    yr.backward(g)
+    tol = TOL[dtype]
+    assert_close(y.float(), yr, **tol, what="y")
+    assert_close(xd.grad.float(), xr.grad, **tol, what="dx")
+    for name, prm in m.named_parameters():
+        assert_close(prm.grad, P[name].grad, **tol, what=name)
 
 
 def test_conv_golden_fixture():

@@ -14,6 +14,7 @@
 //   cls pass per (b, a): SlideLoss-modulated BCE over nc classes (mu = max(0.2, mean CIoU of positives)),
 //            and the full 4*reg_max + nc gradient row for the anchor.
 #include "adr_common.h"
+#include <cstdlib>
 
 namespace adr {
 
@@ -466,14 +467,24 @@ __device__ __forceinline__ void store8(T* p, const float* v) {
 //      weight and its gradient), lanes 12..15 own one ltrb side each (16 DFL bins: DFL + CIoU/NWD gradient through
 //      the softmax expectation), so every access is a 16-byte vector of one row. A block walks 256 anchors;
 //      block partial of sum bce*mod in a fixed-order tree. ----
-constexpr int CLS_ANCHORS_PER_BLOCK = 256;
+// anchors per workgroup of loss_cls_grad_kernel (16 per pass): small, so the whole batch's rows are in flight
+// at once instead of 16 dependent passes per workgroup; ADR_CLS_APB overrides it (multiple of 16) for A/B runs
+static int cls_apb() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ADR_CLS_APB");
+    v = e ? atoi(e) : 32;
+    if (v < 16 || v % 16) v = 32;
+  }
+  return v;
+}
 
 template <typename T>
 __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, int B, int nmax, int nc, float gscale,
                                                             const float* gt, const float* pbox, const int* tgi,
                                                             const uint8_t* fg, const float* tnorm, const float* scal,
                                                             float* part, float box_gain, float cls_gain,
-                                                            float dfl_gain) {
+                                                            float dfl_gain, int apb) {
   __shared__ float sh[256];
   const int slot = threadIdx.x & 15, sub = threadIdx.x >> 4;
   const float tss = scal[0], mu = scal[1];
@@ -481,8 +492,8 @@ __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, 
   const float cscale = gscale * cls_gain / tss;
   const long nanch = (long)B * L.A;
   float acc = 0.f;
-  for (int it = 0; it < CLS_ANCHORS_PER_BLOCK / 16; ++it) {
-    const long i = (long)blockIdx.x * CLS_ANCHORS_PER_BLOCK + it * 16 + sub;
+  for (int it = 0; it < apb / 16; ++it) {
+    const long i = (long)blockIdx.x * apb + it * 16 + sub;
     if (i >= nanch) break;
     const int b = (int)((unsigned)i / (unsigned)L.A), a = (int)i - b * L.A;  // B * A < 2^31
     int lvl;
@@ -611,7 +622,7 @@ extern "C" size_t adr_det_loss_workspace(int B, int nmax, int A) {
          + rows * 2 * 4            // pos
          + n * 4                   // tnorm
          + nblk * 6 * 4 + 64       // fg partials + scalars
-         + nblk * 4 + 256;         // cls partials
+         + (n + 15) / 16 * 4 + 256; // cls partials (>= 16 anchors per workgroup)
 }
 
 extern "C" int adr_det_loss(int dtype, const void* f0, const void* f1, const void* f2, int cs0, int cs1, int cs2,
@@ -670,10 +681,11 @@ extern "C" int adr_det_loss(int dtype, const void* f0, const void* f1, const voi
   }
   LDISPATCH(loss_fg_kernel, dim3(nblk), dim3(256), L, B, nmax, gt, pbox, align, tgi, fg, pos, tnorm, part);
   hipLaunchKernelGGL(loss_scalars_kernel, dim3(1), dim3(256), 0, st, part, nblk, scal);
-  LDISPATCH(loss_cls_grad_kernel, dim3(cdiv((long)n, CLS_ANCHORS_PER_BLOCK)), dim3(256), L, G, B, nmax, nc, grad_scale, gt, pbox, tgi, fg, tnorm, scal,
-            part2, box_gain, cls_gain, dfl_gain);
-  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, part2, (int)cdiv((long)n, CLS_ANCHORS_PER_BLOCK), scal, B, box_gain, cls_gain, dfl_gain,
-                     out);
+  const int apb = cls_apb();
+  LDISPATCH(loss_cls_grad_kernel, dim3(cdiv((long)n, apb)), dim3(256), L, G, B, nmax, nc, grad_scale, gt, pbox, tgi, fg,
+            tnorm, scal, part2, box_gain, cls_gain, dfl_gain, apb);
+  hipLaunchKernelGGL(loss_final_kernel, dim3(1), dim3(256), 0, st, part2, (int)cdiv((long)n, apb), scal, B, box_gain,
+                     cls_gain, dfl_gain, out);
 #undef LDISPATCH
   return check_launch("adr_det_loss");
 }

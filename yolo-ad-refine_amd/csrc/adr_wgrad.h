@@ -17,6 +17,7 @@ struct WgPlan {
   int bm, bn, R, tiles, splits;
   long per;  // reduction rows per split (multiple of R); for the 3x3 halo kernel: output tiles per split
   int tw3;   // > 0: 3x3 stride-1 halo-tile kernel (wgrad3_kernel<tw3>) with `per` 128-pixel tiles per split
+  int thin;  // > 0: thin-channel 3x3 halo kernel (wgrad3t_kernel, stride `thin`), `per` tiles per split
 };
 WgPlan wgrad_bf16_plan(const adr_conv_desc* d);
 int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,

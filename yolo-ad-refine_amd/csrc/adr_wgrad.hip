@@ -16,6 +16,7 @@
 // partials are reduced in fixed order by adr_gemm.hip's wgrad_reduce (deterministic).
 #include "adr_common.h"
 #include "adr_wgrad.h"
+#include <cstdlib>
 
 namespace adr {
 
@@ -362,12 +363,175 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
       }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Thin-channel 3x3 weight gradient (stride 1 or 2, pad 1, C <= 16, K <= 32: the 8/16-channel convs of the first
+// C3k2 bottleneck at 160x160 and the 16 -> 32 stride-2 model.1 conv), on 128-pixel TH x 16 output tiles. The
+// general kernel above gathers x per tap with 8-32-channel rows (a few bytes per pixel and tap) and re-reads dy
+// for all nine taps; here each tile's dy rows (KB = 16 or 32 channels, zero-padded) and its input halo
+// ((TH-1)*S+3 rows x 15*S+3 columns x 16 channels, zero-padded) are staged in LDS once, and wave w accumulates
+// output pixels [32w, 32w+32) of every tile for all nine taps; the four waves' sums are combined at the end.
+// Partials [split][K][9][C] as the other kernels write them.
+template <int S, int KB>
+__global__ void __launch_bounds__(256) wgrad3t_kernel(WgArgs a) {
+  constexpr int TW = 16, TH = 8, KT = KB / 16;
+  constexpr int HWW = (TW - 1) * S + 3, HH = (TH - 1) * S + 3, NPIX = HH * HWW;
+  constexpr int PD = KB == 16 ? 16 : 48, PX = 16;  // LDS pitches (elements): odd multiples of 32 bytes
+  constexpr int KQ = KB / 8, D_TOT = 128 * KQ, D_CH = (D_TOT + 255) / 256;
+  constexpr int X_TOT = NPIX * 2, X_CH = (X_TOT + 255) / 256;
+  constexpr int SM_TILES = (128 * PD + NPIX * PX) * 2, SM_RED = KB * 9 * 16 * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SM_TILES > SM_RED ? SM_TILES : SM_RED];
+  __bf16* Ds = reinterpret_cast<__bf16*>(smem);
+  __bf16* Xs = Ds + 128 * PD;
+  float* red = reinterpret_cast<float*>(smem);  // the wave combine reuses the tile buffers after the last tile
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int bx, split;
+  wg_xcd_block(bx, split);
+  (void)bx;
+  const int H = a.ho, W = a.wo;
+  const int tx = W / TW, ty = (H + TH - 1) / TH, ntile = a.n * tx * ty;
+  const int t_beg = split * (int)a.red_per_split;
+  const int t_end = min(ntile, t_beg + (int)a.red_per_split);
+
+  constexpr unsigned OOR = 0x7FFFFFF0u;
+  const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t dy_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
+  u32x4 rd[D_CH], rx[X_CH];
+  auto load = [&](int tile) {
+    const int img = tile / (tx * ty), trem = tile - img * (tx * ty);
+    const int y0 = (trem / tx) * TH, x0 = (trem - (trem / tx) * tx) * TW;
+#pragma unroll
+    for (int i = 0; i < D_CH; ++i) {
+      const int e = tid + 256 * i, p = e / KQ, kq = e % KQ;
+      const int y = y0 + p / TW, xx = x0 + p % TW;
+      const bool ok = e < D_TOT && y < H && kq * 8 < a.k;
+      rd[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          dy_rs, ok ? (unsigned)(((img * H + y) * W + xx) * a.ycs + a.yco + kq * 8) * 2u : OOR, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < X_CH; ++i) {
+      const int e = tid + 256 * i, q = e >> 1, cq = e & 1;
+      const int hy = q / HWW, hx = q - (q / HWW) * HWW;
+      const int gy = y0 * S - 1 + hy, gx = x0 * S - 1 + hx;
+      const bool ok = e < X_TOT && cq * 8 < a.c && gy >= 0 && gy < a.h && gx >= 0 && gx < a.w;
+      rx[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          x_rs, ok ? (unsigned)(((img * a.h + gy) * a.w + gx) * a.xcs + a.xco + cq * 8) * 2u : OOR, 0, 0);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < D_CH; ++i) {
+      const int e = tid + 256 * i;
+      if (e < D_TOT) st16(&Ds[(e / KQ) * PD + (e % KQ) * 8], rd[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < X_CH; ++i) {
+      const int e = tid + 256 * i;
+      if (e < X_TOT) st16(&Xs[(e >> 1) * PX + (e & 1) * 8], rx[i]);
+    }
+  };
+
+  const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  f32x4 acc[9][KT];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) acc[t][kt] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // wave w: tile pixels [32w, 32w + 32); the transposed-read rows 4g + q4 and +16
+  const int plo = wave * 32 + 4 * g + q4, phi = plo + 16;
+  const int qlo = (plo / TW) * S * HWW + (plo % TW) * S, qhi = (phi / TW) * S * HWW + (phi % TW) * S;
+
+  if (t_beg < t_end) load(t_beg);
+  for (int tile = t_beg; tile < t_end; ++tile) {
+    store();
+    __syncthreads();
+    if (tile + 1 < t_end) load(tile + 1);
+    bf16x8 fa[KT];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt) {
+      const __bf16* da = Ds + kt * 16 + 4 * p4;
+      v4s lo = tr_read(da + plo * PD), hi = tr_read(da + phi * PD);
+      v4s both[2] = {lo, hi};
+      fa[kt] = *reinterpret_cast<bf16x8*>(both);
+    }
+    const __bf16* xb = Xs + 4 * p4;
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const int dq = (t / 3) * HWW + (t % 3);
+      v4s blo = tr_read(xb + (qlo + dq) * PX), bhi = tr_read(xb + (qhi + dq) * PX);
+      v4s bb[2] = {blo, bhi};
+      const bf16x8 fb = *reinterpret_cast<bf16x8*>(bb);
+#pragma unroll
+      for (int kt = 0; kt < KT; ++kt)
+        acc[t][kt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[kt], fb, acc[t][kt], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // combine the four waves in a fixed order (((w0 + w1) + w2) + w3), one wave's slab at a time through LDS
+  __syncthreads();
+  for (int w = 1; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) red[((kt * 16 + 4 * g + e) * 9 + t) * 16 + (lane & 15)] = acc[t][kt][e];
+    }
+    __syncthreads();
+    if (wave == 0) {
+#pragma unroll
+      for (int t = 0; t < 9; ++t)
+#pragma unroll
+        for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[t][kt][e] += red[((kt * 16 + 4 * g + e) * 9 + t) * 16 + (lane & 15)];
+    }
+    __syncthreads();
+  }
+  if (wave > 0) return;
+  float* part = a.out + (long)split * a.k * (9L * a.c);
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int co = kt * 16 + 4 * g + e, ci = lane & 15;
+        const float v = acc[t][kt][e];
+        if (co < a.k && ci < a.c) {
+          float* o = part + ((long)co * 9 + t) * a.c + ci;
+          *o = a.accumulate ? *o + v : v;
+        }
+      }
+}
+
+static int wg3_thin(const adr_conv_desc* d) {
+  if (d->r != 3 || d->s != 3 || d->pad_h != 1 || d->pad_w != 1 || d->stride_h != d->stride_w) return 0;
+  if (d->stride_h != 1 && d->stride_h != 2) return 0;
+  if (d->c > 16 || d->c % 8 || d->k > 32 || d->k % 8 || d->wo % 16) return 0;
+  if (d->x_cstride % 8 || d->x_coff % 8 || d->y_cstride % 8 || d->y_coff % 8) return 0;
+  if (d->stride_h == 2 && (d->h != 2 * d->ho || d->w != 2 * d->wo)) return 0;
+  return d->stride_h;
+}
+
 static int wg3_tw(const adr_conv_desc* d) {
   if (d->r != 3 || d->s != 3 || d->stride_h != 1 || d->stride_w != 1 || d->pad_h != 1 || d->pad_w != 1) return 0;
   if (d->c % 32 || d->k % 32) return 0;
   if (d->wo % 16 == 0 && d->ho >= 8) return 16;
   if (d->wo % 8 == 0) return 8;
   return 0;
+}
+
+// ADR_WGRAD_THIN=0 routes the thin-channel shapes back to the general kernel (A/B runs)
+static bool thin_enabled() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ADR_WGRAD_THIN");
+    v = e ? atoi(e) != 0 : 1;
+  }
+  return v != 0;
 }
 
 static int wg_pick16(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128; }
@@ -386,6 +550,23 @@ static void launch_bm(int bn, dim3 grid, const WgArgs& g, hipStream_t st) {
 
 WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   WgPlan p;
+  p.tw3 = 0;
+  p.thin = thin_enabled() ? wg3_thin(d) : 0;
+  if (p.thin) {
+    const long ntile = (long)d->n * ((d->ho + 7) / 8) * (d->wo / 16);
+    p.bm = d->k <= 16 ? 16 : 32;
+    p.bn = 16;
+    p.R = 128;
+    p.tiles = 1;
+    long s = 768;                                                // ~3 workgroups per CU
+    const long by_work = ntile / 4;                              // >= 4 tiles per split
+    if (s > by_work) s = by_work;
+    if (s < 1) s = 1;
+    const long per = (ntile + s - 1) / s;
+    p.splits = (int)((ntile + per - 1) / per);
+    p.per = per;
+    return p;
+  }
   p.tw3 = wg3_tw(d);
   if (p.tw3) {
     const int th = 128 / p.tw3;
@@ -445,6 +626,16 @@ int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, flo
   g.x_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
   g.dy_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
   dim3 grid(p.tiles, p.splits);
+  if (p.thin) {
+    if (p.thin == 1) {
+      if (p.bm == 16) hipLaunchKernelGGL((wgrad3t_kernel<1, 16>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((wgrad3t_kernel<1, 32>), grid, dim3(256), 0, st, g);
+    } else {
+      if (p.bm == 16) hipLaunchKernelGGL((wgrad3t_kernel<2, 16>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((wgrad3t_kernel<2, 32>), grid, dim3(256), 0, st, g);
+    }
+    return check_launch("adr_conv2d_wgrad(bf16, thin 3x3 halo)");
+  }
   if (p.tw3) {
     if (p.bm == 64) {
       if (p.tw3 == 16) hipLaunchKernelGGL((wgrad3_kernel<16, 4>), grid, dim3(256), 0, st, g);
