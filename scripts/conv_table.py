@@ -36,6 +36,6 @@ for tag, shape, nb, fl, t in K.timing_detail():  # every timed libadr launch, ke
     a[0] += 1; a[1] += nb or 0; a[2] += fl or 0; a[3] += t
 tot = sum(v[3] for v in agg.values()) / args.steps
 print(f"timed total per step: {1e3 * tot:.2f} ms")
-for shape, (n, nb, fl, t) in sorted(agg.items(), key=lambda kv: -kv[1][3])[:80]:
+for shape, (n, nb, fl, t) in sorted(agg.items(), key=lambda kv: -kv[1][3])[:200]:
     print(f"{1e3 * t / args.steps:7.3f} ms {n // args.steps:3d}x {1e6 * t / n:8.1f}us {nb / t / 1e9:7.0f} GB/s "
           f"{fl / t / 1e12:6.1f} TF/s  {shape}")

@@ -130,6 +130,23 @@ def _ptr(v):
 _UNTIMED = ("_symbol", "_workspace", "_splits", "_tiles", "_chunks", "_size", "_floats", "adr_set_f32")
 
 
+_SITE_LABELS = ("adr_ew", "adr_affine_act", "adr_affine_act_bwd", "adr_nc_reduce", "adr_memset_zero",
+                "adr_bcast_mul", "adr_cast")
+
+
+def _call_site():
+    """The first caller outside this module's launch helpers (timing detail labels: which op issued a launch)."""
+    import sys
+    f = sys._getframe(2)
+    while f is not None and f.f_code.co_name in ("_ew", "_hook_call", "wrapper", "call", "__call__", "_call"):
+        f = f.f_back
+    if f is None:
+        return "?"
+    cls = f.f_locals.get("ctx")
+    owner = type(cls).__name__.replace("Backward", "") if cls is not None else ""
+    return f"{owner}.{f.f_code.co_name}:{f.f_lineno}" if owner else f"{f.f_code.co_name}:{f.f_lineno}"
+
+
 def _hook_call(name, fn, args):
     """Generic timing of one libadr call (outside annotated regions; host-side queries are not timed)."""
     if _TIMING is None or _ANNOT[0] > 0 or name.endswith(_UNTIMED):
@@ -143,6 +160,9 @@ def _hook_call(name, fn, args):
                 label = label.replace("__bf16", "float")
             nbytes = int(spec[1](args))
             rep = TIMING_REPEAT if spec[2](args) else 1
+        shape = _call_site() if name in _SITE_LABELS else ""
+        if name == "adr_ew":
+            shape = f"op{args[1]}{'+acc' if args[15] else ''} {args[11]}px x{args[12]}ch @{shape}"
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         rc = 0
@@ -151,7 +171,7 @@ def _hook_call(name, fn, args):
             if rc != 0:
                 break
         e1.record()
-        _TIMING.append((label, nbytes, 0, e0, e1, "", rep))
+        _TIMING.append((label, nbytes, 0, e0, e1, shape, rep))
     if rc != 0:
         raise RuntimeError(f"{name}: {lib.lib.adr_last_error().decode()}")
     return rc

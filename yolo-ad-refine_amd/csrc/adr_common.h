@@ -52,37 +52,79 @@ __device__ __forceinline__ void ld_coef(const float* p, float* out) {
 // ---- activations (shared by norm epilogues and elementwise kernels) ----
 enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_RELU = 3, ACT_SIGMOID = 4, ACT_HSWISH = 5 };
 
+// logistic sigmoid; FAST (the bf16 kernels) uses the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE
+// division sequence — the BN/GN activation kernels are VALU-bound on exp + divide, and bf16 storage rounds far
+// coarser than 1 ulp of fp32; the fp32 parity mode keeps the exact division
+template <bool FAST>
+__device__ __forceinline__ float sigmoid_fast(float v) {
+  if constexpr (FAST) return __builtin_amdgcn_rcpf(1.f + __expf(-v));
+  else return 1.f / (1.f + __expf(-v));
+}
+
+template <int ACT, bool FAST = false>
+__device__ __forceinline__ float act_fwd_c(float v) {
+  if constexpr (ACT == ACT_SILU) return FAST ? v * sigmoid_fast<true>(v) : v / (1.f + __expf(-v));
+  else if constexpr (ACT == ACT_GELU) return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
+  else if constexpr (ACT == ACT_RELU) return v > 0.f ? v : 0.f;
+  else if constexpr (ACT == ACT_SIGMOID) return sigmoid_fast<FAST>(v);
+  else if constexpr (ACT == ACT_HSWISH) return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+  else return v;
+}
+// derivative d act(v) / dv
+template <int ACT, bool FAST = false>
+__device__ __forceinline__ float act_bwd_c(float v) {
+  if constexpr (ACT == ACT_SILU) {
+    const float s = sigmoid_fast<FAST>(v);
+    return s * (1.f + v * (1.f - s));
+  } else if constexpr (ACT == ACT_GELU) {
+    const float cdf = 0.5f * (1.f + erff(v * 0.70710678118654752f));
+    const float pdf = 0.39894228040143268f * __expf(-0.5f * v * v);
+    return cdf + v * pdf;
+  } else if constexpr (ACT == ACT_RELU) {
+    return v > 0.f ? 1.f : 0.f;
+  } else if constexpr (ACT == ACT_SIGMOID) {
+    const float s = sigmoid_fast<FAST>(v);
+    return s * (1.f - s);
+  } else if constexpr (ACT == ACT_HSWISH) {
+    return v < -3.f ? 0.f : (v > 3.f ? 1.f : (2.f * v + 3.f) * (1.f / 6.f));
+  } else {
+    return 1.f;
+  }
+}
+
 __device__ __forceinline__ float act_fwd(int act, float v) {
   switch (act) {
-    case ACT_SILU: return v / (1.f + __expf(-v));
-    case ACT_GELU: return 0.5f * v * (1.f + erff(v * 0.70710678118654752f));
-    case ACT_RELU: return v > 0.f ? v : 0.f;
-    case ACT_SIGMOID: return 1.f / (1.f + __expf(-v));
-    case ACT_HSWISH: return v * fminf(fmaxf(v + 3.f, 0.f), 6.f) * (1.f / 6.f);
+    case ACT_SILU: return act_fwd_c<ACT_SILU>(v);
+    case ACT_GELU: return act_fwd_c<ACT_GELU>(v);
+    case ACT_RELU: return act_fwd_c<ACT_RELU>(v);
+    case ACT_SIGMOID: return act_fwd_c<ACT_SIGMOID>(v);
+    case ACT_HSWISH: return act_fwd_c<ACT_HSWISH>(v);
     default: return v;
   }
 }
-// derivative d act(v) / dv
 __device__ __forceinline__ float act_bwd(int act, float v) {
   switch (act) {
-    case ACT_SILU: {
-      float s = 1.f / (1.f + __expf(-v));
-      return s * (1.f + v * (1.f - s));
-    }
-    case ACT_GELU: {
-      float cdf = 0.5f * (1.f + erff(v * 0.70710678118654752f));
-      float pdf = 0.39894228040143268f * __expf(-0.5f * v * v);
-      return cdf + v * pdf;
-    }
-    case ACT_RELU: return v > 0.f ? 1.f : 0.f;
-    case ACT_SIGMOID: {
-      float s = 1.f / (1.f + __expf(-v));
-      return s * (1.f - s);
-    }
-    case ACT_HSWISH: return v < -3.f ? 0.f : (v > 3.f ? 1.f : (2.f * v + 3.f) * (1.f / 6.f));
+    case ACT_SILU: return act_bwd_c<ACT_SILU>(v);
+    case ACT_GELU: return act_bwd_c<ACT_GELU>(v);
+    case ACT_RELU: return act_bwd_c<ACT_RELU>(v);
+    case ACT_SIGMOID: return act_bwd_c<ACT_SIGMOID>(v);
+    case ACT_HSWISH: return act_bwd_c<ACT_HSWISH>(v);
     default: return 1.f;
   }
 }
+
+// host: run F(std::integral_constant<int, ACT>) for a runtime activation code (kernels templated on ACT)
+#define ADR_ACT_DISPATCH(act, F)                                                         \
+  do {                                                                                    \
+    switch (act) {                                                                        \
+      case ACT_SILU: F(ACT_SILU); break;                                                  \
+      case ACT_GELU: F(ACT_GELU); break;                                                  \
+      case ACT_RELU: F(ACT_RELU); break;                                                  \
+      case ACT_SIGMOID: F(ACT_SIGMOID); break;                                            \
+      case ACT_HSWISH: F(ACT_HSWISH); break;                                              \
+      default: F(ACT_NONE); break;                                                        \
+    }                                                                                     \
+  } while (0)
 
 // Thread -> (channel group, pixel row) mapping for 256-thread NHWC elementwise kernels: G = C / vector width
 // lanes per pixel, 256 / G pixels per block pass; the channel group is fixed for the thread's whole loop (so

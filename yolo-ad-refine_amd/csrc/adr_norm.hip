@@ -15,7 +15,7 @@ namespace adr {
 enum RedMode { RED_STATS = 0, RED_BWD = 1, RED_SUM = 2 };
 
 // partial[(n * chunks + chunk)][2][C]
-template <typename T, int MODE>
+template <typename T, int MODE, int ACT = ACT_NONE>
 __global__ void __launch_bounds__(256) nc_reduce_kernel(const T* __restrict__ x, int xcs, int xco,
                                                         const T* __restrict__ dz, int dcs, int dco,
                                                         const float* __restrict__ scale,
@@ -68,7 +68,7 @@ __global__ void __launch_bounds__(256) nc_reduce_kernel(const T* __restrict__ x,
 #pragma unroll
           for (int e = 0; e < VEC; ++e) {
             float xf = to_f(xe[e]);
-            float g = to_f(de[e]) * act_bwd(act, xf * sc[e] + sf[e]);
+            float g = to_f(de[e]) * act_bwd_c<ACT, sizeof(T) == 2>(xf * sc[e] + sf[e]);
             s1[e] += g;
             s2[e] += g * xf;
           }
@@ -330,7 +330,7 @@ __global__ void __launch_bounds__(256) gn_bwd_param_kernel(const float* __restri
 }
 
 // z = act(x * scale + shift) ; NHWC; scale/shift per channel or per (n, channel)
-template <typename T>
+template <typename T, int ACT>
 __global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x, int xcs, int xco, T* __restrict__ z,
                                                          int zcs, int zco, const float* __restrict__ scale,
                                                          const float* __restrict__ shift, int per_sample, int act,
@@ -359,13 +359,13 @@ __global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x
     u32x4 o;
     T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(act_fwd(act, to_f(e[k]) * sc[k] + sh[k]));
+    for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(act_fwd_c<ACT, sizeof(T) == 2>(to_f(e[k]) * sc[k] + sh[k]));
     st16(z + pix * zcs + zco + c0, o);
   }
 }
 
 // dx = A*g + B*x + C with g = dz * act'(x*scale+shift) ; optional accumulate into dx
-template <typename T>
+template <typename T, int ACT>
 __global__ void __launch_bounds__(256) affine_act_bwd_kernel(const T* __restrict__ x, int xcs, int xco,
                                                              const T* __restrict__ dz, int dcs, int dco,
                                                              T* __restrict__ dx, int ocs, int oco,
@@ -418,7 +418,7 @@ __global__ void __launch_bounds__(256) affine_act_bwd_kernel(const T* __restrict
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
       const float xf = to_f(xe[k]);
-      const float g = to_f(de[k]) * act_bwd(act, xf * sc[k] + sh[k]);
+      const float g = to_f(de[k]) * act_bwd_c<ACT, sizeof(T) == 2>(xf * sc[k] + sh[k]);
       float r = ca[k] * g + cbv[k] * xf + cc[k];
       if (accumulate) r += to_f(pe[k]);
       oe[k] = from_f<T>(r);
@@ -481,14 +481,17 @@ extern "C" int adr_nc_reduce(int dtype, int mode, const void* x, int xcs, int xc
   dim3 grid(chunks, N);
   hipStream_t st = (hipStream_t)stream;
   if (mode == RED_BWD) {
-    if (dtype == ADR_BF16)
-      hipLaunchKernelGGL((nc_reduce_kernel<__bf16, RED_BWD>), grid, dim3(256), 0, st, (const __bf16*)x, xcs, xco,
-                         (const __bf16*)dz, dcs, dco, scale, shift, per_sample, act, HW, C, rows_per_chunk, chunks,
-                         partial);
-    else
-      hipLaunchKernelGGL((nc_reduce_kernel<float, RED_BWD>), grid, dim3(256), 0, st, (const float*)x, xcs, xco,
-                         (const float*)dz, dcs, dco, scale, shift, per_sample, act, HW, C, rows_per_chunk, chunks,
-                         partial);
+#define ADR_NCR(A)                                                                                                  \
+  if (dtype == ADR_BF16)                                                                                            \
+    hipLaunchKernelGGL((nc_reduce_kernel<__bf16, RED_BWD, A>), grid, dim3(256), 0, st, (const __bf16*)x, xcs, xco,  \
+                       (const __bf16*)dz, dcs, dco, scale, shift, per_sample, act, HW, C, rows_per_chunk, chunks,   \
+                       partial);                                                                                    \
+  else                                                                                                              \
+    hipLaunchKernelGGL((nc_reduce_kernel<float, RED_BWD, A>), grid, dim3(256), 0, st, (const float*)x, xcs, xco,    \
+                       (const float*)dz, dcs, dco, scale, shift, per_sample, act, HW, C, rows_per_chunk, chunks,    \
+                       partial)
+    ADR_ACT_DISPATCH(act, ADR_NCR);
+#undef ADR_NCR
   } else {
     if (dtype == ADR_BF16)
       hipLaunchKernelGGL((nc_reduce_kernel<__bf16, RED_STATS>), grid, dim3(256), 0, st, (const __bf16*)x, xcs, xco,
@@ -551,12 +554,15 @@ extern "C" int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* 
   ADR_REQUIRE(C / vec <= 256, "affine_act: C=%d too wide", C);
   int grid = grid_for(npix, C / vec);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(affine_act_kernel<__bf16>, dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, xco,
-                       (__bf16*)z, zcs, zco, scale, shift, per_sample, act, npix, HW, C);
-  else
-    hipLaunchKernelGGL(affine_act_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, xcs, xco, (float*)z,
-                       zcs, zco, scale, shift, per_sample, act, npix, HW, C);
+#define ADR_AA(A)                                                                                                   \
+  if (dtype == ADR_BF16)                                                                                            \
+    hipLaunchKernelGGL((affine_act_kernel<__bf16, A>), dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, xco,    \
+                       (__bf16*)z, zcs, zco, scale, shift, per_sample, act, npix, HW, C);                           \
+  else                                                                                                              \
+    hipLaunchKernelGGL((affine_act_kernel<float, A>), dim3(grid), dim3(256), 0, st, (const float*)x, xcs, xco,      \
+                       (float*)z, zcs, zco, scale, shift, per_sample, act, npix, HW, C)
+  ADR_ACT_DISPATCH(act, ADR_AA);
+#undef ADR_AA
   return check_launch("adr_affine_act");
 }
 
@@ -572,14 +578,17 @@ extern "C" int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, co
   ADR_REQUIRE(C / vec <= 256, "affine_act_bwd: C=%d too wide", C);
   int grid = grid_for(npix, C / vec);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == ADR_BF16)
-    hipLaunchKernelGGL(affine_act_bwd_kernel<__bf16>, dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, xco,
-                       (const __bf16*)dz, dcs, dco, (__bf16*)dx, ocs, oco, scale, shift, A, B, Cc, per_sample,
-                       coef_per_sample, act, npix, HW, C, accumulate);
-  else
-    hipLaunchKernelGGL(affine_act_bwd_kernel<float>, dim3(grid), dim3(256), 0, st, (const float*)x, xcs, xco,
-                       (const float*)dz, dcs, dco, (float*)dx, ocs, oco, scale, shift, A, B, Cc, per_sample,
-                       coef_per_sample, act, npix, HW, C, accumulate);
+#define ADR_AAB(AC)                                                                                                 \
+  if (dtype == ADR_BF16)                                                                                            \
+    hipLaunchKernelGGL((affine_act_bwd_kernel<__bf16, AC>), dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs,   \
+                       xco, (const __bf16*)dz, dcs, dco, (__bf16*)dx, ocs, oco, scale, shift, A, B, Cc, per_sample, \
+                       coef_per_sample, act, npix, HW, C, accumulate);                                              \
+  else                                                                                                              \
+    hipLaunchKernelGGL((affine_act_bwd_kernel<float, AC>), dim3(grid), dim3(256), 0, st, (const float*)x, xcs, xco, \
+                       (const float*)dz, dcs, dco, (float*)dx, ocs, oco, scale, shift, A, B, Cc, per_sample,        \
+                       coef_per_sample, act, npix, HW, C, accumulate)
+  ADR_ACT_DISPATCH(act, ADR_AAB);
+#undef ADR_AAB
   return check_launch("adr_affine_act_bwd");
 }
 
