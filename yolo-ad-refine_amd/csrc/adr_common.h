@@ -57,7 +57,9 @@ enum Act { ACT_NONE = 0, ACT_SILU = 1, ACT_GELU = 2, ACT_RELU = 3, ACT_SIGMOID =
 // coarser than 1 ulp of fp32; the fp32 parity mode keeps the exact division
 template <bool FAST>
 __device__ __forceinline__ float sigmoid_fast(float v) {
-  if constexpr (FAST) return __builtin_amdgcn_rcpf(1.f + __expf(-v));
+  // exp(-v) as a bare v_exp_f32 (2^x): no denormal-range guards; -v*log2(e) beyond the fp32 range gives 0 or inf,
+  // and rcp(inf) = 0, the sigmoid's own limit
+  if constexpr (FAST) return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(v * -1.44269504088896341f));
   else return 1.f / (1.f + __expf(-v));
 }
 
