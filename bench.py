@@ -15,6 +15,7 @@ import argparse
 import json
 import math
 import os
+import re
 import sys
 import time
 from pathlib import Path
@@ -144,9 +145,11 @@ def pmc_traffic(symbol):
     rec = doc["kernels"].get(name)
     if rec is None:
         hits = [k for k in doc["kernels"] if k.replace("void ", "").startswith(name + "(")]
-        if not hits and name.startswith("adr::") and name.endswith("<__bf16>"):
-            base = name[5:-8]  # rocprofv3 leaves these templates mangled: _ZN3adr<len><name>IDF16b...
-            hits = [k for k in doc["kernels"] if k.startswith(f"_ZN3adr{len(base)}{base}IDF16b")]
+        m = re.match(r"adr::(\w+)<__bf16((?:, \d+)*)>$", name)
+        if not hits and m:  # rocprofv3 leaves these templates mangled: _ZN3adr<len><name>IDF16b[Li<n>E...]E...
+            base, nums = m.group(1), [int(v) for v in re.findall(r"\d+", m.group(2))]
+            pre = f"_ZN3adr{len(base)}{base}IDF16b" + "".join(f"Li{v}E" for v in nums) + "E"
+            hits = [k for k in doc["kernels"] if k.startswith(pre)]
         if len(hits) != 1:
             return None, None
         rec = doc["kernels"][hits[0]]

@@ -111,11 +111,11 @@ def _es(dtype_code):
 # entry point -> (kernel label as rocprofv3 names it, algorithmic bytes from the call's arguments, idempotent?)
 # Algorithmic bytes: every tensor the launch must touch, read or written once (NHWC activations, compute dtype).
 _ALG_BYTES = {
-    "adr_affine_act_bwd": ("adr::affine_act_bwd_kernel<__bf16>",
+    "adr_affine_act_bwd": (lambda a: f"adr::affine_act_bwd_kernel<__bf16, {a[17]}>",
                            lambda a: _es(a[0]) * a[18] * a[19] * a[20] * (3 + a[21]), lambda a: a[21] == 0),
-    "adr_affine_act": ("adr::affine_act_kernel<__bf16>", lambda a: _es(a[0]) * a[11] * a[12] * a[13] * 2,
-                       lambda a: True),
-    "adr_nc_reduce": (lambda a: f"adr::nc_reduce_kernel<__bf16, {1 if a[1] == 1 else 0}>",
+    "adr_affine_act": (lambda a: f"adr::affine_act_kernel<__bf16, {a[10]}>",
+                       lambda a: _es(a[0]) * a[11] * a[12] * a[13] * 2, lambda a: True),
+    "adr_nc_reduce": (lambda a: f"adr::nc_reduce_kernel<__bf16, {1 if a[1] == 1 else 0}, {a[11] if a[1] == 1 else 0}>",
                       lambda a: _es(a[0]) * a[12] * a[13] * a[14] * (2 if a[1] == 1 else 1), lambda a: True),
     "adr_ew": ("adr::ew_kernel<__bf16>",
                lambda a: _es(a[0]) * a[11] * a[12] * (2 + (a[5] is not None) + (a[7] is not None) + a[15]),
