@@ -25,7 +25,11 @@ namespace adr {
 
 static constexpr int HD = 64;      // head dim
 static constexpr int BLK = 64;     // queries or keys per workgroup
-static constexpr int LDT = HD + 8; // LDS row stride (elements)
+static constexpr int LDT = HD + 16;  // LDS row stride (elements): 160 bytes, an odd multiple of 32 (conflict-free
+                                     // transposing reads)
+
+typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 template <typename T, int D = HD>
 __device__ __forceinline__ void load_rows(T* dst, const T* src, long row0, int L, int cs, int coff) {
@@ -39,6 +43,39 @@ __device__ __forceinline__ void load_rows(T* dst, const T* src, long row0, int L
     st16(dst + r * LDT + c, v);
   }
 }
+
+// 2^x: the bare v_exp_f32 for bf16 (the softmax exponentials were most of the kernels' VALU work: ~20 VALU
+// instructions per MFMA with the range-checked exp2f); exp2f in the fp32 parity mode
+template <typename T>
+__device__ __forceinline__ float fexp2(float x) {
+  if constexpr (sizeof(T) == 2) return __builtin_amdgcn_exp2f(x);
+  else return exp2f(x);
+}
+constexpr float LOG2E = 1.44269504088896341f;
+
+// Register prefetch of one 64-row x D tile: load() issues the global reads of the next tile before the current
+// one is consumed; store() writes them to LDS after the consumers' barrier (rows >= nrows are zero).
+template <typename T, int D>
+struct TilePrefetch {
+  static constexpr int V = 16 / sizeof(T), CPR = D / V, CH = BLK * CPR, PER = (CH + 255) / 256;
+  u32x4 r[PER];
+  __device__ __forceinline__ void load(const T* src, long row0, int nrows, int cs, int coff) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + 256 * i, rr = idx / CPR, cc = (idx % CPR) * V;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (idx < CH && rr < nrows) v = ld16(src + (row0 + rr) * cs + coff + cc);
+      r[i] = v;
+    }
+  }
+  __device__ __forceinline__ void store(T* dst) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int idx = threadIdx.x + 256 * i, rr = idx / CPR, cc = (idx % CPR) * V;
+      if (idx < CH) st16(dst + rr * LDT + cc, r[i]);
+    }
+  }
+};
 
 // C[i][j] += sum_{d<D} A[i][d] * B[j][d] for i in [ai, ai+16), j in [bj, bj+16)
 template <typename T, int D>
@@ -68,6 +105,11 @@ template <typename T, int DT>
 __device__ __forceinline__ void tn_reg(const T* Xs, const float (&p)[4][4], f32x4 (&acc)[DT]) {
   const int lane = threadIdx.x & 63, g = lane >> 4, c = lane & 15;
   if constexpr (sizeof(T) == 2) {
+    // A = X^T: the reduction index k runs over LDS rows, so each fragment is two transposing LDS reads
+    // (ds_read_b64_tr_b16) whose row sets {4g..4g+3} and {16+4g..16+4g+3} are exactly the k slots that the P
+    // registers hold — no scalar gathers
+    const int q4 = (lane >> 2) & 3, p4 = lane & 3;
+    (void)c;
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 b;
@@ -78,12 +120,10 @@ __device__ __forceinline__ void tn_reg(const T* Xs, const float (&p)[4][4], f32x
       }
 #pragma unroll
       for (int dt = 0; dt < DT; ++dt) {
-        bf16x8 a;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          a[j] = Xs[(ks * 32 + 4 * g + j) * LDT + dt * 16 + c];
-          a[4 + j] = Xs[(ks * 32 + 16 + 4 * g + j) * LDT + dt * 16 + c];
-        }
+        const T* base = Xs + (ks * 32 + 4 * g + q4) * LDT + dt * 16 + 4 * p4;
+        v4s both[2] = {__builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base)),
+                       __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(base + 16 * LDT))};
+        const bf16x8 a = *reinterpret_cast<bf16x8*>(both);
         acc[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[dt], 0, 0, 0);
       }
     }
@@ -123,11 +163,19 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* q, const T* k, c
 #pragma unroll
   for (int i = 0; i < 4; ++i) oacc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const float sl2 = scale * 1.44269504088896341f;  // exp2 domain
+  TilePrefetch<T, DQK> pk;
+  TilePrefetch<T, HD> pv;
+  pk.load(k, rowb, L, cs, ko + h * hs);
+  pv.load(v, rowb, L, cs, vo + h * hs);
   for (int k0 = 0; k0 < L; k0 += BLK) {
     __syncthreads();
-    load_rows<T, DQK>(Ks, k, rowb + k0, L - k0, cs, ko + h * hs);
-    load_rows(Vs, v, rowb + k0, L - k0, cs, vo + h * hs);
+    pk.store(Ks);
+    pv.store(Vs);
     __syncthreads();
+    if (k0 + BLK < L) {  // next key block in flight while this one is consumed
+      pk.load(k, rowb + k0 + BLK, L - k0 - BLK, cs, ko + h * hs);
+      pv.load(v, rowb + k0 + BLK, L - k0 - BLK, cs, vo + h * hs);
+    }
     float p[4][4];
     float mx = -INFINITY;
 #pragma unroll
@@ -144,13 +192,13 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* q, const T* k, c
     mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
     mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
     float mnew = fmaxf(m, mx);
-    float alpha = exp2f(m - mnew);
+    float alpha = fexp2<T>(m - mnew);
     float rs = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        float e = exp2f(p[kt][r] - mnew);
+        float e = fexp2<T>(p[kt][r] - mnew);
         p[kt][r] = e;
         rs += e;
       }
@@ -219,16 +267,29 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(const T* q, const T* k
   for (int i = 0; i < 4; ++i) dva[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int i = 0; i < KT; ++i) dka[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  TilePrefetch<T, DQK> pq;
+  TilePrefetch<T, HD> pd;
+  float nls = INFINITY, ndd = 0.f;  // thread i < 64: the next query block's lse / dvec entry i
+  auto fetch = [&](int qn) {
+    pq.load(q, rowb + qn, L - qn, cs, qo + h * hs);
+    pd.load(dout, rowb + qn, L - qn, dcs, h * HD);
+    if (threadIdx.x < BLK) {
+      const int qq = qn + threadIdx.x;
+      nls = qq < L ? lse[(long)bh * L + qq] : INFINITY;
+      ndd = qq < L ? dvec[(long)bh * L + qq] : 0.f;
+    }
+  };
+  fetch(0);
   for (int q0 = 0; q0 < L; q0 += BLK) {
     __syncthreads();
-    load_rows<T, DQK>(Qs, q, rowb + q0, L - q0, cs, qo + h * hs);
-    load_rows(Ds, dout, rowb + q0, L - q0, dcs, h * HD);
-    for (int i = threadIdx.x; i < BLK; i += 256) {
-      int qq = q0 + i;
-      ls[i] = qq < L ? lse[(long)bh * L + qq] : INFINITY;
-      dd[i] = qq < L ? dvec[(long)bh * L + qq] : 0.f;
+    pq.store(Qs);
+    pd.store(Ds);
+    if (threadIdx.x < BLK) {
+      ls[threadIdx.x] = nls;
+      dd[threadIdx.x] = ndd;
     }
     __syncthreads();
+    if (q0 + BLK < L) fetch(q0 + BLK);
     float p[4][4], ds[4][4];
 #pragma unroll
     for (int qt = 0; qt < 4; ++qt) {
@@ -238,7 +299,7 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(const T* q, const T* k
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int qi = qt * 16 + 4 * g + r;
-        float pv = __expf(s[r] * scale - ls[qi]);  // 0 for padded queries (ls = +inf)
+        float pv = fexp2<T>((s[r] * scale - ls[qi]) * LOG2E);  // 0 for padded queries (ls = +inf)
         p[qt][r] = pv;
         ds[qt][r] = pv * (dp[r] - dd[qi]);
       }
@@ -291,11 +352,19 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(const T* q, const T* k,
   f32x4 dqa[KT];
 #pragma unroll
   for (int i = 0; i < KT; ++i) dqa[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  TilePrefetch<T, DQK> pk;
+  TilePrefetch<T, HD> pv;
+  pk.load(k, rowb, L, cs, ko + h * hs);
+  pv.load(v, rowb, L, cs, vo + h * hs);
   for (int k0 = 0; k0 < L; k0 += BLK) {
     __syncthreads();
-    load_rows<T, DQK>(Ks, k, rowb + k0, L - k0, cs, ko + h * hs);
-    load_rows(Vs, v, rowb + k0, L - k0, cs, vo + h * hs);
+    pk.store(Ks);
+    pv.store(Vs);
     __syncthreads();
+    if (k0 + BLK < L) {
+      pk.load(k, rowb + k0 + BLK, L - k0 - BLK, cs, ko + h * hs);
+      pv.load(v, rowb + k0 + BLK, L - k0 - BLK, cs, vo + h * hs);
+    }
     float ds[4][4];
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt) {
@@ -305,7 +374,7 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(const T* q, const T* k,
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         int key = k0 + kt * 16 + 4 * g + r;
-        float pv = key < L ? __expf(s[r] * scale - lq) : 0.f;
+        float pv = key < L ? fexp2<T>((s[r] * scale - lq) * LOG2E) : 0.f;
         ds[kt][r] = pv * (dp[r] - dq_d);
       }
     }

@@ -10,6 +10,7 @@
 //     a constant basis built once on the host in float64), crop. Backward folds the reflected border and
 //     returns dfft[c,uv] = <B_uv, sum_patches dy x^T>.
 #include "adr_common.h"
+#include <cstdlib>
 
 namespace adr {
 
@@ -145,6 +146,26 @@ __device__ __forceinline__ void stage_img(const T* src, int cs, int H, int W, in
   }
 }
 
+// the padded image staged as fp32 in LDS (converted once, not per tap read): CB channels per pixel row
+template <typename T>
+__device__ __forceinline__ void stage_img_f32(const T* src, int cs, int H, int W, int pad, int cb0, int C, int CB,
+                                              float* dst) {
+  constexpr int VW = 16 / sizeof(T);
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad, nv = CB / VW;
+  for (int i = threadIdx.x; i < Hp * Wp * nv; i += blockDim.x) {
+    const int pp = i / nv, cv = i % nv;
+    const int yy = pp / Wp - pad, xx = pp % Wp - pad;
+    const int c = cb0 + cv * VW;
+    float f[VW];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) f[e] = 0.f;
+    if (yy >= 0 && yy < H && xx >= 0 && xx < W && c < C) vload<T, VW>(src + ((long)yy * W + xx) * cs + c, f);
+    float* d = dst + (long)pp * CB + cv * VW;
+#pragma unroll
+    for (int e = 0; e < VW; e += 4) *reinterpret_cast<f32x4*>(d + e) = (f32x4){f[e], f[e + 1], f[e + 2], f[e + 3]};
+  }
+}
+
 // y = dwconv(x, w) (+b) or dx (+)= dwconv^T(dy, w): items (pixel, VW-channel vector), taps from the LDS image
 template <typename T, bool BWD, int CB>
 __global__ void __launch_bounds__(256) dw_img_kernel(const T* x, int xcs, const float* w, const float* b, T* y,
@@ -193,30 +214,28 @@ __global__ void __launch_bounds__(256) dw_img_kernel(const T* x, int xcs, const 
   }
 }
 
-// weight gradient: items (tap, VW-channel vector, pixel split PS), partial sums combined in LDS in fixed order;
-// partial[n][t][c]
+// weight gradient: items (tap, 4-channel group, pixel split PS) over fp32 copies of the padded image and of dy
+// in LDS (converted once at staging), partial sums combined in LDS in fixed order; partial[n][t][c]
 template <typename T, int CB>
 __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, const T* dy, int dcs, int H, int W,
                                                            int C, int k, float* partial) {
-  constexpr int VW = 16 / sizeof(T), NV = CB / VW;
+  constexpr int NV = CB / 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
   const int n = blockIdx.x, cb0 = blockIdx.y * CB, p = k / 2, kk = k * k;
   const int Hp = H + 2 * p, Wp = W + 2 * p;
-  T* xs = reinterpret_cast<T*>(dwsm);
-  T* ds = xs + (long)Hp * Wp * CB;
-  float* red = reinterpret_cast<float*>(ds + (long)H * W * CB);  // [256][VW]
-  stage_img<T>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
-  stage_img<T>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
+  float* xs = reinterpret_cast<float*>(dwsm);
+  float* ds = xs + (long)Hp * Wp * CB;
+  float* red = ds + (long)H * W * CB;  // [256][4]
+  stage_img_f32<T>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
+  stage_img_f32<T>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
   __syncthreads();
   const int pairs = kk * NV;
-  int PS = 1;  // pixel splits per (tap, vector): a power of two, so split groups never straddle a 256 pass
+  int PS = 1;  // pixel splits per (tap, group): a power of two, so split groups never straddle a 256 pass
   while (PS * 2 * pairs <= 256) PS *= 2;
   for (int base = 0; base < pairs * PS; base += 256) {
     const int it = base + threadIdx.x;
     const int pr = it / PS, ps = it % PS;
-    float acc[VW];
-#pragma unroll
-    for (int e = 0; e < VW; ++e) acc[e] = 0.f;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     if (pr < pairs) {
       const int t = pr / NV, cv = pr % NV, ky = t / k, kx = t % k;
       int oy = 0, ox = ps;  // (oy, ox) of pix, stepped by PS without dividing
@@ -225,12 +244,9 @@ __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, 
         ++oy;
       }
       for (int pix = ps; pix < H * W; pix += PS) {
-        const u32x4 dv = *reinterpret_cast<const u32x4*>(ds + (long)pix * CB + cv * VW);
-        const u32x4 xv = *reinterpret_cast<const u32x4*>(xs + ((long)(oy + ky) * Wp + ox + kx) * CB + cv * VW);
-        const T* d8 = reinterpret_cast<const T*>(&dv);
-        const T* x8 = reinterpret_cast<const T*>(&xv);
-#pragma unroll
-        for (int e = 0; e < VW; ++e) acc[e] += to_f(d8[e]) * to_f(x8[e]);
+        const f32x4 d4 = *reinterpret_cast<const f32x4*>(ds + (long)pix * CB + cv * 4);
+        const f32x4 x4 = *reinterpret_cast<const f32x4*>(xs + ((long)(oy + ky) * Wp + ox + kx) * CB + cv * 4);
+        acc += d4 * x4;
         ox += PS;
         while (ox >= W) {
           ox -= W;
@@ -238,15 +254,14 @@ __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, 
         }
       }
     }
-#pragma unroll
-    for (int e = 0; e < VW; ++e) red[threadIdx.x * VW + e] = acc[e];
+    *reinterpret_cast<f32x4*>(red + threadIdx.x * 4) = acc;
     __syncthreads();
     if (ps == 0 && pr < pairs) {
-      const int t = pr / NV, cv = pr % NV, c = cb0 + cv * VW;
+      const int t = pr / NV, cv = pr % NV, c = cb0 + cv * 4;
 #pragma unroll
-      for (int e = 0; e < VW; ++e) {
+      for (int e = 0; e < 4; ++e) {
         float s2 = 0.f;
-        for (int q = 0; q < PS; ++q) s2 += red[(threadIdx.x + q) * VW + e];
+        for (int q = 0; q < PS; ++q) s2 += red[(threadIdx.x + q) * 4 + e];
         if (c + e < C) partial[((long)n * kk + t) * C + c + e] = s2;
       }
     }
@@ -794,22 +809,43 @@ using namespace adr;
     else hipLaunchKernelGGL(KERN<float>, grid, block, sm, st, __VA_ARGS__);                             \
   } while (0)
 
-static constexpr int DW_CB_BF16 = 16, DW_CB_F32 = 8;
-static size_t dw_img_smem(int dtype, int H, int W, int k) {  // weight-gradient kernel
+static constexpr int DW_CB_BF16 = 16, DW_CB_F32 = 8, DW_CB_WG = 8;  // DW_CB_WG: weight-gradient channel slab
+// channel slab of the bf16 whole-image forward / data-gradient kernel (ADR_DW_CB=32 selects 32 for A/B runs)
+static int dw_cb_fwd() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ADR_DW_CB");
+    v = e && atoi(e) == 32 ? 32 : DW_CB_BF16;
+  }
+  return v;
+}
+// ADR_DW_IMG=0 routes the forward / data gradient to the direct (global-load) kernel for A/B runs
+static bool dw_img_ok() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ADR_DW_IMG");
+    v = e ? atoi(e) != 0 : 1;
+  }
+  return v != 0;
+}
+static size_t dw_img_smem(int dtype, int H, int W, int k) {  // weight-gradient kernel (fp32 copies in LDS)
+  (void)dtype;
   const int p = k / 2;
-  const size_t cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
-  return ((size_t)(H + 2 * p) * (W + 2 * p) + (size_t)H * W) * cb * es + 256 * 16;
+  return ((size_t)(H + 2 * p) * (W + 2 * p) + (size_t)H * W) * DW_CB_WG * 4 + 256 * 16;
 }
 static size_t dw_fwd_smem(int dtype, int H, int W, int k) {  // forward / data-gradient kernel
   const int p = k / 2;
-  const size_t cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
+  const size_t cb = dtype == ADR_BF16 ? dw_cb_fwd() : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
   return (size_t)k * k * cb * 4 + (size_t)(H + 2 * p) * (W + 2 * p) * cb * es;
 }
 template <bool BWD>
 static void dw_img_launch(int dtype, hipStream_t st, const void* x, int xcs, const float* w, const float* b, void* y,
                           int ycs, int N, int H, int W, int C, int k, int acc) {
   const size_t sm = dw_fwd_smem(dtype, H, W, k);
-  if (dtype == ADR_BF16)
+  if (dtype == ADR_BF16 && dw_cb_fwd() == 32)
+    hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, 32>), dim3(N, cdiv(C, 32)), dim3(256), sm, st, (const __bf16*)x,
+                       xcs, w, b, (__bf16*)y, ycs, H, W, C, k, acc);
+  else if (dtype == ADR_BF16)
     hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
                        (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, H, W, C, k, acc);
   else
@@ -838,7 +874,7 @@ extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w,
   long total = (long)N * H * W * (C / v);
   size_t sm = (size_t)k * k * C * sizeof(float);
   ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
-  if (dw_fwd_smem(dtype, H, W, k) <= 64 * 1024 && xcs % v == 0 && ycs % v == 0) {
+  if (dw_img_ok() && dw_fwd_smem(dtype, H, W, k) <= 64 * 1024 && xcs % v == 0 && ycs % v == 0) {
     dw_img_launch<false>(dtype, st, x, xcs, w, b, y, ycs, N, H, W, C, k, 0);
   } else if (dtype == ADR_BF16)
     dw_launch<__bf16, false>(k, dim3(cdiv(total, 256)), sm, st, (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, N, H, W,
@@ -866,7 +902,7 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
   if (dx) {
     size_t sm = (size_t)k * k * C * sizeof(float);
     ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv_bwd: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
-    if (dw_fwd_smem(dtype, H, W, k) <= 64 * 1024 && dcs % v == 0 && ocs % v == 0)
+    if (dw_img_ok() && dw_fwd_smem(dtype, H, W, k) <= 64 * 1024 && dcs % v == 0 && ocs % v == 0)
       dw_img_launch<true>(dtype, st, dy, dcs, w, nullptr, dx, ocs, N, H, W, C, k, accumulate);
     else if (dtype == ADR_BF16)
       dw_launch<__bf16, true>(k, dim3(cdiv(total, 256)), sm, st, (const __bf16*)dy, dcs, w, nullptr, (__bf16*)dx, ocs, N,
@@ -884,10 +920,10 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
     if (ism <= 64 * 1024 && xcs % v == 0 && dcs % v == 0) {  // small maps (the 20x20 C2PTSSA / EDFFN / Mona path): whole image in LDS
       chunks = N;
       if (dtype == ADR_BF16)
-        hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), ism, st,
+        hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, DW_CB_WG>), dim3(N, cdiv(C, DW_CB_WG)), dim3(256), ism, st,
                            (const __bf16*)x, xcs, (const __bf16*)dy, dcs, H, W, C, k, ws);
       else
-        hipLaunchKernelGGL((dw_wgrad_img_kernel<float, DW_CB_F32>), dim3(N, cdiv(C, DW_CB_F32)), dim3(256), ism, st,
+        hipLaunchKernelGGL((dw_wgrad_img_kernel<float, DW_CB_WG>), dim3(N, cdiv(C, DW_CB_WG)), dim3(256), ism, st,
                            (const float*)x, xcs, (const float*)dy, dcs, H, W, C, k, ws);
     } else if (dtype == ADR_BF16)
       hipLaunchKernelGGL(dw_bwd_w_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dy, dcs, N,
