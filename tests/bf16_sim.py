@@ -41,8 +41,10 @@ class _Bf16F(types.ModuleType):
 
 
 def oracle_forward(P, cfg, x, train, bf16):
-    """O.forward on the parsed yaml, with bf16 rounding of every functional op's output when bf16."""
-    layers, save = O.parse(yaml.safe_load(open(cfg).read()), 3, None)
+    """O.forward on the parsed yaml (a path or an already-loaded dict), with bf16 rounding of every functional
+    op's output when bf16."""
+    d = cfg if isinstance(cfg, dict) else yaml.safe_load(open(cfg).read())
+    layers, save = O.parse(d, 3, None)
     prev = O.F
     O.F = _Bf16F("F") if bf16 else Freal
     try:
