@@ -192,7 +192,11 @@ def main():
     ap.add_argument("--infer", action="store_true", help="measure BASELINE.json configs[1] (batched inference) only")
     ap.add_argument("--infer-bs", type=int, default=32)
     ap.add_argument("--infer-steps", type=int, default=20)
+    ap.add_argument("--scale", default="n", choices=["n", "s", "m", "l", "x"],
+                    help="model scale of the 701 yaml (configs[4] = l at 1280^2, bs 16/GPU)")
     args = ap.parse_args()
+    if args.scale != "n":  # configs[4]: its own line; the n/640 baselines (CPU, inference) do not apply
+        args.no_cpu_baseline, args.infer_steps = True, 0
 
     import torch
     import torch.distributed as dist
@@ -211,7 +215,13 @@ def main():
 
     dtype = torch.bfloat16 if args.dtype == "bf16" else torch.float32
     torch.manual_seed(0)
-    model = DetectionModel(str(CFG), compute_dtype=dtype).to(dev)
+    if args.scale == "n":
+        model = DetectionModel(str(CFG), compute_dtype=dtype).to(dev)
+    else:
+        import yaml
+        cfg = yaml.safe_load(CFG.read_text())
+        cfg["scale"] = args.scale
+        model = DetectionModel(cfg, compute_dtype=dtype).to(dev)
     if args.infer:
         ips, ms, roof, dets = infer_bench(model, args.infer_bs, args.img, args.steps, args.warmup, dev,
                                           graph=not args.no_graph, roofline=True)
@@ -280,9 +290,13 @@ def main():
         roof = K.roofline_report(ktimes, dtype, HBM_PEAK_GBS, mfma_peak)
         if roof is not None:
             roof["traffic"], roof["traffic_source"] = pmc_traffic(roof["kernel"])
-            roof["network"] = {"bytes_per_img": NET_BYTES_PER_IMG, "flops_per_img": NET_FLOPS_PER_IMG,
-                               "hbm_frac": round(ips * NET_BYTES_PER_IMG / (HBM_PEAK_GBS * 1e9), 4),
-                               "mfma_frac": round(ips * NET_FLOPS_PER_IMG / (mfma_peak * 1e12), 4)}
+            if args.scale == "n" and args.img == 640:
+                roof["network"] = {"bytes_per_img": NET_BYTES_PER_IMG, "flops_per_img": NET_FLOPS_PER_IMG,
+                                   "hbm_frac": round(ips * NET_BYTES_PER_IMG / (HBM_PEAK_GBS * 1e9), 4),
+                                   "mfma_frac": round(ips * NET_FLOPS_PER_IMG / (mfma_peak * 1e12), 4)}
+            elif args.scale == "l" and args.img == 1280:  # 765.6 GFLOP fwd per image, bwd = 2x fwd
+                roof["network"] = {"flops_per_img": 3 * 765.6e9,
+                                   "mfma_frac": round(ips * 3 * 765.6e9 / (mfma_peak * 1e12), 4)}
             roof["conv_family"] = conv_attainable(K.timing_detail(), HBM_PEAK_GBS, mfma_peak)
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(budget_s=args.cpu_budget)
         infer = None
@@ -294,12 +308,13 @@ def main():
                      "pipeline": "uint8 -> eval fwd (bf16) -> DFL decode -> NMS(0.25, 0.7, 300), one hipGraph",
                      "detections_per_batch": dets}
         out = {
-            "metric": "images/sec whole-node (640x640) fwd+bwd, YOLO-AD-Refine-n at 1/2/4/8 GPU",
+            "metric": ("images/sec whole-node (640x640) fwd+bwd, YOLO-AD-Refine-n at 1/2/4/8 GPU" if args.scale == "n"
+                       else f"images/sec whole-node ({args.img}x{args.img}) fwd+bwd, YOLO-AD-Refine-{args.scale}"),
             "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
             "data": "synthetic (uint8 images + COCO-shape labels)" if not args.float_images else "synthetic (fp32 images)",
-            "config": {"workload": f"yolo11-701-YOLO-AD-Refine.yaml (n) train step bs={args.bs}/GPU "
+            "config": {"workload": f"yolo11-701-YOLO-AD-Refine.yaml ({args.scale}) train step bs={args.bs}/GPU "
                                    f"{args.img}x{args.img}, synthetic COCO-shape labels, TAL+DFL+CIoU/NWD loss, "
                                    f"SGD+EMA", "global_batch": world * args.bs, "img": args.img,
                        "parallelism": f"dp{world}"},

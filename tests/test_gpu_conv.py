@@ -136,10 +136,11 @@ def test_conv_transpose_fixture(dtype):
     assert abs(float(m.bias.grad.norm()) - ref["bias"]) <= tol["rtol"] * ref["bias"]
 
 
-@pytest.mark.parametrize("S,K", [(64, 16), (40, 32)])
+@pytest.mark.parametrize("S,K", [(64, 16), (40, 32), (1280, 64), (1000, 64)])
 def test_stem_from_image(S, K):
     """model.0 Conv(3, K, 3, 2) through the stem kernels (fp32 NCHW image in, bf16 compute) against the generic
-    path (image_to_nhwc + implicit GEMM): pre-BN output, BN statistics (via the BN'd output), weight gradient."""
+    path (image_to_nhwc + implicit GEMM): pre-BN output, BN statistics (via the BN'd output), weight gradient.
+    1280 / 1000 (the l-scale configs[4] width) take the column-segmented weight-gradient plan."""
     from adrefine import kernels as Kn
     from adrefine.nn.modules import Conv
     torch.manual_seed(0)

@@ -95,21 +95,37 @@ __device__ __forceinline__ void stage_rows(const float* __restrict__ img, int n,
 // weight gradient partials: block per (image, pair of output rows); the 5 input rows it needs (3 channels,
 // columns -1..W zero-padded) and its dy rows are staged in LDS as bf16, then 4 waves run the MFMA steps over
 // the block's 2*Wo pixels (32 per step). part[block][KT*16][32].
+// Wide images (the l-scale 1280^2 configuration) split each row pair into column segments of wseg output columns
+// (segs per row pair) so the staged rows fit the LDS plan; segs == 1 is the whole row.
+template <int IR, typename TI>
+__device__ __forceinline__ void stage_cols(const TI* __restrict__ img, int n, int H, int W, int iy0, int ix0, int Wc,
+                                           int Wp, __bf16* xs) {
+  for (int q = threadIdx.x; q < 3 * IR * Wc; q += blockDim.x) {
+    const int row = q / Wc, col = q - row * Wc;
+    const int c = row / IR, iy = iy0 + row % IR, ix = ix0 + col;
+    const bool ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+    xs[row * Wp + col] = (__bf16)(ok ? img_val(img[(((long)n * 3 + c) * H + iy) * W + ix]) : 0.f);
+  }
+}
+
 template <int KT, typename TI>
 __global__ void __launch_bounds__(256) stem_wgrad_kernel(const TI* __restrict__ img, int H, int W,
                                                          const __bf16* __restrict__ dy, int dcs, int Ho, int Wo,
-                                                         float* __restrict__ part) {
+                                                         int segs, int wseg, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
   constexpr int IR = 2 * STEM_ROWS + 1;  // input rows
-  const int Wp = W + 2;
+  const int Wp = segs == 1 ? W + 2 : 2 * wseg + 2;
   __bf16* xs = reinterpret_cast<__bf16*>(smraw);                 // [3][IR][Wp]
-  __bf16* ds = xs + ((3 * IR * Wp + 7) & ~7);                    // [STEM_ROWS * Wo][KT * 16]
-  float* red = reinterpret_cast<float*>(ds + (long)STEM_ROWS * Wo * KT * 16);  // [4][KT*16][32]
-  const int rb = blockIdx.x % ((Ho + STEM_ROWS - 1) / STEM_ROWS), n = blockIdx.x / ((Ho + STEM_ROWS - 1) / STEM_ROWS);
+  __bf16* ds = xs + ((3 * IR * Wp + 7) & ~7);                    // [STEM_ROWS * wseg][KT * 16]
+  float* red = reinterpret_cast<float*>(ds + (long)STEM_ROWS * wseg * KT * 16);  // [4][KT*16][32]
+  const int nrb = (Ho + STEM_ROWS - 1) / STEM_ROWS;
+  const int seg = blockIdx.x % segs, rb = (blockIdx.x / segs) % nrb, n = blockIdx.x / segs / nrb;
   const int oy0 = rb * STEM_ROWS, nrow = min(STEM_ROWS, Ho - oy0), iy0 = 2 * oy0 - 1;
-  stage_rows<IR>(img, n, H, W, iy0, xs);
-  const int npx = nrow * Wo;
-  const __bf16* dyb = dy + ((long)n * Ho + oy0) * Wo * (long)dcs;
+  const int ox0 = seg * wseg, nox = min(wseg, Wo - ox0);
+  if (segs == 1) stage_rows<IR>(img, n, H, W, iy0, xs);
+  else stage_cols<IR>(img, n, H, W, iy0, 2 * ox0 - 1, 2 * nox + 1, Wp, xs);
+  const int npx = nrow * nox;
+  const __bf16* dyb = dy + (((long)n * Ho + oy0) * Wo + ox0) * (long)dcs;
   {  // 16-byte chunks of 8 channels, four loads in flight per thread
     const int nch = npx * KT * 2;
     for (int i0 = threadIdx.x; i0 < nch; i0 += 4 * 256) {
@@ -117,7 +133,8 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const TI* __restrict__ 
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int i = i0 + u * 256;
-        if (i < nch) v[u] = ld16(dyb + (long)(i / (KT * 2)) * dcs + (i % (KT * 2)) * 8);
+        const int px = i / (KT * 2), pr = px / nox;  // segment pixel -> (row, column) of the dy image
+        if (i < nch) v[u] = ld16(dyb + ((long)pr * Wo + (px - pr * nox)) * dcs + (i % (KT * 2)) * 8);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
@@ -146,7 +163,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const TI* __restrict__ 
   const int nsteps = (npx + 31) / 32;
   for (int s = wave; s < nsteps; s += 4) {
     const int pbase = s * 32 + 8 * g;
-    int r = pbase / Wo, ox = pbase - r * Wo;
+    int r = pbase / nox, ox = pbase - r * nox;
     s16x8 a[KT], b[2];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -162,7 +179,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const TI* __restrict__ 
                                           : (__bf16)0.f;
         b[jt][e] = *reinterpret_cast<const short*>(&v);
       }
-      if (++ox == Wo) {
+      if (++ox == nox) {
         ox = 0;
         ++r;
       }
@@ -187,10 +204,23 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const TI* __restrict__ 
   }
 }
 
-static size_t stem_wgrad_smem(int W, int Wo, int KT) {
+static size_t stem_wgrad_smem(int Wp, int wseg, int KT) {
   const int IR = 2 * STEM_ROWS + 1;
-  return (((size_t)3 * IR * (W + 2) + 7) & ~(size_t)7) * 2 + (size_t)STEM_ROWS * Wo * KT * 16 * 2 +
+  return (((size_t)3 * IR * Wp + 7) & ~(size_t)7) * 2 + (size_t)STEM_ROWS * wseg * KT * 16 * 2 +
          (size_t)4 * KT * 16 * 32 * 4;
+}
+
+// column plan of the weight gradient: (segments per row pair, output columns per segment) within 64 KB of LDS
+static void stem_wgrad_plan(int W, int Wo, int KT, int* segs, int* wseg) {
+  if (stem_wgrad_smem(W + 2, Wo, KT) <= 64 * 1024) {
+    *segs = 1;
+    *wseg = Wo;
+    return;
+  }
+  int ws = (Wo + 15) / 16 * 16;
+  while (ws > 16 && stem_wgrad_smem(2 * ws + 2, ws, KT) > 64 * 1024) ws -= 16;
+  *wseg = ws;
+  *segs = (Wo + ws - 1) / ws;
 }
 
 // forward on MFMA: block per (image, pair of output rows), image rows staged in LDS exactly as for the weight
@@ -339,8 +369,10 @@ extern "C" int adr_stem_conv_fwd_u8(const uint8_t* img, int N, int H, int W, con
 }
 
 extern "C" size_t adr_stem_wgrad_workspace(int N, int H, int W, int K) {
-  const int Ho = (H - 1) / 2 + 1;
-  const long blocks = (long)N * ((Ho + STEM_ROWS - 1) / STEM_ROWS);
+  const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
+  int segs, wseg;
+  stem_wgrad_plan(W, Wo, K / 16 > 0 ? K / 16 : 1, &segs, &wseg);
+  const long blocks = (long)N * ((Ho + STEM_ROWS - 1) / STEM_ROWS) * segs;
   return (size_t)blocks * K * 32 * sizeof(float);
 }
 
@@ -351,20 +383,22 @@ static int stem_wgrad(const TI* img, int N, int H, int W, const void* dy, int dc
               "stem_conv_wgrad: N=%d H=%d W=%d K=%d", N, H, W, K);
   ADR_REQUIRE(ws_bytes >= adr_stem_wgrad_workspace(N, H, W, K), "stem_conv_wgrad: workspace");
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
-  const int blocks = N * ((Ho + STEM_ROWS - 1) / STEM_ROWS);
   const int KT = K / 16;
-  const size_t sm = stem_wgrad_smem(W, Wo, KT);
+  int segs, wseg;
+  stem_wgrad_plan(W, Wo, KT, &segs, &wseg);
+  const int blocks = N * ((Ho + STEM_ROWS - 1) / STEM_ROWS) * segs;
+  const size_t sm = stem_wgrad_smem(segs == 1 ? W + 2 : 2 * wseg + 2, wseg, KT);
   ADR_REQUIRE(sm <= 64 * 1024 && dcs % 8 == 0, "stem_conv_wgrad: W=%d too wide for the LDS plan", W);
   hipStream_t st = (hipStream_t)stream;
   if (K == 16)
     hipLaunchKernelGGL((stem_wgrad_kernel<1, TI>), dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs,
-                       Ho, Wo, ws);
+                       Ho, Wo, segs, wseg, ws);
   else if (K == 32)
     hipLaunchKernelGGL((stem_wgrad_kernel<2, TI>), dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs,
-                       Ho, Wo, ws);
+                       Ho, Wo, segs, wseg, ws);
   else
     hipLaunchKernelGGL((stem_wgrad_kernel<4, TI>), dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs,
-                       Ho, Wo, ws);
+                       Ho, Wo, segs, wseg, ws);
   hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(K * 27), dim3(256), 0, st, ws, blocks, K, dw, accumulate);
   return check_launch("adr_stem_conv_wgrad");
 }

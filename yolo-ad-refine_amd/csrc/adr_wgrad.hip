@@ -547,6 +547,12 @@ static void launch_bm(int bn, dim3 grid, const WgArgs& g, hipStream_t st) {
 }
 
 // tiles, k-step rows and split count for a bf16 WGRAD; splits bounded so the fp32 partials stay small
+// (ADR_WG_PART_MB / ADR_WG3_PART_MB override the per-conv partial budgets of the generic / 3x3-halo plans, A/B only)
+static long part_budget(const char* var, long def_mb) {
+  const char* e = getenv(var);
+  const long v = e ? atol(e) : def_mb;
+  return (v > 0 ? v : def_mb) << 20;
+}
 
 WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   WgPlan p;
@@ -577,7 +583,8 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
     p.tiles = (d->k / p.bm) * (d->c / 32);
     long s = (768 + p.tiles - 1) / p.tiles;                      // ~3 workgroups per CU
     const long by_work = ntile / 4;                              // >= 4 tiles per split
-    const long by_bytes = (64l << 20) / ((long)d->k * 9 * d->c * 4);
+    static const long b3 = part_budget("ADR_WG3_PART_MB", 64);
+    const long by_bytes = b3 / ((long)d->k * 9 * d->c * 4);
     if (s > by_work) s = by_work;
     if (s > by_bytes) s = by_bytes;
     if (s < 1) s = 1;
@@ -595,7 +602,8 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   p.tiles = cdiv(d->k, p.bm) * d->r * d->s * cdiv(d->c, p.bn);
   long s = (1024 + p.tiles - 1) / p.tiles;                  // ~4 workgroups per CU
   const long by_work = red / ((long)p.R * 8);               // >= 8 k-steps per split
-  const long by_bytes = (24l << 20) / (outsz * 4);          // <= 24 MB of partials (stays in L2/MALL)
+  static const long bg = part_budget("ADR_WG_PART_MB", 24);
+  const long by_bytes = bg / (outsz * 4);                   // <= 24 MB of partials (stays in L2/MALL)
   if (s > by_work) s = by_work;
   if (s > by_bytes) s = by_bytes;
   if (s < 1) s = 1;
