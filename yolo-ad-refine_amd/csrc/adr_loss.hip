@@ -30,6 +30,13 @@ struct Levels {
   int A;
 };
 
+// Levels is a by-value kernel argument: indexing its arrays with a run-time level would copy the struct to scratch
+// memory, so every per-level field is picked with selects
+template <typename V>
+__device__ __forceinline__ V lsel(const V (&v)[3], int lvl) {
+  return lvl == 0 ? v[0] : (lvl == 1 ? v[1] : v[2]);
+}
+
 __device__ __forceinline__ void anchor_of(const Levels& L, int a, int& lvl, int& loc) {
   int n0 = L.H[0] * L.W[0], n1 = L.H[1] * L.W[1];
   if (a < n0) { lvl = 0; loc = a; }
@@ -41,10 +48,15 @@ template <typename T>
 __device__ __forceinline__ const T* feat_row(const Levels& L, int b, int a, int& lvl, float& ax, float& ay) {
   int loc;
   anchor_of(L, a, lvl, loc);
-  int W = L.W[lvl], HW = L.H[lvl] * W;
+  const int W = lsel(L.W, lvl), HW = lsel(L.H, lvl) * W;
   ax = (float)(loc % W) + 0.5f;
   ay = (float)(loc / W) + 0.5f;
-  return reinterpret_cast<const T*>(L.f[lvl]) + ((long)b * HW + loc) * L.cs[lvl];
+  return reinterpret_cast<const T*>(lsel(L.f, lvl)) + ((long)b * HW + loc) * lsel(L.cs, lvl);
+}
+
+// v[k] for a run-time k < 4 without a scratch copy of v
+__device__ __forceinline__ float pick4(const float* v, int k) {
+  return k == 0 ? v[0] : (k == 1 ? v[1] : (k == 2 ? v[2] : v[3]));
 }
 
 // CIoU value (metrics.py:74-125, xywh=False, CIoU=True, eps=1e-7); box = x1, y1, x2, y2
@@ -135,6 +147,36 @@ __device__ __forceinline__ float nwd(const float* a, const float* b, float* g) {
   return r;
 }
 
+// 8 consecutive row elements <-> fp32 (one 16-byte access for bf16, two for fp32)
+template <typename T>
+__device__ __forceinline__ void load8(const T* p, float* v) {
+  if constexpr (sizeof(T) == 2) {
+    u32x4 r = ld16(p);
+    const T* e = reinterpret_cast<const T*>(&r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = to_f(e[k]);
+  } else {
+    u32x4 r0 = ld16(p), r1 = ld16(p + 4);
+    const float* a = reinterpret_cast<const float*>(&r0);
+    const float* b = reinterpret_cast<const float*>(&r1);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[k] = a[k]; v[4 + k] = b[k]; }
+  }
+}
+template <typename T>
+__device__ __forceinline__ void store8(T* p, const float* v) {
+  if constexpr (sizeof(T) == 2) {
+    u32x4 r;
+    T* e = reinterpret_cast<T*>(&r);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = from_f<T>(v[k]);
+    st16(p, r);
+  } else {
+    st16(p, *reinterpret_cast<const u32x4*>(v));
+    st16(p + 4, *reinterpret_cast<const u32x4*>(v + 4));
+  }
+}
+
 // ---- decode ----
 template <typename T>
 __global__ void __launch_bounds__(256) loss_decode_kernel(Levels L, int B, float* pbox) {
@@ -145,12 +187,21 @@ __global__ void __launch_bounds__(256) loss_decode_kernel(Levels L, int B, float
   float ax, ay;
   const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
   float d[4];
+  float lg[4][RM];  // the row's 64 box logits, 16-byte loads all issued before use
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    load8<T>(p + k * RM, lg[k]);
+    load8<T>(p + k * RM + 8, lg[k] + 8);
+  }
+#pragma unroll
   for (int k = 0; k < 4; ++k) {
     float mx = -INFINITY;
-    for (int j = 0; j < RM; ++j) mx = fmaxf(mx, to_f(p[k * RM + j]));
+#pragma unroll
+    for (int j = 0; j < RM; ++j) mx = fmaxf(mx, lg[k][j]);
     float z = 0.f, e = 0.f;
+#pragma unroll
     for (int j = 0; j < RM; ++j) {
-      float ex = expf(to_f(p[k * RM + j]) - mx);
+      float ex = expf(lg[k][j] - mx);
       z += ex;
       e += ex * (float)j;
     }
@@ -180,7 +231,7 @@ __global__ void __launch_bounds__(256) tal_metrics_kernel(Levels L, int B, int n
   int lvl;
   float ax, ay;
   const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
-  float st = L.st[lvl];
+  float st = lsel(L.st, lvl);
   float px = ax * st, py = ay * st;
   float dmin = fminf(fminf(px - gb[0], py - gb[1]), fminf(gb[2] - px, gb[3] - py));
   bool in = dmin > 1e-9f;
@@ -254,9 +305,21 @@ __global__ void __launch_bounds__(256) tal_topk_kernel(const float* align, uint8
     }
   }
   __builtin_amdgcn_wave_barrier();
+  // the scan's only loop-carried state is the heap (LDS): the align rows are read PF chunks ahead, so each step
+  // waits on an LDS read of the heap top instead of a global load
+  constexpr int PF = 8;
+  float pre[PF];
+#pragma unroll
+  for (int u = 0; u < PF; ++u) {
+    const int a = TOPK + 64 * u + lane;
+    pre[u] = a < A ? m[a] : -INFINITY;
+  }
   for (int a0 = TOPK; a0 < A; a0 += 64) {
-    const int a = a0 + lane;
-    const float v = a < A ? m[a] : -INFINITY;
+    const float v = pre[0];
+#pragma unroll
+    for (int u = 0; u + 1 < PF; ++u) pre[u] = pre[u + 1];
+    const int an = a0 + 64 * PF + lane;
+    pre[PF - 1] = an < A ? m[an] : -INFINITY;
     unsigned long long cand = __ballot(v > h[0].v);
     while (cand) {
       const int j = __ffsll((long long)cand) - 1;
@@ -351,7 +414,7 @@ __global__ void __launch_bounds__(256) loss_fg_kernel(Levels L, int B, int nmax,
       int lvl;
       float ax, ay;
       const T* p = feat_row<T>(L, b, a, lvl, ax, ay);
-      float st = L.st[lvl];
+      float st = lsel(L.st, lvl);
       const float* g = gt + r * 5;
       float tb[4] = {g[1] / st, g[2] / st, g[3] / st, g[4] / st};
       const float* pb = pbox + i * 4;
@@ -397,14 +460,23 @@ __global__ void __launch_bounds__(256) loss_fg_kernel(Levels L, int B, int nmax,
 template <int Q>
 __device__ __forceinline__ void reduce_partials(const float* part, int nblk, double* out) {
   __shared__ double sh[Q][256];
-  double s[Q];
+  // four rows in flight per thread (independent accumulators, combined in a fixed order)
+  double s[4][Q];
 #pragma unroll
-  for (int q = 0; q < Q; ++q) s[q] = 0.0;
-  for (int k = threadIdx.x; k < nblk; k += 256)
+  for (int u = 0; u < 4; ++u)
 #pragma unroll
-    for (int q = 0; q < Q; ++q) s[q] += part[(long)k * Q + q];
+    for (int q = 0; q < Q; ++q) s[u][q] = 0.0;
+  int k = threadIdx.x;
+  for (; k + 768 < nblk; k += 1024)
 #pragma unroll
-  for (int q = 0; q < Q; ++q) sh[q][threadIdx.x] = s[q];
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) s[u][q] += part[(long)(k + 256 * u) * Q + q];
+  for (; k < nblk; k += 256)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) s[0][q] += part[(long)k * Q + q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) sh[q][threadIdx.x] = (s[0][q] + s[1][q]) + (s[2][q] + s[3][q]);
   __syncthreads();
   for (int o = 128; o > 0; o >>= 1) {
     if (threadIdx.x < o)
@@ -431,36 +503,6 @@ __global__ void __launch_bounds__(256) loss_scalars_kernel(const float* part, in
   scal[3] = (float)s[2];
   scal[4] = (float)s[3];
   scal[5] = (float)s[5];
-}
-
-// 8 consecutive row elements <-> fp32 (one 16-byte access for bf16, two for fp32)
-template <typename T>
-__device__ __forceinline__ void load8(const T* p, float* v) {
-  if constexpr (sizeof(T) == 2) {
-    u32x4 r = ld16(p);
-    const T* e = reinterpret_cast<const T*>(&r);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = to_f(e[k]);
-  } else {
-    u32x4 r0 = ld16(p), r1 = ld16(p + 4);
-    const float* a = reinterpret_cast<const float*>(&r0);
-    const float* b = reinterpret_cast<const float*>(&r1);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) { v[k] = a[k]; v[4 + k] = b[k]; }
-  }
-}
-template <typename T>
-__device__ __forceinline__ void store8(T* p, const float* v) {
-  if constexpr (sizeof(T) == 2) {
-    u32x4 r;
-    T* e = reinterpret_cast<T*>(&r);
-#pragma unroll
-    for (int k = 0; k < 8; ++k) e[k] = from_f<T>(v[k]);
-    st16(p, r);
-  } else {
-    st16(p, *reinterpret_cast<const u32x4*>(v));
-    st16(p + 4, *reinterpret_cast<const u32x4*>(v + 4));
-  }
 }
 
 // ---- cls pass + gradient rows. 16 lanes per anchor row: lanes 0..11 each own 8 class channels (BCE x SlideLoss
@@ -518,10 +560,20 @@ __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, 
           const float t = (c0 + k == lab) ? nrm : 0.f;
           // one exponential per logit: e = exp(-|x|) gives both the stable softplus term and the sigmoid
           const float e = __expf(-fabsf(x[k]));
-          const float bce = fmaxf(x[k], 0.f) - x[k] * t + log1pf(e);
+          float l1p, r1;
+          if constexpr (sizeof(T) == 2) {
+            // bf16 mode: log1p(e) = log(u) * e / (u - 1) with u = 1 + e (exact where u == 1) on the hardware log,
+            // and the sigmoid's reciprocal on v_rcp — the fp32 parity mode keeps log1pf and the IEEE divide
+            const float u = 1.f + e;
+            l1p = u == 1.f ? e : __logf(u) * e * __builtin_amdgcn_rcpf(u - 1.f);
+            r1 = __builtin_amdgcn_rcpf(u);
+          } else {
+            l1p = log1pf(e);
+            r1 = 1.f / (1.f + e);
+          }
+          const float bce = fmaxf(x[k], 0.f) - x[k] * t + l1p;
           const float mod = (t <= mu - 0.1f) ? 1.f : ((t < mu) ? e21 : __expf(-(t - 1.f)));
           acc += bce * mod;
-          const float r1 = 1.f / (1.f + e);
           const float sg = x[k] >= 0.f ? r1 : e * r1;
           g[k] = (sg - t) * mod * cscale;
         }
@@ -533,7 +585,7 @@ __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, 
 #pragma unroll
       for (int q = 0; q < RM; ++q) gl[q] = 0.f;
       if (isfg) {
-        const float st = L.st[lvl];
+        const float st = lsel(L.st, lvl);
         const float* gg = gt + r * 5;
         const float tb[4] = {gg[1] / st, gg[2] / st, gg[3] / st, gg[4] / st};
         const float* pb = pbox + i * 4;
@@ -543,7 +595,7 @@ __global__ void __launch_bounds__(256) loss_cls_grad_kernel(Levels L, Levels G, 
         nwd(pbv, tb, gn);
         const float wb = gscale * box_gain * 0.5f * nrm / tss;
         // d/d dist: x1 = ax - d0, y1 = ay - d1, x2 = ax + d2, y2 = ay + d3
-        const float gbk = -wb * (gc[k] + gn[k]);
+        const float gbk = -wb * (pick4(gc, k) + pick4(gn, k));
         const float gdk = (k < 2) ? -gbk : gbk;
         const float tt = (k == 0) ? ax - tb[0] : (k == 1) ? ay - tb[1] : (k == 2) ? tb[2] - ax : tb[3] - ay;
         const float wd = gscale * dfl_gain * 0.25f * nrm / tss;
