@@ -125,6 +125,24 @@ int adr_gn_finalize(const float* partial, int N, int chunks, int C, int G, doubl
 int adr_gn_bwd_finalize(const float* partial, int N, int chunks, int C, int G, double count, const float* mean,
                         const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* A, float* B,
                         float* Cc, int accumulate, void* stream);
+/* GroupNorm(G) + activation fused per image (one 1024-thread workgroup per image: channel sums -> group
+ * statistics -> z = act(x*scale + shift)); writes scale/shift per (image, channel) and mean/rstd per
+ * (image, group) for the backward. Replaces adr_nc_reduce + adr_gn_finalize + adr_affine_act when
+ * adr_gn_fused_supported(dtype, C, G) (the LDS plan fits). Conv_GN / TaskDecomposition / DyDCNv2
+ * (nn/modules/head.py:607-669, 751-782), ELA_HSFPN's GroupNorm+Sigmoid (block.py:1413-1416). */
+int adr_gn_fused_supported(int dtype, int C, int G);
+int adr_gn_act_fused(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco, const float* gamma,
+                     const float* beta, float eps, int N, int HW, int C, int G, int act, float* scale,
+                     float* shift, float* mean, float* rstd, void* stream);
+/* Backward of adr_gn_act_fused per image: dx = A*g + B*x + C (g = dz * act'(x*scale+shift)), and the
+ * per-image rows (sum g, sum g*x) -> partial[N][2][C] for adr_gn_param_grad. */
+int adr_gn_act_bwd_fused(int dtype, const void* x, int xcs, int xco, const void* dz, int dcs, int dco, void* dx,
+                         int ocs, int oco, const float* scale, const float* shift, const float* mean,
+                         const float* rstd, const float* gamma, int N, int HW, int C, int G, int act,
+                         float* partial, void* stream);
+/* dgamma / dbeta (+)= column sums over images of the adr_gn_act_bwd_fused rows. */
+int adr_gn_param_grad(const float* partial, int N, int C, int G, const float* mean, const float* rstd,
+                      float* dgamma, float* dbeta, int accumulate, void* stream);
 /* z = act(x * scale + shift), scale/shift per channel or (per_sample) per (image, channel). */
 int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco, const float* scale,
                    const float* shift, int per_sample, int act, int N, int HW, int C, void* stream);

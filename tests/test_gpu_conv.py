@@ -159,3 +159,28 @@ def test_stem_from_image(S, K):
     assert float(d) < 2e-2, float(d)
     dg = (ga - gb).norm() / gb.norm()
     assert float(dg) < 1e-2, float(dg)
+
+
+@pytest.mark.parametrize("shape,k,pad", [((8, 64, 40, 1), (7, 1), (3, 0)), ((8, 64, 1, 40), (1, 7), (0, 3)),
+                                         ((4, 32, 20, 12), (5, 3), (2, 1))])
+def test_conv_anisotropic_pad_bf16(shape, k, pad):
+    """ELA_HSFPN's Conv1d(7) over the pooled (H x 1) / (1 x W) strips (block.py:1413-1416) runs on the bf16 engine
+    with separate row / column paddings: forward, input gradient and weight gradient vs torch's fp32 conv on the
+    same bf16 operands."""
+    import torch.nn.functional as F
+    from adrefine import kernels as K
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    x = torch.randn(shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(C, C, *k, device="cuda") * 0.05).to(torch.bfloat16).float().requires_grad_(True)
+    xd = x.clone().requires_grad_(True)
+    y, _ = K.conv2d(xd, w, None, 1, pad)
+    g = torch.randn(y.shape, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    xr = x.float().requires_grad_(True)
+    wr = w.detach().clone().requires_grad_(True)
+    yr = F.conv2d(xr, wr, None, 1, pad)
+    yr.backward(g.float())
+    rel = lambda a, b: float((a.float() - b).norm() / b.norm())  # noqa: E731
+    assert rel(y, yr) < 1e-2 and rel(xd.grad, xr.grad) < 1e-2 and rel(w.grad, wr.grad) < 1e-2, \
+        (rel(y, yr), rel(xd.grad, xr.grad), rel(w.grad, wr.grad))

@@ -127,7 +127,7 @@ def _ptr(v):
     return v.value if isinstance(v, ctypes.c_void_p) else v
 
 
-_UNTIMED = ("_symbol", "_workspace", "_splits", "_tiles", "_chunks", "_size", "_floats", "adr_set_f32")
+_UNTIMED = ("_symbol", "_workspace", "_splits", "_tiles", "_chunks", "_size", "_floats", "_supported", "adr_set_f32")
 
 
 _SITE_LABELS = ("adr_ew", "adr_affine_act", "adr_affine_act_bwd", "adr_nc_reduce", "adr_memset_zero",
@@ -378,9 +378,9 @@ def _conv_work(d):
 
 def _engine2(d, red_channels):
     """Every bf16 contraction runs on the BK-64 engine (adr_conv.hip); with its division-free tap decoder it
-    measures faster than the generic engine on every shape of the step (scripts/conv_s1.sh, conv_shapes.sh).
-    Anisotropic stride / padding (the ELA 7x1 Conv1d) stays on the generic engine."""
-    return d.dtype == BF16 and d.stride_h == d.stride_w and d.pad_h == d.pad_w
+    measures faster than the generic engine on every shape of the step (scripts/conv_s1.sh, conv_shapes.sh),
+    including the ELA 7x1 Conv1d (padding (3, 0)): 33-65 us per launch on the generic engine."""
+    return d.dtype == BF16 and d.stride_h == d.stride_w
 
 
 def _conv2_symbol(d, dgrad):
@@ -539,14 +539,100 @@ class AxpyEntry(ctypes.Structure):
     _fields_ = [("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("n", ctypes.c_long)]
 
 
+# Off by default: measured on the bench step (hipGraph replay) the forked branch runs on other hardware queues and
+# the cross-queue waits cost more than the overlap wins (26.72 ms/step off vs 27.32 on, 28.65 with a fork per
+# WGRAD) — kept as an option (ADR_SIDE_STREAM=1), bitwise equal to the inline order (scripts/side_diff.py)
+_SIDE_ON = bool(int(__import__("os").environ.get("ADR_SIDE_STREAM", "0")))
+_SIDE_GROUP = int(__import__("os").environ.get("ADR_SIDE_GROUP", "8"))
+_SIDE_KINDS = set(__import__("os").environ.get("ADR_SIDE_KINDS", "wgrad,bias,dcn,stem,flush").split(","))
+_SIDE_STREAMS = {}
+
+
+class SideWork:
+    """Parameter-gradient work that nothing in the backward chain waits for — the conv WGRAD split-K GEMMs, bias
+    sums, the DCN weight gradient and the deferred arena reductions — forked onto a second stream: each fork makes
+    the side stream wait for everything enqueued so far on the current stream (dy and x are complete), and
+    `join()` makes the current stream wait for the side stream (before the DDP bucket all-reduce / optimizer read
+    the arena). The WGRADs then overlap the dgrad / BN-backward chain, whose many small launches leave most of
+    the chip idle. Captured into the same hipGraph as a forked branch. The tensors a forked launch reads stay
+    referenced until the join, so the caching allocator cannot hand their memory to the main stream while the
+    side stream may still read it. Arena slices written on the side stream belong to parameters whose every
+    gradient contribution goes through this path (conv / DCN weights and conv biases)."""
+
+    def __init__(self, device):
+        st = _SIDE_STREAMS.get(device)
+        if st is None:
+            st = _SIDE_STREAMS[device] = torch.cuda.Stream(device)
+        self.s, self.keep, self.used, self.pending, self.main = st, [], False, [], None
+        self.stores = set()  # storages of the kept tensors (guard_write)
+
+    def _hold(self, keep):
+        self.keep.extend(keep)
+        for t in keep:
+            self.stores.add(t.untyped_storage().data_ptr())
+
+    def guard_write(self, t):
+        """Before the current stream modifies `t` in place (FanOutFn adds into an exclusive concat-gradient slice
+        that an AddFn may also have handed to a conv as its dy): if side work reads t's storage, join first."""
+        if (self.used or self.pending) and t.untyped_storage().data_ptr() in self.stores:
+            self.join()
+
+    def fork(self, *keep):
+        self._hold(keep)
+        cur = torch.cuda.current_stream()
+        if cur == self.s:  # already on the side stream (a flush from inside side work): catch up with main
+            if self.main is not None:
+                self.s.wait_stream(self.main)
+            return _nullctx()
+        self.main = cur
+        self.s.wait_stream(cur)
+        self.used = True
+        return torch.cuda.stream(self.s)
+
+    def submit(self, fn, *keep):
+        """Queue side work; every _SIDE_GROUP submissions go out behind one fork (fewer cross-stream edges)."""
+        self._hold(keep)
+        self.pending.append(fn)
+        if len(self.pending) >= _SIDE_GROUP:
+            self.drain()
+
+    def drain(self):
+        if self.pending:
+            fns, self.pending = self.pending, []
+            with self.fork():
+                for fn in fns:
+                    fn()
+
+    def join(self):
+        self.drain()
+        if self.used:
+            torch.cuda.current_stream().wait_stream(self.s)
+            self.keep, self.used = [], False
+            self.stores = set()
+
+
+def _nullctx():
+    import contextlib
+    return contextlib.nullcontext()
+
+
+def _side(kind):
+    """The active side stream for parameter-gradient work of this kind (None: run inline)."""
+    if _DEFER is None or _TIMING is not None or _DEFER.side is None or kind not in _SIDE_KINDS:
+        return None
+    return _DEFER.side
+
+
 class WgradDeferral:
     """Collects the split-K reductions of every conv weight gradient that lands in the trainer's gradient arena
     and runs them as a few batched launches (adr_wgrad_reduce_batched) when the backward pass ends, instead of
     one launch per conv. The partial slabs stay alive until then. A second entry for the same destination (a
     weight shared by several calls, e.g. the head's shared convs) flushes the pending batch first, so every
-    destination's contributions still accumulate in program order."""
+    destination's contributions still accumulate in program order. With a SideWork, the flush runs on the side
+    stream (behind the WGRADs that produced the slabs)."""
 
-    def __init__(self):
+    def __init__(self, side=None):
+        self.side = side
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
         self.axpys, self.akeep, self.adsts = [], [], set()
@@ -578,6 +664,17 @@ class WgradDeferral:
         self.dsts.add(dst)
 
     def flush(self):
+        if self.side is not None:
+            self.side.drain()  # queued WGRADs add their entries first
+        if self.side is not None and "flush" in _SIDE_KINDS and (self.entries or self.psums or self.axpys):
+            # sources allocated on the current stream (a sink()'s temporary, a main-stream WGRAD's slabs) must
+            # outlive the side-stream reads: the side stream holds them until the join
+            with self.side.fork(*self.keep, *self.pkeep, *self.akeep):
+                self._flush()
+        else:
+            self._flush()
+
+    def _flush(self):
         if self.entries:
             arr = (WgradEntry * len(self.entries))(*self.entries)
             lib.adr_wgrad_reduce_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.entries), stream())
@@ -605,21 +702,36 @@ def defer_wgrad():
     @contextlib.contextmanager
     def _cm():
         global _DEFER
-        prev, _DEFER = _DEFER, WgradDeferral()
+        dev = torch.cuda.current_device()
+        prev, _DEFER = _DEFER, WgradDeferral(SideWork(dev) if _SIDE_ON else None)
         try:
             yield _DEFER
             _DEFER.flush()
+            if _DEFER.side is not None:
+                _DEFER.side.join()
         finally:
             _DEFER = prev
     return _cm()
 
 
-def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device):
+def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device, keep=()):
     """Weight gradient of a conv contraction straight into its parameter's gradient destination: the split-K
     WGRAD GEMM writes [split][K][RS][C] fp32 slabs, and one fused reduce+unpack kernel sums the splits in a
     fixed order and scatters them into the (K, C, R, S) layout of `param` (the trainer's arena slice when
     present, accumulating; otherwise a fresh tensor returned for autograd). wshape may cover only the first
     rows / unpadded channels of the GEMM (padded convs, DCN's [Cout][9C] columns)."""
+    K_, C_ = wshape[0], wshape[1]
+    RS_ = 1
+    for v in wshape[2:]:
+        RS_ *= v
+    side = _side("wgrad") if keep and _target(param) is not None else None
+    if side is not None:  # arena destination: the GEMM and its deferred reduction run on the side stream
+        side.submit(lambda: _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device), *keep)
+        return None
+    return _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device)
+
+
+def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device):
     splits = lib.adr_conv2d_wgrad_splits(ctypes.byref(d))
     stride = K * RS * C
     es = 2 if d.dtype == BF16 else 4
@@ -634,10 +746,6 @@ def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device):
         lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(ws), 0,
                                       stream())
     _t1(tok)
-    K_, C_ = wshape[0], wshape[1]
-    RS_ = 1
-    for v in wshape[2:]:
-        RS_ *= v
     Cp = max(C_, cpad)
     out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
     if _DEFER is not None and acc and _TIMING is None and splits * stride * 4 <= DEFER_MAX_BYTES:
@@ -652,7 +760,15 @@ def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device):
 
 def _bias_grad(dy, K, N, HW, cs, param=None):
     """Per-channel sum of dy. With `param`, accumulates into its gradient destination (grad_dst) and returns
-    the autograd value; otherwise returns a fresh (K,) tensor."""
+    the autograd value; otherwise returns a fresh (K,) tensor. Arena destinations run on the side stream."""
+    side = _side("bias") if param is not None and _target(param) is not None else None
+    if side is not None:
+        side.submit(lambda: _bias_grad1(dy, K, N, HW, cs, param), dy)
+        return None
+    return _bias_grad1(dy, K, N, HW, cs, param)
+
+
+def _bias_grad1(dy, K, N, HW, cs, param=None):
     dt = dcode(dy.dtype)
     chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
     part = torch.empty(N * chunks * 2 * K, dtype=torch.float32, device=dy.device)
@@ -712,7 +828,7 @@ class Conv2dFn(torch.autograd.Function):
         dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
         N, C, H, W = x.shape
         K, _, R, S = wshape
-        _, xp, xcs = nhwc(x)
+        x, xp, xcs = nhwc(x)
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
@@ -720,7 +836,7 @@ class Conv2dFn(torch.autograd.Function):
             d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
             conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr())
         if ctx.needs_input_grad[1]:
-            dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device)
+            dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
         if has_b and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, K, N, Ho * Wo, dycs, ctx.pb)
         return dx, dw, db, None, None, None, None
@@ -754,7 +870,7 @@ class ConvT2dFn(torch.autograd.Function):
         x, wp = ctx.saved_tensors
         stride, pad, wshape, has_b, Ho, Wo = ctx.meta
         dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
-        _, xp, xcs = nhwc(x)
+        x, xp, xcs = nhwc(x)
         N, Ci, H, W = x.shape
         _, Co, R, S = wshape
         dx = dw = db = None
@@ -765,7 +881,7 @@ class ConvT2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             # equivalent conv: input = dy_T (N, Ho, Wo, Co), output grad = x_T (N, H, W, Ci)
             d, _, _ = conv_desc(N, Ho, Wo, Co, dycs, Ci, R, S, stride, stride, pad, pad, xcs, x.dtype)
-            dw = wgrad_param(ctx.pw, d, dyp, xp, Ci, Co, R * S, wshape, 0, x.device)
+            dw = wgrad_param(ctx.pw, d, dyp, xp, Ci, Co, R * S, wshape, 0, x.device, keep=(x, dy))
         if has_b and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, Co, N, Ho * Wo, dycs, ctx.pb)
         return dx, dw, db, None, None, None
@@ -832,6 +948,12 @@ class BNActFn(torch.autograd.Function):
         return dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None, None, None
 
 
+_GN_FUSED = bool(int(__import__("os").environ.get("ADR_GN_FUSED", "1")))  # 0: the 3-launch path (A/B, parity)
+# one workgroup per image streams the image twice from one CU: past ~40x40 maps the three-launch path (the whole
+# chip on every pass) is faster
+_GN_FUSED_MAXHW = int(__import__("os").environ.get("ADR_GN_FUSED_MAXHW", "400"))
+
+
 class GNActFn(torch.autograd.Function):
     """act(GroupNorm(G)(y)) with per-(image, group) statistics."""
 
@@ -842,6 +964,20 @@ class GNActFn(torch.autograd.Function):
         N, C, H, W = y.shape
         HW = H * W
         dev = y.device
+        ctx.fused = _GN_FUSED and HW <= _GN_FUSED_MAXHW and bool(lib.adr_gn_fused_supported(dcode(dtype), C, groups))
+        if ctx.fused:  # one launch per layer: a workgroup per image does statistics + affine + activation
+            scale = torch.empty(N * C, dtype=torch.float32, device=dev)
+            shift = torch.empty(N * C, dtype=torch.float32, device=dev)
+            mean = torch.empty(N * groups, dtype=torch.float32, device=dev)
+            rstd = torch.empty(N * groups, dtype=torch.float32, device=dev)
+            z = empty_act(N, C, H, W, dtype, dev)
+            lib.adr_gn_act_fused(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(z.data_ptr()), C, 0,
+                                 fptr(gamma.detach()), fptr(beta.detach()), float(eps), N, HW, C, groups, ACT[act],
+                                 fptr(scale), fptr(shift), fptr(mean), fptr(rstd), stream())
+            ctx.save_for_backward(y, scale, shift, mean, rstd, gamma)
+            ctx.meta = (groups, act)
+            ctx.pbeta = beta
+            return z
         chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
         part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
         lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, N, HW, C,
@@ -871,6 +1007,19 @@ class GNActFn(torch.autograd.Function):
         HW = H * W
         dev = y.device
         dt = dcode(y.dtype)
+        if ctx.fused:
+            part = torch.empty(N * 2 * C, dtype=torch.float32, device=dev)
+            dy = empty_act(N, C, H, W, y.dtype, dev)
+            lib.adr_gn_act_bwd_fused(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
+                                     ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(mean),
+                                     fptr(rstd), fptr(gamma.detach()), N, HW, C, groups, ACT[act], fptr(part),
+                                     stream())
+            dgamma, pg, acc_g = grad_dst(gamma, C, dev)
+            dbeta, pb, acc_b = grad_dst(ctx.pbeta, C, dev)
+            if acc_g != acc_b:
+                raise RuntimeError("GN gamma/beta gradients must share one destination kind")
+            lib.adr_gn_param_grad(fptr(part), N, C, groups, fptr(mean), fptr(rstd), pg, pb, acc_g, stream())
+            return dy, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None
         chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
         part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
         lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale), fptr(shift),
@@ -929,11 +1078,15 @@ class StemConvFn(torch.autograd.Function):
         w = ctx.pw
         Kc = w.shape[0]
         dy, dyp, dycs = nhwc(dy.to(torch.bfloat16) if dy.dtype != torch.bfloat16 else dy)
-        dw, pdw, acc = grad_dst(w, w.numel(), img.device)
-        wsb = lib.adr_stem_wgrad_workspace(N, H, W, Kc)
-        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=img.device)
-        (lib.adr_stem_conv_wgrad_u8 if img.dtype == torch.uint8 else lib.adr_stem_conv_wgrad)(
-            fptr(img), N, H, W, ctypes.c_void_p(dyp), dycs, Kc, pdw, acc, fptr(ws), wsb, stream())
+        side = _side("stem") if _target(w) is not None else None
+        with (side.fork(img, dy) if side is not None else _nullctx()):
+            dw, pdw, acc = grad_dst(w, w.numel(), img.device)
+            wsb = lib.adr_stem_wgrad_workspace(N, H, W, Kc)
+            ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=img.device)
+            (lib.adr_stem_conv_wgrad_u8 if img.dtype == torch.uint8 else lib.adr_stem_conv_wgrad)(
+                fptr(img), N, H, W, ctypes.c_void_p(dyp), dycs, Kc, pdw, acc, fptr(ws), wsb, stream())
+            if side is not None:
+                side.keep.append(ws)
         return None, grad_ret(w, dw), None
 
 
@@ -1169,6 +1322,9 @@ class FanOutFn(torch.autograd.Function):
         excl = [g for g in gs if getattr(g, "_adr_excl", False) and _v(g)[0] is g]
         if excl:  # accumulate the others into the exclusive slice in place
             acc = excl[0]
+            side = _side("wgrad") or _side("bias")
+            if side is not None:
+                side.guard_write(acc)
             rest = [g for g in gs if g is not acc]
             va = _v(acc)
             while rest:
@@ -1750,7 +1906,7 @@ class PaddedConvFn(torch.autograd.Function):
         dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
         N, C, H, W = x.shape
         K, _, R, S = wshape
-        _, xp, xcs = nhwc(x)
+        x, xp, xcs = nhwc(x)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = empty_act(N, C, H, W, x.dtype, x.device)
@@ -1847,22 +2003,25 @@ class DCNFn(torch.autograd.Function):
                                  stream())
             _t1(tok)
             if ctx.needs_input_grad[2]:
-                splits = lib.adr_dcn_wgrad_bf16_splits(N, H, W, C, Cout)
-                stride = Cout * 9 * C
-                ws = torch.empty(splits * stride, dtype=torch.float32, device=dev)
-                rep = _reps()
-                tok = _t0("adr::dcn_wgrad_kernel(adr::DcnArgs)", nb + 4 * splits * stride, fl,
-                          f"dcn wgrad/{splits} n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "", rep)
-                for _ in range(rep):
-                    lib.adr_dcn_wgrad_bf16(ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, ctypes.c_void_p(dyp),
-                                           dycs, fptr(ws), splits, N, H, W, C, Cout, stream())
-                _t1(tok)
-                out, ptr, acc = grad_dst(ctx.pw, stride, dev)
-                if _DEFER is not None and acc and _TIMING is None:
-                    _DEFER.add(ws, stride, splits, ptr, Cout, C, C, 9, 0, acc)
-                else:
-                    lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, Cout, C, C, 9, 0, acc, stream())
-                dw = grad_ret(ctx.pw, out)
+                side = _side("dcn") if _target(ctx.pw) is not None else None
+                with (side.fork(x, om, dy) if side is not None else _nullctx()):
+                    splits = lib.adr_dcn_wgrad_bf16_splits(N, H, W, C, Cout)
+                    stride = Cout * 9 * C
+                    ws = torch.empty(splits * stride, dtype=torch.float32, device=dev)
+                    rep = _reps()
+                    tok = _t0("adr::dcn_wgrad_kernel(adr::DcnArgs)", nb + 4 * splits * stride, fl,
+                              f"dcn wgrad/{splits} n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "", rep)
+                    for _ in range(rep):
+                        lib.adr_dcn_wgrad_bf16(ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs,
+                                               ctypes.c_void_p(dyp), dycs, fptr(ws), splits, N, H, W, C, Cout,
+                                               stream())
+                    _t1(tok)
+                    out, ptr, acc = grad_dst(ctx.pw, stride, dev)
+                    if _DEFER is not None and acc and _TIMING is None:
+                        _DEFER.add(ws, stride, splits, ptr, Cout, C, C, 9, 0, acc)
+                    else:
+                        lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, Cout, C, C, 9, 0, acc, stream())
+                    dw = grad_ret(ctx.pw, out)
         else:
             # dcols = dy x W^T  (1x1 GEMM: Cin = Cout, K = 9C)
             dcols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=dev)
@@ -1870,7 +2029,7 @@ class DCNFn(torch.autograd.Function):
             conv_fwd(d, dyp, wt.data_ptr(), None, dcols.data_ptr())
             if ctx.needs_input_grad[2]:
                 dwd, _, _ = conv_desc(N, H, W, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, dycs, dtype)
-                dw = wgrad_param(ctx.pw, dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, w.shape, 0, dev)
+                dw = wgrad_param(ctx.pw, dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, w.shape, 0, dev, keep=(cols, dy))
             lib.adr_dcn_col2im(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(dcols),
                                fptr(dx32), ctypes.c_void_p(dom.data_ptr()), om.shape[1], N, H, W, C,
                                int(dtype == torch.float32), stream())

@@ -581,7 +581,8 @@ static int conv_check(const adr_conv_desc* d) {
   ADR_REQUIRE(d->x_cstride % 8 == 0 && d->x_coff % 8 == 0 && d->y_cstride % 8 == 0 && d->y_coff % 8 == 0,
               "conv: channel views must be 16-byte aligned");
   ADR_REQUIRE(d->x_cstride >= d->x_coff + d->c && d->y_cstride >= d->y_coff + d->k, "conv: view exceeds stride");
-  ADR_REQUIRE(d->stride_h == d->stride_w && d->pad_h == d->pad_w, "conv: anisotropic stride/padding");
+  // the row decoder keeps one stride but separate paddings (ELA_HSFPN's 7x1 Conv1d pads (3, 0))
+  ADR_REQUIRE(d->stride_h == d->stride_w, "conv: anisotropic stride");
   const int ho = (d->h + 2 * d->pad_h - d->r) / d->stride_h + 1, wo = (d->w + 2 * d->pad_w - d->s) / d->stride_w + 1;
   ADR_REQUIRE(ho == d->ho && wo == d->wo, "conv: output size mismatch (%dx%d vs %dx%d)", d->ho, d->wo, ho, wo);
   ADR_REQUIRE((long)d->n * d->h * d->w * d->x_cstride < (1l << 30) && (long)d->n * d->ho * d->wo * d->y_cstride < (1l << 30)

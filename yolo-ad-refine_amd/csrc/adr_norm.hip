@@ -329,6 +329,248 @@ __global__ void __launch_bounds__(256) gn_bwd_param_kernel(const float* __restri
   }
 }
 
+// ---- GroupNorm + activation fused per image (Conv_GN / TaskDecomposition / DyDCNv2 / ELA gates: GN statistics
+//      are per image, so one 1024-thread workgroup owns an image and needs no cross-workgroup reduction). Forward:
+//      channel sums -> group mean / rstd -> per-channel scale/shift -> z = act(x*scale + shift), one launch
+//      instead of nc_reduce + gn_finalize + affine_act. Backward: channel sums of g = dz * act'(.) and g*x ->
+//      (A, B, C) -> dx = A*g + B*x + C, plus the per-image (sum g, sum g*x) rows gn_bwd_param reduces for
+//      dgamma / dbeta. Fixed-order sums (per-thread fp32 over its rows, then double in LDS): deterministic. ----
+constexpr int GNF_T = 1024;
+
+// per-channel (double) sums of a per-thread accumulator over the row-threads of each channel group (one LDS image
+// of GNF_T x VEC floats, reused for the second accumulator)
+template <int VEC>
+__device__ __forceinline__ void gnf_sum1(const float* s, int G8, int RP, int C, float* shf, double* out) {
+  const int t = threadIdx.x;
+  if (t / G8 < RP) {
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) shf[t * VEC + e] = s[e];
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += GNF_T) {
+    const int g = c / VEC, e = c % VEC;
+    double a = 0.0;
+    for (int r = 0; r < RP; ++r) a += shf[(g + r * G8) * VEC + e];
+    out[c] = a;
+  }
+  __syncthreads();
+}
+
+template <int VEC>
+__device__ __forceinline__ void gnf_channel_sums(const float* s1, const float* s2, int G8, int RP, int C, float* shf,
+                                                 double* ca, double* cb) {
+  gnf_sum1<VEC>(s1, G8, RP, C, shf, ca);
+  gnf_sum1<VEC>(s2, G8, RP, C, shf, cb);
+}
+
+template <typename T, int ACT>
+__global__ void __launch_bounds__(GNF_T) gn_fused_fwd_kernel(const T* __restrict__ x, int xcs, int xco, T* __restrict__ z,
+                                                             int zcs, int zco, const float* __restrict__ gamma,
+                                                             const float* __restrict__ beta, float eps, int HW, int C,
+                                                             int G, float* scale, float* shift, float* mean_out,
+                                                             float* rstd_out) {
+  constexpr int VEC = 16 / sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) unsigned char gnf_raw[];
+  float* shf = reinterpret_cast<float*>(gnf_raw);                       // [GNF_T * VEC]
+  double* ca = reinterpret_cast<double*>(shf + GNF_T * VEC);           // [C]
+  double* cb = ca + C;                                                  // [C]
+  float* sc = reinterpret_cast<float*>(cb + C);                         // [C]
+  float* sf = sc + C;                                                   // [C]
+  double* gstat = reinterpret_cast<double*>(sf + C);                    // [2][G]
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int G8 = C / VEC, RP = GNF_T / G8;
+  const int cg = t % G8, r0 = t / G8, c0 = cg * VEC;
+  const bool act_t = r0 < RP;
+  const T* xb = x + (long)n * HW * xcs + xco + c0;
+  float s1[VEC], s2[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
+  if (act_t) {
+    constexpr int NU = 4;
+    for (int r = r0; r < HW; r += NU * RP) {
+      u32x4 v[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        if (r + u * RP < HW) v[u] = ld16(xb + (long)(r + u * RP) * xcs);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        if (r + u * RP >= HW) break;
+        const T* ve = reinterpret_cast<const T*>(&v[u]);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float f = to_f(ve[e]);
+          s1[e] += f;
+          s2[e] += f * f;
+        }
+      }
+    }
+  }
+  gnf_channel_sums<VEC>(s1, s2, G8, RP, C, shf, ca, cb);
+  const int cpg = C / G;
+  const double count = (double)HW * cpg;
+  for (int g = t; g < G; g += GNF_T) {
+    double a = 0.0, b = 0.0;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      a += ca[c];
+      b += cb[c];
+    }
+    const double mu = a / count;
+    double var = b / count - mu * mu;
+    if (var < 0) var = 0;
+    const double rs = 1.0 / sqrt(var + (double)eps);
+    gstat[g] = mu;
+    gstat[G + g] = rs;
+    mean_out[n * G + g] = (float)mu;
+    rstd_out[n * G + g] = (float)rs;
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += GNF_T) {
+    const int g = c / cpg;
+    const double gg = gamma ? gamma[c] : 1.0, bb = beta ? beta[c] : 0.0;
+    const float a = (float)(gg * gstat[G + g]), b = (float)(bb - gstat[g] * gg * gstat[G + g]);
+    sc[c] = a;
+    sf[c] = b;
+    scale[n * C + c] = a;
+    shift[n * C + c] = b;
+  }
+  __syncthreads();
+  if (!act_t) return;
+  float a[VEC], b[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    a[e] = sc[c0 + e];
+    b[e] = sf[c0 + e];
+  }
+  T* zb = z + (long)n * HW * zcs + zco + c0;
+  for (int r = r0; r < HW; r += RP) {
+    const u32x4 v = ld16(xb + (long)r * xcs);
+    const T* ve = reinterpret_cast<const T*>(&v);
+    u32x4 o;
+    T* oe = reinterpret_cast<T*>(&o);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) oe[e] = from_f<T>(act_fwd_c<ACT, sizeof(T) == 2>(to_f(ve[e]) * a[e] + b[e]));
+    st16(zb + (long)r * zcs, o);
+  }
+}
+
+template <typename T, int ACT>
+__global__ void __launch_bounds__(GNF_T) gn_fused_bwd_kernel(const T* __restrict__ x, int xcs, int xco,
+                                                             const T* __restrict__ dz, int dcs, int dco,
+                                                             T* __restrict__ dx, int ocs, int oco,
+                                                             const float* __restrict__ scale,
+                                                             const float* __restrict__ shift,
+                                                             const float* __restrict__ mean,
+                                                             const float* __restrict__ rstd,
+                                                             const float* __restrict__ gamma, int HW, int C, int G,
+                                                             float* part) {
+  constexpr int VEC = 16 / sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) unsigned char gnf_raw[];
+  float* shf = reinterpret_cast<float*>(gnf_raw);
+  double* ca = reinterpret_cast<double*>(shf + GNF_T * VEC);
+  double* cb = ca + C;
+  float* cA = reinterpret_cast<float*>(cb + C);
+  float* cB = cA + C;
+  float* cC = cB + C;
+  double* gsum = reinterpret_cast<double*>(cC + C + (C & 1));  // [2][G] (8-byte aligned)
+  const int n = blockIdx.x, t = threadIdx.x;
+  const int G8 = C / VEC, RP = GNF_T / G8;
+  const int cg = t % G8, r0 = t / G8, c0 = cg * VEC;
+  const bool act_t = r0 < RP;
+  float sc[VEC], sf[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    sc[e] = act_t ? scale[n * C + c0 + e] : 0.f;
+    sf[e] = act_t ? shift[n * C + c0 + e] : 0.f;
+  }
+  const T* xb = x + (long)n * HW * xcs + xco + c0;
+  const T* db = dz + (long)n * HW * dcs + dco + c0;
+  float s1[VEC], s2[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) s1[e] = s2[e] = 0.f;
+  if (act_t) {
+    constexpr int NU = 4;
+    for (int r = r0; r < HW; r += NU * RP) {
+      u32x4 xv[NU], dv[NU];
+#pragma unroll
+      for (int u = 0; u < NU; ++u)
+        if (r + u * RP < HW) {
+          xv[u] = ld16(xb + (long)(r + u * RP) * xcs);
+          dv[u] = ld16(db + (long)(r + u * RP) * dcs);
+        }
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        if (r + u * RP >= HW) break;
+        const T* xe = reinterpret_cast<const T*>(&xv[u]);
+        const T* de = reinterpret_cast<const T*>(&dv[u]);
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const float xf = to_f(xe[e]);
+          const float g = to_f(de[e]) * act_bwd_c<ACT, sizeof(T) == 2>(xf * sc[e] + sf[e]);
+          s1[e] += g;
+          s2[e] += g * xf;
+        }
+      }
+    }
+  }
+  gnf_channel_sums<VEC>(s1, s2, G8, RP, C, shf, ca, cb);
+  const int cpg = C / G;
+  const double count = (double)HW * cpg;
+  for (int c = t; c < C; c += GNF_T) {
+    part[((long)n * 2) * C + c] = (float)ca[c];      // (sum g, sum g*x) rows for gn_bwd_param (chunks = 1)
+    part[((long)n * 2 + 1) * C + c] = (float)cb[c];
+  }
+  for (int g = t; g < G; g += GNF_T) {
+    const double mu = mean[n * G + g], rs = rstd[n * G + g];
+    double S1 = 0.0, S2 = 0.0;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      const double gm = gamma ? gamma[c] : 1.0;
+      S1 += gm * ca[c];                   // sum dxhat
+      S2 += gm * (cb[c] - mu * ca[c]) * rs;  // sum dxhat * xhat
+    }
+    gsum[g] = S1;
+    gsum[G + g] = S2;
+  }
+  __syncthreads();
+  for (int c = t; c < C; c += GNF_T) {
+    const int g = c / cpg;
+    const double mu = mean[n * G + g], rs = rstd[n * G + g];
+    const double gm = gamma ? gamma[c] : 1.0;
+    const double Bk = -rs * rs * gsum[G + g] / count;
+    cA[c] = (float)(rs * gm);
+    cB[c] = (float)Bk;
+    cC[c] = (float)(-rs * gsum[g] / count - Bk * mu);
+  }
+  __syncthreads();
+  if (!act_t) return;
+  float A[VEC], B[VEC], Cc[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) {
+    A[e] = cA[c0 + e];
+    B[e] = cB[c0 + e];
+    Cc[e] = cC[c0 + e];
+  }
+  T* ob = dx + (long)n * HW * ocs + oco + c0;
+  for (int r = r0; r < HW; r += RP) {
+    const u32x4 xv = ld16(xb + (long)r * xcs);
+    const u32x4 dv = ld16(db + (long)r * dcs);
+    const T* xe = reinterpret_cast<const T*>(&xv);
+    const T* de = reinterpret_cast<const T*>(&dv);
+    u32x4 o;
+    T* oe = reinterpret_cast<T*>(&o);
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) {
+      const float xf = to_f(xe[e]);
+      const float g = to_f(de[e]) * act_bwd_c<ACT, sizeof(T) == 2>(xf * sc[e] + sf[e]);
+      oe[e] = from_f<T>(A[e] * g + B[e] * xf + Cc[e]);
+    }
+    st16(ob + (long)r * ocs, o);
+  }
+}
+
+static size_t gnf_smem(int vec, int C, int G) {
+  return (size_t)GNF_T * vec * 4 + (size_t)2 * C * 8 + (size_t)4 * C * 4 + 8 + (size_t)2 * G * 8;
+}
+
 // z = act(x * scale + shift) ; NHWC; scale/shift per channel or per (n, channel)
 template <typename T, int ACT>
 __global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x, int xcs, int xco, T* __restrict__ z,
@@ -618,4 +860,64 @@ extern "C" int adr_partial_sum(const float* partial, int P, int C, int which, fl
   hipLaunchKernelGGL(partial_sum_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, P, C, which, out,
                      accumulate);
   return check_launch("adr_partial_sum");
+}
+
+extern "C" int adr_gn_fused_supported(int dtype, int C, int G) {
+  const int vec = dtype == ADR_BF16 ? 8 : 4;
+  return C % vec == 0 && C / vec <= GNF_T && G > 0 && C % G == 0 && gnf_smem(vec, C, G) + (size_t)C * 4 <= 64 * 1024;
+}
+
+extern "C" int adr_gn_act_fused(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco,
+                                const float* gamma, const float* beta, float eps, int N, int HW, int C, int G, int act,
+                                float* scale, float* shift, float* mean, float* rstd, void* stream) {
+  const int vec = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(N > 0 && HW > 0 && C % vec == 0 && C / vec <= GNF_T && G > 0 && C % G == 0 && xcs % vec == 0 &&
+                  xco % vec == 0 && zcs % vec == 0 && zco % vec == 0,
+              "gn_act_fused: N=%d HW=%d C=%d G=%d (views must be 16-byte aligned)", N, HW, C, G);
+  const size_t sm = gnf_smem(vec, C, G);
+  ADR_REQUIRE(sm <= 64 * 1024, "gn_act_fused: C=%d needs %zu bytes of LDS", C, sm);
+  hipStream_t st = (hipStream_t)stream;
+#define ADR_GNF(A)                                                                                                  \
+  if (dtype == ADR_BF16)                                                                                            \
+    hipLaunchKernelGGL((gn_fused_fwd_kernel<__bf16, A>), dim3(N), dim3(GNF_T), sm, st, (const __bf16*)x, xcs, xco,  \
+                       (__bf16*)z, zcs, zco, gamma, beta, eps, HW, C, G, scale, shift, mean, rstd);                 \
+  else                                                                                                              \
+    hipLaunchKernelGGL((gn_fused_fwd_kernel<float, A>), dim3(N), dim3(GNF_T), sm, st, (const float*)x, xcs, xco,    \
+                       (float*)z, zcs, zco, gamma, beta, eps, HW, C, G, scale, shift, mean, rstd)
+  ADR_ACT_DISPATCH(act, ADR_GNF);
+#undef ADR_GNF
+  return check_launch("adr_gn_act_fused");
+}
+
+extern "C" int adr_gn_act_bwd_fused(int dtype, const void* x, int xcs, int xco, const void* dz, int dcs, int dco,
+                                    void* dx, int ocs, int oco, const float* scale, const float* shift,
+                                    const float* mean, const float* rstd, const float* gamma, int N, int HW, int C,
+                                    int G, int act, float* partial, void* stream) {
+  const int vec = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(N > 0 && HW > 0 && C % vec == 0 && C / vec <= GNF_T && G > 0 && C % G == 0 && xcs % vec == 0 &&
+                  xco % vec == 0 && dcs % vec == 0 && dco % vec == 0 && ocs % vec == 0 && oco % vec == 0,
+              "gn_act_bwd_fused: N=%d HW=%d C=%d G=%d (views must be 16-byte aligned)", N, HW, C, G);
+  const size_t sm = gnf_smem(vec, C, G) + (size_t)C * 4;
+  ADR_REQUIRE(sm <= 64 * 1024, "gn_act_bwd_fused: C=%d needs %zu bytes of LDS", C, sm);
+  hipStream_t st = (hipStream_t)stream;
+#define ADR_GNB(A)                                                                                                  \
+  if (dtype == ADR_BF16)                                                                                            \
+    hipLaunchKernelGGL((gn_fused_bwd_kernel<__bf16, A>), dim3(N), dim3(GNF_T), sm, st, (const __bf16*)x, xcs, xco,  \
+                       (const __bf16*)dz, dcs, dco, (__bf16*)dx, ocs, oco, scale, shift, mean, rstd, gamma, HW, C, \
+                       G, partial);                                                                                 \
+  else                                                                                                              \
+    hipLaunchKernelGGL((gn_fused_bwd_kernel<float, A>), dim3(N), dim3(GNF_T), sm, st, (const float*)x, xcs, xco,    \
+                       (const float*)dz, dcs, dco, (float*)dx, ocs, oco, scale, shift, mean, rstd, gamma, HW, C, G, \
+                       partial)
+  ADR_ACT_DISPATCH(act, ADR_GNB);
+#undef ADR_GNB
+  return check_launch("adr_gn_act_bwd_fused");
+}
+
+extern "C" int adr_gn_param_grad(const float* partial, int N, int C, int G, const float* mean, const float* rstd,
+                                 float* dgamma, float* dbeta, int accumulate, void* stream) {
+  ADR_REQUIRE(G > 0 && C % G == 0, "gn_param_grad: C=%d G=%d", C, G);
+  hipLaunchKernelGGL(gn_bwd_param_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, N, 1, C, G, mean, rstd,
+                     dgamma, dbeta, accumulate);
+  return check_launch("adr_gn_param_grad");
 }
