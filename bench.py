@@ -194,6 +194,8 @@ def main():
     ap.add_argument("--infer-steps", type=int, default=20)
     ap.add_argument("--scale", default="n", choices=["n", "s", "m", "l", "x"],
                     help="model scale of the 701 yaml (configs[4] = l at 1280^2, bs 16/GPU)")
+    ap.add_argument("--conv-fp8", action="store_true",
+                    help="forward convs on the fp8 (e4m3) MFMA engine (configs[4]'s fp8 conv path; backward bf16)")
     args = ap.parse_args()
     if args.scale != "n":  # configs[4]: its own line; the n/640 baselines (CPU, inference) do not apply
         args.no_cpu_baseline, args.infer_steps = True, 0
@@ -209,6 +211,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
     import adrefine.kernels as K
+    K.CONV_FP8 = K.CONV_FP8 or args.conv_fp8
     from adrefine.engine.trainer import FusedTrainer
     from adrefine.data.synthetic import train_batch
     from adrefine.nn.tasks import DetectionModel
@@ -312,7 +315,7 @@ def main():
                        else f"images/sec whole-node ({args.img}x{args.img}) fwd+bwd, YOLO-AD-Refine-{args.scale}"),
             "value": round(ips, 2), "unit": "images/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(1000 * dt / args.steps, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype,
+            "scaling": "weak", "vs_baseline": None, "dtype": args.dtype + ("+fp8-fwd-conv" if K.CONV_FP8 else ""),
             "data": "synthetic (uint8 images + COCO-shape labels)" if not args.float_images else "synthetic (fp32 images)",
             "config": {"workload": f"yolo11-701-YOLO-AD-Refine.yaml ({args.scale}) train step bs={args.bs}/GPU "
                                    f"{args.img}x{args.img}, synthetic COCO-shape labels, TAL+DFL+CIoU/NWD loss, "

@@ -65,6 +65,22 @@ int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w_krs
 int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
                           int accumulate, void* stream);
 int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d);
+/* fp8 (OCP e4m3) forward conv for BASELINE.json configs[4] (l-scale "fp8 MFMA conv path"), replacing the same
+ * nn.Conv2d forward as adr_conv2d_fwd_bf16 (nn/modules/conv.py:44-50) on v_mfma_scale_f32_16x16x128_f8f6f4.
+ * Delayed per-tensor activation scaling: sa = 448 / max(amax_part[0 .. adr_fp8_amax_blocks())) — last step's
+ * |x| maxima of this conv's input, collected by the previous launch into amax_next (atomicMax slots, zeroed
+ * and rotated by adr_pack_weight_fp8: prev <- cur, cur <- 0; seed both once with adr_amax_bf16). Weights per
+ * output channel (adr_pack_weight_fp8: fp8 KRSC rows + 1/sw[k]). Output bf16 + optional BN partial statistics
+ * per 128-row tile (adr_conv2d_fwd_fp8_stat_tiles). Backward stays on the bf16 engine. */
+int adr_fp8_amax_blocks(void);
+int adr_amax_bf16(const void* x, int cs, int co, long npix, int C, float* part, void* stream);
+int adr_pack_weight_fp8(const float* w, int K, int C, int Cp, int RS, uint8_t* out, float* inv_scale,
+                        float* amax_cur, float* amax_prev, void* stream);
+int adr_conv2d_fp8_supported(const adr_conv_desc* d);
+int adr_conv2d_fwd_fp8_stat_tiles(const adr_conv_desc* d);
+int adr_conv2d_fwd_fp8(const adr_conv_desc* d, const void* x, const uint8_t* w_fp8, const float* w_inv_scale,
+                       const float* amax_part, float* amax_next, const float* bias, void* y, float* stats,
+                       void* stream);
 /* Mangled name of the kernel the bf16 engine launches for this contraction (dgrad != 0: the data gradient),
  * written to buf (len >= 64) — the label the bench's roofline and rocprofv3 share. */
 int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, char* buf, int len);

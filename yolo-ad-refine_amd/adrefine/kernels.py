@@ -403,6 +403,36 @@ def conv_fwd(d, xp, wp, bias, yp, stats=None, accumulate=0):
     _t1(tok)
 
 
+# BASELINE.json configs[4]'s fp8 MFMA conv path: bias-free forward convs (Conv-BN-act) with a spatial kernel and
+# >= _FP8_MIN_C input channels run on the e4m3 engine (adr_conv_fp8.hip) when set (bench.py --conv-fp8, or
+# ADR_CONV_FP8=1); backward stays bf16. Measured (scripts/fp8_micro.py, l-scale 1280^2 bs16 shapes): 3x3 convs
+# with C >= 128 run 1.04-1.24x faster than on the bf16 engine; 1x1 and 64-channel convs are memory-bound and
+# gain nothing (the staging conversion costs VALU), so they stay bf16.
+CONV_FP8 = bool(int(__import__("os").environ.get("ADR_CONV_FP8", "0")))
+_FP8_MIN_C = 128
+
+
+def conv_fwd_fp8(d, xp, w, Cw, Cp, bias, yp, stats):
+    """y = conv(x, w) (+bias) on the fp8 engine with delayed per-tensor activation scaling: the conv collects its
+    input's |x| maxima for the next step as it stages x; the per-step weight pack (per output channel) rotates
+    them (state on the weight tensor: [amax_cur, amax_prev]). The first call seeds the maxima with one
+    adr_amax_bf16 pass over x."""
+    dev = w.device
+    K_, RS = w.shape[0], w.shape[2] * w.shape[3]
+    nb = lib.adr_fp8_amax_blocks()
+    st = getattr(w, "_adr_fp8", None)
+    if st is None:
+        st = [torch.zeros(nb, dtype=torch.float32, device=dev), torch.zeros(nb, dtype=torch.float32, device=dev)]
+        w._adr_fp8 = st
+        lib.adr_amax_bf16(ctypes.c_void_p(xp), d.x_cstride, 0, d.n * d.h * d.w, d.c, fptr(st[0]), stream())
+    w8 = torch.empty(K_ * RS * Cp, dtype=torch.uint8, device=dev)
+    winv = torch.empty(K_, dtype=torch.float32, device=dev)
+    lib.adr_pack_weight_fp8(fptr(w.detach().float().contiguous()), K_, Cw, Cp, RS, fptr(w8), fptr(winv), fptr(st[0]),
+                            fptr(st[1]), stream())
+    lib.adr_conv2d_fwd_fp8(ctypes.byref(d), ctypes.c_void_p(xp), fptr(w8), fptr(winv), fptr(st[1]), fptr(st[0]),
+                           fptr(bias), ctypes.c_void_p(yp), fptr(stats), stream())
+
+
 def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0):
     """dx (+)= conv_transpose(dy, w); wpair = (KRSC, CRSK-or-None) packed weights (pack_weight2)."""
     krsc, crsk = wpair
@@ -809,7 +839,16 @@ class Conv2dFn(torch.autograd.Function):
                 ctypes.byref(d))
             stats = torch.empty(tiles * 2 * K, dtype=torch.float32, device=x.device)
         bf = b.detach().float().contiguous() if b is not None else None
-        conv_fwd(d, xp, wp.data_ptr(), fptr(bf), y.data_ptr(), fptr(stats))
+        # fp8 for the Conv-BN-act convs only: biased nn.Conv2d rows (the heads' output projections: logits, box
+        # bins, offsets) stay bf16, as fp8 training recipes keep the output layers in higher precision
+        if CONV_FP8 and b is None and dtype == torch.bfloat16 and C >= _FP8_MIN_C and R * S > 1 and \
+                lib.adr_conv2d_fp8_supported(ctypes.byref(d)):
+            if want_stats:  # the fp8 engine tiles every geometry by 128 output rows
+                stats = torch.empty(lib.adr_conv2d_fwd_fp8_stat_tiles(ctypes.byref(d)) * 2 * K, dtype=torch.float32,
+                                    device=x.device)
+            conv_fwd_fp8(d, xp, w, Cw, Cp, bf, y.data_ptr(), stats)
+        else:
+            conv_fwd(d, xp, wp.data_ptr(), fptr(bf), y.data_ptr(), fptr(stats))
         ctx.save_for_backward(x, wp, wt)
         ctx.meta = (stride, pad, cpad, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
