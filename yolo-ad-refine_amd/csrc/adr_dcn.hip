@@ -25,6 +25,8 @@
 
 #include "adr_common.h"
 
+#include <cstdlib>
+
 namespace adr {
 
 namespace {
@@ -381,7 +383,9 @@ constexpr int SPITCH = 72;              // S_t row pitch (bf16): 64 pixels + 8
 constexpr int DPITCH = 80;              // dcols row pitch (bf16): odd multiple of 16 elements for transposing reads
 constexpr int BOVF = 256;               // overflow queue (out-of-window corners) per tap
 
-__global__ void __launch_bounds__(256, 2) dcn_bwd_kernel(DcnArgs a) {
+// OCC = workgroups per CU the register budget is sized for: 2 (256 VGPRs, a few spilled) or 1 (AGPRs too, no spill)
+template <int OCC>
+__global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a) {
   __shared__ __attribute__((aligned(16))) __bf16 S[BROWS * SPITCH];   // [cell][pixel]
   __shared__ __attribute__((aligned(16))) __bf16 D[64 * DPITCH];      // dcols [pixel][channel]
   __shared__ __attribute__((aligned(16))) __bf16 oms[64 * 32];
@@ -704,6 +708,8 @@ extern "C" int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs
   a.x_bytes = (int)((long)N * H * W * xcs * 2);
   a.w_bytes = 9 * C * Cout * 2;
   const int blocks = N * cdiv(H, BT) * cdiv(W, BT);
-  hipLaunchKernelGGL(dcn_bwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+  static const int occ = getenv("ADR_DCN_BWD_OCC") ? atoi(getenv("ADR_DCN_BWD_OCC")) : 2;
+  if (occ == 1) hipLaunchKernelGGL(dcn_bwd_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(dcn_bwd_kernel<2>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("adr_dcn_bwd_bf16");
 }
