@@ -822,6 +822,8 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, want_stats, cpad):
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
+        sink = getattr(x, "_adr_sink", None)
+        ctx.sink = sink if sink is not None and sink.fits(x) else None
         dtype = x.dtype
         x, xp, xcs = nhwc(x)
         N, C, H, W = x.shape
@@ -871,9 +873,13 @@ class Conv2dFn(torch.autograd.Function):
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = empty_act(N, C, H, W, x.dtype, x.device)
             d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
-            conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr())
+            if ctx.sink is not None:  # into the fan-out's shared gradient (accumulating after the first consumer)
+                buf, acc = ctx.sink.claim(x.device)
+                conv_dgrad(d2, dyp, (wp, wt), None, buf.data_ptr(), accumulate=acc)
+            else:
+                dx = empty_act(N, C, H, W, x.dtype, x.device)
+                conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr())
         if ctx.needs_input_grad[1]:
             dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
         if has_b and ctx.needs_input_grad[2]:
@@ -1338,6 +1344,31 @@ def _adjacent_slices(grads, sizes, dtype):
     return torch.as_strided(g0, (n, off, h, w), g0.stride(), g0.storage_offset())
 
 
+class GradSink:
+    """Gradient destination shared by the views of one FanOutFn: a consumer whose backward can accumulate in its
+    epilogue (Conv2dFn's dgrad) writes its input gradient here — the first one plainly, later ones accumulating —
+    and hands autograd None, so FanOutFn sums one gradient fewer (per conv consumer: a 2-read + 1-write pass and a
+    launch become one extra read in the dgrad epilogue). Single stream, so the order is autograd's."""
+    __slots__ = ("buf", "shape", "dtype")
+
+    def __init__(self, shape, dtype):
+        self.buf, self.shape, self.dtype = None, tuple(shape), dtype
+
+    def fits(self, t):
+        return t is not None and tuple(t.shape) == self.shape and t.dtype == self.dtype
+
+    def claim(self, device):
+        """(NHWC gradient buffer, accumulate flag) for the next consumer."""
+        if self.buf is None:
+            N, C, H, W = self.shape
+            self.buf = empty_act(N, C, H, W, self.dtype, device)
+            return self.buf, 0
+        return self.buf, 1
+
+
+_FANOUT_SINK = bool(int(__import__("os").environ.get("ADR_FANOUT_SINK", "1")))
+
+
 class FanOutFn(torch.autograd.Function):
     """x used by n consumers, as n views. Backward sums the n gradients with HIP launches (one for 2 or 3 of
     them) — into one that is an exclusive concat-gradient slice when there is one (no new buffer, and the split
@@ -1345,17 +1376,22 @@ class FanOutFn(torch.autograd.Function):
     is one PyTorch add per extra consumer (a slow strided kernel on channel slices)."""
 
     @staticmethod
-    def forward(ctx, x, n):
+    def forward(ctx, x, n, sink):
         ctx.set_materialize_grads(False)
+        ctx.sink = sink
         return tuple(x[:, :] for _ in range(n))
 
     @staticmethod
     def backward(ctx, *grads):
         gs = [g for g in grads if g is not None]
+        sink = ctx.sink
+        if sink is not None and sink.buf is not None:  # the consumers that accumulated into the shared buffer
+            gs.append(sink.buf)
+            sink.buf = None
         if not gs:
-            return None, None
+            return None, None, None
         if len(gs) == 1:
-            return gs[0], None
+            return gs[0], None, None
         dt = gs[0].dtype
         gs = [g if g.dtype == dt else g.to(dt) for g in gs]
         excl = [g for g in gs if getattr(g, "_adr_excl", False) and _v(g)[0] is g]
@@ -1373,7 +1409,7 @@ class FanOutFn(torch.autograd.Function):
                 else:
                     _ew(EW_COPY, va, _v(rest[0]), accumulate=1)
                     rest = rest[1:]
-            return acc, None
+            return acc, None, None
         out = _new_like(_v(gs[0])[0])
         vo = (out, out.data_ptr(), out.shape[1])
         if len(gs) >= 3:
@@ -1389,12 +1425,18 @@ class FanOutFn(torch.autograd.Function):
             else:
                 _ew(EW_COPY, vo, _v(rest[0]), accumulate=1)
                 rest = rest[1:]
-        return out, None
+        return out, None, None
 
 
 def fanout(x, n=2):
-    """n views of x whose gradients are summed by libadr (see FanOutFn)."""
-    return FanOutFn.apply(x, n)
+    """n views of x whose gradients are summed by libadr (see FanOutFn); conv consumers deliver theirs through a
+    shared GradSink."""
+    sink = GradSink(x.shape, x.dtype) if _FANOUT_SINK else None
+    outs = FanOutFn.apply(x, n, sink)
+    if sink is not None:
+        for o in outs:
+            o._adr_sink = sink
+    return outs
 
 
 class AddFn(torch.autograd.Function):
