@@ -820,7 +820,7 @@ class Conv2dFn(torch.autograd.Function):
     """y = conv2d(x, w) + b (dense, groups=1). Optionally also returns per-tile BN partial statistics."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, want_stats, cpad):
+    def forward(ctx, x, w, b, stride, pad, want_stats, cpad, box=None):
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         sink = getattr(x, "_adr_sink", None)
         ctx.sink = sink if sink is not None and sink.fits(x) else None
@@ -833,8 +833,9 @@ class Conv2dFn(torch.autograd.Function):
             raise RuntimeError(f"Conv2dFn: input has {C} channels, weight expects {Cw} (padded {Cp})")
         wp, wt = pack_weight2(w, dtype, cpad)
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
-        d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, K, dtype)
-        y = empty_act(N, K, Ho, Wo, dtype, x.device)
+        Ho, Wo = (H + 2 * ph - R) // sh + 1, (W + 2 * pw - S) // sw + 1
+        y, yp, ycs = _out_view(box, N, K, Ho, Wo, dtype, x.device)  # a concat slice when the caller boxes one
+        d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, ycs, dtype)
         stats = None
         if want_stats:
             tiles = (lib.adr_conv2d_fwd_bf16_stat_tiles if _engine2(d, d.c) else lib.adr_conv2d_fwd_stat_tiles)(
@@ -848,21 +849,21 @@ class Conv2dFn(torch.autograd.Function):
             if want_stats:  # the fp8 engine tiles every geometry by 128 output rows
                 stats = torch.empty(lib.adr_conv2d_fwd_fp8_stat_tiles(ctypes.byref(d)) * 2 * K, dtype=torch.float32,
                                     device=x.device)
-            conv_fwd_fp8(d, xp, w, Cw, Cp, bf, y.data_ptr(), stats)
+            conv_fwd_fp8(d, xp, w, Cw, Cp, bf, yp, stats)
         else:
-            conv_fwd(d, xp, wp.data_ptr(), fptr(bf), y.data_ptr(), fptr(stats))
+            conv_fwd(d, xp, wp.data_ptr(), fptr(bf), yp, fptr(stats))
         ctx.save_for_backward(x, wp, wt)
         ctx.meta = (stride, pad, cpad, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
         if stats is None:
             stats = torch.empty(0, device=x.device)
         ctx.mark_non_differentiable(stats)
-        return y, stats
+        return (y if box is None else y[:, :]), stats
 
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         x, wp, wt = ctx.saved_tensors
         stride, pad, cpad, wshape, has_b = ctx.meta
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
@@ -884,7 +885,7 @@ class Conv2dFn(torch.autograd.Function):
             dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
         if has_b and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, K, N, Ho * Wo, dycs, ctx.pb)
-        return dx, dw, db, None, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 class ConvT2dFn(torch.autograd.Function):
@@ -1162,8 +1163,9 @@ def image_to_nhwc(img: torch.Tensor, dtype, cpad=8):
 # ---------------------------------------------------------------------------------------------------------
 
 
-def conv2d(x, w, b=None, stride=1, pad=0, want_stats=False, cpad=0):
-    y, stats = Conv2dFn.apply(x, w, b, stride, pad, want_stats, cpad)
+def conv2d(x, w, b=None, stride=1, pad=0, want_stats=False, cpad=0, out=None):
+    """y = conv2d(x, w) (+b); with `out` (an NHWC channel slice of a concat buffer) y is written into it."""
+    y, stats = Conv2dFn.apply(x, w, b, stride, pad, want_stats, cpad, None if out is None else OutBox(out))
     return y, stats
 
 
@@ -1558,20 +1560,20 @@ class ScaleFn(torch.autograd.Function):
     """x * g (+ res) with g a device tensor broadcast as: 'scalar' (shape ()), 'n' (N,), 'c' (C,), 'nc' (N, C)."""
 
     @staticmethod
-    def forward(ctx, x, g, res, mode):
+    def forward(ctx, x, g, res, mode, box=None):
         vx = _v(x)
         N, C, H, W = x.shape
         gs = g.detach().float().contiguous()
         gns, gcs = {"scalar": (0, 0), "n": (1, 0), "c": (0, 1), "nc": (C, 1)}[mode]
-        out = _new_like(vx[0])
+        out, op, ocs = _out_view(box, N, C, H, W, x.dtype, x.device)
         vr = _v(res) if res is not None else None
         lib.adr_bcast_mul(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], fptr(gs), gns, gcs,
-                          ctypes.c_void_p(vr[1]) if vr else None, vr[2] if vr else 0, ctypes.c_void_p(out.data_ptr()),
-                          C, N, H * W, C, 0, stream())
+                          ctypes.c_void_p(vr[1]) if vr else None, vr[2] if vr else 0, ctypes.c_void_p(op),
+                          ocs, N, H * W, C, 0, stream())
         ctx.save_for_backward(vx[0], gs)
         ctx.meta = (mode, g.shape, res is not None)
         ctx.pg = g
-        return out
+        return out if box is None else out[:, :]
 
     @staticmethod
     def backward(ctx, dy):
@@ -1589,11 +1591,11 @@ class ScaleFn(torch.autograd.Function):
             sum_n = mode in ("scalar", "c")
             sum_c = mode in ("scalar", "n")
             dg = sink(ctx.pg, _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape))
-        return dx, dg, (dy if has_res else None), None
+        return dx, dg, (dy if has_res else None), None, None
 
 
-def scale(x, g, mode, res=None):
-    return ScaleFn.apply(x, g, res, mode)
+def scale(x, g, mode, res=None, out=None):
+    return ScaleFn.apply(x, g, res, mode, None if out is None else OutBox(out))
 
 
 class WeightedSumFn(torch.autograd.Function):
@@ -1680,16 +1682,16 @@ def fusion(fw, xs):
 
 class MaxPoolFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, k):
+    def forward(ctx, x, k, box=None):
         vx = _v(x)
         N, C, H, W = x.shape
-        y = _new_like(vx[0])
+        y, yp, ycs = _out_view(box, N, C, H, W, x.dtype, x.device)
         arg = torch.empty(N * H * W * C, dtype=torch.uint8, device=x.device)
-        lib.adr_maxpool(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(y.data_ptr()), C, fptr(arg),
+        lib.adr_maxpool(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(yp), ycs, fptr(arg),
                         N, H, W, C, k, stream())
         ctx.save_for_backward(arg)
         ctx.meta = (k, x.shape, x.dtype)
-        return y
+        return y if box is None else y[:, :]
 
     @staticmethod
     def backward(ctx, dy):
@@ -1700,11 +1702,11 @@ class MaxPoolFn(torch.autograd.Function):
         dx = empty_act(N, C, H, W, dtype, dy.device)
         lib.adr_maxpool_bwd(dcode(dtype), ctypes.c_void_p(vd[1]), vd[2], fptr(arg), ctypes.c_void_p(dx.data_ptr()), C,
                             N, H, W, C, k, 0, stream())
-        return dx, None
+        return dx, None, None
 
 
-def maxpool(x, k):
-    return MaxPoolFn.apply(x, k)
+def maxpool(x, k, out=None):
+    return MaxPoolFn.apply(x, k, None if out is None else OutBox(out))
 
 
 class MLCAFn(torch.autograd.Function):

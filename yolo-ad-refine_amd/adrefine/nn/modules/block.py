@@ -110,11 +110,15 @@ class SPPF(nn.Module):
         self.k = k
 
     def forward(self, x):
-        y = [self.cv1(x)]
-        for _ in range(3):
+        # cv1 and the three pools write straight into their slices of the concat buffer (no copies)
+        N, _, H, W = x.shape
+        c_ = self.cv1.conv.out_channels
+        buf = K.empty_act(N, 4 * c_, H, W, x.dtype, x.device)
+        y = [self.cv1(x, out=buf[:, :c_])]
+        for i in range(3):
             y[-1], feed = K.fanout(y[-1])
-            y.append(K.maxpool(feed, self.k))
-        return self.cv2(K.cat(y))
+            y.append(K.maxpool(feed, self.k, out=buf[:, (i + 1) * c_:(i + 2) * c_]))
+        return self.cv2(K.cat(y, out=buf))
 
 
 class MLCA(nn.Module):

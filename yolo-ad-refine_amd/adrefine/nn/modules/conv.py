@@ -44,11 +44,12 @@ def _in_pad(x, w):
 class Conv2d(nn.Conv2d):
     """nn.Conv2d drop-in (dense, dilation 1). Used for the yaml `nn.Conv2d` rows (tasks.py:1016)."""
 
-    def forward(self, x):
+    def forward(self, x, out=None):
         if self.groups != 1 or self.dilation != (1, 1) or self.stride[0] != self.stride[1] or \
                 self.padding[0] != self.padding[1]:
             raise NotImplementedError("adrefine Conv2d: grouped / dilated / anisotropic convs use DWConv kernels")
-        y, _ = K.conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], False, _in_pad(x, self.weight))
+        y, _ = K.conv2d(x, self.weight, self.bias, self.stride[0], self.padding[0], False, _in_pad(x, self.weight),
+                        out=out)
         return y
 
 

@@ -150,10 +150,14 @@ class CrossTaskInteraction(nn.Module):
     def forward(self, cls_feat, reg_feat):
         cf = list(K.fanout(cls_feat, 3))
         rf = list(K.fanout(reg_feat, 3))
-        c2r = list(K.fanout(self.cls_to_reg(cf[0])))
-        r2c = list(K.fanout(self.reg_to_cls(rf[0])))
-        cg = K.act(self.cls_gate[0](K.cat([cf[1], r2c[0]])), "sigmoid")
-        rg = K.act(self.reg_gate[0](K.cat([rf[1], c2r[0]])), "sigmoid")
+        # the gates' concat inputs: the cross convs write their halves in place (one copy per concat, not two)
+        N, C, H, W = cls_feat.shape
+        bc = K.empty_act(N, 2 * C, H, W, cls_feat.dtype, cls_feat.device)
+        br = K.empty_act(N, 2 * C, H, W, reg_feat.dtype, reg_feat.device)
+        c2r = list(K.fanout(self.cls_to_reg(cf[0], out=br[:, C:])))
+        r2c = list(K.fanout(self.reg_to_cls(rf[0], out=bc[:, C:])))
+        cg = K.act(self.cls_gate[0](K.cat([cf[1], r2c[0]], out=bc)), "sigmoid")
+        rg = K.act(self.reg_gate[0](K.cat([rf[1], c2r[0]], out=br)), "sigmoid")
         return K.fma(cf[2], r2c[1], cg), K.fma(rf[2], c2r[1], rg)
 
 
@@ -191,8 +195,8 @@ class Scale(nn.Module):
         super().__init__()
         self.scale = nn.Parameter(torch.tensor(scale, dtype=torch.float))
 
-    def forward(self, x):
-        return K.scale(x, self.scale, "scalar")
+    def forward(self, x, out=None):
+        return K.scale(x, self.scale, "scalar", out=out)
 
 
 class ResidualBlockGN(nn.Module):
@@ -264,9 +268,12 @@ class AYHead1(nn.Module):
         c0, c2 = self.cls_prob_conv[0], self.cls_prob_conv[2]
         cp = K.act(K.conv2d(fv[4], c0.weight, c0.bias, 1, 0)[0], "relu")
         cp = K.act(K.padded_conv2d(cp, c2.weight, c2.bias, 1, 1, 8), "sigmoid")  # channel 0 valid
-        reg_out = self.scale[i](self.cv2(r))
-        cls_out = self.cv3(K.mul_pixel(cls_e, cp))
-        return K.cat([reg_out, cls_out])
+        # both halves of the level's output row written in place into one buffer (no concat copies)
+        N, _, H, W = r.shape
+        buf = K.empty_act(N, 4 * self.reg_max + self.nc, H, W, r.dtype, r.device)
+        reg_out = self.scale[i](self.cv2(r), out=buf[:, :4 * self.reg_max])
+        cls_out = self.cv3(K.mul_pixel(cls_e, cp), out=buf[:, 4 * self.reg_max:])
+        return K.cat([reg_out, cls_out], out=buf)
 
     def forward(self, x):
         outputs = [self._level(x[i], i) for i in range(self.nl)]
