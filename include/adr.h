@@ -65,6 +65,12 @@ int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w_krs
 int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
                           int accumulate, void* stream);
 int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d);
+/* Eval Conv-BN-act in one launch: y = act(conv(x, w_krsc) * scale + shift) on the bf16 engine, the BatchNorm's
+ * running-statistics affine (scale/shift from adr_bn_finalize with training = 0) and the activation applied to the
+ * fp32 accumulator before the bf16 store. Replaces the reference predictor's fused Conv.forward_fuse
+ * (nn/modules/conv.py:52-54, after utils/torch_utils.py:fuse_conv_and_bn); no bias, statistics or accumulation. */
+int adr_conv2d_fwd_bf16_act(const adr_conv_desc* d, const void* x, const void* w_krsc, const float* scale,
+                            const float* shift, int act, void* y, void* stream);
 /* fp8 (OCP e4m3) forward conv for BASELINE.json configs[4] (l-scale "fp8 MFMA conv path"), replacing the same
  * nn.Conv2d forward as adr_conv2d_fwd_bf16 (nn/modules/conv.py:44-50) on v_mfma_scale_f32_16x16x128_f8f6f4.
  * Delayed per-tensor activation scaling: sa = 448 / max(amax_part[0 .. adr_fp8_amax_blocks())) — last step's

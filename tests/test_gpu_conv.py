@@ -184,3 +184,45 @@ def test_conv_anisotropic_pad_bf16(shape, k, pad):
     rel = lambda a, b: float((a.float() - b).norm() / b.norm())  # noqa: E731
     assert rel(y, yr) < 1e-2 and rel(xd.grad, xr.grad) < 1e-2 and rel(w.grad, wr.grad) < 1e-2, \
         (rel(y, yr), rel(xd.grad, xr.grad), rel(w.grad, wr.grad))
+
+
+@pytest.mark.parametrize("act", [True, False])
+@pytest.mark.parametrize("c1,c2,k,s,hw", [(16, 32, 3, 2, 24), (32, 64, 1, 1, 20), (64, 128, 3, 1, 13),
+                                           (128, 256, 3, 2, 20), (48, 16, 1, 1, 9), (64, 64, 3, 1, 16),
+                                           (64, 128, 3, 1, 24), (32, 64, 3, 1, 40), (64, 32, 3, 1, 16),
+                                           (128, 192, 1, 1, 10)])
+def test_conv_bn_act_eval_fused(act, c1, c2, k, s, hw):
+    """Inference Conv-BN-act in one launch (adr_conv2d_fwd_bf16_act; conv_bf16_act_kernel / conv3_act_kernel):
+    against a torch fp32 Conv2d -> BatchNorm2d(eval) -> SiLU on the same bf16-rounded operands (bound: 1.5 % of the
+    output's max |value|, a few bf16 ulps) and against the unfused HIP pair (conv, then BN + act on the bf16
+    conv output), also written into a concat slice through out=."""
+    import adrefine.kernels as K
+    from adrefine.nn.modules import Conv
+    torch.manual_seed(0)
+    m = Conv(c1, c2, k, s, act=act)
+    load_recipe_into(m)
+    with torch.no_grad():  # non-trivial running statistics
+        m.bn.running_mean.copy_(torch.randn(c2) * 0.3)
+        m.bn.running_var.copy_(torch.rand(c2) * 2 + 0.2)
+    m = m.cuda().eval()
+    x = seeded_randn(2, c1, hw, hw, seed=7).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = m(x)
+        K.EVAL_CONV_BN_ACT = False
+        try:
+            y_pair = m(x)
+        finally:
+            K.EVAL_CONV_BN_ACT = True
+        buf = torch.zeros(2, *y.shape[2:], c2 + 16, device="cuda", dtype=torch.bfloat16).permute(0, 3, 1, 2)
+        y_out = m(x, out=buf[:, 8:8 + c2])
+        ref = torch.nn.functional.conv2d(x.float(), m.conv.weight.to(torch.bfloat16).float(), None, s, k // 2)
+        ref = torch.nn.functional.batch_norm(ref, m.bn.running_mean, m.bn.running_var, m.bn.weight, m.bn.bias,
+                                             False, 0.0, m.bn.eps)
+        if act:
+            ref = torch.nn.functional.silu(ref)
+    scale = float(ref.abs().max())
+    err = float((y.float() - ref).abs().max()) / scale
+    err_pair = float((y.float() - y_pair.float()).abs().max()) / scale
+    assert err <= 0.015 and err_pair <= 0.02, (err, err_pair)
+    assert torch.equal(y_out, y) and torch.equal(buf[:, 8:8 + c2], y)
+    assert float(buf[:, :8].abs().max()) == 0 and float(buf[:, 8 + c2:].abs().max()) == 0

@@ -30,11 +30,14 @@ class FusedPredictor:
         self.graph = None
         self.static_in = None
         self.static_out = None
-        self.packs = K.PackCache()  # bf16 conv operands packed once, not per batch (weights are fixed here)
+        # bf16 conv operands and the eval BatchNorm scale/shift computed once, not per batch (weights are fixed here)
+        self.packs = K.PackCache(cache_bn_coefs=True)
 
     def sync_weights(self):
-        """Repack the bf16 conv operands after the model's weights changed (e.g. between training epochs)."""
+        """Repack the bf16 conv operands and recompute the eval BatchNorm coefficients after the model's weights or
+        running statistics changed (e.g. between training epochs)."""
         self.packs.pack_all()
+        self.packs.refresh_bn_coefs()
 
     def _run(self, img):
         with torch.no_grad(), K.pack_scope(self.packs):

@@ -460,12 +460,20 @@ class PackCache:
 
     CHUNK = 1 << 13
 
-    def __init__(self):
+    def __init__(self, cache_bn_coefs=False):
         self.specs = {}
         self.valid = False
         self.table = None
         self.nchunks = 0
         self.tab_dev = None
+        # eval Conv-BN-act: the running-statistics scale/shift per BatchNorm, computed once and refreshed by
+        # refresh_bn_coefs() (the predictor's sync_weights) — only where the owner guarantees fixed weights
+        self.cache_bn_coefs = cache_bn_coefs
+        self.bn_coefs = {}
+
+    def refresh_bn_coefs(self):
+        for bn, scale, shift in self.bn_coefs.values():
+            _bn_eval_coefs_into(bn, scale, shift)
 
     def _build(self):
         import numpy as np
@@ -1194,6 +1202,64 @@ def _out_view(box, N, C, H, W, dtype, dev):
     if z is not box.t:
         raise RuntimeError("out view is not an NHWC channel slice")
     return z, ptr, cs
+
+
+def _bn_eval_coefs_into(bn, scale, shift):
+    C = scale.numel()
+    lib.adr_bn_finalize(None, 0, C, 1.0, fptr(bn.weight.detach()), fptr(bn.bias.detach()), fptr(bn.running_mean),
+                        fptr(bn.running_var), float(bn.momentum), float(bn.eps), 0, fptr(scale), fptr(shift), None,
+                        None, stream())
+
+
+def _bn_eval_coefs(bn, dev):
+    """(scale, shift) of BatchNorm2d with running statistics (one adr_bn_finalize launch, or the predictor's
+    cached pair)."""
+    pc = _PACK
+    if pc is not None and pc.cache_bn_coefs:
+        hit = pc.bn_coefs.get(id(bn))
+        if hit is not None and hit[0] is bn:
+            return hit[1], hit[2]
+    C = bn.num_features
+    scale = torch.empty(C, dtype=torch.float32, device=dev)
+    shift = torch.empty(C, dtype=torch.float32, device=dev)
+    _bn_eval_coefs_into(bn, scale, shift)
+    if pc is not None and pc.cache_bn_coefs:
+        pc.bn_coefs[id(bn)] = (bn, scale, shift)
+    return scale, shift
+
+
+EVAL_CONV_BN_ACT = bool(int(__import__("os").environ.get("ADR_EVAL_FUSE", "1")))  # 0: conv, then BN + act
+
+
+def conv_bn_act_eval(x, w, stride, pad, bn, act: str, cpad=0, out=None):
+    """Inference Conv-BN-act (no autograd): act(BN_eval(conv2d(x, w))) in ONE bf16-engine launch — the BatchNorm
+    affine and the activation run on the fp32 accumulator in the conv epilogue (adr_conv2d_fwd_bf16_act), as the
+    reference predictor runs Conv.forward_fuse after fuse_conv_and_bn (nn/modules/conv.py:52-54,
+    nn/tasks.py:203-218). Returns None when the contraction is not on the bf16 engine (the caller then runs the
+    unfused pair)."""
+    dtype = x.dtype
+    if dtype != torch.bfloat16 or torch.is_grad_enabled():
+        return None
+    x, xp, xcs = nhwc(x)
+    N, C, H, W = x.shape
+    K, Cw, R, S = w.shape
+    Cp = max(Cw, cpad)
+    if C != Cp:
+        raise RuntimeError(f"conv_bn_act_eval: input has {C} channels, weight expects {Cw} (padded {Cp})")
+    (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+    Ho, Wo = (H + 2 * ph - R) // sh + 1, (W + 2 * pw - S) // sw + 1
+    y, yp, ycs = _out_view(None if out is None else OutBox(out), N, K, Ho, Wo, dtype, x.device)
+    d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, ycs, dtype)
+    if not _engine2(d, d.c) or (CONV_FP8 and C >= _FP8_MIN_C and R * S > 1):
+        return None
+    wp, _ = pack_weight2(w, dtype, cpad)
+    scale, shift = _bn_eval_coefs(bn, x.device)
+    sym = "" if _TIMING is None else _conv2_symbol(d, False).replace("conv_bf16_kernel", "conv_bf16_act_kernel")
+    tok = _t0(sym, *_conv_work(d), _shape(d, "fwd+bn+act") if _TIMING is not None else "")
+    lib.adr_conv2d_fwd_bf16_act(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(wp.data_ptr()), fptr(scale),
+                                fptr(shift), ACT[act], ctypes.c_void_p(yp), stream())
+    _t1(tok)
+    return y if out is None else out
 
 
 def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None):

@@ -85,6 +85,11 @@ class Conv(nn.Module):
                     and cv.kernel_size == (k, k) and cv.padding == (k // 2, k // 2)):
                 raise NotImplementedError("adrefine Conv: grouped convs are depthwise, stride 1, 'same' padding")
             return K.bn_act(K.dwconv(x, cv.weight, None, k), None, self.bn, self.act_name, self.training, out=out)
+        if not self.training and K.EVAL_CONV_BN_ACT:  # inference: BN + act in the conv epilogue (forward_fuse)
+            z = K.conv_bn_act_eval(x, cv.weight, cv.stride[0], cv.padding[0], self.bn, self.act_name,
+                                   _in_pad(x, cv.weight), out=out)
+            if z is not None:
+                return z
         y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight))
         return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out)
 

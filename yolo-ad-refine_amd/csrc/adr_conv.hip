@@ -40,9 +40,27 @@ struct ConvArgs {
   int ntiles;
   int accumulate;
   int src_bytes, wt_bytes;     // extents of src / wt (buffer-load range checks; < 2^31)
+  // eval Conv-BN-act epilogue (adr_conv2d_fwd_bf16_act): out = act(acc * escale[col] + eshift[col]), the
+  // BatchNorm with running statistics and the activation applied to the fp32 accumulator (null: acc + bias)
+  const float* escale;
+  const float* eshift;
+  int eact;
 };
 
 constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
+
+// the eval epilogue's activation (block-uniform code; 0 = none keeps the plain acc + bias path: fma by 1 is exact).
+// bf16 output: the hardware exp/rcp sigmoid, as the bf16 affine_act kernels use
+__device__ __forceinline__ float epi_act(int act, float v) {
+  switch (act) {
+    case ACT_SILU: return act_fwd_c<ACT_SILU, true>(v);
+    case ACT_SIGMOID: return act_fwd_c<ACT_SIGMOID, true>(v);
+    case ACT_RELU: return act_fwd_c<ACT_RELU>(v);
+    case ACT_GELU: return act_fwd_c<ACT_GELU>(v);
+    case ACT_HSWISH: return act_fwd_c<ACT_HSWISH>(v);
+    default: return v;
+  }
+}
 
 // XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin over the 8 XCDs (each with
 // its own L2), so the column tiles of one row tile — which read the same A rows — would land on different XCDs
@@ -52,8 +70,8 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
   return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
 }
 
-template <int BN, int MODE>
-__global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvArgs a) {
+template <int BN, int MODE, bool EPI>
+__device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
   constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
   constexpr int WROWS = CBM / WAVES_M, WCOLS = BN / WAVES_N;
   constexpr int TM = WROWS / 16, TN = WCOLS / 16;
@@ -302,11 +320,16 @@ __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvAr
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = wc0 + j * 16 + (lane & 15);
-    const float b = (a.bias && n0 + col < a.N) ? a.bias[n0 + col] : 0.f;
+    const bool cok = n0 + col < a.N;
+    const float b = (a.bias && cok) ? a.bias[n0 + col] : 0.f;
+    const float es = EPI && cok ? a.escale[n0 + col] : 1.f;
+    const float eb = EPI && cok ? a.eshift[n0 + col] + b : b;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Os[(wr0 + i * 16 + 4 * (lane >> 4) + e) * OPITCH + col] = (__bf16)(acc[i][j][e] + b);
+      for (int e = 0; e < 4; ++e)
+        Os[(wr0 + i * 16 + 4 * (lane >> 4) + e) * OPITCH + col] = 
+            (__bf16)(EPI ? epi_act(a.eact, fmaf(acc[i][j][e], es, eb)) : acc[i][j][e] + b);
   }
   __syncthreads();
   constexpr int CPR = BN / 8;          // 16-byte chunks per row
@@ -372,8 +395,8 @@ constexpr int C3_CK = 32, C3_LD = C3_CK;  // chunk channels; unpadded 64-byte LD
 // group reads cover 16 disjoint bank quads (48 KB per block: 3 blocks per CU)
 __device__ __forceinline__ int c3_swz(int row, int kq) { return row * C3_LD + ((kq ^ ((row >> 2) & 3)) << 3); }
 
-template <int TW, bool DG, int BN>
-__global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
+template <int TW, bool DG, int BN, bool EPI>
+__device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   constexpr int TH = 128 / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
   constexpr int A_TOT = NPIX * (C3_CK / 8), A_CH = (A_TOT + 255) / 256;
   constexpr int TPP = 256 / (BN * (C3_CK / 8));      // taps per pass of the 256 threads over the weight slab
@@ -482,11 +505,16 @@ __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = j * 16 + (lane & 15);
-    const float b = (a.bias && n0 + col < a.N) ? a.bias[n0 + col] : 0.f;
+    const bool cok = n0 + col < a.N;
+    const float b = (a.bias && cok) ? a.bias[n0 + col] : 0.f;
+    const float es = EPI && cok ? a.escale[n0 + col] : 1.f;
+    const float eb = EPI && cok ? a.eshift[n0 + col] + b : b;
 #pragma unroll
     for (int i = 0; i < TM; ++i)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Os[(wr0 + i * 16 + 4 * (lane >> 4) + e) * OPITCH + col] = (__bf16)(acc[i][j][e] + b);
+      for (int e = 0; e < 4; ++e)
+        Os[(wr0 + i * 16 + 4 * (lane >> 4) + e) * OPITCH + col] = 
+            (__bf16)(EPI ? epi_act(a.eact, fmaf(acc[i][j][e], es, eb)) : acc[i][j][e] + b);
   }
   __syncthreads();
   const int oc = tid % CPR, orow = tid / CPR;
@@ -537,6 +565,17 @@ __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) {
   }
 }
 
+// entry points (the bodies are shared; the eval Conv-BN-act variants are separate symbols so the training
+// kernels keep their code and register allocation)
+template <int BN, int MODE>
+__global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvArgs a) { conv_bf16_body<BN, MODE, false>(a); }
+template <int BN>
+__global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_act_kernel(ConvArgs a) { conv_bf16_body<BN, CV_FWD, true>(a); }
+template <int TW, bool DG, int BN>
+__global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) { conv3_body<TW, DG, BN, false>(a); }
+template <int TW, int BN>
+__global__ void __launch_bounds__(256, 3) conv3_act_kernel(ConvArgs a) { conv3_body<TW, false, BN, true>(a); }
+
 // tile width of the 3x3 path for this geometry, or 0 when it does not apply
 static int conv3_tw(const adr_conv_desc* d, int red_ch, int out_ch) {
   if (d->r != 3 || d->s != 3 || d->stride_h != 1 || d->pad_h != 1 || red_ch % C3_CK || out_ch % 32) return 0;
@@ -552,6 +591,16 @@ template <bool DG>
 static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hipStream_t st) {
   g.ntiles = g.N / bn;
   dim3 grid(conv3_tiles(d, tw) * g.ntiles);
+  if (!DG && g.escale) {
+    if (bn == 64) {
+      if (tw == 16) hipLaunchKernelGGL((conv3_act_kernel<16, 64>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((conv3_act_kernel<8, 64>), grid, dim3(256), 0, st, g);
+    } else {
+      if (tw == 16) hipLaunchKernelGGL((conv3_act_kernel<16, 32>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((conv3_act_kernel<8, 32>), grid, dim3(256), 0, st, g);
+    }
+    return;
+  }
   if (bn == 64) {
     if (tw == 16) hipLaunchKernelGGL((conv3_kernel<16, DG, 64>), grid, dim3(256), 0, st, g);
     else hipLaunchKernelGGL((conv3_kernel<8, DG, 64>), grid, dim3(256), 0, st, g);
@@ -563,6 +612,15 @@ static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hi
 
 template <int MODE>
 static void launch_conv(int bn, dim3 grid, const ConvArgs& g, hipStream_t st) {
+  if (MODE == CV_FWD && g.escale) {
+    switch (bn) {
+      case 16: hipLaunchKernelGGL((conv_bf16_act_kernel<16>), grid, dim3(256), 0, st, g); break;
+      case 32: hipLaunchKernelGGL((conv_bf16_act_kernel<32>), grid, dim3(256), 0, st, g); break;
+      case 64: hipLaunchKernelGGL((conv_bf16_act_kernel<64>), grid, dim3(256), 0, st, g); break;
+      default: hipLaunchKernelGGL((conv_bf16_act_kernel<128>), grid, dim3(256), 0, st, g); break;
+    }
+    return;
+  }
   switch (bn) {
     case 16: hipLaunchKernelGGL((conv_bf16_kernel<16, MODE>), grid, dim3(256), 0, st, g); break;
     case 32: hipLaunchKernelGGL((conv_bf16_kernel<32, MODE>), grid, dim3(256), 0, st, g); break;
@@ -611,12 +669,14 @@ static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad) {
 
 using namespace adr;
 
-extern "C" int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
-                                   float* stats, int accumulate, void* stream) {
+static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                         float* stats, int accumulate, const float* escale, const float* eshift, int eact,
+                         void* stream) {
   int rc = conv_check(d);
   if (rc) return rc;
   ConvArgs g{};
   g.src = (const __bf16*)x; g.wt = (const __bf16*)w; g.out = (__bf16*)y; g.bias = bias; g.stats = stats;
+  g.escale = escale; g.eshift = eshift; g.eact = escale ? eact : 0;
   g.n = d->n; g.sh_ = d->h; g.sw_ = d->w; g.scs = d->x_cstride; g.sco = d->x_coff; g.sc = d->c;
   g.rh = d->ho; g.rw = d->wo; g.ocs = d->y_cstride; g.oco = d->y_coff;
   g.r = d->r; g.s = d->s; g.str = d->stride_h; g.ph = d->pad_h; g.pw = d->pad_w;
@@ -633,6 +693,20 @@ extern "C" int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const 
   dim3 grid(cdiv((long)d->n * d->ho * d->wo, CBM) * g.ntiles);
   launch_conv<CV_FWD>(bn, grid, g, (hipStream_t)stream);
   return check_launch("adr_conv2d_fwd_bf16");
+}
+
+extern "C" int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
+                                   float* stats, int accumulate, void* stream) {
+  return conv_fwd_impl(d, x, w, bias, y, stats, accumulate, nullptr, nullptr, 0, stream);
+}
+
+// Eval Conv-BN-act (reference: the predictor's fused Conv.forward_fuse, nn/modules/conv.py:52-54 after
+// fuse_conv_and_bn): y = act(conv(x, w) * scale + shift) in one launch, scale/shift from adr_bn_finalize with
+// training = 0. Same dispatch as adr_conv2d_fwd_bf16 (bias-free, no statistics, no accumulation).
+extern "C" int adr_conv2d_fwd_bf16_act(const adr_conv_desc* d, const void* x, const void* w, const float* scale,
+                                       const float* shift, int act, void* y, void* stream) {
+  ADR_REQUIRE(scale && shift && act >= ACT_NONE && act <= ACT_HSWISH, "conv fwd act: scale/shift/act");
+  return conv_fwd_impl(d, x, w, nullptr, y, nullptr, 0, scale, shift, act, stream);
 }
 
 extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias,

@@ -103,23 +103,44 @@ __global__ void __launch_bounds__(256) nc_reduce_kernel(const T* __restrict__ x,
   }
 }
 
-// block per channel: deterministic tree over P partial rows in double
+// block per channel: deterministic fixed-order sum over P partial rows in double. Each thread keeps four rows in
+// flight (the finalize kernels are latency-bound: P is a few hundred rows on most layers), then a wave butterfly
+// and one LDS exchange across the four waves.
 __device__ __forceinline__ void block_sum2(double& a, double& b) {
-  __shared__ double sa[256], sb[256];
-  int t = threadIdx.x;
-  sa[t] = a;
-  sb[t] = b;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (t < o) {
-      sa[t] += sa[t + o];
-      sb[t] += sb[t + o];
-    }
-    __syncthreads();
+  __shared__ double sa[4], sb[4];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    a += __shfl_xor(a, o, 64);
+    b += __shfl_xor(b, o, 64);
   }
-  a = sa[0];
-  b = sb[0];
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sa[w] = a;
+    sb[w] = b;
+  }
   __syncthreads();
+  a = (sa[0] + sa[1]) + (sa[2] + sa[3]);
+  b = (sb[0] + sb[1]) + (sb[2] + sb[3]);
+  __syncthreads();
+}
+
+// this thread's share of column c over P rows of [P][2][C] partials: (sum row[c], sum row[C + c])
+__device__ __forceinline__ void col_sums2(const float* __restrict__ partial, int P, int C, int c, double& a, double& b) {
+  double a1 = 0.0, b1 = 0.0, a2 = 0.0, b2 = 0.0, a3 = 0.0, b3 = 0.0;
+  int p = threadIdx.x;
+  for (; p + 768 < P; p += 1024) {
+    const float* r0 = partial + (long)p * 2 * C + c;
+    const long st = 256l * 2 * C;
+    const float x0 = r0[0], y0 = r0[C], x1 = r0[st], y1 = r0[st + C];
+    const float x2 = r0[2 * st], y2 = r0[2 * st + C], x3 = r0[3 * st], y3 = r0[3 * st + C];
+    a += x0; b += y0; a1 += x1; b1 += y1; a2 += x2; b2 += y2; a3 += x3; b3 += y3;
+  }
+  for (; p < P; p += 256) {
+    a += partial[(long)p * 2 * C + c];
+    b += partial[(long)p * 2 * C + C + c];
+  }
+  a = (a + a1) + (a2 + a3);
+  b = (b + b1) + (b2 + b3);
 }
 
 __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ partial, int P, int C, double count,
@@ -132,10 +153,7 @@ __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restric
   double mean, var;
   if (training) {
     double a = 0.0, b = 0.0;
-    for (int p = threadIdx.x; p < P; p += 256) {
-      a += partial[(long)p * 2 * C + c];
-      b += partial[(long)p * 2 * C + C + c];
-    }
+    col_sums2(partial, P, C, c, a, b);
     block_sum2(a, b);
     mean = a / count;
     var = b / count - mean * mean;
@@ -168,10 +186,7 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
                                                               int training, int accumulate) {
   int c = blockIdx.x;
   double a = 0.0, b = 0.0;
-  for (int p = threadIdx.x; p < P; p += 256) {
-    a += partial[(long)p * 2 * C + c];
-    b += partial[(long)p * 2 * C + C + c];
-  }
+  col_sums2(partial, P, C, c, a, b);
   block_sum2(a, b);
   if (threadIdx.x == 0) {
     double mu = mean[c], rs = rstd[c], g = gamma ? gamma[c] : 1.0;
