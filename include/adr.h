@@ -65,6 +65,13 @@ int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w_krs
 int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
                           int accumulate, void* stream);
 int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d);
+/* dx (+)= dgrad(dy, w_crsk) + addend in one launch (bf16 engine): `addend` is an NHWC view shaped like dx with
+ * channel stride addend_cstride, added in the epilogue with a single rounding. Used by the fan-out gradient sink:
+ * a residual add's pass-through gradient (nn/modules/block.py:354 `x + self.cv2(self.cv1(x))`, autograd's
+ * gradient accumulation for a tensor read twice) folds into the first conv consumer's data gradient instead of
+ * an elementwise add of its own. */
+int adr_conv2d_dgrad_bf16_add(const adr_conv_desc* d, const void* dy, const void* w_crsk, void* dx, int accumulate,
+                              const void* addend, int addend_cstride, void* stream);
 /* Eval Conv-BN-act in one launch: y = act(conv(x, w_krsc) * scale + shift) on the bf16 engine, the BatchNorm's
  * running-statistics affine (scale/shift from adr_bn_finalize with training = 0) and the activation applied to the
  * fp32 accumulator before the bf16 store. Replaces the reference predictor's fused Conv.forward_fuse

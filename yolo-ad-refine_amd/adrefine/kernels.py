@@ -433,13 +433,23 @@ def conv_fwd_fp8(d, xp, w, Cw, Cp, bias, yp, stats):
                            fptr(bias), ctypes.c_void_p(yp), fptr(stats), stream())
 
 
-def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0):
-    """dx (+)= conv_transpose(dy, w); wpair = (KRSC, CRSK-or-None) packed weights (pack_weight2)."""
+def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0, addend=None):
+    """dx (+)= conv_transpose(dy, w) (+ addend); wpair = (KRSC, CRSK-or-None) packed weights (pack_weight2).
+    `addend` (an NHWC bf16 view shaped like dx) is added in the bf16 engine's epilogue."""
     krsc, crsk = wpair
     e2 = crsk is not None and _engine2(d, d.k)
     mode = 2 if d.stride_h == 2 else 1
     sym = "" if _TIMING is None else (_conv2_symbol(d, True) if e2 else
                                       _gemm_symbol(d.dtype, _bn_of(d.c), 3 if mode == 2 else 1))
+    if addend is not None:
+        if not e2 or bias is not None:
+            raise RuntimeError("conv_dgrad: an addend needs the bf16 engine and no bias")
+        tok = _t0(sym, *_conv_work(d), _shape(d, "dgrad+add") if _TIMING is not None else "")
+        lib.adr_conv2d_dgrad_bf16_add(ctypes.byref(d), ctypes.c_void_p(dyp), ctypes.c_void_p(crsk.data_ptr()),
+                                      ctypes.c_void_p(dxp), int(accumulate), ctypes.c_void_p(addend.data_ptr()),
+                                      addend.stride(3), stream())
+        _t1(tok)
+        return
     rep = _reps(accumulate)
     tok = _t0(sym, *_conv_work(d), _shape(d, "dgrad") if _TIMING is not None else "", rep)
     for _ in range(rep):
@@ -884,8 +894,10 @@ class Conv2dFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
             if ctx.sink is not None:  # into the fan-out's shared gradient (accumulating after the first consumer)
-                buf, acc = ctx.sink.claim(x.device)
-                conv_dgrad(d2, dyp, (wp, wt), None, buf.data_ptr(), accumulate=acc)
+                buf, acc, add = ctx.sink.claim(x.device, can_add=wt is not None and _engine2(d2, d2.k))
+                if buf.stride(3) != C:  # a seeded concat-gradient slice: the concat's channel stride
+                    d2, _, _ = conv_desc(N, H, W, C, buf.stride(3), K, R, S, sh, sw, ph, pw, dycs, x.dtype)
+                conv_dgrad(d2, dyp, (wp, wt), None, buf.data_ptr(), accumulate=acc, addend=add)
             else:
                 dx = empty_act(N, C, H, W, x.dtype, x.device)
                 conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr())
@@ -1328,16 +1340,19 @@ class CatFn(torch.autograd.Function):
             sizes.append(x.shape[1])
             off += x.shape[1]
         ctx.sizes = sizes
+        # pieces that are fan-out views with a gradient sink: backward can make their slice the sink's buffer
+        ctx.sinks = [getattr(x, "_adr_sink", None) for x in xs]
         return out if box is None else out[:, :]
 
     @staticmethod
     def backward(ctx, dy):
         dy, _, _ = _v(dy)
         outs, off = [], 0
-        for s in ctx.sizes:
+        for s, sk in zip(ctx.sizes, ctx.sinks):
             piece = dy[:, off:off + s]
             piece._adr_excl = True  # a disjoint slice handed to exactly one consumer: FanOutFn may add into it
-            outs.append(piece)
+            # a fan-out view whose conv consumers have not run backward yet: they accumulate into the slice
+            outs.append(None if sk is not None and _side("wgrad") is None and sk.seed(piece) else piece)
             off += s
         return (None,) + tuple(outs)
 
@@ -1417,24 +1432,55 @@ class GradSink:
     epilogue (Conv2dFn's dgrad) writes its input gradient here — the first one plainly, later ones accumulating —
     and hands autograd None, so FanOutFn sums one gradient fewer (per conv consumer: a 2-read + 1-write pass and a
     launch become one extra read in the dgrad epilogue). Single stream, so the order is autograd's."""
-    __slots__ = ("buf", "shape", "dtype")
+    __slots__ = ("buf", "shape", "dtype", "pend")
 
     def __init__(self, shape, dtype):
         self.buf, self.shape, self.dtype = None, tuple(shape), dtype
+        self.pend = []  # pass-through gradients (AddFn's) waiting to be folded into a conv consumer's dgrad
+
+    @staticmethod
+    def _aligned(t):
+        n, c, h, w = t.shape
+        s0, s1, s2, s3 = t.stride()
+        return s1 == 1 and s2 == w * s3 and s0 == h * w * s3 and t.data_ptr() % 16 == 0 and s3 % 8 == 0
+
+    def defer(self, g):
+        """Hold a pass-through gradient (a residual add hands its output gradient unchanged to this input): the next
+        conv consumer to claim the buffer adds it in its dgrad epilogue, FanOutFn adds whatever is left. bf16 only
+        (the bf16 engine's epilogue); `g` is marked so FanOutFn never accumulates into it in place."""
+        if not _DEFER_ADD or g is None or not self.fits(g) or g.dtype != torch.bfloat16 or not self._aligned(g):
+            return False
+        g._adr_pinned = True
+        self.pend.append(g)
+        return True
 
     def fits(self, t):
         return t is not None and tuple(t.shape) == self.shape and t.dtype == self.dtype
 
-    def claim(self, device):
-        """(NHWC gradient buffer, accumulate flag) for the next consumer."""
+    def seed(self, piece):
+        """Make an exclusive concat-gradient slice (CatFn.backward) the shared buffer before any conv consumer
+        has claimed one: the convs then accumulate straight into it and FanOutFn gets one gradient fewer to add
+        (the acc += sink pass). False when a consumer already claimed a buffer or the slice is not an aligned NHWC
+        view the dgrad epilogue can write."""
+        if self.buf is not None or not self.fits(piece) or not _SEED_CAT or not self._aligned(piece):
+            return False
+        self.buf = piece
+        return True
+
+    def claim(self, device, can_add=False):
+        """(NHWC gradient buffer, accumulate flag, addend or None) for the next consumer; with can_add the
+        consumer takes one pending pass-through gradient into its epilogue."""
+        add = self.pend.pop(0) if can_add and self.pend else None
         if self.buf is None:
             N, C, H, W = self.shape
             self.buf = empty_act(N, C, H, W, self.dtype, device)
-            return self.buf, 0
-        return self.buf, 1
+            return self.buf, 0, add
+        return self.buf, 1, add
 
 
 _FANOUT_SINK = bool(int(__import__("os").environ.get("ADR_FANOUT_SINK", "1")))
+_SEED_CAT = bool(int(__import__("os").environ.get("ADR_SEED_CAT", "1")))  # 0: CatFn hands every slice to autograd
+_DEFER_ADD = bool(int(__import__("os").environ.get("ADR_DEFER_ADD", "1")))  # 0: AddFn returns its gradient as is
 
 
 class FanOutFn(torch.autograd.Function):
@@ -1454,15 +1500,24 @@ class FanOutFn(torch.autograd.Function):
         gs = [g for g in grads if g is not None]
         sink = ctx.sink
         if sink is not None and sink.buf is not None:  # the consumers that accumulated into the shared buffer
-            gs.append(sink.buf)
+            # a seeded concat slice (GradSink.seed) goes first: it is the accumulation target below, so x's
+            # gradient stays that slice (SplitFn can then join it with its neighbours without a copy)
+            if getattr(sink.buf, "_adr_excl", False):
+                gs.insert(0, sink.buf)
+            else:
+                gs.append(sink.buf)
             sink.buf = None
+        if sink is not None and sink.pend:  # pass-through gradients no conv consumer took
+            gs.extend(sink.pend)
+            sink.pend = []
         if not gs:
             return None, None, None
         if len(gs) == 1:
             return gs[0], None, None
         dt = gs[0].dtype
         gs = [g if g.dtype == dt else g.to(dt) for g in gs]
-        excl = [g for g in gs if getattr(g, "_adr_excl", False) and _v(g)[0] is g]
+        excl = [g for g in gs if getattr(g, "_adr_excl", False) and not getattr(g, "_adr_pinned", False)
+                and _v(g)[0] is g]
         if excl:  # accumulate the others into the exclusive slice in place
             acc = excl[0]
             side = _side("wgrad") or _side("bias")
@@ -1520,11 +1575,17 @@ class AddFn(torch.autograd.Function):
         else:
             _ew(EW_ADD3, o, va, vb, _v(c))
         ctx.three = c is not None
+        # inputs that are fan-out views with a gradient sink: backward defers its pass-through gradient there
+        ctx.sinks = [getattr(t, "_adr_sink", None) for t in (a, b, c)]
         return o[0]
 
     @staticmethod
     def backward(ctx, dy):
-        return (dy, dy, dy, None) if ctx.three else (dy, dy, None, None)
+        outs = [dy, dy, dy if ctx.three else None]
+        for i, sk in enumerate(ctx.sinks):
+            if outs[i] is not None and sk is not None and sk.defer(dy):
+                outs[i] = None  # a conv consumer of that fan-out adds dy in its dgrad epilogue
+        return outs[0], outs[1], outs[2], None
 
 
 def add(a, b, c=None, out=None):

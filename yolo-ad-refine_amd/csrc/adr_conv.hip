@@ -45,6 +45,10 @@ struct ConvArgs {
   const float* escale;
   const float* eshift;
   int eact;
+  // DGRAD: a second gradient added in the epilogue (a fan-out's pass-through gradient, adr_conv2d_dgrad_bf16_add):
+  // out = conv (+ out) + addend, NHWC with channel stride adcs (null: none)
+  const __bf16* addend;
+  int adcs;
 };
 
 constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
@@ -343,8 +347,16 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
     const long m = (long)m0 + r;
     if (m >= Mrows || !col_ok) continue;
     u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
-    __bf16* dst = a.out + pixel_of(m) * a.ocs + a.oco + n0 + oc * 8;
-    if (a.accumulate) {
+    const long pix = pixel_of(m);
+    __bf16* dst = a.out + pix * a.ocs + a.oco + n0 + oc * 8;
+    if (MODE != CV_FWD && a.addend) {  // one rounding for conv + previous + addend
+      const u32x4 q = ld16(a.addend + pix * a.adcs + n0 + oc * 8);
+      const u32x4 o = a.accumulate ? ld16(dst) : u32x4{0u, 0u, 0u, 0u};
+      const __bf16 *qv = reinterpret_cast<const __bf16*>(&q), *ov = reinterpret_cast<const __bf16*>(&o);
+      __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e] + (float)qv[e]);
+    } else if (a.accumulate) {
       const u32x4 o = ld16(dst);
       const __bf16* ov = reinterpret_cast<const __bf16*>(&o);
       __bf16* nv = reinterpret_cast<__bf16*>(&v);
@@ -526,8 +538,16 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
     const int y = y0 + r / TW;
     if (y >= H || !col_ok) continue;
     u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
-    __bf16* dst = a.out + ((long)(img * H + y) * W + x0 + r % TW) * a.ocs + a.oco + n0 + oc * 8;
-    if (a.accumulate) {
+    const long pix = (long)(img * H + y) * W + x0 + r % TW;
+    __bf16* dst = a.out + pix * a.ocs + a.oco + n0 + oc * 8;
+    if (DG && a.addend) {
+      const u32x4 q = ld16(a.addend + pix * a.adcs + n0 + oc * 8);
+      const u32x4 o = a.accumulate ? ld16(dst) : u32x4{0u, 0u, 0u, 0u};
+      const __bf16 *qv = reinterpret_cast<const __bf16*>(&q), *ov = reinterpret_cast<const __bf16*>(&o);
+      __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e] + (float)qv[e]);
+    } else if (a.accumulate) {
       const u32x4 o = ld16(dst);
       const __bf16* ov = reinterpret_cast<const __bf16*>(&o);
       __bf16* nv = reinterpret_cast<__bf16*>(&v);
@@ -709,12 +729,13 @@ extern "C" int adr_conv2d_fwd_bf16_act(const adr_conv_desc* d, const void* x, co
   return conv_fwd_impl(d, x, w, nullptr, y, nullptr, 0, scale, shift, act, stream);
 }
 
-extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias,
-                                     void* dx, int accumulate, void* stream) {
+static int conv_dgrad_impl(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
+                           int accumulate, const void* addend, int adcs, void* stream) {
   int rc = conv_check(d);
   if (rc) return rc;
   ConvArgs g{};
   g.src = (const __bf16*)dy; g.wt = (const __bf16*)w_crsk; g.out = (__bf16*)dx; g.bias = bias; g.stats = nullptr;
+  g.addend = (const __bf16*)addend; g.adcs = adcs;
   g.n = d->n; g.sh_ = d->ho; g.sw_ = d->wo; g.scs = d->y_cstride; g.sco = d->y_coff; g.sc = d->k;
   g.rh = d->h; g.rw = d->w; g.ocs = d->x_cstride; g.oco = d->x_coff;
   g.r = d->r; g.s = d->s; g.str = d->stride_h; g.ph = d->pad_h; g.pw = d->pad_w;
@@ -736,6 +757,20 @@ extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, con
     launch_conv<CV_DGRAD>(bn, grid, g, st);
   }
   return check_launch("adr_conv2d_dgrad_bf16");
+}
+
+extern "C" int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias,
+                                     void* dx, int accumulate, void* stream) {
+  return conv_dgrad_impl(d, dy, w_crsk, bias, dx, accumulate, nullptr, 0, stream);
+}
+
+// dx (+)= dgrad(dy) + addend in one launch: the fan-out gradient sink's first conv consumer folds in a pass-through
+// gradient (a residual add's) that FanOutFn would otherwise add with its own elementwise launch
+extern "C" int adr_conv2d_dgrad_bf16_add(const adr_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                                         int accumulate, const void* addend, int addend_cstride, void* stream) {
+  ADR_REQUIRE(addend && addend_cstride >= d->c && addend_cstride % 8 == 0 && ((uintptr_t)addend & 15) == 0,
+              "conv dgrad add: addend must be a 16-byte aligned NHWC view with channel stride >= C");
+  return conv_dgrad_impl(d, dy, w_crsk, nullptr, dx, accumulate, addend, addend_cstride, stream);
 }
 
 extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) {
