@@ -535,7 +535,10 @@ def pack_weight2(w: torch.Tensor, dtype, cpad: int = 0, transpose_kc: int = 0, k
     (the CRSK copy feeds the bf16 data-gradient engine); (KRSC, None) for fp32. Under an active PackCache the
     operands come from (or are recorded into) its persistent buffers."""
     pc = _PACK
-    key = (id(w), cpad, transpose_kc, kpad)
+    # a reshaped view of a parameter (nn.Linear / Conv1d weights used as 1x1 / 7x1 conv weights) is a new tensor
+    # on every call: it is keyed by its storage and geometry instead, so it is packed once too
+    view = isinstance(w._base, torch.nn.Parameter)  # (a leaf under no_grad, but still a new object per call)
+    key = ((w.data_ptr(), tuple(w.shape), tuple(w.stride())) if view else id(w), cpad, transpose_kc, kpad)
     if pc is not None and dtype == torch.bfloat16 and pc.valid and key in pc.specs:
         sp = pc.specs[key]
         return sp[7], sp[8]
@@ -556,7 +559,7 @@ def pack_weight2(w: torch.Tensor, dtype, cpad: int = 0, transpose_kc: int = 0, k
     if not direct:
         relayout_count[0] += 1
         wf = wf.float().contiguous()
-    if pc is not None and direct and w.is_leaf:  # record: persistent buffers, repacked by pack_all
+    if pc is not None and direct and (w.is_leaf or view):  # record: persistent buffers, repacked by pack_all
         sp = pc.specs.get(key)
         if sp is None:
             sp = (w, K, Kp, C, Cp, RS, transpose_kc, torch.empty(Kp * RS * Cp, dtype=dtype, device=w.device),
