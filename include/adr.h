@@ -364,6 +364,12 @@ int adr_detect_decode(int dtype, const void* f0, const void* f1, const void* f2,
  * weights (C, 1, k, k) fp32. dw / dx may be NULL to skip. */
 int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w, const float* b, void* y, int ycs, int N, int H,
                    int W, int C, int k, void* stream);
+/* Eval DWConv-BN-act in one launch (bf16, whole-image kernel; adr_dwconv_fwd_act_supported says whether the shape
+ * fits it): y = act(dwconv(x, w * scale) + shift), scale/shift from adr_bn_finalize with training = 0. Replaces
+ * Conv.forward_fuse after fuse_conv_and_bn on a depthwise Conv (nn/modules/conv.py:52-54, 101-106). */
+int adr_dwconv_fwd_act_supported(int H, int W, int C, int k);
+int adr_dwconv_fwd_act(const void* x, int xcs, const float* w, const float* scale, const float* shift, int act,
+                       void* y, int ycs, int N, int H, int W, int C, int k, void* stream);
 size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k);
 int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* w, void* dx, int ocs,
                    float* dw, int N, int H, int W, int C, int k, int accumulate, int dw_accumulate, float* ws,

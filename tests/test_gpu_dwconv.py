@@ -32,3 +32,39 @@ def test_dwconv_vs_torch(dtype, N, C, H, W, k):
     assert rel(xd.grad, xr.grad) < tol, rel(xd.grad, xr.grad)
     assert rel(w.grad, wr.grad) < tol, rel(w.grad, wr.grad)
     assert rel(b.grad, br.grad) < tol, rel(b.grad, br.grad)
+
+
+@pytest.mark.parametrize("act", [True, False])
+@pytest.mark.parametrize("c,k,hw", [(64, 3, 20), (128, 3, 40), (256, 5, 20), (32, 7, 16)])
+def test_dwconv_bn_act_eval_fused(act, c, k, hw):
+    """Inference DWConv-BN-act in one launch (adr_dwconv_fwd_act) against a torch fp32 depthwise Conv2d ->
+    BatchNorm2d(eval) -> SiLU on the same bf16 operands (bound: 1.5 % of max |y|) and against the unfused HIP
+    pair (depthwise conv, then BN + act: 2 %)."""
+    import adrefine.kernels as K
+    from adrefine.nn.modules import Conv
+    from gpu_util import load_recipe_into
+    from recipe import seeded_randn
+    torch.manual_seed(1)
+    m = Conv(c, c, k, 1, g=c, act=act)
+    load_recipe_into(m)
+    with torch.no_grad():
+        m.bn.running_mean.copy_(torch.randn(c) * 0.3)
+        m.bn.running_var.copy_(torch.rand(c) * 2 + 0.2)
+    m = m.cuda().eval()
+    x = seeded_randn(2, c, hw, hw, seed=9).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    with torch.no_grad():
+        y = m(x)
+        K.EVAL_CONV_BN_ACT = False
+        try:
+            y_pair = m(x)
+        finally:
+            K.EVAL_CONV_BN_ACT = True
+        ref = torch.nn.functional.conv2d(x.float(), m.conv.weight.float(), None, 1, k // 2, 1, c)
+        ref = torch.nn.functional.batch_norm(ref, m.bn.running_mean, m.bn.running_var, m.bn.weight, m.bn.bias,
+                                             False, 0.0, m.bn.eps)
+        if act:
+            ref = torch.nn.functional.silu(ref)
+    scale = float(ref.abs().max())
+    err = float((y.float() - ref).abs().max()) / scale
+    err_pair = float((y.float() - y_pair.float()).abs().max()) / scale
+    assert err <= 0.015 and err_pair <= 0.02, (err, err_pair)

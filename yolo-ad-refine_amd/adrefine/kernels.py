@@ -2342,6 +2342,24 @@ def dwconv(x, w, b, k):
     return DWConvFn.apply(x, w, b, k)
 
 
+def dwconv_bn_act_eval(x, w, k, bn, act: str, out=None):
+    """Inference DWConv-BN-act (no autograd) in one launch (adr_dwconv_fwd_act): the BatchNorm scale folded into
+    the staged fp32 taps, the shift as the bias, the activation before the store — Conv.forward_fuse after
+    fuse_conv_and_bn on a depthwise Conv (nn/modules/conv.py:52-54, 101-106). None when not applicable."""
+    if x.dtype != torch.bfloat16 or torch.is_grad_enabled():
+        return None
+    N, C, H, W = x.shape
+    if not lib.adr_dwconv_fwd_act_supported(H, W, C, k):
+        return None
+    vx = _v(x)
+    y, yp, ycs = _out_view(None if out is None else OutBox(out), N, C, H, W, x.dtype, x.device)
+    wf = w.detach().float().contiguous()
+    scale, shift = _bn_eval_coefs(bn, x.device)
+    lib.adr_dwconv_fwd_act(ctypes.c_void_p(vx[1]), vx[2], fptr(wf), fptr(scale), fptr(shift), ACT[act],
+                           ctypes.c_void_p(yp), ycs, N, H, W, C, k, stream())
+    return y if out is None else out
+
+
 class ADyTFn(torch.autograd.Function):
     """AdaptiveDynamicTanh apply (block.py:2547-2575) given the softmax importance imp (N, 3)."""
 

@@ -84,6 +84,10 @@ class Conv(nn.Module):
             if not (cv.groups == cv.in_channels == cv.out_channels and cv.stride == (1, 1) and cv.dilation == (1, 1)
                     and cv.kernel_size == (k, k) and cv.padding == (k // 2, k // 2)):
                 raise NotImplementedError("adrefine Conv: grouped convs are depthwise, stride 1, 'same' padding")
+            if not self.training and K.EVAL_CONV_BN_ACT:  # inference: BN + act in the depthwise kernel
+                z = K.dwconv_bn_act_eval(x, cv.weight, k, self.bn, self.act_name, out=out)
+                if z is not None:
+                    return z
             return K.bn_act(K.dwconv(x, cv.weight, None, k), None, self.bn, self.act_name, self.training, out=out)
         if not self.training and K.EVAL_CONV_BN_ACT:  # inference: BN + act in the conv epilogue (forward_fuse)
             z = K.conv_bn_act_eval(x, cv.weight, cv.stride[0], cv.padding[0], self.bn, self.act_name,

@@ -167,9 +167,11 @@ __device__ __forceinline__ void stage_img_f32(const T* src, int cs, int H, int W
 }
 
 // y = dwconv(x, w) (+b) or dx (+)= dwconv^T(dy, w): items (pixel, VW-channel vector), taps from the LDS image
-template <typename T, bool BWD, int CB>
-__global__ void __launch_bounds__(256) dw_img_kernel(const T* x, int xcs, const float* w, const float* b, T* y,
-                                                     int ycs, int H, int W, int C, int k, int accumulate) {
+// EPI (eval DWConv-BN-act, adr_dwconv_fwd_act): the BatchNorm scale folds into the staged fp32 taps, the shift is
+// the bias, and the activation is applied before the store — the reference's fuse_conv_and_bn on a depthwise conv
+template <typename T, bool BWD, int CB, bool EPI>
+__device__ __forceinline__ void dw_img_body(const T* x, int xcs, const float* w, const float* b, T* y, int ycs, int H,
+                                            int W, int C, int k, int accumulate, const float* escale, int eact) {
   constexpr int VW = 16 / sizeof(T), NV = CB / VW;
   extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
   const int n = blockIdx.x, cb0 = blockIdx.y * CB, p = k / 2, kk = k * k;
@@ -178,7 +180,7 @@ __global__ void __launch_bounds__(256) dw_img_kernel(const T* x, int xcs, const 
   T* xs = reinterpret_cast<T*>(dwsm + (size_t)kk * CB * sizeof(float));
   for (int i = threadIdx.x; i < kk * CB; i += 256) {
     const int t = i / CB, c = cb0 + i % CB;
-    wl[i] = c < C ? w[(long)c * kk + t] : 0.f;
+    wl[i] = c < C ? w[(long)c * kk + t] * (EPI ? escale[c] : 1.f) : 0.f;
   }
   stage_img<T>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
   __syncthreads();
@@ -206,12 +208,32 @@ __global__ void __launch_bounds__(256) dw_img_kernel(const T* x, int xcs, const 
 #pragma unroll
       for (int e = 0; e < VW; ++e) acc[e] += to_f(pe[e]);
     }
+    if constexpr (EPI) {
+#pragma unroll
+      for (int e = 0; e < VW; ++e) {
+        const float v = acc[e];
+        acc[e] = eact == ACT_SILU ? act_fwd_c<ACT_SILU, true>(v) : eact == ACT_SIGMOID ? act_fwd_c<ACT_SIGMOID, true>(v)
+                                                                    : act_fwd(eact, v);
+      }
+    }
     u32x4 o;
     T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
     for (int e = 0; e < VW; ++e) oe[e] = from_f<T>(acc[e]);
     st16(dst, o);
   }
+}
+
+template <typename T, bool BWD, int CB>
+__global__ void __launch_bounds__(256) dw_img_kernel(const T* x, int xcs, const float* w, const float* b, T* y,
+                                                     int ycs, int H, int W, int C, int k, int accumulate) {
+  dw_img_body<T, BWD, CB, false>(x, xcs, w, b, y, ycs, H, W, C, k, accumulate, nullptr, 0);
+}
+template <int CB>
+__global__ void __launch_bounds__(256) dw_img_act_kernel(const __bf16* x, int xcs, const float* w, const float* scale,
+                                                         const float* shift, int act, __bf16* y, int ycs, int H, int W,
+                                                         int C, int k) {
+  dw_img_body<__bf16, false, CB, true>(x, xcs, w, shift, y, ycs, H, W, C, k, 0, scale, act);
 }
 
 // weight gradient: items (tap, 4-channel group, pixel split PS) over fp32 copies of the padded image and of dy
@@ -883,6 +905,29 @@ extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w,
     dw_launch<float, false>(k, dim3(cdiv(total, 256)), sm, st, (const float*)x, xcs, w, b, (float*)y, ycs, N, H, W, C,
                             0);
   return check_launch("adr_dwconv_fwd");
+}
+
+extern "C" int adr_dwconv_fwd_act_supported(int H, int W, int C, int k) {
+  return dw_img_ok() && k % 2 == 1 && C % 8 == 0 && dw_fwd_smem(ADR_BF16, H, W, k) <= 64 * 1024 ? 1 : 0;
+}
+
+// Eval DWConv-BN-act (reference: Conv.forward_fuse after fuse_conv_and_bn on a depthwise Conv, nn/modules/conv.py:52-54
+// / 101-106): y = act(dwconv(x, w * scale) + shift) in one launch, bf16, whole-image kernel only.
+extern "C" int adr_dwconv_fwd_act(const void* x, int xcs, const float* w, const float* scale, const float* shift,
+                                  int act, void* y, int ycs, int N, int H, int W, int C, int k, void* stream) {
+  ADR_REQUIRE(scale && shift && xcs % 8 == 0 && ycs % 8 == 0 && act >= ACT_NONE && act <= ACT_HSWISH,
+              "dwconv act: bad arguments");
+  ADR_REQUIRE(adr_dwconv_fwd_act_supported(H, W, C, k), "dwconv act: H=%d W=%d C=%d k=%d not on the image kernel", H, W,
+              C, k);
+  const size_t sm = dw_fwd_smem(ADR_BF16, H, W, k);
+  hipStream_t st = (hipStream_t)stream;
+  if (dw_cb_fwd() == 32)
+    hipLaunchKernelGGL((dw_img_act_kernel<32>), dim3(N, cdiv(C, 32)), dim3(256), sm, st, (const __bf16*)x, xcs, w,
+                       scale, shift, act, (__bf16*)y, ycs, H, W, C, k);
+  else
+    hipLaunchKernelGGL((dw_img_act_kernel<DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
+                       (const __bf16*)x, xcs, w, scale, shift, act, (__bf16*)y, ycs, H, W, C, k);
+  return check_launch("adr_dwconv_fwd_act");
 }
 
 extern "C" size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k) {
