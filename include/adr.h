@@ -190,6 +190,16 @@ typedef struct {
   int P, C, which, accumulate;
 } adr_psum_entry;
 int adr_partial_sum_batched(const adr_psum_entry* entries, int count, void* stream);
+/* Many bf16 adr_nc_reduce(RED_STATS) column-sum reductions in one launch (the bias gradients of every biased conv,
+ * nn.Conv2d(bias=True) rows, nn/tasks.py:1005-1016, deferred to the end of backward): entry e reads x (NHWC,
+ * channel stride xcs, N images of HW pixels, C channels) in chunks of rows_per_chunk pixels and writes
+ * partial[(n * chunks + chunk)][2][C] exactly as adr_nc_reduce does (chunks = ceil(HW / rows_per_chunk)). */
+typedef struct adr_colsum_entry {
+  const void* x;
+  float* partial;
+  int xcs, N, HW, C, rows_per_chunk, chunks;
+} adr_colsum_entry;
+int adr_nc_reduce_batched(const adr_colsum_entry* entries, int count, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Parameter plumbing: (K, C, R*S) fp32 <-> KRSC operand (compute dtype); transpose_kc=1 reads a

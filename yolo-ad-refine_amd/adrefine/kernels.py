@@ -585,6 +585,12 @@ class PsumEntry(ctypes.Structure):
         (n, ctypes.c_int) for n in ("P", "C", "which", "accumulate")]
 
 
+class ColsumEntry(ctypes.Structure):
+    """adr_colsum_entry (include/adr.h)."""
+    _fields_ = [("x", ctypes.c_void_p), ("partial", ctypes.c_void_p)] + [
+        (n, ctypes.c_int) for n in ("xcs", "N", "HW", "C", "rows_per_chunk", "chunks")]
+
+
 class AxpyEntry(ctypes.Structure):
     """adr_axpy_entry (include/adr.h)."""
     _fields_ = [("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("n", ctypes.c_long)]
@@ -687,6 +693,14 @@ class WgradDeferral:
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
         self.axpys, self.akeep, self.adsts = [], [], set()
+        self.cols, self.ckeep = [], []
+
+    def add_colsum(self, x, part, xcs, N, HW, C, rows, chunks):
+        """A bias gradient's column sums (adr_nc_reduce RED_STATS of dy into `part`), run in one batched launch
+        before the partial sums at the flush; dy stays alive until then."""
+        self.cols.append(ColsumEntry(x.data_ptr(), part.data_ptr(), xcs, N, HW, C, rows, chunks))
+        self.ckeep.append(x)
+        self.ckeep.append(part)
 
     def add_axpy(self, src, dst, n):
         """A parameter gradient computed into a temporary, to be added into the arena (sink)."""
@@ -720,12 +734,15 @@ class WgradDeferral:
         if self.side is not None and "flush" in _SIDE_KINDS and (self.entries or self.psums or self.axpys):
             # sources allocated on the current stream (a sink()'s temporary, a main-stream WGRAD's slabs) must
             # outlive the side-stream reads: the side stream holds them until the join
-            with self.side.fork(*self.keep, *self.pkeep, *self.akeep):
+            with self.side.fork(*self.keep, *self.pkeep, *self.akeep, *self.ckeep):
                 self._flush()
         else:
             self._flush()
 
     def _flush(self):
+        if self.cols:  # before the partial sums that read their rows
+            arr = (ColsumEntry * len(self.cols))(*self.cols)
+            lib.adr_nc_reduce_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.cols), stream())
         if self.entries:
             arr = (WgradEntry * len(self.entries))(*self.entries)
             lib.adr_wgrad_reduce_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.entries), stream())
@@ -738,8 +755,11 @@ class WgradDeferral:
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
         self.axpys, self.akeep, self.adsts = [], [], set()
+        self.cols, self.ckeep = [], []
 
 
+# bias-gradient column sums batched at the flush (ADR_DEFER_COLSUM=0: one adr_nc_reduce per biased conv)
+_DEFER_COLSUM = bool(int(__import__("os").environ.get("ADR_DEFER_COLSUM", "1")))
 _DEFER = None  # the active WgradDeferral (set by the trainer around its backward pass)
 # Partial sets above this size are reduced right away (while still in L2) instead of deferred. Measured
 # (scripts/ab_env.sh): deferring all of them is fastest — 32.39 ms vs 32.49 / 32.64 / 32.70 ms for 16 / 4 / 1 MB.
@@ -823,6 +843,13 @@ def _bias_grad1(dy, K, N, HW, cs, param=None):
     dt = dcode(dy.dtype)
     chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
     part = torch.empty(N * chunks * 2 * K, dtype=torch.float32, device=dy.device)
+    if param is not None and _DEFER is not None and _TIMING is None and _DEFER_COLSUM and dt == BF16 and \
+            dy.data_ptr() % 16 == 0 and cs % 8 == 0 and K % 8 == 0 and _DEFER.side is None and \
+            _target(param) is not None:  # an arena destination: column sums and partial sums at the flush, batched
+        db, p, acc = grad_dst(param, K, dy.device)
+        _DEFER.add_colsum(dy, part, cs, N, HW, K, _stats_rows(N, HW), chunks)
+        _DEFER.add_psum(part, N * chunks, K, 0, p, acc)
+        return grad_ret(param, db)
     lib.adr_nc_reduce(dt, 0, ctypes.c_void_p(dy.data_ptr()), cs, 0, None, 0, 0, None, None, 0, 0, N, HW, K,
                       _stats_rows(N, HW), fptr(part), stream())
     if param is not None:

@@ -15,16 +15,14 @@ namespace adr {
 enum RedMode { RED_STATS = 0, RED_BWD = 1, RED_SUM = 2 };
 
 // partial[(n * chunks + chunk)][2][C]
-template <typename T, int MODE, int ACT = ACT_NONE>
-__global__ void __launch_bounds__(256) nc_reduce_kernel(const T* __restrict__ x, int xcs, int xco,
-                                                        const T* __restrict__ dz, int dcs, int dco,
-                                                        const float* __restrict__ scale,
-                                                        const float* __restrict__ shift, int per_sample, int act,
-                                                        int HW, int C, int rows_per_chunk, int chunks,
-                                                        float* __restrict__ partial) {
+template <typename T, int MODE, int ACT>
+__device__ __forceinline__ void nc_reduce_body(const T* __restrict__ x, int xcs, int xco, const T* __restrict__ dz,
+                                               int dcs, int dco, const float* __restrict__ scale,
+                                               const float* __restrict__ shift, int per_sample, int HW, int C,
+                                               int rows_per_chunk, int chunks, float* __restrict__ partial,
+                                               const int chunk, const int n) {
   constexpr int VEC = 16 / sizeof(T);
   __shared__ float sh[2][256 * VEC];
-  const int chunk = blockIdx.x, n = blockIdx.y;
   const int G = C / VEC;
   const int rpp = 256 / G;  // rows per pass
   const int t = threadIdx.x;
@@ -101,6 +99,36 @@ __global__ void __launch_bounds__(256) nc_reduce_kernel(const T* __restrict__ x,
     out[c] = a;
     out[C + c] = b;
   }
+}
+
+template <typename T, int MODE, int ACT = ACT_NONE>
+__global__ void __launch_bounds__(256) nc_reduce_kernel(const T* __restrict__ x, int xcs, int xco,
+                                                        const T* __restrict__ dz, int dcs, int dco,
+                                                        const float* __restrict__ scale,
+                                                        const float* __restrict__ shift, int per_sample, int act,
+                                                        int HW, int C, int rows_per_chunk, int chunks,
+                                                        float* __restrict__ partial) {
+  nc_reduce_body<T, MODE, ACT>(x, xcs, xco, dz, dcs, dco, scale, shift, per_sample, HW, C, rows_per_chunk, chunks,
+                               partial, blockIdx.x, blockIdx.y);
+}
+
+// Many RED_STATS reductions in one launch (the trainer defers the bias-gradient column sums of every biased conv
+// to the end of backward): block b of the grid is (chunk, image) (b - start[e]) of entry e, reduced exactly as
+// nc_reduce_kernel reduces it, so the partial rows — and the bias gradients — are bitwise those of one launch each.
+constexpr int NCB_MAX = 48;
+struct NcrBatch {
+  adr_colsum_entry e[NCB_MAX];
+  int start[NCB_MAX + 1];
+  int count;
+};
+__global__ void __launch_bounds__(256) nc_reduce_batched_kernel(NcrBatch b) {
+  int j = 0;
+  while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  const adr_colsum_entry& en = b.e[j];
+  const int local = blockIdx.x - b.start[j];
+  nc_reduce_body<__bf16, RED_STATS, ACT_NONE>((const __bf16*)en.x, en.xcs, 0, nullptr, 0, 0, nullptr, nullptr, 0,
+                                              en.HW, en.C, en.rows_per_chunk, en.chunks, en.partial,
+                                              local % en.chunks, local / en.chunks);
 }
 
 // block per channel: deterministic fixed-order sum over P partial rows in double. Each thread keeps four rows in
@@ -847,6 +875,29 @@ extern "C" int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, co
   ADR_ACT_DISPATCH(act, ADR_AAB);
 #undef ADR_AAB
   return check_launch("adr_affine_act_bwd");
+}
+
+extern "C" int adr_nc_reduce_batched(const adr_colsum_entry* entries, int count, void* stream) {
+  ADR_REQUIRE(count >= 0 && (count == 0 || entries), "nc_reduce_batched: count=%d", count);
+  for (int b0 = 0; b0 < count; b0 += NCB_MAX) {
+    NcrBatch nb{};
+    nb.count = count - b0 < NCB_MAX ? count - b0 : NCB_MAX;
+    long blocks = 0;
+    for (int j = 0; j < nb.count; ++j) {
+      const adr_colsum_entry& en = entries[b0 + j];
+      ADR_REQUIRE(en.x && en.partial && en.N > 0 && en.HW > 0 && en.C % 8 == 0 && en.C / 8 <= 256 &&
+                      en.xcs % 8 == 0 && ((uintptr_t)en.x & 15) == 0 && en.rows_per_chunk > 0 &&
+                      en.chunks == cdiv(en.HW, en.rows_per_chunk),
+                  "nc_reduce_batched: entry %d", b0 + j);
+      nb.e[j] = en;
+      nb.start[j] = (int)blocks;
+      blocks += (long)en.N * en.chunks;
+    }
+    ADR_REQUIRE(blocks < (1l << 31), "nc_reduce_batched: grid");
+    nb.start[nb.count] = (int)blocks;
+    hipLaunchKernelGGL(nc_reduce_batched_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, nb);
+  }
+  return check_launch("adr_nc_reduce_batched");
 }
 
 extern "C" int adr_partial_sum_batched(const adr_psum_entry* entries, int count, void* stream) {
