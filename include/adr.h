@@ -200,6 +200,19 @@ typedef struct adr_colsum_entry {
   int xcs, N, HW, C, rows_per_chunk, chunks;
 } adr_colsum_entry;
 int adr_nc_reduce_batched(const adr_colsum_entry* entries, int count, void* stream);
+/* Many GroupNorm dgamma / dbeta reductions (the gn_bwd_param part of adr_gn_bwd_finalize / adr_gn_param_grad,
+ * nn.GroupNorm in Conv_GN, nn/modules/head.py:607-620) in as few launches as the destinations allow: entries
+ * with a destination already in the current launch go to the next one, so repeated modules (the AYHead's shared
+ * per-level convs) accumulate in entry order. partial is [N][chunks][2][C] (sum g, sum g*x). */
+typedef struct adr_gnparam_entry {
+  const float* partial;
+  const float* mean;
+  const float* rstd;
+  float* dgamma;
+  float* dbeta;
+  int N, chunks, C, G, accumulate, pad_;
+} adr_gnparam_entry;
+int adr_gn_param_grad_batched(const adr_gnparam_entry* entries, int count, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Parameter plumbing: (K, C, R*S) fp32 <-> KRSC operand (compute dtype); transpose_kc=1 reads a

@@ -591,6 +591,12 @@ class ColsumEntry(ctypes.Structure):
         (n, ctypes.c_int) for n in ("xcs", "N", "HW", "C", "rows_per_chunk", "chunks")]
 
 
+class GnParamEntry(ctypes.Structure):
+    """adr_gnparam_entry (include/adr.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("partial", "mean", "rstd", "dgamma", "dbeta")] + [
+        (n, ctypes.c_int) for n in ("N", "chunks", "C", "G", "accumulate", "pad_")]
+
+
 class AxpyEntry(ctypes.Structure):
     """adr_axpy_entry (include/adr.h)."""
     _fields_ = [("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("n", ctypes.c_long)]
@@ -694,6 +700,14 @@ class WgradDeferral:
         self.psums, self.pkeep, self.pdsts = [], [], set()
         self.axpys, self.akeep, self.adsts = [], [], set()
         self.cols, self.ckeep = [], []
+        self.gnps, self.gkeep = [], []
+
+    def add_gnparam(self, part, mean, rstd, pg, pb, N, chunks, C, G, acc):
+        """A GroupNorm dgamma / dbeta reduction (arena destinations), batched at the flush."""
+        val = lambda q: q.value if isinstance(q, ctypes.c_void_p) else q  # noqa: E731
+        self.gnps.append(GnParamEntry(part.data_ptr(), mean.data_ptr(), rstd.data_ptr(), val(pg), val(pb), N, chunks,
+                                      C, G, acc, 0))
+        self.gkeep += [part, mean, rstd]
 
     def add_colsum(self, x, part, xcs, N, HW, C, rows, chunks):
         """A bias gradient's column sums (adr_nc_reduce RED_STATS of dy into `part`), run in one batched launch
@@ -734,7 +748,7 @@ class WgradDeferral:
         if self.side is not None and "flush" in _SIDE_KINDS and (self.entries or self.psums or self.axpys):
             # sources allocated on the current stream (a sink()'s temporary, a main-stream WGRAD's slabs) must
             # outlive the side-stream reads: the side stream holds them until the join
-            with self.side.fork(*self.keep, *self.pkeep, *self.akeep, *self.ckeep):
+            with self.side.fork(*self.keep, *self.pkeep, *self.akeep, *self.ckeep, *self.gkeep):
                 self._flush()
         else:
             self._flush()
@@ -752,10 +766,14 @@ class WgradDeferral:
         if self.axpys:
             arr = (AxpyEntry * len(self.axpys))(*self.axpys)
             lib.adr_axpy_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.axpys), stream())
+        if self.gnps:
+            arr = (GnParamEntry * len(self.gnps))(*self.gnps)
+            lib.adr_gn_param_grad_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.gnps), stream())
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
         self.axpys, self.akeep, self.adsts = [], [], set()
         self.cols, self.ckeep = [], []
+        self.gnps, self.gkeep = [], []
 
 
 # bias-gradient column sums batched at the flush (ADR_DEFER_COLSUM=0: one adr_nc_reduce per biased conv)
@@ -1050,6 +1068,14 @@ _GN_FUSED = bool(int(__import__("os").environ.get("ADR_GN_FUSED", "1")))  # 0: t
 _GN_FUSED_MAXHW = int(__import__("os").environ.get("ADR_GN_FUSED_MAXHW", "400"))
 
 
+_DEFER_GN = bool(int(__import__("os").environ.get("ADR_DEFER_GN", "1")))  # 0: GN param grads launched in place
+
+
+def _defer_gn(acc):
+    """Whether a GroupNorm dgamma / dbeta reduction goes to the deferral's batched flush (arena destinations)."""
+    return bool(acc) and _DEFER_GN and _DEFER is not None and _TIMING is None and _DEFER.side is None
+
+
 class GNActFn(torch.autograd.Function):
     """act(GroupNorm(G)(y)) with per-(image, group) statistics."""
 
@@ -1114,7 +1140,10 @@ class GNActFn(torch.autograd.Function):
             dbeta, pb, acc_b = grad_dst(ctx.pbeta, C, dev)
             if acc_g != acc_b:
                 raise RuntimeError("GN gamma/beta gradients must share one destination kind")
-            lib.adr_gn_param_grad(fptr(part), N, C, groups, fptr(mean), fptr(rstd), pg, pb, acc_g, stream())
+            if _defer_gn(acc_g):
+                _DEFER.add_gnparam(part, mean, rstd, pg, pb, N, 1, C, groups, acc_g)
+            else:
+                lib.adr_gn_param_grad(fptr(part), N, C, groups, fptr(mean), fptr(rstd), pg, pb, acc_g, stream())
             return dy, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None
         chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
         part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
@@ -1127,8 +1156,12 @@ class GNActFn(torch.autograd.Function):
         A = torch.empty(N * C, dtype=torch.float32, device=dev)
         B = torch.empty(N * C, dtype=torch.float32, device=dev)
         Cc = torch.empty(N * C, dtype=torch.float32, device=dev)
+        dfr = _defer_gn(acc_g)  # dgamma / dbeta at the flush, batched (the coefficients are needed now)
+        if dfr:
+            _DEFER.add_gnparam(part, mean, rstd, pg, pb, N, chunks, C, groups, acc_g)
         lib.adr_gn_bwd_finalize(fptr(part), N, chunks, C, groups, float(HW * (C // groups)), fptr(mean), fptr(rstd),
-                                fptr(gamma.detach()), pg, pb, fptr(A), fptr(B), fptr(Cc), acc_g, stream())
+                                fptr(gamma.detach()), None if dfr else pg, None if dfr else pb, fptr(A), fptr(B),
+                                fptr(Cc), acc_g, stream())
         dy = empty_act(N, C, H, W, y.dtype, dev)
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),

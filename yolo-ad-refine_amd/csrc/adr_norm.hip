@@ -342,11 +342,10 @@ __global__ void __launch_bounds__(256) gn_bwd_coef_kernel(const float* __restric
 
 // GroupNorm dgamma / dbeta, per channel (grid C): fixed-order reduction over (image, chunk) of
 // (sum g*x - mu_n * sum g) * rstd_n and sum g.
-__global__ void __launch_bounds__(256) gn_bwd_param_kernel(const float* __restrict__ partial, int N, int chunks, int C,
-                                                           int G, const float* __restrict__ mean,
-                                                           const float* __restrict__ rstd, float* dgamma,
-                                                           float* dbeta, int accumulate) {
-  const int c = blockIdx.x, g = c / (C / G);
+__device__ __forceinline__ void gn_bwd_param_body(const float* __restrict__ partial, int N, int chunks, int C, int G,
+                                                  const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                  float* dgamma, float* dbeta, int accumulate, const int c) {
+  const int g = c / (C / G);
   double sgx = 0.0, sb = 0.0;
   for (int it = threadIdx.x; it < N * chunks; it += 256) {
     const int n = it / chunks;
@@ -370,6 +369,30 @@ __global__ void __launch_bounds__(256) gn_bwd_param_kernel(const float* __restri
     if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)r1[0] : (float)r1[0];
     if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)r2[0] : (float)r2[0];
   }
+}
+
+__global__ void __launch_bounds__(256) gn_bwd_param_kernel(const float* __restrict__ partial, int N, int chunks, int C,
+                                                           int G, const float* __restrict__ mean,
+                                                           const float* __restrict__ rstd, float* dgamma,
+                                                           float* dbeta, int accumulate) {
+  gn_bwd_param_body(partial, N, chunks, C, G, mean, rstd, dgamma, dbeta, accumulate, blockIdx.x);
+}
+
+// Many GroupNorm dgamma / dbeta reductions per launch (deferred to the end of backward); block b is channel
+// b - start[e] of entry e, reduced exactly as gn_bwd_param_kernel does. Entries of one launch have distinct
+// destinations (the host splits at a repeated one, so a shared module's contributions accumulate in order).
+constexpr int GPB_MAX = 40;
+struct GnParamBatch {
+  adr_gnparam_entry e[GPB_MAX];
+  int start[GPB_MAX + 1];
+  int count;
+};
+__global__ void __launch_bounds__(256) gn_param_batched_kernel(GnParamBatch b) {
+  int j = 0;
+  while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  const adr_gnparam_entry& en = b.e[j];
+  gn_bwd_param_body(en.partial, en.N, en.chunks, en.C, en.G, en.mean, en.rstd, en.dgamma, en.dbeta, en.accumulate,
+                    (int)blockIdx.x - b.start[j]);
 }
 
 // ---- GroupNorm + activation fused per image (Conv_GN / TaskDecomposition / DyDCNv2 / ELA gates: GN statistics
@@ -978,6 +1001,33 @@ extern "C" int adr_gn_act_bwd_fused(int dtype, const void* x, int xcs, int xco, 
   ADR_ACT_DISPATCH(act, ADR_GNB);
 #undef ADR_GNB
   return check_launch("adr_gn_act_bwd_fused");
+}
+
+extern "C" int adr_gn_param_grad_batched(const adr_gnparam_entry* entries, int count, void* stream) {
+  ADR_REQUIRE(count >= 0 && (count == 0 || entries), "gn_param_grad_batched: count=%d", count);
+  int b0 = 0;
+  while (b0 < count) {
+    GnParamBatch gb{};
+    int blocks = 0, j = 0;
+    for (; j < GPB_MAX && b0 + j < count; ++j) {
+      const adr_gnparam_entry& en = entries[b0 + j];
+      ADR_REQUIRE(en.partial && en.mean && en.rstd && (en.dgamma || en.dbeta) && en.N > 0 && en.chunks > 0 &&
+                      en.G > 0 && en.C % en.G == 0,
+                  "gn_param_grad_batched: entry %d", b0 + j);
+      bool dup = false;
+      for (int q = 0; q < j; ++q)
+        dup |= (en.dgamma && gb.e[q].dgamma == en.dgamma) || (en.dbeta && gb.e[q].dbeta == en.dbeta);
+      if (dup) break;  // a repeated destination starts the next launch (program-order accumulation)
+      gb.e[j] = en;
+      gb.start[j] = blocks;
+      blocks += en.C;
+    }
+    gb.count = j;
+    gb.start[j] = blocks;
+    hipLaunchKernelGGL(gn_param_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, gb);
+    b0 += j;
+  }
+  return check_launch("adr_gn_param_grad_batched");
 }
 
 extern "C" int adr_gn_param_grad(const float* partial, int N, int C, int G, const float* mean, const float* rstd,
