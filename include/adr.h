@@ -213,6 +213,18 @@ typedef struct adr_gnparam_entry {
   int N, chunks, C, G, accumulate, pad_;
 } adr_gnparam_entry;
 int adr_gn_param_grad_batched(const adr_gnparam_entry* entries, int count, void* stream);
+/* Deferred scalar parameter gradients, batched: out[0] = sum over all pixels and channels of x * dz for each entry
+ * (bf16 NHWC views) — the Scale (nn/modules/head.py:783 Scale, `x * self.scale`) and weighted-sum weight gradients,
+ * i.e. adr_dot_reduce + adr_nc_collapse(sum_n = sum_c = 1) for many tensors in two launches. partial is the
+ * caller's [N][chunks][2][C] workspace per entry. */
+typedef struct adr_dotsum_entry {
+  const void* x;
+  const void* dz;
+  float* partial;
+  float* out;
+  int xcs, dcs, N, HW, C, rows_per_chunk, chunks, pad_;
+} adr_dotsum_entry;
+int adr_dotsum_batched(const adr_dotsum_entry* entries, int count, void* stream);
 
 /* ---------------------------------------------------------------------------------------------------------
  * Parameter plumbing: (K, C, R*S) fp32 <-> KRSC operand (compute dtype); transpose_kc=1 reads a

@@ -597,6 +597,12 @@ class GnParamEntry(ctypes.Structure):
         (n, ctypes.c_int) for n in ("N", "chunks", "C", "G", "accumulate", "pad_")]
 
 
+class DotsumEntry(ctypes.Structure):
+    """adr_dotsum_entry (include/adr.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("x", "dz", "partial", "out")] + [
+        (n, ctypes.c_int) for n in ("xcs", "dcs", "N", "HW", "C", "rows_per_chunk", "chunks", "pad_")]
+
+
 class AxpyEntry(ctypes.Structure):
     """adr_axpy_entry (include/adr.h)."""
     _fields_ = [("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("n", ctypes.c_long)]
@@ -701,6 +707,21 @@ class WgradDeferral:
         self.axpys, self.akeep, self.adsts = [], [], set()
         self.cols, self.ckeep = [], []
         self.gnps, self.gkeep = [], []
+        self.dots, self.dkeep = [], []
+
+    def add_dotsum(self, x, dy, out):
+        """out[0] = sum(x * dy) over every pixel and channel (a scalar parameter gradient), at the flush.
+        dy is pinned so no fan-out accumulates into it in place before then."""
+        N, C, H, W = dy.shape
+        vx, vd = _v(x), _v(dy)
+        rows = _stats_rows(N, H * W)
+        chunks = lib.adr_nc_reduce_chunks(H * W, rows)
+        part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dy.device)
+        vd[0]._adr_pinned = True
+        dy._adr_pinned = True
+        self.dots.append(DotsumEntry(vx[1], vd[1], part.data_ptr(), out.data_ptr(), vx[2], vd[2], N, H * W, C, rows,
+                                     chunks, 0))
+        self.dkeep += [vx[0], vd[0], part, out]
 
     def add_gnparam(self, part, mean, rstd, pg, pb, N, chunks, C, G, acc):
         """A GroupNorm dgamma / dbeta reduction (arena destinations), batched at the flush."""
@@ -748,12 +769,15 @@ class WgradDeferral:
         if self.side is not None and "flush" in _SIDE_KINDS and (self.entries or self.psums or self.axpys):
             # sources allocated on the current stream (a sink()'s temporary, a main-stream WGRAD's slabs) must
             # outlive the side-stream reads: the side stream holds them until the join
-            with self.side.fork(*self.keep, *self.pkeep, *self.akeep, *self.ckeep, *self.gkeep):
+            with self.side.fork(*self.keep, *self.pkeep, *self.akeep, *self.ckeep, *self.gkeep, *self.dkeep):
                 self._flush()
         else:
             self._flush()
 
     def _flush(self):
+        if self.dots:  # before the axpys that add their outputs into the arena
+            arr = (DotsumEntry * len(self.dots))(*self.dots)
+            lib.adr_dotsum_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.dots), stream())
         if self.cols:  # before the partial sums that read their rows
             arr = (ColsumEntry * len(self.cols))(*self.cols)
             lib.adr_nc_reduce_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.cols), stream())
@@ -774,9 +798,19 @@ class WgradDeferral:
         self.axpys, self.akeep, self.adsts = [], [], set()
         self.cols, self.ckeep = [], []
         self.gnps, self.gkeep = [], []
+        self.dots, self.dkeep = [], []
+
+
+def _defer_dot(param, x, dy):
+    """Whether sum(x * dy) for a scalar parameter gradient can go to the deferral's batched flush."""
+    return (_DEFER_DOT and _DEFER is not None and _TIMING is None and _DEFER.side is None and
+            _target(param) is not None and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and
+            dy.shape[1] % 8 == 0 and _v(dy)[2] % 8 == 0 and _v(x)[2] % 8 == 0 and _v(dy)[1] % 16 == 0 and
+            _v(x)[1] % 16 == 0)
 
 
 # bias-gradient column sums batched at the flush (ADR_DEFER_COLSUM=0: one adr_nc_reduce per biased conv)
+_DEFER_DOT = bool(int(__import__("os").environ.get("ADR_DEFER_DOT", "1")))  # scalar dot gradients at the flush
 _DEFER_COLSUM = bool(int(__import__("os").environ.get("ADR_DEFER_COLSUM", "1")))
 _DEFER = None  # the active WgradDeferral (set by the trainer around its backward pass)
 # Partial sets above this size are reduced right away (while still in L2) instead of deferred. Measured
@@ -1780,7 +1814,12 @@ class ScaleFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             sum_n = mode in ("scalar", "c")
             sum_c = mode in ("scalar", "n")
-            dg = sink(ctx.pg, _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape))
+            if sum_n and sum_c and _defer_dot(ctx.pg, x, vd[0]):  # a scalar: sum(x * dy) at the flush
+                out = torch.empty(1, dtype=torch.float32, device=x.device)
+                _DEFER.add_dotsum(x, vd[0], out)
+                dg = sink(ctx.pg, out.view(gshape))
+            else:
+                dg = sink(ctx.pg, _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape))
         return dx, dg, (dy if has_res else None), None, None
 
 
@@ -1819,7 +1858,14 @@ class WeightedSumFn(torch.autograd.Function):
             d = _new_like(x)
             _ew(EW_AXPBY, (d, d.data_ptr(), d.shape[1]), vd, vd, ca=wd[i:i + 1], cb=_const(0.0, dy.device))
             dxs.append(d)
-        dw = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs]) if ctx.needs_input_grad[0] else None
+        if not ctx.needs_input_grad[0]:
+            dw = None
+        elif all(_defer_dot(ctx.pw, x, vd[0]) for x in xs):  # the weights' scalar gradients at the flush
+            dw = torch.empty(len(xs), dtype=torch.float32, device=dy.device)
+            for i, x in enumerate(xs):
+                _DEFER.add_dotsum(x, vd[0], dw[i:i + 1])
+        else:
+            dw = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs])
         return (sink(ctx.pw, dw), dy if ctx.has_base else None, *dxs)
 
 

@@ -111,10 +111,9 @@ __global__ void __launch_bounds__(256) bcast_mul_kernel(const T* x, int xcs, con
 // One workgroup per output element (NT threads: 1024 when everything collapses to a scalar), fixed-order
 // per-thread strides + tree combine (deterministic); the full collapse walks rows division-free, 8 loads in flight.
 template <int NT>
-__global__ void __launch_bounds__(NT) nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which,
-                                                         float* out, int sum_n, int sum_c, int accumulate) {
+__device__ __forceinline__ void nc_collapse_body(const float* partial, int N, int chunks, int C, int which, float* out,
+                                                 int sum_n, int sum_c, int accumulate, const int idx) {
   const int outC = sum_c ? 1 : C;
-  const int idx = blockIdx.x;
   const int on = idx / outC, oc = idx % outC;
   const int nn = sum_n ? N : 1, ncc = sum_c ? C : 1;
   const int n0 = sum_n ? 0 : on, c0 = sum_c ? 0 : oc;
@@ -160,14 +159,19 @@ __global__ void __launch_bounds__(NT) nc_collapse_kernel(const float* partial, i
   if (threadIdx.x == 0) out[idx] = accumulate ? out[idx] + (float)sh[0] : (float)sh[0];
 }
 
+template <int NT>
+__global__ void __launch_bounds__(NT) nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which,
+                                                         float* out, int sum_n, int sum_c, int accumulate) {
+  nc_collapse_body<NT>(partial, N, chunks, C, which, out, sum_n, sum_c, accumulate, blockIdx.x);
+}
+
 // partial[n][chunk][0][c] = sum x*dz ; [1][c] = sum dz   (per image, per channel)
 template <typename T>
-__global__ void __launch_bounds__(256) dot_reduce_kernel(const T* __restrict__ x, int xcs, const T* __restrict__ dz,
-                                                         int dcs, int HW, int C, int rows_per_chunk, int chunks,
-                                                         float* __restrict__ partial) {
+__device__ __forceinline__ void dot_reduce_body(const T* __restrict__ x, int xcs, const T* __restrict__ dz, int dcs,
+                                                int HW, int C, int rows_per_chunk, int chunks,
+                                                float* __restrict__ partial, const int chunk, const int n) {
   constexpr int V = VecIO<T>::V;
   __shared__ float sh[2][256 * V];
-  const int chunk = blockIdx.x, n = blockIdx.y;
   const int G = C / V;
   const int rpp = 256 / G;
   const int t = threadIdx.x;
@@ -216,6 +220,36 @@ __global__ void __launch_bounds__(256) dot_reduce_kernel(const T* __restrict__ x
     out[c] = a;
     out[C + c] = b;
   }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) dot_reduce_kernel(const T* __restrict__ x, int xcs, const T* __restrict__ dz,
+                                                         int dcs, int HW, int C, int rows_per_chunk, int chunks,
+                                                         float* __restrict__ partial) {
+  dot_reduce_body<T>(x, xcs, dz, dcs, HW, C, rows_per_chunk, chunks, partial, blockIdx.x, blockIdx.y);
+}
+
+// Deferred scalar parameter gradients (Scale, weighted-sum weights: sum over every pixel and channel of x * dy),
+// batched at the end of backward: the dot partials of all entries in one launch (block = (chunk, image) of an
+// entry), then one 1024-thread workgroup per entry collapsing its partial rows — the same bodies, so the same
+// fixed summation order as adr_dot_reduce + adr_nc_collapse(sum_n = sum_c = 1).
+constexpr int DTB_MAX = 32;
+struct DotBatch {
+  adr_dotsum_entry e[DTB_MAX];
+  int start[DTB_MAX + 1];
+  int count;
+};
+__global__ void __launch_bounds__(256) dot_reduce_batched_kernel(DotBatch b) {
+  int j = 0;
+  while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  const adr_dotsum_entry& en = b.e[j];
+  const int local = (int)blockIdx.x - b.start[j];
+  dot_reduce_body<__bf16>((const __bf16*)en.x, en.xcs, (const __bf16*)en.dz, en.dcs, en.HW, en.C, en.rows_per_chunk,
+                          en.chunks, en.partial, local % en.chunks, local / en.chunks);
+}
+__global__ void __launch_bounds__(1024) dot_collapse_batched_kernel(DotBatch b) {
+  const adr_dotsum_entry& en = b.e[blockIdx.x];
+  nc_collapse_body<1024>(en.partial, en.N, en.chunks, en.C, 0, en.out, 1, 1, 0, 0);
 }
 
 // BiFPN fusion weights: w = relu(fw) / (sum relu(fw) + eps)   (block.py:1532-1535), and its backward
@@ -325,6 +359,31 @@ extern "C" int adr_dot_reduce(int dtype, const void* x, int xcs, const void* dz,
     hipLaunchKernelGGL(dot_reduce_kernel<float>, grid, dim3(256), 0, st, (const float*)x, xcs, (const float*)dz, dcs,
                        HW, C, rows_per_chunk, chunks, partial);
   return check_launch("adr_dot_reduce");
+}
+
+extern "C" int adr_dotsum_batched(const adr_dotsum_entry* entries, int count, void* stream) {
+  ADR_REQUIRE(count >= 0 && (count == 0 || entries), "dotsum_batched: count=%d", count);
+  hipStream_t st = (hipStream_t)stream;
+  for (int b0 = 0; b0 < count; b0 += DTB_MAX) {
+    DotBatch db{};
+    db.count = count - b0 < DTB_MAX ? count - b0 : DTB_MAX;
+    long blocks = 0;
+    for (int j = 0; j < db.count; ++j) {
+      const adr_dotsum_entry& en = entries[b0 + j];
+      ADR_REQUIRE(en.x && en.dz && en.partial && en.out && en.N > 0 && en.HW > 0 && en.C % 8 == 0 &&
+                      en.C / 8 <= 256 && en.xcs % 8 == 0 && en.dcs % 8 == 0 && en.rows_per_chunk > 0 &&
+                      en.chunks == cdiv(en.HW, en.rows_per_chunk),
+                  "dotsum_batched: entry %d", b0 + j);
+      db.e[j] = en;
+      db.start[j] = (int)blocks;
+      blocks += (long)en.N * en.chunks;
+    }
+    ADR_REQUIRE(blocks < (1l << 31), "dotsum_batched: grid");
+    db.start[db.count] = (int)blocks;
+    hipLaunchKernelGGL(dot_reduce_batched_kernel, dim3((unsigned)blocks), dim3(256), 0, st, db);
+    hipLaunchKernelGGL(dot_collapse_batched_kernel, dim3(db.count), dim3(1024), 0, st, db);
+  }
+  return check_launch("adr_dotsum_batched");
 }
 
 extern "C" int adr_nc_collapse(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n,
