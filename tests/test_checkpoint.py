@@ -59,7 +59,9 @@ def test_save_load_resume(tmp_path):
     # resume into a trainer on a differently initialised model
     tr2, _ = _trainer(2)
     start, best = C.resume(tr2, ck)
-    assert start == 5 and best == 0.3 and tr2.updates == 37 and tr2.ni == 500 and tr2.last_opt_step == 499
+    assert start == 5 and best == 0.3 and tr2.updates == 37 and tr2.ni == 500 and tr2.last_opt_step == -1
+    # reference (trainer.py:331, 396): the first batch after a resume steps the optimizer (accumulate is 4 here)
+    assert tr2.sched.at(tr2.ni)[2] == 4 and tr2.will_step()
     sd2, ema2 = tr2.model.state_dict(), tr2.ema_state_dict()
     for k in sd:
         if not sd[k].is_floating_point():

@@ -125,7 +125,8 @@ def resume(trainer, ckpt):
         best_fitness = ckpt.get("best_fitness") or 0.0
     trainer.updates = int(ckpt.get("updates", 0))
     trainer.packs.valid = False
-    # the batch counter restarts at the resumed epoch (ni = i + nb * epoch, last_opt_step = -1: trainer.py:331, 370)
+    # the batch counter restarts at the resumed epoch (ni = i + nb * epoch: trainer.py:370); _do_train resets
+    # last_opt_step to -1 (trainer.py:331), so the first batch after a resume always runs the optimizer
     trainer.ni = start_epoch * trainer.sched.nb if trainer.sched.nb else 0
-    trainer.last_opt_step = trainer.ni - 1
+    trainer.last_opt_step = -1
     return start_epoch, best_fitness

@@ -732,7 +732,10 @@ class WgradDeferral:
 
     def add_colsum(self, x, part, xcs, N, HW, C, rows, chunks):
         """A bias gradient's column sums (adr_nc_reduce RED_STATS of dy into `part`), run in one batched launch
-        before the partial sums at the flush; dy stays alive until then."""
+        before the partial sums at the flush; dy stays alive until then and is pinned (as in add_dotsum) so no
+        fan-out sum accumulates into it in place before the flush reads it."""
+        x._adr_pinned = True
+        _v(x)[0]._adr_pinned = True
         self.cols.append(ColsumEntry(x.data_ptr(), part.data_ptr(), xcs, N, HW, C, rows, chunks))
         self.ckeep.append(x)
         self.ckeep.append(part)

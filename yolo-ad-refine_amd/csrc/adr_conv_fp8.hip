@@ -58,7 +58,10 @@ __global__ void __launch_bounds__(256) amax_bf16_kernel(const __bf16* x, int cs,
     const u32x4 v = ld16(x + p * cs + co + g * 8);
     const __bf16* e = reinterpret_cast<const __bf16*>(&v);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) m = fmaxf(m, fabsf((float)e[k]));
+    for (int k = 0; k < 8; ++k) {  // finite values only (as the conv's own amax collection)
+      const float f = fabsf((float)e[k]);
+      m = f < INFINITY ? fmaxf(m, f) : m;
+    }
   }
   __shared__ float sh[256];
   sh[threadIdx.x] = m;
@@ -105,20 +108,31 @@ typedef __attribute__((ext_vector_type(2))) short s16x2;
 typedef __attribute__((ext_vector_type(2))) unsigned short u16x2;
 
 // 8 bf16 (one 16-byte chunk) -> 8 e4m3 bytes as x / scale (scale a power of two: v_cvt_scalef32_pk_fp8_bf16, two
-// elements per instruction, straight from the bf16 pairs); m tracks max |x| as bf16 bit patterns (non-negative
-// floats order like their bits) with packed 16-bit maxima
-__device__ __forceinline__ u32x2 to_fp8x8(u32x4 v, float scale, u16x2& m) {
-  const bf16x2* e = reinterpret_cast<const bf16x2*>(&v);
+// elements per instruction, straight from the bf16 pairs); m tracks max |x| of the FINITE inputs as bf16 bit
+// patterns (non-negative floats order like their bits) with packed 16-bit maxima. The conversion does not
+// saturate, so finite magnitudes are first clamped to lim2 (both halves = the bf16 bits of 448 * scale): an input
+// past the delayed scale's 16x headroom becomes +-448, not NaN. Inf / NaN inputs pass through (NaN out, visible)
+// and are left out of the maximum, so one bad value cannot poison the next steps' scale.
+__device__ __forceinline__ u32x2 to_fp8x8(u32x4 v, float scale, unsigned lim2, u16x2& m) {
+  u32x4 c;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const unsigned a = v[q] & 0x7FFF7FFFu;
+    // per 16-bit half: all ones where |x| >= 0x7F80 (Inf / NaN); a half + 0x80 stays below 0x10000
+    const unsigned hb = (a + 0x00800080u) & 0x80008000u;
+    const unsigned nf = hb | (hb - (hb >> 15));
+    const unsigned fin = a & ~nf;
+    m = __builtin_elementwise_max(m, *reinterpret_cast<const u16x2*>(&fin));
+    const u16x2 cl = __builtin_elementwise_min(*reinterpret_cast<const u16x2*>(&fin),
+                                               *reinterpret_cast<const u16x2*>(&lim2));
+    c[q] = (*reinterpret_cast<const unsigned*>(&cl) | (a & nf)) | (v[q] & 0x80008000u);
+  }
+  const bf16x2* e = reinterpret_cast<const bf16x2*>(&c);
   s16x2 lo = {0, 0}, hi = {0, 0};
   lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, e[0], scale, false);
   lo = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(lo, e[1], scale, true);
   hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(hi, e[2], scale, false);
   hi = __builtin_amdgcn_cvt_scalef32_pk_fp8_bf16(hi, e[3], scale, true);
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const unsigned a = v[q] & 0x7FFF7FFFu;
-    m = __builtin_elementwise_max(m, *reinterpret_cast<const u16x2*>(&a));
-  }
   return (u32x2){*reinterpret_cast<const unsigned*>(&lo), *reinterpret_cast<const unsigned*>(&hi)};
 }
 
@@ -169,6 +183,8 @@ __global__ void __launch_bounds__(256, 2) conv_fp8_kernel(Fp8Args a) {
     __syncthreads();
   }
   const float inv_sa = s_inv;  // q = x / inv_sa, dequantised by inv_sa in the epilogue
+  // bf16 bits of 448 * inv_sa (exact: inv_sa is a power of two), in both halves: the saturation bound
+  const unsigned lim = __float_as_uint(fminf(448.f * inv_sa, 3.0e38f)) >> 16, lim2 = lim | (lim << 16);
 
   const int hw = a.rh * a.rw;
   const int kc = tid & 15;  // this thread's 8-element position within the 128-wide step
@@ -227,7 +243,7 @@ __global__ void __launch_bounds__(256, 2) conv_fp8_kernel(Fp8Args a) {
   auto store = [&]() {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i)
-      *reinterpret_cast<u32x2*>(&As[((tid >> 4) + 16 * i) * F8P + kc * 8]) = to_fp8x8(ra[i], inv_sa, xbits);
+      *reinterpret_cast<u32x2*>(&As[((tid >> 4) + 16 * i) * F8P + kc * 8]) = to_fp8x8(ra[i], inv_sa, lim2, xbits);
 #pragma unroll
     for (int i = 0; i < B_CH; ++i)
       if (tid + 256 * i < B_TOT) *reinterpret_cast<u32x4*>(&Bs[(b_row + 32 * i) * F8P + b_pos]) = rb[i];
