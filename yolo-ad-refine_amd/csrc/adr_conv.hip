@@ -20,6 +20,7 @@
 #include <type_traits>
 
 #include "adr_common.h"
+#include "adr_fin.h"
 
 namespace adr {
 
@@ -49,6 +50,8 @@ struct ConvArgs {
   // out = conv (+ out) + addend, NHWC with channel stride adcs (null: none)
   const __bf16* addend;
   int adcs;
+  // FWD with stats: the BatchNorm finalize in the last workgroup of each column tile (adr_conv2d_fwd_bf16_fin)
+  FinArgs fin;
 };
 
 constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
@@ -388,9 +391,18 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
         x1 += red[0][g][tid];
         x2 += red[1][g][tid];
       }
-      a.stats[(long)mt * 2 * a.N + n0 + tid] = x1;
-      a.stats[(long)mt * 2 * a.N + a.N + n0 + tid] = x2;
+      float* s = a.stats + (long)mt * 2 * a.N + n0 + tid;
+      if (MODE == CV_FWD && a.fin.on) {
+        st_coh(s, x1);
+        st_coh(s + a.N, x2);
+      } else {
+        s[0] = x1;
+        s[a.N] = x2;
+      }
     }
+    if constexpr (MODE == CV_FWD && !EPI)
+      if (a.fin.on)
+        fin_bn_tail(a.fin, a.stats, mt, n0, min(BN, a.N - n0), a.fin.f.counters + nt * (1 + a.fin.ngroups), lds_raw);
   }
 }
 
@@ -579,9 +591,18 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
         x1 += red[0][g][tid];
         x2 += red[1][g][tid];
       }
-      a.stats[(long)mt * 2 * a.N + n0 + tid] = x1;
-      a.stats[(long)mt * 2 * a.N + a.N + n0 + tid] = x2;
+      float* s = a.stats + (long)mt * 2 * a.N + n0 + tid;
+      if (!DG && a.fin.on) {
+        st_coh(s, x1);
+        st_coh(s + a.N, x2);
+      } else {
+        s[0] = x1;
+        s[a.N] = x2;
+      }
     }
+    if constexpr (!DG && !EPI)
+      if (a.fin.on)
+        fin_bn_tail(a.fin, a.stats, mt, n0, min(BN, a.N - n0), a.fin.f.counters + nt * (1 + a.fin.ngroups), lds_raw);
   }
 }
 
@@ -691,10 +712,16 @@ using namespace adr;
 
 static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                          float* stats, int accumulate, const float* escale, const float* eshift, int eact,
-                         void* stream) {
+                         void* stream, const adr_norm_fin* fin = nullptr) {
   int rc = conv_check(d);
   if (rc) return rc;
   ConvArgs g{};
+  if (fin) {
+    ADR_REQUIRE(stats && !bias && !accumulate && !escale && fin->kind == ADR_FIN_BN_FWD && fin->C == d->k,
+                "conv fwd fin: needs stats, no bias / accumulation, a BN forward finalize over K channels");
+    rc = fin_setup(fin, adr_conv2d_fwd_bf16_stat_tiles(d), adr_conv2d_fwd_bf16_col_tiles(d), d->n, g.fin);
+    if (rc) return rc;
+  }
   g.src = (const __bf16*)x; g.wt = (const __bf16*)w; g.out = (__bf16*)y; g.bias = bias; g.stats = stats;
   g.escale = escale; g.eshift = eshift; g.eact = escale ? eact : 0;
   g.n = d->n; g.sh_ = d->h; g.sw_ = d->w; g.scs = d->x_cstride; g.sco = d->x_coff; g.sc = d->c;
@@ -777,6 +804,17 @@ extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) {
   const ConvPlan pl = conv_plan(d, false);
   if (pl.tw) return conv3_tiles(d, pl.tw);
   return cdiv((long)d->n * d->ho * d->wo, CBM);
+}
+
+extern "C" int adr_conv2d_fwd_bf16_col_tiles(const adr_conv_desc* d) {
+  const ConvPlan pl = conv_plan(d, false);
+  return pl.tw ? d->k / pl.bn : cdiv(d->k, pl.bn);
+}
+
+extern "C" int adr_conv2d_fwd_bf16_fin(const adr_conv_desc* d, const void* x, const void* w, void* y, float* stats,
+                                       const adr_norm_fin* fin, void* stream) {
+  ADR_REQUIRE(fin, "conv fwd fin: fin");
+  return conv_fwd_impl(d, x, w, nullptr, y, stats, 0, nullptr, nullptr, 0, stream, fin);
 }
 
 extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, char* buf, int len) {
