@@ -94,8 +94,36 @@ int adr_conv2d_fwd_fp8_stat_tiles(const adr_conv_desc* d);
 int adr_conv2d_fwd_fp8(const adr_conv_desc* d, const void* x, const uint8_t* w_fp8, const float* w_inv_scale,
                        const float* amax_part, float* amax_next, const float* bias, void* y, float* stats,
                        void* stream);
-/* Mangled name of the kernel the bf16 engine launches for this contraction (dgrad != 0: the data gradient),
- * written to buf (len >= 64) — the label the bench's roofline and rocprofv3 share. */
+/* Training Conv-BN-act fusion on the bf16 engine (the XF kernels): the operand of a conv is staged through a
+ * training BatchNorm's affine + activation (forward) or its backward, so the elementwise pass and its launch
+ * disappear. Reference: Conv.forward = act(bn(conv(x))) (nn/modules/conv.py:48-50) and its autograd backward.
+ *   forward  (adr_conv2d_fwd_bf16_bnact): the conv input x is the producer's pre-BN output y (desc x view);
+ *            the operand is z = act(y * scale + shift) (0 in the zero padding); z is side-written to `out`
+ *            (every element exactly once) for the layer's other readers and the weight gradient.
+ *   backward (adr_conv2d_dgrad_bf16_bnact): the data gradient of the conv that produced y, fed dz (the gradient of
+ *            z = act(bn(y))); the operand is dy = A * g + B * y + C, g = dz * act'(y * scale + shift) (A / B / Cc
+ *            from adr_bn_bwd_finalize), side-written to `out` for the weight gradient.
+ * The operand values are bitwise those adr_affine_act / adr_affine_act_bwd store (same bf16 arithmetic).
+ * act: ADR_ACT_NONE or ADR_ACT_SILU; at most 512 reduction channels. */
+typedef struct adr_bnact_xf {
+  const void* y;        /* backward: the BN input y (NHWC bf16 over the dz grid, channel stride y_cstride) */
+  const float* scale;
+  const float* shift;
+  const float* A;       /* backward coefficients */
+  const float* B;
+  const float* Cc;
+  void* out;            /* side output (z / dy), NHWC bf16, channel stride out_cstride */
+  int y_cstride, out_cstride, act, pad_;
+} adr_bnact_xf;
+int adr_conv2d_fwd_bf16_bnact(const adr_conv_desc* d, const void* y, const void* w_krsc, void* out, float* stats,
+                              const adr_bnact_xf* xf, void* stream);
+int adr_conv2d_dgrad_bf16_bnact(const adr_conv_desc* d, const void* dz, const void* w_crsk, void* dx, int accumulate,
+                                const void* addend, int addend_cstride, const adr_bnact_xf* xf, void* stream);
+/* Times x100 the XF kernel for this contraction stages each source element (column tiles x gathers per element):
+ * the transform is per-staged-element VALU work, so the fusion pays only near 100. */
+int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad);
+/* Mangled name of the kernel the bf16 engine launches for this contraction (dgrad bit 0: the data gradient; bit 1:
+ * the XF Conv-BN-act variant), written to buf (len >= 64) — the label the bench's roofline and rocprofv3 share. */
 int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, char* buf, int len);
 /* dx = conv_transpose(dy, w) (+ bias[c]) (+ dx if accumulate).  Also ConvTranspose2d forward
  * (nn.ConvTranspose2d weight (Cin_T, Cout_T, R, S) channels_last == KRSC of the equivalent conv). */

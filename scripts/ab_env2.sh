@@ -1,0 +1,11 @@
+# Same-box A/B of environment settings on the bench step: bash scripts/ab_env2.sh <tag> "<envA>" "<envB>" [reps]
+# (each setting runs `reps` times alternately; prints ms_per_step per run)
+set -o pipefail
+TAG=$1; A=$2; B=$3; R=${4:-2}; OUT=gpurun_out/$TAG; mkdir -p $OUT
+for r in $(seq 1 $R); do
+  for v in A B; do
+    E=$([ $v = A ] && echo "$A" || echo "$B")
+    env $E timeout -k 10 240 python bench.py --no-cpu-baseline --steps 30 --infer-steps 0 --roofline-steps 0 > $OUT/$v$r.log 2>&1 || { tail -5 $OUT/$v$r.log; exit 1; }
+    echo "$v [$E] run $r: $(grep -o '"ms_per_step": [0-9.]*' $OUT/$v$r.log)"
+  done
+done

@@ -94,7 +94,12 @@ def test_conv_bn_fin_statistics_vs_float64(n, c, hw):
     x = torch.randn(n, c, hw, hw, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     fin = K.BnFin(m.bn, x.device)
     rm0 = m.bn.running_mean.clone()
-    y, st = K.conv2d(x, m.conv.weight, None, 1, 0, True, 0, bnfin=fin)
+    old = K.NORM_FIN
+    K.NORM_FIN = True
+    try:
+        y, st = K.conv2d(x, m.conv.weight, None, 1, 0, True, 0, bnfin=fin)
+    finally:
+        K.NORM_FIN = old
     assert fin.done
     yd = y.detach().double()
     mean = yd.mean(dim=(0, 2, 3))

@@ -518,12 +518,26 @@ def conv_fwd_fp8(d, xp, w, Cw, Cp, bias, yp, stats):
                            fptr(bias), ctypes.c_void_p(yp), fptr(stats), stream())
 
 
-def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0, addend=None):
+def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0, addend=None, xf=None, dy=None):
     """dx (+)= conv_transpose(dy, w) (+ addend); wpair = (KRSC, CRSK-or-None) packed weights (pack_weight2).
-    `addend` (an NHWC bf16 view shaped like dx) is added in the bf16 engine's epilogue."""
+    `addend` (an NHWC bf16 view shaped like dx) is added in the bf16 engine's epilogue. With `xf` (a BnXf) the
+    operand is the BN-act backward of xf.dz, applied while staging and side-written into `dy` (which dyp is not
+    read from)."""
     krsc, crsk = wpair
     e2 = crsk is not None and _engine2(d, d.k)
     mode = 2 if d.stride_h == 2 else 1
+    if xf is not None:
+        _, dzp, dzcs = nhwc(xf.dz)
+        d.y_cstride = dzcs  # the operand's view: dz (dy shares its pixel grid, written through the side output)
+        st = xf.struct(dy)
+        sym = "" if _TIMING is None else _conv2_symbol(d, 3)
+        tok = _t0(sym, *_conv_work(d), _shape(d, "dgrad+bnact") if _TIMING is not None else "")
+        lib.adr_conv2d_dgrad_bf16_bnact(ctypes.byref(d), ctypes.c_void_p(dzp), ctypes.c_void_p(crsk.data_ptr()),
+                                        ctypes.c_void_p(dxp), int(accumulate),
+                                        None if addend is None else ctypes.c_void_p(addend.data_ptr()),
+                                        0 if addend is None else addend.stride(3), ctypes.byref(st), stream())
+        _t1(tok)
+        return
     sym = "" if _TIMING is None else (_conv2_symbol(d, True) if e2 else
                                       _gemm_symbol(d.dtype, _bn_of(d.c), 3 if mode == 2 else 1))
     if addend is not None:
@@ -1057,22 +1071,29 @@ class Conv2dFn(torch.autograd.Function):
         x, wp, wt = ctx.saved_tensors
         stride, pad, cpad, wshape, has_b = ctx.meta
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+        pend = BnXf.take(dy)  # an unwritten BN-act backward (BNActFn with xfuse): dz + coefficients
         dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
         N, C, H, W = x.shape
         K, _, R, S = wshape
         x, xp, xcs = nhwc(x)
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
         dx = dw = db = None
+        if pend is not None:
+            d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
+            if not (ctx.needs_input_grad[0] and wt is not None and _engine2(d2, d2.k) and d2.stride_h in (1, 2) and
+                    lib.adr_conv2d_bf16_xf_reuse(ctypes.byref(d2), 1) <= BN_XF_MAX_REUSE):
+                pend.materialize(dy)  # no fused data gradient for this conv: write dy first
+                pend = None
         if ctx.needs_input_grad[0]:
             d2, _, _ = conv_desc(N, H, W, C, C, K, R, S, sh, sw, ph, pw, dycs, x.dtype)
             if ctx.sink is not None:  # into the fan-out's shared gradient (accumulating after the first consumer)
                 buf, acc, add = ctx.sink.claim(x.device, can_add=wt is not None and _engine2(d2, d2.k))
                 if buf.stride(3) != C:  # a seeded concat-gradient slice: the concat's channel stride
                     d2, _, _ = conv_desc(N, H, W, C, buf.stride(3), K, R, S, sh, sw, ph, pw, dycs, x.dtype)
-                conv_dgrad(d2, dyp, (wp, wt), None, buf.data_ptr(), accumulate=acc, addend=add)
+                conv_dgrad(d2, dyp, (wp, wt), None, buf.data_ptr(), accumulate=acc, addend=add, xf=pend, dy=dy)
             else:
                 dx = empty_act(N, C, H, W, x.dtype, x.device)
-                conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr())
+                conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr(), xf=pend, dy=dy)
         if ctx.needs_input_grad[1]:
             dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
         if has_b and ctx.needs_input_grad[2]:
@@ -1129,12 +1150,16 @@ class BNActFn(torch.autograd.Function):
     """act(BatchNorm2d(y)) — train mode uses batch statistics (from the conv epilogue when given)."""
 
     @staticmethod
-    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None, bnfin=None):
+    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None, bnfin=None, xfuse=False):
         dtype = y.dtype
         y, yp, ycs = nhwc(y)
         N, C, H, W = y.shape
         HW = H * W
         dev = y.device
+        # the backward may hand its dy to the producing conv unmaterialised (see BnXf): y must come from a dense conv
+        # whose only reader is this BN (Conv.forward), on the bf16 engine's XF coefficient table
+        ctx.xfuse = bool(xfuse) and BN_XF_BWD and training and dtype == torch.bfloat16 and act in ("silu", "none") \
+            and C <= 512 and C % 8 == 0
         if training and bnfin is not None and bnfin.done:  # the conv's last workgroup finalized the statistics
             scale, shift, mean, rstd = bnfin.scale, bnfin.shift, bnfin.mean, bnfin.rstd
         else:
@@ -1200,11 +1225,72 @@ class BNActFn(torch.autograd.Function):
                                     fptr(gamma.detach()), pg, pb, fptr(A), fptr(B), fptr(Cc), int(training), acc_g,
                                     stream())
         dy = empty_act(N, C, H, W, y.dtype, dev)
-        lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
-                               ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
-                               fptr(Cc), 0, 0, ACT[act], N, HW, C, 0, stream())
+        pend = BnXf(y, dz, scale, shift, A, B, Cc, act)
+        if ctx.xfuse:  # the conv's data gradient applies it while staging its operand (and side-writes dy)
+            pend.attach(dy)
+        else:
+            pend.materialize(dy)
         return (dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None, None, None,
-                None)
+                None, None)
+
+
+# Training Conv-BN-act backward fusion: BNActFn.backward computes the coefficients (nc_reduce + bn_bwd_finalize)
+# but leaves dy = A * dz * act'(y * s + t) + B * y + C unwritten; the producing conv's Conv2dFn.backward runs its
+# data gradient on dz with that transform in the operand staging (adr_conv2d_dgrad_bf16_bnact), which also writes
+# dy once for the weight gradient — the affine_act_bwd pass and its launch disappear. ADR_BN_XF_BWD=0 disables.
+BN_XF_BWD = bool(int(__import__("os").environ.get("ADR_BN_XF_BWD", "1")))
+# The transform is VALU work per staged operand element (a sigmoid for SiLU): measured, the fused data gradient of a
+# 3x3 implicit-GEMM conv (each dz element staged 9x) or of a multi-column-tile 1x1 ran 3x slower than the
+# affine_act_bwd + dgrad pair, so the fusion is taken only where each element is staged about once (x100)
+BN_XF_MAX_REUSE = int(__import__("os").environ.get("ADR_BN_XF_MAX_REUSE", "150"))
+_BNXF_PENDING = {}  # data_ptr -> BnXf: unwritten dy buffers handed to a conv backward
+
+
+class BnXfStruct(ctypes.Structure):
+    """adr_bnact_xf (include/adr.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("y", "scale", "shift", "A", "B", "Cc", "out")] + [
+        (n, ctypes.c_int) for n in ("y_cstride", "out_cstride", "act", "pad_")]
+
+
+class BnXf:
+    """A pending BN-act backward: dy (the buffer it is attached to) = A * g + B * y + C, g = dz * act'(y*s + t)."""
+    __slots__ = ("y", "dz", "scale", "shift", "A", "B", "Cc", "act")
+
+    def __init__(self, y, dz, scale, shift, A, B, Cc, act):
+        self.y, self.dz, self.scale, self.shift, self.A, self.B, self.Cc, self.act = y, dz, scale, shift, A, B, Cc, act
+
+    def attach(self, dy):
+        _BNXF_PENDING[dy.data_ptr()] = self
+        dy._adr_bnxf = self
+
+    @staticmethod
+    def take(dy):
+        """The pending transform of a gradient buffer handed to a conv backward (removed from the registry)."""
+        p = getattr(dy, "_adr_bnxf", None)
+        if p is None:
+            p = _BNXF_PENDING.get(dy.data_ptr())
+        if p is not None:
+            _BNXF_PENDING.pop(dy.data_ptr(), None)
+            try:
+                del dy._adr_bnxf
+            except AttributeError:
+                pass
+        return p
+
+    def materialize(self, dy):
+        """Write dy with adr_affine_act_bwd (the unfused path)."""
+        y, yp, ycs = nhwc(self.y)
+        _, dzp, dzcs = nhwc(self.dz)
+        N, C, H, W = y.shape
+        lib.adr_affine_act_bwd(dcode(y.dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
+                               ctypes.c_void_p(dy.data_ptr()), dy.stride(3), 0, fptr(self.scale), fptr(self.shift),
+                               fptr(self.A), fptr(self.B), fptr(self.Cc), 0, 0, ACT[self.act], N, H * W, C, 0,
+                               stream())
+
+    def struct(self, dy):
+        _, yp, ycs = nhwc(self.y)
+        return BnXfStruct(yp, self.scale.data_ptr(), self.shift.data_ptr(), self.A.data_ptr(), self.B.data_ptr(),
+                          self.Cc.data_ptr(), dy.data_ptr(), ycs, dy.stride(3), ACT[self.act], 0)
 
 
 _GN_FUSED = bool(int(__import__("os").environ.get("ADR_GN_FUSED", "1")))  # 0: the 3-launch path (A/B, parity)
@@ -1500,9 +1586,11 @@ def conv_bn_act_eval(x, w, stride, pad, bn, act: str, cpad=0, out=None):
     return y if out is None else out
 
 
-def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None, bnfin=None):
+def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None, bnfin=None, xfuse=False):
+    """act(BatchNorm(y)). xfuse: y is a dense conv's output read only here (Conv.forward), so the backward may hand
+    its dy to that conv's data gradient unwritten (BnXf)."""
     return BNActFn.apply(y, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, act, training, bn.momentum,
-                         bn.eps, None if out is None else OutBox(out), bnfin)
+                         bn.eps, None if out is None else OutBox(out), bnfin, xfuse)
 
 
 def gn_act(y, gn: torch.nn.Module, act: str):

@@ -98,7 +98,7 @@ class Conv(nn.Module):
         fin = K.BnFin(self.bn, x.device) if self.training and K.NORM_FIN else None
         y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight),
                          bnfin=fin)
-        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out, bnfin=fin)
+        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out, bnfin=fin, xfuse=True)
 
     def stem_ok(self):
         """The adr_stem kernels cover Conv(3, K in {16, 32, 64}, 3, 2) with pad 1 (every yaml's model.0)."""

@@ -94,6 +94,21 @@ __device__ __forceinline__ float act_bwd_c(float v) {
   }
 }
 
+// BatchNorm-affine + activation of one element and its backward, with the fma order written out so that every
+// kernel that evaluates them (affine_act / affine_act_bwd, nc_reduce's backward statistics, the conv engine's XF
+// operand staging) produces the same bits:  z = act(y * s + t);  dy = A * g + B * y + C, g = dz * act'(y * s + t)
+template <int ACT, bool FAST = false>
+__device__ __forceinline__ float bn_act_fwd_elem(float y, float s, float t) {
+  return act_fwd_c<ACT, FAST>(__builtin_fmaf(y, s, t));
+}
+template <int ACT, bool FAST = false>
+__device__ __forceinline__ float bn_act_g(float dz, float y, float s, float t) {
+  return dz * act_bwd_c<ACT, FAST>(__builtin_fmaf(y, s, t));
+}
+__device__ __forceinline__ float bn_act_bwd_lin(float g, float y, float A, float B, float C) {
+  return __builtin_fmaf(A, g, __builtin_fmaf(B, y, C));
+}
+
 __device__ __forceinline__ float act_fwd(int act, float v) {
   switch (act) {
     case ACT_SILU: return act_fwd_c<ACT_SILU>(v);

@@ -52,9 +52,92 @@ struct ConvArgs {
   int adcs;
   // FWD with stats: the BatchNorm finalize in the last workgroup of each column tile (adr_conv2d_fwd_bf16_fin)
   FinArgs fin;
+  // A-operand BatchNorm-activation transform (XF kernels, adr_conv2d_{fwd,dgrad}_bf16_bnact): the A source is a
+  // training BatchNorm's input y (FWD: the operand is z = act(y * s + t), 0 in the padding) or the gradient dz of
+  // its output (DGRAD: the operand is dy = A * g + B * y + C with g = dz * act'(y * s + t), 0 outside the image,
+  // y read alongside dz); coefficients per reduction channel, the operand side-written once (unique writer) to xo.
+  const __bf16* xy;
+  int xycs, xy_bytes;
+  const float* xs;
+  const float* xt;
+  const float* xA;
+  const float* xB;
+  const float* xC;
+  int xact;
+  __bf16* xo;
+  int xocs;
 };
 
 constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
+enum XfMode { XF_NONE = 0, XF_FWD = 1, XF_BWD = 2 };
+constexpr int XMAXC = 512;  // reduction channels of the XF coefficient table (LDS)
+
+// XF coefficients of this thread's 8 channels (loaded from the LDS table once per staged K-step: all of a thread's
+// A chunks in a step share their channels)
+template <int XF>
+struct XfCoef {
+  float s[8], t[8], A[XF == XF_BWD ? 8 : 1], B[XF == XF_BWD ? 8 : 1], C[XF == XF_BWD ? 8 : 1];
+  __device__ __forceinline__ void load(const float* tab, int c) {
+    ld_coef<8>(tab + c, s);
+    ld_coef<8>(tab + XMAXC + c, t);
+    if constexpr (XF == XF_BWD) {
+      ld_coef<8>(tab + 2 * XMAXC + c, A);
+      ld_coef<8>(tab + 3 * XMAXC + c, B);
+      ld_coef<8>(tab + 4 * XMAXC + c, C);
+    }
+  }
+};
+
+// the XF transform of one 16-byte chunk (8 channels of the reduction): the element functions affine_act_kernel
+// (FWD) / affine_act_bwd_kernel (BWD) use on the bf16 path, so the operand equals what those kernels store
+template <int XF>
+__device__ __forceinline__ u32x4 xf_chunk(u32x4 v, u32x4 yv, const XfCoef<XF>& k, int act) {
+  const __bf16* e = reinterpret_cast<const __bf16*>(&v);
+  const __bf16* ye = reinterpret_cast<const __bf16*>(&yv);
+  u32x4 o;
+  __bf16* oe = reinterpret_cast<__bf16*>(&o);
+  if constexpr (XF == XF_FWD) {
+    if (act == ACT_SILU) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) oe[q] = (__bf16)bn_act_fwd_elem<ACT_SILU, true>((float)e[q], k.s[q], k.t[q]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) oe[q] = (__bf16)bn_act_fwd_elem<ACT_NONE, true>((float)e[q], k.s[q], k.t[q]);
+    }
+  } else {
+    if (act == ACT_SILU) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float xf = (float)ye[q];
+        oe[q] = (__bf16)bn_act_bwd_lin(bn_act_g<ACT_SILU, true>((float)e[q], xf, k.s[q], k.t[q]), xf, k.A[q], k.B[q],
+                                        k.C[q]);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float xf = (float)ye[q];
+        oe[q] = (__bf16)bn_act_bwd_lin(bn_act_g<ACT_NONE, true>((float)e[q], xf, k.s[q], k.t[q]), xf, k.A[q],
+                                        k.B[q], k.C[q]);
+      }
+    }
+  }
+  return o;
+}
+
+// stage the XF coefficient table (per reduction channel) into LDS
+template <int XF>
+__device__ __forceinline__ void xf_table(const ConvArgs& a, float* tab) {
+  for (int c = threadIdx.x; c < a.sc; c += 256) {
+    tab[c] = a.xs[c];
+    tab[XMAXC + c] = a.xt[c];
+    if constexpr (XF == XF_BWD) {
+      tab[2 * XMAXC + c] = a.xA[c];
+      tab[3 * XMAXC + c] = a.xB[c];
+      tab[4 * XMAXC + c] = a.xC[c];
+    }
+  }
+  __syncthreads();
+}
 
 // the eval epilogue's activation (block-uniform code; 0 = none keeps the plain acc + bias path: fma by 1 is exact).
 // bf16 output: the hardware exp/rcp sigmoid, as the bf16 affine_act kernels use
@@ -77,7 +160,7 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
   return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
 }
 
-template <int BN, int MODE, bool EPI>
+template <int BN, int MODE, bool EPI, int XF = XF_NONE>
 __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
   constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
   constexpr int WROWS = CBM / WAVES_M, WCOLS = BN / WAVES_N;
@@ -146,7 +229,7 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
   // classes keep the general (image, y, x) form.
   constexpr bool LIN = MODE != CV_DGRAD2;
   constexpr int SG = MODE == CV_FWD ? 1 : -1;
-  int r_img[A_CH], r_y[A_CH], r_x[A_CH], r_off[A_CH];
+  int r_img[A_CH], r_y[A_CH], r_x[A_CH], r_off[A_CH], r_pix[A_CH];
   bool r_ok[A_CH];
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
@@ -161,17 +244,29 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
       // origin of the gather window: FWD y*str - pad (+kh) ; DGRAD y + pad (-kh)
       r_y[i] = MODE == CV_FWD ? r_y[i] * a.str - a.ph : r_y[i] + a.ph;
       r_x[i] = MODE == CV_FWD ? r_x[i] * a.str - a.pw : r_x[i] + a.pw;
-      r_off[i] = ((r_img[i] * a.sh_ + r_y[i]) * a.sw_ + r_x[i]) * a.scs + a.sco;
+      r_pix[i] = (r_img[i] * a.sh_ + r_y[i]) * a.sw_ + r_x[i];
+      r_off[i] = r_pix[i] * a.scs + a.sco;
     }
   }
+  // XF: coefficient table, and per register stage the chunk validity / unique-writer bits, the chunk's channel and
+  // its source pixels (the second operand y and the side output use the source grid with their own strides)
+  constexpr int XTAB = XF == XF_BWD ? 5 * XMAXC : XF == XF_FWD ? 2 * XMAXC : 4;
+  __shared__ __attribute__((aligned(16))) float xtab[XTAB];
+  if constexpr (XF != XF_NONE) xf_table<XF>(a, xtab);
   const int RS = a.r * a.s;
   const int ksteps = (ktot + CBK - 1) / CBK;
 
   // DB tiles keep two register stages: the global loads of step t+2 are issued while step t computes, so each
   // load has two K-steps of MFMA work to land behind (one step for the single-buffered narrow tiles)
   constexpr int NR = DB ? 2 : 1;
+  static_assert(XF == XF_NONE || !DB, "XF kernels are single-buffered (BN <= 64)");
   u32x4 ra_s[NR][A_CH], rb_s[NR][B_CH];
   const u32x4 zero = {0u, 0u, 0u, 0u};
+  constexpr int XA = XF == XF_BWD ? A_CH : 1;
+  u32x4 xy_s[XA];          // BWD: y chunks
+  int xp_s[A_CH];          // source pixel of each chunk
+  unsigned xok = 0, xw = 0;
+  int xc = 0;
   // Reduction-position decoder, advanced by CBK per k-step without integer division: this thread's chunk sits
   // at k = t*CBK + kc*8 = (tap ta, channel ca); (kh, kw) are the tap's kernel coordinates. The B rows use the
   // same chunk position (q & 7 == kc for every B chunk of the thread), so one decoder serves both operands.
@@ -210,11 +305,29 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
   constexpr unsigned OOR = 0x7FFFFFF0u;
   const __amdgpu_buffer_rsrc_t src_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, a.src_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, a.wt_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xy_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.xy, (short)0, XF == XF_BWD ? a.xy_bytes : 0, 0x00020000);
+  // XF unique writer: of the (row, tap) pairs that gather one source pixel, the one with the largest tap. FWD
+  // (stride s): the next larger tap kh + s pairs with output row oy - 1; DGRAD (any stride): tap kh + 1 pairs with
+  // dx row iy + 1. Only column tile 0 writes.
+  auto xf_writer = [&](int i, int kh_, int kw_) -> bool {
+    if (nt != 0) return false;
+    if constexpr (MODE == CV_FWD)
+      return (kh_ + a.str >= a.r || r_y[i] == -a.ph) && (kw_ + a.str >= a.s || r_x[i] == -a.pw);
+    else if constexpr (MODE == CV_DGRAD)
+      return (kh_ + 1 >= a.r || r_y[i] - a.ph + 1 >= a.rh) && (kw_ + 1 >= a.s || r_x[i] - a.pw + 1 >= a.rw);
+    else
+      return (kh_ + 1 >= a.r || r_y[i] + 1 >= a.rh) && (kw_ + 1 >= a.s || r_x[i] + 1 >= a.rw);
+  };
   auto load = [&](auto S) {
     u32x4(&ra)[A_CH] = ra_s[decltype(S)::value];
     u32x4(&rb)[B_CH] = rb_s[decltype(S)::value];
     const bool kok = ta < ntaps;
     const int c = ca;
+    if constexpr (XF != XF_NONE) {
+      xok = xw = 0;
+      xc = c;
+    }
     if constexpr (LIN) {
       const int dy = SG * kh, dx = SG * kw;
       const int toff = (dy * a.sw_ + dx) * a.scs + c;
@@ -223,6 +336,14 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
         const bool ok = kok && r_ok[i] && (unsigned)(r_y[i] + dy) < (unsigned)a.sh_ &&
                         (unsigned)(r_x[i] + dx) < (unsigned)a.sw_;
         ra[i] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, ok ? (unsigned)(r_off[i] + toff) * 2u : OOR, 0, 0);
+        if constexpr (XF != XF_NONE) {
+          const int pix = r_pix[i] + dy * a.sw_ + dx;
+          xp_s[i] = pix;
+          xok |= (unsigned)ok << i;
+          xw |= (unsigned)(ok && xf_writer(i, kh, kw)) << i;
+          if constexpr (XF == XF_BWD)
+            xy_s[i] = __builtin_amdgcn_raw_buffer_load_b128(xy_rs, ok ? (unsigned)(pix * a.xycs + c) * 2u : OOR, 0, 0);
+        }
       }
 #pragma unroll
       for (int i = 0; i < B_CH; ++i)
@@ -235,7 +356,14 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
         const int ny = r_y[i] + a.ph - kh, nx = r_x[i] + a.pw - kw;
         const int sy = ny >> 1, sx = nx >> 1;
         const bool ok = kok && r_ok[i] && ny >= 0 && nx >= 0 && sy < a.sh_ && sx < a.sw_;
-        ra[i] = ok ? ld16(a.src + ((long)(r_img[i] * a.sh_ + sy) * a.sw_ + sx) * a.scs + a.sco + c) : zero;
+        const int pix = (r_img[i] * a.sh_ + sy) * a.sw_ + sx;
+        ra[i] = ok ? ld16(a.src + (long)pix * a.scs + a.sco + c) : zero;
+        if constexpr (XF != XF_NONE) {
+          xp_s[i] = pix;
+          xok |= (unsigned)ok << i;
+          xw |= (unsigned)(ok && xf_writer(i, kh, kw)) << i;
+          if constexpr (XF == XF_BWD) xy_s[i] = ok ? ld16(a.xy + (long)pix * a.xycs + c) : zero;
+        }
       }
       const int tf = kh * a.s + kw;
 #pragma unroll
@@ -247,8 +375,19 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
   auto store = [&](auto S) {
     const u32x4(&ra)[A_CH] = ra_s[decltype(S)::value];
     const u32x4(&rb)[B_CH] = rb_s[decltype(S)::value];
+    XfCoef<XF == XF_NONE ? XF_FWD : XF> xk;
+    if constexpr (XF != XF_NONE) xk.load(xtab, xc);
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) st16(&As[((tid >> 3) + 32 * i) * CLD + kc * 8], ra[i]);
+    for (int i = 0; i < A_CH; ++i) {
+      if constexpr (XF == XF_NONE) {
+        st16(&As[((tid >> 3) + 32 * i) * CLD + kc * 8], ra[i]);
+      } else {
+        u32x4 v = zero;
+        if ((xok >> i) & 1) v = xf_chunk<XF>(ra[i], xy_s[XF == XF_BWD ? i : 0], xk, a.xact);
+        if ((xw >> i) & 1) st16(a.xo + (long)xp_s[i] * a.xocs + xc, v);
+        st16(&As[((tid >> 3) + 32 * i) * CLD + kc * 8], v);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int q = tid + 256 * i;
@@ -419,7 +558,7 @@ constexpr int C3_CK = 32, C3_LD = C3_CK;  // chunk channels; unpadded 64-byte LD
 // group reads cover 16 disjoint bank quads (48 KB per block: 3 blocks per CU)
 __device__ __forceinline__ int c3_swz(int row, int kq) { return row * C3_LD + ((kq ^ ((row >> 2) & 3)) << 3); }
 
-template <int TW, bool DG, int BN, bool EPI>
+template <int TW, bool DG, int BN, bool EPI, int XF = XF_NONE>
 __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   constexpr int TH = 128 / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
   constexpr int A_TOT = NPIX * (C3_CK / 8), A_CH = (A_TOT + 255) / 256;
@@ -448,14 +587,25 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   constexpr unsigned OOR = 0x7FFFFFF0u;
   const __amdgpu_buffer_rsrc_t src_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, a.src_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, a.wt_bytes, 0x00020000);
-  int a_off[A_CH];
+  int a_off[A_CH], a_pix[A_CH];
+  unsigned a_in = 0;  // XF: halo chunks in the tile interior (their source pixel belongs to this tile)
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
     const int e = tid + 256 * i, q = e >> 2, hy = q / HWW, hx = q - (q / HWW) * HWW;
     const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
     const bool ok = e < A_TOT && gy >= 0 && gy < a.sh_ && gx >= 0 && gx < a.sw_;
-    a_off[i] = ok ? ((img * a.sh_ + gy) * a.sw_ + gx) * a.scs + a.sco + (e & 3) * 8 : -1;
+    a_pix[i] = ok ? (img * a.sh_ + gy) * a.sw_ + gx : -1;
+    a_off[i] = ok ? a_pix[i] * a.scs + a.sco + (e & 3) * 8 : -1;
+    a_in |= (unsigned)(ok && hy >= 1 && hy <= TH && hx >= 1 && hx <= TW) << i;
   }
+  constexpr int XTAB = XF == XF_BWD ? 5 * XMAXC : XF == XF_FWD ? 2 * XMAXC : 4;
+  __shared__ __attribute__((aligned(16))) float xtab[XTAB];
+  if constexpr (XF != XF_NONE) xf_table<XF>(a, xtab);
+  const __amdgpu_buffer_rsrc_t xy_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.xy, (short)0, XF == XF_BWD ? a.xy_bytes : 0, 0x00020000);
+  constexpr int XA = XF == XF_BWD ? A_CH : 1;
+  u32x4 ry[XA];
+  const int xq = (tid & 3) * 8;  // this thread's channels within a chunk step
   const int b_row = (tid >> 2) % BN, b_tap0 = tid / (4 * BN);
   const bool b_ok = n0 + b_row < a.N;
   const int b_off = (n0 + b_row) * 9 * a.sc + (tid & 3) * 8;  // + tap * sc + c0
@@ -463,8 +613,12 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   u32x4 ra[A_CH], rb[B_CH];
   auto load = [&](int c0) {
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i)
+    for (int i = 0; i < A_CH; ++i) {
       ra[i] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, a_off[i] >= 0 ? (unsigned)(a_off[i] + c0) * 2u : OOR, 0, 0);
+      if constexpr (XF == XF_BWD)
+        ry[i] = __builtin_amdgcn_raw_buffer_load_b128(
+            xy_rs, a_pix[i] >= 0 ? (unsigned)(a_pix[i] * a.xycs + c0 + xq) * 2u : OOR, 0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int tap = i * TPP + b_tap0;
@@ -472,11 +626,20 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
           wt_rs, (b_ok && tap < 9) ? (unsigned)(b_off + tap * a.sc + c0) * 2u : OOR, 0, 0);
     }
   };
-  auto store = [&]() {
+  auto store = [&](int c0) {
+    XfCoef<XF == XF_NONE ? XF_FWD : XF> xk;
+    if constexpr (XF != XF_NONE) xk.load(xtab, c0 + xq);
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int e = tid + 256 * i;
-      if (e < A_TOT) st16(&As[c3_swz(e >> 2, e & 3)], ra[i]);
+      if constexpr (XF == XF_NONE) {
+        if (e < A_TOT) st16(&As[c3_swz(e >> 2, e & 3)], ra[i]);
+      } else {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (a_pix[i] >= 0) v = xf_chunk<XF>(ra[i], ry[XF == XF_BWD ? i : 0], xk, a.xact);
+        if (nt == 0 && ((a_in >> i) & 1)) st16(a.xo + (long)a_pix[i] * a.xocs + c0 + xq, v);
+        if (e < A_TOT) st16(&As[c3_swz(e >> 2, e & 3)], v);
+      }
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
@@ -502,7 +665,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   const int nch = a.sc / C3_CK;
   load(0);
   for (int ch = 0; ch < nch; ++ch) {
-    store();
+    store(ch * C3_CK);
     __syncthreads();
     if (ch + 1 < nch) load((ch + 1) * C3_CK);
 #pragma unroll
@@ -616,6 +779,15 @@ template <int TW, bool DG, int BN>
 __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) { conv3_body<TW, DG, BN, false>(a); }
 template <int TW, int BN>
 __global__ void __launch_bounds__(256, 3) conv3_act_kernel(ConvArgs a) { conv3_body<TW, false, BN, true>(a); }
+// training Conv-BN-act fusion: the A operand is the producer BatchNorm's input (FWD) or the gradient of its output
+// (DGRAD) and the BN-act (backward) is applied while staging it (XF_FWD / XF_BWD); the coefficient table and the
+// second operand cost LDS and registers, so these run at 3 (2 for the 3x3 halo tiles) workgroups per CU
+template <int BN, int MODE, int XF>
+__global__ void __launch_bounds__(256, (XF == XF_BWD && BN == 64) ? 2 : 3) conv_bf16_xf_kernel(ConvArgs a) {
+  conv_bf16_body<BN, MODE, false, XF>(a);
+}
+template <int TW, bool DG, int BN, int XF>
+__global__ void __launch_bounds__(256, 2) conv3_xf_kernel(ConvArgs a) { conv3_body<TW, DG, BN, false, XF>(a); }
 
 // tile width of the 3x3 path for this geometry, or 0 when it does not apply
 static int conv3_tw(const adr_conv_desc* d, int red_ch, int out_ch) {
@@ -632,6 +804,17 @@ template <bool DG>
 static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hipStream_t st) {
   g.ntiles = g.N / bn;
   dim3 grid(conv3_tiles(d, tw) * g.ntiles);
+  if (g.xs) {  // XF: FWD applies the producer's BN-act, DGRAD its backward
+    constexpr int XF = DG ? XF_BWD : XF_FWD;
+    if (bn == 64) {
+      if (tw == 16) hipLaunchKernelGGL((conv3_xf_kernel<16, DG, 64, XF>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((conv3_xf_kernel<8, DG, 64, XF>), grid, dim3(256), 0, st, g);
+    } else {
+      if (tw == 16) hipLaunchKernelGGL((conv3_xf_kernel<16, DG, 32, XF>), grid, dim3(256), 0, st, g);
+      else hipLaunchKernelGGL((conv3_xf_kernel<8, DG, 32, XF>), grid, dim3(256), 0, st, g);
+    }
+    return;
+  }
   if (!DG && g.escale) {
     if (bn == 64) {
       if (tw == 16) hipLaunchKernelGGL((conv3_act_kernel<16, 64>), grid, dim3(256), 0, st, g);
@@ -653,6 +836,15 @@ static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hi
 
 template <int MODE>
 static void launch_conv(int bn, dim3 grid, const ConvArgs& g, hipStream_t st) {
+  if (g.xs) {  // XF (bn <= 64)
+    constexpr int XF = MODE == CV_FWD ? XF_FWD : XF_BWD;
+    switch (bn) {
+      case 16: hipLaunchKernelGGL((conv_bf16_xf_kernel<16, MODE, XF>), grid, dim3(256), 0, st, g); break;
+      case 32: hipLaunchKernelGGL((conv_bf16_xf_kernel<32, MODE, XF>), grid, dim3(256), 0, st, g); break;
+      default: hipLaunchKernelGGL((conv_bf16_xf_kernel<64, MODE, XF>), grid, dim3(256), 0, st, g); break;
+    }
+    return;
+  }
   if (MODE == CV_FWD && g.escale) {
     switch (bn) {
       case 16: hipLaunchKernelGGL((conv_bf16_act_kernel<16>), grid, dim3(256), 0, st, g); break;
@@ -696,14 +888,35 @@ struct ConvPlan {
   int bn;    // else conv_bf16_kernel<bn, mode>
   int mode;  // CV_FWD / CV_DGRAD / CV_DGRAD2
 };
-static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad) {
+static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   ConvPlan p{0, 0, dgrad ? (d->stride_h == 2 ? CV_DGRAD2 : CV_DGRAD) : CV_FWD};
   const int red = dgrad ? d->k : d->c, out = dgrad ? d->c : d->k;
   if (p.mode != CV_DGRAD2) p.tw = conv3_tw(d, red, out);
   // 1x1 contractions are two or three K-steps long: 64-wide column tiles (4 waves/SIMD) hide their load latency
-  // better than 128-wide ones (2 waves/SIMD), at the cost of reading the A rows once per column tile (L2 hits)
-  p.bn = p.tw ? conv3_bn(out) : (d->r * d->s == 1 && out > 64) ? 64 : conv_pick_bn(out);
+  // better than 128-wide ones (2 waves/SIMD), at the cost of reading the A rows once per column tile (L2 hits).
+  // XF kernels are single-buffered: at most 64 columns.
+  p.bn = p.tw ? conv3_bn(out) : ((d->r * d->s == 1 || xf) && out > 64) ? 64 : conv_pick_bn(out);
   return p;
+}
+
+// XF arguments (adr_bnact_xf) into the kernel arguments; `red` = reduction channels, the source grid sh x sw
+static int xf_args(const adr_bnact_xf* xf, bool bwd, int red, int n, int sh, int sw, ConvArgs& g) {
+  ADR_REQUIRE(xf && xf->scale && xf->shift && xf->out && (xf->act == ACT_NONE || xf->act == ACT_SILU),
+              "conv bnact: scale / shift / side output / act (none or silu)");
+  ADR_REQUIRE(red <= XMAXC, "conv bnact: %d reduction channels (table holds %d)", red, XMAXC);
+  ADR_REQUIRE(xf->out_cstride >= red && xf->out_cstride % 8 == 0 && ((uintptr_t)xf->out & 15) == 0,
+              "conv bnact: side output view");
+  g.xs = xf->scale; g.xt = xf->shift; g.xact = xf->act;
+  g.xo = (__bf16*)xf->out; g.xocs = xf->out_cstride;
+  if (bwd) {
+    ADR_REQUIRE(xf->y && xf->A && xf->B && xf->Cc && xf->y_cstride >= red && xf->y_cstride % 8 == 0 &&
+                    ((uintptr_t)xf->y & 15) == 0,
+                "conv bnact (dgrad): y view and A / B / Cc coefficients");
+    ADR_REQUIRE((long)n * sh * sw * xf->y_cstride < (1l << 30), "conv bnact: y exceeds 2^30 elements");
+    g.xy = (const __bf16*)xf->y; g.xycs = xf->y_cstride; g.xy_bytes = (int)(2l * n * sh * sw * xf->y_cstride);
+    g.xA = xf->A; g.xB = xf->B; g.xC = xf->Cc;
+  }
+  return ADR_OK;
 }
 
 }  // namespace adr
@@ -712,10 +925,15 @@ using namespace adr;
 
 static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                          float* stats, int accumulate, const float* escale, const float* eshift, int eact,
-                         void* stream, const adr_norm_fin* fin = nullptr) {
+                         void* stream, const adr_norm_fin* fin = nullptr, const adr_bnact_xf* xf = nullptr) {
   int rc = conv_check(d);
   if (rc) return rc;
   ConvArgs g{};
+  if (xf) {
+    ADR_REQUIRE(!escale && !fin, "conv fwd bnact: no eval epilogue / in-kernel finalize");
+    rc = xf_args(xf, false, d->c, d->n, d->h, d->w, g);
+    if (rc) return rc;
+  }
   if (fin) {
     ADR_REQUIRE(stats && !bias && !accumulate && !escale && fin->kind == ADR_FIN_BN_FWD && fin->C == d->k,
                 "conv fwd fin: needs stats, no bias / accumulation, a BN forward finalize over K channels");
@@ -730,7 +948,7 @@ static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, c
   g.N = d->k; g.ktot = d->r * d->s * d->c; g.accumulate = accumulate;
   g.src_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
   g.wt_bytes = (int)(2l * g.N * g.ktot);
-  const ConvPlan pl = conv_plan(d, false);
+  const ConvPlan pl = conv_plan(d, false, xf != nullptr);
   if (pl.tw) {
     launch_conv3<false>(pl.tw, pl.bn, d, g, (hipStream_t)stream);
     return check_launch("adr_conv2d_fwd_bf16");
@@ -757,10 +975,15 @@ extern "C" int adr_conv2d_fwd_bf16_act(const adr_conv_desc* d, const void* x, co
 }
 
 static int conv_dgrad_impl(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
-                           int accumulate, const void* addend, int adcs, void* stream) {
+                           int accumulate, const void* addend, int adcs, void* stream,
+                           const adr_bnact_xf* xf = nullptr) {
   int rc = conv_check(d);
   if (rc) return rc;
   ConvArgs g{};
+  if (xf) {
+    rc = xf_args(xf, true, d->k, d->n, d->ho, d->wo, g);
+    if (rc) return rc;
+  }
   g.src = (const __bf16*)dy; g.wt = (const __bf16*)w_crsk; g.out = (__bf16*)dx; g.bias = bias; g.stats = nullptr;
   g.addend = (const __bf16*)addend; g.adcs = adcs;
   g.n = d->n; g.sh_ = d->ho; g.sw_ = d->wo; g.scs = d->y_cstride; g.sco = d->y_coff; g.sc = d->k;
@@ -770,7 +993,7 @@ static int conv_dgrad_impl(const adr_conv_desc* d, const void* dy, const void* w
   g.src_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
   g.wt_bytes = (int)(2l * g.N * g.ktot);
   ADR_REQUIRE(d->stride_h == 1 || d->stride_h == 2, "conv dgrad (bf16 engine): stride %d", d->stride_h);
-  const ConvPlan pl = conv_plan(d, true);
+  const ConvPlan pl = conv_plan(d, true, xf != nullptr);
   const int bn = pl.bn;
   g.ntiles = cdiv(g.N, bn);
   hipStream_t st = (hipStream_t)stream;
@@ -800,6 +1023,43 @@ extern "C" int adr_conv2d_dgrad_bf16_add(const adr_conv_desc* d, const void* dy,
   return conv_dgrad_impl(d, dy, w_crsk, nullptr, dx, accumulate, addend, addend_cstride, stream);
 }
 
+// Training Conv-BN-act fusion (XF kernels): the data gradient of a conv whose output y went through a training
+// BatchNorm + activation, taking dz (the gradient of the activation output) and applying the BN-act backward
+// dy = A * dz * act'(y * scale + shift) + B * y + C while staging the operand; dy is side-written once to xf->out
+// (for the weight gradient). Replaces adr_affine_act_bwd + adr_conv2d_dgrad_bf16.
+extern "C" int adr_conv2d_dgrad_bf16_bnact(const adr_conv_desc* d, const void* dz, const void* w_crsk, void* dx,
+                                           int accumulate, const void* addend, int addend_cstride,
+                                           const adr_bnact_xf* xf, void* stream) {
+  ADR_REQUIRE(xf, "conv dgrad bnact: xf");
+  if (addend)
+    ADR_REQUIRE(addend_cstride >= d->c && addend_cstride % 8 == 0 && ((uintptr_t)addend & 15) == 0,
+                "conv dgrad bnact: addend view");
+  return conv_dgrad_impl(d, dz, w_crsk, nullptr, dx, accumulate, addend, addend_cstride, stream, xf);
+}
+
+// The forward counterpart: the conv's input is a training BatchNorm's input y; z = act(y * scale + shift) is
+// applied while staging (0 in the zero padding) and side-written once to xf->out. Replaces adr_affine_act +
+// adr_conv2d_fwd_bf16 (stats as adr_conv2d_fwd_bf16).
+extern "C" int adr_conv2d_fwd_bf16_bnact(const adr_conv_desc* d, const void* y, const void* w, void* out,
+                                         float* stats, const adr_bnact_xf* xf, void* stream) {
+  ADR_REQUIRE(xf, "conv fwd bnact: xf");
+  return conv_fwd_impl(d, y, w, nullptr, out, stats, 0, nullptr, nullptr, 0, stream, nullptr, xf);
+}
+
+// How many times the XF kernel would stage (and transform) each source element, x100: column tiles x gathers per
+// element (taps / stride^2 for FWD implicit GEMM, all taps for DGRAD, the halo overlap for the 3x3 tiles). The XF
+// transform is VALU work per staged element (a sigmoid per element for SiLU); it pays for the elementwise pass it
+// replaces only when each element is staged about once (adr_conv2d_{fwd,dgrad}_bf16_bnact callers test this).
+extern "C" int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad) {
+  const ConvPlan pl = conv_plan(d, dgrad != 0, true);
+  const int out = dgrad ? d->c : d->k;
+  const int nt = pl.tw ? out / pl.bn : cdiv(out, pl.bn);
+  if (pl.tw) return nt * 100 * (128 / pl.tw + 2) * (pl.tw + 2) / 128;
+  const int taps = d->r * d->s;
+  if (!dgrad) return nt * 100 * taps / (d->stride_h * d->stride_w);
+  return nt * 100 * taps;
+}
+
 extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) {
   const ConvPlan pl = conv_plan(d, false);
   if (pl.tw) return conv3_tiles(d, pl.tw);
@@ -819,9 +1079,16 @@ extern "C" int adr_conv2d_fwd_bf16_fin(const adr_conv_desc* d, const void* x, co
 
 extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, char* buf, int len) {
   ADR_REQUIRE(d && buf && len >= 64, "conv kernel symbol: bad arguments");
-  const ConvPlan pl = conv_plan(d, dgrad != 0);
-  if (pl.tw)
-    snprintf(buf, len, "_ZN3adr12conv3_kernelILi%dELb%dELi%dEEEvNS_8ConvArgsE", pl.tw, dgrad ? 1 : 0, pl.bn);
+  const bool dg = (dgrad & 1) != 0, xf = (dgrad & 2) != 0;  // bit 1: the BN-act (XF) variant
+  const ConvPlan pl = conv_plan(d, dg, xf);
+  if (xf && pl.tw)
+    snprintf(buf, len, "_ZN3adr15conv3_xf_kernelILi%dELb%dELi%dELi%dEEEvNS_8ConvArgsE", pl.tw, dg ? 1 : 0, pl.bn,
+             dg ? XF_BWD : XF_FWD);
+  else if (xf)
+    snprintf(buf, len, "_ZN3adr19conv_bf16_xf_kernelILi%dELi%dELi%dEEEvNS_8ConvArgsE", pl.bn, pl.mode,
+             dg ? XF_BWD : XF_FWD);
+  else if (pl.tw)
+    snprintf(buf, len, "_ZN3adr12conv3_kernelILi%dELb%dELi%dEEEvNS_8ConvArgsE", pl.tw, dg ? 1 : 0, pl.bn);
   else
     snprintf(buf, len, "_ZN3adr16conv_bf16_kernelILi%dELi%dEEEvNS_8ConvArgsE", pl.bn, pl.mode);
   return ADR_OK;

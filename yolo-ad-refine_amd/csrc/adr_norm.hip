@@ -67,7 +67,7 @@ __device__ __forceinline__ void nc_reduce_body(const T* __restrict__ x, int xcs,
 #pragma unroll
           for (int e = 0; e < VEC; ++e) {
             float xf = to_f(xe[e]);
-            float g = to_f(de[e]) * act_bwd_c<ACT, sizeof(T) == 2>(xf * sc[e] + sf[e]);
+            float g = bn_act_g<ACT, sizeof(T) == 2>(to_f(de[e]), xf, sc[e], sf[e]);
             s1[e] += g;
             s2[e] += g * xf;
           }
@@ -695,7 +695,7 @@ __global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x
     u32x4 o;
     T* oe = reinterpret_cast<T*>(&o);
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(act_fwd_c<ACT, sizeof(T) == 2>(to_f(e[k]) * sc[k] + sh[k]));
+    for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(bn_act_fwd_elem<ACT, sizeof(T) == 2>(to_f(e[k]), sc[k], sh[k]));
     st16(z + pix * zcs + zco + c0, o);
   }
 }
@@ -754,8 +754,8 @@ __global__ void __launch_bounds__(256) affine_act_bwd_kernel(const T* __restrict
 #pragma unroll
     for (int k = 0; k < VEC; ++k) {
       const float xf = to_f(xe[k]);
-      const float g = to_f(de[k]) * act_bwd_c<ACT, sizeof(T) == 2>(xf * sc[k] + sh[k]);
-      float r = ca[k] * g + cbv[k] * xf + cc[k];
+      const float g = bn_act_g<ACT, sizeof(T) == 2>(to_f(de[k]), xf, sc[k], sh[k]);
+      float r = bn_act_bwd_lin(g, xf, ca[k], cbv[k], cc[k]);
       if (accumulate) r += to_f(pe[k]);
       oe[k] = from_f<T>(r);
     }
