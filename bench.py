@@ -92,10 +92,14 @@ def cpu_baseline_infer(bs=1, img=640, budget_s=8.0):
             "sample": f"{n} batches x {bs} images @{img}^2 (eval fwd + decode + NMS, fp32, torch CPU {threads} threads)"}
 
 
-def infer_bench(model, bs, img, steps, warmup, dev, graph=True, roofline=False):
+def infer_bench(model, bs, img, steps, warmup, dev, graph=True, roofline=False, conf=0.25, multi_label=False,
+                nms_share=False):
     """BASELINE.json configs[1]: uint8 batch -> /255 in the stem -> eval forward (bf16) -> decode -> NMS
-    (conf 0.25, iou 0.7, max_det 300), one hipGraph per batch. Inputs resident in HBM; the timed region is
-    `steps` graph replays between two synchronisations. Returns (images/s, ms/batch, roofline or None)."""
+    (predictor settings conf 0.25, iou 0.7, max_det 300; or the validator's conf 0.001 + multi-label,
+    engine/validator.py:98-99), one hipGraph per batch. Inputs resident in HBM; the timed region is `steps` graph
+    replays between two synchronisations. Returns (images/s, ms/batch, roofline or None, detections per batch,
+    NMS share or None): the share is the adr_nms launches' part of one eagerly timed batch (HIP events per
+    launch)."""
     import torch
     import adrefine.kernels as K
     from adrefine.data.synthetic import images_u8
@@ -103,7 +107,7 @@ def infer_bench(model, bs, img, steps, warmup, dev, graph=True, roofline=False):
     was_training = model.training
     model.eval()
     x = images_u8(bs, img, seed=7).to(dev)
-    pred = FusedPredictor(model, conf=0.25, iou=0.7, max_det=300)
+    pred = FusedPredictor(model, conf=conf, iou=0.7, max_det=300, multi_label=multi_label)
     for _ in range(warmup):
         pred.run_padded(x)
     if graph:
@@ -114,17 +118,24 @@ def infer_bench(model, bs, img, steps, warmup, dev, graph=True, roofline=False):
         out, n = pred.run_padded(x)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    roof = None
-    if roofline:
+    roof = share = None
+    if roofline or nms_share:
         g, pred.graph = pred.graph, None
         K.timing_begin()
         pred.run_padded(x)
-        roof = K.roofline_report(K.timing_end(), model.compute_dtype, HBM_PEAK_GBS,
-                                 BF16_MFMA_PEAK_TF if model.compute_dtype == torch.bfloat16 else F32_MFMA_PEAK_TF)
+        recs = K.timing_end()
+        if roofline:
+            roof = K.roofline_report(recs, model.compute_dtype, HBM_PEAK_GBS,
+                                     BF16_MFMA_PEAK_TF if model.compute_dtype == torch.bfloat16 else F32_MFMA_PEAK_TF)
+        if nms_share:
+            tot = sum(r[-1] for r in recs)
+            nms = sum(r[-1] for r in recs if "nms" in str(r[0]).lower())
+            share = {"nms_ms": round(1e3 * nms, 3), "batch_kernels_ms": round(1e3 * tot, 3),
+                     "share": round(nms / tot, 4) if tot else None}
         pred.graph = g
     dets = int(n.sum())
     model.train(was_training)
-    return bs * steps / dt, 1000 * dt / steps, roof, dets
+    return bs * steps / dt, 1000 * dt / steps, roof, dets, share
 
 
 def pmc_traffic(symbol):
@@ -150,6 +161,9 @@ def pmc_traffic(symbol):
             base, nums = m.group(1), [int(v) for v in re.findall(r"\d+", m.group(2))]
             pre = f"_ZN3adr{len(base)}{base}IDF16b" + "".join(f"Li{v}E" for v in nums) + "E"
             hits = [k for k in doc["kernels"] if k.startswith(pre)]
+        if not hits:  # rocprofv3 prints some instantiations as "adr::k<bool _Accum, int, E>(...)": the base name
+            base = re.sub(r"^void ", "", name.split(" (")[0]).split("<")[0].split("(")[0]
+            hits = [k for k in doc["kernels"] if k.startswith((f"void {base}<", f"{base}(", f"void {base}("))]
         if len(hits) != 1:
             return None, None
         rec = doc["kernels"][hits[0]]
@@ -161,26 +175,58 @@ NET_BYTES_PER_IMG = 210e6
 NET_FLOPS_PER_IMG = 34.6e9
 
 
+# the bf16 conv engine's fwd / dgrad kernels (incl. the Conv-BN-act XF variants)
+_CONV_TAGS = ("_ZN3adr16conv_bf16", "_ZN3adr12conv3", "_ZN3adr19conv_bf16_xf", "_ZN3adr15conv3_xf")
+
+
 def conv_attainable(detail, hbm_gbs, mfma_tf):
     """Attainable-roofline fraction of the conv family (north_star: '>= 70 % CDNA4 bf16 MFMA roofline on the fused
     Conv-BN-SiLU backbone'): sum over conv fwd/dgrad launches of max(bytes / HBM peak, flops / MFMA peak)
     divided by their measured time."""
     ideal = meas = 0.0
     for tag, shape, nb, fl, t in detail:
-        if nb is None or not (tag.startswith("_ZN3adr16conv_bf16") or tag.startswith("_ZN3adr12conv3")):
+        if nb is None or not tag.startswith(_CONV_TAGS):
             continue
         ideal += max(nb / (hbm_gbs * 1e9), fl / (mfma_tf * 1e12))
         meas += t
-    return None if meas == 0 else {"launches_timed": sum(1 for d in detail if d[0].startswith(("_ZN3adr16conv_bf16",
-                                                                                                "_ZN3adr12conv3"))),
+    return None if meas == 0 else {"launches_timed": sum(1 for d in detail if d[0].startswith(_CONV_TAGS)),
                                    "attainable_frac": round(ideal / meas, 4), "ms_total": round(1e3 * meas, 3)}
+
+
+def stage_overhead(model, tr, batch, bs, steps=30):
+    """configs[3] readiness on one GPU: the DDP step is staged (one graph per gradient bucket, the all-reduces
+    between replays, engine/ddp.py); time that staged 1-GPU step against the unstaged one, back to back."""
+    import torch
+    from adrefine.engine.ddp import cuts_for_bucket
+    from adrefine.engine.trainer import DDP_BUCKET_MB, FusedTrainer
+    cuts = cuts_for_bucket(model, DDP_BUCKET_MB)
+    tr2 = FusedTrainer(model, batch_size=bs, world_size=1, stages=cuts)
+    for _ in range(3):
+        tr2.step(batch)
+    tr2.capture(batch)
+    tr2.step(batch)
+
+    def timed(t):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            t.step(batch)
+        torch.cuda.synchronize()
+        return 1000 * (time.perf_counter() - t0) / steps
+
+    a, b = timed(tr), timed(tr2)
+    a2, b2 = timed(tr), timed(tr2)
+    un, st = min(a, a2), min(b, b2)
+    tr2.graphs = None
+    return {"bucket_mb": DDP_BUCKET_MB, "cuts": list(cuts), "stages": len(cuts) + 1, "ms_per_step_unstaged": round(un, 3),
+            "ms_per_step_staged": round(st, 3), "overhead": round(st / un - 1, 4), "steps": steps}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)  # SURVEY.md §8d: 100 timed steps after 20 warm-up, median
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--bs", type=int, default=64)
     ap.add_argument("--img", type=int, default=640)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
@@ -188,6 +234,7 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0)
     ap.add_argument("--no-graph", action="store_true", help="launch every kernel from Python (no hipGraph replay)")
     ap.add_argument("--roofline-steps", type=int, default=2)
+    ap.add_argument("--stage-check", type=int, default=1, help="time the DDP-staged step on 1 GPU (configs[3])")
     ap.add_argument("--float-images", action="store_true", help="feed pre-normalised fp32 images instead of uint8")
     ap.add_argument("--infer", action="store_true", help="measure BASELINE.json configs[1] (batched inference) only")
     ap.add_argument("--infer-bs", type=int, default=32)
@@ -226,8 +273,8 @@ def main():
         cfg["scale"] = args.scale
         model = DetectionModel(cfg, compute_dtype=dtype).to(dev)
     if args.infer:
-        ips, ms, roof, dets = infer_bench(model, args.infer_bs, args.img, args.steps, args.warmup, dev,
-                                          graph=not args.no_graph, roofline=True)
+        ips, ms, roof, dets, _ = infer_bench(model, args.infer_bs, args.img, args.steps, args.warmup, dev,
+                                             graph=not args.no_graph, roofline=True)
         if roof is not None:
             roof["traffic"], roof["traffic_source"] = None, None
         if rank == 0:
@@ -264,9 +311,12 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    ev[0].record()
+    for k in range(args.steps):
         items = tr.step(batch)
+        ev[k + 1].record()  # per-step boundaries on the step's stream (median / p90; the value uses the wall clock)
     t_host = time.perf_counter() - t0  # host-side enqueue time (launch-bound if close to the step time)
     torch.cuda.synchronize()
     if world > 1:
@@ -287,6 +337,9 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t)
     ips = world * args.bs * args.steps / dt
+    per = sorted(ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps))
+    step_stats = {"median": round(per[len(per) // 2], 3), "p10": round(per[len(per) // 10], 3),
+                  "p90": round(per[(9 * len(per)) // 10], 3), "min": round(per[0], 3)}
     if rank == 0:
         finite = bool(torch.isfinite(items).all())
         mfma_peak = BF16_MFMA_PEAK_TF if dtype == torch.bfloat16 else F32_MFMA_PEAK_TF
@@ -301,15 +354,26 @@ def main():
                 roof["network"] = {"flops_per_img": 3 * 765.6e9,
                                    "mfma_frac": round(ips * 3 * 765.6e9 / (mfma_peak * 1e12), 4)}
             roof["conv_family"] = conv_attainable(K.timing_detail(), HBM_PEAK_GBS, mfma_peak)
+        staging = None
+        if world == 1 and args.stage_check and not args.no_graph:
+            staging = stage_overhead(model, tr, batch, args.bs)
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(budget_s=args.cpu_budget)
         infer = None
         if world == 1 and args.infer_steps > 0:  # configs[1] alongside the headline line
-            i_ips, i_ms, _, dets = infer_bench(model, args.infer_bs, args.img, args.infer_steps, 2, dev,
-                                               graph=not args.no_graph)
+            i_ips, i_ms, _, dets, _ = infer_bench(model, args.infer_bs, args.img, args.infer_steps, 2, dev,
+                                                  graph=not args.no_graph)
+            # the validator's NMS settings (conf 0.001, multi-label: engine/validator.py:98-99) give NMS real work on
+            # random-recipe logits (conf 0.25 leaves nothing to sort or suppress)
+            v_ips, v_ms, _, v_dets, v_share = infer_bench(model, args.infer_bs, args.img, args.infer_steps, 2, dev,
+                                                          graph=not args.no_graph, conf=0.001, multi_label=True,
+                                                          nms_share=True)
             infer = {"metric": "images/sec inference (640x640) bs32, 1 GPU", "value": round(i_ips, 2),
                      "ms_per_batch": round(i_ms, 3), "bs": args.infer_bs, "steps": args.infer_steps,
                      "pipeline": "uint8 -> eval fwd (bf16) -> DFL decode -> NMS(0.25, 0.7, 300), one hipGraph",
-                     "detections_per_batch": dets}
+                     "detections_per_batch": dets,
+                     "val_nms": {"pipeline": "same, NMS(conf 0.001, iou 0.7, multi-label, max_det 300)",
+                                 "value": round(v_ips, 2), "ms_per_batch": round(v_ms, 3),
+                                 "detections_per_batch": v_dets, "nms_kernels": v_share}}
         out = {
             "metric": ("images/sec whole-node (640x640) fwd+bwd, YOLO-AD-Refine-n at 1/2/4/8 GPU" if args.scale == "n"
                        else f"images/sec whole-node ({args.img}x{args.img}) fwd+bwd, YOLO-AD-Refine-{args.scale}"),
@@ -320,8 +384,10 @@ def main():
             "config": {"workload": f"yolo11-701-YOLO-AD-Refine.yaml ({args.scale}) train step bs={args.bs}/GPU "
                                    f"{args.img}x{args.img}, synthetic COCO-shape labels, TAL+DFL+CIoU/NWD loss, "
                                    f"SGD+EMA", "global_batch": world * args.bs, "img": args.img,
-                       "parallelism": f"dp{world}"},
+                       "parallelism": f"dp{world}",
+                       "nms": "not in the train step (measured in the inference leg at validator settings)"},
             "roofline": roof, "cpu_baseline": cpu, "loss_finite": finite,
+            "ms_per_step_events": step_stats, "ddp_staging": staging,
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3), "hipgraph": not args.no_graph,
             "inference": infer, "peak_hbm_gib": round(peak_gib, 2),
         }

@@ -43,7 +43,10 @@ def _worker(rank, port, out_dir, q):
         load_recipe_into(m)
         m = m.cuda()
         tr = FusedTrainer(m, nbs=WORLD * BS, batch_size=WORLD * BS, world_size=WORLD)
-        assert tr.cuts == (6, 10) and tr.accumulate == 1
+        from adrefine.engine.ddp import cuts_for_bucket
+        from adrefine.engine.trainer import DDP_BUCKET_MB
+        # ~4 MB gradient buckets: four stages, cuts inside the neck included (after L7, L10, L20)
+        assert tr.cuts == cuts_for_bucket(m, DDP_BUCKET_MB) and len(tr.cuts) >= 3 and tr.accumulate == 1
         x, lab = _shard(0, rank)
         tr.step({"img": x.cuda(), **lab})  # eager: bucket all-reduces launched between backward stages
         x, lab = _shard(1, rank)

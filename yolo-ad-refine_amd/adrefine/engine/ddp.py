@@ -47,6 +47,29 @@ def stage_of(layer: int, cuts) -> int:
     return s
 
 
+def cuts_for_bucket(model, bucket_mb=4.0):
+    """Stage cuts whose parameter-gradient buckets hold about `bucket_mb` MB of fp32 gradients each, filled from the
+    last layer down (the backward's order; the reference's DDP bucket_cap is 25 MB, trainer.py:273 — on
+    point-to-point xGMI links a few MB per bucket starts the first all-reduce early without per-bucket latency
+    dominating). A layer is never split: a single layer larger than the bucket is a bucket of its own. Returns
+    the sorted layer indices after which a stage ends."""
+    per = {}
+    for name, p in model.named_parameters():
+        li = layer_of(name)
+        if li >= 0:
+            per[li] = per.get(li, 0) + 4 * p.numel()
+    if not per:
+        return ()
+    cap = bucket_mb * 2 ** 20
+    cuts, acc = [], 0
+    for li in range(max(per), 0, -1):
+        acc += per.get(li, 0)
+        if acc >= cap:
+            cuts.append(li - 1)  # layers li.. form the bucket; the stage below ends at li - 1
+            acc = 0
+    return tuple(sorted(c for c in cuts if c >= 0))
+
+
 def detach_leaf(t):
     """A leaf view of t (same storage and strides) that collects the gradient flowing back to t."""
     if not torch.is_tensor(t) or not t.requires_grad:

@@ -33,6 +33,7 @@ from __future__ import annotations
 
 import ctypes
 import math
+import os
 
 import numpy as np
 import torch
@@ -40,13 +41,16 @@ import torch.nn as nn
 
 from .. import kernels as K
 from ..native import lib
-from .ddp import BucketReducer, layer_of, stage_of, staged_backward
+from .ddp import BucketReducer, cuts_for_bucket, layer_of, stage_of, staged_backward
 
 _NORM_TYPES = tuple(v for k, v in nn.__dict__.items() if "Norm" in k and isinstance(v, type))
 _ENTRY = np.dtype([("p", "<u8"), ("g", "<u8"), ("b", "<u8"), ("e", "<u8"), ("n", "<i8"), ("grp", "<i4"),
                    ("pad", "<i4")])
 _CHUNK = np.dtype([("e", "<i4"), ("p", "<i4"), ("s", "<i8"), ("l", "<i8")])
-DDP_CUTS = (6, 10)  # stage ends for the bucketed all-reduce: L0-L6 | L7-L10 | L11-L33
+# stage ends for the bucketed all-reduce: buckets of ~ADR_DDP_BUCKET_MB MB of gradients, filled
+# from the last layer down (ddp.cuts_for_bucket); DDP_CUTS overrides with fixed layer cuts (e.g. "6,10")
+DDP_BUCKET_MB = float(os.environ.get("ADR_DDP_BUCKET_MB", "4"))
+DDP_CUTS = tuple(int(v) for v in os.environ["ADR_DDP_CUTS"].split(",")) if os.environ.get("ADR_DDP_CUTS") else None
 
 
 def param_groups(model):
@@ -126,7 +130,10 @@ class FusedTrainer:
         self.lr, self.momentum, _ = self.sched.at(0)
         self.ni, self.last_opt_step = 0, -1
         # backward stages: DDP overlaps bucket all-reduces with the remaining stages (engine/ddp.py)
-        self.cuts = tuple(DDP_CUTS if world_size > 1 else ()) if stages is None else tuple(stages)
+        if stages is None:
+            stages = (DDP_CUTS if DDP_CUTS is not None else cuts_for_bucket(model, DDP_BUCKET_MB)) \
+                if world_size > 1 else ()
+        self.cuts = tuple(stages)
         self.dev = dev = next(model.parameters()).device
         groups = param_groups(model)
         plist = [(name, p, gi) for gi, lst in enumerate(groups) for name, p in lst]

@@ -221,6 +221,8 @@ def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
         y.append(x if m.i in save else None)
         if m.i in cuts:
             x = cut_live(x, y, layers, m.i, bounds)  # y[i] and x stay one leaf when they are one tensor
+            if y[m.i] is not None:  # the next layer reads a saved index, not -1: x must still become the leaf,
+                x = y[m.i]          # or the fan-out below would hand later stages views of the pre-cut tensor
             for j, vs in views.items():  # readers after the cut take views of the new leaves
                 if vs:
                     views[j] = list(K.fanout(y[j], len(vs))) if len(vs) > 1 else [y[j]]
