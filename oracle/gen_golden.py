@@ -355,6 +355,42 @@ def lscale_fixtures(tasks, block, conv, head, uloss, uops, note):
 
 manifest_extra = {}
 
+# parameters whose FULL gradient tensor the 701 train-step fixture keeps (one or more per module family on the
+# path: stem Conv-BN, C3k2_MLCA, C3k bottleneck, C2PTSSA attention / EDFFN, ELA, BiFPN Fusion, nn.Conv2d rows,
+# AYHead stems / shared Conv_GN / DyDCNv2 / CoordAtt BN / output convs / Scale)
+GRAD_KEYS = ("model.0.conv.weight", "model.0.bn.weight", "model.0.bn.bias", "model.6.cv2.conv.weight",
+             "model.6.cv2.bn.weight", "model.8.m.0.cv1.conv.weight", "model.10.m.0.attn.qkv_projections.0.weight",
+             "model.10.m.0.attn.cross_scale_fusion.in_proj_weight", "model.10.m.0.ffn.project_in.weight",
+             "model.12.weight", "model.28.fusion_weight", "model.33.stems.0.conv.weight",
+             "model.33.share_conv.0.conv.weight", "model.33.share_conv.0.gn.weight", "model.33.DyDCNV2.conv.weight",
+             "model.33.coord_attention_reg.bn1.weight", "model.33.cv2.weight", "model.33.cv2.bias",
+             "model.33.cv3.weight", "model.33.cv3.bias", "model.33.scale.0.scale")
+
+
+def grads_fixtures(tasks, block, conv, head, uloss, uops, note):
+    """Elementwise parameter-gradient parity: the reference's 701 train step at 320^2 bs 2 (the inputs, labels and
+    recipe weights of net701_train_320) with the full dL/dtheta tensors of GRAD_KEYS (nn/tasks.py:290-302 loss ->
+    autograd backward; utils/loss.py:419-520)."""
+    model = tasks.DetectionModel(str(REF / "z-yaml" / "yolo11-701-YOLO-AD-Refine.yaml"), verbose=False)
+    rec = load_recipe(model)
+    model.args = _hyp()
+    model.load_state_dict(rec, strict=True)
+    model.train()
+    x = synthetic_images(2, 320, seed=0)
+    batch = synthetic_labels(2, 80, seed=1)
+    preds = model(x)
+    loss, items = uloss.v8DetectionLoss(model)(preds, batch)
+    loss.backward()
+    P = dict(model.named_parameters())
+    d = {"img_seed": np.array(0), "img_size": np.array(320), "batch_idx": _np(batch["batch_idx"]),
+         "cls": _np(batch["cls"]), "bboxes": _np(batch["bboxes"]), "loss": _np(loss), "items": _np(items),
+         "keys": np.array(GRAD_KEYS)}
+    for i, k in enumerate(GRAD_KEYS):
+        d[f"g{i}"] = _np(P[k].grad).astype(np.float32)
+    np.savez_compressed(OUT / "net701_grads_320.npz", **d)
+    note("net701_grads_320", "701 train step bs2 320^2: full parameter gradients of a subset (GRAD_KEYS)",
+         "nn/tasks.py:290-302, utils/loss.py:419-520, head.py:1049-1252", True)
+
 
 def metrics_fixtures(tasks, block, conv, head, uloss, uops, note):
     """Validator metrics tail on synthetic detections: per-image box_iou (utils/metrics.py:52) + greedy

@@ -219,3 +219,26 @@ def test_nms_fixture(name):
         ref = g[f"out{i}"]
         assert o.shape == ref.shape, (o.shape, ref.shape)
         assert np.array_equal(o.numpy(), ref), "NMS output must match bit-exactly"
+
+
+def _grad_close(mine, ref, rtol):
+    """max |mine - ref| <= rtol * max |ref| (elementwise, per parameter tensor)."""
+    mine, ref = mine.detach().double(), torch.as_tensor(ref).double()
+    return float((mine - ref).abs().max()) <= rtol * float(ref.abs().max()) + 1e-12
+
+
+def test_net701_full_param_grads():
+    """The oracle's full dL/dtheta for the GRAD_KEYS subset against the reference's (net701_grads_320), elementwise."""
+    g = golden("net701_grads_320")
+    P, layers, save = _net("701")
+    for k, v in P.items():
+        if v.dtype.is_floating_point and "running" not in k:
+            v.requires_grad_(True)
+    x = synthetic_images(2, int(g["img_size"]), seed=int(g["img_seed"]))
+    preds = O.forward(P, layers, save, x, train=True)
+    loss, _ = O.detection_loss(preds, torch.from_numpy(g["batch_idx"]), torch.from_numpy(g["cls"]),
+                               torch.from_numpy(g["bboxes"]))
+    _close(loss.detach(), g["loss"], rtol=1e-4)
+    loss.backward()
+    bad = [str(k) for i, k in enumerate(g["keys"]) if not _grad_close(P[str(k)].grad, g[f"g{i}"], 2e-4)]
+    assert not bad, bad
