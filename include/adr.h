@@ -437,16 +437,33 @@ int adr_dcn_col2im(int dtype, const void* x, int xcs, const void* om, int omcs, 
  * adr_dcn_fwd_bf16: y[p][co] = sum W_krsc[co][t][c] * m * bilinear(x)  (w_krsc: bf16 [Cout][9][C]).
  * adr_dcn_wgrad_bf16: split-K partials part[split][Cout][9][C] (fp32) of dW, `splits` from
  *   adr_dcn_wgrad_bf16_splits; reduce with adr_wgrad_reduce_unpack(K=Cout, C=C, RS=9).
- * adr_dcn_bwd_bf16 (C == Cout == 64): dx32 (+)= input gradient (fp32, zeroed by the caller, float atomics), dom =
- *   offset / mask-logit gradient (channels [0,27); the caller zeroes the rest); w_t: bf16 [9][C][Cout]
- *   (adr_dcn_weight_t). */
+ * adr_dcn_bwd_bf16 (C == Cout in {64, 128, 256}): dx = input gradient (bf16, every element written once, gathered
+ *   by destination tile), dom = offset / mask-logit gradient (channels [0,27), [27,32) written as zeros; domcs >=
+ *   32); w_t: bf16 [9][C][Cout] (adr_dcn_weight_t). dxf (fp32, N*H*W*C) and tile_flags (adr_dcn_bwd_tiles ints)
+ *   are persistent scratch that must be zero on entry and are zero again on return: corners whose source lies more
+ *   than ~2 px outside the destination tile are added to dxf with float atomics and folded into dx by a second
+ *   launch (with |offsets| < 2 px there are none and dx is bitwise repeatable). */
 int adr_dcn_fwd_bf16(const void* x, int xcs, const void* om, int omcs, const void* w_krsc, void* y, int ycs, int N,
                      int H, int W, int C, int Cout, void* stream);
 int adr_dcn_wgrad_bf16_splits(int N, int H, int W, int C, int Cout);
 int adr_dcn_wgrad_bf16(const void* x, int xcs, const void* om, int omcs, const void* dy, int dycs, float* part,
                        int splits, int N, int H, int W, int C, int Cout, void* stream);
 int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs, const void* dy, int dycs, const void* w_t,
-                     float* dx32, void* dom, int domcs, int N, int H, int W, int C, int Cout, void* stream);
+                     void* dx, int dxcs, void* dom, int domcs, float* dxf, int* tile_flags, int N, int H, int W, int C,
+                     int Cout, void* stream);
+int adr_dcn_bwd_tiles(int N, int H, int W);
+/* ---------------------------------------------------------------------------------------------------------
+ * Training augmentation pixels (data/augment.py v8_transforms :2273-2335, through Format :2072-2100 and
+ * YOLODataset.collate_fn, data/dataset.py:230-246): Mosaic canvas -> warpAffine (RandomPerspective) -> RandomHSV
+ * -> RandomFlip -> CHW RGB, fused, one thread per output pixel, into out (B, 3, H, W) uint8. pool: the batch's
+ * source images (HWC BGR uint8, resized as BaseDataset.load_image leaves them); descs: B device adr_aug_desc
+ * records (4 tiles {int64 byte offset; int sw, x1a, y1a, x2a, y2a, x1b, y1b}, then int ntile, cw, ch, warp,
+ * tab_off, lut_off, flip_ud, flip_lr, rgb, pad; size adr_augment_desc_size()); tables: per warped image adelta[W],
+ * bdelta[W], X0[H], Y0[H] (cv::warpAffine fixed point, from the host); luts: 768 bytes (hue, sat, val) per image
+ * with HSV (lut_off -1: none). Random draws, matrices and labels stay on the host (adrefine/data/augment.py). */
+int adr_augment_u8(const void* pool, const void* descs, int B, const int* tables, const void* luts, void* out, int H,
+                   int W, void* stream);
+int adr_augment_desc_size(void);
 /* W (Cout, C, 3, 3) fp32 -> [(tap*C + c)][Cout] operand for dcols = dy x W. */
 int adr_dcn_weight_t(int dtype, const float* w, void* out, int Cout, int C, void* stream);
 /* Per-image 2-layer gate MLP on pooled vectors: out = act2(W2 act1(W1 (in*in_scale) + b1) + b2);

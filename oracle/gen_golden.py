@@ -448,6 +448,56 @@ def metrics_fixtures(tasks, block, conv, head, uloss, uops, note):
          "models/yolo/detect/val.py:125-229, engine/validator.py:221-261, utils/metrics.py:52,1112-1360")
 
 
+def augment_fixtures(tasks, block, conv, head, uloss, uops, note):
+    """Training augmentation chain (data/augment.py v8_transforms :2273-2335 + Format :1920-2100, collated by
+    YOLODataset.collate_fn, data/dataset.py:230-246) on synthetic items (recipe.synthetic_aug_items), the python /
+    numpy RNGs seeded, through the reference's own transform code. The OpenCV calls in it (RandomHSV cvtColor / LUT,
+    RandomPerspective warpAffine / getRotationMatrix2D) run on oracle/stubs/cv2 (restated, unpinned)."""
+    import random
+    from types import SimpleNamespace
+
+    from recipe import AUG_HYPS, synthetic_aug_items
+    from ultralytics.data.augment import Format, v8_transforms
+    from ultralytics.data.dataset import YOLODataset
+    from ultralytics.utils.instance import Instances
+
+    class _DS:
+        def __init__(self, items, imgsz):
+            self.items, self.imgsz = items, imgsz
+            self.buffer = list(range(len(items)))
+            self.data = {"flip_idx": []}
+            self.use_keypoints = False
+
+        def __len__(self):
+            return len(self.items)
+
+        def get_image_and_label(self, i):
+            it = self.items[i]
+            h, w = it["img"].shape[:2]
+            return {"im_file": f"syn{i}.jpg", "ori_shape": (h, w), "resized_shape": (h, w), "ratio_pad": (1.0, 1.0),
+                    "img": it["img"].copy(), "cls": it["cls"].copy(),
+                    "instances": Instances(it["bboxes"].copy(), np.zeros((0, 1000, 2), dtype=np.float32), None,
+                                           bbox_format="xywh", normalized=True)}
+
+    for name, imgsz, seed, order in (("aug_default_256", 256, 5, [0, 1, 2, 3]),
+                                     ("aug_rot_256", 256, 9, [4, 5, 6, 7, 0, 2])):
+        hyp = SimpleNamespace(**AUG_HYPS[name.split("_")[1]])
+        ds = _DS(synthetic_aug_items(8, imgsz), imgsz)
+        T = v8_transforms(ds, imgsz, hyp)
+        T.append(Format(bbox_format="xywh", normalize=True, return_mask=False, return_keypoint=False,
+                        return_obb=False, batch_idx=True, mask_ratio=4, mask_overlap=True, bgr=hyp.bgr))
+        random.seed(seed)
+        np.random.seed(seed)
+        batch = YOLODataset.collate_fn([T(ds.get_image_and_label(i)) for i in order])
+        np.savez_compressed(OUT / f"{name}.npz", img=_np(batch["img"]), cls=_np(batch["cls"]),
+                            bboxes=_np(batch["bboxes"]), batch_idx=_np(batch["batch_idx"]), seed=seed, imgsz=imgsz,
+                            order=np.array(order))
+        note(name, f"v8_transforms + Format + collate_fn, hyp {name.split('_')[1]}, imgsz {imgsz}, items {order}",
+             ["data/augment.py:489-865", "data/augment.py:951-1298", "data/augment.py:1301-1473",
+              "data/augment.py:1920-2100", "data/augment.py:2273-2335", "data/dataset.py:230-246"], unpinned=True)
+        print(name, batch["img"].shape, batch["bboxes"].shape)
+
+
 def nms_fixtures(uops, note):
     """utils/ops.py:163-312 on the exactly-reproducible synthetic predictions (recipe.synthetic_predictions)."""
     pred = synthetic_predictions(2, 8400, 80, 640, seed=7)

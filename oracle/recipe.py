@@ -123,3 +123,40 @@ def synthetic_predictions(bs: int, na: int, nc: int = 80, img: int = 640, seed: 
     s = s * s
     s = s * s
     return torch.cat((xy, wh, s.view(bs, nc, na)), 1)
+
+
+AUG_SHAPES = [(1.0, 0.75), (0.625, 1.0), (1.0, 1.0), (0.78, 1.0), (1.0, 0.5625), (1.0, 0.906), (0.5, 1.0),
+              (0.875, 0.875)]
+
+
+def synthetic_aug_items(n: int, imgsz: int, seed: int = 3):
+    """Training-augmentation inputs (data/augment.py fixtures): n BGR uint8 HWC images already resized as
+    BaseDataset.load_image leaves them (long side = imgsz, data/base.py:151-172) with smooth gradients + noise,
+    and per-image labels (cls (k, 1) float32, normalised xywh boxes (k, 4) float32, 1 <= k <= 8)."""
+    g = torch.Generator().manual_seed(seed)
+    items = []
+    for i in range(n):
+        fh, fw = AUG_SHAPES[i % len(AUG_SHAPES)]
+        h, w = max(8, int(round(imgsz * fh))), max(8, int(round(imgsz * fw)))
+        yy = torch.arange(h, dtype=torch.float32).view(h, 1, 1)
+        xx = torch.arange(w, dtype=torch.float32).view(1, w, 1)
+        ph = torch.rand(1, 1, 3, generator=g) * 6.0
+        base = 127.5 + 80 * torch.sin(xx * 0.05 + yy * 0.031 + ph) + 30 * torch.cos(yy * 0.09 - ph)
+        img = (base + torch.rand(h, w, 3, generator=g) * 40 - 20).clamp(0, 255).round().to(torch.uint8).numpy()
+        k = int(torch.randint(1, 9, (1,), generator=g))
+        ctr = 0.1 + 0.8 * torch.rand(k, 2, generator=g)
+        wh = 0.05 + 0.45 * torch.rand(k, 2, generator=g)
+        wh = torch.minimum(wh, 2 * torch.minimum(ctr, 1 - ctr))
+        cls = torch.randint(0, 80, (k, 1), generator=g).float()
+        items.append({"img": img, "cls": cls.numpy(), "bboxes": torch.cat((ctr, wh), 1).numpy()})
+    return items
+
+
+AUG_HYPS = {  # default.yaml training augmentation values (cfg/default.yaml) and a rotated / sheared / v-flipped set
+    "default": dict(mosaic=1.0, degrees=0.0, translate=0.1, scale=0.5, shear=0.0, perspective=0.0, flipud=0.0,
+                    fliplr=0.5, hsv_h=0.015, hsv_s=0.7, hsv_v=0.4, mixup=0.0, copy_paste=0.0,
+                    copy_paste_mode="flip", bgr=0.0),
+    "rot": dict(mosaic=1.0, degrees=10.0, translate=0.2, scale=0.6, shear=3.0, perspective=0.0, flipud=0.5,
+                fliplr=0.5, hsv_h=0.03, hsv_s=0.8, hsv_v=0.5, mixup=0.0, copy_paste=0.0, copy_paste_mode="flip",
+                bgr=0.0),
+}

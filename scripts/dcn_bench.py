@@ -1,5 +1,7 @@
 """Time the DCN forward / backward at the AYHead shapes (bs 64, 64 -> 64 channels, 80/40/20 maps, bf16) with HIP
-events; ADR_DCN_FUSED=0 selects the im2col + GEMM + col2im path for an A/B."""
+events; ADR_DCN_FUSED=0 selects the im2col + GEMM + col2im path for an A/B. Env N, C, SIZES (e.g. N=16 C=256
+SIZES=160,80,40 for the l-scale head at 1280), SPREAD (offset range in px)."""
+import os
 import sys
 from pathlib import Path
 
@@ -11,11 +13,12 @@ from adrefine import kernels as K  # noqa: E402
 
 torch.manual_seed(0)
 tot_f = tot_b = 0.0
-for S in (80, 40, 20):
-    N, C = 64, 64
+SPREAD = float(os.environ.get("SPREAD", "1"))
+for S in [int(v) for v in os.environ.get("SIZES", "80,40,20").split(",")]:
+    N, C = int(os.environ.get("N", 64)), int(os.environ.get("C", 64))
     x = torch.randn(N, C, S, S, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     om = torch.zeros(N, 32, S, S, device="cuda")
-    om[:, :18] = torch.rand(N, 18, S, S, device="cuda") * 2 - 1
+    om[:, :18] = (torch.rand(N, 18, S, S, device="cuda") * 2 - 1) * SPREAD
     om[:, 18:27] = torch.randn(N, 9, S, S, device="cuda")
     om = om.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     w = (torch.randn(C, C, 3, 3, device="cuda") * 0.05).requires_grad_(True)

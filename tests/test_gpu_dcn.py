@@ -2,9 +2,10 @@
 against the oracle's mmcv restatement (oracle/adr_oracle.py dcn_v2; mmcv itself is absent, so the
 third-party core is 'parity unpinned' — the whole-head fixtures pin the reference's arithmetic around it).
 
-Offsets spread to +-6 px, so samples leave the image and bilinear corners fall outside the bf16 backward's
-3-pixel LDS window (the direct global-atomic path) as well as inside it; maps that are and are not multiples
-of the 8x8 backward tile; one and two 64-channel chunks.
+Offsets spread to +-6 px, so samples leave the image and bilinear corners come from sources outside the bf16
+backward's per-tap 12x12 source sub-window (the far-list path) as well as inside it; maps that are and are not
+multiples of the 8x8 backward tile; C = Cout in {64, 128, 256} (the n- and l-scale AYHead widths) on the fused
+backward, other shapes on the im2col path.
 
 fp32 (parity mode, im2col + GEMM + deterministic col2im): outputs and all gradients within 1e-4 relative of
 the fp64 oracle, and the input gradient is bitwise identical across two runs.
@@ -22,6 +23,9 @@ CASES = [  # (N, C, Cout, H, W, offset spread px)
     (2, 64, 64, 20, 20, 1.5),
     (3, 128, 64, 13, 11, 3.0),
     (2, 64, 128, 16, 24, 2.5),
+    (2, 128, 128, 24, 20, 2.5),
+    (2, 256, 256, 12, 16, 1.0),
+    (1, 256, 256, 40, 40, 4.0),
 ]
 
 
@@ -67,6 +71,15 @@ def test_dcn_fp32_vs_oracle_and_deterministic(case):
     x, om, w, gy = _inputs(N, C, Cout, H, W, spread, seed=7)
     ry, rdx, rdom, rdw = _oracle(x, om, w, gy)
     y, dx, dom, dw = _run(x, om, w, gy, torch.float32)
+    # a sample coordinate within 1e-5 px of an integer may take the other bilinear cell in fp32 than in the fp64
+    # oracle (e.g. offset 0.9999995 -> 18.0): the offset / mask gradients of that (pixel, tap) are discontinuous
+    # there, so those entries are left out of the comparison
+    fr = om[:, :18].double().frac().abs()
+    edge = (torch.minimum(fr, 1 - fr) < 1e-5).view(N, 9, 2, H, W).any(2)
+    keep = torch.ones(N, 32, H, W, dtype=torch.bool)
+    keep[:, :18] = ~edge.repeat_interleave(2, 1)
+    keep[:, 18:27] = ~edge
+    dom, rdom = dom * keep, rdom * keep
     for name, a, b in (("y", y, ry), ("dx", dx, rdx), ("doffset", dom[:, :18], rdom[:, :18]),
                        ("dmask", dom[:, 18:27], rdom[:, 18:27]), ("dw", dw, rdw)):
         err = float((a - b).abs().max()) / float(b.abs().max())
@@ -90,3 +103,13 @@ def test_dcn_bf16_fused_vs_oracle(case):
     for k, v in errs.items():
         assert v <= bounds[k], (k, v, errs)
     assert float(dom[:, 27:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("C", [64, 128, 256])
+def test_dcn_bf16_backward_repeatable_near(C):
+    """|offsets| < 2 px: every corner is gathered by its destination tile (no far entries), so the bf16 backward
+    is bitwise repeatable."""
+    x, om, w, gy = _inputs(2, C, C, 24, 17, 1.9, seed=5)
+    _, dx, dom, dw = _run(x, om, w, gy, torch.bfloat16)
+    _, dx2, dom2, dw2 = _run(x, om, w, gy, torch.bfloat16)
+    assert torch.equal(dx, dx2) and torch.equal(dom, dom2) and torch.equal(dw, dw2)

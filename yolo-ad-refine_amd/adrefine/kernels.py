@@ -2466,6 +2466,19 @@ def _dcn_fused(dtype, C, Cout, omcs):
 _DCN_FUSED = bool(int(__import__("os").environ.get("ADR_DCN_FUSED", "1")))  # 0: im2col path (A/B only)
 
 
+_DCN_FAR = {}
+
+
+def _dcn_far_scratch(dev, N, H, W, C):
+    """Persistent zeroed scratch of adr_dcn_bwd_bf16 per shape: the fp32 far-corner buffer and the tile flags
+    (the kernels leave both zero again, so one allocation serves every step and graph replay)."""
+    key = (str(dev), N, H, W, C)
+    if key not in _DCN_FAR:
+        _DCN_FAR[key] = (torch.zeros(N * H * W * C, dtype=torch.float32, device=dev),
+                         torch.zeros(int(lib.adr_dcn_bwd_tiles(N, H, W)), dtype=torch.int32, device=dev))
+    return _DCN_FAR[key]
+
+
 def _dcn_work(N, H, W, C, Cout, es=2):
     """Algorithmic (bytes, flops) of one DCN pass: x, the 27 offset/mask channels, the weight and y (or dy) once."""
     pix = N * H * W
@@ -2486,7 +2499,7 @@ class DCNFn(torch.autograd.Function):
         Cout = w.shape[0]
         y = empty_act(N, Cout, H, W, dtype, x.device)
         ctx.fused = _dcn_fused(dtype, C, Cout, omcs)
-        ctx.fused_bwd = ctx.fused and C == 64 and Cout == 64
+        ctx.fused_bwd = ctx.fused and C == Cout and C in (64, 128, 256)
         if ctx.fused:
             wp = pack_weight2(w, dtype)[0]  # KRSC [co][tap][c]
             tok = _t0("adr::dcn_fwd_kernel(adr::DcnArgs)", *_dcn_work(N, H, W, C, Cout),
@@ -2523,20 +2536,22 @@ class DCNFn(torch.autograd.Function):
         dev = x.device
         wt = torch.empty(9 * C * Cout, dtype=dtype, device=dev)  # W^T [(tap*C + c)][co]
         lib.adr_dcn_weight_t(dcode(dtype), fptr(w.detach().float().contiguous()), fptr(wt), Cout, C, stream())
-        dx32 = zero_(torch.empty(N * H * W * C, dtype=torch.float32, device=dev))
-        dom = zero_(empty_act(N, om.shape[1], H, W, dtype, dev))
         dw = None
         if ctx.fused and not ctx.fused_bwd:  # fused forward, other shapes: rebuild the columns for the GEMMs
             cols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=dev)
             lib.adr_dcn_im2col(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(cols), N, H,
                                W, C, stream())
         if ctx.fused_bwd:
+            # gathered by destination tile: bf16 dx written once, dom rows written whole (adr_dcn.hip)
+            dx = empty_act(N, C, H, W, dtype, dev)
+            dom = empty_act(N, om.shape[1], H, W, dtype, dev)
+            dxf, flags = _dcn_far_scratch(dev, N, H, W, C)
             nb, fl = _dcn_work(N, H, W, C, Cout)
             tok = _t0("adr::dcn_bwd_kernel(adr::DcnArgs)", nb + 2 * N * H * W * C, 2 * fl,
                       f"dcn bwd n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "")
             lib.adr_dcn_bwd_bf16(ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, ctypes.c_void_p(dyp), dycs,
-                                 fptr(wt), fptr(dx32), ctypes.c_void_p(dom.data_ptr()), om.shape[1], N, H, W, C, Cout,
-                                 stream())
+                                 fptr(wt), ctypes.c_void_p(dx.data_ptr()), C, ctypes.c_void_p(dom.data_ptr()),
+                                 om.shape[1], fptr(dxf), fptr(flags), N, H, W, C, Cout, stream())
             _t1(tok)
             if ctx.needs_input_grad[2]:
                 side = _side("dcn") if _target(ctx.pw) is not None else None
@@ -2559,6 +2574,8 @@ class DCNFn(torch.autograd.Function):
                         lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, Cout, C, C, 9, 0, acc, stream())
                     dw = grad_ret(ctx.pw, out)
         else:
+            dx32 = zero_(torch.empty(N * H * W * C, dtype=torch.float32, device=dev))
+            dom = zero_(empty_act(N, om.shape[1], H, W, dtype, dev))
             # dcols = dy x W^T  (1x1 GEMM: Cin = Cout, K = 9C)
             dcols = torch.empty(N * H * W * 9 * C, dtype=dtype, device=dev)
             d, _, _ = conv_desc(N, H, W, Cout, dycs, 9 * C, 1, 1, 1, 1, 0, 0, 9 * C, dtype)
@@ -2569,8 +2586,8 @@ class DCNFn(torch.autograd.Function):
             lib.adr_dcn_col2im(dcode(dtype), ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs, fptr(dcols),
                                fptr(dx32), ctypes.c_void_p(dom.data_ptr()), om.shape[1], N, H, W, C,
                                int(dtype == torch.float32), stream())
-        dx = empty_act(N, C, H, W, dtype, dev)
-        lib.adr_cast(F32, fptr(dx32), dcode(dtype), ctypes.c_void_p(dx.data_ptr()), N * H * W * C, stream())
+            dx = empty_act(N, C, H, W, dtype, dev)
+            lib.adr_cast(F32, fptr(dx32), dcode(dtype), ctypes.c_void_p(dx.data_ptr()), N * H * W * C, stream())
         return dx, dom, dw
 
 

@@ -10,17 +10,15 @@
 //   dcn_wgrad   dW[co][t][c] = sum_p dy[p][co] * cols[p][t][c]: the same sampling produces the B slab of a
 //               split-K GEMM over pixels (transposing LDS reads), partials [split][Cout][9][C] reduced by
 //               adr_wgrad_reduce (fixed order).
-//   dcn_bwd     per 8x8 pixel tile: dcols_t^T = W_t^T dy^T on MFMA (in registers, never stored), then for every
-//               (pixel, tap) the offset / mask-logit gradients (reductions over channels: DPP-free cross-lane
-//               xor shuffles, fixed order) and the input-gradient scatter. The scatter lands in an LDS window
-//               of the tile's input neighbourhood (corners within 3 pixels of the tile: offsets up to ~2 px)
-//               with LDS float atomics; the window is flushed to the fp32 input gradient with one global atomic
-//               per (cell, channel), corners outside it go to global atomics directly (unordered float atomics,
-//               as mmcv's own modulated_deformable_col2im_gpu_kernel; fp32 parity mode uses the
-//               deterministic path in adr_head.hip).
+//   dcn_bwd     per 8x8 pixel tile: the offset / mask-logit gradients of its pixels (dcols = W^T dy on MFMA,
+//               dotted with the bilinear samples), and dx of its pixels GATHERED from every source whose sample
+//               has a corner there (sampling matrix x dy on MFMA, then x W): dx written once in bf16, no fp32
+//               buffer, no float atomics except for corners more than ~2 px away (see below; fp32 parity mode
+//               uses the deterministic path in adr_head.hip).
 // Sampling follows mmcv dmcn_im2col_bilinear / dmcn_get_coordinate_weight: point (h - 1 + i + dy, w - 1 + j + dx),
 // zero unless -1 < py < H and -1 < px < W, every bilinear corner bounds-checked.
-// Shapes: C % 64 == 0, Cout % 64 == 0, omcs % 8 == 0 and >= 32 (the head pads the 27 channels to 32).
+// Shapes: C % 64 == 0, Cout % 64 == 0 (backward: C == Cout in {64, 128, 256}), omcs % 8 == 0 and >= 32 (the
+// head pads the 27 channels to 32).
 #include <type_traits>
 
 #include "adr_common.h"
@@ -84,9 +82,9 @@ struct DcnArgs {
   const __bf16* dy;
   __bf16* y;
   float* part;       // wgrad partials [split][Cout][9][C]
-  float* dx32;       // bwd: fp32 input gradient (accumulated with atomics; caller zeroes it)
+  __bf16* dx;        // bwd: input gradient (written once per element, far entries added afterwards)
   __bf16* dom;       // bwd: offset / mask-logit gradient (caller zeroes the padding channels)
-  int xcs, omcs, ycs, dycs, domcs;
+  int xcs, omcs, ycs, dycs, domcs, dxcs;
   int N, H, W, C, Cout;
   int x_bytes, w_bytes, dy_bytes;
   long rows_per_split;
@@ -361,252 +359,421 @@ __global__ void __launch_bounds__(256, 2) dcn_wgrad_kernel(DcnArgs a) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// data / offset / mask gradients (C == Cout == 64): 8x8 pixel tile per block, all taps
+// data / offset / mask gradients, gathered by destination tile (C == Cout in {64, 128, 256})
 //
-// Per tap: (1) lane (pixel, channel group) computes the tap's sampling point, issues its corner loads and, on
-// MFMA, its column of dcols^T = W_t^T dy^T (W_t^T fragments from L2, the tile's dy fragments held in
-// registers); (2) the offset / mask-logit gradients are channel reductions in-lane plus two xor shuffles,
-// written straight to dom; (3) the input-gradient scatter is a second GEMM: the tap's sampling matrix S_t
-// (window cell x pixel, four bilinear weights x mask per pixel column, built in LDS) times dcols (pixel x
-// channel) accumulates the tile's input-gradient window — 196 cells (corners within 3 px of the tile) x 64
-// channels — in fp32 MFMA accumulators across all nine taps. No LDS read-modify-write scatter at all (LDS float
-// atomics measured ~4x slower than this whole kernel). At the end the window goes to the fp32 input gradient
-// with one global atomic per (cell, channel); valid corners outside it are queued per tap and added with
-// global atomics.
+// A block owns an 8x8 tile of pixels: as output pixels p it produces their offset / mask-logit gradients, as
+// input pixels q their dx. dx is written once, in bf16, from fp32 MFMA accumulators:
+//
+//   phase 1 (dom): per 64-channel chunk, the chunk of x over the tile's 14x14 neighbourhood is staged in LDS
+//     once; per tap, dcols^T = W_t^T dy^T for the tile's 64 pixels on MFMA (dy fragments in registers, W_t^T
+//     slabs double-buffered through LDS), dotted with the bilinear samples of x and their derivatives read from
+//     the staged neighbourhood (channel reductions in-lane + two xor shuffles, fixed order) -> partial sums per
+//     (pixel, tap) in LDS, finalised into one 64-byte dom row per pixel.
+//   phase 2 (dx): dx_q = sum_t W_t . G_t[q], G_t[q][co] = sum_{p, corner -> q} m w dy[p][co]. The sources whose
+//     tap-t sample can put a corner in the tile lie in a 12x12 sub-window of the neighbourhood (|offset| < 2
+//     px); their dy rows are staged once per 64-channel chunk. The tap's sampling matrix S_t [64 dest x 144 src]
+//     (bilinear weight x mask, bf16; column k written and cleared only by thread k) is built in LDS, then
+//     G_t^T = dy_sub^T . S_t^T and dx^T += W_t^T . G_t^T on MFMA, G_t^T passed from accumulators to the next
+//     operand in registers (k order permuted identically on both operands). 32-source K steps whose S_t columns
+//     are all zero for a wave's 16 destinations are skipped (bitmask built with the matrix).
+//   far corners (|offset| >= ~2 px: the source is outside its destination tile's sub-window) are added by the
+//     SOURCE's block in phase 1 straight from the dcols accumulators into `dxf` (fp32 side buffer, global
+//     atomics) and flag the destination tile; dcn_far_apply_kernel folds flagged tiles into dx afterwards and
+//     re-zeroes them. With |offsets| < 2 px nothing is flagged and dx is bitwise repeatable.
+// Near/far is decided by the same arithmetic (sample()) on both sides, so each valid corner is counted once.
 // ------------------------------------------------------------------------------------------------------------
-constexpr int BT = 8;                   // tile side (pixels)
-constexpr int BHALO = 3;                // window margin: corners of samples with |offset| <~ 2 px
-constexpr int BWIN = BT + 2 * BHALO;    // 14 window cells per side
-constexpr int BCELL = BWIN * BWIN;      // 196 cells
-constexpr int BROWS = 208;              // cells padded to 13 MFMA row blocks
-constexpr int SPITCH = 72;              // S_t row pitch (bf16): 64 pixels + 8
-constexpr int DPITCH = 80;              // dcols row pitch (bf16): odd multiple of 16 elements for transposing reads
-constexpr int BOVF = 256;               // overflow queue (out-of-window corners) per tap
+constexpr int GT = 8;                  // tile side (pixels)
+constexpr int GM = 3;                  // neighbourhood margin
+constexpr int GWIN = GT + 2 * GM;      // 14
+constexpr int GCELL = GWIN * GWIN;     // 196 neighbourhood cells (+ one zero row)
+constexpr int GSUB = 12;               // per-tap source sub-window side
+constexpr int GK = GSUB * GSUB;        // 144 sources per tap
+constexpr int GKS = 5;                 // K steps of 32 (160)
+constexpr int GSP = 168;               // S row pitch (bf16)
+constexpr int GDP = 80;                // dy-window row pitch: odd multiple of 16 elements (transposing reads)
+constexpr int GXP = 72;                // x-window row pitch (bf16)
 
-// OCC = workgroups per CU the register budget is sized for: 2 (256 VGPRs, a few spilled) or 1 (AGPRs too, no spill)
-template <int OCC>
-__global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a) {
-  __shared__ __attribute__((aligned(16))) __bf16 S[BROWS * SPITCH];   // [cell][pixel]
-  __shared__ __attribute__((aligned(16))) __bf16 D[64 * DPITCH];      // dcols [pixel][channel]
-  __shared__ __attribute__((aligned(16))) __bf16 oms[64 * 32];
-  __shared__ __attribute__((aligned(16))) __bf16 WT[2][64 * 72];     // W_t^T [c][co], two taps
-  __shared__ int ovf[BOVF];                                            // pixel * 4 + corner
-  __shared__ int novf[2];                                              // per-tap queue length (alternating)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int tw = (a.W + BT - 1) / BT, th = (a.H + BT - 1) / BT;
+__device__ __forceinline__ int gsrc_row(int k, int sy, int sx) {  // neighbourhood row of sub-window source k
+  const int ky = k / GSUB, kx = k - ky * GSUB;
+  return k < GK ? (ky + 1 - sy) * GWIN + kx + 1 - sx : GCELL;
+}
+
+template <int CO>
+struct GLds {
+  static constexpr int PW1 = 64 * CO + 8;                                  // phase-1 slab pitch [c][co]
+  static constexpr int OMS = GCELL * 32 * 2;                               // om rows of the neighbourhood
+  static constexpr int P1X = GCELL * GXP * 2, P1W = 2 * 64 * PW1 * 2, P1D = 64 * 27 * 4;
+  static constexpr int P1 = P1X + P1W + P1D;                               // x window | W_t^T slabs | dom sums
+  static constexpr int P2Y = (GCELL + 1) * GDP * 2, P2S = 64 * GSP * 2, P2W = 64 * 72 * 2;
+  static constexpr int P2 = P2Y + P2S + P2W;                               // dy window | S_t | W_t slab
+  static constexpr int TOTAL = OMS + (P1 > P2 ? P1 : P2) + 64;             // + K-step masks
+};
+
+template <int CC, int CO, int OCC>
+__global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf, int* flags, int mode) {
+  using L = GLds<CO>;
+  __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
+  __bf16* oms = reinterpret_cast<__bf16*>(smem);
+  char* reg = smem + L::OMS;
+  unsigned* kmask = reinterpret_cast<unsigned*>(smem + L::TOTAL - 64);  // [2 taps][4 waves]
+  constexpr int C = 64 * CC, Cout = 64 * CO;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
+  const int tw = (a.W + GT - 1) / GT, th = (a.H + GT - 1) / GT;
   const int bid = xcd_order(blockIdx.x, gridDim.x);
   const int n = bid / (tw * th);
   const int rem = bid - n * tw * th;
-  const int h0 = (rem / tw) * BT, w0 = (rem % tw) * BT;
-  const int wy0 = h0 - BHALO, wx0 = w0 - BHALO;
+  const int h0 = (rem / tw) * GT, w0 = (rem % tw) * GT;
+  const int wy0 = h0 - GM, wx0 = w0 - GM;
   const int ibase = n * a.H * a.W;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
+  const u32x4 z4 = {0u, 0u, 0u, 0u};
+  auto inimg = [&](int yy, int xx) { return yy >= 0 && yy < a.H && xx >= 0 && xx < a.W; };
 
-  {
-    const int p = tid >> 2, ch = (tid & 3) * 8;
-    const int hh = h0 + (p >> 3), ww = w0 + (p & 7);
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (hh < a.H && ww < a.W) v = ld16(a.om + (long)(ibase + hh * a.W + ww) * a.omcs + ch);
-    st16(&oms[p * 32 + ch], v);
+  // offset / mask rows of the 14x14 neighbourhood (zero outside the image)
+  for (int q = tid; q < GCELL * 4; q += 256) {
+    const int cell = q >> 2, ch = (q & 3) * 8;
+    const int yy = wy0 + cell / GWIN, xx = wx0 + cell % GWIN;
+    st16(&oms[cell * 32 + ch], inimg(yy, xx) ? ld16(a.om + (long)(ibase + yy * a.W + xx) * a.omcs + ch) : z4);
   }
-  {
-    const u32x4 z = {0u, 0u, 0u, 0u};
-    for (int i = tid; i < BROWS * SPITCH / 8; i += 256) st16(&S[8 * i], z);
-  }
-  if (tid < 2) novf[tid] = 0;
 
-  // this lane's pixel and channel group (dcols^T layout of the MFMA result: row = channel, column = pixel)
-  const int pl = 16 * wave + (lane & 15);
-  const int ph = h0 + (pl >> 3), pw = w0 + (pl & 7);
-  const bool pok = ph < a.H && pw < a.W;
-  const int g = lane >> 4;
-  const long ppix = ibase + (long)ph * a.W + pw;
-  bf16x8 fb[2];  // dy fragments of this lane's pixel (B operand, k = output channel)
+  // ---------------- phase 1: offset / mask-logit gradients of the tile's 64 output pixels ----------------
+  if (!(mode & 1)) {
+    __bf16* xwin = reinterpret_cast<__bf16*>(reg);
+    __bf16* slab0 = reinterpret_cast<__bf16*>(reg + L::P1X);
+    __bf16* slab1 = slab0 + 64 * L::PW1;
+    float* dsum = reinterpret_cast<float*>(reg + L::P1X + L::P1W);  // [pixel][tap][3]: mask, dy, dx sums
+    for (int i = tid; i < 64 * 27; i += 256) dsum[i] = 0.f;
+    const int pl = 16 * wave + (lane & 15);
+    const int ph = h0 + (pl >> 3), pw = w0 + (pl & 7);
+    const bool pok = ph < a.H && pw < a.W;
+    const long ppix = ibase + (long)ph * a.W + pw;
+    const __bf16* om_p = oms + ((ph - wy0) * GWIN + pw - wx0) * 32;
+    bf16x8 fb[2 * CO];  // dy fragments of this lane's pixel (B operand, k = output channel)
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (pok) v = ld16(a.dy + ppix * a.dycs + 32 * k + 8 * g);
-    fb[k] = *reinterpret_cast<bf16x8*>(&v);
+    for (int k = 0; k < 2 * CO; ++k) {
+      u32x4 v = z4;
+      if (pok) v = ld16(a.dy + ppix * a.dycs + 32 * k + 8 * g);
+      fb[k] = *reinterpret_cast<bf16x8*>(&v);
+    }
+    u32x4 wreg[2 * CO];
+    auto wload = [&](int t, int cc) {
+#pragma unroll
+      for (int i = 0; i < 2 * CO; ++i) {
+        const int q = tid + 256 * i, row = q / (8 * CO), cch = q - row * 8 * CO;
+        wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, (unsigned)(((t * C + cc * 64 + row) * Cout) + cch * 8) * 2u, 0, 0);
+      }
+    };
+    auto wstore = [&](__bf16* sl) {
+#pragma unroll
+      for (int i = 0; i < 2 * CO; ++i) {
+        const int q = tid + 256 * i, row = q / (8 * CO), cch = q - row * 8 * CO;
+        st16(&sl[row * L::PW1 + cch * 8], wreg[i]);
+      }
+    };
+#pragma unroll 1
+    for (int cc = 0; cc < CC; ++cc) {
+      wload(0, cc);
+      __syncthreads();  // the previous chunk's x window and slabs no longer read
+      for (int q = tid; q < GCELL * 8; q += 256) {
+        const int cell = q >> 3, ch = (q & 7) * 8;
+        const int yy = wy0 + cell / GWIN, xx = wx0 + cell % GWIN;
+        st16(&xwin[cell * GXP + ch],
+             inimg(yy, xx) ? ld16(a.x + (long)(ibase + yy * a.W + xx) * a.xcs + cc * 64 + ch) : z4);
+      }
+      wstore(slab0);
+      __syncthreads();
+#pragma unroll 1
+      for (int t = 0; t < 9; ++t) {
+        const __bf16* sl = (t & 1) ? slab1 : slab0;
+        if (t + 1 < 9) wload(t + 1, cc);
+        f32x4 acc[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int k = 0; k < 2 * CO; ++k)
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                *reinterpret_cast<const bf16x8*>(&sl[(16 * i + (lane & 15)) * L::PW1 + 32 * k + 8 * g]), fb[k], acc[i], 0,
+                0, 0);
+        }
+        if (t + 1 < 9) wstore((t & 1) ? slab0 : slab1);  // last read in tap t-1, before the barrier below
+        const float oy = (float)om_p[2 * t], ox = (float)om_p[2 * t + 1];
+        const float mk = sigm((float)om_p[18 + t]);
+        Corners c0;
+        sample((float)(ph - 1 + t / 3) + oy, (float)(pw - 1 + t % 3) + ox, a.H, a.W, c0);
+        // the four corners' channels 16 i + 4 g .. +3: from the staged neighbourhood, or (corner outside it) global
+        u32x2 xv[4][4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int yy = c0.y0 + (q >> 1), xx = c0.x0 + (q & 1);
+          const int cy = yy - wy0, cx = xx - wx0;
+          const bool ok = pok && c0.ok[q];
+          if (cy >= 0 && cy < GWIN && cx >= 0 && cx < GWIN) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const u32x2 v = *reinterpret_cast<const u32x2*>(&xwin[(cy * GWIN + cx) * GXP + 16 * i + 4 * g]);
+              xv[q][i] = ok ? v : (u32x2){0u, 0u};
+            }
+          } else {
+            const int pix = ibase + yy * a.W + xx;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              xv[q][i] = __builtin_amdgcn_raw_buffer_load_b64(
+                  xr, ok ? (unsigned)(pix * a.xcs + cc * 64 + 16 * i + 4 * g) * 2u : OOR, 0, 0);
+          }
+        }
+        float smk = 0.f, spy = 0.f, spx = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          float xf[4][4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const __bf16* e = reinterpret_cast<const __bf16*>(&xv[q][i]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) xf[q][k] = (float)e[k];
+          }
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float top = xf[0][e] + c0.lx * (xf[1][e] - xf[0][e]);
+            const float bot = xf[2][e] + c0.lx * (xf[3][e] - xf[2][e]);
+            const float d01 = xf[1][e] - xf[0][e], d23 = xf[3][e] - xf[2][e];
+            const float val = top + c0.ly * (bot - top);
+            const float sy = bot - top, sx = d01 + c0.ly * (d23 - d01);
+            const float gv = acc[i][e];
+            smk += gv * val;
+            spy += gv * sy;
+            spx += gv * sx;
+          }
+        }
+        smk += __shfl_xor(smk, 16, 64);
+        smk += __shfl_xor(smk, 32, 64);
+        spy += __shfl_xor(spy, 16, 64);
+        spy += __shfl_xor(spy, 32, 64);
+        spx += __shfl_xor(spx, 16, 64);
+        spx += __shfl_xor(spx, 32, 64);
+        if (g == 0) {
+          float* d = dsum + (pl * 9 + t) * 3;
+          d[0] += smk;
+          d[1] += spy;
+          d[2] += spx;
+        }
+        // corners whose destination tile cannot see this source: scatter this chunk of dcols into dxf
+        if (pok) {
+          const int sy = t / 3 - 1, sx = t % 3 - 1;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            if (!c0.ok[q]) continue;
+            const int yy = c0.y0 + (q >> 1), xx = c0.x0 + (q & 1);
+            const int ry = ph - (yy & ~(GT - 1)) + sy, rx = pw - (xx & ~(GT - 1)) + sx;
+            if (ry < -2 || ry > GSUB - 3 || rx < -2 || rx > GSUB - 3) {
+              const float wq = mk * c0.w[q];
+              float* dst = dxf + (long)(ibase + yy * a.W + xx) * C + cc * 64 + 4 * g;
+#pragma unroll
+              for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) unsafeAtomicAdd(dst + 16 * i + e, wq * acc[i][e]);
+              if (g == 0) flags[(n * th + (yy >> 3)) * tw + (xx >> 3)] = 1;
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // dom rows: offsets d = m * sum(g * d sample / d p), mask logit d = sum(g * sample) * m (1 - m)
+    if (tid < 64) {
+      const int hh = h0 + (tid >> 3), ww = w0 + (tid & 7);
+      if (hh < a.H && ww < a.W) {
+        const __bf16* o = oms + ((hh - wy0) * GWIN + ww - wx0) * 32;
+        __bf16 row[32];
+#pragma unroll
+        for (int k = 27; k < 32; ++k) row[k] = (__bf16)0.f;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+          const float mk = sigm((float)o[18 + t]);
+          const float* d = dsum + (tid * 9 + t) * 3;
+          row[2 * t] = (__bf16)(mk * d[1]);
+          row[2 * t + 1] = (__bf16)(mk * d[2]);
+          row[18 + t] = (__bf16)(d[0] * mk * (1.f - mk));
+        }
+        __bf16* dst = a.dom + (long)(ibase + hh * a.W + ww) * a.domcs;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) st16(dst + 8 * k, *reinterpret_cast<const u32x4*>(&row[8 * k]));
+      }
+    }
   }
-  // the tap's W^T slab (LDS, loaded cooperatively) and this lane's bilinear-corner loads, both issued one tap
-  // ahead: the corners into the other of two register sets, the slab through registers into the other LDS buffer
-  u32x2 xv[2][4][4];
-  Corners cs[2];
-  float mks[2];
-  u32x4 wreg[2];
-  auto issue = [&](int t, auto SB) {
-    constexpr int b = decltype(SB)::value;
+
+  // ---------------- phase 2: dx of the tile's 64 input pixels ----------------
+  if (mode & 2) return;
+  __bf16* dyw = reinterpret_cast<__bf16*>(reg);
+  __bf16* S = reinterpret_cast<__bf16*>(reg + L::P2Y);
+  __bf16* Wsl = reinterpret_cast<__bf16*>(reg + L::P2Y + L::P2S);
+  f32x4 dxa[CC][4];  // dx^T: [c chunk][c tile] rows c = 16 i + 4 g + e, column q = 16 wave + (lane & 15)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + 256 * i;
-      wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(wr, (unsigned)((t * 64 + (q >> 3)) * 64 + (q & 7) * 8) * 2u, 0, 0);
-    }
-    const float oy = (float)oms[pl * 32 + 2 * t], ox = (float)oms[pl * 32 + 2 * t + 1];
-    mks[b] = sigm((float)oms[pl * 32 + 18 + t]);
-    sample((float)(ph - 1 + t / 3) + oy, (float)(pw - 1 + t % 3) + ox, a.H, a.W, cs[b]);
+  for (int cc = 0; cc < CC; ++cc)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const bool ok = pok && cs[b].ok[q];
-      const int pix = ibase + (cs[b].y0 + (q >> 1)) * a.W + cs[b].x0 + (q & 1);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        xv[b][q][i] =
-            __builtin_amdgcn_raw_buffer_load_b64(xr, ok ? (unsigned)(pix * a.xcs + 16 * i + 4 * g) * 2u : OOR, 0, 0);
-    }
-  };
-  auto wstore = [&](int b) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + 256 * i;
-      st16(&WT[b][(q >> 3) * 72 + (q & 7) * 8], wreg[i]);
-    }
-  };
-  // window accumulators: wave w owns channels 16 w .. +15, all 13 cell blocks
-  f32x4 win[13];
-#pragma unroll
-  for (int b = 0; b < 13; ++b) win[b] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // transposing-read lane map for the B operand of the scatter GEMM (see adr_wgrad.hip): k-slot (g, j) is
-  // pixel row 4 g + j (j < 4) / 16 + 4 g + j - 4; the A operand (S) reads the same pixels as two 8-byte pieces
+    for (int i = 0; i < 4; ++i) dxa[cc][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int q4 = (lane >> 2) & 3, p4 = lane & 3;
-  const __bf16* dtr = D + (4 * g + q4) * DPITCH + 16 * wave + 4 * p4;
-  int prev[4] = {-1, -1, -1, -1};  // S cells written in the previous tap (g == 0 lanes)
-  __syncthreads();  // oms / S ready
-  using B0 = std::integral_constant<int, 0>;
-  using B1 = std::integral_constant<int, 1>;
-  issue(0, B0{});
-  wstore(0);
-  __syncthreads();
-
-  auto tap = [&](int t, auto SB) {
-    constexpr int cur = decltype(SB)::value;
-    using NB = std::integral_constant<int, 1 - cur>;
-    if (t + 1 < 9) issue(t + 1, NB{});  // WT[1 - cur] was last read before the previous tap's first barrier
-    const Corners& c0 = cs[cur];
-    const float mk = mks[cur];
-    // the sampling-matrix column of this pixel: clear the previous tap's entries, write this tap's
-    if (g == 0) {
+  const __bf16* Sq = S + (16 * wave + (lane & 15)) * GSP;  // this lane's destination row of S_t
+  u32x4 wreg[2];
+  auto wissue = [&](int t, int cc, int coc) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if (prev[q] >= 0) S[prev[q] * SPITCH + pl] = (__bf16)0.f;
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + 256 * i;
+      wreg[i] = __builtin_amdgcn_raw_buffer_load_b128(
+          wr, (unsigned)(((t * C + cc * 64 + (q >> 3)) * Cout) + coc * 64 + (q & 7) * 8) * 2u, 0, 0);
+    }
+  };
+  auto wst = [&]() {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int yy = c0.y0 + (q >> 1), xx = c0.x0 + (q & 1);
-        const int cy = yy - wy0, cx = xx - wx0;
-        const bool valid = pok && c0.ok[q];
-        const bool inwin = cy >= 0 && cy < BWIN && cx >= 0 && cx < BWIN;
-        prev[q] = -1;
-        if (valid && inwin) {
-          prev[q] = cy * BWIN + cx;
-          S[prev[q] * SPITCH + pl] = (__bf16)(mk * c0.w[q]);
-        } else if (valid) {
-          const int k = atomicAdd(&novf[t & 1], 1);  // at most 64 x 4 = BOVF entries
-          ovf[k] = pl * 4 + q;
+    for (int i = 0; i < 2; ++i) {
+      const int q = tid + 256 * i;
+      st16(&Wsl[(q >> 3) * 72 + (q & 7) * 8], wreg[i]);
+    }
+  };
+  bf16x8 gb[2];  // G_t^T as the B operand of dx^T += W_t^T G_t^T (k = co, slots {16 (2kk+h) + 4 g + e})
+  auto dxmma = [&](int cc) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const __bf16* wrow = Wsl + (16 * i + (lane & 15)) * 72 + 32 * kk + 4 * g;
+        u32x2 aa[2] = {*reinterpret_cast<const u32x2*>(wrow), *reinterpret_cast<const u32x2*>(wrow + 16)};
+        dxa[cc][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(aa), gb[kk], dxa[cc][i], 0, 0, 0);
+      }
+  };
+  // S_t starts all-zero; thread k (< 144) writes and later clears only its own column
+  for (int q = tid; q < 64 * GSP / 8; q += 256) st16(&S[8 * q], z4);
+  if (tid < 8) kmask[tid] = 0u;
+  int prevq[4] = {-1, -1, -1, -1};
+#pragma unroll 1
+  for (int coc = 0; coc < CO; ++coc) {
+    wissue(0, 0, coc);
+    __syncthreads();  // phase-1 buffers / the previous chunk's dy window no longer read
+    for (int q = tid; q < (GCELL + 1) * 8; q += 256) {
+      const int row = q >> 3, ch = (q & 7) * 8;
+      const int yy = wy0 + row / GWIN, xx = wx0 + row % GWIN;
+      st16(&dyw[row * GDP + ch], row < GCELL && inimg(yy, xx)
+                                     ? ld16(a.dy + (long)(ibase + yy * a.W + xx) * a.dycs + coc * 64 + ch)
+                                     : z4);
+    }
+#pragma unroll 1
+    for (int t = 0; t < 9; ++t) {
+      const int sy = t / 3 - 1, sx = t % 3 - 1;
+      const int tt = coc * 9 + t;
+      __syncthreads();  // the previous tap's S_t / W slab / masks no longer read; dy window staged
+      wst();
+      if (CC > 1) wissue(t, 1, coc);
+      else if (t + 1 < 9) wissue(t + 1, 0, coc);
+      else if (coc + 1 < CO) wissue(0, 0, coc + 1);
+      if (tid < 4) kmask[4 * ((tt + 1) & 1) + tid] = 0u;  // next tap's masks (read after two more barriers)
+      if (tid < GK) {  // source k = tid of the tap's sub-window: its corners that land in this tile
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if (prevq[q] >= 0) S[prevq[q] * GSP + tid] = (__bf16)0.f;
+        const int ky = tid / GSUB, kx = tid - ky * GSUB;
+        const int cy = ky + 1 - sy, cx = kx + 1 - sx;
+        const int py = wy0 + cy, px = wx0 + cx;
+        const bool sok = inimg(py, px);
+        const __bf16* o = oms + (cy * GWIN + cx) * 32;
+        const float mk = sigm((float)o[18 + t]);
+        Corners c0;
+        sample((float)(py - 1 + t / 3) + (float)o[2 * t], (float)(px - 1 + t % 3) + (float)o[2 * t + 1], a.H, a.W, c0);
+        unsigned bits[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int qy = c0.y0 + (q >> 1) - h0, qx = c0.x0 + (q & 1) - w0;
+          prevq[q] = -1;
+          if (sok && c0.ok[q] && qy >= 0 && qy < GT && qx >= 0 && qx < GT) {
+            prevq[q] = qy * GT + qx;
+            S[prevq[q] * GSP + tid] = (__bf16)(mk * c0.w[q]);
+            bits[qy >> 1] |= 1u << (tid >> 5);
+          }
+        }
+#pragma unroll
+        for (int w4 = 0; w4 < 4; ++w4)
+          if (bits[w4]) atomicOr(&kmask[4 * (tt & 1) + w4], bits[w4]);
+      }
+      __syncthreads();  // S_t, masks and the W slab complete
+      // G_t^T (64 co x this wave's 16 destinations) = dy_sub^T . S_t^T, skipping all-zero K steps
+      const unsigned km = kmask[4 * (tt & 1) + wave];
+      f32x4 ga[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) ga[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kk = 0; kk < GKS; ++kk) {
+        if (!(km & (1u << kk))) continue;
+        const __bf16* sr = Sq + 32 * kk + 4 * g;
+        u32x2 bs[2] = {*reinterpret_cast<const u32x2*>(sr), *reinterpret_cast<const u32x2*>(sr + 16)};
+        const bf16x8 fbs = *reinterpret_cast<bf16x8*>(bs);
+        const int rlo = gsrc_row(32 * kk + 4 * g + q4, sy, sx), rhi = gsrc_row(32 * kk + 16 + 4 * g + q4, sy, sx);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          v4s aa[2] = {tr16(dyw + rlo * GDP + 16 * j + 4 * p4), tr16(dyw + rhi * GDP + 16 * j + 4 * p4)};
+          ga[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(aa), fbs, ga[j], 0, 0, 0);
         }
       }
-    }
-    // dcols^T (64 channels x this wave's 16 pixels) = W_t^T . dy^T
-    f32x4 acc[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      acc[i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+      for (int kk = 0; kk < 2; ++kk) {
+        __bf16* e = reinterpret_cast<__bf16*>(&gb[kk]);
 #pragma unroll
-      for (int k = 0; k < 2; ++k)
-        acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            *reinterpret_cast<const bf16x8*>(&WT[cur][(16 * i + (lane & 15)) * 72 + 32 * k + 8 * g]), fb[k], acc[i], 0,
-            0, 0);
-    }
-    if (t + 1 < 9) wstore(1 - cur);
+        for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      __bf16 v4[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v4[e] = (__bf16)acc[i][e];
-      *reinterpret_cast<u32x2*>(&D[pl * DPITCH + 16 * i + 4 * g]) = *reinterpret_cast<u32x2*>(v4);
-    }
-    // offset / mask-logit gradients: value, d/dpy, d/dpx of the bilinear sample per channel (invalid corners
-    // read as zero), dotted with dcols over this lane's 16 channels, then over the four channel groups
-    float smk = 0.f, spy = 0.f, spx = 0.f;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      float xf[4][4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const __bf16* e = reinterpret_cast<const __bf16*>(&xv[cur][q][i]);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) xf[q][k] = (float)e[k];
+          for (int r = 0; r < 4; ++r) e[4 * h + r] = (__bf16)ga[2 * kk + h][r];
       }
+      dxmma(0);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float top = xf[0][e] + c0.lx * (xf[1][e] - xf[0][e]);
-        const float bot = xf[2][e] + c0.lx * (xf[3][e] - xf[2][e]);
-        const float d01 = xf[1][e] - xf[0][e], d23 = xf[3][e] - xf[2][e];
-        const float val = top + c0.ly * (bot - top);
-        const float sy = bot - top, sx = d01 + c0.ly * (d23 - d01);
-        const float gv = acc[i][e];
-        smk += gv * val;
-        spy += gv * sy;
-        spx += gv * sx;
+      for (int cc = 1; cc < CC; ++cc) {
+        __syncthreads();
+        wst();
+        if (cc + 1 < CC) wissue(t, cc + 1, coc);
+        else if (t + 1 < 9) wissue(t + 1, 0, coc);
+        else if (coc + 1 < CO) wissue(0, 0, coc + 1);
+        __syncthreads();
+        dxmma(cc);
       }
     }
-    smk += __shfl_xor(smk, 16, 64);
-    smk += __shfl_xor(smk, 32, 64);
-    spy += __shfl_xor(spy, 16, 64);
-    spy += __shfl_xor(spy, 32, 64);
-    spx += __shfl_xor(spx, 16, 64);
-    spx += __shfl_xor(spx, 32, 64);
-    if (g == 0 && pok) {
-      __bf16* d = a.dom + ppix * a.domcs;
-      d[2 * t] = (__bf16)(mk * spy);
-      d[2 * t + 1] = (__bf16)(mk * spx);
-      d[18 + t] = (__bf16)(smk * mk * (1.f - mk));
-    }
-    __syncthreads();  // S column entries and dcols complete
-    if (tid == 0) novf[(t + 1) & 1] = 0;  // last read in tap t-1
-    // window[cell][c] += S_t[cell][pixel] . dcols[pixel][c]  (K = 64 pixels in two 32-steps)
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      v4s blo = tr16(dtr + kk * 32 * DPITCH), bhi = tr16(dtr + (kk * 32 + 16) * DPITCH);
-      v4s bb[2] = {blo, bhi};
-      const bf16x8 fbw = *reinterpret_cast<bf16x8*>(bb);
-#pragma unroll
-      for (int b = 0; b < 13; ++b) {
-        const __bf16* sr = S + (16 * b + (lane & 15)) * SPITCH + 32 * kk + 4 * g;
-        u32x2 alo = *reinterpret_cast<const u32x2*>(sr), ahi = *reinterpret_cast<const u32x2*>(sr + 16);
-        u32x2 aa[2] = {alo, ahi};
-        win[b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(aa), fbw, win[b], 0, 0, 0);
-      }
-    }
-    // out-of-window corners: global atomics, one queued (pixel, corner) per wave at a time, lanes = channels
-    const int nq = novf[t & 1];
-    for (int k = wave; k < nq; k += 4) {
-      const int pq = ovf[k], p = pq >> 2, qq = pq & 3;
-      const int ph2 = h0 + (p >> 3), pw2 = w0 + (p & 7);
-      const float oy2 = (float)oms[p * 32 + 2 * t], ox2 = (float)oms[p * 32 + 2 * t + 1];
-      const float mk2 = sigm((float)oms[p * 32 + 18 + t]);
-      Corners c2;
-      sample((float)(ph2 - 1 + t / 3) + oy2, (float)(pw2 - 1 + t % 3) + ox2, a.H, a.W, c2);
-      const int yy = c2.y0 + (qq >> 1), xx = c2.x0 + (qq & 1);
-      unsafeAtomicAdd(a.dx32 + (long)(ibase + yy * a.W + xx) * 64 + lane, (float)D[p * DPITCH + lane] * mk2 * c2.w[qq]);
-    }
-    __syncthreads();  // before the next tap rewrites S / dcols
-  };
-#pragma unroll 1
-  for (int t = 0; t < 9; t += 2) {
-    tap(t, B0{});
-    if (t + 1 < 9) tap(t + 1, B1{});
   }
-  // flush the window: one global atomic per (cell, channel) that received anything
+  // dx rows: lane (g, q) holds channels 16 i + 4 g .. +3 of destination q
+  const int ql = 16 * wave + (lane & 15), qy = h0 + (ql >> 3), qx = w0 + (ql & 7);
+  if (qy < a.H && qx < a.W) {
+    __bf16* dst = a.dx + (long)(ibase + qy * a.W + qx) * a.dxcs + 4 * g;
 #pragma unroll
-  for (int b = 0; b < 13; ++b)
+    for (int cc = 0; cc < CC; ++cc)
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int cell = 16 * b + 4 * g + e;
-      const int yy = wy0 + cell / BWIN, xx = wx0 + cell % BWIN;
-      const float v = win[b][e];
-      if (cell < BCELL && v != 0.f && yy >= 0 && yy < a.H && xx >= 0 && xx < a.W)
-        unsafeAtomicAdd(a.dx32 + (long)(ibase + yy * a.W + xx) * 64 + 16 * wave + (lane & 15), v);
-    }
+      for (int i = 0; i < 4; ++i) {
+        __bf16 v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (__bf16)dxa[cc][i][e];
+        *reinterpret_cast<u32x2*>(dst + cc * 64 + 16 * i) = *reinterpret_cast<u32x2*>(v);
+      }
+  }
+}
+
+// flagged tiles: dx += dxf (far corners), then dxf and the flag back to zero
+__global__ void __launch_bounds__(256) dcn_far_apply_kernel(DcnArgs a, float* dxf, int* flags) {
+  const int tw = (a.W + GT - 1) / GT, th = (a.H + GT - 1) / GT;
+  const int b = blockIdx.x;
+  if (flags[b] == 0) return;
+  const int n = b / (tw * th), rem = b - n * tw * th;
+  const int h0 = (rem / tw) * GT, w0 = (rem % tw) * GT;
+  const int cq = a.C / 4;  // float4 groups per pixel
+  for (int i = threadIdx.x; i < 64 * cq; i += 256) {
+    const int p = i / cq, c = (i - p * cq) * 4;
+    const int hh = h0 + (p >> 3), ww = w0 + (p & 7);
+    if (hh >= a.H || ww >= a.W) continue;
+    const long pix = (long)n * a.H * a.W + (long)hh * a.W + ww;
+    float4* f = reinterpret_cast<float4*>(dxf + pix * a.C + c);
+    const float4 v = *f;
+    __bf16* d = a.dx + pix * a.dxcs + c;
+    d[0] = (__bf16)((float)d[0] + v.x);
+    d[1] = (__bf16)((float)d[1] + v.y);
+    d[2] = (__bf16)((float)d[2] + v.z);
+    d[3] = (__bf16)((float)d[3] + v.w);
+    *f = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) flags[b] = 0;
 }
 
 }  // namespace adr
@@ -684,21 +851,24 @@ extern "C" int adr_dcn_wgrad_bf16(const void* x, int xcs, const void* om, int om
 }
 
 extern "C" int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs, const void* dy, int dycs,
-                                const void* w_t, float* dx32, void* dom, int domcs, int N, int H, int W, int C, int Cout,
-                                void* stream) {
+                                const void* w_t, void* dx, int dxcs, void* dom, int domcs, float* dxf, int* tile_flags,
+                                int N, int H, int W, int C, int Cout, void* stream) {
   if (int rc = dcn_check(N, H, W, C, Cout, xcs, omcs)) return rc;
-  ADR_REQUIRE(C == 64 && Cout == 64, "dcn_bwd (bf16 fused): C == Cout == 64 only (C=%d Cout=%d)", C, Cout);
-  ADR_REQUIRE(domcs >= 27 && dycs % 8 == 0, "dcn_bwd: domcs=%d dycs=%d", domcs, dycs);
+  ADR_REQUIRE(C == Cout && (C == 64 || C == 128 || C == 256),
+              "dcn_bwd (bf16 fused): C == Cout in {64, 128, 256} (C=%d Cout=%d)", C, Cout);
+  ADR_REQUIRE(domcs >= 32 && domcs % 8 == 0 && dycs % 8 == 0 && dxcs % 8 == 0 && dxcs >= C,
+              "dcn_bwd: domcs=%d dycs=%d dxcs=%d", domcs, dycs, dxcs);
   DcnArgs a{};
   a.x = (const __bf16*)x;
   a.om = (const __bf16*)om;
   a.dy = (const __bf16*)dy;
   a.w = (const __bf16*)w_t;
-  a.dx32 = dx32;
+  a.dx = (__bf16*)dx;
   a.dom = (__bf16*)dom;
   a.xcs = xcs;
   a.omcs = omcs;
   a.dycs = dycs;
+  a.dxcs = dxcs;
   a.domcs = domcs;
   a.N = N;
   a.H = H;
@@ -707,9 +877,16 @@ extern "C" int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs
   a.Cout = Cout;
   a.x_bytes = (int)((long)N * H * W * xcs * 2);
   a.w_bytes = 9 * C * Cout * 2;
-  const int blocks = N * cdiv(H, BT) * cdiv(W, BT);
-  static const int occ = getenv("ADR_DCN_BWD_OCC") ? atoi(getenv("ADR_DCN_BWD_OCC")) : 2;
-  if (occ == 1) hipLaunchKernelGGL(dcn_bwd_kernel<1>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
-  else hipLaunchKernelGGL(dcn_bwd_kernel<2>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
-  return check_launch("adr_dcn_bwd_bf16");
+  hipStream_t s = (hipStream_t)stream;
+  const int blocks = N * cdiv(H, GT) * cdiv(W, GT);
+  static const int mode = getenv("ADR_DCN_BWD_MODE") ? atoi(getenv("ADR_DCN_BWD_MODE")) : 0;  // A/B: 1/2 skip a phase
+  if (C == 64) hipLaunchKernelGGL((dcn_bwd_kernel<1, 1, 2>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
+  else if (C == 128) hipLaunchKernelGGL((dcn_bwd_kernel<2, 2, 1>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
+  else hipLaunchKernelGGL((dcn_bwd_kernel<4, 4, 1>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
+  if (int rc = check_launch("adr_dcn_bwd_bf16")) return rc;
+  hipLaunchKernelGGL(dcn_far_apply_kernel, dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags);
+  return check_launch("adr_dcn_bwd_bf16 (far corners)");
 }
+
+/* Number of 8x8 tiles (the tile_flags length adr_dcn_bwd_bf16 needs). */
+extern "C" int adr_dcn_bwd_tiles(int N, int H, int W) { return N * cdiv(H, GT) * cdiv(W, GT); }

@@ -88,6 +88,22 @@ __global__ void __launch_bounds__(256) dcn_im2col_kernel(const T* x, int xcs, co
 // window go straight to dx32. The same pass computes d_offset / d_mask_logit from the corner values (DPP wave
 // sums). All loads of a tap group are unconditional at clamped addresses (masked afterwards), so they are in
 // flight together instead of each waiting behind a branch.
+__device__ __forceinline__ float ld_coh(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_coh(const __bf16* p) {
+  const unsigned short b = __hip_atomic_load(reinterpret_cast<const unsigned short*>(p), __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+  return __uint_as_float((unsigned)b << 16);
+}
+__device__ __forceinline__ void st_coh(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_coh(__bf16* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned short*>(p), __builtin_bit_cast(unsigned short, (__bf16)v),
+                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 constexpr int DCN_SL = 10;             // strip length (rows per wave; 10 beat 20 and 40 by 0.1 / 0.2 ms per step)
 constexpr int DCN_WIN = 7;             // window rows / columns (pixel +-3)
 constexpr int DCN_CC = 64;             // channels per pass (= lanes)
@@ -191,13 +207,16 @@ __global__ void __launch_bounds__(256) dcn_col2im_kernel(const T* x, int xcs, co
           }
           const float spy = wave_sum_dpp(gm * sy), spx = wave_sum_dpp(gm * sx), smk = wave_sum_dpp(g[u] * val);
           if (lane == 0) {
+            // partial sums carried across channel chunks through dom itself: device-coherent loads / stores, so
+            // the read-back of the previous chunk's value cannot hit a stale vector-L1 line (C >= 256 with far
+            // corners lost updates that way)
             const bool first = c0 == 0, last = c0 + DCN_CC >= C;
-            const float a = first ? 0.f : to_f(d[2 * t]), b = first ? 0.f : to_f(d[2 * t + 1]);
-            d[2 * t] = from_f<T>(a + spy);
-            d[2 * t + 1] = from_f<T>(b + spx);
+            const float a = first ? 0.f : ld_coh(d + 2 * t), b = first ? 0.f : ld_coh(d + 2 * t + 1);
+            st_coh(d + 2 * t, a + spy);
+            st_coh(d + 2 * t + 1, b + spx);
             // d mask logit: raw channel sum across chunks, times sigmoid'(logit) on the last chunk
-            const float e = (first ? 0.f : to_f(d[18 + t])) + smk;
-            d[18 + t] = from_f<T>(last ? e * m[u] * (1.f - m[u]) : e);
+            const float e = (first ? 0.f : ld_coh(d + 18 + t)) + smk;
+            st_coh(d + 18 + t, last ? e * m[u] * (1.f - m[u]) : e);
           }
         }
       }
