@@ -222,6 +222,54 @@ def stage_overhead(model, tr, batch, bs, steps=30):
             "ms_per_step_staged": round(st, 3), "overhead": round(st / un - 1, 4), "steps": steps}
 
 
+def augment_bench(bs, img, dev, reps=5):
+    """The training augmentation chain (data/augment.py v8_transforms, default hyp) on a synthetic dataset: host side
+    (draws, labels, plans) per batch and the fused GPU render (adr_augment_u8) per batch, HIP events on its stream."""
+    import random
+    from types import SimpleNamespace
+
+    import numpy as np
+    import torch
+
+    from adrefine.data.augment import Format, collate_fn, render, v8_transforms
+    from adrefine.data.synthetic import AugSourceDataset
+
+    hyp = SimpleNamespace(mosaic=1.0, degrees=0.0, translate=0.1, scale=0.5, shear=0.0, perspective=0.0, flipud=0.0,
+                          fliplr=0.5, hsv_h=0.015, hsv_s=0.7, hsv_v=0.4, mixup=0.0, copy_paste=0.0,
+                          copy_paste_mode="flip", bgr=0.0)
+    ds = AugSourceDataset(2 * bs, img, seed=4)
+    T = v8_transforms(ds, img, hyp)
+    T.append(Format(bbox_format="xywh", normalize=True, batch_idx=True, bgr=0.0))
+    random.seed(0)
+    np.random.seed(0)
+    host, kern = [], []
+    out = torch.empty(bs, 3, img, img, dtype=torch.uint8, device=dev)
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        samples = [T(ds.get_image_and_label(i % len(ds))) for i in range(bs)]
+        t1 = time.perf_counter()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        plans = [smp["img"] for smp in samples]
+        render(plans, dev, out=out)  # uploads the sources, then the kernel
+        torch.cuda.synchronize()
+        e0.record()
+        render(plans, dev, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        if r:
+            host.append(t1 - t0)
+            kern.append(e0.elapsed_time(e1))
+    _ = collate_fn(samples, dev)
+    host.sort()
+    kern.sort()
+    return {"pipeline": "Mosaic(4) -> RandomPerspective(warpAffine) -> RandomHSV -> RandomFlip -> Format, default hyp; "
+                        "pixels: one adr_augment_u8 launch per batch (render incl. the H2D upload of the sources)",
+            "bs": bs, "img": img, "host_ms_per_batch": round(1000 * host[len(host) // 2], 2),
+            "render_ms_per_batch": round(kern[len(kern) // 2], 3),
+            "render_images_per_s": round(bs / (kern[len(kern) // 2] / 1000), 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -241,6 +289,7 @@ def main():
     ap.add_argument("--infer-steps", type=int, default=20)
     ap.add_argument("--scale", default="n", choices=["n", "s", "m", "l", "x"],
                     help="model scale of the 701 yaml (configs[4] = l at 1280^2, bs 16/GPU)")
+    ap.add_argument("--augment-bench", type=int, default=1, help="time the GPU training augmentation chain")
     ap.add_argument("--conv-fp8", action="store_true",
                     help="forward convs on the fp8 (e4m3) MFMA engine (configs[4]'s fp8 conv path; backward bf16)")
     args = ap.parse_args()
@@ -390,6 +439,8 @@ def main():
             "ms_per_step_events": step_stats, "ddp_staging": staging,
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3), "hipgraph": not args.no_graph,
             "inference": infer, "peak_hbm_gib": round(peak_gib, 2),
+            "augment": (augment_bench(args.bs, args.img, dev) if world == 1 and args.augment_bench and
+                        args.scale == "n" else None),
         }
         print(json.dumps(out), flush=True)
     if world > 1:

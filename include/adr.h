@@ -65,6 +65,9 @@ int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w_krs
 int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
                           int accumulate, void* stream);
 int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d);
+/* Stats rows of adr_conv2d_fwd_bf16_fin (the in-producer finalize always runs the per-tile kernels; the plain
+ * forward's 1x1 streaming kernel writes one row per block group instead). */
+int adr_conv2d_fwd_bf16_fin_stat_tiles(const adr_conv_desc* d);
 /* dx (+)= dgrad(dy, w_crsk) + addend in one launch (bf16 engine): `addend` is an NHWC view shaped like dx with
  * channel stride addend_cstride, added in the epilogue with a single rounding. Used by the fan-out gradient sink:
  * a residual add's pass-through gradient (nn/modules/block.py:354 `x + self.cv2(self.cv1(x))`, autograd's

@@ -226,3 +226,32 @@ def test_conv_bn_act_eval_fused(act, c1, c2, k, s, hw):
     assert err <= 0.015 and err_pair <= 0.02, (err, err_pair)
     assert torch.equal(y_out, y) and torch.equal(buf[:, 8:8 + c2], y)
     assert float(buf[:, :8].abs().max()) == 0 and float(buf[:, 8 + c2:].abs().max()) == 0
+
+
+@pytest.mark.parametrize("c1,c2", [(64, 64), (32, 128), (128, 64), (16, 16), (128, 256), (48, 24), (96, 32)])
+def test_conv1_streaming_bf16(c1, c2):
+    """1x1 Conv-BN-SiLU on the streaming 1x1 kernel (adr_conv.hip conv1_kernel: weights resident in LDS, the next
+    128-row tile prefetched, stats rows per block group) at a size where blocks walk several row tiles (32 x 80^2
+    rows), forward (y + BN statistics) and data gradient, against torch fp32 on the same bf16 operands."""
+    from adrefine.nn.modules import Conv
+    m = Conv(c1, c2, 1, 1)
+    rec = load_recipe_into(m)
+    m = m.cuda().train()
+    x = seeded_randn(32, c1, 80, 80, seed=15)
+    xd = to_dev(x, torch.bfloat16)
+    y = m(xd)
+    g = seeded_randn(*y.shape, seed=16)
+    y.backward(g.to("cuda", torch.bfloat16))
+    xb = x.bfloat16().float().requires_grad_(True)
+    conv = torch.nn.Conv2d(c1, c2, 1, bias=False)
+    conv.weight.data = rec["conv.weight"].bfloat16().float()
+    bn = torch.nn.BatchNorm2d(c2, eps=1e-3, momentum=0.03)
+    bn.weight.data, bn.bias.data = rec["bn.weight"].clone(), rec["bn.bias"].clone()
+    bn.running_mean.data, bn.running_var.data = rec["bn.running_mean"].clone(), rec["bn.running_var"].clone()
+    yr = torch.nn.functional.silu(bn(conv(xb)))
+    yr.backward(g.bfloat16().float())
+    rel = lambda a, b: float((a.float().cpu() - b).norm() / (b.norm() + 1e-30))  # noqa: E731
+    assert rel(y, yr.detach()) < 1e-2, rel(y, yr.detach())
+    assert rel(xd.grad, xb.grad) < 2e-2, rel(xd.grad, xb.grad)
+    assert rel(m.conv.weight.grad, conv.weight.grad) < 2e-2
+    assert rel(m.bn.running_mean, bn.running_mean) < 1e-2 and rel(m.bn.running_var, bn.running_var) < 1e-2

@@ -49,3 +49,45 @@ def train_batch(bs: int, img: int, seed: int, device, nc: int = 80, u8: bool = F
     gt = preprocess_targets(lab["batch_idx"], lab["cls"], lab["bboxes"], bs, (img, img)).to(device)
     im = images_u8(bs, img, seed=seed) if u8 else images(bs, img, seed=seed)
     return {"img": im.to(device), "gt": gt}, lab
+
+
+class AugSourceDataset:
+    """Synthetic stand-in for a training dataset under augmentation (the reference dataset interface the mix
+    transforms use: buffer, get_image_and_label, __len__; data/base.py:290-301): n BGR uint8 images with their long
+    side at imgsz (as BaseDataset.load_image leaves them) and 1-8 normalised xywh boxes each."""
+
+    SHAPES = [(1.0, 0.75), (0.625, 1.0), (1.0, 1.0), (0.78, 1.0), (1.0, 0.5625), (1.0, 0.906), (0.5, 1.0),
+              (0.875, 0.875)]
+
+    def __init__(self, n: int, imgsz: int, seed: int = 0):
+        import numpy as np
+
+        from .instance import Instances
+        self._I = Instances
+        g = torch.Generator().manual_seed(seed)
+        self.items = []
+        for i in range(n):
+            fh, fw = self.SHAPES[i % len(self.SHAPES)]
+            h, w = max(8, int(round(imgsz * fh))), max(8, int(round(imgsz * fw)))
+            img = torch.randint(0, 256, (h, w, 3), generator=g, dtype=torch.uint8).numpy()
+            k = int(torch.randint(1, 9, (1,), generator=g))
+            ctr = 0.1 + 0.8 * torch.rand(k, 2, generator=g)
+            wh = torch.minimum(0.05 + 0.45 * torch.rand(k, 2, generator=g), 2 * torch.minimum(ctr, 1 - ctr))
+            self.items.append({"img": img, "cls": torch.randint(0, 80, (k, 1), generator=g).float().numpy(),
+                               "bboxes": torch.cat((ctr, wh), 1).numpy().astype(np.float32)})
+        self.imgsz = imgsz
+        self.buffer = list(range(n))
+        self.data = {"flip_idx": []}
+        self.use_keypoints = False
+
+    def __len__(self):
+        return len(self.items)
+
+    def get_image_and_label(self, i):
+        import numpy as np
+        it = self.items[i]
+        h, w = it["img"].shape[:2]
+        return {"im_file": f"syn{i}.jpg", "ori_shape": (h, w), "resized_shape": (h, w), "ratio_pad": (1.0, 1.0),
+                "img": it["img"], "cls": it["cls"].copy(),
+                "instances": self._I(it["bboxes"].copy(), np.zeros((0, 1000, 2), dtype=np.float32), None,
+                                     bbox_format="xywh", normalized=True)}

@@ -1040,8 +1040,8 @@ class Conv2dFn(torch.autograd.Function):
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, ycs, dtype)
         stats = None
         if want_stats:
-            tiles = (lib.adr_conv2d_fwd_bf16_stat_tiles if _engine2(d, d.c) else lib.adr_conv2d_fwd_stat_tiles)(
-                ctypes.byref(d))
+            tiles = ((lib.adr_conv2d_fwd_bf16_fin_stat_tiles if bnfin is not None else lib.adr_conv2d_fwd_bf16_stat_tiles)
+                     if _engine2(d, d.c) else lib.adr_conv2d_fwd_stat_tiles)(ctypes.byref(d))
             stats = torch.empty(tiles * 2 * K, dtype=torch.float32, device=x.device)
         bf = b.detach().float().contiguous() if b is not None else None
         # fp8 for the Conv-BN-act convs only: biased nn.Conv2d rows (the heads' output projections: logits, box

@@ -126,7 +126,8 @@ _NONSTATUS = {"adr_abi_version", "adr_conv2d_fwd_stat_tiles", "adr_conv2d_fwd_bf
               "adr_opt_chunk_size", "adr_dcn_wgrad_bf16_splits", "adr_gn_fused_supported",
               "adr_fp8_amax_blocks", "adr_conv2d_fp8_supported", "adr_conv2d_fwd_fp8_stat_tiles",
               "adr_dwconv_fwd_act_supported", "adr_fin_counters_needed", "adr_conv2d_fwd_bf16_col_tiles",
-              "adr_conv2d_bf16_xf_reuse", "adr_augment_desc_size", "adr_dcn_bwd_tiles"}
+              "adr_conv2d_bf16_xf_reuse", "adr_augment_desc_size", "adr_dcn_bwd_tiles",
+              "adr_conv2d_fwd_bf16_fin_stat_tiles"}
 _ = _NONSTATUS
 
 lib = _Lib()

@@ -546,6 +546,175 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// 1x1 / stride-1 / unpadded contractions with a short reduction (C <= 128), FWD and stride-1 DGRAD: streaming
+// GEMM. These convs move ~256 bytes per output row and do almost no math, so the per-tile kernel above is bound by
+// load latency: one short K-step per tile leaves nothing to hide its gather behind (~0.3 of HBM peak). Here a block
+// keeps its column tile's weights in LDS and walks a strided sequence of 128-row tiles: the next tile's rows are
+// in flight (registers) while the current tile's MFMAs, epilogue and stores run. The MFMA produces C^T (weights as
+// the A operand), so a lane holds four consecutive columns of one row and the output image is written to LDS with
+// 8-byte stores. BatchNorm partial sums accumulate across the block's tiles: the stats rows are per block group
+// (adr_conv2d_fwd_bf16_stat_tiles), still reduced in a fixed order.
+typedef __attribute__((ext_vector_type(2))) unsigned int u32x2c;
+
+template <int BN, int MODE, int KT>
+__device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
+  static_assert(MODE == CV_FWD || MODE == CV_DGRAD, "conv1: FWD or stride-1 DGRAD");
+  constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
+  constexpr int WROWS = CBM / WAVES_M, WCOLS = BN / WAVES_N;
+  constexpr int TM = WROWS / 16, TN = WCOLS / 16;
+  constexpr int KP = KT + 8;                       // A / B row pitch (elements)
+  constexpr int CPR_A = KT / 8;                    // 16-byte chunks per A row
+  constexpr int A_CH = CBM * CPR_A / 256;          // A chunks per thread
+  constexpr int B_TOT = BN * CPR_A, B_CH = (B_TOT + 255) / 256;
+  constexpr int OPITCH = BN + 8;
+  constexpr int CPR = BN / 8, RPP = 256 / CPR;     // output: 16-byte chunks per row, rows per pass
+  constexpr int SMEM_A = CBM * KP, SMEM_B = BN * KP, SMEM_O = CBM * OPITCH;
+  constexpr int SMEM_BYTES = 2 * (SMEM_A + SMEM_B + SMEM_O) > 2 * RPP * BN * 4 ? 2 * (SMEM_A + SMEM_B + SMEM_O)
+                                                                                : 2 * RPP * BN * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[SMEM_BYTES];
+  __bf16* As = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* Bs = As + SMEM_A;
+  __bf16* Os = Bs + SMEM_B;
+  float (*red)[RPP][BN] = reinterpret_cast<float (*)[RPP][BN]>(lds_raw);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WAVES_N, wn = wave % WAVES_N;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int grp = bid / a.ntiles, nt = bid % a.ntiles;
+  const int n0 = nt * BN;
+  const long Mrows = (long)a.n * a.rh * a.rw;
+  const int mtiles = (int)((Mrows + CBM - 1) / CBM);
+  constexpr unsigned OOR = 0x7FFFFFF0u;
+  const __amdgpu_buffer_rsrc_t src_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, a.src_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, a.wt_bytes, 0x00020000);
+  const int kc = tid % CPR_A;                      // this thread's reduction chunk (same for all its A / B chunks)
+  const bool kok = kc * 8 < a.ktot;
+
+  // weights of the column tile, once
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) {
+    const int q = tid + 256 * i, row = q / CPR_A;
+    if (q < B_TOT) {
+      const bool ok = kok && n0 + row < a.N;
+      st16(&Bs[row * KP + kc * 8], __builtin_amdgcn_raw_buffer_load_b128(
+                                      wt_rs, ok ? (unsigned)((n0 + row) * a.ktot + kc * 8) * 2u : OOR, 0, 0));
+    }
+  }
+  u32x4 ra[A_CH];
+  auto load = [&](int mt) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const long m = (long)mt * CBM + (tid / CPR_A) + (256 / CPR_A) * i;
+      const bool ok = kok && m < Mrows;
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, ok ? (unsigned)(m * a.scs + a.sco + kc * 8) * 2u : OOR, 0, 0);
+    }
+  };
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+  const int oc = tid % CPR, orow = tid / CPR;
+  const bool col_ok = n0 + oc * 8 < a.N;
+  const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
+  float bias4[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int col = n0 + wc0 + 16 * j + 4 * (lane >> 4) + e;
+      bias4[j][e] = (a.bias && col < a.N) ? a.bias[col] : 0.f;
+    }
+
+  int mt = grp;
+  if (mt < mtiles) load(mt);
+  for (; mt < mtiles; mt += groups) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) st16(&As[((tid / CPR_A) + (256 / CPR_A) * i) * KP + kc * 8], ra[i]);
+    __syncthreads();  // A tile (and, first time, the weights) in LDS; the previous tile's output image read out
+    if (mt + groups < mtiles) load(mt + groups);
+    f32x4 acc[TN][TM];  // C^T: rows = columns n, columns = rows m
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kk = 0; kk < KT / 32; ++kk) {
+      bf16x8 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[i] = *reinterpret_cast<const bf16x8*>(&As[(wr0 + i * 16 + (lane & 15)) * KP + kk * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[(wc0 + j * 16 + (lane & 15)) * KP + kk * 32 + 8 * (lane >> 4)]);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[j][i], 0, 0, 0);
+    }
+    // lane: row wr0 + 16 i + (lane & 15), columns wc0 + 16 j + 4 (lane >> 4) .. +3
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        __bf16 v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (__bf16)(acc[j][i][e] + bias4[j][e]);
+        *reinterpret_cast<u32x2c*>(&Os[(wr0 + 16 * i + (lane & 15)) * OPITCH + wc0 + 16 * j + 4 * (lane >> 4)]) =
+            *reinterpret_cast<u32x2c*>(v);
+      }
+    __syncthreads();  // output image complete; every wave is done with the A tile
+    for (int r = orow; r < CBM; r += RPP) {
+      const long m = (long)mt * CBM + r;
+      if (m >= Mrows || !col_ok) continue;
+      u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
+      __bf16* dst = a.out + m * a.ocs + a.oco + n0 + oc * 8;
+      if (MODE == CV_DGRAD && a.addend) {
+        const u32x4 q = ld16(a.addend + m * a.adcs + n0 + oc * 8);
+        const u32x4 o = a.accumulate ? ld16(dst) : u32x4{0u, 0u, 0u, 0u};
+        const __bf16 *qv = reinterpret_cast<const __bf16*>(&q), *ov = reinterpret_cast<const __bf16*>(&o);
+        __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e] + (float)qv[e]);
+      } else if (a.accumulate) {
+        const u32x4 o = ld16(dst);
+        const __bf16* ov = reinterpret_cast<const __bf16*>(&o);
+        __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e]);
+      }
+      st16(dst, v);
+      if (a.stats) {
+        const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float f = (float)sv[e];
+          s1[e] += f;
+          s2[e] += f * f;
+        }
+      }
+    }
+  }
+  if (a.stats) {  // fixed-order reduction over the row groups of each column, one stats row per block group
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[0][orow][oc * 8 + e] = s1[e];
+      red[1][orow][oc * 8 + e] = s2[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      float x1 = 0.f, x2 = 0.f;
+      for (int g = 0; g < RPP; ++g) {
+        x1 += red[0][g][tid];
+        x2 += red[1][g][tid];
+      }
+      float* s = a.stats + (long)grp * 2 * a.N + n0 + tid;
+      s[0] = x1;
+      s[a.N] = x2;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // 3x3 / stride 1 / pad 1 convolutions (FWD, and DGRAD which is the same contraction with the taps mirrored):
 // the implicit GEMM above gathers every input pixel once per tap, i.e. nine times through L2, and its K-steps
 // are too short to hide those loads. Here a block owns a TH x TW output tile (TH*TW = 128 rows) and 64 output
@@ -773,6 +942,10 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
 // kernels keep their code and register allocation)
 template <int BN, int MODE>
 __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvArgs a) { conv_bf16_body<BN, MODE, false>(a); }
+template <int BN, int MODE, int KT>
+__global__ void __launch_bounds__(256, (KT == 64 && BN <= 64) ? 3 : 2) conv1_kernel(ConvArgs a, int groups) {
+  conv1_body<BN, MODE, KT>(a, groups);
+}
 template <int BN>
 __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_act_kernel(ConvArgs a) { conv_bf16_body<BN, CV_FWD, true>(a); }
 template <int TW, bool DG, int BN>
@@ -862,6 +1035,44 @@ static void launch_conv(int bn, dim3 grid, const ConvArgs& g, hipStream_t st) {
   }
 }
 
+static int conv1_enabled() {
+  static const int on = getenv("ADR_CONV1") ? atoi(getenv("ADR_CONV1")) : 1;  // A/B: 0 = per-tile kernel
+  return on;
+}
+// column-tile count and block groups of a conv1 launch: about one resident wave of blocks (3 or 2 per CU)
+static int conv1_groups(long rows, int ntiles, int kt, int bn) {
+  const int mtiles = cdiv(rows, CBM);
+  // resident blocks per CU (LDS: 27 / 33 / 46 / 72 KB at KT 64, 45 / 54 / 71 / 104 KB at KT 128)
+  const int occ = kt == 64 ? (bn <= 32 ? 4 : bn == 64 ? 3 : 2) : (bn <= 32 ? 3 : bn == 64 ? 2 : 1);
+  const int target = 256 * occ;
+  int g = target / ntiles;
+  if (g < 1) g = 1;
+  return g < mtiles ? g : mtiles;
+}
+
+template <int MODE>
+static void launch_conv1(int bn, int kt, long rows, ConvArgs& g, hipStream_t st) {
+  const int groups = conv1_groups(rows, g.ntiles, kt, bn);
+  const dim3 grid(groups * g.ntiles);
+#define ADR_C1(BN, KT) hipLaunchKernelGGL((conv1_kernel<BN, MODE, KT>), grid, dim3(256), 0, st, g, groups)
+  if (kt == 64) {
+    switch (bn) {
+      case 16: ADR_C1(16, 64); break;
+      case 32: ADR_C1(32, 64); break;
+      case 64: ADR_C1(64, 64); break;
+      default: ADR_C1(128, 64); break;
+    }
+  } else {
+    switch (bn) {
+      case 16: ADR_C1(16, 128); break;
+      case 32: ADR_C1(32, 128); break;
+      case 64: ADR_C1(64, 128); break;
+      default: ADR_C1(128, 128); break;
+    }
+  }
+#undef ADR_C1
+}
+
 static int conv_pick_bn(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128; }
 
 static int conv_check(const adr_conv_desc* d) {
@@ -887,6 +1098,7 @@ struct ConvPlan {
   int tw;    // > 0: conv3_kernel<tw, dgrad> (3x3 stride-1 halo tiles)
   int bn;    // else conv_bf16_kernel<bn, mode>
   int mode;  // CV_FWD / CV_DGRAD / CV_DGRAD2
+  int kt;    // > 0: conv1_kernel<bn, mode, kt> (streaming 1x1, reduction <= kt)
 };
 static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   ConvPlan p{0, 0, dgrad ? (d->stride_h == 2 ? CV_DGRAD2 : CV_DGRAD) : CV_FWD};
@@ -896,6 +1108,10 @@ static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   // better than 128-wide ones (2 waves/SIMD), at the cost of reading the A rows once per column tile (L2 hits).
   // XF kernels are single-buffered: at most 64 columns.
   p.bn = p.tw ? conv3_bn(out) : ((d->r * d->s == 1 || xf) && out > 64) ? 64 : conv_pick_bn(out);
+  p.kt = 0;
+  if (!xf && !p.tw && p.mode != CV_DGRAD2 && d->r == 1 && d->s == 1 && d->stride_h == 1 && d->pad_h == 0 &&
+      d->pad_w == 0 && red <= 128 && conv1_enabled())
+    p.kt = red <= 64 ? 64 : 128;
   return p;
 }
 
@@ -923,6 +1139,8 @@ static int xf_args(const adr_bnact_xf* xf, bool bwd, int red, int n, int sh, int
 
 using namespace adr;
 
+extern "C" int adr_conv2d_fwd_bf16_fin_stat_tiles(const adr_conv_desc* d);
+
 static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                          float* stats, int accumulate, const float* escale, const float* eshift, int eact,
                          void* stream, const adr_norm_fin* fin = nullptr, const adr_bnact_xf* xf = nullptr) {
@@ -937,7 +1155,7 @@ static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, c
   if (fin) {
     ADR_REQUIRE(stats && !bias && !accumulate && !escale && fin->kind == ADR_FIN_BN_FWD && fin->C == d->k,
                 "conv fwd fin: needs stats, no bias / accumulation, a BN forward finalize over K channels");
-    rc = fin_setup(fin, adr_conv2d_fwd_bf16_stat_tiles(d), adr_conv2d_fwd_bf16_col_tiles(d), d->n, g.fin);
+    rc = fin_setup(fin, adr_conv2d_fwd_bf16_fin_stat_tiles(d), adr_conv2d_fwd_bf16_col_tiles(d), d->n, g.fin);
     if (rc) return rc;
   }
   g.src = (const __bf16*)x; g.wt = (const __bf16*)w; g.out = (__bf16*)y; g.bias = bias; g.stats = stats;
@@ -955,6 +1173,10 @@ static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, c
   }
   const int bn = pl.bn;
   g.ntiles = cdiv(g.N, bn);
+  if (pl.kt && !fin && !escale) {
+    launch_conv1<CV_FWD>(bn, pl.kt, (long)d->n * d->ho * d->wo, g, (hipStream_t)stream);
+    return check_launch("adr_conv2d_fwd_bf16");
+  }
   dim3 grid(cdiv((long)d->n * d->ho * d->wo, CBM) * g.ntiles);
   launch_conv<CV_FWD>(bn, grid, g, (hipStream_t)stream);
   return check_launch("adr_conv2d_fwd_bf16");
@@ -1002,6 +1224,8 @@ static int conv_dgrad_impl(const adr_conv_desc* d, const void* dy, const void* w
     launch_conv<CV_DGRAD2>(bn, grid, g, st);
   } else if (pl.tw) {
     launch_conv3<true>(pl.tw, pl.bn, d, g, st);
+  } else if (pl.kt) {
+    launch_conv1<CV_DGRAD>(bn, pl.kt, (long)d->n * d->h * d->w, g, st);
   } else {
     dim3 grid(cdiv((long)d->n * d->h * d->w, CBM) * g.ntiles);
     launch_conv<CV_DGRAD>(bn, grid, g, st);
@@ -1060,9 +1284,17 @@ extern "C" int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad) {
   return nt * 100 * taps;
 }
 
+// the in-producer finalize (adr_conv2d_fwd_bf16_fin) always runs the per-tile kernels: one stats row per tile
+extern "C" int adr_conv2d_fwd_bf16_fin_stat_tiles(const adr_conv_desc* d) {
+  const ConvPlan pl = conv_plan(d, false);
+  if (pl.tw) return conv3_tiles(d, pl.tw);
+  return cdiv((long)d->n * d->ho * d->wo, CBM);
+}
+
 extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) {
   const ConvPlan pl = conv_plan(d, false);
   if (pl.tw) return conv3_tiles(d, pl.tw);
+  if (pl.kt) return conv1_groups((long)d->n * d->ho * d->wo, cdiv(d->k, pl.bn), pl.kt, pl.bn);
   return cdiv((long)d->n * d->ho * d->wo, CBM);
 }
 
@@ -1089,6 +1321,8 @@ extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, 
              dg ? XF_BWD : XF_FWD);
   else if (pl.tw)
     snprintf(buf, len, "_ZN3adr12conv3_kernelILi%dELb%dELi%dEEEvNS_8ConvArgsE", pl.tw, dg ? 1 : 0, pl.bn);
+  else if (pl.kt)
+    snprintf(buf, len, "_ZN3adr12conv1_kernelILi%dELi%dELi%dEEEvNS_8ConvArgsEi", pl.bn, pl.mode, pl.kt);
   else
     snprintf(buf, len, "_ZN3adr16conv_bf16_kernelILi%dELi%dEEEvNS_8ConvArgsE", pl.bn, pl.mode);
   return ADR_OK;

@@ -605,6 +605,7 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
 
   // ---------------- phase 2: dx of the tile's 64 input pixels ----------------
   if (mode & 2) return;
+  __syncthreads();  // the dom rows are read out of the phase-1 sums that S_t is about to overwrite
   __bf16* dyw = reinterpret_cast<__bf16*>(reg);
   __bf16* S = reinterpret_cast<__bf16*>(reg + L::P2Y);
   __bf16* Wsl = reinterpret_cast<__bf16*>(reg + L::P2Y + L::P2S);
@@ -667,6 +668,7 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
       else if (t + 1 < 9) wissue(t + 1, 0, coc);
       else if (coc + 1 < CO) wissue(0, 0, coc + 1);
       if (tid < 4) kmask[4 * ((tt + 1) & 1) + tid] = 0u;  // next tap's masks (read after two more barriers)
+      unsigned bits[4] = {0u, 0u, 0u, 0u};  // K steps (bit) with entries in each wave's destination rows
       if (tid < GK) {  // source k = tid of the tap's sub-window: its corners that land in this tile
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -679,7 +681,6 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
         const float mk = sigm((float)o[18 + t]);
         Corners c0;
         sample((float)(py - 1 + t / 3) + (float)o[2 * t], (float)(px - 1 + t % 3) + (float)o[2 * t + 1], a.H, a.W, c0);
-        unsigned bits[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int qy = c0.y0 + (q >> 1) - h0, qx = c0.x0 + (q & 1) - w0;
@@ -690,13 +691,19 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
             bits[qy >> 1] |= 1u << (tid >> 5);
           }
         }
+      }
+      // OR over the wave first (xor butterfly), then one LDS atomic per wave and destination wave: same-address
+      // LDS atomics from every lane serialise
 #pragma unroll
-        for (int w4 = 0; w4 < 4; ++w4)
-          if (bits[w4]) atomicOr(&kmask[4 * (tt & 1) + w4], bits[w4]);
+      for (int w4 = 0; w4 < 4; ++w4) {
+        unsigned b = bits[w4];
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) b |= (unsigned)__shfl_xor((int)b, o, 64);
+        if (lane == 0 && b) atomicOr(&kmask[4 * (tt & 1) + w4], b);
       }
       __syncthreads();  // S_t, masks and the W slab complete
       // G_t^T (64 co x this wave's 16 destinations) = dy_sub^T . S_t^T, skipping all-zero K steps
-      const unsigned km = kmask[4 * (tt & 1) + wave];
+      const unsigned km = (mode & 4) ? 0xFFFFFFFFu : kmask[4 * (tt & 1) + wave];
       f32x4 ga[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) ga[j] = (f32x4){0.f, 0.f, 0.f, 0.f};
