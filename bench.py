@@ -176,7 +176,7 @@ NET_FLOPS_PER_IMG = 34.6e9
 
 
 # the bf16 conv engine's fwd / dgrad kernels (incl. the Conv-BN-act XF variants)
-_CONV_TAGS = ("_ZN3adr16conv_bf16", "_ZN3adr12conv3", "_ZN3adr19conv_bf16_xf", "_ZN3adr15conv3_xf")
+_CONV_TAGS = ("_ZN3adr16conv_bf16", "_ZN3adr12conv3", "_ZN3adr12conv1", "_ZN3adr19conv_bf16_xf", "_ZN3adr15conv3_xf")
 
 
 def conv_attainable(detail, hbm_gbs, mfma_tf):
