@@ -556,7 +556,7 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
 // (adr_conv2d_fwd_bf16_stat_tiles), still reduced in a fixed order.
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2c;
 
-template <int BN, int MODE, int KT>
+template <int BN, int MODE, int KT, bool EPI = false>
 __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
   static_assert(MODE == CV_FWD || MODE == CV_DGRAD, "conv1: FWD or stride-1 DGRAD");
   constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
@@ -615,13 +615,18 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
   const int oc = tid % CPR, orow = tid / CPR;
   const bool col_ok = n0 + oc * 8 < a.N;
   const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
-  float bias4[TN][4];
+  float bias4[TN][4], es4[EPI ? TN : 1][4];  // bias, or (EPI: eval Conv-BN-act) the affine shift + bias and scale
 #pragma unroll
   for (int j = 0; j < TN; ++j)
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const int col = n0 + wc0 + 16 * j + 4 * (lane >> 4) + e;
-      bias4[j][e] = (a.bias && col < a.N) ? a.bias[col] : 0.f;
+      const bool cok = col < a.N;
+      bias4[j][e] = (a.bias && cok) ? a.bias[col] : 0.f;
+      if constexpr (EPI) {
+        es4[j][e] = cok ? a.escale[col] : 1.f;
+        bias4[j][e] += cok ? a.eshift[col] : 0.f;
+      }
     }
 
   int mt = grp;
@@ -657,7 +662,10 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
       for (int i = 0; i < TM; ++i) {
         __bf16 v[4];
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (__bf16)(acc[j][i][e] + bias4[j][e]);
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (EPI) v[e] = (__bf16)epi_act(a.eact, fmaf(acc[j][i][e], es4[j][e], bias4[j][e]));
+          else v[e] = (__bf16)(acc[j][i][e] + bias4[j][e]);
+        }
         *reinterpret_cast<u32x2c*>(&Os[(wr0 + 16 * i + (lane & 15)) * OPITCH + wc0 + 16 * j + 4 * (lane >> 4)]) =
             *reinterpret_cast<u32x2c*>(v);
       }
@@ -946,6 +954,10 @@ template <int BN, int MODE, int KT>
 __global__ void __launch_bounds__(256, (KT == 64 && BN <= 64) ? 3 : 2) conv1_kernel(ConvArgs a, int groups) {
   conv1_body<BN, MODE, KT>(a, groups);
 }
+template <int BN, int KT>
+__global__ void __launch_bounds__(256, (KT == 64 && BN <= 64) ? 3 : 2) conv1_act_kernel(ConvArgs a, int groups) {
+  conv1_body<BN, CV_FWD, KT, true>(a, groups);
+}
 template <int BN>
 __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_act_kernel(ConvArgs a) { conv_bf16_body<BN, CV_FWD, true>(a); }
 template <int TW, bool DG, int BN>
@@ -1054,7 +1066,13 @@ template <int MODE>
 static void launch_conv1(int bn, int kt, long rows, ConvArgs& g, hipStream_t st) {
   const int groups = conv1_groups(rows, g.ntiles, kt, bn);
   const dim3 grid(groups * g.ntiles);
-#define ADR_C1(BN, KT) hipLaunchKernelGGL((conv1_kernel<BN, MODE, KT>), grid, dim3(256), 0, st, g, groups)
+#define ADR_C1(BN, KT)                                                                                     \
+  do {                                                                                                     \
+    if (MODE == CV_FWD && g.escale)                                                                        \
+      hipLaunchKernelGGL((conv1_act_kernel<BN, KT>), grid, dim3(256), 0, st, g, groups);                   \
+    else                                                                                                   \
+      hipLaunchKernelGGL((conv1_kernel<BN, MODE, KT>), grid, dim3(256), 0, st, g, groups);                 \
+  } while (0)
   if (kt == 64) {
     switch (bn) {
       case 16: ADR_C1(16, 64); break;
@@ -1173,7 +1191,7 @@ static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, c
   }
   const int bn = pl.bn;
   g.ntiles = cdiv(g.N, bn);
-  if (pl.kt && !fin && !escale) {
+  if (pl.kt && !fin) {  // (escale: eval Conv-BN-act epilogue)
     launch_conv1<CV_FWD>(bn, pl.kt, (long)d->n * d->ho * d->wo, g, (hipStream_t)stream);
     return check_launch("adr_conv2d_fwd_bf16");
   }
