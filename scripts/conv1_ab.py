@@ -12,7 +12,8 @@ import adrefine.kernels as K  # noqa: E402
 from adrefine.native import lib  # noqa: E402
 
 SHAPES = [(64, 160, 160, 32, 32), (64, 80, 80, 64, 64), (64, 80, 80, 128, 64), (64, 40, 40, 128, 128),
-          (64, 160, 160, 48, 32), (64, 80, 80, 96, 64), (64, 20, 20, 256, 128), (64, 80, 80, 64, 128)]
+          (64, 160, 160, 48, 32), (64, 80, 80, 96, 64), (64, 20, 20, 256, 128), (64, 80, 80, 64, 128),
+          (16, 160, 160, 256, 128), (16, 80, 80, 256, 256), (16, 160, 160, 192, 64), (64, 40, 40, 256, 64)]
 dt = torch.bfloat16
 s = K.stream()
 tag = os.environ.get("ADR_CONV1", "1")

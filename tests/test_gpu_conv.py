@@ -228,7 +228,8 @@ def test_conv_bn_act_eval_fused(act, c1, c2, k, s, hw):
     assert float(buf[:, :8].abs().max()) == 0 and float(buf[:, 8 + c2:].abs().max()) == 0
 
 
-@pytest.mark.parametrize("c1,c2", [(64, 64), (32, 128), (128, 64), (16, 16), (128, 256), (48, 24), (96, 32)])
+@pytest.mark.parametrize("c1,c2", [(64, 64), (32, 128), (128, 64), (16, 16), (128, 256), (48, 24), (96, 32), (256, 64),
+                                   (192, 128), (256, 16)])
 def test_conv1_streaming_bf16(c1, c2):
     """1x1 Conv-BN-SiLU on the streaming 1x1 kernel (adr_conv.hip conv1_kernel: weights resident in LDS, the next
     128-row tile prefetched, stats rows per block group) at a size where blocks walk several row tiles (32 x 80^2

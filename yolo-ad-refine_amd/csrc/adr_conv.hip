@@ -546,7 +546,7 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// 1x1 / stride-1 / unpadded contractions with a short reduction (C <= 128), FWD and stride-1 DGRAD: streaming
+// 1x1 / stride-1 / unpadded contractions with a short reduction (C <= 256), FWD and stride-1 DGRAD: streaming
 // GEMM. These convs move ~256 bytes per output row and do almost no math, so the per-tile kernel above is bound by
 // load latency: one short K-step per tile leaves nothing to hide its gather behind (~0.3 of HBM peak). Here a block
 // keeps its column tile's weights in LDS and walks a strided sequence of 128-row tiles: the next tile's rows are
@@ -951,11 +951,11 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
 template <int BN, int MODE>
 __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_kernel(ConvArgs a) { conv_bf16_body<BN, MODE, false>(a); }
 template <int BN, int MODE, int KT>
-__global__ void __launch_bounds__(256, (KT == 64 && BN <= 64) ? 3 : 2) conv1_kernel(ConvArgs a, int groups) {
+__global__ void __launch_bounds__(256, KT == 256 ? 1 : (KT == 64 && BN <= 64) ? 3 : 2) conv1_kernel(ConvArgs a, int groups) {
   conv1_body<BN, MODE, KT>(a, groups);
 }
 template <int BN, int KT>
-__global__ void __launch_bounds__(256, (KT == 64 && BN <= 64) ? 3 : 2) conv1_act_kernel(ConvArgs a, int groups) {
+__global__ void __launch_bounds__(256, KT == 256 ? 1 : (KT == 64 && BN <= 64) ? 3 : 2) conv1_act_kernel(ConvArgs a, int groups) {
   conv1_body<BN, CV_FWD, KT, true>(a, groups);
 }
 template <int BN>
@@ -1055,7 +1055,7 @@ static int conv1_enabled() {
 static int conv1_groups(long rows, int ntiles, int kt, int bn) {
   const int mtiles = cdiv(rows, CBM);
   // resident blocks per CU (LDS: 27 / 33 / 46 / 72 KB at KT 64, 45 / 54 / 71 / 104 KB at KT 128)
-  const int occ = kt == 64 ? (bn <= 32 ? 4 : bn == 64 ? 3 : 2) : (bn <= 32 ? 3 : bn == 64 ? 2 : 1);
+  const int occ = kt == 256 ? 1 : kt == 64 ? (bn <= 32 ? 4 : bn == 64 ? 3 : 2) : (bn <= 32 ? 3 : bn == 64 ? 2 : 1);
   const int target = 256 * occ;
   int g = target / ntiles;
   if (g < 1) g = 1;
@@ -1080,12 +1080,18 @@ static void launch_conv1(int bn, int kt, long rows, ConvArgs& g, hipStream_t st)
       case 64: ADR_C1(64, 64); break;
       default: ADR_C1(128, 64); break;
     }
-  } else {
+  } else if (kt == 128) {
     switch (bn) {
       case 16: ADR_C1(16, 128); break;
       case 32: ADR_C1(32, 128); break;
       case 64: ADR_C1(64, 128); break;
       default: ADR_C1(128, 128); break;
+    }
+  } else {  // KT 256: column tiles of at most 64 (LDS)
+    switch (bn) {
+      case 16: ADR_C1(16, 256); break;
+      case 32: ADR_C1(32, 256); break;
+      default: ADR_C1(64, 256); break;
     }
   }
 #undef ADR_C1
@@ -1128,8 +1134,8 @@ static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   p.bn = p.tw ? conv3_bn(out) : ((d->r * d->s == 1 || xf) && out > 64) ? 64 : conv_pick_bn(out);
   p.kt = 0;
   if (!xf && !p.tw && p.mode != CV_DGRAD2 && d->r == 1 && d->s == 1 && d->stride_h == 1 && d->pad_h == 0 &&
-      d->pad_w == 0 && red <= 128 && conv1_enabled())
-    p.kt = red <= 64 ? 64 : 128;
+      d->pad_w == 0 && red <= (dgrad && p.bn <= 64 ? 256 : 128) && conv1_enabled())
+    p.kt = red <= 64 ? 64 : red <= 128 ? 128 : 256;  // KT 256 (1 block per CU) measured a gain for DGRAD only
   return p;
 }
 
