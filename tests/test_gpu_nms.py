@@ -80,3 +80,31 @@ def test_nms_rejects_cpu_and_unsupported():
         ops.non_max_suppression(pred)  # CPU tensor: no fallback
     with pytest.raises(NotImplementedError):
         ops.non_max_suppression(pred.cuda(), multi_label=True, agnostic=True)
+
+
+@pytest.mark.parametrize("layout", ["direct", "scanned"])
+@pytest.mark.parametrize("conf,multi,kw", [(0.25, False, {}), (0.001, True, {}), (0.001, True, {"max_nms": 3000}),
+                                           (0.05, False, {"agnostic": True}), (0.001, False, {"max_nms": 2000})])
+def test_nms_persistent_matches_chain(monkeypatch, layout, conf, multi, kw):
+    """The single persistent launch (default) in both bucket layouts against the six-kernel chain
+    (ADR_NMS_MODE=chain) on a full-size batch (8 x 8400 anchors x 80 classes): identical rows, also when the
+    workspace holds another shape's data and when a direct launch skips its cursor-zeroing pass (second call, same
+    shape); the grid barrier never timed out."""
+    ops = _ops()
+    if layout == "scanned":
+        monkeypatch.setenv("ADR_NMS_DIRECT", "0")
+    pred = synthetic_predictions(8, 8400, 80, 640, seed=11).cuda()
+    out_p, n_p = ops.non_max_suppression_padded(pred, conf, 0.7, multi_label=multi, **kw)
+    ops.non_max_suppression_padded(pred[:3, :, :1000].contiguous(), 0.001, 0.5, multi_label=True)  # other shape
+    out_p2, n_p2 = ops.non_max_suppression_padded(pred, conf, 0.7, multi_label=multi, **kw)
+    out_p3, n_p3 = ops.non_max_suppression_padded(pred, conf, 0.7, multi_label=multi, **kw)  # record reused
+    torch.cuda.synchronize()
+    ctl = ops._WS[pred.device][:64].view(torch.int32).cpu()
+    assert int(ctl[2]) == 0, "grid barrier timed out"
+    assert int(ctl[6]) == (1 if layout == "direct" else 0), "cursor record"
+    monkeypatch.setenv("ADR_NMS_MODE", "chain")
+    out_c, n_c = ops.non_max_suppression_padded(pred, conf, 0.7, multi_label=multi, **kw)
+    assert int(n_c.sum()) > 0
+    for o, n in ((out_p, n_p), (out_p2, n_p2), (out_p3, n_p3)):
+        assert torch.equal(n, n_c)
+        assert torch.equal(o, out_c)

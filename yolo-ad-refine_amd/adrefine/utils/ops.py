@@ -1,7 +1,7 @@
 """Post-processing on the device — drop-in for the reference's ultralytics/utils/ops.py:163-312
 `non_max_suppression` (the detect predict/val callers: models/yolo/detect/predict.py:25,
-models/yolo/detect/val.py:94). The whole batch runs in one HIP pass (adr_nms: candidate extraction, max_nms
-radix select, per-class greedy NMS, max_det merge); the only host sync is reading the per-image counts to
+models/yolo/detect/val.py:94). The whole batch runs in one persistent HIP launch (adr_nms: candidate
+extraction, max_nms radix select, per-class greedy NMS, max_det merge, separated by grid barriers); the only host sync is reading the per-image counts to
 split the padded result into the reference's list of (n, 6) tensors."""
 from __future__ import annotations
 
@@ -16,9 +16,11 @@ _WS = {}
 
 
 def _workspace(device, nbytes):
+    """adr_nms keeps its grid barrier's control words in the first 64 bytes of the workspace: zero on first use
+    (the buffer is zero-filled when (re)allocated) and left zero by every call."""
     ws = _WS.get(device)
     if ws is None or ws.numel() < nbytes:
-        ws = torch.empty(nbytes, dtype=torch.uint8, device=device)
+        ws = torch.zeros(nbytes, dtype=torch.uint8, device=device)
         _WS[device] = ws
     return ws
 
