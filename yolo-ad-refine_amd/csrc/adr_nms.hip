@@ -705,23 +705,44 @@ struct NmspLds {
   int wsum[NMSP_WAVES];
   unsigned long long bcast;
   unsigned long long supw;              // P2 tile: candidates suppressed by earlier tiles' kept boxes
+  unsigned long long mt[64];            // P2 tile: per candidate, the earlier in-tile candidates overlapping it
   int sel[2];
   int cnt;
 };
 
-// ascending bitonic sort of sk[0..n) (n a power of two) by the workgroup
+// ascending bitonic sort of sk[0..n) (n a power of two) by the workgroup, one compare-exchange pair per thread and
+// step; up to 128 keys wave 0 sorts alone (no workgroup barriers between steps)
 __device__ void nmsp_bitonic(unsigned long long* sk, int n) {
+  if (n <= 128) {
+    if (threadIdx.x < 64) {
+      const int t = threadIdx.x;
+      for (int size = 2; size <= n; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          const int i = (t / stride) * 2 * stride + (t % stride), j = i + stride;
+          if (j < n) {
+            const bool up = (i & size) == 0;
+            const unsigned long long x = sk[i], y = sk[j];
+            if ((x > y) == up) {
+              sk[i] = y;
+              sk[j] = x;
+            }
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        }
+    }
+    __syncthreads();
+    return;
+  }
   for (int size = 2; size <= n; size <<= 1)
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int i = threadIdx.x; i < n; i += NMSP_THREADS) {
-        const int j = i ^ stride;
-        if (j > i) {
-          const bool up = (i & size) == 0;
-          const unsigned long long x = sk[i], y = sk[j];
-          if ((x > y) == up) {
-            sk[i] = y;
-            sk[j] = x;
-          }
+      for (int t = threadIdx.x; t < n / 2; t += NMSP_THREADS) {
+        const int i = (t / stride) * 2 * stride + (t % stride), j = i + stride;
+        const bool up = (i & size) == 0;
+        const unsigned long long x = sk[i], y = sk[j];
+        if ((x > y) == up) {
+          sk[i] = y;
+          sk[j] = x;
         }
       }
       __syncthreads();
@@ -844,6 +865,56 @@ __device__ void nmsp_select(const NmsP& p, NmspLds& L, int b, int total) {
   if (tid == 0) p.thr[b] = prefix;
 }
 
+// the k-th smallest of the n (> k) distinct keys keys[0..n) in LDS (outside the histogram's first 16 KiB of L.sk)
+__device__ unsigned long long nmsp_kth_lds(const unsigned long long* keys, int n, int k, NmspLds& L) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int* hist = reinterpret_cast<int*>(L.sk);
+  unsigned long long prefix = 0ull, mask = 0ull;
+  int need = k;
+  for (int hi = 64; hi > 0;) {
+    const int w = hi < SEL_W ? hi : SEL_W, shift = hi - w;
+    for (int i = tid; i < SEL_BINS; i += NMSP_THREADS) hist[i] = 0;
+    __syncthreads();
+    for (int i0 = wave * 64; i0 < n; i0 += NMSP_THREADS) {
+      const int i = i0 + lane;
+      const unsigned long long v = i < n ? keys[i] : ~0ull;
+      const bool in = i < n && (v & mask) == prefix;
+      const int d = (int)(v >> shift) & ((1 << w) - 1);
+      unsigned long long left = __ballot(in);
+      while (left) {
+        const int lead = __builtin_ctzll(left);
+        const int d0 = __shfl(d, lead, 64);
+        const unsigned long long mm = __ballot(in && d == d0);
+        if (lane == lead) atomicAdd(&hist[d0], __popcll(mm));
+        left &= ~mm;
+      }
+    }
+    __syncthreads();
+    int loc[SEL_BINS / NMSP_THREADS], sum = 0;
+#pragma unroll
+    for (int q = 0; q < SEL_BINS / NMSP_THREADS; ++q) sum += loc[q] = hist[tid * (SEL_BINS / NMSP_THREADS) + q];
+    int acc = nmsp_block_scan(sum, L.wsum);
+    if (acc < need && need <= acc + sum) {
+#pragma unroll
+      for (int q = 0; q < SEL_BINS / NMSP_THREADS; ++q) {
+        if (need <= acc + loc[q]) {
+          L.bcast = prefix | ((unsigned long long)(tid * (SEL_BINS / NMSP_THREADS) + q) << shift);
+          L.sel[0] = need - acc;
+          break;
+        }
+        acc += loc[q];
+      }
+    }
+    __syncthreads();
+    prefix = L.bcast;
+    need = L.sel[0];
+    mask |= (unsigned long long)((1 << w) - 1) << shift;
+    hi = shift;
+    __syncthreads();
+  }
+  return prefix;
+}
+
 // Greedy NMS over the sorted bucket L.sk[0..n) by the whole workgroup, 64 candidates (one per lane) per tile, with
 // the same survivors as torchvision's sequential scan: a candidate is dropped iff an earlier KEPT box overlaps it
 // by more than iou. Per tile: (1) every wave tests the tile against its share of the kept boxes of earlier tiles;
@@ -871,6 +942,7 @@ __device__ int nmsp_greedy(const NmsP& p, NmspLds& L, int b, int c, int item, in
     }
     const float area = (q2 - q0) * (q3 - q1);
     if (tid == 0) L.supw = 0ull;
+    if (tid < 64) L.mt[tid] = 0ull;
     __syncthreads();
     bool sup = !live;
     for (int k = wave; k < nk; k += NMSP_WAVES) {
@@ -885,10 +957,9 @@ __device__ int nmsp_greedy(const NmsP& p, NmspLds& L, int b, int c, int item, in
     }
     const unsigned long long sm = __ballot(sup);
     if (lane == 0 && sm) atomicOr(&L.supw, sm);
-    __syncthreads();
-    if (wave == 0) {
-      unsigned long long M = 0ull;  // earlier in-tile candidates overlapping this one
-      for (int j = 0; j < 63; ++j) {
+    {  // in-tile overlap bits: wave w tests the earlier candidates j = w, w + 16, ...
+      unsigned long long M = 0ull;
+      for (int j = wave; j < 63; j += NMSP_WAVES) {
         const float o0 = __shfl(q0, j, 64), o1 = __shfl(q1, j, 64), o2 = __shfl(q2, j, 64), o3 = __shfl(q3, j, 64);
         const float aj = __shfl(area, j, 64);
         if (j < lane && live) {
@@ -900,6 +971,11 @@ __device__ int nmsp_greedy(const NmsP& p, NmspLds& L, int b, int c, int item, in
           if (ovr > a.iou) M |= 1ull << j;
         }
       }
+      if (M) atomicOr(&L.mt[lane], M);
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const unsigned long long M = L.mt[lane];  // earlier in-tile candidates overlapping this one
       unsigned long long alive = ~L.supw & __ballot(live), keptm = 0ull;
       int room = a.max_det - nk;
       while (alive && room > 0) {
@@ -1030,78 +1106,69 @@ __global__ void __launch_bounds__(NMSP_THREADS) nms_persistent_kernel(NmsP p) {
   nmsp_grid_sync(ctl);
   if (p.stop == 3) return;
 
-  // P3 merge per image (workgroup b): the groups' kept lists gathered into LDS and sorted by key; the first max_det
-  // keys are the output rows. More kept keys than LDS holds: one wave merges the list heads (lane g & 63 owns g).
+  // P3 merge per image (workgroup b): the groups' kept lists are gathered into LDS in batches that fit; whenever
+  // more than max_det keys are held, an LDS radix select keeps the max_det smallest. The survivors, sorted, are the
+  // output rows (the max_det smallest keys over all kept lists, i.e. the reference's final order and cut).
   for (int b = blockIdx.x; b < B; b += gridDim.x) {
     const long kb0 = (long)b * ng * a.max_det;
+    unsigned long long* buf = L.sk + SEL_BINS / 2;  // SEL_CAP keys after the select histogram
+    unsigned long long* tmp = L.sk;                 // <= max_det survivors (histogram space, free after a select)
     const int c = tid < ng ? a.nkept[b * ng + tid] : 0;
     const int off = nmsp_block_scan(c, L.wsum);
     if (tid < ng) L.head[tid] = off;
-    if (tid == ng - 1) L.sel[0] = off + c;
+    if (tid == ng - 1) L.head[ng] = off + c;
     __syncthreads();
-    const int total = L.sel[0];
-    int nout = 0;
-    if (total <= NMS_SORT_CAP) {
-      for (int g = tid >> 6; g < ng; g += NMSP_WAVES) {
-        const int nk = (g + 1 < ng ? L.head[g + 1] : total) - L.head[g];
-        for (int i = lane; i < nk; i += 64) L.sk[L.head[g] + i] = p.kept[kb0 + (long)g * a.max_det + i];
+    int run = 0;
+    for (int g = 0; g < ng;) {
+      int g2 = g + 1;  // groups [g, g2) fit after the run (one group holds <= max_det <= SEL_CAP - max_det keys)
+      while (g2 < ng && run + L.head[g2 + 1] - L.head[g] <= SEL_CAP) ++g2;
+      for (int gg = g + (tid >> 6); gg < g2; gg += NMSP_WAVES) {
+        const int nk = L.head[gg + 1] - L.head[gg];
+        unsigned long long* dst = buf + run + L.head[gg] - L.head[g];
+        for (int i = lane; i < nk; i += 64) dst[i] = p.kept[kb0 + (long)gg * a.max_det + i];
       }
-      int n = 1;
-      while (n < total) n <<= 1;
-      for (int i = total + tid; i < n; i += NMSP_THREADS) L.sk[i] = ~0ull;
+      int n = run + L.head[g2] - L.head[g];
       __syncthreads();
-      nmsp_bitonic(L.sk, n);
-      nout = total < a.max_det ? total : a.max_det;
-      for (int r = tid; r < nout; r += NMSP_THREADS) {
-        const unsigned long long v = L.sk[r];
-        const int key = (int)(unsigned)v;
-        float bx[4];
-        box_of_anchor(a, b, key / nc, bx);
-        float* o = a.out + ((long)b * a.max_det + r) * 6;
-        o[0] = bx[0];
-        o[1] = bx[1];
-        o[2] = bx[2];
-        o[3] = bx[3];
-        o[4] = key_score(v);
-        o[5] = (float)(key % nc);
+      if (n > a.max_det) {
+        const unsigned long long T = nmsp_kth_lds(buf, n, a.max_det, L);
+        if (tid == 0) L.cnt = 0;
+        __syncthreads();
+        for (int i0 = (tid >> 6) * 64; i0 < n; i0 += NMSP_THREADS) {
+          const int i = i0 + lane;
+          const bool keep = i < n && buf[i] <= T;
+          const unsigned long long m = __ballot(keep);
+          if (!m) continue;
+          int base = 0;
+          if (lane == 0) base = atomicAdd(&L.cnt, __popcll(m));
+          base = __shfl(base, 0, 64);
+          if (keep) tmp[base + __popcll(m & ((1ull << lane) - 1ull))] = buf[i];
+        }
+        __syncthreads();
+        for (int i = tid; i < a.max_det; i += NMSP_THREADS) buf[i] = tmp[i];
+        n = a.max_det;
+        __syncthreads();
       }
-    } else if (tid < 64) {
-      for (int g = lane; g < ng; g += 64) L.head[g] = 0;
-      for (; nout < a.max_det; ++nout) {
-        unsigned long long best = ~0ull;
-        int bc = -1;
-        for (int g = lane; g < ng; g += 64) {
-          const int h = L.head[g];
-          if (h >= a.nkept[b * ng + g]) continue;
-          const unsigned long long v = p.kept[kb0 + (long)g * a.max_det + h];
-          if (v < best) {
-            best = v;
-            bc = g;
-          }
-        }
-        for (int o = 32; o > 0; o >>= 1) {
-          const unsigned long long ov = __shfl_xor(best, o, 64);
-          const int oc = __shfl_xor(bc, o, 64);
-          if (ov < best) {
-            best = ov;
-            bc = oc;
-          }
-        }
-        if (bc < 0) break;
-        if (lane == (bc & 63)) {
-          const int key = (int)(unsigned)best;
-          float bx[4];
-          box_of_anchor(a, b, key / nc, bx);
-          float* o = a.out + ((long)b * a.max_det + nout) * 6;
-          o[0] = bx[0];
-          o[1] = bx[1];
-          o[2] = bx[2];
-          o[3] = bx[3];
-          o[4] = key_score(best);
-          o[5] = (float)(key % nc);
-          L.head[bc]++;
-        }
-      }
+      run = n;
+      g = g2;
+    }
+    int n = 1;
+    while (n < run) n <<= 1;
+    for (int i = run + tid; i < n; i += NMSP_THREADS) buf[i] = ~0ull;
+    __syncthreads();
+    nmsp_bitonic(buf, n);
+    const int nout = run;
+    for (int r = tid; r < nout; r += NMSP_THREADS) {
+      const unsigned long long v = buf[r];
+      const int key = (int)(unsigned)v;
+      float bx[4];
+      box_of_anchor(a, b, key / nc, bx);
+      float* o = a.out + ((long)b * a.max_det + r) * 6;
+      o[0] = bx[0];
+      o[1] = bx[1];
+      o[2] = bx[2];
+      o[3] = bx[3];
+      o[4] = key_score(v);
+      o[5] = (float)(key % nc);
     }
     if (tid == 0) a.nout[b] = nout;
     __syncthreads();
