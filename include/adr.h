@@ -626,7 +626,8 @@ int adr_seed_advance(int64_t* seed, void* stream);
  * scores. multi != 0: every (anchor, class) with score > conf (multi_label=True, the val path); else best class.
  * agnostic: one NMS over all classes (single-label only); class_mask[nc] (nullable): the `classes` filter.
  * out (B, max_det, 6) rows x1 y1 x2 y2 conf cls in the reference's output order; nout[B] valid rows per image.
- * Requires A <= 16384, nc <= 1024, max_det <= 300. */
+ * Requires A <= 16384, nc <= 1024, max_det <= 300. One persistent launch (one 1024-thread workgroup per CU, grid
+ * barriers); ws (adr_nms_workspace bytes) must be zero-filled when first used and not shared by concurrent calls. */
 /* Pairwise IoU of xyxy boxes a (N,4) and b (M,4) -> out (N,M), eps added to the union (utils/metrics.py:52-72);
  * the validator's TP matching (models/yolo/detect/val.py:213-214). */
 int adr_box_iou(const float* a, int N, const float* b, int M, float eps, float* out, void* stream);
