@@ -256,3 +256,45 @@ def test_conv1_streaming_bf16(c1, c2):
     assert rel(xd.grad, xb.grad) < 2e-2, rel(xd.grad, xb.grad)
     assert rel(m.conv.weight.grad, conv.weight.grad) < 2e-2
     assert rel(m.bn.running_mean, bn.running_mean) < 1e-2 and rel(m.bn.running_var, bn.running_var) < 1e-2
+
+
+@pytest.mark.parametrize("act", ["sigmoid", "relu"])
+@pytest.mark.parametrize("c1,c2,hw", [(256, 128, 40), (64, 64, 20), (8, 128, 60), (128, 64, 13)])
+def test_conv_act_train_fused(act, c1, c2, hw):
+    """Training conv + bias + sigmoid / relu in one launch (K.conv_act: the activation on the fp32 accumulator in
+    the conv epilogue; backward forms the pre-activation gradient from the saved output, as torch's
+    sigmoid_backward / threshold_backward) against torch fp32 on the same bf16 operands: output within 1.5 % of
+    max |y|, dx / dw / db within 3 % of their max |value|; and against the unfused HIP pair (conv, then act)."""
+    import adrefine.kernels as K
+    torch.manual_seed(0)
+    w = (torch.randn(c2, c1, 1, 1) / c1 ** 0.5).cuda().requires_grad_()
+    b = (torch.randn(c2) * 0.5).cuda().requires_grad_()
+    x0 = seeded_randn(2, c1, hw, hw, seed=3).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    dz = seeded_randn(2, c2, hw, hw, seed=4).to("cuda", torch.bfloat16).contiguous(memory_format=torch.channels_last)
+
+    def run(fuse):
+        K.CONV_ACT_FUSE = fuse
+        try:
+            x = x0.clone().requires_grad_()
+            w.grad = b.grad = None
+            y = K.conv_act(x, w, b, 1, 0, act)
+            y.backward(dz)
+            return y.detach().float(), x.grad.float(), w.grad.clone(), b.grad.clone()
+        finally:
+            K.CONV_ACT_FUSE = True
+
+    yf, dxf, dwf, dbf = run(True)
+    yu, dxu, dwu, dbu = run(False)
+    xr = x0.float().requires_grad_()
+    wr = w.detach().to(torch.bfloat16).float().requires_grad_()
+    br = b.detach().clone().requires_grad_()
+    pre = torch.nn.functional.conv2d(xr, wr, br)
+    yr = torch.sigmoid(pre) if act == "sigmoid" else torch.relu(pre)
+    yr.backward(dz.float())
+
+    def rel(a, r):
+        return float((a - r).abs().max()) / max(float(r.abs().max()), 1e-6)
+
+    assert rel(yf, yr.detach()) <= 0.015 and rel(yf, yu) <= 0.02
+    for got, pair, ref in ((dxf, dxu, xr.grad), (dwf, dwu, wr.grad), (dbf, dbu, br.grad)):
+        assert rel(got, ref) <= 0.03 and rel(got, pair) <= 0.03, (rel(got, ref), rel(got, pair))

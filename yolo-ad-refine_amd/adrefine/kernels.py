@@ -1022,7 +1022,7 @@ class Conv2dFn(torch.autograd.Function):
     """y = conv2d(x, w) + b (dense, groups=1). Optionally also returns per-tile BN partial statistics."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, want_stats, cpad, box=None, bnfin=None):
+    def forward(ctx, x, w, b, stride, pad, want_stats, cpad, box=None, bnfin=None, act=None):
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         sink = getattr(x, "_adr_sink", None)
         ctx.sink = sink if sink is not None and sink.fits(x) else None
@@ -1046,7 +1046,7 @@ class Conv2dFn(torch.autograd.Function):
         bf = b.detach().float().contiguous() if b is not None else None
         # fp8 for the Conv-BN-act convs only: biased nn.Conv2d rows (the heads' output projections: logits, box
         # bins, offsets) stay bf16, as fp8 training recipes keep the output layers in higher precision
-        if CONV_FP8 and b is None and dtype == torch.bfloat16 and C >= _FP8_MIN_C and R * S > 1 and \
+        if CONV_FP8 and b is None and act is None and dtype == torch.bfloat16 and C >= _FP8_MIN_C and R * S > 1 and \
                 lib.adr_conv2d_fp8_supported(ctypes.byref(d)):
             if want_stats:  # the fp8 engine tiles every geometry by 128 output rows
                 stats = torch.empty(lib.adr_conv2d_fwd_fp8_stat_tiles(ctypes.byref(d)) * 2 * K, dtype=torch.float32,
@@ -1054,9 +1054,12 @@ class Conv2dFn(torch.autograd.Function):
             conv_fwd_fp8(d, xp, w, Cw, Cp, bf, yp, stats)
         elif bnfin is not None and want_stats and b is None and _engine2(d, d.c):
             conv_fwd_fin(d, xp, wp.data_ptr(), yp, stats, bnfin)  # conv + BN statistics + BN finalize
+        elif act is not None:  # act(conv + b) on the fp32 accumulator (conv_act checked the engine)
+            conv_fwd_act(d, xp, wp.data_ptr(), bf, K, act, yp)
         else:
             conv_fwd(d, xp, wp.data_ptr(), fptr(bf), yp, fptr(stats))
-        ctx.save_for_backward(x, wp, wt)
+        ctx.act = act
+        ctx.save_for_backward(x, wp, wt, y if act is not None else None)  # the activation's backward reads its output
         ctx.meta = (stride, pad, cpad, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
         if stats is None:
@@ -1067,10 +1070,14 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return None, None, None, None, None, None, None, None, None
-        x, wp, wt = ctx.saved_tensors
+            return None, None, None, None, None, None, None, None, None, None
+        x, wp, wt, z = ctx.saved_tensors
         stride, pad, cpad, wshape, has_b = ctx.meta
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+        if ctx.act is not None:  # dy of the pre-activation from the saved output (torch sigmoid/threshold_backward)
+            dz = dy.to(x.dtype) if dy.dtype != x.dtype else dy
+            dy = _new_like(z)
+            _ew(EW_ACT_BWD_OUT, _v(dy), _v(z), _v(dz), act=ACT[ctx.act])
         pend = BnXf.take(dy)  # an unwritten BN-act backward (BNActFn with xfuse): dz + coefficients
         dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
         N, C, H, W = x.shape
@@ -1098,7 +1105,7 @@ class Conv2dFn(torch.autograd.Function):
             dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
         if has_b and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, K, N, Ho * Wo, dycs, ctx.pb)
-        return dx, dw, db, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None, None
 
 
 class ConvT2dFn(torch.autograd.Function):
@@ -1501,6 +1508,52 @@ def conv2d(x, w, b=None, stride=1, pad=0, want_stats=False, cpad=0, out=None, bn
     return y, stats
 
 
+# Training conv + bias + activation in one launch for the activations whose derivative follows from the output
+# (relu, sigmoid: the AYHead gates and the cls_prob branch, head.py:135-136, 159-160, 269-270); ADR_CONV_ACT_FUSE=0
+# runs the conv, then the activation kernel
+CONV_ACT_FUSE = bool(int(__import__("os").environ.get("ADR_CONV_ACT_FUSE", "1")))
+_ONES = {}
+
+
+def _ones(n, dev):
+    t = _ONES.get((n, dev))
+    if t is None:
+        t = _ONES[(n, dev)] = torch.ones(n, dtype=torch.float32, device=dev)
+    return t
+
+
+def conv_fwd_act(d, xp, wp, bf, K, act, yp):
+    """act(conv + b) on the bf16 engine's epilogue (adr_conv2d_fwd_bf16_act with scale 1, shift = bias)."""
+    dev = torch.device("cuda", torch.cuda.current_device())
+    shift = bf if bf is not None else _zeros_f32(K, dev)
+    sym = "" if _TIMING is None else _conv2_symbol(d, False).replace("conv_bf16_kernel", "conv_bf16_act_kernel")
+    tok = _t0(sym, *_conv_work(d), _shape(d, "fwd+act") if _TIMING is not None else "")
+    lib.adr_conv2d_fwd_bf16_act(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(wp), fptr(_ones(K, dev)),
+                                fptr(shift), ACT[act], ctypes.c_void_p(yp), stream())
+    _t1(tok)
+
+
+def _zeros_f32(n, dev):
+    t = _ONES.get(("z", n, dev))
+    if t is None:
+        t = _ONES[("z", n, dev)] = torch.zeros(n, dtype=torch.float32, device=dev)
+    return t
+
+
+def conv_act(x, w, b, stride, pad, act, cpad=0):
+    """act(conv2d(x, w) + b) for act in (relu, sigmoid); fused into the conv epilogue on the bf16 engine."""
+    if CONV_ACT_FUSE and act in ("relu", "sigmoid") and x.dtype == torch.bfloat16:
+        _, _, xcs = nhwc(x)
+        N, C, H, W = x.shape
+        K, Cw, R, S = w.shape
+        (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+        d, _, _ = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, K, x.dtype)
+        if _engine2(d, d.c):
+            y, _ = Conv2dFn.apply(x, w, b, stride, pad, False, cpad, None, None, act)
+            return y
+    return ActFn.apply(conv2d(x, w, b, stride, pad, False, cpad)[0], act)
+
+
 def conv_transpose2d(x, w, b, stride, pad, out_pad):
     return ConvT2dFn.apply(x, w, b, stride, pad, out_pad)
 
@@ -1600,7 +1653,7 @@ def gn_act(y, gn: torch.nn.Module, act: str):
 # ---------------------------------------------------------------------------------------------------------
 # elementwise glue
 # ---------------------------------------------------------------------------------------------------------
-EW_COPY, EW_AXPBY, EW_MUL, EW_FMA, EW_ACT, EW_ACT_BWD, EW_ADD3 = range(7)
+EW_COPY, EW_AXPBY, EW_MUL, EW_FMA, EW_ACT, EW_ACT_BWD, EW_ADD3, EW_ACT_BWD_OUT = range(8)
 
 
 _CONSTS = {}

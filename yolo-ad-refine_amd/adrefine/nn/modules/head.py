@@ -132,8 +132,8 @@ class CoordAtt(nn.Module):
         y = K.axis_mean(x, "coord")  # (N, C, H+W, 1): [row means ; column means]
         y, _ = K.conv2d(y, self.conv1.weight, self.conv1.bias, 1, 0)
         y = K.bn_act(y, None, self.bn1, "hswish", self.training)
-        a_h = K.act(K.conv2d(y, self.conv_h.weight, self.conv_h.bias, 1, 0)[0], "sigmoid")
-        a_w = K.act(K.conv2d(y, self.conv_w.weight, self.conv_w.bias, 1, 0)[0], "sigmoid")
+        a_h = K.conv_act(y, self.conv_h.weight, self.conv_h.bias, 1, 0, "sigmoid")
+        a_w = K.conv_act(y, self.conv_w.weight, self.conv_w.bias, 1, 0, "sigmoid")
         return K.gate(xg, a_h, a_w, "coord", x.shape)
 
 
@@ -156,8 +156,9 @@ class CrossTaskInteraction(nn.Module):
         br = K.empty_act(N, 2 * C, H, W, reg_feat.dtype, reg_feat.device)
         c2r = list(K.fanout(self.cls_to_reg(cf[0], out=br[:, C:])))
         r2c = list(K.fanout(self.reg_to_cls(rf[0], out=bc[:, C:])))
-        cg = K.act(self.cls_gate[0](K.cat([cf[1], r2c[0]], out=bc)), "sigmoid")
-        rg = K.act(self.reg_gate[0](K.cat([rf[1], c2r[0]], out=br)), "sigmoid")
+        g0, h0 = self.cls_gate[0], self.reg_gate[0]
+        cg = K.conv_act(K.cat([cf[1], r2c[0]], out=bc), g0.weight, g0.bias, 1, 0, "sigmoid")
+        rg = K.conv_act(K.cat([rf[1], c2r[0]], out=br), h0.weight, h0.bias, 1, 0, "sigmoid")
         return K.fma(cf[2], r2c[1], cg), K.fma(rf[2], c2r[1], rg)
 
 
@@ -266,7 +267,7 @@ class AYHead1(nn.Module):
         r = self.DyDCNV2(reg_f, om)
         r = self.coord_attention_reg(r)
         c0, c2 = self.cls_prob_conv[0], self.cls_prob_conv[2]
-        cp = K.act(K.conv2d(fv[4], c0.weight, c0.bias, 1, 0)[0], "relu")
+        cp = K.conv_act(fv[4], c0.weight, c0.bias, 1, 0, "relu")
         cp = K.act(K.padded_conv2d(cp, c2.weight, c2.bias, 1, 1, 8), "sigmoid")  # channel 0 valid
         # both halves of the level's output row written in place into one buffer (no concat copies)
         N, _, H, W = r.shape
