@@ -298,3 +298,26 @@ def test_conv_act_train_fused(act, c1, c2, hw):
     assert rel(yf, yr.detach()) <= 0.015 and rel(yf, yu) <= 0.02
     for got, pair, ref in ((dxf, dxu, xr.grad), (dwf, dwu, wr.grad), (dbf, dbu, br.grad)):
         assert rel(got, ref) <= 0.03 and rel(got, pair) <= 0.03, (rel(got, ref), rel(got, pair))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("C,hw", [(128, 40), (64, 20), (24, 9)])
+def test_mul_pixel(dtype, C, hw):
+    """K.mul_pixel (AYHead cls_e * cls_prob, head.py:1170-1172): x * p[:, 0:1] and its backward (dx = dout * p,
+    dp[:, 0] = sum_c dout * x, the other channels of dp zero), 16-byte vector path (C = 128 / 64) and the scalar
+    path (C = 24), against torch on the same operands; dp written without a prior memset."""
+    import adrefine.kernels as K
+    x0 = seeded_randn(2, C, hw, hw, seed=1).to("cuda", dtype).contiguous(memory_format=torch.channels_last)
+    p0 = seeded_randn(2, 8, hw, hw, seed=2).to("cuda", dtype).contiguous(memory_format=torch.channels_last)
+    d0 = seeded_randn(2, C, hw, hw, seed=3).to("cuda", dtype).contiguous(memory_format=torch.channels_last)
+    x, p = x0.clone().requires_grad_(), p0.clone().requires_grad_()
+    y = K.mul_pixel(x, p)
+    y.backward(d0)
+    xr, pr = x0.float().requires_grad_(), p0.float().requires_grad_()
+    yr = xr * pr[:, 0:1]
+    yr.backward(d0.float())
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    for got, ref in ((y, yr), (x.grad, xr.grad), (p.grad, pr.grad)):
+        err = float((got.float() - ref.detach()).abs().max()) / max(float(ref.abs().max()), 1e-6)
+        assert err <= tol, err
+    assert float(p.grad[:, 1:].abs().max()) == 0.0

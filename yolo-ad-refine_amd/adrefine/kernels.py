@@ -2462,6 +2462,21 @@ def padded_conv2d(x, w, b, stride, pad, kpad):
     return PaddedConvFn.apply(x, w, b, stride, pad, kpad)
 
 
+_PBIAS = {}
+
+
+def _padded_bias(b, K, kpad, dev):
+    """fp32 bias zero-padded to kpad channels: a persistent buffer per (bias, kpad) whose padding stays zero; each
+    call copies the current K values in (one launch; the optimizer updates the bias in place between steps)."""
+    key = (None if b is None else id(b), kpad, dev)
+    hit = _PBIAS.get(key)
+    if hit is None or (b is not None and hit[0] is not b):
+        hit = _PBIAS[key] = (b, torch.zeros(kpad, dtype=torch.float32, device=dev))
+    if b is not None:
+        lib.adr_cast(F32, fptr(b.detach().float().contiguous()), F32, fptr(hit[1]), K, stream())
+    return hit[1]
+
+
 class PaddedConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, stride, pad, kpad):
@@ -2477,9 +2492,7 @@ class PaddedConvFn(torch.autograd.Function):
             zero_(wp)
             wf = w.detach().float().contiguous()
             lib.adr_pack_weight(dcode(dtype), fptr(wf), fptr(wp), K, C, C, RS, 0, stream())
-        bp = zero_(torch.empty(kpad, dtype=torch.float32, device=x.device))
-        if b is not None:
-            lib.adr_cast(F32, fptr(b.detach().float().contiguous()), F32, fptr(bp), K, stream())
+        bp = _padded_bias(b, K, kpad, x.device)
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, kpad, R, S, stride, stride, pad, pad, kpad, dtype)
         y = empty_act(N, kpad, Ho, Wo, dtype, x.device)
         conv_fwd(d, xp, wp.data_ptr(), fptr(bp), y.data_ptr())
@@ -2667,7 +2680,7 @@ class MulPixelFn(torch.autograd.Function):
         vx, vp, vd = _v(x), _v(p), _v(dout)
         N, C, H, W = x.shape
         dx = _new_like(x)
-        dp = zero_(_new_like(p))
+        dp = _new_like(p)  # adr_mul_pixel_bwd writes the whole row (channel 0, zeros after it)
         lib.adr_mul_pixel_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vp[1]), vp[2],
                               ctypes.c_void_p(vd[1]), vd[2], ctypes.c_void_p(dx.data_ptr()), C,
                               ctypes.c_void_p(dp.data_ptr()), p.shape[1], N * H * W, C, stream())

@@ -146,6 +146,24 @@ __device__ __forceinline__ float act_bwd(int act, float v) {
 // Thread -> (channel group, pixel row) mapping for 256-thread NHWC elementwise kernels: G = C / vector width
 // lanes per pixel, 256 / G pixels per block pass; the channel group is fixed for the thread's whole loop (so
 // per-channel coefficients load once) and the loop has no integer division. Host guarantees G <= 256.
+// 16-byte vector load / store of one NHWC channel chunk as fp32 (elementwise kernels)
+template <typename T> struct VecIO {
+  static constexpr int V = 16 / sizeof(T);
+  __device__ static void load(const T* p, float* f) {
+    u32x4 v = ld16(p);
+    const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+    for (int i = 0; i < V; ++i) f[i] = to_f(e[i]);
+  }
+  __device__ static void store(T* p, const float* f) {
+    u32x4 v;
+    T* e = reinterpret_cast<T*>(&v);
+#pragma unroll
+    for (int i = 0; i < V; ++i) e[i] = from_f<T>(f[i]);
+    st16(p, v);
+  }
+};
+
 struct PixLanes {
   int cg, r0, rpb;
   bool active;

@@ -9,23 +9,6 @@
 
 namespace adr {
 
-template <typename T> struct VecIO {
-  static constexpr int V = 16 / sizeof(T);
-  __device__ static void load(const T* p, float* f) {
-    u32x4 v = ld16(p);
-    const T* e = reinterpret_cast<const T*>(&v);
-#pragma unroll
-    for (int i = 0; i < V; ++i) f[i] = to_f(e[i]);
-  }
-  __device__ static void store(T* p, const float* f) {
-    u32x4 v;
-    T* e = reinterpret_cast<T*>(&v);
-#pragma unroll
-    for (int i = 0; i < V; ++i) e[i] = from_f<T>(f[i]);
-    st16(p, v);
-  }
-};
-
 // op codes for the n-ary kernel:
 //  0 copy          : o = a
 //  1 axpby         : o = ca*a + cb*b               (ca/cb device scalars, null = 1)

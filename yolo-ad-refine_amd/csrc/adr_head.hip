@@ -11,6 +11,9 @@
 //     (head.py:1181-1204, 1236-1252; block.py:63-81; tal.py:303-327).
 #include "adr_common.h"
 
+#include <cstdint>
+#include <initializer_list>
+
 namespace adr {
 
 // ---------------- DCNv2 ----------------
@@ -425,7 +428,69 @@ __global__ void __launch_bounds__(256) mul_pixel_bwd_kernel(const T* x, int xcs,
     dx[pix * ocs + c] = from_f<T>(d * pv);
   }
   s = wave_sum(s);
-  if (lane == 0) dp[pix * dpcs] = from_f<T>(s);
+  if (lane < dpcs) dp[pix * dpcs + lane] = from_f<T>(lane == 0 ? s : 0.f);  // the whole dp row (zeros after channel 0)
+}
+
+// 16-byte vector versions (C / V lanes per pixel, C / V a power of two <= 64; the pixel's lanes are adjacent in a wave)
+template <typename T>
+__global__ void __launch_bounds__(256) mul_pixel_vec_kernel(const T* x, int xcs, const T* p, int pcs, T* o, int ocs,
+                                                            long npix, int C) {
+  constexpr int V = VecIO<T>::V;
+  const PixLanes L(C / V);
+  if (!L.active) return;
+  const int c0 = L.cg * V;
+  for (long pix = (long)blockIdx.x * L.rpb + L.r0; pix < npix; pix += (long)gridDim.x * L.rpb) {
+    float fx[V], fo[V];
+    VecIO<T>::load(x + pix * xcs + c0, fx);
+    const float pv = to_f(p[pix * pcs]);
+#pragma unroll
+    for (int k = 0; k < V; ++k) fo[k] = fx[k] * pv;
+    VecIO<T>::store(o + pix * ocs + c0, fo);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) mul_pixel_bwd_vec_kernel(const T* x, int xcs, const T* p, int pcs,
+                                                                const T* dout, int dcs, T* dx, int ocs, T* dp, int dpcs,
+                                                                long npix, int C) {
+  constexpr int V = VecIO<T>::V;
+  const int G = C / V;
+  const PixLanes L(G);
+  if (!L.active) return;
+  const int c0 = L.cg * V;
+  for (long pix = (long)blockIdx.x * L.rpb + L.r0; pix < npix; pix += (long)gridDim.x * L.rpb) {
+    float fx[V], fd[V], fo[V];
+    VecIO<T>::load(x + pix * xcs + c0, fx);
+    VecIO<T>::load(dout + pix * dcs + c0, fd);
+    const float pv = to_f(p[pix * pcs]);
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      fo[k] = fd[k] * pv;
+      s += fd[k] * fx[k];
+    }
+    VecIO<T>::store(dx + pix * ocs + c0, fo);
+    for (int off = G >> 1; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+    if (L.cg < dpcs) dp[pix * dpcs + L.cg] = from_f<T>(L.cg == 0 ? s : 0.f);
+    for (int c = L.cg + G; c < dpcs; c += G) dp[pix * dpcs + c] = from_f<T>(0.f);
+  }
+}
+
+static bool mul_pixel_vec_ok(int dtype, long npix, int C, std::initializer_list<long> strides,
+                             std::initializer_list<const void*> ptrs) {
+  const int v = dtype == ADR_BF16 ? 8 : 4;
+  const int G = C / v;
+  if (C % v || G > 64 || (G & (G - 1))) return false;
+  for (long st : strides)
+    if (st % v) return false;
+  for (const void* q : ptrs)
+    if ((uintptr_t)q % 16) return false;
+  return npix > 0;
+}
+
+static int mul_pixel_grid(long npix, int G) {
+  long b = (npix + 256 / G - 1) / (256 / G);
+  return (int)(b > 32768 ? 32768 : b < 1 ? 1 : b);
 }
 
 // ---------------- eval decode ----------------
@@ -590,6 +655,16 @@ extern "C" int adr_bcast_fill(int dtype, const float* g, int gns, int gcs, float
 extern "C" int adr_mul_pixel(int dtype, const void* x, int xcs, const void* p, int pcs, void* o, int ocs, long npix,
                              int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (mul_pixel_vec_ok(dtype, npix, C, {xcs, ocs}, {x, o})) {
+    const int v = dtype == ADR_BF16 ? 8 : 4, g = mul_pixel_grid(npix, C / v);
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL(mul_pixel_vec_kernel<__bf16>, dim3(g), dim3(256), 0, st, (const __bf16*)x, xcs,
+                         (const __bf16*)p, pcs, (__bf16*)o, ocs, npix, C);
+    else
+      hipLaunchKernelGGL(mul_pixel_vec_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)x, xcs,
+                         (const float*)p, pcs, (float*)o, ocs, npix, C);
+    return check_launch("adr_mul_pixel");
+  }
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(mul_pixel_kernel<__bf16>, dim3(cdiv(npix * C, 256)), dim3(256), 0, st, (const __bf16*)x, xcs,
                        (const __bf16*)p, pcs, (__bf16*)o, ocs, npix, C);
@@ -602,6 +677,17 @@ extern "C" int adr_mul_pixel(int dtype, const void* x, int xcs, const void* p, i
 extern "C" int adr_mul_pixel_bwd(int dtype, const void* x, int xcs, const void* p, int pcs, const void* dout, int dcs,
                                  void* dx, int ocs, void* dp, int dpcs, long npix, int C, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  ADR_REQUIRE(dpcs >= 1 && dpcs <= 64, "mul_pixel_bwd: dp channel stride %d (the whole row is written)", dpcs);
+  if (mul_pixel_vec_ok(dtype, npix, C, {xcs, dcs, ocs}, {x, dout, dx})) {
+    const int v = dtype == ADR_BF16 ? 8 : 4, gv = mul_pixel_grid(npix, C / v);
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL(mul_pixel_bwd_vec_kernel<__bf16>, dim3(gv), dim3(256), 0, st, (const __bf16*)x, xcs,
+                         (const __bf16*)p, pcs, (const __bf16*)dout, dcs, (__bf16*)dx, ocs, (__bf16*)dp, dpcs, npix, C);
+    else
+      hipLaunchKernelGGL(mul_pixel_bwd_vec_kernel<float>, dim3(gv), dim3(256), 0, st, (const float*)x, xcs,
+                         (const float*)p, pcs, (const float*)dout, dcs, (float*)dx, ocs, (float*)dp, dpcs, npix, C);
+    return check_launch("adr_mul_pixel_bwd");
+  }
   dim3 g(cdiv(npix, 4));
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(mul_pixel_bwd_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)p, pcs,
