@@ -51,12 +51,11 @@ __device__ __forceinline__ void wg_xcd_block(int& bx, int& by) {
   bx = b - by * gx;
 }
 
-template <int BM, int BN>
-__global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
+template <int BM, int BN, int KU>  // KU: 32*WK-row sub-steps per k-step
+__device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a) {
   constexpr int WM = BM / 16 < 2 ? BM / 16 : 2;
   constexpr int WN = BN / 16 < 2 ? BN / 16 : 2;
   constexpr int WK = 4 / (WM * WN);
-  constexpr int KU = wg_ku(BM, BN);  // 32*WK-row sub-steps per k-step (>= ~16-32 MFMAs per wave per barrier)
   constexpr int R = 32 * WK * KU;    // reduction rows per k-step
   constexpr int WROWS = BM / WM, WCOLS = BN / WN;
   constexpr int TM = WROWS / 16, TN = WCOLS / 16;
@@ -242,6 +241,16 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
         }
       }
     }
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
+  wgrad_bf16_body<BM, BN, wg_ku(BM, BN)>(a);
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) wgrad_bf16_ku2_kernel(WgArgs a) {
+  wgrad_bf16_body<BM, BN, 2>(a);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -534,6 +543,15 @@ static bool thin_enabled() {
   return v != 0;
 }
 
+// k-step depth of the 128 x 128 tile (ADR_WG_KU=2: two 32-row sub-steps per barrier pair; A/B)
+static int wg_ku128() {
+  static const int v = [] {
+    const char* e = getenv("ADR_WG_KU");
+    return e && atoi(e) == 2 ? 2 : 1;
+  }();
+  return v;
+}
+
 static int wg_pick16(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128; }
 
 template <int BM>
@@ -542,7 +560,12 @@ static void launch_bm(int bn, dim3 grid, const WgArgs& g, hipStream_t st) {
     case 16: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 16>), grid, dim3(256), 0, st, g); break;
     case 32: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 32>), grid, dim3(256), 0, st, g); break;
     case 64: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 64>), grid, dim3(256), 0, st, g); break;
-    default: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 128>), grid, dim3(256), 0, st, g); break;
+    default:
+      if (BM == 128 && wg_ku128() == 2)
+        hipLaunchKernelGGL((wgrad_bf16_ku2_kernel<BM, 128>), grid, dim3(256), 0, st, g);
+      else
+        hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 128>), grid, dim3(256), 0, st, g);
+      break;
   }
 }
 
@@ -596,14 +619,17 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   p.bm = wg_pick16(d->k);
   p.bn = wg_pick16(d->c);
   const int wm = p.bm / 16 < 2 ? p.bm / 16 : 2, wn = p.bn / 16 < 2 ? p.bn / 16 : 2;
-  p.R = 32 * (4 / (wm * wn)) * wg_ku(p.bm, p.bn);
+  p.R = 32 * (4 / (wm * wn)) * (p.bm == 128 && p.bn == 128 ? wg_ku128() : wg_ku(p.bm, p.bn));
   const long red = (long)d->n * d->ho * d->wo;
   const long outsz = (long)d->k * d->r * d->s * d->c;
   p.tiles = cdiv(d->k, p.bm) * d->r * d->s * cdiv(d->c, p.bn);
   long s = (1024 + p.tiles - 1) / p.tiles;                  // ~4 workgroups per CU
   const long by_work = red / ((long)p.R * 8);               // >= 8 k-steps per split
+  // <= 24 MB of partials (stays in L2/MALL); weights above 1 MB (l-scale: 3x3 256->256, 1x1 512->512) get 96 MB so
+  // their splits still fill the chip (configs[4]: 145.2 -> 142.2 ms/step; the n-scale step is unchanged)
   static const long bg = part_budget("ADR_WG_PART_MB", 24);
-  const long by_bytes = bg / (outsz * 4);                   // <= 24 MB of partials (stays in L2/MALL)
+  static const bool bg_env = getenv("ADR_WG_PART_MB") != nullptr;
+  const long by_bytes = (!bg_env && outsz * 4 > (1l << 20) ? (96l << 20) : bg) / (outsz * 4);
   if (s > by_work) s = by_work;
   if (s > by_bytes) s = by_bytes;
   if (s < 1) s = 1;
