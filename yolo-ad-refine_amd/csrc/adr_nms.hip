@@ -423,6 +423,10 @@ static constexpr int NMSP_WAVES = NMSP_THREADS / 64;
 static constexpr int NMSP_MAX_GRID = 1024;
 static constexpr long NMSP_SPIN_LIMIT = 1l << 25;  // ~2 s of s_sleep: a barrier that never completes sets CTL_ERR
 static constexpr int NMSP_GB = 16;                 // class rows per batch of loads
+static constexpr int SEL_W = 12, SEL_BINS = 1 << SEL_W;        // radix-select digit width / bins
+static constexpr int SEL_CAP = NMS_SORT_CAP - SEL_BINS / 2;   // keys an LDS select holds (u64 slots after the histogram)
+static constexpr int SEL_U = 8, SEL_CH = 64 * SEL_U;
+static constexpr int HIST_W = 16, HIST_BINS = 1 << HIST_W;     // fill-time top-digit histogram (distributed select)
 enum : int {
   CTL_GEN = 1,      // barrier generation
   CTL_ERR = 2,      // a barrier wait timed out
@@ -438,8 +442,13 @@ static constexpr size_t NMSP_CTL_BYTES = CTL_WORDS * 4;
 struct NmsP {
   NmsArgs a;
   unsigned* ctl;
-  int* cur;                       // [B][ng] bucket fill cursors, then tot = cur + B * ng: [B] candidates per image
-  int* tot;
+  int* cur;                       // [B][ng] bucket fill cursors, then tot = cur + B * ng: [B] candidates per image,
+  int* tot;                       // ccur: [B] select compaction cursors, hist: [B][SEL_BINS] top-digit histograms
+  int* ccur;
+  int* hist;
+  int sel_hist;                   // an image may exceed max_nms: the fill builds the top-digit histograms
+  int* seld;                      // [B][3] select: first digit, rank within it, keys under it (-1: no select)
+  unsigned long long* comp;       // [B][SEL_CAP] keys under the first digit (distributed select)
   int* gcnt;                      // scanned: [B][ng] count cursors
   unsigned long long* cand;       // direct: [B][ng][A]; scanned: [B][cap] (bucket at offs)
   unsigned long long* thr;        // [B] max_nms threshold key (keep key <= thr)
@@ -523,6 +532,21 @@ __device__ __forceinline__ void nmsp_best(const NmsArgs& a, int b, int an, bool 
   }
 }
 
+// top-digit histogram of the wave's candidate keys (one atomic per distinct digit); the whole wave calls it
+__device__ __forceinline__ void nmsp_hist_add(const NmsP& p, int b, bool on, unsigned long long key) {
+  if (!p.sel_hist) return;
+  const int lane = threadIdx.x & 63;
+  const int d = (int)(key >> (64 - HIST_W));
+  unsigned long long left = __ballot(on);
+  while (left) {
+    const int lead = __builtin_ctzll(left);
+    const int d0 = __shfl(d, lead, 64);
+    const unsigned long long mm = __ballot(on && d == d0);
+    if (lane == lead) atomicAdd(&p.hist[(long)b * HIST_BINS + d0], __popcll(mm));
+    left &= ~mm;
+  }
+}
+
 // single-label: slot claim for the candidates of one wave (one atomic per distinct group, all issued at once)
 __device__ __forceinline__ void nmsp_put_single(const NmsP& p, int b, bool ok, int g, unsigned long long key,
                                                 unsigned long long* bucket0, long gstride, const int* offs) {
@@ -530,6 +554,7 @@ __device__ __forceinline__ void nmsp_put_single(const NmsP& p, int b, bool ok, i
   const unsigned long long below = (1ull << lane) - 1ull;
   unsigned long long left = __ballot(ok);
   if (!left) return;
+  nmsp_hist_add(p, b, ok, key);
   const int total = __popcll(left);
   int myl = 0, myr = 0, lcnt = 0;
   while (left) {
@@ -551,7 +576,7 @@ __device__ __forceinline__ void nmsp_put_single(const NmsP& p, int b, bool ok, i
 }
 
 // direct fill of the 64 anchors of chunk ch of image b
-__device__ void nmsp_fill_direct(const NmsP& p, int b, int ch) {
+__device__ __forceinline__ void nmsp_fill_direct(const NmsP& p, int b, int ch) {
   const NmsArgs& a = p.a;
   const int lane = threadIdx.x & 63, an = ch * 64 + lane;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -588,7 +613,10 @@ __device__ void nmsp_fill_direct(const NmsP& p, int b, int ch) {
     for (int j = 0; j < NMSP_GB; ++j) {
       const unsigned long long m = __shfl(mine, j, 64);
       const int bj = __shfl(base, j, 64);
-      if ((m >> lane) & 1ull) bucket0[(long)(g0 + j) * A + bj + __popcll(m & below)] = nms_key(s[j], an * nc + g0 + j);
+      const bool on = (m >> lane) & 1ull;
+      const unsigned long long key = nms_key(s[j], an * nc + g0 + j);
+      if (on) bucket0[(long)(g0 + j) * A + bj + __popcll(m & below)] = key;
+      if (m) nmsp_hist_add(p, b, on, key);
     }
   }
 #pragma unroll
@@ -597,7 +625,7 @@ __device__ void nmsp_fill_direct(const NmsP& p, int b, int ch) {
 }
 
 // scanned P0a: counts per (image, group); caches the anchor keys (single) or the per-group ballots (multi)
-__device__ void nmsp_count_scanned(const NmsP& p, int b, int ch) {
+__device__ __forceinline__ void nmsp_count_scanned(const NmsP& p, int b, int ch) {
   const NmsArgs& a = p.a;
   const int lane = threadIdx.x & 63, an = ch * 64 + lane;
   const bool valid = an < a.A;
@@ -639,7 +667,7 @@ __device__ void nmsp_count_scanned(const NmsP& p, int b, int ch) {
 }
 
 // scanned fill from the cached keys / ballots
-__device__ void nmsp_fill_scanned(const NmsP& p, int b, int ch) {
+__device__ __forceinline__ void nmsp_fill_scanned(const NmsP& p, int b, int ch) {
   const NmsArgs& a = p.a;
   const int lane = threadIdx.x & 63, an = ch * 64 + lane;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -665,7 +693,10 @@ __device__ void nmsp_fill_scanned(const NmsP& p, int b, int ch) {
     for (int j = 0; j < NMSP_GB; ++j) {
       const unsigned long long m = __shfl(mine, j, 64);
       const int bj = __shfl(base, j, 64);
-      if ((m >> lane) & 1ull) cv[bj + __popcll(m & below)] = nms_key(s[j], an * nc + g0 + j);
+      const bool on = (m >> lane) & 1ull;
+      const unsigned long long key = nms_key(s[j], an * nc + g0 + j);
+      if (on) cv[bj + __popcll(m & below)] = key;
+      if (m) nmsp_hist_add(p, b, on, key);
     }
   }
 }
@@ -753,11 +784,8 @@ __device__ void nmsp_bitonic(unsigned long long* sk, int n) {
 // Radix select on 12-bit digits from the top; histogram atomics aggregated per wave (one LDS atomic per distinct
 // digit in the wave), SEL_U keys per lane in flight. Once the keys matching the prefix fit in LDS they are
 // compacted there and the remaining digits are resolved without touching HBM.
-static constexpr int SEL_W = 12, SEL_BINS = 1 << SEL_W;
-static constexpr int SEL_CAP = NMS_SORT_CAP - SEL_BINS / 2;  // u64 slots after the int histogram
-static constexpr int SEL_U = 8, SEL_CH = 64 * SEL_U;
 
-__device__ void nmsp_select(const NmsP& p, NmspLds& L, int b, int total) {
+__device__ __forceinline__ void nmsp_select(const NmsP& p, NmspLds& L, int b, int total) {
   const NmsArgs& a = p.a;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, ng = a.ng;
   int* hist = reinterpret_cast<int*>(L.sk);
@@ -921,7 +949,7 @@ __device__ unsigned long long nmsp_kth_lds(const unsigned long long* keys, int n
 // (2) wave 0 computes the in-tile overlap bits (bit j of lane l: candidate j < l overlaps l) and (3) resolves the
 // tile in order with one ballot per kept candidate; kept boxes are appended in order. IoU arithmetic as the
 // reference: inter / (area_kept + area_candidate - inter). Returns the kept count.
-__device__ int nmsp_greedy(const NmsP& p, NmspLds& L, int b, int c, int item, int n) {
+__device__ __forceinline__ int nmsp_greedy(const NmsP& p, NmspLds& L, int b, int c, int item, int n) {
   const NmsArgs& a = p.a;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nc = a.nc;
   const unsigned long long below = (1ull << lane) - 1ull;
@@ -1011,7 +1039,7 @@ __global__ void __launch_bounds__(NMSP_THREADS) nms_persistent_kernel(NmsP p) {
   const int nch64 = cdiv_d(a.A, 64);
   const long nwaves = (long)gridDim.x * NMSP_WAVES;
   const long wave0 = (long)blockIdx.x * NMSP_WAVES + (tid >> 6);
-  const int ncur = B * ng + B;
+  const int ncur = B * ng + 2 * B + (p.sel_hist ? B * HIST_BINS : 0);  // cursors, totals, compaction, histograms
   unsigned* ctl = p.ctl;
 
   // cursors: zero unless the previous launch recorded that it left exactly these words zero
@@ -1057,7 +1085,77 @@ __global__ void __launch_bounds__(NMSP_THREADS) nms_persistent_kernel(NmsP p) {
   // P1 max_nms select (uniform decision: every workgroup reads the same totals)
   bool any_sel = false;
   for (int b = 0; b < B; ++b) any_sel |= ld_rlx(&p.tot[b]) > a.max_nms;
-  if (any_sel) {
+  if (any_sel && p.sel_hist) {
+    // distributed select: (1) per image, the digit of the max_nms-th key from the fill-time histogram
+    for (int b = blockIdx.x; b < B; b += gridDim.x) {
+      const int total = ld_rlx(&p.tot[b]);
+      if (total <= a.max_nms) {  // block-uniform
+        if (tid == 0) p.seld[3 * b] = -1;
+        continue;
+      }
+      constexpr int PER = HIST_BINS / NMSP_THREADS;  // 64 consecutive bins per thread
+      const int* hb = p.hist + (long)b * HIST_BINS + tid * PER;
+      int sum = 0;
+      for (int k = 0; k < PER; ++k) sum += ld_rlx(&hb[k]);
+      int acc = nmsp_block_scan(sum, L.wsum);
+      const int need = a.max_nms;
+      if (acc < need && need <= acc + sum) {
+        for (int k = 0; k < PER; ++k) {
+          const int c = ld_rlx(&hb[k]);
+          if (need <= acc + c) {
+            p.seld[3 * b] = tid * PER + k;
+            p.seld[3 * b + 1] = need - acc;
+            p.seld[3 * b + 2] = c;
+            break;
+          }
+          acc += c;
+        }
+      }
+    }
+    nmsp_grid_sync(ctl);
+    // (2) every wave compacts the keys under its bucket's image digit (images whose digit holds <= SEL_CAP keys)
+    for (long it = wave0; it < (long)B * ng; it += nwaves) {
+      const int b = (int)(it / ng);
+      const int d1 = ld_rlx(&p.seld[3 * b]);
+      if (d1 < 0 || ld_rlx(&p.seld[3 * b + 2]) > SEL_CAP) continue;  // wave-uniform
+      const int n = p.direct ? p.cur[it] : a.counts[it];
+      const unsigned long long* cv = p.direct ? p.cand + it * a.A : p.cand + (long)b * a.cap + a.offs[it];
+      for (int i0 = 0; i0 < n; i0 += SEL_CH) {
+        unsigned long long vv[SEL_U];
+#pragma unroll
+        for (int u = 0; u < SEL_U; ++u) vv[u] = i0 + u * 64 + lane < n ? cv[i0 + u * 64 + lane] : ~0ull;
+#pragma unroll
+        for (int u = 0; u < SEL_U; ++u) {
+          const bool in = i0 + u * 64 + lane < n && (int)(vv[u] >> (64 - HIST_W)) == d1;
+          const unsigned long long m = __ballot(in);
+          if (!m) continue;
+          int base = 0;
+          if (lane == 0) base = atomicAdd(&p.ccur[b], __popcll(m));
+          base = __shfl(base, 0, 64);
+          if (in) p.comp[(long)b * SEL_CAP + base + __popcll(m & ((1ull << lane) - 1ull))] = vv[u];
+        }
+      }
+    }
+    nmsp_grid_sync(ctl);
+    // (3) per image: the rank-th key among the compacted ones (LDS radix select); too many under the digit: the
+    // per-image select over all keys
+    for (int b = blockIdx.x; b < B; b += gridDim.x) {
+      const int d1 = ld_rlx(&p.seld[3 * b]);
+      if (d1 < 0) continue;  // block-uniform
+      const int m1 = ld_rlx(&p.seld[3 * b + 2]);
+      if (m1 > SEL_CAP) {
+        nmsp_select(p, L, b, ld_rlx(&p.tot[b]));
+        continue;
+      }
+      unsigned long long* buf = L.sk + SEL_BINS / 2;
+      for (int i = tid; i < m1; i += NMSP_THREADS) buf[i] = p.comp[(long)b * SEL_CAP + i];
+      __syncthreads();
+      const unsigned long long T = nmsp_kth_lds(buf, m1, ld_rlx(&p.seld[3 * b + 1]), L);
+      if (tid == 0) p.thr[b] = T;
+      __syncthreads();
+    }
+    nmsp_grid_sync(ctl);
+  } else if (any_sel) {
     for (int b = blockIdx.x; b < B; b += gridDim.x) {
       const int total = ld_rlx(&p.tot[b]);
       if (total > a.max_nms) nmsp_select(p, L, b, total);  // block-uniform
@@ -1218,7 +1316,10 @@ void carve_chain(NmsArgs& a, WsCarve& w, int B, int nc, int A, int multi, int ma
 
 void carve_persistent(NmsP& p, WsCarve& w, int B, int nc, int A, int multi, int max_det, bool direct) {
   const size_t cap = (size_t)A * (multi ? nc : 1);
-  p.cur = w.take<int>((size_t)B * nc + B);  // fill cursors, then per-image totals (contiguous: one record)
+  // fill cursors, per-image totals, select compaction cursors, top-digit histograms (contiguous: one record)
+  p.cur = w.take<int>((size_t)B * nc + 2 * B + (size_t)B * HIST_BINS);
+  p.seld = w.take<int>((size_t)B * 3);
+  p.comp = w.take<unsigned long long>((size_t)B * SEL_CAP);
   p.a.nkept = w.take<int>((size_t)B * nc);
   p.thr = w.take<unsigned long long>(B);
   p.kept = w.take<unsigned long long>((size_t)B * nc * max_det);
@@ -1261,6 +1362,11 @@ int nmsp_grid(int want) {
     dev_cached = dev;
   }
   return cap < want ? cap : want;
+}
+
+bool getenv_is(const char* k, const char* v) {
+  const char* e = getenv(k);
+  return e && !strcmp(e, v);
 }
 
 bool nms_chain_mode() {
@@ -1314,6 +1420,9 @@ extern "C" int adr_nms(const float* y, int B, int nc, int A, float conf, float i
   p.direct = nms_direct(B, nc, A);
   carve_persistent(p, w, B, nc, A, multi, max_det, p.direct);
   p.tot = p.cur + (size_t)B * a.ng;
+  p.ccur = p.tot + B;
+  p.hist = p.ccur + B;
+  p.sel_hist = (long)A * (multi ? a.ng : 1) > max_nms && !getenv_is("ADR_NMS_DSEL", "0");
   const long waves = (long)B * cdiv(A, 64);
   const long want = std::max<long>(cdiv(waves, NMSP_WAVES), (long)B * a.ng);
   const int grid = nmsp_grid((int)std::min<long>(want, NMSP_MAX_GRID));
