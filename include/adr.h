@@ -380,7 +380,9 @@ int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, f
  * Pooling / resampling (NHWC). Max pool k x k stride 1 pad k/2 with uint8 argmax (SPPF block.py:177-196);
  * axis means + separable gate (ELA_HSFPN block.py:1408-1424, CoordAtt head.py:671-707); adaptive average
  * pooling (block.py:1558-1581, 2455); bilinear resize align_corners=False (block.py:2459-2462).
- * Axis-mean outputs / gate inputs are [n][l][c] planes addressed as base + n*stride_n + l*C + c. */
+ * Axis-mean outputs / gate inputs are [n][l][c] planes addressed as base + n*stride_n + l*C + c. adr_gate_bwd's
+ * zero_other (CoordAtt: both gate gradients span H + W rows): also write zeros to the rows the gate does not read
+ * (dah rows H.., daw rows ..H of the (H + W)-row tensors; daw passed at row H as usual). */
 int adr_maxpool(int dtype, const void* x, int xcs, void* y, int ycs, uint8_t* arg, int N, int H, int W, int C, int k,
                 void* stream);
 int adr_maxpool_bwd(int dtype, const void* dy, int dcs, const uint8_t* arg, void* dx, int ocs, int N, int H, int W,
@@ -393,7 +395,7 @@ int adr_gate(int dtype, const void* x, int xcs, const void* ah, long ahn, const 
              int N, int H, int W, int C, void* stream);
 int adr_gate_bwd(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw, long awn,
                  const void* dout, int dcs, void* dx, int ocs, void* dah, long dahn, void* daw, long dawn, int N,
-                 int H, int W, int C, int accumulate, void* stream);
+                 int H, int W, int C, int accumulate, int zero_other, void* stream);
 int adr_adapool(int dtype, const void* x, int xcs, int N, int H, int W, int C, void* y, int ycs, int OH, int OW,
                 void* stream);
 int adr_adapool_bwd(int dtype, const void* dy, int dcs, int N, int H, int W, int C, void* dx, int ocs, int OH, int OW,

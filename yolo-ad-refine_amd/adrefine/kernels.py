@@ -2350,8 +2350,9 @@ class GateFn(torch.autograd.Function):
             dah, dahn, daw, dawn = da.data_ptr(), H * C, da.data_ptr() + N * H * C * es, W * C
             dah_t = daw_t = None
         else:
-            dah_t = torch.zeros_like(ah_t, memory_format=torch.channels_last)
-            daw_t = torch.zeros_like(aw_t, memory_format=torch.channels_last)
+            # the kernel zeroes the rows the gate does not use (dah rows H.., daw rows ..H): no fill launches
+            dah_t = torch.empty_like(ah_t, memory_format=torch.channels_last)
+            daw_t = torch.empty_like(aw_t, memory_format=torch.channels_last)
             dah, dahn = dah_t.data_ptr(), (H + W) * C
             daw, dawn = daw_t.data_ptr() + H * C * es, (H + W) * C
         dx = empty_act(N, C, H, W, dtype, dout.device) if has_x else None
@@ -2359,7 +2360,7 @@ class GateFn(torch.autograd.Function):
         lib.adr_gate_bwd(dcode(dtype), ctypes.c_void_p(vx[1]) if has_x else None, vx[2], ctypes.c_void_p(ah), ahn,
                          ctypes.c_void_p(aw), awn, ctypes.c_void_p(vd[1]), vd[2],
                          ctypes.c_void_p(dx.data_ptr()) if has_x else None, C, ctypes.c_void_p(dah), dahn,
-                         ctypes.c_void_p(daw), dawn, N, H, W, C, 0, stream())
+                         ctypes.c_void_p(daw), dawn, N, H, W, C, 0, int(layout != "ela"), stream())
         if layout == "ela":
             return dx, da, None, None, None
         return dx, dah_t, daw_t, None, None
@@ -2815,7 +2816,9 @@ def tokens(x):
     if cs != C:
         t = t.contiguous(memory_format=torch.channels_last)
         relayout_count[0] += 1
-    return t.as_strided((B, C, H * W, 1), (H * W * C, 1, C, C))
+    # a view (H and W merge: stride W*C = W x C), not as_strided: as_strided's backward zero-fills the base storage
+    # and scatters into it (a fill + copy launch per call)
+    return t.view(B, C, H * W, 1)
 
 
 def untokens(t, H, W):
@@ -2824,7 +2827,7 @@ def untokens(t, H, W):
     if cs != C:
         t = t.contiguous(memory_format=torch.channels_last)
         relayout_count[0] += 1
-    return t.as_strided((B, C, H, W), (H * W * C, 1, W * C, C))
+    return t.view(B, C, H, W)
 
 
 class TSSAStackFn(torch.autograd.Function):

@@ -186,7 +186,8 @@ __global__ void __launch_bounds__(256) gate_kernel(const T* x, int xcs, const T*
 template <typename T, int VW>
 __global__ void __launch_bounds__(256) gate_bwd_reduce_kernel(const T* x, int xcs, const T* ah, long ahn, const T* aw,
                                                               long awn, const T* dout, int dcs, T* dah, long dahn,
-                                                              T* daw, long dawn, int N, int H, int W, int C) {
+                                                              T* daw, long dawn, int N, int H, int W, int C,
+                                                              int zero_other) {
   __shared__ float red[256 * VW];
   const int n = blockIdx.y, b = blockIdx.x;
   const bool row = b < H;
@@ -228,6 +229,13 @@ __global__ void __launch_bounds__(256) gate_bwd_reduce_kernel(const T* x, int xc
         for (int e = 0; e < VW; ++e) t[e] += red[(q * gn + threadIdx.x) * VW + e];
       T* dst = row ? dah + n * dahn + (long)idx * C : daw + n * dawn + (long)idx * C;
       vstore<T, VW>(dst + c0, t);
+      if (zero_other) {  // coord layout: row b of the other (H + W)-row gradient is unused by the gate: zero it
+        float z[VW];
+#pragma unroll
+        for (int e = 0; e < VW; ++e) z[e] = 0.f;
+        T* oth = row ? daw + n * dawn + (long)(idx - H) * C : dah + n * dahn + (long)(idx + H) * C;
+        vstore<T, VW>(oth + c0, z);
+      }
     }
     __syncthreads();
   }
@@ -550,16 +558,16 @@ extern "C" int adr_gate(int dtype, const void* x, int xcs, const void* ah, long 
 
 extern "C" int adr_gate_bwd(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw, long awn,
                             const void* dout, int dcs, void* dx, int ocs, void* dah, long dahn, void* daw, long dawn,
-                            int N, int H, int W, int C, int accumulate, void* stream) {
+                            int N, int H, int W, int C, int accumulate, int zero_other, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const bool v = vec_ok(C, VW_OF(dtype), {xcs, ahn, awn, dcs, ocs, dahn, dawn}, {x, ah, aw, dout, dx, dah, daw});
   const dim3 g = dim3(H + W, N);
   if (dtype == ADR_BF16) {
-    if (v) hipLaunchKernelGGL((gate_bwd_reduce_kernel<__bf16, 8>), g, dim3(256), 0, st, P(const __bf16, x), xcs, P(const __bf16, ah), ahn, P(const __bf16, aw), awn, P(const __bf16, dout), dcs, P(__bf16, dah), dahn, P(__bf16, daw), dawn, N, H, W, C);
-    else hipLaunchKernelGGL((gate_bwd_reduce_kernel<__bf16, 1>), g, dim3(256), 0, st, P(const __bf16, x), xcs, P(const __bf16, ah), ahn, P(const __bf16, aw), awn, P(const __bf16, dout), dcs, P(__bf16, dah), dahn, P(__bf16, daw), dawn, N, H, W, C);
+    if (v) hipLaunchKernelGGL((gate_bwd_reduce_kernel<__bf16, 8>), g, dim3(256), 0, st, P(const __bf16, x), xcs, P(const __bf16, ah), ahn, P(const __bf16, aw), awn, P(const __bf16, dout), dcs, P(__bf16, dah), dahn, P(__bf16, daw), dawn, N, H, W, C, zero_other);
+    else hipLaunchKernelGGL((gate_bwd_reduce_kernel<__bf16, 1>), g, dim3(256), 0, st, P(const __bf16, x), xcs, P(const __bf16, ah), ahn, P(const __bf16, aw), awn, P(const __bf16, dout), dcs, P(__bf16, dah), dahn, P(__bf16, daw), dawn, N, H, W, C, zero_other);
   } else {
-    if (v) hipLaunchKernelGGL((gate_bwd_reduce_kernel<float, 4>), g, dim3(256), 0, st, P(const float, x), xcs, P(const float, ah), ahn, P(const float, aw), awn, P(const float, dout), dcs, P(float, dah), dahn, P(float, daw), dawn, N, H, W, C);
-    else hipLaunchKernelGGL((gate_bwd_reduce_kernel<float, 1>), g, dim3(256), 0, st, P(const float, x), xcs, P(const float, ah), ahn, P(const float, aw), awn, P(const float, dout), dcs, P(float, dah), dahn, P(float, daw), dawn, N, H, W, C);
+    if (v) hipLaunchKernelGGL((gate_bwd_reduce_kernel<float, 4>), g, dim3(256), 0, st, P(const float, x), xcs, P(const float, ah), ahn, P(const float, aw), awn, P(const float, dout), dcs, P(float, dah), dahn, P(float, daw), dawn, N, H, W, C, zero_other);
+    else hipLaunchKernelGGL((gate_bwd_reduce_kernel<float, 1>), g, dim3(256), 0, st, P(const float, x), xcs, P(const float, ah), ahn, P(const float, aw), awn, P(const float, dout), dcs, P(float, dah), dahn, P(float, daw), dawn, N, H, W, C, zero_other);
   }
   int rc = check_launch("adr_gate_bwd(reduce)");
   if (rc || !dx) return rc;
