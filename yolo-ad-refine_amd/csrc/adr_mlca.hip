@@ -331,12 +331,15 @@ __global__ void __launch_bounds__(256) mlca_bwd_y_kernel(const T* dout, int dcs,
   }
 }
 
-__global__ void sum_rows_kernel(const float* part, int rows, int cols, float* out) {
-  int c = blockIdx.x * blockDim.x + threadIdx.x;
+// the local and global 1-D conv weight gradients: block 0 sums part[0..rows) into out0, block 1 the next rows
+// (part + rows * cols) into out1 — one launch for both (cols <= blockDim)
+__global__ void sum_rows_kernel(const float* part, int rows, int cols, float* out0, float* out1) {
+  const int c = threadIdx.x;
   if (c >= cols) return;
+  const float* p = part + (long)blockIdx.x * rows * cols;
   float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += part[(long)r * cols + c];
-  out[c] = s;
+  for (int r = 0; r < rows; ++r) s += p[(long)r * cols + c];
+  (blockIdx.x ? out1 : out0)[c] = s;
 }
 
 }  // namespace adr
@@ -414,7 +417,7 @@ extern "C" int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout,
                      local_weight, dlocal, dwl_part, dwg_part);
   MLCA_DISPATCH(dtype, v, mlca_bwd_y_kernel, mlca_grid((long)N * H * W, dtype, v, C), (const TT*)dout, dcs, att,
                 dlocal, (TT*)dy, ocs, N, H, W, C);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(64), 0, st, dwl_part, N, k, dwl);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(1), dim3(64), 0, st, dwg_part, N, k, dwg);
+  ADR_REQUIRE(k <= 64, "mlca_bwd: kernel size %d", k);
+  hipLaunchKernelGGL(sum_rows_kernel, dim3(2), dim3(64), 0, st, dwl_part, N, k, dwl, dwg);  // dwg_part follows dwl_part
   return check_launch("adr_mlca_bwd");
 }
