@@ -807,6 +807,7 @@ class WgradDeferral:
         self.cols, self.ckeep = [], []
         self.gnps, self.gkeep = [], []
         self.dots, self.dkeep = [], []
+        self.post_dots = []  # callables run right after the batched dot sums (they consume their outputs)
 
     def add_dotsum(self, x, dy, out):
         """out[0] = sum(x * dy) over every pixel and channel (a scalar parameter gradient), at the flush.
@@ -880,6 +881,8 @@ class WgradDeferral:
         if self.dots:  # before the axpys that add their outputs into the arena
             arr = (DotsumEntry * len(self.dots))(*self.dots)
             lib.adr_dotsum_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.dots), stream())
+        for fn in self.post_dots:
+            fn()
         if self.cols:  # before the partial sums that read their rows
             arr = (ColsumEntry * len(self.cols))(*self.cols)
             lib.adr_nc_reduce_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.cols), stream())
@@ -901,6 +904,7 @@ class WgradDeferral:
         self.cols, self.ckeep = [], []
         self.gnps, self.gkeep = [], []
         self.dots, self.dkeep = [], []
+        self.post_dots = []
 
 
 def _defer_dot(param, x, dy):
@@ -2171,9 +2175,19 @@ class FusionFn(torch.autograd.Function):
             d = _new_like(x)
             _ew(EW_AXPBY, (d, d.data_ptr(), d.shape[1]), vd, vd, ca=w[i:i + 1], cb=z)
             dxs.append(d)
-        dwn = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs])
         dfw = torch.empty_like(fwd)
-        lib.adr_fusion_weights_bwd(fptr(fwd), fwd.numel(), 1e-4, fptr(dwn), fptr(dfw), stream())
+        if ctx.needs_input_grad[0] and all(_defer_dot(ctx.pfw, x, vd[0]) for x in xs):
+            # the per-input dot sums at the flush (one batched launch with the other scalar gradients), then the
+            # normalisation backward, then the arena add (the flush runs dots -> post_dots -> axpys)
+            dwn = torch.empty(len(xs), dtype=torch.float32, device=dy.device)
+            for i, x in enumerate(xs):
+                _DEFER.add_dotsum(x, vd[0], dwn[i:i + 1])
+            n = fwd.numel()
+            _DEFER.post_dots.append(lambda: lib.adr_fusion_weights_bwd(fptr(fwd), n, 1e-4, fptr(dwn), fptr(dfw),
+                                                                       stream()))
+        else:
+            dwn = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs])
+            lib.adr_fusion_weights_bwd(fptr(fwd), fwd.numel(), 1e-4, fptr(dwn), fptr(dfw), stream())
         return (sink(ctx.pfw, dfw), *dxs)
 
 
