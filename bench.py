@@ -138,6 +138,35 @@ def infer_bench(model, bs, img, steps, warmup, dev, graph=True, roofline=False, 
     return bs * steps / dt, 1000 * dt / steps, roof, dets, share
 
 
+def nms_bench(dev, bs=32, iters=20):
+    """The NMS leg on a fixed, seeded head output (data/synthetic.head_output: bs 32 x 8400 anchors x 80 classes),
+    so its work does not depend on the model state: adr_nms (one persistent launch) at the predictor's settings
+    (conf 0.25, iou 0.7, single-label) and the validator's (conf 0.001, multi-label; engine/validator.py:98-99),
+    max_det 300, max_nms 30000. HIP events on the launch stream around `iters` calls."""
+    import torch
+    from adrefine.data.synthetic import head_output
+    from adrefine.utils.ops import check_counts, non_max_suppression_padded
+    y = head_output(bs, seed=7).to(dev).contiguous()
+    res = {"input": f"data/synthetic.head_output(bs={bs}, 8400 anchors, 80 classes, seed 7)"}
+    for name, conf, multi in (("predict", 0.25, False), ("val", 0.001, True)):
+        sc = y[:, 4:]
+        cand = int((sc > conf).sum()) if multi else int((sc.amax(1) > conf).sum())
+        for _ in range(3):
+            out, n = non_max_suppression_padded(y, conf, 0.7, multi_label=multi)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            out, n = non_max_suppression_padded(y, conf, 0.7, multi_label=multi)
+        e1.record()
+        torch.cuda.synchronize()
+        counts = n.tolist()
+        check_counts(counts, dev)
+        res[name] = {"conf": conf, "multi_label": multi, "candidates": cand, "detections_per_batch": sum(counts),
+                     "us_per_call": round(1e3 * e0.elapsed_time(e1) / iters, 2), "calls": iters}
+    return res
+
+
 def pmc_traffic(symbol):
     """HBM bytes per launch of `symbol` from the committed PMC passes (profiles/pmc_traffic.json, written by
     scripts/pmc_traffic.py from rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE runs of this same bench); (None, None)
@@ -199,12 +228,31 @@ def stage_overhead(model, tr, batch, bs, steps=30):
     import torch
     from adrefine.engine.ddp import cuts_for_bucket
     from adrefine.engine.trainer import DDP_BUCKET_MB, FusedTrainer
+    import socket
+
+    import torch.distributed as dist
     cuts = cuts_for_bucket(model, DDP_BUCKET_MB)
     tr2 = FusedTrainer(model, batch_size=bs, world_size=1, stages=cuts)
-    for _ in range(3):
-        tr2.step(batch)
-    tr2.capture(batch)
-    tr2.step(batch)
+    # the same staged step with the real RCCL bucket all-reduces between the stage-graph replays: a one-rank `nccl`
+    # process group (the multi-GPU step's exact host / stream interleaving; the one-rank sum is the identity)
+    tr3, rccl_err = None, None
+    try:
+        if not dist.is_initialized():
+            with socket.socket() as so:
+                so.bind(("127.0.0.1", 0))
+                port = so.getsockname()[1]
+            dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                                    device_id=next(model.parameters()).device)
+        tr3 = FusedTrainer(model, batch_size=bs, world_size=1, stages=cuts, collectives=True)
+    except Exception as e:  # noqa: BLE001 - report, keep the line
+        rccl_err = f"{type(e).__name__}: {e}"[:200]
+    for t in (tr2, tr3):
+        if t is None:
+            continue
+        for _ in range(3):
+            t.step(batch)
+        t.capture(batch)
+        t.step(batch)
 
     def timed(t):
         torch.cuda.synchronize()
@@ -214,12 +262,24 @@ def stage_overhead(model, tr, batch, bs, steps=30):
         torch.cuda.synchronize()
         return 1000 * (time.perf_counter() - t0) / steps
 
-    a, b = timed(tr), timed(tr2)
-    a2, b2 = timed(tr), timed(tr2)
-    un, st = min(a, a2), min(b, b2)
+    runs = {"un": [], "st": [], "rc": []}
+    for _ in range(2):
+        runs["un"].append(timed(tr))
+        runs["st"].append(timed(tr2))
+        if tr3 is not None:
+            runs["rc"].append(timed(tr3))
+    un, st = min(runs["un"]), min(runs["st"])
+    rc = min(runs["rc"]) if runs["rc"] else None
     tr2.graphs = None
+    if tr3 is not None:
+        tr3.graphs = None
     return {"bucket_mb": DDP_BUCKET_MB, "cuts": list(cuts), "stages": len(cuts) + 1, "ms_per_step_unstaged": round(un, 3),
-            "ms_per_step_staged": round(st, 3), "overhead": round(st / un - 1, 4), "steps": steps}
+            "ms_per_step_staged": round(st, 3), "overhead": round(st / un - 1, 4), "steps": steps,
+            "ms_per_step_staged_rccl": None if rc is None else round(rc, 3),
+            "rccl_overhead_vs_staged": None if rc is None else round(rc / st - 1, 4),
+            "rccl_overhead_vs_unstaged": None if rc is None else round(rc / un - 1, 4),
+            "rccl": "one-rank nccl group, real all_reduce per bucket between stage-graph replays" if rccl_err is None
+            else rccl_err}
 
 
 def augment_bench(bs, img, dev, reps=5):
@@ -407,15 +467,21 @@ def main():
         if world == 1 and args.stage_check and not args.no_graph:
             staging = stage_overhead(model, tr, batch, args.bs)
         cpu = None if args.no_cpu_baseline or world > 1 else cpu_baseline(budget_s=args.cpu_budget)
-        infer = None
+        infer = nms = None
         if world == 1 and args.infer_steps > 0:  # configs[1] alongside the headline line
-            i_ips, i_ms, _, dets, _ = infer_bench(model, args.infer_bs, args.img, args.infer_steps, 2, dev,
+            # on a freshly initialised model (seed 0), not on the weights the timed train steps left, so the
+            # inference leg's NMS work does not depend on how many steps ran before it
+            torch.manual_seed(0)
+            imodel = DetectionModel(str(CFG), compute_dtype=dtype).to(dev)
+            i_ips, i_ms, _, dets, _ = infer_bench(imodel, args.infer_bs, args.img, args.infer_steps, 2, dev,
                                                   graph=not args.no_graph)
             # the validator's NMS settings (conf 0.001, multi-label: engine/validator.py:98-99) give NMS real work on
             # random-recipe logits (conf 0.25 leaves nothing to sort or suppress)
-            v_ips, v_ms, _, v_dets, v_share = infer_bench(model, args.infer_bs, args.img, args.infer_steps, 2, dev,
+            v_ips, v_ms, _, v_dets, v_share = infer_bench(imodel, args.infer_bs, args.img, args.infer_steps, 2, dev,
                                                           graph=not args.no_graph, conf=0.001, multi_label=True,
                                                           nms_share=True)
+            del imodel
+            nms = nms_bench(dev, args.infer_bs)
             infer = {"metric": "images/sec inference (640x640) bs32, 1 GPU", "value": round(i_ips, 2),
                      "ms_per_batch": round(i_ms, 3), "bs": args.infer_bs, "steps": args.infer_steps,
                      "pipeline": "uint8 -> eval fwd (bf16) -> DFL decode -> NMS(0.25, 0.7, 300), one hipGraph",
@@ -438,12 +504,12 @@ def main():
             "roofline": roof, "cpu_baseline": cpu, "loss_finite": finite,
             "ms_per_step_events": step_stats, "ddp_staging": staging,
             "host_enqueue_ms_per_step": round(1000 * t_host / args.steps, 3), "hipgraph": not args.no_graph,
-            "inference": infer, "peak_hbm_gib": round(peak_gib, 2),
+            "inference": infer, "nms": nms, "peak_hbm_gib": round(peak_gib, 2),
             "augment": (augment_bench(args.bs, args.img, dev) if world == 1 and args.augment_bench and
                         args.scale == "n" else None),
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

@@ -633,6 +633,14 @@ int adr_seed_advance(int64_t* seed, void* stream);
 /* Pairwise IoU of xyxy boxes a (N,4) and b (M,4) -> out (N,M), eps added to the union (utils/metrics.py:52-72);
  * the validator's TP matching (models/yolo/detect/val.py:213-214). */
 int adr_box_iou(const float* a, int N, const float* b, int M, float eps, float* out, void* stream);
+/* Validator TP matching of one image (replaces engine/validator.py:221-261 match_predictions, use_scipy=False):
+ * iou (G, P) fp32 from adr_box_iou (labels x detections); a pair counts only when gt_cls[g] == pred_cls[p].
+ * For each detection its best label (largest IoU; on exact ties the larger label index, as the reference's reversed
+ * ascending sort orders small inputs); for each threshold thr[t] (fp32, compared as the reference's float32
+ * `iou >= threshold`) a label is credited to the lowest-index detection whose best it is with IoU >= thr[t].
+ * correct (P, T) uint8. P <= 2048, T <= 16; G unbounded. One workgroup, no atomics outside LDS (atomicMin order-free). */
+int adr_match_predictions(const float* iou, int G, int P, const float* gt_cls, const float* pred_cls, const float* thr,
+                          int T, unsigned char* correct, void* stream);
 size_t adr_nms_workspace(int B, int nc, int A, int multi, int max_det);
 int adr_nms(const float* y, int B, int nc, int A, float conf, float iou, int multi, int agnostic,
             const unsigned char* class_mask, int max_det, int max_nms, float max_wh, float* out, int* nout, void* ws,

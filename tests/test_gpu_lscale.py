@@ -1,5 +1,5 @@
 """BASELINE.json configs[4] at its real image size: the 701 yaml at scale l (C3k2 c3k=True, C2PTSSA 4 heads,
-AYHead hidc 512 / task_ch 256 -> DyDCNv2 with C = Cout = 256) at 1280^2, bs 2 per GPU (the bench runs bs 16).
+AYHead hidc 512 / task_ch 256 -> DyDCNv2 with C = Cout = 256) at 1280^2 and its real per-GPU batch, bs 16.
 
 * a captured hipGraph train step vs an eager one from the same state and batch: loss items and parameter
   updates within 10x the eager-vs-eager spread (+1e-4 / 1e-3), everything finite;
@@ -14,7 +14,7 @@ from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 CFG = ROOT / "tests" / "configs" / "yolo11-701-YOLO-AD-Refine.yaml"
-S, BS = 1280, 2
+S, BS = 1280, 16
 
 
 def _model():
@@ -47,10 +47,21 @@ def _run(graph, fp8=False, state=None):
         return items, after, init
     finally:
         K.CONV_FP8 = old
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
 
 
-def test_l1280_graph_vs_eager_and_fp8():
-    ie, pe, init = _run(False)
+_STATE = {}
+
+
+def _eager():
+    if not _STATE:
+        _STATE["e"] = _run(False)
+    return _STATE["e"]
+
+
+def test_l1280_graph_vs_eager():
+    ie, pe, init = _eager()
     ie2, pe2, _ = _run(False, state=init)
     ig, pg, _ = _run(True, state=init)
     for t in (ie, ie2, ig):
@@ -72,6 +83,10 @@ def test_l1280_graph_vs_eager_and_fp8():
           f"eager-eager {pspread:.3f}, eager-graph {pd:.3f}")
     assert dgi <= 10 * spread + 1e-4, (ie, ie2, ig)
     assert pd <= 10 * pspread + 1e-3, (pd, pspread)
+
+
+def test_l1280_fp8_vs_bf16():
+    ie, _, init = _eager()
     i8, p8, _ = _run(False, fp8=True, state=init)
     assert torch.isfinite(i8).all() and all(torch.isfinite(v).all() for v in p8.values())
     tot, tot8 = float(ie.sum()), float(i8.sum())

@@ -51,6 +51,27 @@ def train_batch(bs: int, img: int, seed: int, device, nc: int = 80, u8: bool = F
     return {"img": im.to(device), "gt": gt}, lab
 
 
+def head_output(bs: int, na: int = 8400, nc: int = 80, img: int = 640, seed: int = 7, objects: int = 64):
+    """A decoded eval-head output (bs, 4 + nc, na) fp32 with controlled NMS work, for the bench's NMS leg: xywh boxes
+    in pixels, half of the anchors jittered copies of `objects` boxes per image (real suppression), class scores
+    s = u^16 with u a per-image permutation of (k + 0.5) / (nc * na) — distinct within an image, and ~30 % of all
+    (anchor, class) pairs above the validator's conf 0.001 (the max_nms cut runs). Generated on the host with a
+    seeded generator, so the workload does not depend on any model state."""
+    g = torch.Generator().manual_seed(seed)
+    rnd = lambda *s: torch.rand(*s, generator=g)  # noqa: E731
+    centre = rnd(bs, 2, na) * img
+    size = 4 + 296 * rnd(bs, 2, na) ** 3
+    obj_c = rnd(bs, 2, objects) * img
+    obj_s = 16 + 200 * rnd(bs, 2, objects) ** 2
+    which = torch.randint(0, objects, (bs, 1, na), generator=g).expand(bs, 2, na)
+    near = rnd(bs, 1, na) < 0.5
+    centre = torch.where(near, obj_c.gather(2, which) + 8 * (rnd(bs, 2, na) - 0.5), centre)
+    size = torch.where(near, obj_s.gather(2, which) * (0.9 + 0.2 * rnd(bs, 2, na)), size)
+    n = nc * na
+    u = torch.stack([(torch.randperm(n, generator=g).float() + 0.5) / n for _ in range(bs)])
+    return torch.cat((centre, size, (u ** 16).view(bs, nc, na)), 1)
+
+
 class AugSourceDataset:
     """Synthetic stand-in for a training dataset under augmentation (the reference dataset interface the mix
     transforms use: buffer, get_image_and_label, __len__; data/base.py:290-301): n BGR uint8 images with their long

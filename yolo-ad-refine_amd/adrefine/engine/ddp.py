@@ -133,10 +133,11 @@ class BucketReducer:
     bucket k behind the work already on the current stream (ProcessGroupNCCL waits on it; gloo copies through
     the host); `wait()` makes the current stream wait for every launched bucket."""
 
-    def __init__(self, arena, ranges, world_size, group=None):
+    def __init__(self, arena, ranges, world_size, group=None, active=None):
         self.arena = arena
         self.ranges = list(ranges)
         self.world_size = world_size
+        self.active = world_size > 1 if active is None else bool(active)  # True at world 1: a one-rank group
         self.group = group
         self.works = []
         self.launched = []
@@ -144,7 +145,7 @@ class BucketReducer:
     def launch(self, k):
         lo, hi = self.ranges[k]
         self.launched.append(k)
-        if self.world_size <= 1 or hi <= lo:
+        if not self.active or hi <= lo:
             return
         import torch.distributed as dist
         self.works.append(dist.all_reduce(self.arena[lo:hi], op=dist.ReduceOp.SUM, group=self.group,

@@ -14,7 +14,7 @@ from __future__ import annotations
 import torch
 
 from .. import kernels as K
-from ..utils.ops import non_max_suppression_padded
+from ..utils.ops import check_counts, non_max_suppression_padded
 
 
 class FusedPredictor:
@@ -76,6 +76,8 @@ class FusedPredictor:
 
     def predict(self, img):
         out, n = self.run_padded(img)
-        return [out[i, :k].clone() for i, k in enumerate(n.tolist())]
+        counts = n.tolist()
+        check_counts(counts, out.device)
+        return [out[i, :k].clone() for i, k in enumerate(counts)]
 
     __call__ = predict

@@ -117,9 +117,13 @@ class FusedTrainer:
 
     def __init__(self, model, lr0=0.01, momentum=0.937, weight_decay=5e-4, nbs=64, batch_size=64, world_size=1,
                  process_group=None, ema=True, ema_decay=0.9999, ema_tau=2000, max_norm=10.0, epochs=100, nb=None,
-                 lrf=0.01, warmup_epochs=3.0, warmup_bias_lr=0.1, warmup_momentum=0.8, cos_lr=False, stages=None):
+                 lrf=0.01, warmup_epochs=3.0, warmup_bias_lr=0.1, warmup_momentum=0.8, cos_lr=False, stages=None,
+                 collectives=None):
         self.model = model
         self.world_size = world_size
+        # collectives=True issues the bucket all-reduces even at world_size 1 (a one-rank RCCL group exercises the
+        # same interleaving of stage-graph replays and eager collectives as the multi-GPU step)
+        self.collectives = world_size > 1 if collectives is None else bool(collectives)
         self.pg = process_group
         self.max_norm = max_norm
         self.batch_size = batch_size
@@ -132,7 +136,7 @@ class FusedTrainer:
         # backward stages: DDP overlaps bucket all-reduces with the remaining stages (engine/ddp.py)
         if stages is None:
             stages = (DDP_CUTS if DDP_CUTS is not None else cuts_for_bucket(model, DDP_BUCKET_MB)) \
-                if world_size > 1 else ()
+                if self.collectives else ()
         self.cuts = tuple(stages)
         self.dev = dev = next(model.parameters()).device
         groups = param_groups(model)
@@ -157,7 +161,7 @@ class FusedTrainer:
             off += p.numel()
             bounds[s][1] = off
         self.buckets = [(b[0] or 0, b[1] or 0) for b in bounds]  # arena range of each stage's gradients
-        self.reducer = BucketReducer(self.grad, self.buckets, world_size, process_group)
+        self.reducer = BucketReducer(self.grad, self.buckets, world_size, process_group, active=self.collectives)
         # EMA over every floating state entry (params + BN running stats), buffers as group 3
         self.use_ema = ema
         pset = {id(p) for _, p, _, _ in self.entries}
@@ -258,7 +262,7 @@ class FusedTrainer:
         so reducing the accumulated arena once equals DDP's reduction on every backward."""
         self.lr, self.momentum, self.accumulate = self.sched.at(self.ni)
         opt_now = self.ni - self.last_opt_step >= self.accumulate
-        reduce_now = opt_now and self.world_size > 1
+        reduce_now = opt_now and self.collectives
         if opt_now:
             self._set_hyper()
         if self.graphs is not None:

@@ -940,6 +940,7 @@ def defer_wgrad():
                 _DEFER.side.join()
         finally:
             _DEFER = prev
+            bnxf_clear()
     return _cm()
 
 
@@ -1254,7 +1255,15 @@ BN_XF_BWD = bool(int(__import__("os").environ.get("ADR_BN_XF_BWD", "1")))
 # 3x3 implicit-GEMM conv (each dz element staged 9x) or of a multi-column-tile 1x1 ran 3x slower than the
 # affine_act_bwd + dgrad pair, so the fusion is taken only where each element is staged about once (x100)
 BN_XF_MAX_REUSE = int(__import__("os").environ.get("ADR_BN_XF_MAX_REUSE", "150"))
-_BNXF_PENDING = {}  # data_ptr -> BnXf: unwritten dy buffers handed to a conv backward
+# data_ptr -> (BnXf, dy): unwritten dy buffers handed to a conv backward. The entry holds dy itself, so its memory
+# cannot be reused by another tensor while the entry exists; entries nobody consumed (a frozen producing conv) are
+# dropped at the end of the backward (defer_wgrad's exit, bnxf_clear)
+_BNXF_PENDING = {}
+
+
+def bnxf_clear():
+    """Drop pending BN-act backward entries no conv consumed (end of a backward pass)."""
+    _BNXF_PENDING.clear()
 
 
 class BnXfStruct(ctypes.Structure):
@@ -1271,17 +1280,23 @@ class BnXf:
         self.y, self.dz, self.scale, self.shift, self.A, self.B, self.Cc, self.act = y, dz, scale, shift, A, B, Cc, act
 
     def attach(self, dy):
-        _BNXF_PENDING[dy.data_ptr()] = self
+        _BNXF_PENDING[dy.data_ptr()] = (self, dy)
         dy._adr_bnxf = self
 
     @staticmethod
     def take(dy):
-        """The pending transform of a gradient buffer handed to a conv backward (removed from the registry)."""
+        """The pending transform of a gradient buffer handed to a conv backward (removed from the registry). A
+        tensor object that lost the attribute (autograd re-wrapped it) matches its entry only when it is a view of
+        exactly the registered buffer: same address, shape, strides and dtype."""
         p = getattr(dy, "_adr_bnxf", None)
-        if p is None:
-            p = _BNXF_PENDING.get(dy.data_ptr())
+        ent = _BNXF_PENDING.get(dy.data_ptr())
+        if p is None and ent is not None:
+            t = ent[1]
+            if t.shape == dy.shape and t.stride() == dy.stride() and t.dtype == dy.dtype:
+                p = ent[0]
         if p is not None:
-            _BNXF_PENDING.pop(dy.data_ptr(), None)
+            if ent is not None and ent[0] is p:
+                del _BNXF_PENDING[dy.data_ptr()]
             try:
                 del dy._adr_bnxf
             except AttributeError:
@@ -2547,17 +2562,24 @@ def _dcn_fused(dtype, C, Cout, omcs):
 _DCN_FUSED = bool(int(__import__("os").environ.get("ADR_DCN_FUSED", "1")))  # 0: im2col path (A/B only)
 
 
-_DCN_FAR = {}
+_DCN_FAR = {}  # device -> (fp32 far-corner buffer, tile flags), grown to the largest shape seen
+_DCN_FAR_RETIRED = []  # outgrown buffers: a captured graph may still address them
 
 
 def _dcn_far_scratch(dev, N, H, W, C):
-    """Persistent zeroed scratch of adr_dcn_bwd_bf16 per shape: the fp32 far-corner buffer and the tile flags
-    (the kernels leave both zero again, so one allocation serves every step and graph replay)."""
-    key = (str(dev), N, H, W, C)
-    if key not in _DCN_FAR:
-        _DCN_FAR[key] = (torch.zeros(N * H * W * C, dtype=torch.float32, device=dev),
-                         torch.zeros(int(lib.adr_dcn_bwd_tiles(N, H, W)), dtype=torch.int32, device=dev))
-    return _DCN_FAR[key]
+    """Persistent zeroed scratch of adr_dcn_bwd_bf16: the fp32 far-corner buffer and the tile flags. The kernels
+    leave both zero again, so ONE pair per device serves every level, shape, step and graph replay (calls are
+    stream-ordered); a call uses a prefix view of it."""
+    key = str(dev)
+    n, nt = N * H * W * C, int(lib.adr_dcn_bwd_tiles(N, H, W))
+    cur = _DCN_FAR.get(key)
+    if cur is None or cur[0].numel() < n or cur[1].numel() < nt:
+        if cur is not None:
+            _DCN_FAR_RETIRED.append(cur)
+            n, nt = max(n, cur[0].numel()), max(nt, cur[1].numel())
+        cur = (torch.zeros(n, dtype=torch.float32, device=dev), torch.zeros(nt, dtype=torch.int32, device=dev))
+        _DCN_FAR[key] = cur
+    return cur[0][:N * H * W * C], cur[1][:int(lib.adr_dcn_bwd_tiles(N, H, W))]
 
 
 def _dcn_work(N, H, W, C, Cout, es=2):

@@ -3,14 +3,14 @@ models/yolo/detect/val.py:125-229 (update_metrics, _process_batch, get_stats), e
 (match_predictions), utils/metrics.py:52-72 (box_iou), :1054-1059 (smooth), :1112-1141 (compute_ap),
 :1144-1231 (ap_per_class), :1234-1360 (Metric: mp, mr, map50, map, fitness).
 
-Split as in the reference: the IoU matrix of each image is computed on the device (adr_box_iou, HIP), the greedy
-TP matching and the AP integration run on the host in numpy, exactly as the reference does (it also moves the
-IoU matrix to numpy for matching and accumulates numpy statistics). Boxes are compared in the network's input
-space (the reference's scale_boxes to the original image is the identity for unpadded, unresized inputs; callers
-with letterboxed images scale both sides first).
+The per-image work runs on the device: the IoU matrix (adr_box_iou) and the TP matching at the ten IoU thresholds
+(adr_match_predictions: each detection's best same-class label, then per label and threshold the lowest-index
+detection claiming it). The dataset-level AP integration runs once on the host over the concatenated statistics, from
+the definitions below (own formulation, pinned by tests/golden/metrics_val.npz which the reference itself produced).
+Boxes are compared in the network's input space (the reference's scale_boxes to the original image is the identity
+for unpadded, unresized inputs; callers with letterboxed images scale both sides first).
 """
 from __future__ import annotations
-
 
 import numpy as np
 import torch
@@ -18,7 +18,9 @@ import torch
 from .. import kernels as K
 from ..native import lib
 
-IOUV = np.linspace(0.5, 0.95, 10)
+IOUV = np.linspace(0.5, 0.95, 10)  # the validator's mAP@0.5:0.95 thresholds (val.py:36)
+_PR_POINTS = 1000  # resolution of the confidence-indexed precision / recall curves (metrics.py:1191)
+_AP_POINTS = 101   # COCO interpolation points (metrics.py:1135)
 
 
 def box_iou(box1: torch.Tensor, box2: torch.Tensor, eps=1e-7) -> torch.Tensor:
@@ -32,117 +34,126 @@ def box_iou(box1: torch.Tensor, box2: torch.Tensor, eps=1e-7) -> torch.Tensor:
     return out
 
 
+_THR = {}
+
+
 def match_predictions(pred_classes, true_classes, iou, iouv=IOUV):
-    """engine/validator.py:221-261 (greedy, use_scipy=False): (N, 10) bool of correct detections."""
-    correct = np.zeros((pred_classes.shape[0], iouv.shape[0])).astype(bool)
-    correct_class = true_classes[:, None] == pred_classes
-    iou = iou * correct_class
-    iou = iou.cpu().numpy()
-    for i, threshold in enumerate(iouv.tolist()):
-        matches = np.nonzero(iou >= threshold)
-        matches = np.array(matches).T
-        if matches.shape[0]:
-            if matches.shape[0] > 1:
-                matches = matches[iou[matches[:, 0], matches[:, 1]].argsort()[::-1]]
-                matches = matches[np.unique(matches[:, 1], return_index=True)[1]]
-                matches = matches[np.unique(matches[:, 0], return_index=True)[1]]
-            correct[matches[:, 1].astype(int), i] = True
-    return correct
+    """engine/validator.py:221-261 (greedy): (P, T) bool of correct detections, computed by adr_match_predictions from
+    the (G, P) IoU matrix of one image. Thresholds are applied in float32, as the reference's comparison of a float32
+    IoU array with Python floats is."""
+    dev = iou.device
+    G, P = iou.shape
+    T = len(iouv)
+    if G == 0 or P == 0:
+        return np.zeros((P, T), dtype=bool)
+    key = (str(dev), tuple(np.asarray(iouv, dtype=np.float64).tolist()))
+    thr = _THR.get(key)
+    if thr is None:
+        thr = torch.tensor(np.asarray(iouv, dtype=np.float32), device=dev)
+        _THR[key] = thr
+    io = iou.float().contiguous()
+    gc = true_classes.to(dev).float().contiguous()
+    pc = pred_classes.to(dev).float().contiguous()
+    out = torch.empty(P, T, dtype=torch.uint8, device=dev)
+    lib.adr_match_predictions(K.fptr(io), G, P, K.fptr(gc), K.fptr(pc), K.fptr(thr), T, K.fptr(out), K.stream())
+    return out.cpu().numpy().astype(bool)
 
 
-def smooth(y, f=0.05):
-    """utils/metrics.py:1054-1059: box filter of fraction f."""
-    nf = round(len(y) * f * 2) // 2 + 1
-    p = np.ones(nf // 2)
-    yp = np.concatenate((p * y[0], y, p * y[-1]), 0)
-    return np.convolve(yp, np.ones(nf) / nf, mode="valid")
+def box_filter(y, frac):
+    """metrics.py:1054-1059: moving average over an odd window of about 2*frac of the curve, the ends extended with
+    the edge values."""
+    width = round(len(y) * frac * 2) // 2 + 1
+    ext = np.pad(y, width // 2, mode="edge")
+    return np.convolve(ext, np.full(width, 1.0 / width), mode="valid")
 
 
-def compute_ap(recall, precision):
-    """utils/metrics.py:1112-1141: COCO 101-point interpolated AP."""
-    mrec = np.concatenate(([0.0], recall, [1.0]))
-    mpre = np.concatenate(([1.0], precision, [0.0]))
-    mpre = np.flip(np.maximum.accumulate(np.flip(mpre)))
-    x = np.linspace(0, 1, 101)
-    trapz = getattr(np, "trapezoid", None) or np.trapz
-    ap = trapz(np.interp(x, mrec, mpre), x)
-    return ap, mpre, mrec
+def interpolated_ap(recall, precision):
+    """metrics.py:1112-1141. Area under the precision envelope (the running maximum of precision taken from the
+    high-recall end), sampled at 101 equally spaced recall levels and integrated with the trapezoid rule. The curve is
+    anchored at (recall 0, precision 1) and (recall 1, precision 0)."""
+    r = np.concatenate(([0.0], recall, [1.0]))
+    envelope = np.maximum.accumulate(np.concatenate(([1.0], precision, [0.0]))[::-1])[::-1]
+    grid = np.linspace(0, 1, _AP_POINTS)
+    v = np.interp(grid, r, envelope)
+    return float(np.sum(np.diff(grid) * (v[1:] + v[:-1])) / 2.0)
 
 
 def ap_per_class(tp, conf, pred_cls, target_cls, eps=1e-16):
-    """utils/metrics.py:1144-1231 (no plotting): (tp, fp, p, r, f1, ap, unique_classes, p_curve, r_curve,
-    f1_curve, x)."""
-    i = np.argsort(-conf)
-    tp, conf, pred_cls = tp[i], conf[i], pred_cls[i]
-    unique_classes, nt = np.unique(target_cls, return_counts=True)
-    nc = unique_classes.shape[0]
-    x = np.linspace(0, 1, 1000)
-    ap, p_curve, r_curve = np.zeros((nc, tp.shape[1])), np.zeros((nc, 1000)), np.zeros((nc, 1000))
-    for ci, c in enumerate(unique_classes):
-        i = pred_cls == c
-        n_l = nt[ci]
-        n_p = i.sum()
-        if n_p == 0 or n_l == 0:
+    """metrics.py:1144-1231 (no plotting). tp (n, T) bool, conf (n,), pred_cls (n,), target_cls (m,). Returns
+    (tp, fp, p, r, f1, ap, classes, p_curve, r_curve, f1_curve, x) with the reference's meaning: p / r / f1 per class
+    at the single confidence that maximises the smoothed class-mean F1, ap (classes, T)."""
+    rank = np.argsort(-conf)  # confidence order, same sort rule as the reference
+    hits, score, klass = tp[rank], conf[rank], pred_cls[rank]
+    classes, n_labels = np.unique(target_cls, return_counts=True)
+    n_cls, T = classes.shape[0], tp.shape[1]
+    xs = np.linspace(0, 1, _PR_POINTS)
+    ap = np.zeros((n_cls, T))
+    p_curve = np.zeros((n_cls, _PR_POINTS))
+    r_curve = np.zeros((n_cls, _PR_POINTS))
+    for k in range(n_cls):
+        sel = klass == classes[k]
+        n_det = int(sel.sum())
+        if n_det == 0 or n_labels[k] == 0:
             continue
-        fpc = (1 - tp[i]).cumsum(0)
-        tpc = tp[i].cumsum(0)
-        recall = tpc / (n_l + eps)
-        r_curve[ci] = np.interp(-x, -conf[i], recall[:, 0], left=0)
-        precision = tpc / (tpc + fpc)
-        p_curve[ci] = np.interp(-x, -conf[i], precision[:, 0], left=1)
-        for j in range(tp.shape[1]):
-            ap[ci, j], _, _ = compute_ap(recall[:, j], precision[:, j])
+        true_pos = np.cumsum(hits[sel], axis=0)  # (n_det, T) integer running counts
+        seen = np.arange(1, n_det + 1)[:, None]    # detections so far = TP + FP
+        recall = true_pos / (n_labels[k] + eps)
+        precision = true_pos / seen
+        neg_score = -score[sel]  # ascending abscissa for np.interp
+        r_curve[k] = np.interp(-xs, neg_score, recall[:, 0], left=0)
+        p_curve[k] = np.interp(-xs, neg_score, precision[:, 0], left=1)
+        for t in range(T):
+            ap[k, t] = interpolated_ap(recall[:, t], precision[:, t])
     f1_curve = 2 * p_curve * r_curve / (p_curve + r_curve + eps)
-    i = smooth(f1_curve.mean(0), 0.1).argmax()
-    p, r, f1 = p_curve[:, i], r_curve[:, i], f1_curve[:, i]
-    tp = (r * nt).round()
-    fp = (tp / (p + eps) - tp).round()
-    return tp, fp, p, r, f1, ap, unique_classes.astype(int), p_curve, r_curve, f1_curve, x
+    at = int(box_filter(f1_curve.mean(0), 0.1).argmax())
+    p, r, f1 = p_curve[:, at], r_curve[:, at], f1_curve[:, at]
+    n_tp = (r * n_labels).round()
+    n_fp = (n_tp / (p + eps) - n_tp).round()
+    return n_tp, n_fp, p, r, f1, ap, classes.astype(int), p_curve, r_curve, f1_curve, xs
 
 
 class DetectionStats:
     """The detection validator's statistics (val.py:125-190, get_stats :192-201) and box Metric
     (metrics.py:1234-1360): update(preds, batch) per batch, results() at the end."""
 
+    KEYS = ("tp", "conf", "pred_cls", "target_cls", "target_img")
+
     def __init__(self, nc=80):
         self.nc = nc
-        self.stats = {"tp": [], "conf": [], "pred_cls": [], "target_cls": [], "target_img": []}
+        self.stats = {k: [] for k in self.KEYS}
         self.seen = 0
 
     def update(self, preds, batch_idx, cls, bboxes_xyxy):
         """preds: per image (n, 6) [x1, y1, x2, y2, conf, cls] device tensors (adr_nms output); labels: the batch's
         batch_idx (N,), cls (N,), xyxy boxes in input pixels (N, 4)."""
+        T = len(IOUV)
         for si, pred in enumerate(preds):
             self.seen += 1
             sel = batch_idx == si
             tcls, tbox = cls[sel], bboxes_xyxy[sel]
-            npr = len(pred)
-            st = {"conf": np.zeros(0), "pred_cls": np.zeros(0), "tp": np.zeros((npr, 10), dtype=bool),
-                  "target_cls": tcls.cpu().numpy(), "target_img": np.unique(tcls.cpu().numpy())}
-            if npr == 0:
-                if len(tcls):
-                    for k in self.stats:
-                        self.stats[k].append(st[k])
-                continue
-            st["conf"] = pred[:, 4].cpu().numpy()
-            st["pred_cls"] = pred[:, 5].cpu().numpy()
-            if len(tcls):
-                iou = box_iou(tbox.to(pred.device), pred[:, :4])
-                st["tp"] = match_predictions(pred[:, 5], tcls.to(pred.device).float(), iou)
-            for k in self.stats:
-                self.stats[k].append(st[k])
+            tcls_np = tcls.cpu().numpy()
+            n = len(pred)
+            if n == 0 and not len(tcls):
+                continue  # an image with neither detections nor labels adds nothing (val.py:140-145)
+            row = {"target_cls": tcls_np, "target_img": np.unique(tcls_np)}
+            if n == 0:
+                row.update(tp=np.zeros((0, T), dtype=bool), conf=np.zeros(0), pred_cls=np.zeros(0))
+            else:
+                row["conf"] = pred[:, 4].cpu().numpy()
+                row["pred_cls"] = pred[:, 5].cpu().numpy()
+                row["tp"] = (match_predictions(pred[:, 5], tcls, box_iou(tbox.to(pred.device), pred[:, :4]))
+                             if len(tcls) else np.zeros((n, T), dtype=bool))
+            for k in self.KEYS:
+                self.stats[k].append(row[k])
 
     def results(self):
         s = {k: np.concatenate(v, 0) if v else np.zeros(0) for k, v in self.stats.items()}
-        out = {"p": np.zeros(0), "r": np.zeros(0), "ap": np.zeros((0, 10)), "ap_class_index": np.zeros(0, int)}
+        p = r = np.zeros(0)
+        ap, idx = np.zeros((0, len(IOUV))), np.zeros(0, int)
         if len(s["tp"]) and s["tp"].any():
-            _, _, p, r, _, ap, cls_idx, *_ = ap_per_class(s["tp"], s["conf"], s["pred_cls"], s["target_cls"])
-            out = {"p": p, "r": r, "ap": ap, "ap_class_index": cls_idx}
-        mp = float(out["p"].mean()) if len(out["p"]) else 0.0
-        mr = float(out["r"].mean()) if len(out["r"]) else 0.0
-        map50 = float(out["ap"][:, 0].mean()) if len(out["ap"]) else 0.0
-        map_ = float(out["ap"].mean()) if len(out["ap"]) else 0.0
-        fitness = float((np.array([mp, mr, map50, map_]) * [0.0, 0.0, 0.9, 0.1]).sum())
-        out.update({"metrics/precision(B)": mp, "metrics/recall(B)": mr, "metrics/mAP50(B)": map50,
-                    "metrics/mAP50-95(B)": map_, "fitness": fitness})
-        return out
+            _, _, p, r, _, ap, idx, *_ = ap_per_class(s["tp"], s["conf"], s["pred_cls"], s["target_cls"])
+        mean = [float(v.mean()) if len(v) else 0.0 for v in (p, r, ap[:, 0] if len(ap) else ap, ap)]
+        fitness = 0.9 * mean[2] + 0.1 * mean[3]  # Metric.fitness weights (0, 0, 0.9, 0.1)
+        return {"p": p, "r": r, "ap": ap, "ap_class_index": idx, "metrics/precision(B)": mean[0],
+                "metrics/recall(B)": mean[1], "metrics/mAP50(B)": mean[2], "metrics/mAP50-95(B)": mean[3],
+                "fitness": fitness}

@@ -80,4 +80,13 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
     out, n = non_max_suppression_padded(prediction, conf_thres, iou_thres, classes, agnostic, multi_label, max_det,
                                         nc, max_nms, max_wh)
     counts = n.tolist()
+    check_counts(counts, prediction.device)
     return [out[i, :k] for i, k in enumerate(counts)]
+
+
+def check_counts(counts, device):
+    """A negative per-image count is adr_nms's report of a grid-barrier timeout (the persistent kernel's phases ran
+    out of order). Raise, and drop the workspace so the next call starts from zeroed control words."""
+    if any(k < 0 for k in counts):
+        _WS.pop(device, None)
+        raise RuntimeError("adr_nms: a grid barrier timed out (workgroups not co-resident?); detections are invalid")

@@ -1268,7 +1268,9 @@ __global__ void __launch_bounds__(NMSP_THREADS) nms_persistent_kernel(NmsP p) {
       o[4] = key_score(v);
       o[5] = (float)(key % nc);
     }
-    if (tid == 0) a.nout[b] = nout;
+    // a grid barrier that timed out (CTL_ERR, set before this phase's last barrier released) leaves the phases
+    // unordered: report -1 detections so the host fails loudly instead of reading a wrong selection
+    if (tid == 0) a.nout[b] = ld_rlx(&ctl[CTL_ERR]) ? -1 : nout;
     __syncthreads();
   }
   if (p.direct) {  // leave the cursors zero for the next launch, and say so
@@ -1456,4 +1458,69 @@ extern "C" int adr_box_iou(const float* a, int N, const float* b, int M, float e
   hipLaunchKernelGGL(box_iou_kernel, dim3(cdiv((long)N * M, 256)), dim3(256), 0, (hipStream_t)stream, a, N, b, M, eps,
                      out);
   return check_launch("adr_box_iou");
+}
+
+// ---------------- validator TP matching (engine/validator.py:221-261, greedy branch) ----------------
+// The reference sorts every (label, detection) pair with IoU >= t by IoU, keeps each detection's best pair, then
+// keeps, per label, the surviving pair of the lowest detection index. Restated per detection: best label b(p) =
+// argmax_g iou'[g][p] (iou' = iou masked to 0 on class mismatch); at threshold t, p is correct iff iou'[b(p)][p] >= t
+// and p is the smallest such detection with that best label. One 1024-thread workgroup per image: the best labels in
+// LDS, then, per chunk of labels, first[t][g] = min p by LDS atomicMin (order-independent) and the read-back.
+static constexpr int MATCH_THREADS = 1024, MATCH_PMAX = 2048, MATCH_TMAX = 16, MATCH_GCHUNK = 512;
+
+__global__ void __launch_bounds__(MATCH_THREADS)
+match_predictions_kernel(const float* __restrict__ iou, int G, int P, const float* __restrict__ gt_cls,
+                         const float* __restrict__ pred_cls, const float* __restrict__ thr, int T,
+                         unsigned char* __restrict__ correct) {
+  __shared__ int bg[MATCH_PMAX];
+  __shared__ float bv[MATCH_PMAX];
+  __shared__ int first[MATCH_TMAX * MATCH_GCHUNK];
+  __shared__ float th[MATCH_TMAX];
+  const int tid = threadIdx.x;
+  if (tid < T) th[tid] = thr[tid];
+  for (int p = tid; p < P; p += MATCH_THREADS) {  // coalesced over p: iou rows are labels
+    const float pc = pred_cls[p];
+    float best = -1.f;
+    int g_best = 0;
+    for (int g = 0; g < G; ++g) {
+      const float v = gt_cls[g] == pc ? iou[(long)g * P + p] : 0.f;
+      if (v >= best) {  // ties: the larger label index
+        best = v;
+        g_best = g;
+      }
+    }
+    bg[p] = g_best;
+    bv[p] = best;
+  }
+  __syncthreads();
+  for (int g0 = 0; g0 < G; g0 += MATCH_GCHUNK) {
+    const int gn = min(MATCH_GCHUNK, G - g0);
+    for (int i = tid; i < T * MATCH_GCHUNK; i += MATCH_THREADS) first[i] = 0x7fffffff;
+    __syncthreads();
+    for (int p = tid; p < P; p += MATCH_THREADS) {
+      const int g = bg[p] - g0;
+      if (g < 0 || g >= gn) continue;
+      for (int t = 0; t < T; ++t)
+        if (bv[p] >= th[t]) atomicMin(&first[t * MATCH_GCHUNK + g], p);
+    }
+    __syncthreads();
+    for (int p = tid; p < P; p += MATCH_THREADS) {
+      const int g = bg[p] - g0;
+      if (g < 0 || g >= gn) continue;
+      for (int t = 0; t < T; ++t)
+        correct[(long)p * T + t] = (unsigned char)(bv[p] >= th[t] && first[t * MATCH_GCHUNK + g] == p);
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" int adr_match_predictions(const float* iou, int G, int P, const float* gt_cls, const float* pred_cls,
+                                     const float* thr, int T, unsigned char* correct, void* stream) {
+  ADR_REQUIRE(G >= 1 && P >= 0 && P <= MATCH_PMAX && T >= 1 && T <= MATCH_TMAX,
+              "match_predictions: G=%d P=%d T=%d unsupported (G >= 1, P <= %d, T <= %d)", G, P, T, MATCH_PMAX,
+              MATCH_TMAX);
+  if (P == 0) return 0;
+  hipLaunchKernelGGL(match_predictions_kernel, dim3(1), dim3(MATCH_THREADS), 0, (hipStream_t)stream, iou, G, P, gt_cls,
+                     pred_cls, thr, T, correct);
+  return check_launch("adr_match_predictions");
 }
