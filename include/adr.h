@@ -120,6 +120,8 @@ typedef struct adr_bnact_xf {
 } adr_bnact_xf;
 int adr_conv2d_fwd_bf16_bnact(const adr_conv_desc* d, const void* y, const void* w_krsc, void* out, float* stats,
                               const adr_bnact_xf* xf, void* stream);
+/* Rows of its BatchNorm partial statistics (stats holds rows x 2 x K floats). */
+int adr_conv2d_fwd_bf16_bnact_stat_tiles(const adr_conv_desc* d);
 int adr_conv2d_dgrad_bf16_bnact(const adr_conv_desc* d, const void* dz, const void* w_crsk, void* dx, int accumulate,
                                 const void* addend, int addend_cstride, const adr_bnact_xf* xf, void* stream);
 /* Times x100 the XF kernel for this contraction stages each source element (column tiles x gathers per element):
@@ -372,6 +374,8 @@ typedef struct {
   long n;
 } adr_axpy_entry;
 int adr_axpy_batched(const adr_axpy_entry* entries, int count, void* stream);
+/* Same, and x_i = 0 afterwards (the per-level gradient slabs of AYHead's concurrent levels folded into the arena). */
+int adr_axpy_zero_batched(const adr_axpy_entry* entries, int count, void* stream);
 /* BiFPN weights w = relu(fw)/(sum relu(fw)+eps) and backward (block.py:1532-1535). */
 int adr_fusion_weights(const float* fw, int n, float eps, float* w, void* stream);
 int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream);

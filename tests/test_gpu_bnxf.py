@@ -112,3 +112,114 @@ def test_dgrad_bnact_whole_net_step():
     assert set(ga) == set(gb)
     bad = [n for n in ga if not torch.equal(ga[n], gb[n])]
     assert not bad, bad[:10]
+
+
+# ---- forward fusion: the consumer conv stages the producer's pre-BN output through the BN-act (BnFwd) ----
+
+def _pair_run(p, q, x, g, fused):
+    """q(p(x)) with p's output handed lazily to q (Conv.forward(lazy=True)); returns outputs, input gradient, the
+    parameter gradients and p's BN running statistics; the fused and unfused runs start from the same state."""
+    from adrefine import kernels as K
+    old = K.BN_XF_FWD
+    K.BN_XF_FWD = fused
+    sd = ({k: v.clone() for k, v in p.state_dict().items()}, {k: v.clone() for k, v in q.state_dict().items()})
+    try:
+        xx = x.detach().clone().requires_grad_(True)
+        z1 = p(xx, lazy=True)
+        assert bool(K._BNF_PENDING) == fused
+        z2 = q(z1)
+        assert not K._BNF_PENDING
+        z2.backward(g)
+        res = [z2.detach().clone(), z1.detach().clone(), xx.grad.clone()]
+        res += [t.grad.clone() for t in (p.conv.weight, p.bn.weight, p.bn.bias, q.conv.weight, q.bn.weight, q.bn.bias)]
+        res += [p.bn.running_mean.clone(), p.bn.running_var.clone(), q.bn.running_mean.clone()]
+    finally:
+        K.BN_XF_FWD = old
+        p.zero_grad(set_to_none=True)
+        q.zero_grad(set_to_none=True)
+        p.load_state_dict(sd[0])
+        q.load_state_dict(sd[1])
+    return res
+
+
+FWD_CASES = [  # n, c1, c, k1, s1, k2, h, w : p = Conv(c1, c, k1, s1), q = Conv(c, c, k2)
+    (4, 32, 32, 3, 1, 3, 16, 16),    # bottleneck 3x3 -> 3x3 on the halo tiles (TW 16)
+    (2, 64, 64, 3, 1, 3, 24, 8),     # halo tiles TW 8, two 32-channel chunks
+    (4, 16, 32, 3, 2, 1, 40, 40),    # Conv s2 -> C3k2.cv1 1x1 on the streaming kernel (KT 64)
+    (2, 64, 128, 3, 2, 1, 20, 20),   # 1x1 128 -> 128: streaming kernel, two column tiles (KT 128)
+    (2, 16, 16, 3, 1, 3, 20, 20),    # 16-channel 3x3: the implicit GEMM would stage x9 -> written first (no fusion)
+]
+
+
+@pytest.mark.parametrize("n,c1,c,k1,s1,k2,h,w", FWD_CASES)
+def test_fwd_bnact_matches_unfused(n, c1, c, k1, s1, k2, h, w):
+    """Bitwise: the fused forward stages exactly the bf16 values adr_affine_act stores and runs the plain forward's
+    tiling, so outputs, the side-written z, every gradient and the running statistics equal the unfused pair's."""
+    from adrefine.nn.modules.conv import Conv
+    torch.manual_seed(1)
+    p = Conv(c1, c, k1, s1).cuda().train()
+    q = Conv(c, c, k2, 1).cuda().train()
+    with torch.no_grad():
+        for m in (p, q):
+            m.bn.weight.uniform_(0.5, 1.5)
+            m.bn.bias.uniform_(-0.3, 0.3)
+    x = (torch.randn(n, c1, h, w, device="cuda") * 1.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    ho, wo = (h + 2 * (k1 // 2) - k1) // s1 + 1, (w + 2 * (k1 // 2) - k1) // s1 + 1
+    g = torch.randn(n, c, ho, wo, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    a = _pair_run(p, q, x, g, True)
+    b = _pair_run(p, q, x, g, False)
+    names = ("out", "z", "dx", "dw1", "dgamma1", "dbeta1", "dw2", "dgamma2", "dbeta2", "rm1", "rv1", "rm2")
+    for name, u, v in zip(names, a, b):
+        assert torch.equal(u, v), (name, float((u.float() - v.float()).abs().max()))
+
+
+def test_fwd_bnact_other_reader_writes_first():
+    """A pending BN-act output read by anything but its consumer conv (here a channel slice through an elementwise
+    kernel) is written first, so the reader sees the true activation."""
+    from adrefine import kernels as K
+    from adrefine.nn.modules.conv import Conv
+    torch.manual_seed(2)
+    p = Conv(32, 32, 3, 1).cuda().train()
+    x = torch.randn(2, 32, 16, 16, device="cuda").to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    z_ref = p(x).detach().clone()
+    z = p(x, lazy=True)
+    assert K._BNF_PENDING
+    s = K.act(z[:, 8:24], "relu")  # another reader of a view of z
+    assert not K._BNF_PENDING
+    assert torch.equal(z.detach(), z_ref) and torch.equal(s.detach(), torch.relu(z_ref[:, 8:24]))
+
+
+def test_fwd_bnact_whole_net_step():
+    """One bf16 train step of the 701 graph at 320^2 bs 2 with and without the forward fusion (11 Conv -> Conv
+    pairs: the bottlenecks and the Conv layers feeding C3k2 cv1): same loss, bitwise parameter gradients."""
+    from adrefine import kernels as K
+    from adrefine.nn.tasks import DetectionModel
+    from conftest import ROOT
+    from gpu_util import load_recipe_into
+    from recipe import synthetic_images
+    m = DetectionModel(str(ROOT / "tests/configs/yolo11-701-YOLO-AD-Refine.yaml"), compute_dtype=torch.bfloat16)
+    load_recipe_into(m)
+    m = m.cuda().train()
+    img = synthetic_images(2, 320, seed=3).cuda()
+    batch = {"img": img, "batch_idx": torch.tensor([0., 0., 1.]), "cls": torch.tensor([[1.], [5.], [7.]]),
+             "bboxes": torch.tensor([[0.5, 0.5, 0.3, 0.4], [0.2, 0.3, 0.1, 0.2], [0.6, 0.6, 0.5, 0.3]])}
+    runs = []
+    for fused in (True, False):
+        old = K.BN_XF_FWD
+        K.BN_XF_FWD = fused
+        try:
+            sd = {k: v.clone() for k, v in m.state_dict().items()}
+            loss, _ = m(batch)
+            loss.backward()
+            runs.append((float(loss), {n: p.grad.clone() for n, p in m.named_parameters() if p.grad is not None},
+                         {k: v.clone() for k, v in m.state_dict().items()}))
+            m.zero_grad(set_to_none=True)
+            m.load_state_dict(sd)
+        finally:
+            K.BN_XF_FWD = old
+    (la, ga, sa), (lb, gb, sb) = runs
+    assert la == lb
+    bad = [n for n in ga if not torch.equal(ga[n], gb[n])]
+    assert not bad, bad[:10]
+    bad = [k for k in sa if not torch.equal(sa[k], sb[k])]
+    assert not bad, bad[:10]

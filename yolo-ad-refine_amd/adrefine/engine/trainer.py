@@ -153,6 +153,7 @@ class FusedTrainer:
         bounds = [[None, None] for _ in range(nst)]
         for name, p, _, _ in self.entries:
             p._adr_grad = self.grad[off:off + p.numel()]
+            p._adr_arena, p._adr_goff = self.grad, off  # (the concurrent head levels' gradient slabs use the offset)
             p._adr_used = False
             self._goff.append(off)
             s = stage_of(layer_of(name), self.cuts)

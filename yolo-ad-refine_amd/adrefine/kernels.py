@@ -230,8 +230,11 @@ def _req_cuda(t: torch.Tensor):
 
 
 def nhwc(t: torch.Tensor):
-    """(tensor, ptr, cstride) for a logical NCHW tensor whose memory is an NHWC view; re-lays out otherwise."""
+    """(tensor, ptr, cstride) for a logical NCHW tensor whose memory is an NHWC view; re-lays out otherwise. A
+    BN-act output still pending for its consumer conv (BnFwd) is written first when anything else reads it."""
     _req_cuda(t)
+    if _BNF_PENDING:
+        _bnf_settle(t)
     n, c, h, w = t.shape
     s0, s1, s2, s3 = t.stride()
     ok = (s1 == 1 or c == 1) and (s2 == w * s3 or h == 1) and (s0 == h * w * s3 or n == 1)
@@ -280,10 +283,11 @@ def sink(t, g):
         gc = gc.contiguous()
     if gc.numel() != tgt.numel():
         raise RuntimeError("sink: gradient size mismatch")
-    if _DEFER is not None and _TIMING is None:
-        _DEFER.add_axpy(gc, tgt._adr_grad.data_ptr(), gc.numel())
+    dst = _grad_buf(tgt)
+    if _dfr() is not None and _TIMING is None:
+        _dfr().add_axpy(gc, dst.data_ptr(), gc.numel())
     else:
-        lib.adr_axpy(gc.numel(), 1.0, fptr(gc), fptr(tgt._adr_grad), stream())
+        lib.adr_axpy(gc.numel(), 1.0, fptr(gc), fptr(dst), stream())
     tgt._adr_used = True
     return None
 
@@ -297,7 +301,7 @@ def grad_dst(t, numel, device):
         if tgt.numel() != numel:
             raise RuntimeError("grad_dst: gradient size mismatch")
         tgt._adr_used = True
-        return None, fptr(tgt._adr_grad), 1
+        return None, fptr(_grad_buf(tgt)), 1
     out = torch.empty(numel, dtype=torch.float32, device=device)
     return out, fptr(out), 0
 
@@ -386,7 +390,7 @@ def sink_unpack(t, dw_krsc, shape, cpad=0):
     RS = 1
     for d in shape[2:]:
         RS *= d
-    lib.adr_unpack_weight_grad(fptr(dw_krsc), fptr(tgt._adr_grad), K_, C_, max(C_, cpad), RS, 0, 1, stream())
+    lib.adr_unpack_weight_grad(fptr(dw_krsc), fptr(_grad_buf(tgt)), K_, C_, max(C_, cpad), RS, 0, 1, stream())
     tgt._adr_used = True
     return None
 
@@ -510,6 +514,7 @@ def conv_fwd_fp8(d, xp, w, Cw, Cp, bias, yp, stats):
         st = [torch.zeros(nb, dtype=torch.float32, device=dev), torch.zeros(nb, dtype=torch.float32, device=dev)]
         w._adr_fp8 = st
         lib.adr_amax_bf16(ctypes.c_void_p(xp), d.x_cstride, 0, d.n * d.h * d.w, d.c, fptr(st[0]), stream())
+        _ready()
     w8 = torch.empty(K_ * RS * Cp, dtype=torch.uint8, device=dev)
     winv = torch.empty(K_, dtype=torch.float32, device=dev)
     lib.adr_pack_weight_fp8(fptr(w.detach().float().contiguous()), K_, Cw, Cp, RS, fptr(w8), fptr(winv), fptr(st[0]),
@@ -707,88 +712,9 @@ class AxpyEntry(ctypes.Structure):
     _fields_ = [("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("n", ctypes.c_long)]
 
 
-# Off by default: measured on the bench step (hipGraph replay) the forked branch runs on other hardware queues and
-# the cross-queue waits cost more than the overlap wins (26.72 ms/step off vs 27.32 on, 28.65 with a fork per
-# WGRAD) — kept as an option (ADR_SIDE_STREAM=1), bitwise equal to the inline order (scripts/side_diff.py)
-_SIDE_ON = bool(int(__import__("os").environ.get("ADR_SIDE_STREAM", "0")))
-_SIDE_GROUP = int(__import__("os").environ.get("ADR_SIDE_GROUP", "8"))
-_SIDE_KINDS = set(__import__("os").environ.get("ADR_SIDE_KINDS", "wgrad,bias,dcn,stem,flush").split(","))
-_SIDE_STREAMS = {}
-
-
-class SideWork:
-    """Parameter-gradient work that nothing in the backward chain waits for — the conv WGRAD split-K GEMMs, bias
-    sums, the DCN weight gradient and the deferred arena reductions — forked onto a second stream: each fork makes
-    the side stream wait for everything enqueued so far on the current stream (dy and x are complete), and
-    `join()` makes the current stream wait for the side stream (before the DDP bucket all-reduce / optimizer read
-    the arena). The WGRADs then overlap the dgrad / BN-backward chain, whose many small launches leave most of
-    the chip idle. Captured into the same hipGraph as a forked branch. The tensors a forked launch reads stay
-    referenced until the join, so the caching allocator cannot hand their memory to the main stream while the
-    side stream may still read it. Arena slices written on the side stream belong to parameters whose every
-    gradient contribution goes through this path (conv / DCN weights and conv biases)."""
-
-    def __init__(self, device):
-        st = _SIDE_STREAMS.get(device)
-        if st is None:
-            st = _SIDE_STREAMS[device] = torch.cuda.Stream(device)
-        self.s, self.keep, self.used, self.pending, self.main = st, [], False, [], None
-        self.stores = set()  # storages of the kept tensors (guard_write)
-
-    def _hold(self, keep):
-        self.keep.extend(keep)
-        for t in keep:
-            self.stores.add(t.untyped_storage().data_ptr())
-
-    def guard_write(self, t):
-        """Before the current stream modifies `t` in place (FanOutFn adds into an exclusive concat-gradient slice
-        that an AddFn may also have handed to a conv as its dy): if side work reads t's storage, join first."""
-        if (self.used or self.pending) and t.untyped_storage().data_ptr() in self.stores:
-            self.join()
-
-    def fork(self, *keep):
-        self._hold(keep)
-        cur = torch.cuda.current_stream()
-        if cur == self.s:  # already on the side stream (a flush from inside side work): catch up with main
-            if self.main is not None:
-                self.s.wait_stream(self.main)
-            return _nullctx()
-        self.main = cur
-        self.s.wait_stream(cur)
-        self.used = True
-        return torch.cuda.stream(self.s)
-
-    def submit(self, fn, *keep):
-        """Queue side work; every _SIDE_GROUP submissions go out behind one fork (fewer cross-stream edges)."""
-        self._hold(keep)
-        self.pending.append(fn)
-        if len(self.pending) >= _SIDE_GROUP:
-            self.drain()
-
-    def drain(self):
-        if self.pending:
-            fns, self.pending = self.pending, []
-            with self.fork():
-                for fn in fns:
-                    fn()
-
-    def join(self):
-        self.drain()
-        if self.used:
-            torch.cuda.current_stream().wait_stream(self.s)
-            self.keep, self.used = [], False
-            self.stores = set()
-
-
 def _nullctx():
     import contextlib
     return contextlib.nullcontext()
-
-
-def _side(kind):
-    """The active side stream for parameter-gradient work of this kind (None: run inline)."""
-    if _DEFER is None or _TIMING is not None or _DEFER.side is None or kind not in _SIDE_KINDS:
-        return None
-    return _DEFER.side
 
 
 class WgradDeferral:
@@ -796,11 +722,9 @@ class WgradDeferral:
     and runs them as a few batched launches (adr_wgrad_reduce_batched) when the backward pass ends, instead of
     one launch per conv. The partial slabs stay alive until then. A second entry for the same destination (a
     weight shared by several calls, e.g. the head's shared convs) flushes the pending batch first, so every
-    destination's contributions still accumulate in program order. With a SideWork, the flush runs on the side
-    stream (behind the WGRADs that produced the slabs)."""
+    destination's contributions still accumulate in program order."""
 
-    def __init__(self, side=None):
-        self.side = side
+    def __init__(self):
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
         self.axpys, self.akeep, self.adsts = [], [], set()
@@ -867,15 +791,7 @@ class WgradDeferral:
         self.dsts.add(dst)
 
     def flush(self):
-        if self.side is not None:
-            self.side.drain()  # queued WGRADs add their entries first
-        if self.side is not None and "flush" in _SIDE_KINDS and (self.entries or self.psums or self.axpys):
-            # sources allocated on the current stream (a sink()'s temporary, a main-stream WGRAD's slabs) must
-            # outlive the side-stream reads: the side stream holds them until the join
-            with self.side.fork(*self.keep, *self.pkeep, *self.akeep, *self.ckeep, *self.gkeep, *self.dkeep):
-                self._flush()
-        else:
-            self._flush()
+        self._flush()
 
     def _flush(self):
         if self.dots:  # before the axpys that add their outputs into the arena
@@ -909,7 +825,7 @@ class WgradDeferral:
 
 def _defer_dot(param, x, dy):
     """Whether sum(x * dy) for a scalar parameter gradient can go to the deferral's batched flush."""
-    return (_DEFER_DOT and _DEFER is not None and _TIMING is None and _DEFER.side is None and
+    return (_DEFER_DOT and _dfr() is not None and _TIMING is None and
             _target(param) is not None and dy.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and
             dy.shape[1] % 8 == 0 and _v(dy)[2] % 8 == 0 and _v(x)[2] % 8 == 0 and _v(dy)[1] % 16 == 0 and
             _v(x)[1] % 16 == 0)
@@ -925,23 +841,226 @@ DEFER_MAX_BYTES = int(__import__("os").environ.get("ADR_DEFER_MAX_BYTES", 1 << 6
 
 
 def defer_wgrad():
-    """Context manager: defer arena-bound WGRAD reductions to one batched flush at exit."""
+    """Context manager: defer arena-bound WGRAD reductions to one batched flush at exit. Work the backward ran on
+    the concurrent head-level streams is joined first (their deferrals flushed on their own streams, the current
+    stream waits for them, their gradient slabs folded into the arena in the serial order: _join_levels)."""
     import contextlib
 
     @contextlib.contextmanager
     def _cm():
         global _DEFER
-        dev = torch.cuda.current_device()
-        prev, _DEFER = _DEFER, WgradDeferral(SideWork(dev) if _SIDE_ON else None)
+        prev, _DEFER = _DEFER, WgradDeferral()
         try:
             yield _DEFER
+            _join_levels()
             _DEFER.flush()
-            if _DEFER.side is not None:
-                _DEFER.side.join()
         finally:
             _DEFER = prev
+            _DEFER_LVL.clear()
+            _SLAB_USE.clear()
             bnxf_clear()
     return _cm()
+
+
+# ---------------------------------------------------------------------------------------------------------
+# Concurrent AYHead levels. The head runs the same chain of ~70 small kernels per pyramid level (head.py:1132 loops
+# the levels); at P4 (40x40) and P5 (20x20) those kernels fill a fraction of the chip. run_levels() runs each level
+# on its own stream (forked from and joined back into the current stream; inside a hipGraph capture the branches
+# become parallel graph branches), and autograd runs every backward op on its forward op's stream, so the levels'
+# backward chains overlap the same way. What the levels share is handled here:
+#   * shared parameters (share_conv, the decompositions, cross-task, DCN, ...): every arena write made on a level
+#     stream goes to that stream's gradient slab (_grad_buf); at the end of the backward the slabs are folded into
+#     the arena in the order the serial path accumulates them (first-use order per parameter), so the arena is
+#     bitwise the serial one;
+#   * deferred reductions: one WgradDeferral per level stream (_dfr), flushed on that stream;
+#   * BatchNorm running statistics of a shared BN (CoordAtt.bn1): updated at the forward join, in level order;
+#   * the level input's fan-out gradient sink: the level reads a fresh view (_LevelIn), so its input gradient
+#     returns through autograd (stream-synchronised) instead of being accumulated into a buffer the main stream
+#     also writes;
+#   * tensors crossing streams are record_stream()-ed so the caching allocator never hands their memory to the
+#     other stream early.
+# ADR_LEVEL_STREAMS=0 runs the levels serially on the current stream (A/B, timing mode).
+# ---------------------------------------------------------------------------------------------------------
+LEVEL_STREAMS = bool(int(__import__("os").environ.get("ADR_LEVEL_STREAMS", "1")))
+_LVL_STREAMS = {}   # device index -> [torch.cuda.Stream]
+_LVL_IDS = {}       # stream handle -> torch.cuda.Stream (every level stream ever created)
+_DEFER_LVL = {}     # level stream handle -> WgradDeferral (during a deferred backward)
+_SLABS = {}         # level stream handle -> fp32 gradient slab (arena-sized, zero between backwards)
+_SLABS_RETIRED = []
+_SLAB_USE = []      # (stream handle, arena, offset, numel) in first-use order
+_SLAB_SEEN = set()
+_LVL_BN = []        # deferred running-statistics updates of BatchNorms run on level streams (forward order)
+_LVL_FORKED = {}    # level streams forked since the last backward join (handle -> stream)
+
+
+def _cur_sid():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _on_level_stream():
+    return bool(_LVL_IDS) and _cur_sid() in _LVL_IDS
+
+
+def _dfr():
+    """The active WgradDeferral for the current stream (a level stream gets its own)."""
+    if _DEFER is None:
+        return None
+    if _LVL_IDS:
+        sid = _cur_sid()
+        if sid in _LVL_IDS:
+            d = _DEFER_LVL.get(sid)
+            if d is None:
+                d = _DEFER_LVL[sid] = WgradDeferral()
+            return d
+    return _DEFER
+
+
+def _grad_buf(tgt):
+    """The gradient destination of arena parameter tgt for the current stream: its arena slice, or on a level
+    stream the same offsets of that stream's slab."""
+    if _LVL_IDS:
+        sid = _cur_sid()
+        if sid in _LVL_IDS:
+            arena, off, n = tgt._adr_arena, tgt._adr_goff, tgt.numel()
+            slab = _SLABS.get(sid)
+            if slab is None or slab.numel() < arena.numel():
+                if slab is not None:
+                    _SLABS_RETIRED.append(slab)
+                slab = _SLABS[sid] = torch.zeros(arena.numel(), dtype=torch.float32, device=arena.device)
+                _ready()
+            if (sid, arena.data_ptr(), off) not in _SLAB_SEEN:
+                _SLAB_SEEN.add((sid, arena.data_ptr(), off))
+                _SLAB_USE.append((sid, arena, off, n))
+            return slab[off:off + n]
+    return tgt._adr_grad
+
+
+def _ready():
+    """A persistent buffer just initialised on a level stream is read by the other levels' streams: wait for it
+    (eager warm-up only; never inside a graph capture, where it already exists)."""
+    if _on_level_stream() and not torch.cuda.is_current_stream_capturing():
+        torch.cuda.current_stream().synchronize()
+
+
+def level_streams(dev, n):
+    key = torch.device(dev).index
+    lst = _LVL_STREAMS.setdefault(key, [])
+    while len(lst) < n:
+        st = torch.cuda.Stream(dev)
+        lst.append(st)
+        _LVL_IDS[st.cuda_stream] = st
+    return lst[:n]
+
+
+def _levels_on(xs):
+    return (LEVEL_STREAMS and len(xs) > 1 and all(isinstance(x, torch.Tensor) and x.is_cuda for x in xs) and
+            _TIMING is None and not NORM_FIN and not _on_level_stream())
+
+
+class _LevelIn(torch.autograd.Function):
+    """Identity at the fork (on the forking stream): a fresh view without the fan-out sink; the gradient coming back
+    from the level stream is marked as used on this stream."""
+
+    @staticmethod
+    def forward(ctx, x):
+        ctx.set_materialize_grads(False)
+        return x[:, :]
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None:
+            g.record_stream(torch.cuda.current_stream())
+        return g
+
+
+class _LevelOut(torch.autograd.Function):
+    """Identity at the end of a level (on the level stream): the gradient arriving from the joined stream is marked
+    as used on the level stream."""
+
+    @staticmethod
+    def forward(ctx, y):
+        ctx.set_materialize_grads(False)
+        return y[:, :]
+
+    @staticmethod
+    def backward(ctx, g):
+        if g is not None:
+            g.record_stream(torch.cuda.current_stream())
+        return g
+
+
+def run_levels(fn, xs):
+    """[fn(i, xs[i]) for each level], each level on its own stream when enabled (see above); the results are ready
+    on the current stream when this returns."""
+    if not _levels_on(xs):
+        return [fn(i, x) for i, x in enumerate(xs)]
+    main = torch.cuda.current_stream()
+    sts = level_streams(xs[0].device, len(xs))
+    ins = [_LevelIn.apply(x) for x in xs]
+    outs = []
+    for i, (x, st) in enumerate(zip(ins, sts)):
+        _LVL_FORKED[st.cuda_stream] = st
+        st.wait_stream(main)
+        x.record_stream(st)
+        with torch.cuda.stream(st):
+            y = fn(i, x)
+            outs.append(_LevelOut.apply(y) if isinstance(y, torch.Tensor) else y)
+    for y, st in zip(outs, sts):
+        main.wait_stream(st)
+        if isinstance(y, torch.Tensor):
+            y.record_stream(main)
+    _flush_level_bn()
+    return outs
+
+
+def _flush_level_bn():
+    """Running-statistics updates of BatchNorms that ran on level streams, in forward (level) order on the current
+    stream: the same adr_bn_finalize arithmetic over the saved partial statistics, coefficients discarded."""
+    if not _LVL_BN:
+        return
+    for stats, P, C, count, gamma, beta, rm, rv, momentum, eps in _LVL_BN:
+        dev = stats.device
+        stats.record_stream(torch.cuda.current_stream())  # written on a level stream, read here
+        scr = torch.empty(4 * C, dtype=torch.float32, device=dev)
+        lib.adr_bn_finalize(fptr(stats), P, C, float(count), fptr(gamma.detach()), fptr(beta.detach()), fptr(rm),
+                            fptr(rv), float(momentum), float(eps), 1, fptr(scr[:C]), fptr(scr[C:2 * C]),
+                            fptr(scr[2 * C:3 * C]), fptr(scr[3 * C:]), stream())
+    _LVL_BN.clear()
+
+
+def _join_levels():
+    """End of a deferred backward: flush each level stream's deferral on that stream, make the current stream wait
+    for the level streams, then fold the gradient slabs into the arena (adr_axpy_zero_batched, which also clears
+    them). A parameter that several levels contributed to receives the contributions in first-use order — the
+    order in which the serial path accumulated them — one batched launch per rank."""
+    if not _LVL_IDS:
+        return
+    main = torch.cuda.current_stream()
+    for sid, d in list(_DEFER_LVL.items()):
+        with torch.cuda.stream(_LVL_IDS[sid]):
+            d.flush()
+    used = {e[0] for e in _SLAB_USE} | set(_DEFER_LVL) | set(_LVL_FORKED)
+    for sid in used:
+        main.wait_stream(_LVL_IDS[sid])
+    _DEFER_LVL.clear()
+    _LVL_FORKED.clear()
+    if not _SLAB_USE:
+        return
+    ranks = {}
+    rounds = []
+    for sid, arena, off, n in _SLAB_USE:
+        key = (arena.data_ptr(), off)
+        r = ranks.get(key, 0)
+        ranks[key] = r + 1
+        while len(rounds) <= r:
+            rounds.append([])
+        slab = _SLABS[sid]
+        rounds[r].append(AxpyEntry(slab.data_ptr() + 4 * off, arena.data_ptr() + 4 * off, n))
+    for ents in rounds:
+        arr = (AxpyEntry * len(ents))(*ents)
+        lib.adr_axpy_zero_batched(ctypes.cast(arr, ctypes.c_void_p), len(ents), stream())
+    _SLAB_USE.clear()
+    _SLAB_SEEN.clear()
 
 
 def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device, keep=()):
@@ -954,10 +1073,6 @@ def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device, keep=()):
     RS_ = 1
     for v in wshape[2:]:
         RS_ *= v
-    side = _side("wgrad") if keep and _target(param) is not None else None
-    if side is not None:  # arena destination: the GEMM and its deferred reduction run on the side stream
-        side.submit(lambda: _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device), *keep)
-        return None
     return _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device)
 
 
@@ -978,8 +1093,8 @@ def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device):
     _t1(tok)
     Cp = max(C_, cpad)
     out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
-    if _DEFER is not None and acc and _TIMING is None and splits * stride * 4 <= DEFER_MAX_BYTES:
-        _DEFER.add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
+    if _dfr() is not None and acc and _TIMING is None and splits * stride * 4 <= DEFER_MAX_BYTES:
+        _dfr().add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
         return grad_ret(param, out)
     tok = _t0("adr::wgrad_reduce_kernel<true, OUT, SL> (split reduce + unpack)",
               4 * stride * (splits + 1), stride * splits, shp)
@@ -990,11 +1105,7 @@ def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device):
 
 def _bias_grad(dy, K, N, HW, cs, param=None):
     """Per-channel sum of dy. With `param`, accumulates into its gradient destination (grad_dst) and returns
-    the autograd value; otherwise returns a fresh (K,) tensor. Arena destinations run on the side stream."""
-    side = _side("bias") if param is not None and _target(param) is not None else None
-    if side is not None:
-        side.submit(lambda: _bias_grad1(dy, K, N, HW, cs, param), dy)
-        return None
+    the autograd value; otherwise returns a fresh (K,) tensor."""
     return _bias_grad1(dy, K, N, HW, cs, param)
 
 
@@ -1002,25 +1113,66 @@ def _bias_grad1(dy, K, N, HW, cs, param=None):
     dt = dcode(dy.dtype)
     chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
     part = torch.empty(N * chunks * 2 * K, dtype=torch.float32, device=dy.device)
-    if param is not None and _DEFER is not None and _TIMING is None and _DEFER_COLSUM and dt == BF16 and \
-            dy.data_ptr() % 16 == 0 and cs % 8 == 0 and K % 8 == 0 and _DEFER.side is None and \
+    if param is not None and _dfr() is not None and _TIMING is None and _DEFER_COLSUM and dt == BF16 and \
+            dy.data_ptr() % 16 == 0 and cs % 8 == 0 and K % 8 == 0 and \
             _target(param) is not None:  # an arena destination: column sums and partial sums at the flush, batched
         db, p, acc = grad_dst(param, K, dy.device)
-        _DEFER.add_colsum(dy, part, cs, N, HW, K, _stats_rows(N, HW), chunks)
-        _DEFER.add_psum(part, N * chunks, K, 0, p, acc)
+        _dfr().add_colsum(dy, part, cs, N, HW, K, _stats_rows(N, HW), chunks)
+        _dfr().add_psum(part, N * chunks, K, 0, p, acc)
         return grad_ret(param, db)
     lib.adr_nc_reduce(dt, 0, ctypes.c_void_p(dy.data_ptr()), cs, 0, None, 0, 0, None, None, 0, 0, N, HW, K,
                       _stats_rows(N, HW), fptr(part), stream())
     if param is not None:
         db, p, acc = grad_dst(param, K, dy.device)
-        if _DEFER is not None and acc and _TIMING is None:
-            _DEFER.add_psum(part, N * chunks, K, 0, p, acc)
+        if _dfr() is not None and acc and _TIMING is None:
+            _dfr().add_psum(part, N * chunks, K, 0, p, acc)
         else:
             lib.adr_partial_sum(fptr(part), N * chunks, K, 0, p, acc, stream())
         return grad_ret(param, db)
     db = torch.empty(K, dtype=torch.float32, device=dy.device)
     lib.adr_partial_sum(fptr(part), N * chunks, K, 0, fptr(db), 0, stream())
     return db
+
+
+def _conv_fwd_bnact(ctx, pend, w, stride, pad, want_stats, box):
+    """Conv2dFn's forward on a pending BN-act input (BnFwd): one adr_conv2d_fwd_bf16_bnact launch reads y, applies
+    z = act(y * s + t) while staging, side-writes z and computes the conv (+ BN partial statistics). Returns
+    (None, None) when the fused kernel would stage each element more than BN_XF_MAX_REUSE / 100 times (then the
+    caller writes z first and runs the plain conv)."""
+    z = pend.z
+    y, yp, ycs = nhwc(pend.y)
+    N, C, H, W = y.shape
+    K, Cw, R, S = w.shape
+    if Cw != C:
+        raise RuntimeError(f"Conv2dFn: input has {C} channels, weight expects {Cw}")
+    (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
+    Ho, Wo = (H + 2 * ph - R) // sh + 1, (W + 2 * pw - S) // sw + 1
+    d, Ho, Wo = conv_desc(N, H, W, C, ycs, K, R, S, sh, sw, ph, pw, K, torch.bfloat16)
+    if not _engine2(d, d.c) or lib.adr_conv2d_bf16_xf_reuse(ctypes.byref(d), 0) > BN_XF_FWD_MAX_REUSE:
+        pend.materialize()
+        return None, None
+    wp, wt = pack_weight2(w, torch.bfloat16)
+    out, op, ocs = _out_view(box, N, K, Ho, Wo, torch.bfloat16, y.device)
+    d.y_cstride = ocs
+    stats = None
+    if want_stats:
+        stats = torch.empty(lib.adr_conv2d_fwd_bf16_bnact_stat_tiles(ctypes.byref(d)) * 2 * K, dtype=torch.float32,
+                            device=y.device)
+    st = pend.struct()
+    pend.done()
+    sym = "" if _TIMING is None else _conv2_symbol(d, 2)
+    tok = _t0(sym, *_conv_work(d), _shape(d, "fwd+bnact") if _TIMING is not None else "")
+    lib.adr_conv2d_fwd_bf16_bnact(ctypes.byref(d), ctypes.c_void_p(yp), ctypes.c_void_p(wp.data_ptr()),
+                                  ctypes.c_void_p(op), fptr(stats), ctypes.byref(st), stream())
+    _t1(tok)
+    ctx.act = None
+    ctx.save_for_backward(z, wp, wt, None)
+    ctx.meta = (stride, pad, 0, w.shape, False)
+    ctx.pw, ctx.pb = w, None
+    if stats is None:
+        stats = torch.empty(0, device=y.device)
+    ctx.mark_non_differentiable(stats)
+    return (out if box is None else out[:, :]), stats
 
 
 class Conv2dFn(torch.autograd.Function):
@@ -1032,6 +1184,15 @@ class Conv2dFn(torch.autograd.Function):
         sink = getattr(x, "_adr_sink", None)
         ctx.sink = sink if sink is not None and sink.fits(x) else None
         dtype = x.dtype
+        pend = _bnf_of(x)  # x = act(bn(y)) not written yet: stage y through the BN-act here
+        if pend is not None and not (b is None and act is None and bnfin is None and cpad == 0 and not CONV_FP8):
+            pend.materialize()
+            pend = None
+        if pend is not None:
+            y, stats = _conv_fwd_bnact(ctx, pend, w, stride, pad, want_stats, box)
+            if y is not None:
+                return y, stats
+            pend = None
         x, xp, xcs = nhwc(x)
         N, C, H, W = x.shape
         K, Cw, R, S = w.shape
@@ -1162,7 +1323,8 @@ class BNActFn(torch.autograd.Function):
     """act(BatchNorm2d(y)) — train mode uses batch statistics (from the conv epilogue when given)."""
 
     @staticmethod
-    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None, bnfin=None, xfuse=False):
+    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None, bnfin=None, xfuse=False,
+                lazy=False):
         dtype = y.dtype
         y, yp, ycs = nhwc(y)
         N, C, H, W = y.shape
@@ -1195,12 +1357,22 @@ class BNActFn(torch.autograd.Function):
                     P = stats.numel() // (2 * C)
                 else:
                     P = 0
+                # on a concurrent head-level stream the running statistics of a shared BN are updated at the join,
+                # in level order (run_levels / _flush_level_bn)
+                lvl = training and rm is not None and _on_level_stream()
+                if lvl:
+                    _LVL_BN.append((stats, P, C, N * HW, gamma, beta, rm, rv, momentum, eps))
                 lib.adr_bn_finalize(fptr(stats) if training else None, P, C, float(N * HW), fptr(gamma.detach()),
-                                    fptr(beta.detach()), fptr(rm), fptr(rv), float(momentum), float(eps),
-                                    int(training), fptr(scale), fptr(shift), fptr(mean), fptr(rstd), stream())
+                                    fptr(beta.detach()), None if lvl else fptr(rm), None if lvl else fptr(rv),
+                                    float(momentum), float(eps), int(training), fptr(scale), fptr(shift), fptr(mean),
+                                    fptr(rstd), stream())
         z, zp, zcs = _out_view(box, N, C, H, W, dtype, dev)
-        lib.adr_affine_act(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(zp), zcs, 0,
-                           fptr(scale), fptr(shift), 0, ACT[act], N, HW, C, stream())
+        if lazy and box is None and BN_XF_FWD and training and dtype == torch.bfloat16 and act in ("silu", "none") \
+                and C % 8 == 0 and C <= 512:
+            BnFwd(y, scale, shift, act, z).attach()  # z is written by its consumer conv (or on first other read)
+        else:
+            lib.adr_affine_act(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(zp), zcs, 0,
+                               fptr(scale), fptr(shift), 0, ACT[act], N, HW, C, stream())
         ctx.save_for_backward(y, scale, shift, mean, rstd, gamma)
         ctx.meta = (act, training)
         ctx.pbeta = beta
@@ -1243,7 +1415,7 @@ class BNActFn(torch.autograd.Function):
         else:
             pend.materialize(dy)
         return (dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None, None, None,
-                None, None)
+                None, None, None)
 
 
 # Training Conv-BN-act backward fusion: BNActFn.backward computes the coefficients (nc_reduce + bn_bwd_finalize)
@@ -1259,6 +1431,78 @@ BN_XF_MAX_REUSE = int(__import__("os").environ.get("ADR_BN_XF_MAX_REUSE", "150")
 # cannot be reused by another tensor while the entry exists; entries nobody consumed (a frozen producing conv) are
 # dropped at the end of the backward (defer_wgrad's exit, bnxf_clear)
 _BNXF_PENDING = {}
+
+
+# Training Conv-BN-act forward fusion: BNActFn (lazy) computes the batch statistics and coefficients but leaves
+# z = act(y * s + t) unwritten; the consumer conv (Conv2dFn) stages y through the transform
+# (adr_conv2d_fwd_bf16_bnact: streaming 1x1 / 3x3 halo tiles / implicit GEMM) and side-writes z once for the
+# layer's weight gradient — the affine_act pass (a read of y, a launch) disappears. Taken where the consumer stages
+# each element about once (BN_XF_MAX_REUSE); any other reader of a pending z writes it first (nhwc -> _bnf_settle).
+# ADR_BN_XF_FWD=0 disables.
+BN_XF_FWD = bool(int(__import__("os").environ.get("ADR_BN_XF_FWD", "1")))
+# the forward transform is one affine + activation per staged element (the backward's needs a second operand and
+# the BN-backward linear term): two column tiles of the streaming 1x1 kernel still qualify
+BN_XF_FWD_MAX_REUSE = 200
+_BNF_PENDING = {}  # storage data_ptr -> BnFwd
+
+
+class BnFwd:
+    """A pending BN-act forward: z (allocated, unwritten) = act(y * scale + shift)."""
+    __slots__ = ("y", "scale", "shift", "act", "z", "key")
+
+    def __init__(self, y, scale, shift, act, z):
+        self.y, self.scale, self.shift, self.act, self.z = y, scale, shift, act, z
+        self.key = z.untyped_storage().data_ptr()
+
+    def attach(self):
+        _BNF_PENDING[self.key] = self
+
+    def done(self):
+        _BNF_PENDING.pop(self.key, None)
+
+    def materialize(self):
+        self.done()
+        y, yp, ycs = nhwc(self.y)
+        z, zp, zcs = nhwc(self.z)
+        N, C, H, W = y.shape
+        lib.adr_affine_act(dcode(y.dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(zp), zcs, 0, fptr(self.scale),
+                           fptr(self.shift), 0, ACT[self.act], N, H * W, C, stream())
+
+    def struct(self):
+        _, yp, ycs = nhwc(self.y)
+        return BnXfStruct(yp, self.scale.data_ptr(), self.shift.data_ptr(), None, None, None, self.z.data_ptr(), ycs,
+                          self.z.stride(1) if self.z.shape[1] == 1 else self.z.stride(3), ACT[self.act], 0)
+
+
+def _bnf_settle(t):
+    """Write a pending BN-act output before t (it, or a view of its storage) is read."""
+    try:
+        key = t.untyped_storage().data_ptr()
+    except RuntimeError:
+        return
+    p = _BNF_PENDING.get(key)
+    if p is not None:
+        p.materialize()
+
+
+def _bnf_of(x):
+    """The pending BN-act forward whose output is exactly x (whole tensor, same view), or None. A partial view of a
+    pending output is written first (nhwc) instead."""
+    if not _BNF_PENDING or not x.is_cuda:
+        return None
+    p = _BNF_PENDING.get(x.untyped_storage().data_ptr())
+    if p is None:
+        return None
+    z = p.z
+    if x.data_ptr() == z.data_ptr() and x.shape == z.shape and x.stride() == z.stride():
+        return p
+    return None
+
+
+def bnf_clear():
+    """Write every pending BN-act output (end of a forward: nothing may stay unwritten)."""
+    for p in list(_BNF_PENDING.values()):
+        p.materialize()
 
 
 def bnxf_clear():
@@ -1330,7 +1574,7 @@ _DEFER_GN = bool(int(__import__("os").environ.get("ADR_DEFER_GN", "1")))  # 0: G
 
 def _defer_gn(acc):
     """Whether a GroupNorm dgamma / dbeta reduction goes to the deferral's batched flush (arena destinations)."""
-    return bool(acc) and _DEFER_GN and _DEFER is not None and _TIMING is None and _DEFER.side is None
+    return bool(acc) and _DEFER_GN and _dfr() is not None and _TIMING is None
 
 
 class GNActFn(torch.autograd.Function):
@@ -1404,7 +1648,7 @@ class GNActFn(torch.autograd.Function):
             if acc_g != acc_b:
                 raise RuntimeError("GN gamma/beta gradients must share one destination kind")
             if _defer_gn(acc_g):
-                _DEFER.add_gnparam(part, mean, rstd, pg, pb, N, 1, C, groups, acc_g)
+                _dfr().add_gnparam(part, mean, rstd, pg, pb, N, 1, C, groups, acc_g)
             else:
                 lib.adr_gn_param_grad(fptr(part), N, C, groups, fptr(mean), fptr(rstd), pg, pb, acc_g, stream())
             return dy, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None
@@ -1419,7 +1663,7 @@ class GNActFn(torch.autograd.Function):
         Cc = torch.empty(N * C, dtype=torch.float32, device=dev)
         dfr = _defer_gn(acc_g)  # dgamma / dbeta at the flush, batched (the coefficients are needed now)
         if dfr:
-            _DEFER.add_gnparam(part, mean, rstd, pg, pb, N, chunks, C, groups, acc_g)
+            _dfr().add_gnparam(part, mean, rstd, pg, pb, N, chunks, C, groups, acc_g)
         if NORM_FIN and C <= 1024:  # rows + per-image coefficients in one launch; dgamma / dbeta from the rows
             fin = norm_fin(FIN_GN_BWD, C, HW * (C // groups), dev, G=groups, gamma=gamma, mean=mean, rstd=rstd,
                            A=A, B=B, Cc=Cc)
@@ -1481,15 +1725,11 @@ class StemConvFn(torch.autograd.Function):
         w = ctx.pw
         Kc = w.shape[0]
         dy, dyp, dycs = nhwc(dy.to(torch.bfloat16) if dy.dtype != torch.bfloat16 else dy)
-        side = _side("stem") if _target(w) is not None else None
-        with (side.fork(img, dy) if side is not None else _nullctx()):
-            dw, pdw, acc = grad_dst(w, w.numel(), img.device)
-            wsb = lib.adr_stem_wgrad_workspace(N, H, W, Kc)
-            ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=img.device)
-            (lib.adr_stem_conv_wgrad_u8 if img.dtype == torch.uint8 else lib.adr_stem_conv_wgrad)(
-                fptr(img), N, H, W, ctypes.c_void_p(dyp), dycs, Kc, pdw, acc, fptr(ws), wsb, stream())
-            if side is not None:
-                side.keep.append(ws)
+        dw, pdw, acc = grad_dst(w, w.numel(), img.device)
+        wsb = lib.adr_stem_wgrad_workspace(N, H, W, Kc)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=img.device)
+        (lib.adr_stem_conv_wgrad_u8 if img.dtype == torch.uint8 else lib.adr_stem_conv_wgrad)(
+            fptr(img), N, H, W, ctypes.c_void_p(dyp), dycs, Kc, pdw, acc, fptr(ws), wsb, stream())
         return None, grad_ret(w, dw), None
 
 
@@ -1538,6 +1778,7 @@ def _ones(n, dev):
     t = _ONES.get((n, dev))
     if t is None:
         t = _ONES[(n, dev)] = torch.ones(n, dtype=torch.float32, device=dev)
+        _ready()
     return t
 
 
@@ -1556,6 +1797,7 @@ def _zeros_f32(n, dev):
     t = _ONES.get(("z", n, dev))
     if t is None:
         t = _ONES[("z", n, dev)] = torch.zeros(n, dtype=torch.float32, device=dev)
+        _ready()
     return t
 
 
@@ -1658,11 +1900,12 @@ def conv_bn_act_eval(x, w, stride, pad, bn, act: str, cpad=0, out=None):
     return y if out is None else out
 
 
-def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None, bnfin=None, xfuse=False):
+def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None, bnfin=None, xfuse=False, lazy=False):
     """act(BatchNorm(y)). xfuse: y is a dense conv's output read only here (Conv.forward), so the backward may hand
-    its dy to that conv's data gradient unwritten (BnXf)."""
+    its dy to that conv's data gradient unwritten (BnXf). lazy: the caller's consumer is a conv that can stage y
+    through the BN-act itself (BnFwd)."""
     return BNActFn.apply(y, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, act, training, bn.momentum,
-                         bn.eps, None if out is None else OutBox(out), bnfin, xfuse)
+                         bn.eps, None if out is None else OutBox(out), bnfin, xfuse, lazy)
 
 
 def gn_act(y, gn: torch.nn.Module, act: str):
@@ -1684,6 +1927,7 @@ def _const(value, device):
     t = _CONSTS.get(key)
     if t is None:
         t = _CONSTS[key] = torch.full((1,), float(value), dtype=torch.float32, device=device)
+        _ready()
     return t
 
 
@@ -1738,7 +1982,7 @@ class CatFn(torch.autograd.Function):
             piece = dy[:, off:off + s]
             piece._adr_excl = True  # a disjoint slice handed to exactly one consumer: FanOutFn may add into it
             # a fan-out view whose conv consumers have not run backward yet: they accumulate into the slice
-            outs.append(None if sk is not None and _side("wgrad") is None and sk.seed(piece) else piece)
+            outs.append(None if sk is not None and sk.seed(piece) else piece)
             off += s
         return (None,) + tuple(outs)
 
@@ -1906,9 +2150,6 @@ class FanOutFn(torch.autograd.Function):
                 and _v(g)[0] is g]
         if excl:  # accumulate the others into the exclusive slice in place
             acc = excl[0]
-            side = _side("wgrad") or _side("bias")
-            if side is not None:
-                side.guard_write(acc)
             rest = [g for g in gs if g is not acc]
             va = _v(acc)
             while rest:
@@ -2105,7 +2346,7 @@ class ScaleFn(torch.autograd.Function):
             sum_c = mode in ("scalar", "n")
             if sum_n and sum_c and _defer_dot(ctx.pg, x, vd[0]):  # a scalar: sum(x * dy) at the flush
                 out = torch.empty(1, dtype=torch.float32, device=x.device)
-                _DEFER.add_dotsum(x, vd[0], out)
+                _dfr().add_dotsum(x, vd[0], out)
                 dg = sink(ctx.pg, out.view(gshape))
             else:
                 dg = sink(ctx.pg, _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape))
@@ -2152,7 +2393,7 @@ class WeightedSumFn(torch.autograd.Function):
         elif all(_defer_dot(ctx.pw, x, vd[0]) for x in xs):  # the weights' scalar gradients at the flush
             dw = torch.empty(len(xs), dtype=torch.float32, device=dy.device)
             for i, x in enumerate(xs):
-                _DEFER.add_dotsum(x, vd[0], dw[i:i + 1])
+                _dfr().add_dotsum(x, vd[0], dw[i:i + 1])
         else:
             dw = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs])
         return (sink(ctx.pw, dw), dy if ctx.has_base else None, *dxs)
@@ -2196,9 +2437,9 @@ class FusionFn(torch.autograd.Function):
             # normalisation backward, then the arena add (the flush runs dots -> post_dots -> axpys)
             dwn = torch.empty(len(xs), dtype=torch.float32, device=dy.device)
             for i, x in enumerate(xs):
-                _DEFER.add_dotsum(x, vd[0], dwn[i:i + 1])
+                _dfr().add_dotsum(x, vd[0], dwn[i:i + 1])
             n = fwd.numel()
-            _DEFER.post_dots.append(lambda: lib.adr_fusion_weights_bwd(fptr(fwd), n, 1e-4, fptr(dwn), fptr(dfw),
+            _dfr().post_dots.append(lambda: lib.adr_fusion_weights_bwd(fptr(fwd), n, 1e-4, fptr(dwn), fptr(dfw),
                                                                        stream()))
         else:
             dwn = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs])
@@ -2502,6 +2743,7 @@ def _padded_bias(b, K, kpad, dev):
     hit = _PBIAS.get(key)
     if hit is None or (b is not None and hit[0] is not b):
         hit = _PBIAS[key] = (b, torch.zeros(kpad, dtype=torch.float32, device=dev))
+        _ready()
     if b is not None:
         lib.adr_cast(F32, fptr(b.detach().float().contiguous()), F32, fptr(hit[1]), K, stream())
     return hit[1]
@@ -2569,8 +2811,8 @@ _DCN_FAR_RETIRED = []  # outgrown buffers: a captured graph may still address th
 def _dcn_far_scratch(dev, N, H, W, C):
     """Persistent zeroed scratch of adr_dcn_bwd_bf16: the fp32 far-corner buffer and the tile flags. The kernels
     leave both zero again, so ONE pair per device serves every level, shape, step and graph replay (calls are
-    stream-ordered); a call uses a prefix view of it."""
-    key = str(dev)
+    stream-ordered; the concurrent head levels each have their own pair); a call uses a prefix view of it."""
+    key = (str(dev), _cur_sid() if _on_level_stream() else 0)
     n, nt = N * H * W * C, int(lib.adr_dcn_bwd_tiles(N, H, W))
     cur = _DCN_FAR.get(key)
     if cur is None or cur[0].numel() < n or cur[1].numel() < nt:
@@ -2579,6 +2821,7 @@ def _dcn_far_scratch(dev, N, H, W, C):
             n, nt = max(n, cur[0].numel()), max(nt, cur[1].numel())
         cur = (torch.zeros(n, dtype=torch.float32, device=dev), torch.zeros(nt, dtype=torch.int32, device=dev))
         _DCN_FAR[key] = cur
+        _ready()
     return cur[0][:N * H * W * C], cur[1][:int(lib.adr_dcn_bwd_tiles(N, H, W))]
 
 
@@ -2657,25 +2900,23 @@ class DCNFn(torch.autograd.Function):
                                  om.shape[1], fptr(dxf), fptr(flags), N, H, W, C, Cout, stream())
             _t1(tok)
             if ctx.needs_input_grad[2]:
-                side = _side("dcn") if _target(ctx.pw) is not None else None
-                with (side.fork(x, om, dy) if side is not None else _nullctx()):
-                    splits = lib.adr_dcn_wgrad_bf16_splits(N, H, W, C, Cout)
-                    stride = Cout * 9 * C
-                    ws = torch.empty(splits * stride, dtype=torch.float32, device=dev)
-                    rep = _reps()
-                    tok = _t0("adr::dcn_wgrad_kernel(adr::DcnArgs)", nb + 4 * splits * stride, fl,
-                              f"dcn wgrad/{splits} n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "", rep)
-                    for _ in range(rep):
-                        lib.adr_dcn_wgrad_bf16(ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs,
-                                               ctypes.c_void_p(dyp), dycs, fptr(ws), splits, N, H, W, C, Cout,
-                                               stream())
-                    _t1(tok)
-                    out, ptr, acc = grad_dst(ctx.pw, stride, dev)
-                    if _DEFER is not None and acc and _TIMING is None:
-                        _DEFER.add(ws, stride, splits, ptr, Cout, C, C, 9, 0, acc)
-                    else:
-                        lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, Cout, C, C, 9, 0, acc, stream())
-                    dw = grad_ret(ctx.pw, out)
+                splits = lib.adr_dcn_wgrad_bf16_splits(N, H, W, C, Cout)
+                stride = Cout * 9 * C
+                ws = torch.empty(splits * stride, dtype=torch.float32, device=dev)
+                rep = _reps()
+                tok = _t0("adr::dcn_wgrad_kernel(adr::DcnArgs)", nb + 4 * splits * stride, fl,
+                          f"dcn wgrad/{splits} n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "", rep)
+                for _ in range(rep):
+                    lib.adr_dcn_wgrad_bf16(ctypes.c_void_p(xp), xcs, ctypes.c_void_p(omp), omcs,
+                                           ctypes.c_void_p(dyp), dycs, fptr(ws), splits, N, H, W, C, Cout,
+                                           stream())
+                _t1(tok)
+                out, ptr, acc = grad_dst(ctx.pw, stride, dev)
+                if _dfr() is not None and acc and _TIMING is None:
+                    _dfr().add(ws, stride, splits, ptr, Cout, C, C, 9, 0, acc)
+                else:
+                    lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, Cout, C, C, 9, 0, acc, stream())
+                dw = grad_ret(ctx.pw, out)
         else:
             dx32 = zero_(torch.empty(N * H * W * C, dtype=torch.float32, device=dev))
             dom = zero_(empty_act(N, om.shape[1], H, W, dtype, dev))

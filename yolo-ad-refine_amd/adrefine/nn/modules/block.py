@@ -35,8 +35,8 @@ class Bottleneck(nn.Module):
     def forward(self, x, out=None):
         if self.add:
             xa, xb = K.fanout(x)  # residual + branch: one HIP gradient sum instead of an autograd add
-            return K.add(xa, self.cv2(self.cv1(xb)), out=out)
-        return self.cv2(self.cv1(x), out=out)
+            return K.add(xa, self.cv2(self.cv1(xb, lazy=True)), out=out)
+        return self.cv2(self.cv1(x, lazy=True), out=out)
 
 
 class C2f(nn.Module):
@@ -150,9 +150,9 @@ class Bottleneck_MLCA(Bottleneck):
 
     def forward(self, x):
         if not self.add:
-            return self.attention(self.cv2(self.cv1(x)), None)
+            return self.attention(self.cv2(self.cv1(x, lazy=True)), None)
         xa, xb = K.fanout(x)
-        return self.attention(self.cv2(self.cv1(xa)), xb)
+        return self.attention(self.cv2(self.cv1(xa, lazy=True)), xb)
 
 
 class C3k_MLCA(C3k):

@@ -77,7 +77,9 @@ class Conv(nn.Module):
 
     accepts_out = True  # forward(x, out=view) writes the activation into a caller's concat slice
 
-    def forward(self, x, out=None):
+    def forward(self, x, out=None, lazy=False):
+        """lazy (training): the caller hands the output straight to a conv, which applies this BN-act while staging
+        it (kernels.BnFwd) — the output is written by that conv, not by an elementwise pass here."""
         cv = self.conv
         if cv.groups != 1:
             k = cv.kernel_size[0]
@@ -98,7 +100,8 @@ class Conv(nn.Module):
         fin = K.BnFin(self.bn, x.device) if self.training and K.NORM_FIN else None
         y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight),
                          bnfin=fin)
-        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out, bnfin=fin, xfuse=True)
+        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out, bnfin=fin, xfuse=True,
+                        lazy=lazy and out is None and fin is None)
 
     def stem_ok(self):
         """The adr_stem kernels cover Conv(3, K in {16, 32, 64}, 3, 2) with pad 1 (every yaml's model.0)."""

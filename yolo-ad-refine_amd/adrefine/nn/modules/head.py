@@ -277,7 +277,9 @@ class AYHead1(nn.Module):
         return K.cat([reg_out, cls_out], out=buf)
 
     def forward(self, x):
-        outputs = [self._level(x[i], i) for i in range(self.nl)]
+        # the reference loops the levels (head.py:1132); here each level runs on its own stream when enabled
+        # (kernels.run_levels: the P4 / P5 chains overlap P3's instead of leaving the chip idle)
+        outputs = K.run_levels(lambda i, xi: self._level(xi, i), list(x))
         if self.training:
             return outputs
         y = K.detect_decode(outputs, [float(s) for s in self.stride], self.nc, self.reg_max)

@@ -210,6 +210,17 @@ def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
 
     if start > 0:
         fan(start - 1, x)
+    from .modules.block import C2f, SPPF
+    from .modules.conv import Conv
+    nxt = {m.i: layers[k + 1] for k, m in enumerate(layers[:-1])}
+
+    def lazy_ok(m):
+        """A Conv layer whose output only the next layer reads, first through a Conv on the whole tensor: the
+        consumer conv applies the BN-act while staging it (kernels.BnFwd)."""
+        n = nxt.get(m.i)
+        return (type(m) is Conv and m.training and n is not None and n.f == -1 and m.i not in save and
+                m.i not in cuts and (uses or {}).get(m.i, 1) == 1 and isinstance(n, (C2f, SPPF, Conv)))
+
     for m in layers[start:]:
         if m.f == -1:
             x = take(m.i - 1, x)
@@ -217,7 +228,7 @@ def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
             x = take(m.f, y[m.f])
         else:
             x = [take(m.i - 1, x) if j == -1 else take(j, y[j]) for j in m.f]
-        x = m(x)
+        x = m(x, lazy=True) if lazy_ok(m) else m(x)
         y.append(x if m.i in save else None)
         if m.i in cuts:
             x = cut_live(x, y, layers, m.i, bounds)  # y[i] and x stay one leaf when they are one tensor
@@ -287,6 +298,7 @@ class DetectionModel(nn.Module):
         if getattr(self, "_uses", None) is None:
             self._uses = consumer_counts(self.model)
         x, bounds = route_layers(layers, self.save, x, y, first, cuts, self._uses)
+        K.bnf_clear()  # (every lazy BN-act output has been consumed; nothing may stay unwritten)
         if cuts:
             self.stage_bounds = bounds
         return x

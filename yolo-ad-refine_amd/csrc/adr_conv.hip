@@ -556,9 +556,13 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
 // (adr_conv2d_fwd_bf16_stat_tiles), still reduced in a fixed order.
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2c;
 
-template <int BN, int MODE, int KT, bool EPI = false>
+// XF_FWD (adr_conv2d_fwd_bf16_bnact): the A rows are the producer BatchNorm's input y; each staged chunk becomes
+// z = act(y * s + t) (the thread's 8 reduction channels are fixed, so their coefficients live in registers) and
+// column tile 0 side-writes it once (every z element exactly once: rows are pixels).
+template <int BN, int MODE, int KT, bool EPI = false, int XF = XF_NONE>
 __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
   static_assert(MODE == CV_FWD || MODE == CV_DGRAD, "conv1: FWD or stride-1 DGRAD");
+  static_assert(XF == XF_NONE || (XF == XF_FWD && MODE == CV_FWD && !EPI), "conv1: forward XF only");
   constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
   constexpr int WROWS = CBM / WAVES_M, WCOLS = BN / WAVES_N;
   constexpr int TM = WROWS / 16, TN = WCOLS / 16;
@@ -589,6 +593,14 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
   const __amdgpu_buffer_rsrc_t wt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, a.wt_bytes, 0x00020000);
   const int kc = tid % CPR_A;                      // this thread's reduction chunk (same for all its A / B chunks)
   const bool kok = kc * 8 < a.ktot;
+  XfCoef<XF_FWD> xk;
+  if constexpr (XF == XF_FWD) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      xk.s[q] = kok ? a.xs[kc * 8 + q] : 0.f;
+      xk.t[q] = kok ? a.xt[kc * 8 + q] : 0.f;
+    }
+  }
 
   // weights of the column tile, once
 #pragma unroll
@@ -633,7 +645,17 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
   if (mt < mtiles) load(mt);
   for (; mt < mtiles; mt += groups) {
 #pragma unroll
-    for (int i = 0; i < A_CH; ++i) st16(&As[((tid / CPR_A) + (256 / CPR_A) * i) * KP + kc * 8], ra[i]);
+    for (int i = 0; i < A_CH; ++i) {
+      if constexpr (XF == XF_FWD) {
+        const long m = (long)mt * CBM + (tid / CPR_A) + (256 / CPR_A) * i;
+        const bool ok = kok && m < Mrows;
+        const u32x4 v = ok ? xf_chunk<XF_FWD>(ra[i], ra[i], xk, a.xact) : u32x4{0u, 0u, 0u, 0u};
+        if (ok && nt == 0) st16(a.xo + m * a.xocs + kc * 8, v);
+        st16(&As[((tid / CPR_A) + (256 / CPR_A) * i) * KP + kc * 8], v);
+      } else {
+        st16(&As[((tid / CPR_A) + (256 / CPR_A) * i) * KP + kc * 8], ra[i]);
+      }
+    }
     __syncthreads();  // A tile (and, first time, the weights) in LDS; the previous tile's output image read out
     if (mt + groups < mtiles) load(mt + groups);
     f32x4 acc[TN][TM];  // C^T: rows = columns n, columns = rows m
@@ -958,6 +980,10 @@ template <int BN, int KT>
 __global__ void __launch_bounds__(256, KT == 256 ? 1 : (KT == 64 && BN <= 64) ? 3 : 2) conv1_act_kernel(ConvArgs a, int groups) {
   conv1_body<BN, CV_FWD, KT, true>(a, groups);
 }
+template <int BN, int KT>
+__global__ void __launch_bounds__(256, KT == 256 ? 1 : (KT == 64 && BN <= 64) ? 3 : 2) conv1_xf_kernel(ConvArgs a, int groups) {
+  conv1_body<BN, CV_FWD, KT, false, XF_FWD>(a, groups);
+}
 template <int BN>
 __global__ void __launch_bounds__(256, BN <= 64 ? 4 : 2) conv_bf16_act_kernel(ConvArgs a) { conv_bf16_body<BN, CV_FWD, true>(a); }
 template <int TW, bool DG, int BN>
@@ -1070,6 +1096,8 @@ static void launch_conv1(int bn, int kt, long rows, ConvArgs& g, hipStream_t st)
   do {                                                                                                     \
     if (MODE == CV_FWD && g.escale)                                                                        \
       hipLaunchKernelGGL((conv1_act_kernel<BN, KT>), grid, dim3(256), 0, st, g, groups);                   \
+    else if (MODE == CV_FWD && g.xs)                                                                       \
+      hipLaunchKernelGGL((conv1_xf_kernel<BN, KT>), grid, dim3(256), 0, st, g, groups);                    \
     else                                                                                                   \
       hipLaunchKernelGGL((conv1_kernel<BN, MODE, KT>), grid, dim3(256), 0, st, g, groups);                 \
   } while (0)
@@ -1133,8 +1161,11 @@ static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   // XF kernels are single-buffered: at most 64 columns.
   p.bn = p.tw ? conv3_bn(out) : ((d->r * d->s == 1 || xf) && out > 64) ? 64 : conv_pick_bn(out);
   p.kt = 0;
-  if (!xf && !p.tw && p.mode != CV_DGRAD2 && d->r == 1 && d->s == 1 && d->stride_h == 1 && d->pad_h == 0 &&
-      d->pad_w == 0 && red <= (dgrad && p.bn <= 64 ? 256 : 128) && conv1_enabled())
+  const bool c1 = !p.tw && p.mode != CV_DGRAD2 && d->r == 1 && d->s == 1 && d->stride_h == 1 && d->pad_h == 0 &&
+                  d->pad_w == 0 && conv1_enabled();
+  // forward XF runs on the streaming kernel with the plain forward's tiling (so its output and statistics rows are
+  // bitwise the unfused pair's); the data-gradient XF keeps the per-tile kernel
+  if (c1 && (!xf || !dgrad) && red <= (dgrad && p.bn <= 64 ? 256 : 128))
     p.kt = red <= 64 ? 64 : red <= 128 ? 128 : 256;  // KT 256 (1 block per CU) measured a gain for DGRAD only
   return p;
 }
@@ -1197,7 +1228,7 @@ static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, c
   }
   const int bn = pl.bn;
   g.ntiles = cdiv(g.N, bn);
-  if (pl.kt && !fin) {  // (escale: eval Conv-BN-act epilogue)
+  if (pl.kt && !fin) {  // (escale: eval Conv-BN-act epilogue; xs: the XF forward)
     launch_conv1<CV_FWD>(bn, pl.kt, (long)d->n * d->ho * d->wo, g, (hipStream_t)stream);
     return check_launch("adr_conv2d_fwd_bf16");
   }
@@ -1315,12 +1346,17 @@ extern "C" int adr_conv2d_fwd_bf16_fin_stat_tiles(const adr_conv_desc* d) {
   return cdiv((long)d->n * d->ho * d->wo, CBM);
 }
 
-extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) {
-  const ConvPlan pl = conv_plan(d, false);
+static int fwd_stat_tiles(const adr_conv_desc* d, bool xf) {
+  const ConvPlan pl = conv_plan(d, false, xf);
   if (pl.tw) return conv3_tiles(d, pl.tw);
   if (pl.kt) return conv1_groups((long)d->n * d->ho * d->wo, cdiv(d->k, pl.bn), pl.kt, pl.bn);
   return cdiv((long)d->n * d->ho * d->wo, CBM);
 }
+
+extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) { return fwd_stat_tiles(d, false); }
+
+// statistics rows of adr_conv2d_fwd_bf16_bnact (its kernel choice can differ from the plain forward's)
+extern "C" int adr_conv2d_fwd_bf16_bnact_stat_tiles(const adr_conv_desc* d) { return fwd_stat_tiles(d, true); }
 
 extern "C" int adr_conv2d_fwd_bf16_col_tiles(const adr_conv_desc* d) {
   const ConvPlan pl = conv_plan(d, false);
@@ -1345,6 +1381,8 @@ extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, 
              dg ? XF_BWD : XF_FWD);
   else if (pl.tw)
     snprintf(buf, len, "_ZN3adr12conv3_kernelILi%dELb%dELi%dEEEvNS_8ConvArgsE", pl.tw, dg ? 1 : 0, pl.bn);
+  else if (pl.kt && xf)
+    snprintf(buf, len, "_ZN3adr15conv1_xf_kernelILi%dELi%dEEEvNS_8ConvArgsEi", pl.bn, pl.kt);
   else if (pl.kt)
     snprintf(buf, len, "_ZN3adr12conv1_kernelILi%dELi%dELi%dEEEvNS_8ConvArgsEi", pl.bn, pl.mode, pl.kt);
   else
