@@ -65,9 +65,6 @@ int adr_conv2d_fwd_bf16(const adr_conv_desc* d, const void* x, const void* w_krs
 int adr_conv2d_dgrad_bf16(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
                           int accumulate, void* stream);
 int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d);
-/* Stats rows of adr_conv2d_fwd_bf16_fin (the in-producer finalize always runs the per-tile kernels; the plain
- * forward's 1x1 streaming kernel writes one row per block group instead). */
-int adr_conv2d_fwd_bf16_fin_stat_tiles(const adr_conv_desc* d);
 /* dx (+)= dgrad(dy, w_crsk) + addend in one launch (bf16 engine): `addend` is an NHWC view shaped like dx with
  * channel stride addend_cstride, added in the epilogue with a single rounding. Used by the fan-out gradient sink:
  * a residual add's pass-through gradient (nn/modules/block.py:354 `x + self.cv2(self.cv1(x))`, autograd's
@@ -187,56 +184,6 @@ int adr_gn_finalize(const float* partial, int N, int chunks, int C, int G, doubl
 int adr_gn_bwd_finalize(const float* partial, int N, int chunks, int C, int G, double count, const float* mean,
                         const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* A, float* B,
                         float* Cc, int accumulate, void* stream);
-/* In-producer finalize: the producer of the partial-statistics rows (a bf16 conv epilogue, adr_nc_reduce) also
- * runs the *_finalize arithmetic above — the workgroup that writes the last row of a reduction does it (agent-
- * scope coherent row stores, an arrival counter, fixed-order double sums: deterministic) — so no separate finalize
- * launch follows. Same outputs as the finalize calls it replaces:
- *   ADR_FIN_BN_FWD  (adr_bn_finalize, training):  scale, shift, mean, rstd [C]; running_mean / running_var updated
- *   ADR_FIN_BN_BWD  (adr_bn_bwd_finalize, training): A, B, Cc [C]; dgamma / dbeta (+)= (accumulate)
- *   ADR_FIN_GN_FWD  (adr_gn_finalize):  scale, shift [N][C], mean, rstd [N][G]
- *   ADR_FIN_GN_BWD  (the coefficient part of adr_gn_bwd_finalize): A, B, Cc [N][C] (dgamma / dbeta stay with
- *                    adr_gn_param_grad(_batched) over the same rows)
- * counters: caller-owned uint32 words, all zero on entry; the kernel leaves them zero. One buffer may serve any
- * number of launches on one stream (adr_fin_counters_needed words each). scratch: doubles, no initialisation
- * (adr_fin_scratch_needed). Replaces the same reference BatchNorm2d / GroupNorm semantics as the finalize calls
- * (nn/modules/conv.py:44-50, nn/modules/head.py:607-620). */
-enum adr_fin_kind { ADR_FIN_BN_FWD = 0, ADR_FIN_BN_BWD = 1, ADR_FIN_GN_FWD = 2, ADR_FIN_GN_BWD = 3 };
-typedef struct adr_norm_fin {
-  unsigned* counters;
-  double* scratch;
-  int counters_cap, scratch_cap;  /* capacities (words / doubles), checked */
-  int kind, C, G, accumulate;
-  double count;                   /* elements per statistic: BN N*HW, GN HW*C/G */
-  const float* gamma;
-  const float* beta;
-  float* running_mean;
-  float* running_var;
-  float momentum, eps;
-  float* scale;
-  float* shift;
-  float* mean;                    /* BN_FWD / GN_FWD: written; BN_BWD / GN_BWD: read */
-  float* rstd;
-  float* dgamma;
-  float* dbeta;
-  float* A;
-  float* B;
-  float* Cc;
-} adr_norm_fin;
-/* counter words / scratch doubles a finalize over P rows per column tile (`tiles` column tiles; GN: N images
- * of P rows, tiles = N) needs */
-int adr_fin_counters_needed(int kind, int P, int tiles);
-long adr_fin_scratch_needed(int kind, int P, int C);
-/* adr_nc_reduce (mode 0 for the *_FWD kinds, 1 for *_BWD) followed in the same launch by the finalize of `fin`
- * (fin->C == C). BN kinds: P = N * chunks rows, one column tile; GN kinds: N images of chunks rows. */
-int adr_nc_reduce_fin(int dtype, int mode, const void* x, int xcs, int xco, const void* dz, int dcs, int dco,
-                      const float* scale, const float* shift, int per_sample, int act, int N, int HW, int C,
-                      int rows_per_chunk, float* partial, const adr_norm_fin* fin, void* stream);
-/* Training Conv-BN: adr_conv2d_fwd_bf16 (no bias, no accumulation) with the BatchNorm partial statistics of the
- * stored outputs AND their ADR_FIN_BN_FWD finalize in one launch (fin->C == d->k). Stats rows: as
- * adr_conv2d_fwd_bf16 (adr_conv2d_fwd_bf16_stat_tiles rows); column tiles: adr_conv2d_fwd_bf16_col_tiles. */
-int adr_conv2d_fwd_bf16_col_tiles(const adr_conv_desc* d);
-int adr_conv2d_fwd_bf16_fin(const adr_conv_desc* d, const void* x, const void* w_krsc, void* y, float* stats,
-                            const adr_norm_fin* fin, void* stream);
 /* GroupNorm(G) + activation fused per image (one 1024-thread workgroup per image: channel sums -> group
  * statistics -> z = act(x*scale + shift)); writes scale/shift per (image, channel) and mean/rstd per
  * (image, group) for the backward. Replaces adr_nc_reduce + adr_gn_finalize + adr_affine_act when

@@ -14,7 +14,7 @@ import ctypes
 
 import torch
 
-from .native import ConvDesc, NormFin, lib
+from .native import ConvDesc, lib
 
 F32, BF16 = 0, 1
 ACT = {"none": 0, "silu": 1, "gelu": 2, "relu": 3, "sigmoid": 4, "hswish": 5}
@@ -311,76 +311,6 @@ def grad_ret(t, buf):
     return None if buf is None else buf.view(t.shape)
 
 
-# ---------------------------------------------------------------------------------------------------------
-# in-producer normalisation finalize (adr_norm_fin): the conv epilogue / adr_nc_reduce that writes the partial
-# statistics rows also turns them into the BN / GN coefficients in its last workgroup, so no *_finalize launch
-# follows. Off by default (ADR_NORM_FIN=1 enables it): measured on the bench step (profiles/r03a_*) it removes 155
-# launches per step but every producer grows by the tail's chain of memory round trips (coherent row stores
-# drained before the arrival, the last workgroup's row loads, a second level for large reductions): nc_reduce
-# with the BN-backward finalize 32 us vs 17.6 + 6.7 us for the pair, conv<64,0> 21.6 vs 18.7 us — 26.9 vs
-# 26.3 ms of kernel time per step. On this chip a kernel boundary costs about what an in-kernel cross-workgroup
-# hand-off costs.
-# ---------------------------------------------------------------------------------------------------------
-NORM_FIN = bool(int(__import__("os").environ.get("ADR_NORM_FIN", "0")))
-FIN_BN_FWD, FIN_BN_BWD, FIN_GN_FWD, FIN_GN_BWD = range(4)
-_FIN_COUNTERS, _FIN_SCRATCH = 1 << 16, 1 << 21
-_FIN_POOLS = {}
-
-
-def _fin_pool(dev):
-    """Per-device (counters, scratch): the counters are zeroed once and every finalize leaves them zero; the
-    scratch (level-2 group sums) needs no initialisation. Launches on one stream share them in turn."""
-    key = torch.device(dev).index
-    p = _FIN_POOLS.get(key)
-    if p is None:
-        p = _FIN_POOLS[key] = (torch.zeros(_FIN_COUNTERS, dtype=torch.int32, device=dev),
-                               torch.empty(_FIN_SCRATCH, dtype=torch.float64, device=dev))
-    return p
-
-
-def _pv(x):
-    """Raw pointer value of a tensor / c_void_p / None for a ctypes struct field."""
-    if x is None:
-        return None
-    if isinstance(x, torch.Tensor):
-        return x.data_ptr()
-    if isinstance(x, ctypes.c_void_p):
-        return x.value
-    return int(x)
-
-
-def norm_fin(kind, C, count, dev, G=0, **kw):
-    """An adr_norm_fin for one producer launch (kw: gamma, beta, running_mean, running_var, momentum, eps, scale,
-    shift, mean, rstd, dgamma, dbeta, accumulate, A, B, Cc)."""
-    cnt, scr = _fin_pool(dev)
-    f = NormFin()
-    f.counters, f.scratch = cnt.data_ptr(), scr.data_ptr()
-    f.counters_cap, f.scratch_cap = cnt.numel(), scr.numel()
-    f.kind, f.C, f.G, f.count = kind, C, G, float(count)
-    f.accumulate = int(kw.pop("accumulate", 0))
-    f.momentum, f.eps = float(kw.pop("momentum", 0.0)), float(kw.pop("eps", 0.0))
-    for k, v in kw.items():
-        setattr(f, k, _pv(v.detach() if isinstance(v, torch.Tensor) else v))
-    return f
-
-
-class BnFin:
-    """The training BatchNorm's coefficient buffers, created before its conv so the conv can finalize them
-    (adr_conv2d_fwd_bf16_fin); `done` tells BNActFn whether that happened (else it finalizes as before)."""
-    __slots__ = ("bn", "scale", "shift", "mean", "rstd", "done")
-
-    def __init__(self, bn, dev):
-        C = bn.num_features
-        f = lambda: torch.empty(C, dtype=torch.float32, device=dev)  # noqa: E731
-        self.bn, self.scale, self.shift, self.mean, self.rstd, self.done = bn, f(), f(), f(), f(), False
-
-    def fin(self, count):
-        bn = self.bn
-        return norm_fin(FIN_BN_FWD, bn.num_features, count, self.scale.device, gamma=bn.weight, beta=bn.bias,
-                        running_mean=bn.running_mean, running_var=bn.running_var, momentum=bn.momentum, eps=bn.eps,
-                        scale=self.scale, shift=self.shift, mean=self.mean, rstd=self.rstd)
-
-
 def sink_unpack(t, dw_krsc, shape, cpad=0):
     """unpack_weight_grad straight into the gradient arena (accumulate) when t has one."""
     tgt = _target(t)
@@ -475,21 +405,6 @@ def conv_fwd(d, xp, wp, bias, yp, stats=None, accumulate=0):
         fn(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(wp), bias, ctypes.c_void_p(yp), stats,
            int(accumulate), stream())
     _t1(tok)
-
-
-def conv_fwd_fin(d, xp, wp, yp, stats, bnfin):
-    """Training Conv-BN: y = conv(x, w_krsc) with the BN partial statistics and, when NORM_FIN, their finalize
-    (batch mean / rstd, scale / shift, running statistics) in the same launch (adr_conv2d_fwd_bf16_fin)."""
-    if not NORM_FIN:
-        conv_fwd(d, xp, wp, None, yp, fptr(stats))
-        return
-    sym = "" if _TIMING is None else _conv2_symbol(d, False)
-    tok = _t0(sym, *_conv_work(d), _shape(d, "fwd+bnfin") if _TIMING is not None else "")
-    f = bnfin.fin(d.n * d.ho * d.wo)
-    lib.adr_conv2d_fwd_bf16_fin(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(wp), ctypes.c_void_p(yp),
-                                fptr(stats), ctypes.byref(f), stream())
-    _t1(tok)
-    bnfin.done = True
 
 
 # BASELINE.json configs[4]'s fp8 MFMA conv path: bias-free forward convs (Conv-BN-act) with a spatial kernel and
@@ -954,7 +869,7 @@ def level_streams(dev, n):
 
 def _levels_on(xs):
     return (LEVEL_STREAMS and len(xs) > 1 and all(isinstance(x, torch.Tensor) and x.is_cuda for x in xs) and
-            _TIMING is None and not NORM_FIN and not _on_level_stream())
+            _TIMING is None and not _on_level_stream())
 
 
 class _LevelIn(torch.autograd.Function):
@@ -1179,13 +1094,13 @@ class Conv2dFn(torch.autograd.Function):
     """y = conv2d(x, w) + b (dense, groups=1). Optionally also returns per-tile BN partial statistics."""
 
     @staticmethod
-    def forward(ctx, x, w, b, stride, pad, want_stats, cpad, box=None, bnfin=None, act=None):
+    def forward(ctx, x, w, b, stride, pad, want_stats, cpad, box=None, act=None):
         ctx.set_materialize_grads(False)  # no zero-filled gradient for the statistics output
         sink = getattr(x, "_adr_sink", None)
         ctx.sink = sink if sink is not None and sink.fits(x) else None
         dtype = x.dtype
         pend = _bnf_of(x)  # x = act(bn(y)) not written yet: stage y through the BN-act here
-        if pend is not None and not (b is None and act is None and bnfin is None and cpad == 0 and not CONV_FP8):
+        if pend is not None and not (b is None and act is None and cpad == 0 and not CONV_FP8):
             pend.materialize()
             pend = None
         if pend is not None:
@@ -1206,8 +1121,8 @@ class Conv2dFn(torch.autograd.Function):
         d, Ho, Wo = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, ycs, dtype)
         stats = None
         if want_stats:
-            tiles = ((lib.adr_conv2d_fwd_bf16_fin_stat_tiles if bnfin is not None else lib.adr_conv2d_fwd_bf16_stat_tiles)
-                     if _engine2(d, d.c) else lib.adr_conv2d_fwd_stat_tiles)(ctypes.byref(d))
+            tiles = (lib.adr_conv2d_fwd_bf16_stat_tiles if _engine2(d, d.c) else
+                     lib.adr_conv2d_fwd_stat_tiles)(ctypes.byref(d))
             stats = torch.empty(tiles * 2 * K, dtype=torch.float32, device=x.device)
         bf = b.detach().float().contiguous() if b is not None else None
         # fp8 for the Conv-BN-act convs only: biased nn.Conv2d rows (the heads' output projections: logits, box
@@ -1218,8 +1133,6 @@ class Conv2dFn(torch.autograd.Function):
                 stats = torch.empty(lib.adr_conv2d_fwd_fp8_stat_tiles(ctypes.byref(d)) * 2 * K, dtype=torch.float32,
                                     device=x.device)
             conv_fwd_fp8(d, xp, w, Cw, Cp, bf, yp, stats)
-        elif bnfin is not None and want_stats and b is None and _engine2(d, d.c):
-            conv_fwd_fin(d, xp, wp.data_ptr(), yp, stats, bnfin)  # conv + BN statistics + BN finalize
         elif act is not None:  # act(conv + b) on the fp32 accumulator (conv_act checked the engine)
             conv_fwd_act(d, xp, wp.data_ptr(), bf, K, act, yp)
         else:
@@ -1236,7 +1149,7 @@ class Conv2dFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dstats):
         if dy is None:
-            return None, None, None, None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None, None
         x, wp, wt, z = ctx.saved_tensors
         stride, pad, cpad, wshape, has_b = ctx.meta
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
@@ -1271,7 +1184,7 @@ class Conv2dFn(torch.autograd.Function):
             dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
         if has_b and ctx.needs_input_grad[2]:
             db = _bias_grad(dy, K, N, Ho * Wo, dycs, ctx.pb)
-        return dx, dw, db, None, None, None, None, None, None, None
+        return dx, dw, db, None, None, None, None, None, None
 
 
 class ConvT2dFn(torch.autograd.Function):
@@ -1323,8 +1236,7 @@ class BNActFn(torch.autograd.Function):
     """act(BatchNorm2d(y)) — train mode uses batch statistics (from the conv epilogue when given)."""
 
     @staticmethod
-    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None, bnfin=None, xfuse=False,
-                lazy=False):
+    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None, xfuse=False, lazy=False):
         dtype = y.dtype
         y, yp, ycs = nhwc(y)
         N, C, H, W = y.shape
@@ -1334,38 +1246,25 @@ class BNActFn(torch.autograd.Function):
         # whose only reader is this BN (Conv.forward), on the bf16 engine's XF coefficient table
         ctx.xfuse = bool(xfuse) and BN_XF_BWD and training and dtype == torch.bfloat16 and act in ("silu", "none") \
             and C <= 512 and C % 8 == 0
-        if training and bnfin is not None and bnfin.done:  # the conv's last workgroup finalized the statistics
-            scale, shift, mean, rstd = bnfin.scale, bnfin.shift, bnfin.mean, bnfin.rstd
-        else:
-            f = lambda: torch.empty(C, dtype=torch.float32, device=dev)  # noqa: E731
-            scale, shift, mean, rstd = f(), f(), f(), f()
-            if training and (stats is None or stats.numel() == 0) and NORM_FIN:  # statistics + finalize, 1 launch
-                rows = _stats_rows(N, HW)
-                chunks = lib.adr_nc_reduce_chunks(HW, rows)
+        f = lambda: torch.empty(C, dtype=torch.float32, device=dev)  # noqa: E731
+        scale, shift, mean, rstd = f(), f(), f(), f()
+        if training:
+            if stats is None or stats.numel() == 0:
+                chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
                 stats = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
-                fin = norm_fin(FIN_BN_FWD, C, N * HW, dev, gamma=gamma, beta=beta, running_mean=rm, running_var=rv,
-                               momentum=momentum, eps=eps, scale=scale, shift=shift, mean=mean, rstd=rstd)
-                lib.adr_nc_reduce_fin(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, N,
-                                      HW, C, rows, fptr(stats), ctypes.byref(fin), stream())
-            else:
-                if training:
-                    if stats is None or stats.numel() == 0:
-                        chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
-                        stats = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
-                        lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0,
-                                          N, HW, C, _stats_rows(N, HW), fptr(stats), stream())
-                    P = stats.numel() // (2 * C)
-                else:
-                    P = 0
-                # on a concurrent head-level stream the running statistics of a shared BN are updated at the join,
-                # in level order (run_levels / _flush_level_bn)
-                lvl = training and rm is not None and _on_level_stream()
-                if lvl:
-                    _LVL_BN.append((stats, P, C, N * HW, gamma, beta, rm, rv, momentum, eps))
-                lib.adr_bn_finalize(fptr(stats) if training else None, P, C, float(N * HW), fptr(gamma.detach()),
-                                    fptr(beta.detach()), None if lvl else fptr(rm), None if lvl else fptr(rv),
-                                    float(momentum), float(eps), int(training), fptr(scale), fptr(shift), fptr(mean),
-                                    fptr(rstd), stream())
+                lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0,
+                                  N, HW, C, _stats_rows(N, HW), fptr(stats), stream())
+            P = stats.numel() // (2 * C)
+        else:
+            P = 0
+        # on a concurrent head-level stream the running statistics of a shared BN are updated at the join, in level
+        # order (run_levels / _flush_level_bn)
+        lvl = training and rm is not None and _on_level_stream()
+        if lvl:
+            _LVL_BN.append((stats, P, C, N * HW, gamma, beta, rm, rv, momentum, eps))
+        lib.adr_bn_finalize(fptr(stats) if training else None, P, C, float(N * HW), fptr(gamma.detach()),
+                            fptr(beta.detach()), None if lvl else fptr(rm), None if lvl else fptr(rv), float(momentum),
+                            float(eps), int(training), fptr(scale), fptr(shift), fptr(mean), fptr(rstd), stream())
         z, zp, zcs = _out_view(box, N, C, H, W, dtype, dev)
         if lazy and box is None and BN_XF_FWD and training and dtype == torch.bfloat16 and act in ("silu", "none") \
                 and C % 8 == 0 and C <= 512:
@@ -1396,18 +1295,11 @@ class BNActFn(torch.autograd.Function):
         dbeta, pb, acc_b = grad_dst(ctx.pbeta, C, dev)
         if acc_g != acc_b:
             raise RuntimeError("BN gamma/beta gradients must share one destination kind")
-        if training and NORM_FIN:  # (sum g, sum g*x) rows + the backward finalize in one launch
-            fin = norm_fin(FIN_BN_BWD, C, N * HW, dev, gamma=gamma, mean=mean, rstd=rstd, dgamma=pg, dbeta=pb,
-                           accumulate=acc_g, A=A, B=B, Cc=Cc)
-            lib.adr_nc_reduce_fin(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
-                                  fptr(shift), 0, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part),
-                                  ctypes.byref(fin), stream())
-        else:
-            lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
-                              fptr(shift), 0, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
-            lib.adr_bn_bwd_finalize(fptr(part), N * chunks, C, float(N * HW), fptr(mean), fptr(rstd),
-                                    fptr(gamma.detach()), pg, pb, fptr(A), fptr(B), fptr(Cc), int(training), acc_g,
-                                    stream())
+        lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
+                          fptr(shift), 0, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
+        lib.adr_bn_bwd_finalize(fptr(part), N * chunks, C, float(N * HW), fptr(mean), fptr(rstd),
+                                fptr(gamma.detach()), pg, pb, fptr(A), fptr(B), fptr(Cc), int(training), acc_g,
+                                stream())
         dy = empty_act(N, C, H, W, y.dtype, dev)
         pend = BnXf(y, dz, scale, shift, A, B, Cc, act)
         if ctx.xfuse:  # the conv's data gradient applies it while staging its operand (and side-writes dy)
@@ -1415,7 +1307,7 @@ class BNActFn(torch.autograd.Function):
         else:
             pend.materialize(dy)
         return (dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None, None, None,
-                None, None, None)
+                None, None)
 
 
 # Training Conv-BN-act backward fusion: BNActFn.backward computes the coefficients (nc_reduce + bn_bwd_finalize)
@@ -1607,17 +1499,11 @@ class GNActFn(torch.autograd.Function):
         shift = torch.empty(N * C, dtype=torch.float32, device=dev)
         mean = torch.empty(N * groups, dtype=torch.float32, device=dev)
         rstd = torch.empty(N * groups, dtype=torch.float32, device=dev)
-        if NORM_FIN and C <= 1024:  # statistics + per-image finalize in one launch
-            fin = norm_fin(FIN_GN_FWD, C, HW * (C // groups), dev, G=groups, gamma=gamma, beta=beta, eps=eps,
-                           scale=scale, shift=shift, mean=mean, rstd=rstd)
-            lib.adr_nc_reduce_fin(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, N, HW,
-                                  C, _stats_rows(N, HW), fptr(part), ctypes.byref(fin), stream())
-        else:
-            lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, N, HW, C,
-                              _stats_rows(N, HW), fptr(part), stream())
-            lib.adr_gn_finalize(fptr(part), N, chunks, C, groups, float(HW * (C // groups)), fptr(gamma.detach()),
-                                fptr(beta.detach()), float(eps), fptr(scale), fptr(shift), fptr(mean), fptr(rstd),
-                                stream())
+        lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, N, HW, C,
+                          _stats_rows(N, HW), fptr(part), stream())
+        lib.adr_gn_finalize(fptr(part), N, chunks, C, groups, float(HW * (C // groups)), fptr(gamma.detach()),
+                            fptr(beta.detach()), float(eps), fptr(scale), fptr(shift), fptr(mean), fptr(rstd),
+                            stream())
         z = empty_act(N, C, H, W, dtype, dev)
         lib.adr_affine_act(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(z.data_ptr()), C, 0,
                            fptr(scale), fptr(shift), 1, ACT[act], N, HW, C, stream())
@@ -1664,22 +1550,11 @@ class GNActFn(torch.autograd.Function):
         dfr = _defer_gn(acc_g)  # dgamma / dbeta at the flush, batched (the coefficients are needed now)
         if dfr:
             _dfr().add_gnparam(part, mean, rstd, pg, pb, N, chunks, C, groups, acc_g)
-        if NORM_FIN and C <= 1024:  # rows + per-image coefficients in one launch; dgamma / dbeta from the rows
-            fin = norm_fin(FIN_GN_BWD, C, HW * (C // groups), dev, G=groups, gamma=gamma, mean=mean, rstd=rstd,
-                           A=A, B=B, Cc=Cc)
-            lib.adr_nc_reduce_fin(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
-                                  fptr(shift), 1, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part),
-                                  ctypes.byref(fin), stream())
-            if not dfr:  # dgamma / dbeta now: the per-channel reduction over (image, chunk) rows
-                ent = (GnParamEntry * 1)(GnParamEntry(part.data_ptr(), mean.data_ptr(), rstd.data_ptr(), _pv(pg),
-                                                      _pv(pb), N, chunks, C, groups, acc_g, 0))
-                lib.adr_gn_param_grad_batched(ctypes.cast(ent, ctypes.c_void_p), 1, stream())
-        else:
-            lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
-                              fptr(shift), 1, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
-            lib.adr_gn_bwd_finalize(fptr(part), N, chunks, C, groups, float(HW * (C // groups)), fptr(mean),
-                                    fptr(rstd), fptr(gamma.detach()), None if dfr else pg, None if dfr else pb,
-                                    fptr(A), fptr(B), fptr(Cc), acc_g, stream())
+        lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
+                          fptr(shift), 1, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
+        lib.adr_gn_bwd_finalize(fptr(part), N, chunks, C, groups, float(HW * (C // groups)), fptr(mean),
+                                fptr(rstd), fptr(gamma.detach()), None if dfr else pg, None if dfr else pb,
+                                fptr(A), fptr(B), fptr(Cc), acc_g, stream())
         dy = empty_act(N, C, H, W, y.dtype, dev)
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
@@ -1760,10 +1635,9 @@ def image_to_nhwc(img: torch.Tensor, dtype, cpad=8):
 # ---------------------------------------------------------------------------------------------------------
 
 
-def conv2d(x, w, b=None, stride=1, pad=0, want_stats=False, cpad=0, out=None, bnfin=None):
-    """y = conv2d(x, w) (+b); with `out` (an NHWC channel slice of a concat buffer) y is written into it. With
-    `bnfin` (a BnFin, training Conv-BN) the conv launch also finalizes the BatchNorm when its engine can."""
-    y, stats = Conv2dFn.apply(x, w, b, stride, pad, want_stats, cpad, None if out is None else OutBox(out), bnfin)
+def conv2d(x, w, b=None, stride=1, pad=0, want_stats=False, cpad=0, out=None):
+    """y = conv2d(x, w) (+b); with `out` (an NHWC channel slice of a concat buffer) y is written into it."""
+    y, stats = Conv2dFn.apply(x, w, b, stride, pad, want_stats, cpad, None if out is None else OutBox(out))
     return y, stats
 
 
@@ -1810,7 +1684,7 @@ def conv_act(x, w, b, stride, pad, act, cpad=0):
         (sh, sw), (ph, pw) = _pair(stride), _pair(pad)
         d, _, _ = conv_desc(N, H, W, C, xcs, K, R, S, sh, sw, ph, pw, K, x.dtype)
         if _engine2(d, d.c):
-            y, _ = Conv2dFn.apply(x, w, b, stride, pad, False, cpad, None, None, act)
+            y, _ = Conv2dFn.apply(x, w, b, stride, pad, False, cpad, None, act)
             return y
     return ActFn.apply(conv2d(x, w, b, stride, pad, False, cpad)[0], act)
 
@@ -1900,12 +1774,12 @@ def conv_bn_act_eval(x, w, stride, pad, bn, act: str, cpad=0, out=None):
     return y if out is None else out
 
 
-def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None, bnfin=None, xfuse=False, lazy=False):
+def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None, xfuse=False, lazy=False):
     """act(BatchNorm(y)). xfuse: y is a dense conv's output read only here (Conv.forward), so the backward may hand
     its dy to that conv's data gradient unwritten (BnXf). lazy: the caller's consumer is a conv that can stage y
     through the BN-act itself (BnFwd)."""
     return BNActFn.apply(y, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, act, training, bn.momentum,
-                         bn.eps, None if out is None else OutBox(out), bnfin, xfuse, lazy)
+                         bn.eps, None if out is None else OutBox(out), xfuse, lazy)
 
 
 def gn_act(y, gn: torch.nn.Module, act: str):

@@ -20,18 +20,7 @@ class ConvDesc(ctypes.Structure):
         "ho", "wo", "y_cstride", "y_coff", "dtype")]
 
 
-class NormFin(ctypes.Structure):
-    """adr_norm_fin (include/adr.h): the in-producer BatchNorm / GroupNorm finalize."""
-    _fields_ = ([("counters", ctypes.c_void_p), ("scratch", ctypes.c_void_p)] +
-                [(n, ctypes.c_int) for n in ("counters_cap", "scratch_cap", "kind", "C", "G", "accumulate")] +
-                [("count", ctypes.c_double)] +
-                [(n, ctypes.c_void_p) for n in ("gamma", "beta", "running_mean", "running_var")] +
-                [("momentum", ctypes.c_float), ("eps", ctypes.c_float)] +
-                [(n, ctypes.c_void_p) for n in ("scale", "shift", "mean", "rstd", "dgamma", "dbeta", "A", "B",
-                                                  "Cc")])
-
-
-_STRUCTS = {"adr_conv_desc": ConvDesc, "adr_norm_fin": NormFin}
+_STRUCTS = {"adr_conv_desc": ConvDesc}
 
 
 def _ctype(t: str):
@@ -125,9 +114,8 @@ def _traced(name, fn, a):
 _NONSTATUS = {"adr_abi_version", "adr_conv2d_fwd_stat_tiles", "adr_conv2d_fwd_bf16_stat_tiles", "adr_conv2d_wgrad_splits", "adr_nc_reduce_chunks", "adr_opt_entry_size", "adr_pack_chunk_size", "adr_stem_fwd_tiles",
               "adr_opt_chunk_size", "adr_dcn_wgrad_bf16_splits", "adr_gn_fused_supported",
               "adr_fp8_amax_blocks", "adr_conv2d_fp8_supported", "adr_conv2d_fwd_fp8_stat_tiles",
-              "adr_dwconv_fwd_act_supported", "adr_fin_counters_needed", "adr_conv2d_fwd_bf16_col_tiles",
-              "adr_conv2d_bf16_xf_reuse", "adr_augment_desc_size", "adr_dcn_bwd_tiles",
-              "adr_conv2d_fwd_bf16_fin_stat_tiles"}
+              "adr_dwconv_fwd_act_supported", "adr_conv2d_bf16_xf_reuse", "adr_augment_desc_size",
+              "adr_dcn_bwd_tiles", "adr_conv2d_fwd_bf16_bnact_stat_tiles"}
 _ = _NONSTATUS
 
 lib = _Lib()

@@ -96,12 +96,10 @@ class Conv(nn.Module):
                                    _in_pad(x, cv.weight), out=out)
             if z is not None:
                 return z
-        # training: the conv's last workgroup also finalizes the batch statistics (no bn_finalize launch)
-        fin = K.BnFin(self.bn, x.device) if self.training and K.NORM_FIN else None
-        y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight),
-                         bnfin=fin)
-        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out, bnfin=fin, xfuse=True,
-                        lazy=lazy and out is None and fin is None)
+        # training: BN partial statistics in the conv epilogue, then finalize + affine + act (or, lazily, the
+        # consumer conv applies the affine + act while staging)
+        y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight))
+        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out, xfuse=True, lazy=lazy and out is None)
 
     def stem_ok(self):
         """The adr_stem kernels cover Conv(3, K in {16, 32, 64}, 3, 2) with pad 1 (every yaml's model.0)."""

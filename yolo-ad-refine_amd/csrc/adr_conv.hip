@@ -20,7 +20,6 @@
 #include <type_traits>
 
 #include "adr_common.h"
-#include "adr_fin.h"
 
 namespace adr {
 
@@ -50,8 +49,6 @@ struct ConvArgs {
   // out = conv (+ out) + addend, NHWC with channel stride adcs (null: none)
   const __bf16* addend;
   int adcs;
-  // FWD with stats: the BatchNorm finalize in the last workgroup of each column tile (adr_conv2d_fwd_bf16_fin)
-  FinArgs fin;
   // A-operand BatchNorm-activation transform (XF kernels, adr_conv2d_{fwd,dgrad}_bf16_bnact): the A source is a
   // training BatchNorm's input y (FWD: the operand is z = act(y * s + t), 0 in the padding) or the gradient dz of
   // its output (DGRAD: the operand is dy = A * g + B * y + C with g = dz * act'(y * s + t), 0 outside the image,
@@ -531,17 +528,9 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
         x2 += red[1][g][tid];
       }
       float* s = a.stats + (long)mt * 2 * a.N + n0 + tid;
-      if (MODE == CV_FWD && a.fin.on) {
-        st_coh(s, x1);
-        st_coh(s + a.N, x2);
-      } else {
-        s[0] = x1;
-        s[a.N] = x2;
-      }
+      s[0] = x1;
+      s[a.N] = x2;
     }
-    if constexpr (MODE == CV_FWD && !EPI)
-      if (a.fin.on)
-        fin_bn_tail(a.fin, a.stats, mt, n0, min(BN, a.N - n0), a.fin.f.counters + nt * (1 + a.fin.ngroups), lds_raw);
   }
 }
 
@@ -954,17 +943,9 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
         x2 += red[1][g][tid];
       }
       float* s = a.stats + (long)mt * 2 * a.N + n0 + tid;
-      if (!DG && a.fin.on) {
-        st_coh(s, x1);
-        st_coh(s + a.N, x2);
-      } else {
-        s[0] = x1;
-        s[a.N] = x2;
-      }
+      s[0] = x1;
+      s[a.N] = x2;
     }
-    if constexpr (!DG && !EPI)
-      if (a.fin.on)
-        fin_bn_tail(a.fin, a.stats, mt, n0, min(BN, a.N - n0), a.fin.f.counters + nt * (1 + a.fin.ngroups), lds_raw);
   }
 }
 
@@ -1194,23 +1175,15 @@ static int xf_args(const adr_bnact_xf* xf, bool bwd, int red, int n, int sh, int
 
 using namespace adr;
 
-extern "C" int adr_conv2d_fwd_bf16_fin_stat_tiles(const adr_conv_desc* d);
-
 static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, const float* bias, void* y,
                          float* stats, int accumulate, const float* escale, const float* eshift, int eact,
-                         void* stream, const adr_norm_fin* fin = nullptr, const adr_bnact_xf* xf = nullptr) {
+                         void* stream, const adr_bnact_xf* xf = nullptr) {
   int rc = conv_check(d);
   if (rc) return rc;
   ConvArgs g{};
   if (xf) {
-    ADR_REQUIRE(!escale && !fin, "conv fwd bnact: no eval epilogue / in-kernel finalize");
+    ADR_REQUIRE(!escale, "conv fwd bnact: no eval epilogue");
     rc = xf_args(xf, false, d->c, d->n, d->h, d->w, g);
-    if (rc) return rc;
-  }
-  if (fin) {
-    ADR_REQUIRE(stats && !bias && !accumulate && !escale && fin->kind == ADR_FIN_BN_FWD && fin->C == d->k,
-                "conv fwd fin: needs stats, no bias / accumulation, a BN forward finalize over K channels");
-    rc = fin_setup(fin, adr_conv2d_fwd_bf16_fin_stat_tiles(d), adr_conv2d_fwd_bf16_col_tiles(d), d->n, g.fin);
     if (rc) return rc;
   }
   g.src = (const __bf16*)x; g.wt = (const __bf16*)w; g.out = (__bf16*)y; g.bias = bias; g.stats = stats;
@@ -1228,7 +1201,7 @@ static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, c
   }
   const int bn = pl.bn;
   g.ntiles = cdiv(g.N, bn);
-  if (pl.kt && !fin) {  // (escale: eval Conv-BN-act epilogue; xs: the XF forward)
+  if (pl.kt) {  // (escale: eval Conv-BN-act epilogue; xs: the XF forward)
     launch_conv1<CV_FWD>(bn, pl.kt, (long)d->n * d->ho * d->wo, g, (hipStream_t)stream);
     return check_launch("adr_conv2d_fwd_bf16");
   }
@@ -1322,7 +1295,7 @@ extern "C" int adr_conv2d_dgrad_bf16_bnact(const adr_conv_desc* d, const void* d
 extern "C" int adr_conv2d_fwd_bf16_bnact(const adr_conv_desc* d, const void* y, const void* w, void* out,
                                          float* stats, const adr_bnact_xf* xf, void* stream) {
   ADR_REQUIRE(xf, "conv fwd bnact: xf");
-  return conv_fwd_impl(d, y, w, nullptr, out, stats, 0, nullptr, nullptr, 0, stream, nullptr, xf);
+  return conv_fwd_impl(d, y, w, nullptr, out, stats, 0, nullptr, nullptr, 0, stream, xf);
 }
 
 // How many times the XF kernel would stage (and transform) each source element, x100: column tiles x gathers per
@@ -1339,13 +1312,6 @@ extern "C" int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad) {
   return nt * 100 * taps;
 }
 
-// the in-producer finalize (adr_conv2d_fwd_bf16_fin) always runs the per-tile kernels: one stats row per tile
-extern "C" int adr_conv2d_fwd_bf16_fin_stat_tiles(const adr_conv_desc* d) {
-  const ConvPlan pl = conv_plan(d, false);
-  if (pl.tw) return conv3_tiles(d, pl.tw);
-  return cdiv((long)d->n * d->ho * d->wo, CBM);
-}
-
 static int fwd_stat_tiles(const adr_conv_desc* d, bool xf) {
   const ConvPlan pl = conv_plan(d, false, xf);
   if (pl.tw) return conv3_tiles(d, pl.tw);
@@ -1357,17 +1323,6 @@ extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) { return f
 
 // statistics rows of adr_conv2d_fwd_bf16_bnact (its kernel choice can differ from the plain forward's)
 extern "C" int adr_conv2d_fwd_bf16_bnact_stat_tiles(const adr_conv_desc* d) { return fwd_stat_tiles(d, true); }
-
-extern "C" int adr_conv2d_fwd_bf16_col_tiles(const adr_conv_desc* d) {
-  const ConvPlan pl = conv_plan(d, false);
-  return pl.tw ? d->k / pl.bn : cdiv(d->k, pl.bn);
-}
-
-extern "C" int adr_conv2d_fwd_bf16_fin(const adr_conv_desc* d, const void* x, const void* w, void* y, float* stats,
-                                       const adr_norm_fin* fin, void* stream) {
-  ADR_REQUIRE(fin, "conv fwd fin: fin");
-  return conv_fwd_impl(d, x, w, nullptr, y, stats, 0, nullptr, nullptr, 0, stream, fin);
-}
 
 extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, char* buf, int len) {
   ADR_REQUIRE(d && buf && len >= 64, "conv kernel symbol: bad arguments");

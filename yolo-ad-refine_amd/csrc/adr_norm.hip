@@ -9,14 +9,13 @@
 // Reference semantics: nn.BatchNorm2d with eps 1e-3 / momentum 0.03 (utils/torch_utils.py:426-436),
 // unbiased running_var update; GroupNorm(16, C) eps 1e-5 (nn/modules/head.py:613).
 #include "adr_common.h"
-#include "adr_fin.h"
 
 namespace adr {
 
 enum RedMode { RED_STATS = 0, RED_BWD = 1, RED_SUM = 2 };
 
-// partial[(n * chunks + chunk)][2][C]; COH: rows stored with agent-coherent stores (an in-kernel finalize reads them)
-template <typename T, int MODE, int ACT, bool COH = false>
+// partial[(n * chunks + chunk)][2][C]
+template <typename T, int MODE, int ACT>
 __device__ __forceinline__ void nc_reduce_body(const T* __restrict__ x, int xcs, int xco, const T* __restrict__ dz,
                                                int dcs, int dco, const float* __restrict__ scale,
                                                const float* __restrict__ shift, int per_sample, int HW, int C,
@@ -97,35 +96,8 @@ __device__ __forceinline__ void nc_reduce_body(const T* __restrict__ x, int xcs,
       a += sh[0][(g + r * G) * VEC + e];
       b += sh[1][(g + r * G) * VEC + e];
     }
-    if constexpr (COH) {
-      st_coh(out + c, a);
-      st_coh(out + C + c, b);
-    } else {
-      out[c] = a;
-      out[C + c] = b;
-    }
-  }
-}
-
-// adr_nc_reduce with the finalize in the last workgroup (adr_fin.h): BN kinds reduce all N * chunks rows (one
-// column range of C channels), GN kinds finalize image n when its `chunks` rows are in
-constexpr int FIN_MAXC = 1024;
-template <typename T, int MODE, int ACT>
-__global__ void __launch_bounds__(256) nc_reduce_fin_kernel(const T* __restrict__ x, int xcs, int xco,
-                                                            const T* __restrict__ dz, int dcs, int dco,
-                                                            const float* __restrict__ scale,
-                                                            const float* __restrict__ shift, int per_sample, int HW,
-                                                            int C, int rows_per_chunk, int chunks,
-                                                            float* __restrict__ partial, FinArgs fa) {
-  __shared__ __attribute__((aligned(16))) unsigned char fin_lds[(2 * FIN_MAXC + 2 * 256 + 2 * 64) * 8 + 16];
-  const int chunk = blockIdx.x, n = blockIdx.y;
-  nc_reduce_body<T, MODE, ACT, true>(x, xcs, xco, dz, dcs, dco, scale, shift, per_sample, HW, C, rows_per_chunk,
-                                     chunks, partial, chunk, n);
-  if (fa.f.kind == FIN_GN_FWD || fa.f.kind == FIN_GN_BWD) {
-    unsigned* flag = reinterpret_cast<unsigned*>(fin_lds + (2 * FIN_MAXC + 2 * 256 + 2 * 64) * 8);
-    if (fin_arrive(fa.f.counters + n, (unsigned)chunks, flag)) fin_gn_image(fa, partial, n, fin_lds);
-  } else {
-    fin_bn_tail(fa, partial, n * chunks + chunk, 0, C, fa.f.counters, fin_lds);
+    out[c] = a;
+    out[C + c] = b;
   }
 }
 
@@ -839,91 +811,6 @@ extern "C" int adr_nc_reduce(int dtype, int mode, const void* x, int xcs, int xc
                          partial);
   }
   return check_launch("adr_nc_reduce");
-}
-
-namespace adr {
-int fin_setup(const adr_norm_fin* f, int P, int tiles, int N, FinArgs& fa) {
-  ADR_REQUIRE(f && f->counters && P > 0 && tiles > 0 && f->C > 0 && f->count > 0, "norm fin: bad arguments");
-  ADR_REQUIRE(f->kind >= ADR_FIN_BN_FWD && f->kind <= ADR_FIN_GN_BWD, "norm fin: kind %d", f->kind);
-  fa = FinArgs{};
-  fa.f = *f;
-  fa.on = 1;
-  fa.P = P;
-  const bool gn = f->kind == ADR_FIN_GN_FWD || f->kind == ADR_FIN_GN_BWD;
-  fa.gs = gn ? P : fin_group_rows(P);
-  fa.ngroups = cdiv(P, fa.gs);
-  const int need_c = adr_fin_counters_needed(f->kind, P, gn ? N : tiles);
-  const long need_s = adr_fin_scratch_needed(f->kind, P, f->C);
-  ADR_REQUIRE(need_c <= f->counters_cap && need_s <= f->scratch_cap && (need_s == 0 || f->scratch),
-              "norm fin: needs %d counters / %ld scratch doubles (have %d / %d)", need_c, need_s, f->counters_cap,
-              f->scratch_cap);
-  if (f->kind == ADR_FIN_BN_FWD)
-    ADR_REQUIRE(f->scale && f->shift && f->mean && f->rstd, "norm fin (BN fwd): outputs");
-  if (f->kind == ADR_FIN_BN_BWD)
-    ADR_REQUIRE(f->mean && f->rstd && f->A && f->B && f->Cc, "norm fin (BN bwd): mean/rstd/A/B/Cc");
-  if (gn) {
-    ADR_REQUIRE(f->G > 0 && f->G <= 64 && f->C % f->G == 0 && f->C <= FIN_MAXC, "norm fin (GN): C=%d G=%d", f->C,
-                f->G);
-    ADR_REQUIRE(f->mean && f->rstd && (f->kind == ADR_FIN_GN_FWD ? (f->scale && f->shift) : (f->A && f->B && f->Cc)),
-                "norm fin (GN): outputs");
-  }
-  return ADR_OK;
-}
-}  // namespace adr
-
-extern "C" int adr_fin_counters_needed(int kind, int P, int tiles) {
-  if (kind == ADR_FIN_GN_FWD || kind == ADR_FIN_GN_BWD) return tiles;
-  return tiles * (1 + cdiv(P, fin_group_rows(P)));
-}
-
-extern "C" long adr_fin_scratch_needed(int kind, int P, int C) {
-  if (kind == ADR_FIN_GN_FWD || kind == ADR_FIN_GN_BWD) return 0;
-  const int ng = cdiv(P, fin_group_rows(P));
-  return ng > 1 ? (long)ng * 2 * C : 0;
-}
-
-// adr_nc_reduce + the finalize of `fin` in the last workgroup (one launch instead of two)
-extern "C" int adr_nc_reduce_fin(int dtype, int mode, const void* x, int xcs, int xco, const void* dz, int dcs,
-                                 int dco, const float* scale, const float* shift, int per_sample, int act, int N,
-                                 int HW, int C, int rows_per_chunk, float* partial, const adr_norm_fin* fin,
-                                 void* stream) {
-  int vec = dtype == ADR_BF16 ? 8 : 4;
-  ADR_REQUIRE(C % vec == 0 && C / vec <= 256, "nc_reduce_fin: C=%d unsupported", C);
-  ADR_REQUIRE(xcs % vec == 0 && xco % vec == 0 && dcs % vec == 0 && dco % vec == 0, "nc_reduce_fin: misaligned view");
-  ADR_REQUIRE(mode == RED_STATS || mode == RED_BWD, "nc_reduce_fin: mode");
-  ADR_REQUIRE(fin && fin->C == C, "nc_reduce_fin: fin channels");
-  const bool gn = fin->kind == ADR_FIN_GN_FWD || fin->kind == ADR_FIN_GN_BWD;
-  const bool bwd = fin->kind == ADR_FIN_BN_BWD || fin->kind == ADR_FIN_GN_BWD;
-  ADR_REQUIRE(bwd == (mode == RED_BWD), "nc_reduce_fin: mode %d does not produce kind %d rows", mode, fin->kind);
-  int chunks = cdiv(HW, rows_per_chunk);
-  FinArgs fa;
-  int rc = fin_setup(fin, gn ? chunks : N * chunks, 1, N, fa);
-  if (rc) return rc;
-  dim3 grid(chunks, N);
-  hipStream_t st = (hipStream_t)stream;
-  if (mode == RED_BWD) {
-#define ADR_NCRF(A)                                                                                                 \
-  if (dtype == ADR_BF16)                                                                                            \
-    hipLaunchKernelGGL((nc_reduce_fin_kernel<__bf16, RED_BWD, A>), grid, dim3(256), 0, st, (const __bf16*)x, xcs,  \
-                       xco, (const __bf16*)dz, dcs, dco, scale, shift, per_sample, HW, C, rows_per_chunk, chunks,   \
-                       partial, fa);                                                                                \
-  else                                                                                                              \
-    hipLaunchKernelGGL((nc_reduce_fin_kernel<float, RED_BWD, A>), grid, dim3(256), 0, st, (const float*)x, xcs,    \
-                       xco, (const float*)dz, dcs, dco, scale, shift, per_sample, HW, C, rows_per_chunk, chunks,    \
-                       partial, fa)
-    ADR_ACT_DISPATCH(act, ADR_NCRF);
-#undef ADR_NCRF
-  } else {
-    if (dtype == ADR_BF16)
-      hipLaunchKernelGGL((nc_reduce_fin_kernel<__bf16, RED_STATS, ACT_NONE>), grid, dim3(256), 0, st,
-                         (const __bf16*)x, xcs, xco, (const __bf16*)nullptr, 0, 0, scale, shift, per_sample, HW, C,
-                         rows_per_chunk, chunks, partial, fa);
-    else
-      hipLaunchKernelGGL((nc_reduce_fin_kernel<float, RED_STATS, ACT_NONE>), grid, dim3(256), 0, st,
-                         (const float*)x, xcs, xco, (const float*)nullptr, 0, 0, scale, shift, per_sample, HW, C,
-                         rows_per_chunk, chunks, partial, fa);
-  }
-  return check_launch("adr_nc_reduce_fin");
 }
 
 extern "C" int adr_bn_finalize(const float* partial, int P, int C, double count, const float* gamma, const float* beta,
