@@ -321,3 +321,35 @@ def test_mul_pixel(dtype, C, hw):
         err = float((got.float() - ref.detach()).abs().max()) / max(float(ref.abs().max()), 1e-6)
         assert err <= tol, err
     assert float(p.grad[:, 1:].abs().max()) == 0.0
+
+
+@pytest.mark.parametrize("c1,c2,n,hw", [(128, 128, 16, 128), (256, 128, 8, 160), (128, 256, 16, 96)])
+def test_conv3_wide_tile_bf16(c1, c2, n, hw):
+    """The wide 256-pixel x 128-channel 3x3 tile (conv3w_kernel: big-channel convs with >= 512 tiles; l-scale
+    shapes) in the forward and the data gradient, with the BN partial statistics, vs torch fp32 on the same bf16
+    operands, and against the 128 x 64 halo-tile kernel it replaces (ADR_CONV3W is read once per process, so the
+    reference here is torch)."""
+    from adrefine import kernels as K
+    from adrefine.native import lib
+    torch.manual_seed(11)
+    x = (torch.randn(n, c1, hw, hw, device="cuda")).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    w = torch.randn(c2, c1, 3, 3, device="cuda") * (1.0 / (9 * c1) ** 0.5)
+    d, _, _ = K.conv_desc(n, hw, hw, c1, c1, c2, 3, 3, 1, 1, 1, 1, c2, torch.bfloat16)
+    assert "conv3w" in K._conv2_symbol(d, False) and "conv3w" in K._conv2_symbol(d, True), \
+        "the wide tile should take this shape (forward and data gradient)"
+    xx = x.detach().clone().requires_grad_(True)
+    y, st = K.conv2d(xx, w, None, 1, 1, want_stats=True)
+    g = torch.randn_like(y.float()).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    y.backward(g)
+    xr = x.float().requires_grad_(True)
+    yr = torch.nn.functional.conv2d(xr, w.to(torch.bfloat16).float(), None, 1, 1)
+    yr.backward(g.float())
+    rel = lambda a, b: float((a.float() - b).norm() / b.norm())  # noqa: E731
+    assert rel(y, yr) < 1e-2, rel(y, yr)
+    assert rel(xx.grad, xr.grad) < 1e-2, rel(xx.grad, xr.grad)
+    # BN partial statistics: per-tile rows of (sum, sum of squares) of the stored bf16 outputs
+    tiles = lib.adr_conv2d_fwd_bf16_stat_tiles(K.ctypes.byref(d))
+    s = st.view(tiles, 2, c2).double().sum(0)
+    yf = y.detach().double()
+    assert torch.allclose(s[0], yf.sum((0, 2, 3)), rtol=1e-4, atol=1e-2)
+    assert torch.allclose(s[1], (yf * yf).sum((0, 2, 3)), rtol=1e-4, atol=1e-2)

@@ -746,16 +746,22 @@ constexpr int C3_CK = 32, C3_LD = C3_CK;  // chunk channels; unpadded 64-byte LD
 // group reads cover 16 disjoint bank quads (48 KB per block: 3 blocks per CU)
 __device__ __forceinline__ int c3_swz(int row, int kq) { return row * C3_LD + ((kq ^ ((row >> 2) & 3)) << 3); }
 
-template <int TW, bool DG, int BN, bool EPI, int XF = XF_NONE>
+// WN = 2 (the wide tile, `conv3w_kernel`): 512 threads own a 256-pixel x 128-channel tile — waves 4 along M (64 rows
+// each) x 2 along N — so each staged byte of the halo and of the weight slab feeds twice the MFMA work of the
+// 128 x 64 tile: the big-channel 3x3 convs (l-scale C, K >= 128) were L2-bound at ~0.37 of the bf16 MFMA peak.
+template <int TW, bool DG, int BN, bool EPI, int XF = XF_NONE, int WN = 1>
 __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
-  constexpr int TH = 128 / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
-  constexpr int A_TOT = NPIX * (C3_CK / 8), A_CH = (A_TOT + 255) / 256;
-  constexpr int TPP = 256 / (BN * (C3_CK / 8));      // taps per pass of the 256 threads over the weight slab
+  constexpr int NT = 256 * WN, PIX = 128 * WN;         // threads, tile pixels
+  constexpr int TH = PIX / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
+  constexpr int A_TOT = NPIX * (C3_CK / 8), A_CH = (A_TOT + NT - 1) / NT;
+  constexpr int TPP = NT / (BN * (C3_CK / 8));       // taps per pass of the threads over the weight slab
+  static_assert(TPP >= 1, "conv3: BN too wide for the thread count");
   constexpr int B_CH = (9 + TPP - 1) / TPP;          // chunk i of a thread is tap i * TPP + tid / (4 BN)
-  constexpr int TM = 2, TN = BN / 16;                // 4 waves along M (32 rows each) x all BN columns
-  constexpr int OPITCH = BN + 8, CPR = BN / 8, RPP = 256 / CPR;
+  constexpr int WROWS = PIX / 4, WCOLS = BN / WN;    // 4 waves along M x WN along N
+  constexpr int TM = WROWS / 16, TN = WCOLS / 16;
+  constexpr int OPITCH = BN + 8, CPR = BN / 8, RPP = NT / CPR;
   constexpr int SMEM_A = NPIX * C3_LD, SMEM_B = 9 * BN * C3_LD;
-  constexpr int SMEM_AB = 2 * (SMEM_A + SMEM_B), SMEM_O = 2 * 128 * OPITCH, SMEM_R = 2 * RPP * BN * 4;
+  constexpr int SMEM_AB = 2 * (SMEM_A + SMEM_B), SMEM_O = 2 * PIX * OPITCH, SMEM_R = 2 * RPP * BN * 4;
   constexpr int SMEM_BYTES = SMEM_AB > SMEM_O ? (SMEM_AB > SMEM_R ? SMEM_AB : SMEM_R) : (SMEM_O > SMEM_R ? SMEM_O : SMEM_R);
   __shared__ __attribute__((aligned(16))) unsigned char lds_raw[SMEM_BYTES];
   __bf16* As = reinterpret_cast<__bf16*>(lds_raw);
@@ -763,6 +769,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   float (*red)[RPP][BN] = reinterpret_cast<float (*)[RPP][BN]>(lds_raw);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % 4, wn = wave / 4;
   const int H = a.rh, W = a.rw;
   const int tx = W / TW, ty = (H + TH - 1) / TH;
   const int bid = xcd_block(blockIdx.x, gridDim.x);
@@ -779,7 +786,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   unsigned a_in = 0;  // XF: halo chunks in the tile interior (their source pixel belongs to this tile)
 #pragma unroll
   for (int i = 0; i < A_CH; ++i) {
-    const int e = tid + 256 * i, q = e >> 2, hy = q / HWW, hx = q - (q / HWW) * HWW;
+    const int e = tid + NT * i, q = e >> 2, hy = q / HWW, hx = q - (q / HWW) * HWW;
     const int gy = y0 - 1 + hy, gx = x0 - 1 + hx;
     const bool ok = e < A_TOT && gy >= 0 && gy < a.sh_ && gx >= 0 && gx < a.sw_;
     a_pix[i] = ok ? (img * a.sh_ + gy) * a.sw_ + gx : -1;
@@ -819,7 +826,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
     if constexpr (XF != XF_NONE) xk.load(xtab, c0 + xq);
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
-      const int e = tid + 256 * i;
+      const int e = tid + NT * i;
       if constexpr (XF == XF_NONE) {
         if (e < A_TOT) st16(&As[c3_swz(e >> 2, e & 3)], ra[i]);
       } else {
@@ -836,7 +843,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
     }
   };
 
-  const int wr0 = wave * 32;
+  const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
   int fq[TM];  // halo pixel of this lane's fragment row, tap (0, 0)
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -865,7 +872,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
       for (int i = 0; i < TM; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(&As[c3_swz(fq[i] + dq, kq)]);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[c3_swz(t * BN + j * 16 + (lane & 15), kq)]);
+        fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[c3_swz(t * BN + wc0 + j * 16 + (lane & 15), kq)]);
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -879,7 +886,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   __bf16* Os = reinterpret_cast<__bf16*>(lds_raw);
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
-    const int col = j * 16 + (lane & 15);
+    const int col = wc0 + j * 16 + (lane & 15);
     const bool cok = n0 + col < a.N;
     const float b = (a.bias && cok) ? a.bias[n0 + col] : 0.f;
     const float es = EPI && cok ? a.escale[n0 + col] : 1.f;
@@ -897,7 +904,7 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
   const bool col_ok = n0 + oc * 8 < a.N;
-  for (int r = orow; r < 128; r += RPP) {
+  for (int r = orow; r < PIX; r += RPP) {
     const int y = y0 + r / TW;
     if (y >= H || !col_ok) continue;
     u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
@@ -971,6 +978,8 @@ template <int TW, bool DG, int BN>
 __global__ void __launch_bounds__(256, 3) conv3_kernel(ConvArgs a) { conv3_body<TW, DG, BN, false>(a); }
 template <int TW, int BN>
 __global__ void __launch_bounds__(256, 3) conv3_act_kernel(ConvArgs a) { conv3_body<TW, false, BN, true>(a); }
+template <bool DG, bool EPI>
+__global__ void __launch_bounds__(512, 1) conv3w_kernel(ConvArgs a) { conv3_body<16, DG, 128, EPI, XF_NONE, 2>(a); }
 // training Conv-BN-act fusion: the A operand is the producer BatchNorm's input (FWD) or the gradient of its output
 // (DGRAD) and the BN-act (backward) is applied while staging it (XF_FWD / XF_BWD); the coefficient table and the
 // second operand cost LDS and registers, so these run at 3 (2 for the 3x3 halo tiles) workgroups per CU
@@ -989,11 +998,25 @@ static int conv3_tw(const adr_conv_desc* d, int red_ch, int out_ch) {
   return 0;
 }
 static int conv3_bn(int out_ch) { return out_ch % 64 == 0 ? 64 : 32; }
-static int conv3_tiles(const adr_conv_desc* d, int tw) {
-  return d->n * ((d->h + 128 / tw - 1) / (128 / tw)) * (d->w / tw);
+static int conv3_tiles(const adr_conv_desc* d, int tw, int pix = 128) {
+  return d->n * ((d->h + pix / tw - 1) / (pix / tw)) * (d->w / tw);
+}
+// the wide 256-pixel x 128-channel tile (conv3w_kernel, one 512-thread block per CU) for big-channel 3x3 convs with
+// enough tiles to fill the chip twice over
+static bool conv3_wide(const adr_conv_desc* d, int tw, int red_ch, int out_ch) {
+  static const int on = getenv("ADR_CONV3W") ? atoi(getenv("ADR_CONV3W")) : 1;  // A/B
+  return on && tw == 16 && d->h >= 16 && red_ch >= 128 && out_ch % 128 == 0 &&
+         (long)conv3_tiles(d, 16, 256) * (out_ch / 128) >= 512;
 }
 template <bool DG>
-static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hipStream_t st) {
+static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hipStream_t st, bool wide = false) {
+  if (wide) {
+    g.ntiles = g.N / 128;
+    dim3 grid(conv3_tiles(d, 16, 256) * g.ntiles);
+    if (!DG && g.escale) hipLaunchKernelGGL((conv3w_kernel<false, true>), grid, dim3(512), 0, st, g);
+    else hipLaunchKernelGGL((conv3w_kernel<DG, false>), grid, dim3(512), 0, st, g);
+    return;
+  }
   g.ntiles = g.N / bn;
   dim3 grid(conv3_tiles(d, tw) * g.ntiles);
   if (g.xs) {  // XF: FWD applies the producer's BN-act, DGRAD its backward
@@ -1129,14 +1152,16 @@ static int conv_check(const adr_conv_desc* d) {
 // roofline labels cannot drift from the dispatch.
 struct ConvPlan {
   int tw;    // > 0: conv3_kernel<tw, dgrad> (3x3 stride-1 halo tiles)
+  int wide;  // with tw: the 256 x 128 tile (conv3w_kernel)
   int bn;    // else conv_bf16_kernel<bn, mode>
   int mode;  // CV_FWD / CV_DGRAD / CV_DGRAD2
   int kt;    // > 0: conv1_kernel<bn, mode, kt> (streaming 1x1, reduction <= kt)
 };
 static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
-  ConvPlan p{0, 0, dgrad ? (d->stride_h == 2 ? CV_DGRAD2 : CV_DGRAD) : CV_FWD};
+  ConvPlan p{0, 0, 0, dgrad ? (d->stride_h == 2 ? CV_DGRAD2 : CV_DGRAD) : CV_FWD};
   const int red = dgrad ? d->k : d->c, out = dgrad ? d->c : d->k;
   if (p.mode != CV_DGRAD2) p.tw = conv3_tw(d, red, out);
+  p.wide = p.tw && !xf && conv3_wide(d, p.tw, red, out);
   // 1x1 contractions are two or three K-steps long: 64-wide column tiles (4 waves/SIMD) hide their load latency
   // better than 128-wide ones (2 waves/SIMD), at the cost of reading the A rows once per column tile (L2 hits).
   // XF kernels are single-buffered: at most 64 columns.
@@ -1196,7 +1221,7 @@ static int conv_fwd_impl(const adr_conv_desc* d, const void* x, const void* w, c
   g.wt_bytes = (int)(2l * g.N * g.ktot);
   const ConvPlan pl = conv_plan(d, false, xf != nullptr);
   if (pl.tw) {
-    launch_conv3<false>(pl.tw, pl.bn, d, g, (hipStream_t)stream);
+    launch_conv3<false>(pl.tw, pl.bn, d, g, (hipStream_t)stream, pl.wide);
     return check_launch("adr_conv2d_fwd_bf16");
   }
   const int bn = pl.bn;
@@ -1251,7 +1276,7 @@ static int conv_dgrad_impl(const adr_conv_desc* d, const void* dy, const void* w
     dim3 grid(cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM) * g.ntiles, 1, 4);
     launch_conv<CV_DGRAD2>(bn, grid, g, st);
   } else if (pl.tw) {
-    launch_conv3<true>(pl.tw, pl.bn, d, g, st);
+    launch_conv3<true>(pl.tw, pl.bn, d, g, st, pl.wide);
   } else if (pl.kt) {
     launch_conv1<CV_DGRAD>(bn, pl.kt, (long)d->n * d->h * d->w, g, st);
   } else {
@@ -1314,7 +1339,7 @@ extern "C" int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad) {
 
 static int fwd_stat_tiles(const adr_conv_desc* d, bool xf) {
   const ConvPlan pl = conv_plan(d, false, xf);
-  if (pl.tw) return conv3_tiles(d, pl.tw);
+  if (pl.tw) return pl.wide ? conv3_tiles(d, 16, 256) : conv3_tiles(d, pl.tw);
   if (pl.kt) return conv1_groups((long)d->n * d->ho * d->wo, cdiv(d->k, pl.bn), pl.kt, pl.bn);
   return cdiv((long)d->n * d->ho * d->wo, CBM);
 }
@@ -1334,6 +1359,8 @@ extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, 
   else if (xf)
     snprintf(buf, len, "_ZN3adr19conv_bf16_xf_kernelILi%dELi%dELi%dEEEvNS_8ConvArgsE", pl.bn, pl.mode,
              dg ? XF_BWD : XF_FWD);
+  else if (pl.tw && pl.wide)
+    snprintf(buf, len, "_ZN3adr13conv3w_kernelILb%dELb0EEEvNS_8ConvArgsE", dg ? 1 : 0);
   else if (pl.tw)
     snprintf(buf, len, "_ZN3adr12conv3_kernelILi%dELb%dELi%dEEEvNS_8ConvArgsE", pl.tw, dg ? 1 : 0, pl.bn);
   else if (pl.kt && xf)
