@@ -1737,6 +1737,7 @@ def _bn_eval_coefs(bn, dev):
     _bn_eval_coefs_into(bn, scale, shift)
     if pc is not None and pc.cache_bn_coefs:
         pc.bn_coefs[id(bn)] = (bn, scale, shift)
+        _ready()  # (a shared BN's cached pair is read by the other head-level streams)
     return scale, shift
 
 
