@@ -32,10 +32,10 @@ def _train(dtype):
     init = torch.cat([p.detach().float().reshape(-1) for _, p in m.named_parameters() if p.requires_grad]).clone()
     batch, _ = train_batch(BS, S, seed=21, device="cuda", u8=True)
     tr = FusedTrainer(m, batch_size=BS, nbs=BS)  # accumulate 1: an optimizer step per batch
-    losses = [tr.step(batch).float()]
+    losses = [tr.step(batch).float().clone()]
     tr.capture(batch)
     for _ in range(STEPS - 1):
-        losses.append(tr.step(batch).float())
+        losses.append(tr.step(batch).float().clone())  # (a replay returns the same static tensor)
     torch.cuda.synchronize()
     final = torch.cat([p.detach().float().reshape(-1) for _, p in m.named_parameters() if p.requires_grad])
     return torch.stack(losses).cpu().double(), (final - init).cpu().double(), names

@@ -72,5 +72,5 @@ def test_levels_concurrent_eval_equal():
             torch.cuda.synchronize()
             outs.append(y[0].clone())
         finally:
-            K.LEVEL_STREAMS = True
+            K.LEVEL_STREAMS = False
     assert torch.equal(outs[0], outs[1])

@@ -794,9 +794,13 @@ def defer_wgrad():
 #     also writes;
 #   * tensors crossing streams are record_stream()-ed so the caching allocator never hands their memory to the
 #     other stream early.
-# ADR_LEVEL_STREAMS=0 runs the levels serially on the current stream (A/B, timing mode).
+# OFF by default (LEVEL_STREAMS / ADR_LEVEL_STREAMS=1 turns it on): measured under hipGraph replay on ROCm 7 the
+# branched graph is slower, not faster — 26.6 vs 24.6 ms/step (scripts/ab_levels.sh, profiles/r04a_ab_levels.txt):
+# the runtime places the branches on separate hardware queues and its cross-queue waits cost more than the overlap
+# wins (DEBUG_HIP_FORCE_GRAPH_QUEUES=1 folds them back onto one queue: 24.7 ms, i.e. serial). The path stays tested
+# bitwise against the serial order (tests/test_gpu_levels.py) for runtimes whose branched graphs overlap cheaply.
 # ---------------------------------------------------------------------------------------------------------
-LEVEL_STREAMS = bool(int(__import__("os").environ.get("ADR_LEVEL_STREAMS", "1")))
+LEVEL_STREAMS = bool(int(__import__("os").environ.get("ADR_LEVEL_STREAMS", "0")))
 _LVL_STREAMS = {}   # device index -> [torch.cuda.Stream]
 _LVL_IDS = {}       # stream handle -> torch.cuda.Stream (every level stream ever created)
 _DEFER_LVL = {}     # level stream handle -> WgradDeferral (during a deferred backward)
