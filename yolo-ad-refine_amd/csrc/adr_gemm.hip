@@ -463,50 +463,75 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
-// Many WGRAD reductions in one launch (the trainer defers them to the end of the backward pass): a block's
-// entry is found from the per-entry block offsets; each entry is reduced exactly as wgrad_reduce_kernel<true, 32,
-// 8> would (same split order), so deferring changes no result. The entries ride in the kernel arguments.
+// Many WGRAD reductions in one launch (the trainer defers them to the end of the backward pass; the immediate
+// adr_wgrad_reduce_unpack is a batch of one, so deferring changes no result). The entries ride in the kernel
+// arguments; a block's entry is found from the per-entry block offsets. A thread owns 4 consecutive outputs (one
+// 16-byte load per split slab: the partial rows are channel-contiguous) and a split lane; `SL` lanes per output quad
+// (per entry, from the host: small outputs with many splits still spread over the chip) each sum their splits in
+// order, 4 slabs in flight, and the lanes are combined in lane order through LDS — a fixed order per entry
+// (deterministic). The sum then lands at its (K, C, RS) parameter slot (or (C, K, RS) with transpose_kc).
+// Round 4: replaces a 32-output x 8-lane scalar version that read 4-byte words (l-scale: 800 us per launch).
 constexpr int RB_MAX = 56;
 struct RedBatch {
-  adr_wgrad_reduce_entry e[RB_MAX];
+  adr_wgrad_reduce_entry e[RB_MAX];  // e[j].pad_ carries the entry's split lanes (SL)
   int start[RB_MAX + 1];
   int count;
 };
 __global__ void __launch_bounds__(256) wgrad_reduce_batched_kernel(RedBatch b) {
-  constexpr int OUT = 32, SL = 8, U = 8;
   int j = 0;
   while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
   const adr_wgrad_reduce_entry& en = b.e[j];
-  __shared__ float sh[SL][OUT];
-  const int o = threadIdx.x % OUT, sl = threadIdx.x / OUT;
-  const long i = (long)(blockIdx.x - b.start[j]) * OUT + o;
+  const int SL = en.pad_, QPB = 256 / SL;
+  const int q = threadIdx.x % QPB, lane = threadIdx.x / QPB;
+  const long i0 = ((long)(blockIdx.x - b.start[j]) * QPB + q) * 4;
   const long n = (long)en.K * en.RS * en.Cp;
-  float acc[U];
-#pragma unroll
-  for (int v = 0; v < U; ++v) acc[v] = 0.f;
-  if (i < n) {
-    int k = sl;
-    for (; k + (U - 1) * SL < en.splits; k += U * SL) {
-#pragma unroll
-      for (int v = 0; v < U; ++v) acc[v] += en.part[(long)(k + v * SL) * en.split_stride + i];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (i0 < n) {
+    const float* p = en.part + i0;
+    int s = lane;
+    for (; s + 3 * SL < en.splits; s += 4 * SL) {
+      const float4 v0 = *reinterpret_cast<const float4*>(p + (long)s * en.split_stride);
+      const float4 v1 = *reinterpret_cast<const float4*>(p + (long)(s + SL) * en.split_stride);
+      const float4 v2 = *reinterpret_cast<const float4*>(p + (long)(s + 2 * SL) * en.split_stride);
+      const float4 v3 = *reinterpret_cast<const float4*>(p + (long)(s + 3 * SL) * en.split_stride);
+      acc.x += v0.x; acc.y += v0.y; acc.z += v0.z; acc.w += v0.w;
+      acc.x += v1.x; acc.y += v1.y; acc.z += v1.z; acc.w += v1.w;
+      acc.x += v2.x; acc.y += v2.y; acc.z += v2.z; acc.w += v2.w;
+      acc.x += v3.x; acc.y += v3.y; acc.z += v3.z; acc.w += v3.w;
     }
-#pragma unroll
-    for (int v = 0; v < U; ++v)
-      if (k + v * SL < en.splits) acc[v] += en.part[(long)(k + v * SL) * en.split_stride + i];
+    for (; s < en.splits; s += SL) {
+      const float4 v = *reinterpret_cast<const float4*>(p + (long)s * en.split_stride);
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
   }
-  sh[sl][o] = ((acc[0] + acc[1]) + (acc[2] + acc[3])) + ((acc[4] + acc[5]) + (acc[6] + acc[7]));
-  __syncthreads();
-  if (sl == 0 && i < n) {
-    float s = 0.f;
+  __shared__ float4 sh[256];
+  if (SL > 1) {
+    sh[threadIdx.x] = acc;
+    __syncthreads();
+    if (lane != 0) return;
+    for (int l = 1; l < SL; ++l) {
+      const float4 v = sh[l * QPB + q];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+  }
+  if (i0 >= n) return;
+  const float r4[4] = {acc.x, acc.y, acc.z, acc.w};
+  const int c0 = (int)(i0 % en.Cp);  // Cp % 4 == 0: the quad shares (k, t)
+  const long r = i0 / en.Cp;
+  const int t = (int)(r % en.RS), kk = (int)(r / en.RS);
 #pragma unroll
-    for (int q = 0; q < SL; ++q) s += sh[q][o];
-    const int c = (int)(i % en.Cp);
-    const long r = i / en.Cp;
-    const int t = (int)(r % en.RS), kk = (int)(r / en.RS);
-    if (c >= en.C) return;
+  for (int e = 0; e < 4; ++e) {
+    const int c = c0 + e;
+    if (c >= en.C) break;
     const long di = en.transpose_kc ? ((long)c * en.K + kk) * en.RS + t : ((long)kk * en.C + c) * en.RS + t;
-    en.dst[di] = en.accumulate ? en.dst[di] + s : s;
+    en.dst[di] = en.accumulate ? en.dst[di] + r4[e] : r4[e];
   }
+}
+
+static int reduce_lanes(long n, int splits) {  // split lanes: enough blocks to spread a small output over the chip
+  int sl = 1;
+  while (sl < 32 && sl < splits && cdiv(n / 4, 256 / sl) < 512) sl *= 2;
+  return sl;
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -674,18 +699,12 @@ extern "C" int adr_wgrad_reduce(const float* part, float* dw, long n, int splits
   return check_launch("adr_wgrad_reduce");
 }
 
+extern "C" int adr_wgrad_reduce_batched(const adr_wgrad_reduce_entry* entries, int count, void* stream);
+
 extern "C" int adr_wgrad_reduce_unpack(const float* part, long split_stride, int splits, float* dst, int K, int C,
                                        int Cp, int RS, int transpose_kc, int accumulate, void* stream) {
-  const long n = (long)K * RS * Cp;
-  ADR_REQUIRE(n > 0 && splits >= 1 && C <= Cp && split_stride >= n, "wgrad_reduce_unpack: K=%d C=%d Cp=%d RS=%d", K, C,
-              Cp, RS);
-  if (splits >= 256)
-    hipLaunchKernelGGL((wgrad_reduce_kernel<true, 16, 16>), dim3(cdiv(n, 16)), dim3(256), 0, (hipStream_t)stream, part,
-                       split_stride, dst, n, splits, accumulate, Unpack{K, C, Cp, RS, transpose_kc});
-  else
-    hipLaunchKernelGGL((wgrad_reduce_kernel<true, 32, 8>), dim3(cdiv(n, 32)), dim3(256), 0, (hipStream_t)stream, part,
-                       split_stride, dst, n, splits, accumulate, Unpack{K, C, Cp, RS, transpose_kc});
-  return check_launch("adr_wgrad_reduce_unpack");
+  adr_wgrad_reduce_entry en{part, dst, split_stride, splits, K, C, Cp, RS, transpose_kc, accumulate, 0};
+  return adr_wgrad_reduce_batched(&en, 1, stream);
 }
 
 extern "C" int adr_wgrad_reduce_batched(const adr_wgrad_reduce_entry* entries, int count, void* stream) {
@@ -697,15 +716,17 @@ extern "C" int adr_wgrad_reduce_batched(const adr_wgrad_reduce_entry* entries, i
     for (int j = 0; j < rb.count; ++j) {
       const adr_wgrad_reduce_entry& en = entries[b0 + j];
       const long n = (long)en.K * en.RS * en.Cp;
-      ADR_REQUIRE(en.part && en.dst && n > 0 && en.splits >= 1 && en.C <= en.Cp && en.split_stride >= n,
+      ADR_REQUIRE(en.part && en.dst && n > 0 && en.splits >= 1 && en.C <= en.Cp && en.split_stride >= n &&
+                      en.Cp % 4 == 0 && en.split_stride % 4 == 0 && ((uintptr_t)en.part & 15) == 0,
                   "wgrad_reduce_batched: entry %d (K=%d C=%d Cp=%d RS=%d splits=%d)", b0 + j, en.K, en.C, en.Cp,
                   en.RS, en.splits);
       for (int q = 0; q < j; ++q)  // same destination twice in one launch would race: the caller must split
         ADR_REQUIRE(rb.e[q].dst != en.dst, "wgrad_reduce_batched: entries %d and %d share a destination", b0 + q,
                     b0 + j);
       rb.e[j] = en;
+      rb.e[j].pad_ = reduce_lanes(n, en.splits);
       rb.start[j] = blocks;
-      blocks += (int)cdiv(n, 32);
+      blocks += (int)cdiv(n / 4, 256 / rb.e[j].pad_);
     }
     rb.start[rb.count] = blocks;
     hipLaunchKernelGGL(wgrad_reduce_batched_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, rb);
