@@ -199,6 +199,28 @@ int adr_gn_act_bwd_fused(int dtype, const void* x, int xcs, int xco, const void*
                          int ocs, int oco, const float* scale, const float* shift, const float* mean,
                          const float* rstd, const float* gamma, int N, int HW, int C, int G, int act,
                          float* partial, void* stream);
+/* Level-packed GroupNorm (AYHead1.forward's per-level loop, nn/modules/head.py:1132-1176, run once over the three
+ * levels): the levels' NHWC rows are stored back to back (level 0's N images, then level 1's, ...) and cut into
+ * sub-images of `sub_rows` rows; an image of level l is k[l] consecutive sub-images (k: host array of `levels`
+ * ints). partial is adr_nc_reduce's [N' sub-images][chunks][2][C] over that row space. Per (level, image):
+ * group statistics over its k[l]*chunks rows, written replicated to each of its sub-images — mean/rstd
+ * [N'][G], scale/shift [N'][C] with level l's gamma/beta (host arrays of `levels` device pointers, entries may
+ * be NULL; the head's shared convs pass the same pointer for every level) — so adr_affine_act(per_sample) and
+ * adr_gn_param_grad(_batched) over the N' sub-images give the per-image GroupNorm of each level. */
+int adr_gn_finalize_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows, int C,
+                           int G, const void* const* gamma, const void* const* beta, float eps, float* scale,
+                           float* shift, float* mean, float* rstd, void* stream);
+/* Backward coefficients of the level-packed GroupNorm (partial from adr_nc_reduce RED_BWD over the sub-images):
+ * dx = A*g + B*x + C with A, B, C [N'][C] replicated per sub-image (adr_gn_bwd_finalize's gn_bwd_coef per image). */
+int adr_gn_bwd_coef_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows, int C,
+                           int G, const void* const* gamma, const float* mean, const float* rstd, float* A, float* B,
+                           float* Cc, void* stream);
+/* Per (level, image) segment of the packed row space: out[j][c] = sum of in[j'][c] over the segment's sub-images
+ * / (k[l] * sub_rows), replicated to each sub-image j of the segment (in, out: [N'][C] fp32). With `in` the
+ * per-sub-image pixel sums this is the head's global average pool (head.py:1142); applied to the pool's output
+ * gradient it is the backward's per-image sum. */
+int adr_seg_mean_packed(const float* in, int levels, const int* k, int N, int sub_rows, int C, float* out,
+                        void* stream);
 /* dgamma / dbeta (+)= column sums over images of the adr_gn_act_bwd_fused rows. */
 int adr_gn_param_grad(const float* partial, int N, int C, int G, const float* mean, const float* rstd,
                       float* dgamma, float* dbeta, int accumulate, void* stream);

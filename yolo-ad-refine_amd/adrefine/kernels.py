@@ -429,7 +429,6 @@ def conv_fwd_fp8(d, xp, w, Cw, Cp, bias, yp, stats):
         st = [torch.zeros(nb, dtype=torch.float32, device=dev), torch.zeros(nb, dtype=torch.float32, device=dev)]
         w._adr_fp8 = st
         lib.adr_amax_bf16(ctypes.c_void_p(xp), d.x_cstride, 0, d.n * d.h * d.w, d.c, fptr(st[0]), stream())
-        _ready()
     w8 = torch.empty(K_ * RS * Cp, dtype=torch.uint8, device=dev)
     winv = torch.empty(K_, dtype=torch.float32, device=dev)
     lib.adr_pack_weight_fp8(fptr(w.detach().float().contiguous()), K_, Cw, Cp, RS, fptr(w8), fptr(winv), fptr(st[0]),
@@ -756,9 +755,7 @@ DEFER_MAX_BYTES = int(__import__("os").environ.get("ADR_DEFER_MAX_BYTES", 1 << 6
 
 
 def defer_wgrad():
-    """Context manager: defer arena-bound WGRAD reductions to one batched flush at exit. Work the backward ran on
-    the concurrent head-level streams is joined first (their deferrals flushed on their own streams, the current
-    stream waits for them, their gradient slabs folded into the arena in the serial order: _join_levels)."""
+    """Context manager: defer arena-bound WGRAD reductions to one batched flush at exit."""
     import contextlib
 
     @contextlib.contextmanager
@@ -767,219 +764,21 @@ def defer_wgrad():
         prev, _DEFER = _DEFER, WgradDeferral()
         try:
             yield _DEFER
-            _join_levels()
             _DEFER.flush()
         finally:
             _DEFER = prev
-            _DEFER_LVL.clear()
-            _SLAB_USE.clear()
             bnxf_clear()
     return _cm()
 
 
-# ---------------------------------------------------------------------------------------------------------
-# Concurrent AYHead levels. The head runs the same chain of ~70 small kernels per pyramid level (head.py:1132 loops
-# the levels); at P4 (40x40) and P5 (20x20) those kernels fill a fraction of the chip. run_levels() runs each level
-# on its own stream (forked from and joined back into the current stream; inside a hipGraph capture the branches
-# become parallel graph branches), and autograd runs every backward op on its forward op's stream, so the levels'
-# backward chains overlap the same way. What the levels share is handled here:
-#   * shared parameters (share_conv, the decompositions, cross-task, DCN, ...): every arena write made on a level
-#     stream goes to that stream's gradient slab (_grad_buf); at the end of the backward the slabs are folded into
-#     the arena in the order the serial path accumulates them (first-use order per parameter), so the arena is
-#     bitwise the serial one;
-#   * deferred reductions: one WgradDeferral per level stream (_dfr), flushed on that stream;
-#   * BatchNorm running statistics of a shared BN (CoordAtt.bn1): updated at the forward join, in level order;
-#   * the level input's fan-out gradient sink: the level reads a fresh view (_LevelIn), so its input gradient
-#     returns through autograd (stream-synchronised) instead of being accumulated into a buffer the main stream
-#     also writes;
-#   * tensors crossing streams are record_stream()-ed so the caching allocator never hands their memory to the
-#     other stream early.
-# OFF by default (LEVEL_STREAMS / ADR_LEVEL_STREAMS=1 turns it on): measured under hipGraph replay on ROCm 7 the
-# branched graph is slower, not faster — 26.6 vs 24.6 ms/step (scripts/ab_levels.sh, profiles/r04a_ab_levels.txt):
-# the runtime places the branches on separate hardware queues and its cross-queue waits cost more than the overlap
-# wins (DEBUG_HIP_FORCE_GRAPH_QUEUES=1 folds them back onto one queue: 24.7 ms, i.e. serial). The path stays tested
-# bitwise against the serial order (tests/test_gpu_levels.py) for runtimes whose branched graphs overlap cheaply.
-# ---------------------------------------------------------------------------------------------------------
-LEVEL_STREAMS = bool(int(__import__("os").environ.get("ADR_LEVEL_STREAMS", "0")))
-_LVL_STREAMS = {}   # device index -> [torch.cuda.Stream]
-_LVL_IDS = {}       # stream handle -> torch.cuda.Stream (every level stream ever created)
-_DEFER_LVL = {}     # level stream handle -> WgradDeferral (during a deferred backward)
-_SLABS = {}         # level stream handle -> fp32 gradient slab (arena-sized, zero between backwards)
-_SLABS_RETIRED = []
-_SLAB_USE = []      # (stream handle, arena, offset, numel) in first-use order
-_SLAB_SEEN = set()
-_LVL_BN = []        # deferred running-statistics updates of BatchNorms run on level streams (forward order)
-_LVL_FORKED = {}    # level streams forked since the last backward join (handle -> stream)
-
-
-def _cur_sid():
-    return torch.cuda.current_stream().cuda_stream
-
-
-def _on_level_stream():
-    return bool(_LVL_IDS) and _cur_sid() in _LVL_IDS
-
-
 def _dfr():
-    """The active WgradDeferral for the current stream (a level stream gets its own)."""
-    if _DEFER is None:
-        return None
-    if _LVL_IDS:
-        sid = _cur_sid()
-        if sid in _LVL_IDS:
-            d = _DEFER_LVL.get(sid)
-            if d is None:
-                d = _DEFER_LVL[sid] = WgradDeferral()
-            return d
+    """The active WgradDeferral (None outside a deferred backward)."""
     return _DEFER
 
 
 def _grad_buf(tgt):
-    """The gradient destination of arena parameter tgt for the current stream: its arena slice, or on a level
-    stream the same offsets of that stream's slab."""
-    if _LVL_IDS:
-        sid = _cur_sid()
-        if sid in _LVL_IDS:
-            arena, off, n = tgt._adr_arena, tgt._adr_goff, tgt.numel()
-            slab = _SLABS.get(sid)
-            if slab is None or slab.numel() < arena.numel():
-                if slab is not None:
-                    _SLABS_RETIRED.append(slab)
-                slab = _SLABS[sid] = torch.zeros(arena.numel(), dtype=torch.float32, device=arena.device)
-                _ready()
-            if (sid, arena.data_ptr(), off) not in _SLAB_SEEN:
-                _SLAB_SEEN.add((sid, arena.data_ptr(), off))
-                _SLAB_USE.append((sid, arena, off, n))
-            return slab[off:off + n]
+    """The gradient destination of arena parameter tgt: its arena slice."""
     return tgt._adr_grad
-
-
-def _ready():
-    """A persistent buffer just initialised on a level stream is read by the other levels' streams: wait for it
-    (eager warm-up only; never inside a graph capture, where it already exists)."""
-    if _on_level_stream() and not torch.cuda.is_current_stream_capturing():
-        torch.cuda.current_stream().synchronize()
-
-
-def level_streams(dev, n):
-    key = torch.device(dev).index
-    lst = _LVL_STREAMS.setdefault(key, [])
-    while len(lst) < n:
-        st = torch.cuda.Stream(dev)
-        lst.append(st)
-        _LVL_IDS[st.cuda_stream] = st
-    return lst[:n]
-
-
-def _levels_on(xs):
-    return (LEVEL_STREAMS and len(xs) > 1 and all(isinstance(x, torch.Tensor) and x.is_cuda for x in xs) and
-            _TIMING is None and not _on_level_stream())
-
-
-class _LevelIn(torch.autograd.Function):
-    """Identity at the fork (on the forking stream): a fresh view without the fan-out sink; the gradient coming back
-    from the level stream is marked as used on this stream."""
-
-    @staticmethod
-    def forward(ctx, x):
-        ctx.set_materialize_grads(False)
-        return x[:, :]
-
-    @staticmethod
-    def backward(ctx, g):
-        if g is not None:
-            g.record_stream(torch.cuda.current_stream())
-        return g
-
-
-class _LevelOut(torch.autograd.Function):
-    """Identity at the end of a level (on the level stream): the gradient arriving from the joined stream is marked
-    as used on the level stream."""
-
-    @staticmethod
-    def forward(ctx, y):
-        ctx.set_materialize_grads(False)
-        return y[:, :]
-
-    @staticmethod
-    def backward(ctx, g):
-        if g is not None:
-            g.record_stream(torch.cuda.current_stream())
-        return g
-
-
-def run_levels(fn, xs):
-    """[fn(i, xs[i]) for each level], each level on its own stream when enabled (see above); the results are ready
-    on the current stream when this returns."""
-    if not _levels_on(xs):
-        return [fn(i, x) for i, x in enumerate(xs)]
-    main = torch.cuda.current_stream()
-    sts = level_streams(xs[0].device, len(xs))
-    ins = [_LevelIn.apply(x) for x in xs]
-    outs = []
-    for i, (x, st) in enumerate(zip(ins, sts)):
-        _LVL_FORKED[st.cuda_stream] = st
-        st.wait_stream(main)
-        x.record_stream(st)
-        with torch.cuda.stream(st):
-            y = fn(i, x)
-            outs.append(_LevelOut.apply(y) if isinstance(y, torch.Tensor) else y)
-    for y, st in zip(outs, sts):
-        main.wait_stream(st)
-        if isinstance(y, torch.Tensor):
-            y.record_stream(main)
-    _flush_level_bn()
-    return outs
-
-
-def _flush_level_bn():
-    """Running-statistics updates of BatchNorms that ran on level streams, in forward (level) order on the current
-    stream: the same adr_bn_finalize arithmetic over the saved partial statistics, coefficients discarded."""
-    if not _LVL_BN:
-        return
-    for stats, P, C, count, gamma, beta, rm, rv, momentum, eps in _LVL_BN:
-        dev = stats.device
-        stats.record_stream(torch.cuda.current_stream())  # written on a level stream, read here
-        scr = torch.empty(4 * C, dtype=torch.float32, device=dev)
-        lib.adr_bn_finalize(fptr(stats), P, C, float(count), fptr(gamma.detach()), fptr(beta.detach()), fptr(rm),
-                            fptr(rv), float(momentum), float(eps), 1, fptr(scr[:C]), fptr(scr[C:2 * C]),
-                            fptr(scr[2 * C:3 * C]), fptr(scr[3 * C:]), stream())
-    _LVL_BN.clear()
-
-
-def _join_levels():
-    """End of a deferred backward: flush each level stream's deferral on that stream, make the current stream wait
-    for the level streams, then fold the gradient slabs into the arena (adr_axpy_zero_batched, which also clears
-    them). A parameter that several levels contributed to receives the contributions in first-use order — the
-    order in which the serial path accumulated them — one batched launch per rank."""
-    if not _LVL_IDS:
-        return
-    main = torch.cuda.current_stream()
-    for sid, d in list(_DEFER_LVL.items()):
-        with torch.cuda.stream(_LVL_IDS[sid]):
-            d.flush()
-    used = {e[0] for e in _SLAB_USE} | set(_DEFER_LVL) | set(_LVL_FORKED)
-    for sid in used:
-        main.wait_stream(_LVL_IDS[sid])
-    _DEFER_LVL.clear()
-    _LVL_FORKED.clear()
-    if not _SLAB_USE:
-        return
-    ranks = {}
-    rounds = []
-    for sid, arena, off, n in _SLAB_USE:
-        key = (arena.data_ptr(), off)
-        r = ranks.get(key, 0)
-        ranks[key] = r + 1
-        while len(rounds) <= r:
-            rounds.append([])
-        slab = _SLABS[sid]
-        rounds[r].append(AxpyEntry(slab.data_ptr() + 4 * off, arena.data_ptr() + 4 * off, n))
-    for ents in rounds:
-        arr = (AxpyEntry * len(ents))(*ents)
-        lib.adr_axpy_zero_batched(ctypes.cast(arr, ctypes.c_void_p), len(ents), stream())
-    _SLAB_USE.clear()
-    _SLAB_SEEN.clear()
 
 
 def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device, keep=()):
@@ -1261,13 +1060,8 @@ class BNActFn(torch.autograd.Function):
             P = stats.numel() // (2 * C)
         else:
             P = 0
-        # on a concurrent head-level stream the running statistics of a shared BN are updated at the join, in level
-        # order (run_levels / _flush_level_bn)
-        lvl = training and rm is not None and _on_level_stream()
-        if lvl:
-            _LVL_BN.append((stats, P, C, N * HW, gamma, beta, rm, rv, momentum, eps))
         lib.adr_bn_finalize(fptr(stats) if training else None, P, C, float(N * HW), fptr(gamma.detach()),
-                            fptr(beta.detach()), None if lvl else fptr(rm), None if lvl else fptr(rv), float(momentum),
+                            fptr(beta.detach()), fptr(rm), fptr(rv), float(momentum),
                             float(eps), int(training), fptr(scale), fptr(shift), fptr(mean), fptr(rstd), stream())
         z, zp, zcs = _out_view(box, N, C, H, W, dtype, dev)
         if lazy and box is None and BN_XF_FWD and training and dtype == torch.bfloat16 and act in ("silu", "none") \
@@ -1656,7 +1450,6 @@ def _ones(n, dev):
     t = _ONES.get((n, dev))
     if t is None:
         t = _ONES[(n, dev)] = torch.ones(n, dtype=torch.float32, device=dev)
-        _ready()
     return t
 
 
@@ -1675,7 +1468,6 @@ def _zeros_f32(n, dev):
     t = _ONES.get(("z", n, dev))
     if t is None:
         t = _ONES[("z", n, dev)] = torch.zeros(n, dtype=torch.float32, device=dev)
-        _ready()
     return t
 
 
@@ -1741,7 +1533,6 @@ def _bn_eval_coefs(bn, dev):
     _bn_eval_coefs_into(bn, scale, shift)
     if pc is not None and pc.cache_bn_coefs:
         pc.bn_coefs[id(bn)] = (bn, scale, shift)
-        _ready()  # (a shared BN's cached pair is read by the other head-level streams)
     return scale, shift
 
 
@@ -1806,7 +1597,6 @@ def _const(value, device):
     t = _CONSTS.get(key)
     if t is None:
         t = _CONSTS[key] = torch.full((1,), float(value), dtype=torch.float32, device=device)
-        _ready()
     return t
 
 
@@ -2622,7 +2412,6 @@ def _padded_bias(b, K, kpad, dev):
     hit = _PBIAS.get(key)
     if hit is None or (b is not None and hit[0] is not b):
         hit = _PBIAS[key] = (b, torch.zeros(kpad, dtype=torch.float32, device=dev))
-        _ready()
     if b is not None:
         lib.adr_cast(F32, fptr(b.detach().float().contiguous()), F32, fptr(hit[1]), K, stream())
     return hit[1]
@@ -2690,8 +2479,8 @@ _DCN_FAR_RETIRED = []  # outgrown buffers: a captured graph may still address th
 def _dcn_far_scratch(dev, N, H, W, C):
     """Persistent zeroed scratch of adr_dcn_bwd_bf16: the fp32 far-corner buffer and the tile flags. The kernels
     leave both zero again, so ONE pair per device serves every level, shape, step and graph replay (calls are
-    stream-ordered; the concurrent head levels each have their own pair); a call uses a prefix view of it."""
-    key = (str(dev), _cur_sid() if _on_level_stream() else 0)
+    stream-ordered); a call uses a prefix view of it."""
+    key = str(dev)
     n, nt = N * H * W * C, int(lib.adr_dcn_bwd_tiles(N, H, W))
     cur = _DCN_FAR.get(key)
     if cur is None or cur[0].numel() < n or cur[1].numel() < nt:
@@ -2700,7 +2489,6 @@ def _dcn_far_scratch(dev, N, H, W, C):
             n, nt = max(n, cur[0].numel()), max(nt, cur[1].numel())
         cur = (torch.zeros(n, dtype=torch.float32, device=dev), torch.zeros(nt, dtype=torch.int32, device=dev))
         _DCN_FAR[key] = cur
-        _ready()
     return cur[0][:N * H * W * C], cur[1][:int(lib.adr_dcn_bwd_tiles(N, H, W))]
 
 
@@ -3479,3 +3267,632 @@ def dropout(x, p, seed, training):
     if not training or p == 0.0:
         return x
     return DropoutFn.apply(x, p, seed)
+
+
+# ------------------------------------------------------------------------------------------------------------
+# Level-packed AYHead. The reference runs the head once per pyramid level (head.py:1132-1176): ~60 launches per
+# level forward, twice that backward, most of them per-pixel kernels that at P4 (40x40) and P5 (20x20) fill a
+# fraction of the chip. Here the three levels live in ONE row space — level l's NHWC rows (image, y, x) stored
+# back to back, P3 first — so every per-pixel op (1x1 convs, gates, elementwise, activations) is one launch over
+# all levels; ops that need the level structure take a LevelPack:
+#   * per-image statistics (GroupNorm, the global average pool): the row space is cut into sub-images of S rows
+#     (S = gcd of the levels' H*W, the P5 map) and segment kernels combine an image's sub-images
+#     (adr_gn_finalize_packed / adr_gn_bwd_coef_packed / adr_seg_mean_packed);
+#   * spatial ops (3x3 convs, DCN, CoordAtt's axis means / gates): one launch per level on the level's view, the
+#     levels' split-K WGRAD slabs reduced by one entry.
+# ------------------------------------------------------------------------------------------------------------
+class LevelPack:
+    """Geometry of the packed row space: N images per level, level dims [(H, W)]; a packed activation is an
+    (N', C, 1, S) NHWC tensor with N' = N * sum(k), k[l] = H_l*W_l / S sub-images per image of level l."""
+
+    def __init__(self, N, dims):
+        import math
+        self.N = int(N)
+        self.dims = tuple((int(h), int(w)) for h, w in dims)
+        hw = [h * w for h, w in self.dims]
+        S = 0
+        for v in hw:
+            S = math.gcd(S, v)
+        self.S = S
+        self.L = len(hw)
+        self.k = tuple(v // S for v in hw)
+        self.Np = self.N * sum(self.k)
+        self.off, o = [], 0
+        for v in hw:
+            self.off.append(o)
+            o += self.N * v
+        self.rows = o
+        self.sub0 = [off // S for off in self.off]
+        self.k_c = (ctypes.c_int * self.L)(*self.k)
+
+    def empty(self, C, dtype, dev):
+        return empty_act(self.Np, C, 1, self.S, dtype, dev)
+
+    def fits(self, t):
+        return t.shape[0] == self.Np and t.shape[2] == 1 and t.shape[3] == self.S
+
+    def view(self, t, l):
+        """Level l of packed t (a whole packed activation or a channel slice of one) as an (N, C, H, W) NHWC view."""
+        H, W = self.dims[l]
+        C, cs = t.shape[1], t.stride(3)
+        return torch.as_strided(t, (self.N, C, H, W), (H * W * cs, 1, W * cs, cs),
+                                t.storage_offset() + self.off[l] * cs)
+
+    def at(self, ptr, cs, es, l):
+        """Address of level l's first row in a packed buffer at ptr with channel stride cs."""
+        return ctypes.c_void_p(ptr + self.off[l] * cs * es)
+
+
+def _ptrs(ts):
+    arr = (ctypes.c_void_p * len(ts))(*[None if t is None else t.data_ptr() for t in ts])
+    return ctypes.cast(arr, ctypes.c_void_p), arr
+
+
+class LevelJoinFn(torch.autograd.Function):
+    """Per-level pieces (N, C, H_l, W_l) -> one packed activation. Pieces already written in place through their
+    level view of the box (conv2d out=) are not copied. Backward: each piece gets its level view of the gradient."""
+
+    @staticmethod
+    def forward(ctx, box, pack, *xs):
+        x0 = xs[0]
+        C = x0.shape[1]
+        out = pack.empty(C, x0.dtype, x0.device) if box is None else box.t
+        if not pack.fits(out) or out.shape[1] != C:
+            raise RuntimeError("level_join: out must be a packed activation of the pieces' channels")
+        for l, x in enumerate(xs):
+            o = pack.view(out, l)
+            v = _v(x)
+            if not (v[1] == o.data_ptr() and v[2] == o.stride(3)):
+                _ew(EW_COPY, (o, o.data_ptr(), o.stride(3)), v)
+        ctx.pack = pack
+        return out if box is None else out[:, :]
+
+    @staticmethod
+    def backward(ctx, dy):
+        dy, _, _ = _v(dy)
+        return (None, None) + tuple(ctx.pack.view(dy, l) for l in range(ctx.pack.L))
+
+
+def level_join(xs, pack, out=None):
+    return LevelJoinFn.apply(None if out is None else OutBox(out), pack, *xs)
+
+
+class LevelSplitFn(torch.autograd.Function):
+    """Packed activation -> its per-level (N, C, H_l, W_l) views (the head's output list). Backward: gradients that
+    are the level views of one packed buffer (the loss writes them so) are handed back as that buffer."""
+
+    @staticmethod
+    def forward(ctx, x, pack):
+        ctx.set_materialize_grads(False)
+        ctx.pack, ctx.meta = pack, (tuple(x.shape), x.dtype)
+        return tuple(pack.view(x, l) for l in range(pack.L))
+
+    @staticmethod
+    def backward(ctx, *grads):
+        pack = ctx.pack
+        (Np, C, _, S), dtype = ctx.meta
+        if all(g is not None and g.dtype == dtype for g in grads):
+            g0 = grads[0]
+            cs, es, st = g0.stride(3), g0.element_size(), g0.untyped_storage().data_ptr()
+            ok = cs >= C and cs % (16 // es) == 0
+            for l, g in enumerate(grads):
+                H, W = pack.dims[l]
+                ok = ok and g.untyped_storage().data_ptr() == st and \
+                    g.stride() == (H * W * cs, 1, W * cs, cs) and \
+                    g.data_ptr() == g0.data_ptr() + (pack.off[l] - pack.off[0]) * cs * es
+            if ok:
+                return torch.as_strided(g0, (Np, C, 1, S), (S * cs, 1, S * cs, cs), g0.storage_offset()), None
+        dev = next(g for g in grads if g is not None).device
+        dx = pack.empty(C, dtype, dev)
+        es = dx.element_size()
+        for l, g in enumerate(grads):
+            o = pack.view(dx, l)
+            if g is None:
+                lib.adr_memset_zero(ctypes.c_void_p(o.data_ptr()), o.numel() * es, stream())
+            else:
+                _ew(EW_COPY, (o, o.data_ptr(), C), _v(g.to(dtype) if g.dtype != dtype else g))
+        return dx, None
+
+
+def level_split(x, pack):
+    outs = LevelSplitFn.apply(x, pack)
+    for o in outs:
+        o._adr_pack = pack
+    return outs
+
+
+class GNPackFn(torch.autograd.Function):
+    """act(GroupNorm(G)(y)) per (level, image) of a packed activation: nc_reduce over the sub-images, one segmented
+    finalize, affine_act with per-sub-image coefficients; backward the same three launches. `params` holds
+    (gamma, beta) of a GroupNorm shared by the levels, or per_level: gamma_0..gamma_{L-1}, beta_0..beta_{L-1}."""
+
+    @staticmethod
+    def forward(ctx, y, pack, groups, act, eps, per_level, *params):
+        dtype = y.dtype
+        y, yp, ycs = nhwc(y)
+        Np, C, _, S = y.shape
+        dev = y.device
+        nl = len(params) // 2
+        gam = [params[l if per_level else 0].detach() for l in range(pack.L)]
+        bet = [params[nl + (l if per_level else 0)].detach() for l in range(pack.L)]
+        rows = _stats_rows(Np, S)
+        chunks = lib.adr_nc_reduce_chunks(S, rows)
+        part = torch.empty(Np * chunks * 2 * C, dtype=torch.float32, device=dev)
+        scale = torch.empty(Np * C, dtype=torch.float32, device=dev)
+        shift = torch.empty(Np * C, dtype=torch.float32, device=dev)
+        mean = torch.empty(Np * groups, dtype=torch.float32, device=dev)
+        rstd = torch.empty(Np * groups, dtype=torch.float32, device=dev)
+        lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, Np, S, C, rows,
+                          fptr(part), stream())
+        (gp, _ga), (bp, _ba) = _ptrs(gam), _ptrs(bet)
+        lib.adr_gn_finalize_packed(fptr(part), pack.L, ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, chunks, S, C,
+                                   groups, gp, bp, float(eps), fptr(scale), fptr(shift), fptr(mean), fptr(rstd),
+                                   stream())
+        z = pack.empty(C, dtype, dev)
+        lib.adr_affine_act(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(z.data_ptr()), C, 0,
+                           fptr(scale), fptr(shift), 1, ACT[act], Np, S, C, stream())
+        ctx.save_for_backward(y, scale, shift, mean, rstd)
+        ctx.meta = (groups, act, bool(per_level), chunks, rows)
+        ctx.pack, ctx.params = pack, params
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        y, scale, shift, mean, rstd = ctx.saved_tensors
+        groups, act, per_level, chunks, rows = ctx.meta
+        pack, params = ctx.pack, ctx.params
+        dz, dzp, dzcs = nhwc(dz.to(y.dtype) if dz.dtype != y.dtype else dz)
+        _, yp, ycs = nhwc(y)
+        Np, C, _, S = y.shape
+        dev = y.device
+        dt = dcode(y.dtype)
+        nl = len(params) // 2
+        part = torch.empty(Np * chunks * 2 * C, dtype=torch.float32, device=dev)
+        lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
+                          fptr(shift), 1, ACT[act], Np, S, C, rows, fptr(part), stream())
+        A = torch.empty(Np * C, dtype=torch.float32, device=dev)
+        B = torch.empty(Np * C, dtype=torch.float32, device=dev)
+        Cc = torch.empty(Np * C, dtype=torch.float32, device=dev)
+        gp, _ga = _ptrs([params[l if per_level else 0].detach() for l in range(pack.L)])
+        lib.adr_gn_bwd_coef_packed(fptr(part), pack.L, ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, chunks, S, C,
+                                   groups, gp, fptr(mean), fptr(rstd), fptr(A), fptr(B), fptr(Cc), stream())
+        dy = pack.empty(C, y.dtype, dev)
+        lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
+                               ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
+                               fptr(Cc), 1, 1, ACT[act], Np, S, C, 0, stream())
+        grads = [None] * len(params)
+        for j in range(nl):  # dgamma / dbeta over the sub-images of level j (or of every level: shared)
+            s0, n = (pack.sub0[j], pack.N * pack.k[j]) if per_level else (0, Np)
+            pv, mv, rv = part[s0 * chunks * 2 * C:], mean[s0 * groups:], rstd[s0 * groups:]
+            gam, bet = params[j], params[nl + j]
+            dgamma, pg, acc_g = grad_dst(gam, C, dev)
+            dbeta, pb, acc_b = grad_dst(bet, C, dev)
+            if acc_g != acc_b:
+                raise RuntimeError("GN gamma/beta gradients must share one destination kind")
+            if _defer_gn(acc_g):
+                _dfr().add_gnparam(pv, mv, rv, pg, pb, n, chunks, C, groups, acc_g)
+            else:
+                val = lambda q: q.value if isinstance(q, ctypes.c_void_p) else q  # noqa: E731
+                arr = (GnParamEntry * 1)(GnParamEntry(pv.data_ptr(), mv.data_ptr(), rv.data_ptr(), val(pg), val(pb),
+                                                      n, chunks, C, groups, acc_g, 0))
+                lib.adr_gn_param_grad_batched(ctypes.cast(arr, ctypes.c_void_p), 1, stream())
+            grads[j], grads[nl + j] = grad_ret(gam, dgamma), grad_ret(bet, dbeta)
+        return (dy, None, None, None, None, None, *grads)
+
+
+def gn_act_packed(y, pack, gns, act):
+    """GroupNorm + activation of a packed activation; gns: one nn.GroupNorm shared by the levels, or one per level."""
+    gns = list(gns)
+    per_level = len(gns) > 1
+    if per_level and len(gns) != pack.L:
+        raise RuntimeError("gn_act_packed: one GroupNorm, or one per level")
+    g0 = gns[0]
+    return GNPackFn.apply(y, pack, g0.num_groups, act, g0.eps, per_level, *[g.weight for g in gns],
+                          *[g.bias for g in gns])
+
+
+class GapPackFn(torch.autograd.Function):
+    """Global average pool per (level, image) of a packed activation, replicated to each sub-image: (N', C) fp32
+    (F.adaptive_avg_pool2d(x, 1), head.py:1142, for every level at once)."""
+
+    @staticmethod
+    def forward(ctx, x, pack):
+        Np, C, _, S = x.shape
+        s = _reduce_dot(None, x, False, False, which=1)  # per-sub-image sums
+        out = torch.empty(Np, C, dtype=torch.float32, device=x.device)
+        lib.adr_seg_mean_packed(fptr(s), pack.L, ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, S, C, fptr(out),
+                                stream())
+        ctx.pack, ctx.meta = pack, (tuple(x.shape), x.dtype)
+        return out
+
+    @staticmethod
+    def backward(ctx, dg):
+        pack = ctx.pack
+        (Np, C, _, S), dtype = ctx.meta
+        dgc = dg.float().contiguous()
+        t = torch.empty_like(dgc)
+        lib.adr_seg_mean_packed(fptr(dgc), pack.L, ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, S, C, fptr(t),
+                                stream())
+        dx = pack.empty(C, dtype, dg.device)
+        lib.adr_bcast_fill(dcode(dtype), fptr(t), C, 1, 1.0, ctypes.c_void_p(dx.data_ptr()), C, Np, S, C, 0, stream())
+        return dx, None
+
+
+def gap_packed(x, pack):
+    return GapPackFn.apply(x, pack)
+
+
+def wgrad_param_multi(param, pieces, K, C, RS, wshape, cpad, device):
+    """wgrad_param over several contractions of one weight (the head's per-level convs): every piece's split-K slabs
+    go to one buffer and ONE reduction sums them all (one deferral entry, no flush for a repeated destination)."""
+    K_, C_ = wshape[0], wshape[1]
+    RS_ = 1
+    for v in wshape[2:]:
+        RS_ *= v
+    stride = K * RS * C
+    splits = [lib.adr_conv2d_wgrad_splits(ctypes.byref(d)) for d, _, _ in pieces]
+    ws = torch.empty(sum(splits) * stride, dtype=torch.float32, device=device)
+    s0 = 0
+    for (d, xp, dyp), sp in zip(pieces, splits):
+        es = 2 if d.dtype == BF16 else 4
+        name = (f"void adr::wgrad_bf16_kernel<{_bn_of(K)}, {_bn_of(C)}>(adr::WgArgs)" if d.dtype == BF16
+                else _gemm_symbol(F32, _bn_of(C), 2))
+        work = (es * (d.n * d.h * d.w * d.c + d.n * d.ho * d.wo * d.k) + 4 * sp * stride,
+                2 * d.n * d.ho * d.wo * d.k * RS * d.c)
+        tok = _t0(name, *work, _shape(d, f"wgrad/{sp}") if _TIMING is not None else "")
+        lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp),
+                                      ctypes.c_void_p(ws.data_ptr() + 4 * s0 * stride), 0, stream())
+        _t1(tok)
+        s0 += sp
+    Cp = max(C_, cpad)
+    out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
+    if _dfr() is not None and acc and _TIMING is None and s0 * stride * 4 <= DEFER_MAX_BYTES:
+        _dfr().add(ws, stride, s0, ptr, K_, C_, Cp, RS_, 0, acc)
+        return grad_ret(param, out)
+    lib.adr_wgrad_reduce_unpack(fptr(ws), stride, s0, ptr, K_, C_, Cp, RS_, 0, acc, stream())
+    return grad_ret(param, out)
+
+
+class LevelConvFn(torch.autograd.Function):
+    """Dense stride-1 k x k conv (pad k//2) of a packed activation, level by level (each level's map is its own
+    image grid): one launch per level forward and data gradient, the levels' WGRAD slabs reduced once. kpad > 0:
+    output channels zero-padded to kpad (PaddedConvFn: 27 -> 32 offsets/mask, 1 -> 8 cls_prob)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, pad, kpad, pack):
+        sink_ = getattr(x, "_adr_sink", None)
+        ctx.sink = sink_ if sink_ is not None and sink_.fits(x) else None
+        dtype = x.dtype
+        x, xp, xcs = nhwc(x)
+        Np, C, _, S = x.shape
+        K, Cw, R, Sk = w.shape
+        if Cw != C or not pack.fits(x):
+            raise RuntimeError(f"level_conv: input {tuple(x.shape)} vs weight {tuple(w.shape)} / pack")
+        dev = x.device
+        Kp = max(K, kpad)
+        if kpad and dtype != torch.bfloat16:
+            wp, wt = torch.empty(Kp * R * Sk * C, dtype=dtype, device=dev), None
+            zero_(wp)
+            lib.adr_pack_weight(dcode(dtype), fptr(w.detach().float().contiguous()), fptr(wp), K, C, C, R * Sk, 0,
+                                stream())
+        else:
+            wp, wt = pack_weight2(w, dtype, kpad=kpad)
+        if kpad:
+            bp = _padded_bias(b, K, kpad, dev)
+        else:
+            bp = b.detach().float().contiguous() if b is not None else None
+        y = pack.empty(Kp, dtype, dev)
+        es = x.element_size()
+        for l, (H, W) in enumerate(pack.dims):
+            d, _, _ = conv_desc(pack.N, H, W, C, xcs, Kp, R, Sk, 1, 1, pad, pad, Kp, dtype)
+            conv_fwd(d, pack.at(xp, xcs, es, l).value, wp.data_ptr(), fptr(bp), pack.at(y.data_ptr(), Kp, es, l).value)
+        ctx.save_for_backward(x, wp, wt)
+        ctx.meta = (pad, kpad, tuple(w.shape), b is not None)
+        ctx.pw, ctx.pb, ctx.pack = w, b, pack
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, wp, wt = ctx.saved_tensors
+        pad, kpad, wshape, has_b = ctx.meta
+        pack = ctx.pack
+        dy, dyp, dycs = nhwc(dy.to(x.dtype) if dy.dtype != x.dtype else dy)
+        Np, C, _, S = x.shape
+        K, _, R, Sk = wshape
+        Kp = max(K, kpad)
+        x, xp, xcs = nhwc(x)
+        es = x.element_size()
+        dev = x.device
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            if ctx.sink is not None:  # into the fan-out's shared gradient (accumulating after the first consumer)
+                buf, acc, _ = ctx.sink.claim(dev)
+            else:
+                buf, acc = pack.empty(C, x.dtype, dev), 0
+            bcs = buf.stride(3)
+            for l, (H, W) in enumerate(pack.dims):
+                d2, _, _ = conv_desc(pack.N, H, W, C, bcs, Kp, R, Sk, 1, 1, pad, pad, dycs, x.dtype)
+                conv_dgrad(d2, pack.at(dyp, dycs, es, l).value, (wp, wt), None, pack.at(buf.data_ptr(), bcs, es, l).value,
+                           accumulate=acc)
+            dx = None if ctx.sink is not None else buf
+        if ctx.needs_input_grad[1]:
+            pieces = []
+            for l, (H, W) in enumerate(pack.dims):
+                d, _, _ = conv_desc(pack.N, H, W, C, xcs, Kp, R, Sk, 1, 1, pad, pad, dycs, x.dtype)
+                pieces.append((d, pack.at(xp, xcs, es, l).value, pack.at(dyp, dycs, es, l).value))
+            dw = wgrad_param_multi(ctx.pw, pieces, Kp, C, R * Sk, wshape, 0, dev)
+        if has_b and ctx.needs_input_grad[2]:
+            if kpad:
+                db = sink(ctx.pb, _bias_grad(dy, Kp, Np, S, dycs)[:K])
+            else:
+                db = _bias_grad(dy, K, Np, S, dycs, ctx.pb)
+        return dx, dw, db, None, None, None
+
+
+def level_conv(x, w, b, pad, pack, kpad=0):
+    return LevelConvFn.apply(x, w, b, pad, kpad, pack)
+
+
+class LevelDCNFn(torch.autograd.Function):
+    """DCNFn (mmcv ModulatedDeformConv2d 3x3, head.py:751-782) on a packed activation, level by level; the fp32
+    path's column GEMMs run once over every level's rows."""
+
+    @staticmethod
+    def forward(ctx, x, om, w, pack):
+        dtype = x.dtype
+        x, xp, xcs = nhwc(x)
+        om, omp, omcs = nhwc(om)
+        Np, C, _, S = x.shape
+        Cout = w.shape[0]
+        dev = x.device
+        es = x.element_size()
+        N = pack.N
+        y = pack.empty(Cout, dtype, dev)
+        ctx.fused = _dcn_fused(dtype, C, Cout, omcs)
+        ctx.fused_bwd = ctx.fused and C == Cout and C in (64, 128, 256)
+        if ctx.fused:
+            wp = pack_weight2(w, dtype)[0]
+            for l, (H, W) in enumerate(pack.dims):
+                tok = _t0("adr::dcn_fwd_kernel(adr::DcnArgs)", *_dcn_work(N, H, W, C, Cout),
+                          f"dcn fwd n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "", _reps())
+                for _ in range(_reps()):
+                    lib.adr_dcn_fwd_bf16(pack.at(xp, xcs, es, l), xcs, pack.at(omp, omcs, es, l), omcs, fptr(wp),
+                                         pack.at(y.data_ptr(), Cout, es, l), Cout, N, H, W, C, Cout, stream())
+                _t1(tok)
+            ctx.save_for_backward(x, om, w)
+        else:
+            cols = torch.empty(pack.rows * 9 * C, dtype=dtype, device=dev)
+            for l, (H, W) in enumerate(pack.dims):
+                lib.adr_dcn_im2col(dcode(dtype), pack.at(xp, xcs, es, l), xcs, pack.at(omp, omcs, es, l), omcs,
+                                   pack.at(cols.data_ptr(), 9 * C, es, l), N, H, W, C, stream())
+            wp = pack_weight(w, dtype)
+            d, _, _ = conv_desc(1, 1, pack.rows, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, Cout, dtype)
+            conv_fwd(d, cols.data_ptr(), wp.data_ptr(), None, y.data_ptr())
+            ctx.save_for_backward(x, om, cols, w)
+        ctx.pw, ctx.pack = w, pack
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        pack = ctx.pack
+        cols = None
+        if ctx.fused:
+            x, om, w = ctx.saved_tensors
+        else:
+            x, om, cols, w = ctx.saved_tensors
+        dtype = x.dtype
+        _, xp, xcs = nhwc(x)
+        _, omp, omcs = nhwc(om)
+        dy, dyp, dycs = nhwc(dy.to(dtype) if dy.dtype != dtype else dy)
+        Np, C, _, S = x.shape
+        Cout, omc = w.shape[0], om.shape[1]
+        dev = x.device
+        es = x.element_size()
+        N = pack.N
+        wt = torch.empty(9 * C * Cout, dtype=dtype, device=dev)
+        lib.adr_dcn_weight_t(dcode(dtype), fptr(w.detach().float().contiguous()), fptr(wt), Cout, C, stream())
+        dw = None
+        if ctx.fused and not ctx.fused_bwd:
+            cols = torch.empty(pack.rows * 9 * C, dtype=dtype, device=dev)
+            for l, (H, W) in enumerate(pack.dims):
+                lib.adr_dcn_im2col(dcode(dtype), pack.at(xp, xcs, es, l), xcs, pack.at(omp, omcs, es, l), omcs,
+                                   pack.at(cols.data_ptr(), 9 * C, es, l), N, H, W, C, stream())
+        if ctx.fused_bwd:
+            dx = pack.empty(C, dtype, dev)
+            dom = pack.empty(omc, dtype, dev)
+            for l, (H, W) in enumerate(pack.dims):
+                dxf, flags = _dcn_far_scratch(dev, N, H, W, C)
+                nb, fl = _dcn_work(N, H, W, C, Cout)
+                tok = _t0("adr::dcn_bwd_kernel(adr::DcnArgs)", nb + 2 * N * H * W * C, 2 * fl,
+                          f"dcn bwd n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "")
+                lib.adr_dcn_bwd_bf16(pack.at(xp, xcs, es, l), xcs, pack.at(omp, omcs, es, l), omcs,
+                                     pack.at(dyp, dycs, es, l), dycs, fptr(wt), pack.at(dx.data_ptr(), C, es, l), C,
+                                     pack.at(dom.data_ptr(), omc, es, l), omc, fptr(dxf), fptr(flags), N, H, W, C,
+                                     Cout, stream())
+                _t1(tok)
+            if ctx.needs_input_grad[2]:
+                stride = Cout * 9 * C
+                splits = [lib.adr_dcn_wgrad_bf16_splits(N, H, W, C, Cout) for H, W in pack.dims]
+                ws = torch.empty(sum(splits) * stride, dtype=torch.float32, device=dev)
+                s0 = 0
+                for l, (H, W) in enumerate(pack.dims):
+                    nb, fl = _dcn_work(N, H, W, C, Cout)
+                    tok = _t0("adr::dcn_wgrad_kernel(adr::DcnArgs)", nb + 4 * splits[l] * stride, fl,
+                              f"dcn wgrad/{splits[l]} n{N} {H}x{W} c{C}->{Cout}" if _TIMING is not None else "")
+                    lib.adr_dcn_wgrad_bf16(pack.at(xp, xcs, es, l), xcs, pack.at(omp, omcs, es, l), omcs,
+                                           pack.at(dyp, dycs, es, l), dycs,
+                                           ctypes.c_void_p(ws.data_ptr() + 4 * s0 * stride), splits[l], N, H, W, C,
+                                           Cout, stream())
+                    _t1(tok)
+                    s0 += splits[l]
+                out, ptr, acc = grad_dst(ctx.pw, stride, dev)
+                if _dfr() is not None and acc and _TIMING is None:
+                    _dfr().add(ws, stride, s0, ptr, Cout, C, C, 9, 0, acc)
+                else:
+                    lib.adr_wgrad_reduce_unpack(fptr(ws), stride, s0, ptr, Cout, C, C, 9, 0, acc, stream())
+                dw = grad_ret(ctx.pw, out)
+        else:
+            dx32 = zero_(torch.empty(pack.rows * C, dtype=torch.float32, device=dev))
+            dom = zero_(pack.empty(omc, dtype, dev))
+            dcols = torch.empty(pack.rows * 9 * C, dtype=dtype, device=dev)
+            d, _, _ = conv_desc(1, 1, pack.rows, Cout, dycs, 9 * C, 1, 1, 1, 1, 0, 0, 9 * C, dtype)
+            conv_fwd(d, dyp, wt.data_ptr(), None, dcols.data_ptr())
+            if ctx.needs_input_grad[2]:
+                dwd, _, _ = conv_desc(1, 1, pack.rows, 9 * C, 9 * C, Cout, 1, 1, 1, 1, 0, 0, dycs, dtype)
+                dw = wgrad_param(ctx.pw, dwd, cols.data_ptr(), dyp, Cout, 9 * C, 1, w.shape, 0, dev)
+            for l, (H, W) in enumerate(pack.dims):
+                lib.adr_dcn_col2im(dcode(dtype), pack.at(xp, xcs, es, l), xcs, pack.at(omp, omcs, es, l), omcs,
+                                   pack.at(dcols.data_ptr(), 9 * C, es, l), pack.at(dx32.data_ptr(), C, 4, l),
+                                   pack.at(dom.data_ptr(), omc, es, l), omc, N, H, W, C, int(dtype == torch.float32),
+                                   stream())
+            dx = pack.empty(C, dtype, dev)
+            lib.adr_cast(F32, fptr(dx32), dcode(dtype), ctypes.c_void_p(dx.data_ptr()), pack.rows * C, stream())
+        return dx, dom, dw, None
+
+
+def dcn_levels(x, om, w, pack):
+    return LevelDCNFn.apply(x, om, w, pack)
+
+
+class LevelAxisMeanFn(torch.autograd.Function):
+    """CoordAtt's row / column means (AxisMeanFn 'coord', head.py:684-690) of each level of a packed activation:
+    one (N, C, H_l + W_l, 1) tensor per level."""
+
+    @staticmethod
+    def forward(ctx, x, pack):
+        ctx.set_materialize_grads(False)
+        vx = _v(x)
+        C = x.shape[1]
+        es = x.element_size()
+        outs = []
+        for l, (H, W) in enumerate(pack.dims):
+            out = empty_act(pack.N, C, H + W, 1, x.dtype, x.device)
+            lib.adr_axis_mean(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], pack.N, H, W, C,
+                              ctypes.c_void_p(out.data_ptr()), (H + W) * C,
+                              ctypes.c_void_p(out.data_ptr() + H * C * es), (H + W) * C, stream())
+            outs.append(out)
+        ctx.pack, ctx.meta = pack, (C, x.dtype)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *dys):
+        pack = ctx.pack
+        C, dtype = ctx.meta
+        dev = next(g for g in dys if g is not None).device
+        dx = pack.empty(C, dtype, dev)
+        es = dx.element_size()
+        for l, (H, W) in enumerate(pack.dims):
+            dy = dys[l]
+            if dy is None:
+                lib.adr_memset_zero(pack.at(dx.data_ptr(), C, es, l), pack.N * H * W * C * es, stream())
+                continue
+            dy = dy.contiguous(memory_format=torch.channels_last) if not _is_dense_nhwc(dy) else dy
+            lib.adr_axis_mean_bwd(dcode(dtype), ctypes.c_void_p(dy.data_ptr()), (H + W) * C,
+                                  ctypes.c_void_p(dy.data_ptr() + H * C * es), (H + W) * C,
+                                  pack.at(dx.data_ptr(), C, es, l), C, pack.N, H, W, C, 0, stream())
+        return dx, None
+
+
+def axis_mean_levels(x, pack):
+    return LevelAxisMeanFn.apply(x, pack)
+
+
+class LevelGateFn(torch.autograd.Function):
+    """CoordAtt's output x * a_h * a_w (GateFn 'coord', head.py:704-706) per level of a packed activation; a_h / a_w
+    are the levels' (N, C, H_l + W_l, 1) tensors."""
+
+    @staticmethod
+    def forward(ctx, x, pack, *a):
+        L = pack.L
+        ahs = [t if _is_dense_nhwc(t) else t.contiguous(memory_format=torch.channels_last) for t in a[:L]]
+        aws = [t if _is_dense_nhwc(t) else t.contiguous(memory_format=torch.channels_last) for t in a[L:]]
+        vx = _v(x)
+        C = x.shape[1]
+        es = x.element_size()
+        out = pack.empty(C, x.dtype, x.device)
+        for l, (H, W) in enumerate(pack.dims):
+            lib.adr_gate(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], ctypes.c_void_p(ahs[l].data_ptr()),
+                         (H + W) * C, ctypes.c_void_p(aws[l].data_ptr() + H * C * es), (H + W) * C,
+                         pack.at(out.data_ptr(), C, es, l), C, pack.N, H, W, C, stream())
+        ctx.save_for_backward(vx[0], *ahs, *aws)
+        ctx.pack = pack
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        pack = ctx.pack
+        L = pack.L
+        saved = ctx.saved_tensors
+        x, ahs, aws = saved[0], saved[1:1 + L], saved[1 + L:]
+        vx, vd = _v(x), _v(dout)
+        C = x.shape[1]
+        es = x.element_size()
+        dx = pack.empty(C, x.dtype, x.device)
+        dahs, daws = [], []
+        for l, (H, W) in enumerate(pack.dims):
+            dah = torch.empty_like(ahs[l], memory_format=torch.channels_last)
+            daw = torch.empty_like(aws[l], memory_format=torch.channels_last)
+            lib.adr_gate_bwd(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], ctypes.c_void_p(ahs[l].data_ptr()),
+                             (H + W) * C, ctypes.c_void_p(aws[l].data_ptr() + H * C * es), (H + W) * C,
+                             pack.at(vd[1], vd[2], es, l), vd[2], pack.at(dx.data_ptr(), C, es, l), C,
+                             ctypes.c_void_p(dah.data_ptr()), (H + W) * C,
+                             ctypes.c_void_p(daw.data_ptr() + H * C * es), (H + W) * C, pack.N, H, W, C, 0, 1,
+                             stream())
+            dahs.append(dah)
+            daws.append(daw)
+        return (dx, None, *dahs, *daws)
+
+
+def gate_levels(x, ahs, aws, pack):
+    return LevelGateFn.apply(x, pack, *ahs, *aws)
+
+
+class ScaleLevelsFn(torch.autograd.Function):
+    """x * s_l on level l of a packed activation (AYHead's per-level Scale modules, head.py:1176), written into
+    `box` when given; the scalars' gradients are per-level dot sums (batched at the WGRAD flush)."""
+
+    @staticmethod
+    def forward(ctx, x, pack, box, *gs):
+        vx = _v(x)
+        Np, C, _, S = x.shape
+        es = x.element_size()
+        out, op, ocs = _out_view(box, Np, C, 1, S, x.dtype, x.device)
+        gf = [g.detach().float().contiguous() for g in gs]
+        for l, (H, W) in enumerate(pack.dims):
+            lib.adr_bcast_mul(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], fptr(gf[l]), 0, 0, None, 0,
+                              pack.at(op, ocs, es, l), ocs, pack.N, H * W, C, 0, stream())
+        ctx.save_for_backward(vx[0], *gf)
+        ctx.pack, ctx.params = pack, gs
+        return out if box is None else out[:, :]
+
+    @staticmethod
+    def backward(ctx, dy):
+        saved = ctx.saved_tensors
+        x, gf = saved[0], saved[1:]
+        pack = ctx.pack
+        vd = _v(dy)
+        C = x.shape[1]
+        es = x.element_size()
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = pack.empty(C, x.dtype, x.device)
+            for l, (H, W) in enumerate(pack.dims):
+                lib.adr_bcast_mul(dcode(x.dtype), pack.at(vd[1], vd[2], es, l), vd[2], fptr(gf[l]), 0, 0, None, 0,
+                                  pack.at(dx.data_ptr(), C, es, l), C, pack.N, H * W, C, 0, stream())
+        dgs = []
+        for l, p in enumerate(ctx.params):
+            if not ctx.needs_input_grad[3 + l]:
+                dgs.append(None)
+                continue
+            xl, dl = pack.view(x, l), pack.view(vd[0], l)
+            if _defer_dot(p, xl, dl):
+                out = torch.empty(1, dtype=torch.float32, device=x.device)
+                _dfr().add_dotsum(xl, dl, out)
+                dgs.append(sink(p, out.view(p.shape)))
+            else:
+                dgs.append(sink(p, _reduce_dot(xl, dl, True, True).view(p.shape)))
+        return (dx, None, None, *dgs)
+
+
+def scale_levels(x, gs, pack, out=None):
+    return ScaleLevelsFn.apply(x, pack, None if out is None else OutBox(out), *gs)

@@ -79,9 +79,18 @@ class Conv_GN(nn.Module):  # noqa: N801
         self.gn = nn.GroupNorm(16, c2)
         self.act_name = "silu" if act is True else ("none" if act is False else act)
 
-    def forward(self, x):
-        y, _ = K.conv2d(x, self.conv.weight, None, self.conv.stride[0], self.conv.padding[0])
-        return K.gn_act(y, self.gn, self.act_name)
+    def forward(self, x, pack=None):
+        """pack: x is a level-packed activation (AYHead1): GroupNorm per (level, image), k x k convs per level."""
+        if pack is None:
+            y, _ = K.conv2d(x, self.conv.weight, None, self.conv.stride[0], self.conv.padding[0])
+            return K.gn_act(y, self.gn, self.act_name)
+        if self.conv.stride[0] != 1 or self.conv.groups != 1:
+            raise NotImplementedError("packed Conv_GN: stride 1, dense")
+        if self.conv.kernel_size[0] == 1:
+            y, _ = K.conv2d(x, self.conv.weight, None, 1, 0)
+        else:
+            y = K.level_conv(x, self.conv.weight, None, self.conv.padding[0], pack)
+        return K.gn_act_packed(y, pack, [self.gn], self.act_name)
 
 
 class TaskDecomposition(nn.Module):
@@ -103,15 +112,17 @@ class TaskDecomposition(nn.Module):
         nn.init.zeros_(self.la_conv2.bias.data)
         nn.init.normal_(self.reduction_conv.conv.weight.data, mean=0, std=0.01)
 
-    def forward(self, feat, avg_feat=None):
+    def forward(self, feat, avg_feat=None, pack=None):
         if self.stacked_convs != 1:
             raise NotImplementedError("AYHead uses TaskDecomposition(stacked_convs=1)")
         if avg_feat is None:
-            avg_feat = K.gap(feat)
+            avg_feat = K.gap(feat) if pack is None else K.gap_packed(feat, pack)
         s = K.gate_mlp(avg_feat, self.la_conv1.weight, self.la_conv1.bias, self.la_conv2.weight, self.la_conv2.bias,
                        "relu", "sigmoid")  # (N, 1)
         y, _ = K.conv2d(feat, self.reduction_conv.conv.weight, None, 1, 0)
-        y = K.scale(y, s.view(-1), "n")
+        y = K.scale(y, s.view(-1), "n")  # packed: one gate per sub-image, each its image's value
+        if pack is not None:
+            return K.gn_act_packed(y, pack, [self.reduction_conv.gn], "silu")
         return K.gn_act(y, self.reduction_conv.gn, "silu")
 
 
@@ -127,14 +138,21 @@ class CoordAtt(nn.Module):
         self.conv_h = Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
         self.conv_w = Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
 
-    def forward(self, x):
-        x, xg = K.fanout(x)
-        y = K.axis_mean(x, "coord")  # (N, C, H+W, 1): [row means ; column means]
+    def _attn(self, y):
         y, _ = K.conv2d(y, self.conv1.weight, self.conv1.bias, 1, 0)
         y = K.bn_act(y, None, self.bn1, "hswish", self.training)
         a_h = K.conv_act(y, self.conv_h.weight, self.conv_h.bias, 1, 0, "sigmoid")
         a_w = K.conv_act(y, self.conv_w.weight, self.conv_w.bias, 1, 0, "sigmoid")
-        return K.gate(xg, a_h, a_w, "coord", x.shape)
+        return a_h, a_w
+
+    def forward(self, x, pack=None):
+        x, xg = K.fanout(x)
+        if pack is None:
+            a_h, a_w = self._attn(K.axis_mean(x, "coord"))  # (N, C, H+W, 1): [row means ; column means]
+            return K.gate(xg, a_h, a_w, "coord", x.shape)
+        # packed: pooled planes, attention and gate per level (BatchNorm statistics per level, as the reference)
+        ahw = [self._attn(y) for y in K.axis_mean_levels(x, pack)]
+        return K.gate_levels(xg, [a for a, _ in ahw], [b for _, b in ahw], pack)
 
 
 class CrossTaskInteraction(nn.Module):
@@ -184,8 +202,10 @@ class DyDCNv2(nn.Module):
         self.conv = _DCNWeight(in_channels, out_channels)
         self.norm = nn.GroupNorm(16, out_channels)
 
-    def forward(self, x, om):
+    def forward(self, x, om, pack=None):
         """`om`: the spatial_conv_offset output (offsets [0,18) and mask LOGITS [18,27); sigmoid fused)."""
+        if pack is not None:
+            return K.gn_act_packed(K.dcn_levels(x, om, self.conv.weight, pack), pack, [self.norm], "none")
         return K.gn_act(K.dcn(x, om, self.conv.weight), self.norm, "none")
 
 
@@ -209,10 +229,10 @@ class ResidualBlockGN(nn.Module):
         self.conv2 = Conv_GN(c2, c2, k, s, p=p, act=act)
         self.shortcut = nn.Identity() if c1 == c2 and s == 1 else Conv_GN(c1, c2, 1, s, act=False)
 
-    def forward(self, x):
+    def forward(self, x, pack=None):
         x, xs = K.fanout(x)
-        res = xs if isinstance(self.shortcut, nn.Identity) else self.shortcut(xs)
-        return K.add(self.conv2(self.conv1(x)), res)
+        res = xs if isinstance(self.shortcut, nn.Identity) else self.shortcut(xs, pack)
+        return K.add(self.conv2(self.conv1(x, pack), pack), res)
 
 
 class AYHead1(nn.Module):
@@ -276,10 +296,43 @@ class AYHead1(nn.Module):
         cls_out = self.cv3(K.mul_pixel(cls_e, cp), out=buf[:, 4 * self.reg_max:])
         return K.cat([reg_out, cls_out], out=buf)
 
+    def _packed(self, xs):
+        """All levels at once in the packed row space (kernels.LevelPack): the per-pixel ops are one launch for the
+        three levels, per-image statistics go through the segment kernels, 3x3 convs / DCN / CoordAtt's pooling run
+        per level on views. Same math as _level per level (per-level stems / Scale, shared everything else)."""
+        pack = K.LevelPack(xs[0].shape[0], [(x.shape[2], x.shape[3]) for x in xs])
+        dtype, dev = xs[0].dtype, xs[0].device
+        hid = self.stems[0].conv.out_channels
+        sb = pack.empty(hid, dtype, dev)  # the stems write their level views in place
+        ys = [K.conv2d(x, st.conv.weight, None, 1, 0, out=pack.view(sb, i))[0] for i, (x, st) in
+              enumerate(zip(xs, self.stems))]
+        ax = K.gn_act_packed(K.level_join(ys, pack, out=sb), pack, [st.gn for st in self.stems], "silu")
+        fv = list(K.fanout(self.share_conv[1](self.share_conv[0](ax, pack), pack), 5))
+        avg = K.gap_packed(fv[0], pack)
+        cls_f = self.cls_decomp(fv[1], avg, pack)
+        reg_f = self.reg_decomp(fv[2], avg, pack)
+        cls_f, reg_f = self.cross_task(cls_f, reg_f)
+        cls_e = self.rep_block_cls(cls_f, pack)
+        so = self.spatial_conv_offset
+        om = K.level_conv(fv[3], so.weight, so.bias, 1, pack, kpad=32)  # 27 channels padded to 32
+        r = self.coord_attention_reg(self.DyDCNV2(reg_f, om, pack), pack)
+        c0, c2 = self.cls_prob_conv[0], self.cls_prob_conv[2]
+        cp = K.conv_act(fv[4], c0.weight, c0.bias, 1, 0, "relu")
+        cp = K.act(K.level_conv(cp, c2.weight, c2.bias, 1, pack, kpad=8), "sigmoid")  # channel 0 valid
+        buf = pack.empty(4 * self.reg_max + self.nc, dtype, dev)
+        reg_out = K.scale_levels(self.cv2(r), [s.scale for s in self.scale], pack, out=buf[:, :4 * self.reg_max])
+        cls_out = self.cv3(K.mul_pixel(cls_e, cp), out=buf[:, 4 * self.reg_max:])
+        return list(K.level_split(K.cat([reg_out, cls_out], out=buf), pack))
+
+    # the packed head (one pass over all levels) is the default; False runs the reference's per-level loop
+    # (tests compare the two)
+    packed = True
+
     def forward(self, x):
-        # the reference loops the levels (head.py:1132); here each level runs on its own stream when enabled
-        # (kernels.run_levels: the P4 / P5 chains overlap P3's instead of leaving the chip idle)
-        outputs = K.run_levels(lambda i, xi: self._level(xi, i), list(x))
+        if self.packed and len(x) > 1:
+            outputs = self._packed(list(x))
+        else:  # the reference loops the levels (head.py:1132)
+            outputs = [self._level(xi, i) for i, xi in enumerate(x)]
         if self.training:
             return outputs
         y = K.detect_decode(outputs, [float(s) for s in self.stride], self.nc, self.reg_max)

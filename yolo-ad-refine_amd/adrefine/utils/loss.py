@@ -51,7 +51,16 @@ class DetLossFn(torch.autograd.Function):
         dev, dtype = f0.device, f0.dtype
         A = sum(f.shape[2] * f.shape[3] for f in feats)
         nmax = gt.shape[1]
-        grads = [K.empty_act(B, no, f.shape[2], f.shape[3], dtype, dev) for f in feats]
+        pk = getattr(f0, "_adr_pack", None)
+        if pk is not None and all(getattr(f, "_adr_pack", None) is pk for f in feats) and pk.N == B:
+            # the head's level-packed output: the gradients are the level views of one packed buffer, so the head's
+            # LevelSplitFn takes them back without a copy and the backward scales them in one launch
+            gbuf = pk.empty(no, dtype, dev)
+            grads = [pk.view(gbuf, l) for l in range(3)]
+            ctx.packed = (gbuf, pk)
+        else:
+            grads = [K.empty_act(B, no, f.shape[2], f.shape[3], dtype, dev) for f in feats]
+            ctx.packed = None
         wsb = lib.adr_det_loss_workspace(B, nmax, A)
         ws = torch.empty(wsb // 4 + 16, dtype=torch.float32, device=dev)
         out = torch.empty(5, dtype=torch.float32, device=dev)
@@ -70,6 +79,10 @@ class DetLossFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dloss, _dout):
         grads = ctx.grads
+        if ctx.packed is not None:
+            gbuf, pk = ctx.packed
+            sg = K.scale(gbuf, dloss.detach().float().reshape(()), "scalar")
+            return (None, None, None, None, *[pk.view(sg, l) for l in range(3)])
         scaled = [K.scale(g, dloss.detach().float().reshape(()), "scalar") for g in grads]
         return (None, None, None, None, *scaled)
 

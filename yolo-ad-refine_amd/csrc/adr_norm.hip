@@ -395,6 +395,129 @@ __global__ void __launch_bounds__(256) gn_param_batched_kernel(GnParamBatch b) {
                     (int)blockIdx.x - b.start[j]);
 }
 
+// ---- Level-packed GroupNorm (AYHead's three levels in one row space). The head stores a level's (image, H, W)
+//      rows back to back, P3 images first, then P4, then P5, and cuts that row space into "sub-images" of S rows,
+//      S = the smallest level's H*W: level l's image is k[l] = H_l*W_l / S consecutive sub-images. The per-pixel
+//      kernels (nc_reduce, affine_act, ...) then run once over all N' sub-images; only the per-image statistics
+//      need the level structure: a block per (level, image) segment sums its k[l]*chunks partial rows and writes
+//      the result replicated to each of its sub-images, so every later per-sub-image kernel (affine_act with
+//      per_sample coefficients, gn_bwd_param over N' sub-images) reads the statistics of the whole image.
+constexpr int LP_MAX = 4;
+struct LevelPackArgs {
+  int levels, N, chunks, C, G;
+  int k[LP_MAX];
+  int sub0[LP_MAX];  // first sub-image of level l
+  double count[LP_MAX];
+  float scale[LP_MAX];
+  const float* gamma[LP_MAX];
+  const float* beta[LP_MAX];
+};
+
+__device__ __forceinline__ void lp_segment(const LevelPackArgs& a, int& l, int& first, int& k) {
+  l = (int)blockIdx.x / a.N;
+  const int n = (int)blockIdx.x % a.N;
+  k = a.k[l];
+  first = a.sub0[l] + n * k;
+}
+
+__global__ void __launch_bounds__(256) gn_finalize_packed_kernel(const float* __restrict__ partial, LevelPackArgs a,
+                                                                 float eps, float* scale, float* shift,
+                                                                 float* mean_out, float* rstd_out) {
+  int l, first, k;
+  lp_segment(a, l, first, k);
+  const int C = a.C, G = a.G, cpg = C / G;
+  __shared__ double gm[64], gr[64];
+  __shared__ double sa[1024], sb[1024], xa[256], xb[256];
+  gn_chan_sums(partial + (long)first * a.chunks * 2 * C, 0, k * a.chunks, C, sa, sb, xa, xb);
+  for (int g = threadIdx.x; g < G; g += 256) {
+    double s = 0.0, q = 0.0;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      s += sa[c];
+      q += sb[c];
+    }
+    double mu = s / a.count[l], var = q / a.count[l] - mu * mu;
+    if (var < 0) var = 0;
+    gm[g] = mu;
+    gr[g] = 1.0 / sqrt(var + (double)eps);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < k * G; i += 256) {
+    const int j = first + i / G, g = i % G;
+    mean_out[(long)j * G + g] = (float)gm[g];
+    rstd_out[(long)j * G + g] = (float)gr[g];
+  }
+  const float* gamma = a.gamma[l];
+  const float* beta = a.beta[l];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int g = c / cpg;
+    const double gg = gamma ? gamma[c] : 1.0, bb = beta ? beta[c] : 0.0;
+    const float sc = (float)(gg * gr[g]), sf = (float)(bb - gm[g] * gg * gr[g]);
+    for (int j = first; j < first + k; ++j) {
+      scale[(long)j * C + c] = sc;
+      shift[(long)j * C + c] = sf;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) gn_bwd_coef_packed_kernel(const float* __restrict__ partial, LevelPackArgs a,
+                                                                 const float* __restrict__ mean,
+                                                                 const float* __restrict__ rstd, float* A, float* B,
+                                                                 float* Cc) {
+  int l, first, k;
+  lp_segment(a, l, first, k);
+  const int C = a.C, G = a.G, cpg = C / G;
+  __shared__ double sa[1024], sg[1024], xa[256], xb[256];
+  __shared__ double s1[64], s2[64];
+  gn_chan_sums(partial + (long)first * a.chunks * 2 * C, 0, k * a.chunks, C, sa, sg, xa, xb);
+  const float* gamma = a.gamma[l];
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int g = c / cpg;
+    const double mu = mean[(long)first * G + g], rs = rstd[(long)first * G + g];
+    const double s = sa[c], q = sg[c];
+    const double gmm = gamma ? gamma[c] : 1.0;
+    sa[c] = gmm * s;
+    sg[c] = gmm * (q - mu * s) * rs;
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g < G; g += 256) {
+    double S1 = 0.0, S2 = 0.0;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      S1 += sa[c];
+      S2 += sg[c];
+    }
+    s1[g] = S1;
+    s2[g] = S2;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int g = c / cpg;
+    const double mu = mean[(long)first * G + g], rs = rstd[(long)first * G + g];
+    const double gmm = gamma ? gamma[c] : 1.0;
+    const double Bk = -rs * rs * s2[g] / a.count[l];
+    const float av = (float)(rs * gmm), bv = (float)Bk, cv = (float)(-rs * s1[g] / a.count[l] - Bk * mu);
+    for (int j = first; j < first + k; ++j) {
+      A[(long)j * C + c] = av;
+      B[(long)j * C + c] = bv;
+      Cc[(long)j * C + c] = cv;
+    }
+  }
+}
+
+// out[j][c] = scale[l] * sum of in[j'][c] over the sub-images j' of j's (level, image) segment: the head's global
+// average pool from per-sub-image sums (forward), and its gradient's per-image sum (backward)
+__global__ void __launch_bounds__(256) seg_sum_packed_kernel(const float* __restrict__ in, LevelPackArgs a,
+                                                             float* out) {
+  int l, first, k;
+  lp_segment(a, l, first, k);
+  const int C = a.C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    double s = 0.0;
+    for (int j = first; j < first + k; ++j) s += in[(long)j * C + c];
+    const float v = (float)(s * (double)a.scale[l]);
+    for (int j = first; j < first + k; ++j) out[(long)j * C + c] = v;
+  }
+}
+
 // ---- GroupNorm + activation fused per image (Conv_GN / TaskDecomposition / DyDCNv2 / ELA gates: GN statistics
 //      are per image, so one 1024-thread workgroup owns an image and needs no cross-workgroup reduction). Forward:
 //      channel sums -> group mean / rstd -> per-channel scale/shift -> z = act(x*scale + shift), one launch
@@ -1028,6 +1151,61 @@ extern "C" int adr_gn_param_grad_batched(const adr_gnparam_entry* entries, int c
     b0 += j;
   }
   return check_launch("adr_gn_param_grad_batched");
+}
+
+// host side of the level-packed statistics: k[l] sub-images per image of level l, `sub_rows` rows per sub-image
+static int level_pack_args(LevelPackArgs& a, int levels, const int* k, int N, int chunks, int sub_rows, int C, int G,
+                           const void* const* gamma, const void* const* beta, const char* who) {
+  ADR_REQUIRE(levels >= 1 && levels <= LP_MAX && k && N > 0 && chunks > 0 && sub_rows > 0 && C > 0,
+              "%s: levels=%d N=%d chunks=%d sub_rows=%d", who, levels, N, chunks, sub_rows);
+  ADR_REQUIRE(G > 0 && G <= 64 && C <= 1024 && C % G == 0, "%s: G=%d C=%d", who, G, C);
+  a = LevelPackArgs{};
+  a.levels = levels;
+  a.N = N;
+  a.chunks = chunks;
+  a.C = C;
+  a.G = G;
+  int sub = 0;
+  for (int l = 0; l < levels; ++l) {
+    ADR_REQUIRE(k[l] > 0, "%s: k[%d]=%d", who, l, k[l]);
+    a.k[l] = k[l];
+    a.sub0[l] = sub;
+    sub += N * k[l];
+    a.count[l] = (double)k[l] * sub_rows * (C / G);
+    a.scale[l] = 1.0f / ((float)k[l] * sub_rows);
+    a.gamma[l] = gamma ? (const float*)gamma[l] : nullptr;
+    a.beta[l] = beta ? (const float*)beta[l] : nullptr;
+  }
+  return 0;
+}
+
+extern "C" int adr_gn_finalize_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows,
+                                      int C, int G, const void* const* gamma, const void* const* beta, float eps,
+                                      float* scale, float* shift, float* mean, float* rstd, void* stream) {
+  LevelPackArgs a;
+  if (int rc = level_pack_args(a, levels, k, N, chunks, sub_rows, C, G, gamma, beta, "gn_finalize_packed")) return rc;
+  hipLaunchKernelGGL(gn_finalize_packed_kernel, dim3(levels * N), dim3(256), 0, (hipStream_t)stream, partial, a, eps,
+                     scale, shift, mean, rstd);
+  return check_launch("adr_gn_finalize_packed");
+}
+
+extern "C" int adr_gn_bwd_coef_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows,
+                                      int C, int G, const void* const* gamma, const float* mean, const float* rstd,
+                                      float* A, float* B, float* Cc, void* stream) {
+  LevelPackArgs a;
+  if (int rc = level_pack_args(a, levels, k, N, chunks, sub_rows, C, G, gamma, nullptr, "gn_bwd_coef_packed")) return rc;
+  hipLaunchKernelGGL(gn_bwd_coef_packed_kernel, dim3(levels * N), dim3(256), 0, (hipStream_t)stream, partial, a, mean,
+                     rstd, A, B, Cc);
+  return check_launch("adr_gn_bwd_coef_packed");
+}
+
+extern "C" int adr_seg_mean_packed(const float* in, int levels, const int* k, int N, int sub_rows, int C, float* out,
+                                   void* stream) {
+  LevelPackArgs a;
+  if (int rc = level_pack_args(a, levels, k, N, 1, sub_rows, C, 1, nullptr, nullptr, "seg_mean_packed")) return rc;
+  ADR_REQUIRE(in != out, "seg_mean_packed: in place");
+  hipLaunchKernelGGL(seg_sum_packed_kernel, dim3(levels * N), dim3(256), 0, (hipStream_t)stream, in, a, out);
+  return check_launch("adr_seg_mean_packed");
 }
 
 extern "C" int adr_gn_param_grad(const float* partial, int N, int C, int G, const float* mean, const float* rstd,
