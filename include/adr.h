@@ -215,12 +215,27 @@ int adr_gn_finalize_packed(const float* partial, int levels, const int* k, int N
 int adr_gn_bwd_coef_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows, int C,
                            int G, const void* const* gamma, const float* mean, const float* rstd, float* A, float* B,
                            float* Cc, void* stream);
-/* Per (level, image) segment of the packed row space: out[j][c] = sum of in[j'][c] over the segment's sub-images
- * / (k[l] * sub_rows), replicated to each sub-image j of the segment (in, out: [N'][C] fp32). With `in` the
- * per-sub-image pixel sums this is the head's global average pool (head.py:1142); applied to the pool's output
- * gradient it is the backward's per-image sum. */
-int adr_seg_mean_packed(const float* in, int levels, const int* k, int N, int sub_rows, int C, float* out,
-                        void* stream);
+/* Per (level, image) segment of the packed row space (segments level-major: s = l * N + n), rows of C fp32:
+ * v = in[s] (in_per_seg) or the sum of in[j] over the segment's sub-images j (in: [N'][C]), times
+ * 1 / (k[l] * sub_rows) when `mean`; written to out[s] (out_per_seg, out: [levels * N][C]) or to every sub-image
+ * row of the segment. With `in` the per-sub-image pixel sums and (0, 1, 1) this is the head's global average pool
+ * (head.py:1142) for every level at once; (1, 0, 0) expands a per-image gate (TaskDecomposition's layer attention,
+ * head.py:655-662) to the sub-images; (0, 1, 0) is that expansion's backward, (1, 0, 1) the pool's. */
+int adr_seg_reduce_packed(const float* in, int in_per_seg, int out_per_seg, int mean, int levels, const int* k, int N,
+                          int sub_rows, int C, float* out, void* stream);
+/* Level-packed training BatchNorm (CoordAtt's bn1 on the pooled planes of the three head levels,
+ * nn/modules/head.py:684-700, one call instead of one per level): rows of level l are the N * k[l] sub-images
+ * starting at sub-image N * (k[0] + ... + k[l-1]); partial from adr_nc_reduce over the sub-images. Statistics per
+ * level, running statistics updated level by level in order (the reference's per-level calls); scale / shift
+ * [N'][C] per sub-image, mean / rstd [levels][C]. The backward writes A / B / C per sub-image and dgamma / dbeta
+ * summed over the levels (+= with accumulate). */
+int adr_bn_finalize_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows, int C,
+                           const float* gamma, const float* beta, float* running_mean, float* running_var,
+                           float momentum, float eps, float* scale, float* shift, float* mean, float* rstd,
+                           void* stream);
+int adr_bn_bwd_finalize_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows, int C,
+                               const float* mean, const float* rstd, const float* gamma, float* dgamma, float* dbeta,
+                               float* A, float* B, float* Cc, int accumulate, void* stream);
 /* dgamma / dbeta (+)= column sums over images of the adr_gn_act_bwd_fused rows. */
 int adr_gn_param_grad(const float* partial, int N, int C, int G, const float* mean, const float* rstd,
                       float* dgamma, float* dbeta, int accumulate, void* stream);
@@ -343,8 +358,6 @@ typedef struct {
   long n;
 } adr_axpy_entry;
 int adr_axpy_batched(const adr_axpy_entry* entries, int count, void* stream);
-/* Same, and x_i = 0 afterwards (the per-level gradient slabs of AYHead's concurrent levels folded into the arena). */
-int adr_axpy_zero_batched(const adr_axpy_entry* entries, int count, void* stream);
 /* BiFPN weights w = relu(fw)/(sum relu(fw)+eps) and backward (block.py:1532-1535). */
 int adr_fusion_weights(const float* fw, int n, float eps, float* w, void* stream);
 int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream);

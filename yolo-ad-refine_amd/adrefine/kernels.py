@@ -3491,28 +3491,31 @@ def gn_act_packed(y, pack, gns, act):
                           *[g.bias for g in gns])
 
 
+def _seg(inp, in_seg, out_seg, mean, pack, C):
+    """adr_seg_reduce_packed over fp32 rows of C: per (level, image) segment <-> per sub-image."""
+    rows = pack.L * pack.N if out_seg else pack.Np
+    out = torch.empty(rows, C, dtype=torch.float32, device=inp.device)
+    lib.adr_seg_reduce_packed(fptr(inp), int(in_seg), int(out_seg), int(mean), pack.L,
+                              ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, pack.S, C, fptr(out), stream())
+    return out
+
+
 class GapPackFn(torch.autograd.Function):
-    """Global average pool per (level, image) of a packed activation, replicated to each sub-image: (N', C) fp32
+    """Global average pool per (level, image) of a packed activation: (L * N, C) fp32, level-major
     (F.adaptive_avg_pool2d(x, 1), head.py:1142, for every level at once)."""
 
     @staticmethod
     def forward(ctx, x, pack):
         Np, C, _, S = x.shape
         s = _reduce_dot(None, x, False, False, which=1)  # per-sub-image sums
-        out = torch.empty(Np, C, dtype=torch.float32, device=x.device)
-        lib.adr_seg_mean_packed(fptr(s), pack.L, ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, S, C, fptr(out),
-                                stream())
         ctx.pack, ctx.meta = pack, (tuple(x.shape), x.dtype)
-        return out
+        return _seg(s, False, True, True, pack, C)
 
     @staticmethod
     def backward(ctx, dg):
         pack = ctx.pack
         (Np, C, _, S), dtype = ctx.meta
-        dgc = dg.float().contiguous()
-        t = torch.empty_like(dgc)
-        lib.adr_seg_mean_packed(fptr(dgc), pack.L, ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, S, C, fptr(t),
-                                stream())
+        t = _seg(dg.float().contiguous(), True, False, True, pack, C)
         dx = pack.empty(C, dtype, dg.device)
         lib.adr_bcast_fill(dcode(dtype), fptr(t), C, 1, 1.0, ctypes.c_void_p(dx.data_ptr()), C, Np, S, C, 0, stream())
         return dx, None
@@ -3520,6 +3523,27 @@ class GapPackFn(torch.autograd.Function):
 
 def gap_packed(x, pack):
     return GapPackFn.apply(x, pack)
+
+
+class SegExpandFn(torch.autograd.Function):
+    """A per-(level, image) vector (L * N,) or rows (L * N, C) -> one copy per sub-image (N', ...): the packed head's
+    per-image gates for scale(..., "n"); backward sums the sub-images' gradients."""
+
+    @staticmethod
+    def forward(ctx, v, pack):
+        C = v.numel() // (pack.L * pack.N)
+        ctx.pack, ctx.meta = pack, (tuple(v.shape), C)
+        out = _seg(v.detach().float().contiguous(), True, False, False, pack, C)
+        return out.view(pack.Np) if v.dim() == 1 else out
+
+    @staticmethod
+    def backward(ctx, g):
+        shape, C = ctx.meta
+        return _seg(g.float().contiguous(), False, True, False, ctx.pack, C).view(shape), None
+
+
+def seg_expand(v, pack):
+    return SegExpandFn.apply(v, pack)
 
 
 def wgrad_param_multi(param, pieces, K, C, RS, wshape, cpad, device):
@@ -3755,96 +3779,152 @@ def dcn_levels(x, om, w, pack):
 
 
 class LevelAxisMeanFn(torch.autograd.Function):
-    """CoordAtt's row / column means (AxisMeanFn 'coord', head.py:684-690) of each level of a packed activation:
-    one (N, C, H_l + W_l, 1) tensor per level."""
+    """CoordAtt's row / column means (AxisMeanFn 'coord', head.py:684-690) of every level of a packed activation, as
+    ONE packed tensor of the pooled planes: `pp` = LevelPack(N, [(1, H_l + W_l)]), so an image's plane is its
+    [H_l row means ; W_l column means] rows, and the 1x1 convs / BatchNorm after it run once for all levels."""
 
     @staticmethod
-    def forward(ctx, x, pack):
-        ctx.set_materialize_grads(False)
+    def forward(ctx, x, pack, pp):
         vx = _v(x)
         C = x.shape[1]
         es = x.element_size()
-        outs = []
+        out = pp.empty(C, x.dtype, x.device)
         for l, (H, W) in enumerate(pack.dims):
-            out = empty_act(pack.N, C, H + W, 1, x.dtype, x.device)
+            o = pp.at(out.data_ptr(), C, es, l).value
             lib.adr_axis_mean(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], pack.N, H, W, C,
-                              ctypes.c_void_p(out.data_ptr()), (H + W) * C,
-                              ctypes.c_void_p(out.data_ptr() + H * C * es), (H + W) * C, stream())
-            outs.append(out)
-        ctx.pack, ctx.meta = pack, (C, x.dtype)
-        return tuple(outs)
+                              ctypes.c_void_p(o), (H + W) * C, ctypes.c_void_p(o + H * C * es), (H + W) * C, stream())
+        ctx.pack, ctx.pp, ctx.meta = pack, pp, (C, x.dtype)
+        return out
 
     @staticmethod
-    def backward(ctx, *dys):
-        pack = ctx.pack
+    def backward(ctx, dy):
+        pack, pp = ctx.pack, ctx.pp
         C, dtype = ctx.meta
-        dev = next(g for g in dys if g is not None).device
-        dx = pack.empty(C, dtype, dev)
+        _, dp, dcs = nhwc(dy)
+        dx = pack.empty(C, dtype, dy.device)
         es = dx.element_size()
         for l, (H, W) in enumerate(pack.dims):
-            dy = dys[l]
-            if dy is None:
-                lib.adr_memset_zero(pack.at(dx.data_ptr(), C, es, l), pack.N * H * W * C * es, stream())
-                continue
-            dy = dy.contiguous(memory_format=torch.channels_last) if not _is_dense_nhwc(dy) else dy
-            lib.adr_axis_mean_bwd(dcode(dtype), ctypes.c_void_p(dy.data_ptr()), (H + W) * C,
-                                  ctypes.c_void_p(dy.data_ptr() + H * C * es), (H + W) * C,
-                                  pack.at(dx.data_ptr(), C, es, l), C, pack.N, H, W, C, 0, stream())
-        return dx, None
+            o = pp.at(dp, dcs, es, l).value
+            lib.adr_axis_mean_bwd(dcode(dtype), ctypes.c_void_p(o), (H + W) * dcs, ctypes.c_void_p(o + H * dcs * es),
+                                  (H + W) * dcs, pack.at(dx.data_ptr(), C, es, l), C, pack.N, H, W, C, 0, stream())
+        return dx, None, None
 
 
-def axis_mean_levels(x, pack):
-    return LevelAxisMeanFn.apply(x, pack)
+def axis_mean_levels(x, pack, pp):
+    return LevelAxisMeanFn.apply(x, pack, pp)
 
 
 class LevelGateFn(torch.autograd.Function):
     """CoordAtt's output x * a_h * a_w (GateFn 'coord', head.py:704-706) per level of a packed activation; a_h / a_w
-    are the levels' (N, C, H_l + W_l, 1) tensors."""
+    are packed pooled planes (LevelAxisMeanFn's layout: the gate reads a_h's row-mean rows and a_w's column-mean
+    rows of each image)."""
 
     @staticmethod
-    def forward(ctx, x, pack, *a):
-        L = pack.L
-        ahs = [t if _is_dense_nhwc(t) else t.contiguous(memory_format=torch.channels_last) for t in a[:L]]
-        aws = [t if _is_dense_nhwc(t) else t.contiguous(memory_format=torch.channels_last) for t in a[L:]]
+    def forward(ctx, x, ah, aw, pack, pp):
+        ah, ahp, ahcs = nhwc(ah)
+        aw, awp, awcs = nhwc(aw)
         vx = _v(x)
         C = x.shape[1]
+        if ahcs != C or awcs != C:
+            raise RuntimeError("gate_levels: a_h / a_w must be dense planes")
         es = x.element_size()
         out = pack.empty(C, x.dtype, x.device)
         for l, (H, W) in enumerate(pack.dims):
-            lib.adr_gate(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], ctypes.c_void_p(ahs[l].data_ptr()),
-                         (H + W) * C, ctypes.c_void_p(aws[l].data_ptr() + H * C * es), (H + W) * C,
+            lib.adr_gate(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], pp.at(ahp, C, es, l), (H + W) * C,
+                         ctypes.c_void_p(pp.at(awp, C, es, l).value + H * C * es), (H + W) * C,
                          pack.at(out.data_ptr(), C, es, l), C, pack.N, H, W, C, stream())
-        ctx.save_for_backward(vx[0], *ahs, *aws)
-        ctx.pack = pack
+        ctx.save_for_backward(vx[0], ah, aw)
+        ctx.pack, ctx.pp = pack, pp
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        pack = ctx.pack
-        L = pack.L
-        saved = ctx.saved_tensors
-        x, ahs, aws = saved[0], saved[1:1 + L], saved[1 + L:]
+        pack, pp = ctx.pack, ctx.pp
+        x, ah, aw = ctx.saved_tensors
         vx, vd = _v(x), _v(dout)
         C = x.shape[1]
         es = x.element_size()
         dx = pack.empty(C, x.dtype, x.device)
-        dahs, daws = [], []
+        dah = pp.empty(C, x.dtype, x.device)
+        daw = pp.empty(C, x.dtype, x.device)
         for l, (H, W) in enumerate(pack.dims):
-            dah = torch.empty_like(ahs[l], memory_format=torch.channels_last)
-            daw = torch.empty_like(aws[l], memory_format=torch.channels_last)
-            lib.adr_gate_bwd(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], ctypes.c_void_p(ahs[l].data_ptr()),
-                             (H + W) * C, ctypes.c_void_p(aws[l].data_ptr() + H * C * es), (H + W) * C,
-                             pack.at(vd[1], vd[2], es, l), vd[2], pack.at(dx.data_ptr(), C, es, l), C,
-                             ctypes.c_void_p(dah.data_ptr()), (H + W) * C,
-                             ctypes.c_void_p(daw.data_ptr() + H * C * es), (H + W) * C, pack.N, H, W, C, 0, 1,
-                             stream())
-            dahs.append(dah)
-            daws.append(daw)
-        return (dx, None, *dahs, *daws)
+            # zero_other: each gradient plane's unused rows (dah's column rows, daw's row rows) are written as 0
+            lib.adr_gate_bwd(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], pp.at(ah.data_ptr(), C, es, l),
+                             (H + W) * C, ctypes.c_void_p(pp.at(aw.data_ptr(), C, es, l).value + H * C * es),
+                             (H + W) * C, pack.at(vd[1], vd[2], es, l), vd[2], pack.at(dx.data_ptr(), C, es, l), C,
+                             pp.at(dah.data_ptr(), C, es, l), (H + W) * C,
+                             ctypes.c_void_p(pp.at(daw.data_ptr(), C, es, l).value + H * C * es), (H + W) * C,
+                             pack.N, H, W, C, 0, 1, stream())
+        return dx, dah, daw, None, None
 
 
-def gate_levels(x, ahs, aws, pack):
-    return LevelGateFn.apply(x, pack, *ahs, *aws)
+def gate_levels(x, ah, aw, pack, pp):
+    return LevelGateFn.apply(x, ah, aw, pack, pp)
+
+
+class BNPackFn(torch.autograd.Function):
+    """act(BatchNorm2d(y)) in training mode with per-LEVEL batch statistics over a packed activation (CoordAtt's bn1
+    on the three levels' pooled planes, head.py:694-700): the reference calls the shared module once per level, so
+    each level normalises with its own statistics and the running statistics are updated level by level."""
+
+    @staticmethod
+    def forward(ctx, y, pack, gamma, beta, rm, rv, act, momentum, eps):
+        dtype = y.dtype
+        y, yp, ycs = nhwc(y)
+        Np, C, _, S = y.shape
+        dev = y.device
+        rows = _stats_rows(Np, S)
+        chunks = lib.adr_nc_reduce_chunks(S, rows)
+        part = torch.empty(Np * chunks * 2 * C, dtype=torch.float32, device=dev)
+        scale = torch.empty(Np * C, dtype=torch.float32, device=dev)
+        shift = torch.empty(Np * C, dtype=torch.float32, device=dev)
+        mean = torch.empty(pack.L * C, dtype=torch.float32, device=dev)
+        rstd = torch.empty(pack.L * C, dtype=torch.float32, device=dev)
+        lib.adr_nc_reduce(dcode(dtype), 0, ctypes.c_void_p(yp), ycs, 0, None, 0, 0, None, None, 0, 0, Np, S, C, rows,
+                          fptr(part), stream())
+        lib.adr_bn_finalize_packed(fptr(part), pack.L, ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, chunks, S, C,
+                                   fptr(gamma.detach()), fptr(beta.detach()), fptr(rm), fptr(rv), float(momentum),
+                                   float(eps), fptr(scale), fptr(shift), fptr(mean), fptr(rstd), stream())
+        z = pack.empty(C, dtype, dev)
+        lib.adr_affine_act(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(z.data_ptr()), C, 0,
+                           fptr(scale), fptr(shift), 1, ACT[act], Np, S, C, stream())
+        ctx.save_for_backward(y, scale, shift, mean, rstd, gamma)
+        ctx.meta = (act, chunks, rows)
+        ctx.pack, ctx.pbeta = pack, beta
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        y, scale, shift, mean, rstd, gamma = ctx.saved_tensors
+        act, chunks, rows = ctx.meta
+        pack = ctx.pack
+        dz, dzp, dzcs = nhwc(dz.to(y.dtype) if dz.dtype != y.dtype else dz)
+        _, yp, ycs = nhwc(y)
+        Np, C, _, S = y.shape
+        dev = y.device
+        dt = dcode(y.dtype)
+        part = torch.empty(Np * chunks * 2 * C, dtype=torch.float32, device=dev)
+        lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
+                          fptr(shift), 1, ACT[act], Np, S, C, rows, fptr(part), stream())
+        f = lambda: torch.empty(Np * C, dtype=torch.float32, device=dev)  # noqa: E731
+        A, B, Cc = f(), f(), f()
+        dgamma, pg, acc_g = grad_dst(gamma, C, dev)
+        dbeta, pb, acc_b = grad_dst(ctx.pbeta, C, dev)
+        if acc_g != acc_b:
+            raise RuntimeError("BN gamma/beta gradients must share one destination kind")
+        lib.adr_bn_bwd_finalize_packed(fptr(part), pack.L, ctypes.cast(pack.k_c, ctypes.c_void_p), pack.N, chunks, S,
+                                       C, fptr(mean), fptr(rstd), fptr(gamma.detach()), pg, pb, fptr(A), fptr(B),
+                                       fptr(Cc), acc_g, stream())
+        dy = pack.empty(C, y.dtype, dev)
+        lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
+                               ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
+                               fptr(Cc), 1, 1, ACT[act], Np, S, C, 0, stream())
+        return dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None
+
+
+def bn_act_packed(y, pack, bn, act):
+    """Training BatchNorm + activation with per-level statistics over a packed activation (BNPackFn)."""
+    return BNPackFn.apply(y, pack, bn.weight, bn.bias, bn.running_mean, bn.running_var, act, bn.momentum, bn.eps)
 
 
 class ScaleLevelsFn(torch.autograd.Function):

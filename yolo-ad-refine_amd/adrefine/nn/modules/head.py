@@ -120,7 +120,8 @@ class TaskDecomposition(nn.Module):
         s = K.gate_mlp(avg_feat, self.la_conv1.weight, self.la_conv1.bias, self.la_conv2.weight, self.la_conv2.bias,
                        "relu", "sigmoid")  # (N, 1)
         y, _ = K.conv2d(feat, self.reduction_conv.conv.weight, None, 1, 0)
-        y = K.scale(y, s.view(-1), "n")  # packed: one gate per sub-image, each its image's value
+        s = s.view(-1) if pack is None else K.seg_expand(s.view(-1), pack)  # packed: the image's gate per sub-image
+        y = K.scale(y, s, "n")
         if pack is not None:
             return K.gn_act_packed(y, pack, [self.reduction_conv.gn], "silu")
         return K.gn_act(y, self.reduction_conv.gn, "silu")
@@ -138,9 +139,12 @@ class CoordAtt(nn.Module):
         self.conv_h = Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
         self.conv_w = Conv2d(mip, oup, kernel_size=1, stride=1, padding=0)
 
-    def _attn(self, y):
+    def _attn(self, y, pp=None):
         y, _ = K.conv2d(y, self.conv1.weight, self.conv1.bias, 1, 0)
-        y = K.bn_act(y, None, self.bn1, "hswish", self.training)
+        if pp is not None and self.training:  # the levels' planes in one tensor: BatchNorm statistics per level
+            y = K.bn_act_packed(y, pp, self.bn1, "hswish")
+        else:
+            y = K.bn_act(y, None, self.bn1, "hswish", self.training)
         a_h = K.conv_act(y, self.conv_h.weight, self.conv_h.bias, 1, 0, "sigmoid")
         a_w = K.conv_act(y, self.conv_w.weight, self.conv_w.bias, 1, 0, "sigmoid")
         return a_h, a_w
@@ -150,9 +154,10 @@ class CoordAtt(nn.Module):
         if pack is None:
             a_h, a_w = self._attn(K.axis_mean(x, "coord"))  # (N, C, H+W, 1): [row means ; column means]
             return K.gate(xg, a_h, a_w, "coord", x.shape)
-        # packed: pooled planes, attention and gate per level (BatchNorm statistics per level, as the reference)
-        ahw = [self._attn(y) for y in K.axis_mean_levels(x, pack)]
-        return K.gate_levels(xg, [a for a, _ in ahw], [b for _, b in ahw], pack)
+        # packed: every level's pooled plane in one tensor (conv1 / BN / conv_h / conv_w once), gates per level
+        pp = K.LevelPack(pack.N, [(1, h + w) for h, w in pack.dims])
+        a_h, a_w = self._attn(K.axis_mean_levels(x, pack, pp), pp)
+        return K.gate_levels(xg, a_h, a_w, pack, pp)
 
 
 class CrossTaskInteraction(nn.Module):

@@ -271,9 +271,6 @@ struct AxpyBatch {
   int start[AXB_MAX + 1];
   int count;
 };
-// ZERO: the source is cleared after it is added (the per-level gradient slabs of the concurrent head levels are
-// folded into the arena and left zero for the next backward)
-template <bool ZERO>
 __global__ void __launch_bounds__(256) axpy_batched_kernel(AxpyBatch b) {
   int j = 0;
   while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
@@ -282,10 +279,7 @@ __global__ void __launch_bounds__(256) axpy_batched_kernel(AxpyBatch b) {
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const long i = base + u * 256;
-    if (i < en.n) {
-      en.y[i] += en.x[i];
-      if constexpr (ZERO) const_cast<float*>(en.x)[i] = 0.f;
-    }
+    if (i < en.n) en.y[i] += en.x[i];
   }
 }
 
@@ -401,8 +395,7 @@ extern "C" int adr_fusion_weights_bwd(const float* fw, int n, float eps, const f
   return check_launch("adr_fusion_weights_bwd");
 }
 
-template <bool ZERO>
-static int axpy_batched(const adr_axpy_entry* entries, int count, void* stream) {
+extern "C" int adr_axpy_batched(const adr_axpy_entry* entries, int count, void* stream) {
   ADR_REQUIRE(count >= 0 && (count == 0 || entries), "axpy_batched: count=%d", count);
   for (int b0 = 0; b0 < count; b0 += AXB_MAX) {
     AxpyBatch ab{};
@@ -419,18 +412,11 @@ static int axpy_batched(const adr_axpy_entry* entries, int count, void* stream) 
     }
     ADR_REQUIRE(blocks < (1l << 31), "axpy_batched: too many elements");
     ab.start[ab.count] = (int)blocks;
-    hipLaunchKernelGGL(axpy_batched_kernel<ZERO>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ab);
+    hipLaunchKernelGGL(axpy_batched_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, ab);
   }
   return check_launch("adr_axpy_batched");
 }
 
-extern "C" int adr_axpy_batched(const adr_axpy_entry* entries, int count, void* stream) {
-  return axpy_batched<false>(entries, count, stream);
-}
-
-extern "C" int adr_axpy_zero_batched(const adr_axpy_entry* entries, int count, void* stream) {
-  return axpy_batched<true>(entries, count, stream);
-}
 
 extern "C" int adr_axpy(long n, float a, const float* x, float* y, void* stream) {
   if (n <= 0) return ADR_OK;

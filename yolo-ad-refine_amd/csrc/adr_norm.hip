@@ -503,18 +503,98 @@ __global__ void __launch_bounds__(256) gn_bwd_coef_packed_kernel(const float* __
   }
 }
 
-// out[j][c] = scale[l] * sum of in[j'][c] over the sub-images j' of j's (level, image) segment: the head's global
-// average pool from per-sub-image sums (forward), and its gradient's per-image sum (backward)
-__global__ void __launch_bounds__(256) seg_sum_packed_kernel(const float* __restrict__ in, LevelPackArgs a,
-                                                             float* out) {
+// Per (level, image) segment, rows of C floats: v = (in_seg ? in[segment] : sum of in[j] over the segment's
+// sub-images j) * (mean ? 1 / pixels of the image : 1), written to out[segment] (out_seg) or to every sub-image's
+// row. The head's global average pool (per-sub-image sums -> per-image means), the expansion of a per-image gate
+// to its sub-images, and both backwards.
+__global__ void __launch_bounds__(256) seg_reduce_packed_kernel(const float* __restrict__ in, int in_seg, int out_seg,
+                                                                int mean, LevelPackArgs a, float* out) {
   int l, first, k;
   lp_segment(a, l, first, k);
-  const int C = a.C;
+  const int C = a.C, seg = blockIdx.x;
   for (int c = threadIdx.x; c < C; c += 256) {
     double s = 0.0;
-    for (int j = first; j < first + k; ++j) s += in[(long)j * C + c];
-    const float v = (float)(s * (double)a.scale[l]);
-    for (int j = first; j < first + k; ++j) out[(long)j * C + c] = v;
+    if (in_seg)
+      s = in[(long)seg * C + c];
+    else
+      for (int j = first; j < first + k; ++j) s += in[(long)j * C + c];
+    const float v = (float)(mean ? s * (double)a.scale[l] : s);
+    if (out_seg)
+      out[(long)seg * C + c] = v;
+    else
+      for (int j = first; j < first + k; ++j) out[(long)j * C + c] = v;
+  }
+}
+
+// Level-packed BatchNorm (CoordAtt's pooled planes of the three head levels in one row space, each level's rows a
+// segment of N * k[l] sub-images): training statistics per level, block per channel looping the levels in order,
+// so the shared module's running statistics are updated level by level as the reference's per-level calls do.
+// scale / shift are written per sub-image (affine_act per_sample), mean / rstd per (level, channel).
+__global__ void __launch_bounds__(256) bn_finalize_packed_kernel(const float* __restrict__ partial, LevelPackArgs a,
+                                                                 const float* __restrict__ gamma,
+                                                                 const float* __restrict__ beta, float* running_mean,
+                                                                 float* running_var, float momentum, float eps,
+                                                                 float* scale, float* shift, float* mean_out,
+                                                                 float* rstd_out) {
+  const int c = blockIdx.x, C = a.C;
+  const double g = gamma ? gamma[c] : 1.0, bb = beta ? beta[c] : 0.0;
+  for (int l = 0; l < a.levels; ++l) {
+    const int subs = a.N * a.k[l];
+    double s = 0.0, q = 0.0;
+    col_sums2(partial + (long)a.sub0[l] * a.chunks * 2 * C, subs * a.chunks, C, c, s, q);
+    block_sum2(s, q);
+    const double cnt = a.count[l];
+    const double mean = s / cnt;
+    double var = q / cnt - mean * mean;
+    if (var < 0) var = 0;
+    const double rstd = 1.0 / sqrt(var + (double)eps);
+    const float sc = (float)(g * rstd), sf = (float)(bb - mean * g * rstd);
+    for (int j = a.sub0[l] + threadIdx.x; j < a.sub0[l] + subs; j += 256) {
+      scale[(long)j * C + c] = sc;
+      shift[(long)j * C + c] = sf;
+    }
+    if (threadIdx.x == 0) {
+      mean_out[l * C + c] = (float)mean;
+      rstd_out[l * C + c] = (float)rstd;
+      if (running_mean) {
+        const double unb = cnt > 1 ? var * cnt / (cnt - 1) : var;
+        running_mean[c] = (float)((1.0 - momentum) * running_mean[c] + momentum * mean);
+        running_var[c] = (float)((1.0 - momentum) * running_var[c] + momentum * unb);
+      }
+    }
+  }
+}
+
+// its backward: per level (sum g, sum g*x) -> dx coefficients A, B, C per sub-image; dgamma / dbeta summed over the
+// levels in order
+__global__ void __launch_bounds__(256) bn_bwd_finalize_packed_kernel(const float* __restrict__ partial,
+                                                                     LevelPackArgs a, const float* __restrict__ mean,
+                                                                     const float* __restrict__ rstd,
+                                                                     const float* __restrict__ gamma, float* dgamma,
+                                                                     float* dbeta, float* A, float* B, float* Cc,
+                                                                     int accumulate) {
+  const int c = blockIdx.x, C = a.C;
+  const double g = gamma ? gamma[c] : 1.0;
+  double dg = 0.0, db = 0.0;
+  for (int l = 0; l < a.levels; ++l) {
+    const int subs = a.N * a.k[l];
+    double s = 0.0, q = 0.0;
+    col_sums2(partial + (long)a.sub0[l] * a.chunks * 2 * C, subs * a.chunks, C, c, s, q);
+    block_sum2(s, q);
+    const double cnt = a.count[l], mu = mean[l * C + c], rs = rstd[l * C + c];
+    const double sgx = (q - mu * s) * rs;
+    dg += sgx;
+    db += s;
+    const double Ak = g * rs, Bk = -Ak * rs * sgx / cnt, Ck = -Ak * s / cnt - Bk * mu;
+    for (int j = a.sub0[l] + threadIdx.x; j < a.sub0[l] + subs; j += 256) {
+      A[(long)j * C + c] = (float)Ak;
+      B[(long)j * C + c] = (float)Bk;
+      Cc[(long)j * C + c] = (float)Ck;
+    }
+  }
+  if (threadIdx.x == 0) {
+    if (dgamma) dgamma[c] = accumulate ? dgamma[c] + (float)dg : (float)dg;
+    if (dbeta) dbeta[c] = accumulate ? dbeta[c] + (float)db : (float)db;
   }
 }
 
@@ -1199,13 +1279,43 @@ extern "C" int adr_gn_bwd_coef_packed(const float* partial, int levels, const in
   return check_launch("adr_gn_bwd_coef_packed");
 }
 
-extern "C" int adr_seg_mean_packed(const float* in, int levels, const int* k, int N, int sub_rows, int C, float* out,
-                                   void* stream) {
+static int bn_pack_args(LevelPackArgs& a, int levels, const int* k, int N, int chunks, int sub_rows, int C,
+                        const char* who) {
+  if (int rc = level_pack_args(a, levels, k, N, chunks, sub_rows, C, 1, nullptr, nullptr, who)) return rc;
+  for (int l = 0; l < levels; ++l) a.count[l] = (double)N * k[l] * sub_rows;  // a level's rows over all images
+  return 0;
+}
+
+extern "C" int adr_bn_finalize_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows,
+                                      int C, const float* gamma, const float* beta, float* running_mean,
+                                      float* running_var, float momentum, float eps, float* scale, float* shift,
+                                      float* mean, float* rstd, void* stream) {
   LevelPackArgs a;
-  if (int rc = level_pack_args(a, levels, k, N, 1, sub_rows, C, 1, nullptr, nullptr, "seg_mean_packed")) return rc;
-  ADR_REQUIRE(in != out, "seg_mean_packed: in place");
-  hipLaunchKernelGGL(seg_sum_packed_kernel, dim3(levels * N), dim3(256), 0, (hipStream_t)stream, in, a, out);
-  return check_launch("adr_seg_mean_packed");
+  if (int rc = bn_pack_args(a, levels, k, N, chunks, sub_rows, C, "bn_finalize_packed")) return rc;
+  hipLaunchKernelGGL(bn_finalize_packed_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, a, gamma, beta,
+                     running_mean, running_var, momentum, eps, scale, shift, mean, rstd);
+  return check_launch("adr_bn_finalize_packed");
+}
+
+extern "C" int adr_bn_bwd_finalize_packed(const float* partial, int levels, const int* k, int N, int chunks,
+                                          int sub_rows, int C, const float* mean, const float* rstd,
+                                          const float* gamma, float* dgamma, float* dbeta, float* A, float* B,
+                                          float* Cc, int accumulate, void* stream) {
+  LevelPackArgs a;
+  if (int rc = bn_pack_args(a, levels, k, N, chunks, sub_rows, C, "bn_bwd_finalize_packed")) return rc;
+  hipLaunchKernelGGL(bn_bwd_finalize_packed_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, a, mean, rstd,
+                     gamma, dgamma, dbeta, A, B, Cc, accumulate);
+  return check_launch("adr_bn_bwd_finalize_packed");
+}
+
+extern "C" int adr_seg_reduce_packed(const float* in, int in_per_seg, int out_per_seg, int mean, int levels,
+                                     const int* k, int N, int sub_rows, int C, float* out, void* stream) {
+  LevelPackArgs a;
+  if (int rc = level_pack_args(a, levels, k, N, 1, sub_rows, C, 1, nullptr, nullptr, "seg_reduce_packed")) return rc;
+  ADR_REQUIRE(in && out && in != out, "seg_reduce_packed: in place / null");
+  hipLaunchKernelGGL(seg_reduce_packed_kernel, dim3(levels * N), dim3(256), 0, (hipStream_t)stream, in, in_per_seg,
+                     out_per_seg, mean, a, out);
+  return check_launch("adr_seg_reduce_packed");
 }
 
 extern "C" int adr_gn_param_grad(const float* partial, int N, int C, int G, const float* mean, const float* rstd,
