@@ -1777,6 +1777,21 @@ class GradSink:
         return self.buf, 1, add
 
 
+def _sink_of(x):
+    """The fan-out gradient sink of x when a consumer's backward can write / accumulate x's gradient into it."""
+    sk = getattr(x, "_adr_sink", None)
+    return sk if sk is not None and sk.fits(x) else None
+
+
+def _dx_dst(ctx, shape, dtype, dev):
+    """(buffer, accumulate) for a consumer's input gradient: the fan-out sink's shared buffer (claimed; the
+    consumer returns None to autograd) or a fresh NHWC tensor."""
+    if ctx.sink is not None:
+        buf, acc, _ = ctx.sink.claim(dev)
+        return buf, acc
+    return empty_act(*shape, dtype, dev), 0
+
+
 _FANOUT_SINK = bool(int(__import__("os").environ.get("ADR_FANOUT_SINK", "1")))
 _SEED_CAT = bool(int(__import__("os").environ.get("ADR_SEED_CAT", "1")))  # 0: CatFn hands every slice to autograd
 _DEFER_ADD = bool(int(__import__("os").environ.get("ADR_DEFER_ADD", "1")))  # 0: AddFn returns its gradient as is
@@ -2222,6 +2237,7 @@ class AxisMeanFn(torch.autograd.Function):
         lib.adr_axis_mean(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], N, H, W, C, ctypes.c_void_p(oh), ohn,
                           ctypes.c_void_p(ow), own, stream())
         ctx.meta = (layout, x.shape, x.dtype)
+        ctx.sink = _sink_of(x)
         return out
 
     @staticmethod
@@ -2234,10 +2250,10 @@ class AxisMeanFn(torch.autograd.Function):
             dh, dhn, dw, dwn = dy.data_ptr(), H * C, dy.data_ptr() + N * H * C * es, W * C
         else:
             dh, dhn, dw, dwn = dy.data_ptr(), (H + W) * C, dy.data_ptr() + H * C * es, (H + W) * C
-        dx = empty_act(N, C, H, W, dtype, dy.device)
+        dx, acc = _dx_dst(ctx, (N, C, H, W), dtype, dy.device)
         lib.adr_axis_mean_bwd(dcode(dtype), ctypes.c_void_p(dh), dhn, ctypes.c_void_p(dw), dwn,
-                              ctypes.c_void_p(dx.data_ptr()), C, N, H, W, C, 0, stream())
-        return dx, None
+                              ctypes.c_void_p(dx.data_ptr()), dx.stride(3), N, H, W, C, acc, stream())
+        return (None if ctx.sink is not None else dx), None
 
 
 def _is_dense_nhwc(t):
@@ -2272,6 +2288,7 @@ class GateFn(torch.autograd.Function):
                      ctypes.c_void_p(aw), awn, ctypes.c_void_p(out.data_ptr()), C, N, H, W, C, stream())
         ctx.save_for_backward(*( [vx[0]] if x is not None else []), ah_t, aw_t)
         ctx.meta = (layout, shape, x is not None, (ah, ahn, aw, awn))
+        ctx.sink = _sink_of(x) if x is not None else None
         return out
 
     @staticmethod
@@ -2294,15 +2311,37 @@ class GateFn(torch.autograd.Function):
             daw_t = torch.empty_like(aw_t, memory_format=torch.channels_last)
             dah, dahn = dah_t.data_ptr(), (H + W) * C
             daw, dawn = daw_t.data_ptr() + H * C * es, (H + W) * C
-        dx = empty_act(N, C, H, W, dtype, dout.device) if has_x else None
+        dx, acc = _dx_dst(ctx, (N, C, H, W), dtype, dout.device) if has_x else (None, 0)
         vx = _v(x) if has_x else (None, 0, 0)
-        lib.adr_gate_bwd(dcode(dtype), ctypes.c_void_p(vx[1]) if has_x else None, vx[2], ctypes.c_void_p(ah), ahn,
-                         ctypes.c_void_p(aw), awn, ctypes.c_void_p(vd[1]), vd[2],
-                         ctypes.c_void_p(dx.data_ptr()) if has_x else None, C, ctypes.c_void_p(dah), dahn,
-                         ctypes.c_void_p(daw), dawn, N, H, W, C, 0, int(layout != "ela"), stream())
+        _gate_bwd(dcode(dtype), vx[1] if has_x else None, vx[2], ah, ahn, aw, awn, vd[1], vd[2],
+                  dx.data_ptr() if has_x else None, dx.stride(3) if has_x else C, dah, dahn, daw, dawn, N, H, W, C,
+                  acc, int(layout != "ela"), dout.device)
+        if ctx.sink is not None:
+            dx = None
         if layout == "ela":
             return dx, da, None, None, None
         return dx, dah_t, daw_t, None, None
+
+
+def _gate_bwd(dt, xp, xcs, ah, ahn, aw, awn, dp, dcs, dx, dxcs, dah, dahn, daw, dawn, N, H, W, C, acc, zero_other,
+              dev):
+    """dx / dah / daw of the gate: the one-pass fused kernel when x and dx exist and the views are 16-byte
+    vectors (adr_gate_bwd_fused), else the reduce + x kernels (adr_gate_bwd)."""
+    vw = 8 if dt == BF16 else 4
+    es = 2 if dt == BF16 else 4
+    ptrs = [p for p in (xp, ah, aw, dp, dx, dah, daw) if p is not None]
+    if xp is not None and dx is not None and C % vw == 0 and C // vw <= 256 and all(
+            v % vw == 0 for v in (xcs, ahn, awn, dcs, dxcs, dahn, dawn)) and all(p % 16 == 0 for p in ptrs):
+        wsb = lib.adr_gate_bwd_fused_workspace(N, H, W, C)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=dev)
+        lib.adr_gate_bwd_fused(dt, ctypes.c_void_p(xp), xcs, ctypes.c_void_p(ah), ahn, ctypes.c_void_p(aw), awn,
+                               ctypes.c_void_p(dp), dcs, ctypes.c_void_p(dx), dxcs, ctypes.c_void_p(dah), dahn,
+                               ctypes.c_void_p(daw), dawn, N, H, W, C, acc, zero_other, fptr(ws), wsb, stream())
+        return
+    lib.adr_gate_bwd(dt, ctypes.c_void_p(xp) if xp is not None else None, xcs, ctypes.c_void_p(ah), ahn,
+                     ctypes.c_void_p(aw), awn, ctypes.c_void_p(dp), dcs,
+                     ctypes.c_void_p(dx) if dx is not None else None, dxcs, ctypes.c_void_p(dah), dahn,
+                     ctypes.c_void_p(daw), dawn, N, H, W, C, acc, zero_other, stream())
 
 
 def gate(x, ah, aw, layout, shape):
@@ -3509,6 +3548,7 @@ class GapPackFn(torch.autograd.Function):
         Np, C, _, S = x.shape
         s = _reduce_dot(None, x, False, False, which=1)  # per-sub-image sums
         ctx.pack, ctx.meta = pack, (tuple(x.shape), x.dtype)
+        ctx.sink = _sink_of(x)
         return _seg(s, False, True, True, pack, C)
 
     @staticmethod
@@ -3516,9 +3556,10 @@ class GapPackFn(torch.autograd.Function):
         pack = ctx.pack
         (Np, C, _, S), dtype = ctx.meta
         t = _seg(dg.float().contiguous(), True, False, True, pack, C)
-        dx = pack.empty(C, dtype, dg.device)
-        lib.adr_bcast_fill(dcode(dtype), fptr(t), C, 1, 1.0, ctypes.c_void_p(dx.data_ptr()), C, Np, S, C, 0, stream())
-        return dx, None
+        dx, acc = _dx_dst(ctx, (Np, C, 1, S), dtype, dg.device)
+        lib.adr_bcast_fill(dcode(dtype), fptr(t), C, 1, 1.0, ctypes.c_void_p(dx.data_ptr()), dx.stride(3), Np, S, C, acc,
+                           stream())
+        return (None if ctx.sink is not None else dx), None
 
 
 def gap_packed(x, pack):
@@ -3794,6 +3835,7 @@ class LevelAxisMeanFn(torch.autograd.Function):
             lib.adr_axis_mean(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], pack.N, H, W, C,
                               ctypes.c_void_p(o), (H + W) * C, ctypes.c_void_p(o + H * C * es), (H + W) * C, stream())
         ctx.pack, ctx.pp, ctx.meta = pack, pp, (C, x.dtype)
+        ctx.sink = _sink_of(x)
         return out
 
     @staticmethod
@@ -3801,13 +3843,14 @@ class LevelAxisMeanFn(torch.autograd.Function):
         pack, pp = ctx.pack, ctx.pp
         C, dtype = ctx.meta
         _, dp, dcs = nhwc(dy)
-        dx = pack.empty(C, dtype, dy.device)
-        es = dx.element_size()
+        dx, acc = _dx_dst(ctx, (pack.Np, C, 1, pack.S), dtype, dy.device)
+        es, xcs = dx.element_size(), dx.stride(3)
         for l, (H, W) in enumerate(pack.dims):
             o = pp.at(dp, dcs, es, l).value
             lib.adr_axis_mean_bwd(dcode(dtype), ctypes.c_void_p(o), (H + W) * dcs, ctypes.c_void_p(o + H * dcs * es),
-                                  (H + W) * dcs, pack.at(dx.data_ptr(), C, es, l), C, pack.N, H, W, C, 0, stream())
-        return dx, None, None
+                                  (H + W) * dcs, pack.at(dx.data_ptr(), xcs, es, l), xcs, pack.N, H, W, C, acc,
+                                  stream())
+        return (None if ctx.sink is not None else dx), None, None
 
 
 def axis_mean_levels(x, pack, pp):
@@ -3835,6 +3878,7 @@ class LevelGateFn(torch.autograd.Function):
                          pack.at(out.data_ptr(), C, es, l), C, pack.N, H, W, C, stream())
         ctx.save_for_backward(vx[0], ah, aw)
         ctx.pack, ctx.pp = pack, pp
+        ctx.sink = _sink_of(x)
         return out
 
     @staticmethod
@@ -3844,18 +3888,19 @@ class LevelGateFn(torch.autograd.Function):
         vx, vd = _v(x), _v(dout)
         C = x.shape[1]
         es = x.element_size()
-        dx = pack.empty(C, x.dtype, x.device)
+        dx, acc = _dx_dst(ctx, (pack.Np, C, 1, pack.S), x.dtype, x.device)
+        xcs = dx.stride(3)
         dah = pp.empty(C, x.dtype, x.device)
         daw = pp.empty(C, x.dtype, x.device)
         for l, (H, W) in enumerate(pack.dims):
             # zero_other: each gradient plane's unused rows (dah's column rows, daw's row rows) are written as 0
-            lib.adr_gate_bwd(dcode(x.dtype), pack.at(vx[1], vx[2], es, l), vx[2], pp.at(ah.data_ptr(), C, es, l),
-                             (H + W) * C, ctypes.c_void_p(pp.at(aw.data_ptr(), C, es, l).value + H * C * es),
-                             (H + W) * C, pack.at(vd[1], vd[2], es, l), vd[2], pack.at(dx.data_ptr(), C, es, l), C,
-                             pp.at(dah.data_ptr(), C, es, l), (H + W) * C,
-                             ctypes.c_void_p(pp.at(daw.data_ptr(), C, es, l).value + H * C * es), (H + W) * C,
-                             pack.N, H, W, C, 0, 1, stream())
-        return dx, dah, daw, None, None
+            _gate_bwd(dcode(x.dtype), pack.at(vx[1], vx[2], es, l).value, vx[2], pp.at(ah.data_ptr(), C, es, l).value,
+                      (H + W) * C, pp.at(aw.data_ptr(), C, es, l).value + H * C * es, (H + W) * C,
+                      pack.at(vd[1], vd[2], es, l).value, vd[2], pack.at(dx.data_ptr(), xcs, es, l).value, xcs,
+                      pp.at(dah.data_ptr(), C, es, l).value, (H + W) * C,
+                      pp.at(daw.data_ptr(), C, es, l).value + H * C * es, (H + W) * C, pack.N, H, W, C, acc, 1,
+                      x.device)
+        return (None if ctx.sink is not None else dx), dah, daw, None, None
 
 
 def gate_levels(x, ah, aw, pack, pp):

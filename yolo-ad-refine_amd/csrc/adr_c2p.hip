@@ -291,6 +291,65 @@ __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, 
   }
 }
 
+// The same weight gradient for k in {3, 5, 7} with a sliding window along the rows: item (ky, 4-channel group, row
+// split rs) walks whole output rows; per pixel it loads ONE dy vector and ONE new padded-x vector (the previous
+// k - 1 stay in registers) for k taps, instead of two LDS loads per tap. The RS row splits of an item are adjacent
+// lanes of one wave, combined by an xor butterfly (fixed order: deterministic).
+template <typename T, int CB, int KS>
+__global__ void __launch_bounds__(256) dw_wgrad_row_kernel(const T* x, int xcs, const T* dy, int dcs, int H, int W,
+                                                           int C, float* partial) {
+  constexpr int NV = CB / 4, P = KS / 2, KK = KS * KS;
+  extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
+  const int n = blockIdx.x, cb0 = blockIdx.y * CB;
+  const int Hp = H + 2 * P, Wp = W + 2 * P;
+  float* xs = reinterpret_cast<float*>(dwsm);
+  float* ds = xs + (long)Hp * Wp * CB;
+  stage_img_f32<T>(x + (long)n * H * W * xcs, xcs, H, W, P, cb0, C, CB, xs);
+  stage_img_f32<T>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
+  __syncthreads();
+  constexpr int pairs = KS * NV;
+  int RS = 1;  // row splits per (ky, group): a power of two <= 64 dividing 256, so a group sits in one wave
+  while (RS * 2 * pairs <= 256 && RS < 64 && RS < H) RS *= 2;
+  for (int base = 0; base < pairs * RS; base += 256) {
+    const int it = base + threadIdx.x;
+    const int pr = it / RS, rs = it % RS;
+    f32x4 acc[KS];
+#pragma unroll
+    for (int kx = 0; kx < KS; ++kx) acc[kx] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    if (pr < pairs) {
+      const int ky = pr / NV, cv = pr % NV;
+      for (int oy = rs; oy < H; oy += RS) {
+        const float* xr = xs + (long)(oy + ky) * Wp * CB + cv * 4;
+        const float* dr = ds + (long)oy * W * CB + cv * 4;
+        f32x4 xw[KS];
+#pragma unroll
+        for (int kx = 0; kx < KS - 1; ++kx) xw[kx] = *reinterpret_cast<const f32x4*>(xr + kx * CB);
+        for (int ox = 0; ox < W; ++ox) {
+          xw[KS - 1] = *reinterpret_cast<const f32x4*>(xr + (ox + KS - 1) * CB);
+          const f32x4 d4 = *reinterpret_cast<const f32x4*>(dr + ox * CB);
+#pragma unroll
+          for (int kx = 0; kx < KS; ++kx) acc[kx] += d4 * xw[kx];
+#pragma unroll
+          for (int kx = 0; kx < KS - 1; ++kx) xw[kx] = xw[kx + 1];
+        }
+      }
+    }
+    for (int o = 1; o < RS; o <<= 1)
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[kx][e] += __shfl_xor(acc[kx][e], o, 64);
+    if (rs == 0 && pr < pairs) {
+      const int ky = pr / NV, cv = pr % NV, c = cb0 + cv * 4;
+#pragma unroll
+      for (int kx = 0; kx < KS; ++kx)
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (c + e < C) partial[((long)n * KK + ky * KS + kx) * C + c + e] = acc[kx][e];
+    }
+  }
+}
+
 // dw[c][t] = sum_chunks partial[chunk][t][c]; threads walk c fastest (coalesced partial rows), 8 chunks in flight
 __global__ void dw_w_reduce_kernel(const float* partial, int chunks, int C, int kk, float* dw, int accumulate) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -832,20 +891,20 @@ using namespace adr;
   } while (0)
 
 static constexpr int DW_CB_BF16 = 16, DW_CB_F32 = 8, DW_CB_WG = 8;  // DW_CB_WG: weight-gradient channel slab
-// channel slab of the bf16 whole-image forward / data-gradient kernel (ADR_DW_CB=32 selects 32 for A/B runs)
-static int dw_cb_fwd() {
-  static int v = -1;
-  if (v < 0) {
-    const char* e = getenv("ADR_DW_CB");
-    v = e && atoi(e) == 32 ? 32 : DW_CB_BF16;
-  }
-  return v;
-}
 // ADR_DW_IMG=0 routes the forward / data gradient to the direct (global-load) kernel for A/B runs
 static bool dw_img_ok() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("ADR_DW_IMG");
+    v = e ? atoi(e) != 0 : 1;
+  }
+  return v != 0;
+}
+// ADR_DW_ROW=0: the per-tap weight-gradient kernel instead of the sliding-window one (A/B)
+static bool dw_row_ok() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("ADR_DW_ROW");
     v = e ? atoi(e) != 0 : 1;
   }
   return v != 0;
@@ -857,17 +916,14 @@ static size_t dw_img_smem(int dtype, int H, int W, int k) {  // weight-gradient 
 }
 static size_t dw_fwd_smem(int dtype, int H, int W, int k) {  // forward / data-gradient kernel
   const int p = k / 2;
-  const size_t cb = dtype == ADR_BF16 ? dw_cb_fwd() : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
+  const size_t cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
   return (size_t)k * k * cb * 4 + (size_t)(H + 2 * p) * (W + 2 * p) * cb * es;
 }
 template <bool BWD>
 static void dw_img_launch(int dtype, hipStream_t st, const void* x, int xcs, const float* w, const float* b, void* y,
                           int ycs, int N, int H, int W, int C, int k, int acc) {
   const size_t sm = dw_fwd_smem(dtype, H, W, k);
-  if (dtype == ADR_BF16 && dw_cb_fwd() == 32)
-    hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, 32>), dim3(N, cdiv(C, 32)), dim3(256), sm, st, (const __bf16*)x,
-                       xcs, w, b, (__bf16*)y, ycs, H, W, C, k, acc);
-  else if (dtype == ADR_BF16)
+  if (dtype == ADR_BF16)
     hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
                        (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, H, W, C, k, acc);
   else
@@ -921,11 +977,7 @@ extern "C" int adr_dwconv_fwd_act(const void* x, int xcs, const float* w, const 
               C, k);
   const size_t sm = dw_fwd_smem(ADR_BF16, H, W, k);
   hipStream_t st = (hipStream_t)stream;
-  if (dw_cb_fwd() == 32)
-    hipLaunchKernelGGL((dw_img_act_kernel<32>), dim3(N, cdiv(C, 32)), dim3(256), sm, st, (const __bf16*)x, xcs, w,
-                       scale, shift, act, (__bf16*)y, ycs, H, W, C, k);
-  else
-    hipLaunchKernelGGL((dw_img_act_kernel<DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
+  hipLaunchKernelGGL((dw_img_act_kernel<DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
                        (const __bf16*)x, xcs, w, scale, shift, act, (__bf16*)y, ycs, H, W, C, k);
   return check_launch("adr_dwconv_fwd_act");
 }
@@ -964,8 +1016,19 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
     const size_t ism = dw_img_smem(dtype, H, W, k);
     if (ism <= 64 * 1024 && xcs % v == 0 && dcs % v == 0) {  // small maps (the 20x20 C2PTSSA / EDFFN / Mona path): whole image in LDS
       chunks = N;
-      if (dtype == ADR_BF16)
-        hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, DW_CB_WG>), dim3(N, cdiv(C, DW_CB_WG)), dim3(256), ism, st,
+      const dim3 ig(N, cdiv(C, DW_CB_WG));
+      if (dtype == ADR_BF16 && dw_row_ok() && (k == 3 || k == 5 || k == 7)) {
+        if (k == 3)
+          hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, DW_CB_WG, 3>), ig, dim3(256), ism, st, (const __bf16*)x,
+                             xcs, (const __bf16*)dy, dcs, H, W, C, ws);
+        else if (k == 5)
+          hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, DW_CB_WG, 5>), ig, dim3(256), ism, st, (const __bf16*)x,
+                             xcs, (const __bf16*)dy, dcs, H, W, C, ws);
+        else
+          hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, DW_CB_WG, 7>), ig, dim3(256), ism, st, (const __bf16*)x,
+                             xcs, (const __bf16*)dy, dcs, H, W, C, ws);
+      } else if (dtype == ADR_BF16)
+        hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, DW_CB_WG>), ig, dim3(256), ism, st,
                            (const __bf16*)x, xcs, (const __bf16*)dy, dcs, H, W, C, k, ws);
       else
         hipLaunchKernelGGL((dw_wgrad_img_kernel<float, DW_CB_WG>), dim3(N, cdiv(C, DW_CB_WG)), dim3(256), ism, st,
@@ -995,8 +1058,16 @@ extern "C" int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alph
   return check_launch("adr_adyt_fwd");
 }
 
+// rows per adyt_bwd workgroup: 256, halved until the grid has ~1024 workgroups (the C2PTSSA maps are 20x20: one
+// 256-row chunk per image left half the chip idle, each thread walking 128 rows of three tanh each)
+static int adyt_rows(int N, int HW) {
+  int r = 256;
+  while (r > 16 && (long)N * cdiv(HW, r) < 1024) r /= 2;
+  return r;
+}
+
 extern "C" size_t adr_adyt_bwd_workspace(int N, int HW, int C) {
-  return ((size_t)N * cdiv(HW, 256) * 8 * C + (size_t)N * 3) * sizeof(float);
+  return ((size_t)N * cdiv(HW, adyt_rows(N, HW)) * 8 * C + (size_t)N * 3) * sizeof(float);
 }
 
 extern "C" int adr_adyt_bwd(int dtype, const void* x, int xcs, const void* dout, int dcs, const float* alphas,
@@ -1005,14 +1076,14 @@ extern "C" int adr_adyt_bwd(int dtype, const void* x, int xcs, const void* dout,
   ADR_REQUIRE(C <= 256, "adyt_bwd: C=%d > 256", C);
   ADR_REQUIRE(ws_bytes >= adr_adyt_bwd_workspace(N, HW, C), "adyt_bwd: workspace");
   hipStream_t st = (hipStream_t)stream;
-  int chunks = cdiv(HW, 256);
+  const int rows = adyt_rows(N, HW), chunks = cdiv(HW, rows);
   dim3 g(chunks, N);
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(adyt_bwd_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dout, dcs,
-                       alphas, imp, w, (__bf16*)dx, ocs, HW, C, 256, chunks, ws);
+                       alphas, imp, w, (__bf16*)dx, ocs, HW, C, rows, chunks, ws);
   else
     hipLaunchKernelGGL(adyt_bwd_kernel<float>, g, dim3(256), 0, st, (const float*)x, xcs, (const float*)dout, dcs,
-                       alphas, imp, w, (float*)dx, ocs, HW, C, 256, chunks, ws);
+                       alphas, imp, w, (float*)dx, ocs, HW, C, rows, chunks, ws);
   float* dan = ws + (size_t)N * chunks * 8 * C;
   hipLaunchKernelGGL(adyt_collapse_kernel, dim3(3 * N + C), dim3(256), 0, st, ws, N, chunks, C, dimp, dan, dw, db);
   hipLaunchKernelGGL(adyt_alpha_kernel, dim3(1), dim3(64), 0, st, dan, imp, N, dalpha);

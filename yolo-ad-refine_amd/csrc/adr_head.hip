@@ -361,12 +361,29 @@ __global__ void __launch_bounds__(256) gate_mlp_bwd_kernel(const float* in, floa
     for (int j = 0; j < H1; ++j) s += W1[(long)j * Cin + c] * dh[n * H1 + j];
     din[i] = s * in_scale;
   }
-  for (int i = gt; i < H1 * Cin; i += gs) {
-    const int j = i / Cin, c = i % Cin;
-    float s = 0.f;
-    for (int n = 0; n < N; ++n) s += dh[n * H1 + j] * in[(long)n * Cin + c];
-    s *= in_scale;
-    dW1[i] = accumulate ? dW1[i] + s : s;
+  // dW1: each block owns a contiguous run of OB outputs, its threads split the image sum P ways (part p takes
+  // images p, p + P, ...), partial sums combined in part order through LDS (deterministic)
+  {
+    __shared__ float red[256];
+    const int O = H1 * Cin, OB = (O + gridDim.x - 1) / gridDim.x;
+    for (int o0 = blockIdx.x * OB; o0 < min(O, (blockIdx.x + 1) * OB); o0 += 256) {
+      const int ob = min(256, min(O, (blockIdx.x + 1) * OB) - o0), P = 256 / ob;
+      const int ol = tid % ob, part = tid / ob, i = o0 + ol;
+      float s = 0.f;
+      if (part < P) {
+        const int j = i / Cin, c = i % Cin;
+        for (int n = part; n < N; n += P) s += dh[n * H1 + j] * in[(long)n * Cin + c];
+      }
+      red[tid] = s;
+      __syncthreads();
+      if (tid < ob) {
+        float t = 0.f;
+        for (int q = 0; q < P; ++q) t += red[q * ob + tid];
+        t *= in_scale;
+        dW1[i] = accumulate ? dW1[i] + t : t;
+      }
+      __syncthreads();
+    }
   }
   for (int i = gt; i < H2 * H1; i += gs) {
     const int j = i / H1, c = i % H1;
@@ -634,7 +651,7 @@ extern "C" int adr_gate_mlp_bwd(const float* in, float in_scale, int N, int Cin,
                                 int accumulate, void* stream) {
   size_t sm = (size_t)N * (H1 + H2) * sizeof(float);
   ADR_REQUIRE(sm <= 64 * 1024, "gate_mlp_bwd: N=%d H1=%d H2=%d exceed the LDS budget", N, H1, H2);
-  hipLaunchKernelGGL(gate_mlp_bwd_kernel, dim3(16), dim3(256), sm, (hipStream_t)stream, in, in_scale, Cin, W1, H1, act1,
+  hipLaunchKernelGGL(gate_mlp_bwd_kernel, dim3(64), dim3(256), sm, (hipStream_t)stream, in, in_scale, Cin, W1, H1, act1,
                      W2, H2, act2, hidden, out, dout, N, din, dW1, db1, dW2, db2, accumulate);
   return check_launch("adr_gate_mlp_bwd");
 }

@@ -112,15 +112,28 @@ __global__ void mlca_mix_kernel(const float* sig_l, const float* sig_g, int N, i
   att[idx] = (1.f - lw) * g + lw * sig_l[idx];
 }
 
-// S[i][c] = sum_n sum_j datt[n][i*5+j][c]
-__global__ void mlca_gsum_kernel(const float* datt, int N, int C, float* S) {
-  int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= LS * C) return;
-  int i = idx / C, c = idx % C;
-  float s = 0.f;
-  for (int n = 0; n < N; ++n)
-    for (int j = 0; j < LS; ++j) s += datt[((long)n * LS * LS + i * LS + j) * C + c];
-  S[idx] = s;
+// S[i][c] = sum_n sum_j datt[n][i*5+j][c]: block i; threads = (image part, channel), parts of the image sum
+// combined in order through LDS (deterministic)
+__global__ void __launch_bounds__(256) mlca_gsum_kernel(const float* datt, int N, int C, float* S) {
+  __shared__ float red[256];
+  const int i = blockIdx.x;
+  for (int c0 = 0; c0 < C; c0 += 256) {
+    const int cb = min(256, C - c0), P = 256 / cb;
+    const int c = c0 + threadIdx.x % cb, part = threadIdx.x / cb;
+    float s = 0.f;
+    if (part < P)
+      for (int n = part; n < N; n += P)
+#pragma unroll
+        for (int j = 0; j < LS; ++j) s += datt[((long)n * LS * LS + i * LS + j) * C + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if ((int)threadIdx.x < cb) {
+      float t = 0.f;
+      for (int q = 0; q < P; ++q) t += red[q * cb + threadIdx.x];
+      S[i * C + c] = t;
+    }
+    __syncthreads();
+  }
 }
 
 // up(att)[h][w][c0..c0+VW) = mean of att over the 5x5 bins in pixel (h, w)'s window
@@ -412,7 +425,7 @@ extern "C" int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout,
                 datt);
   size_t sm = (2 * C + LS * LS * C + 512) * sizeof(float);
   ADR_REQUIRE(sm <= 160 * 1024, "mlca_bwd: C=%d too large for the per-image LDS plan", C);
-  hipLaunchKernelGGL(mlca_gsum_kernel, dim3(cdiv(LS * C, 256)), dim3(256), 0, st, datt, N, C, S);
+  hipLaunchKernelGGL(mlca_gsum_kernel, dim3(LS), dim3(256), 0, st, datt, N, C, S);
   hipLaunchKernelGGL(mlca_att_bwd_kernel, dim3(N), dim3(256), sm, st, local, datt, sig_l, sig_g, S, N, C, wl, wg, k,
                      local_weight, dlocal, dwl_part, dwg_part);
   MLCA_DISPATCH(dtype, v, mlca_bwd_y_kernel, mlca_grid((long)N * H * W, dtype, v, C), (const TT*)dout, dcs, att,

@@ -248,10 +248,6 @@ __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
   wgrad_bf16_body<BM, BN, wg_ku(BM, BN)>(a);
 }
 
-template <int BM, int BN>
-__global__ void __launch_bounds__(256) wgrad_bf16_ku2_kernel(WgArgs a) {
-  wgrad_bf16_body<BM, BN, 2>(a);
-}
 
 // ------------------------------------------------------------------------------------------------------------
 // 3x3 / stride-1 / pad-1 weight gradient on 2-D output tiles (the WGRAD counterpart of adr_conv.hip's
@@ -543,15 +539,6 @@ static bool thin_enabled() {
   return v != 0;
 }
 
-// k-step depth of the 128 x 128 tile (ADR_WG_KU=2: two 32-row sub-steps per barrier pair; A/B)
-static int wg_ku128() {
-  static const int v = [] {
-    const char* e = getenv("ADR_WG_KU");
-    return e && atoi(e) == 2 ? 2 : 1;
-  }();
-  return v;
-}
-
 static int wg_pick16(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128; }
 
 template <int BM>
@@ -561,10 +548,7 @@ static void launch_bm(int bn, dim3 grid, const WgArgs& g, hipStream_t st) {
     case 32: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 32>), grid, dim3(256), 0, st, g); break;
     case 64: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 64>), grid, dim3(256), 0, st, g); break;
     default:
-      if (BM == 128 && wg_ku128() == 2)
-        hipLaunchKernelGGL((wgrad_bf16_ku2_kernel<BM, 128>), grid, dim3(256), 0, st, g);
-      else
-        hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 128>), grid, dim3(256), 0, st, g);
+      hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 128>), grid, dim3(256), 0, st, g);
       break;
   }
 }
@@ -619,7 +603,7 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   p.bm = wg_pick16(d->k);
   p.bn = wg_pick16(d->c);
   const int wm = p.bm / 16 < 2 ? p.bm / 16 : 2, wn = p.bn / 16 < 2 ? p.bn / 16 : 2;
-  p.R = 32 * (4 / (wm * wn)) * (p.bm == 128 && p.bn == 128 ? wg_ku128() : wg_ku(p.bm, p.bn));
+  p.R = 32 * (4 / (wm * wn)) * wg_ku(p.bm, p.bn);
   const long red = (long)d->n * d->ho * d->wo;
   const long outsz = (long)d->k * d->r * d->s * d->c;
   p.tiles = cdiv(d->k, p.bm) * d->r * d->s * cdiv(d->c, p.bn);
