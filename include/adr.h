@@ -379,14 +379,6 @@ int adr_axis_mean_bwd(int dtype, const void* dh, long dhn, const void* dw, long 
                       int W, int C, int accumulate, void* stream);
 int adr_gate(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw, long awn, void* o, int ocs,
              int N, int H, int W, int C, void* stream);
-/* adr_gate_bwd with x and dx (16-byte channel vectors) in ONE pass over dout and x: a workgroup owns a band of
- * rows of one image (dx written / accumulated, the band's dah rows complete, per-band column partials of daw into
- * ws, folded in band order by a second small kernel; zero_other as adr_gate_bwd). ws: fp32,
- * adr_gate_bwd_fused_workspace(N, H, W, C) bytes. ELA_HSFPN / CoordAtt gates (block.py:1418-1424, head.py:689-707). */
-size_t adr_gate_bwd_fused_workspace(int N, int H, int W, int C);
-int adr_gate_bwd_fused(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw, long awn,
-                       const void* dout, int dcs, void* dx, int ocs, void* dah, long dahn, void* daw, long dawn, int N,
-                       int H, int W, int C, int accumulate, int zero_other, float* ws, size_t ws_bytes, void* stream);
 int adr_gate_bwd(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw, long awn,
                  const void* dout, int dcs, void* dx, int ocs, void* dah, long dahn, void* daw, long dawn, int N,
                  int H, int W, int C, int accumulate, int zero_other, void* stream);

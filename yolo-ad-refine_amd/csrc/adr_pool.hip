@@ -263,105 +263,6 @@ __global__ void __launch_bounds__(256) gate_bwd_x_kernel(const T* ah, long ahn, 
   }
 }
 
-// Gate backward in ONE pass over dout and x (the reduce + x kernels above read them three times): block = (band of
-// GB_TH rows, image). Threads = (channel group cg, column lane wl): a thread walks columns wl, wl + WL, ... and for
-// each the band's rows, so
-//   dx = dout * a_h * a_w is written (or accumulated) as it goes,
-//   the band's partial column sum of dout * x * a_h for that column is complete in the thread -> part[n][band][w][c]
-//   (fp32; gate_bwd_cols_kernel folds the bands in order into daw),
-//   the row sums dout * x * a_w per row of the band are per-thread partials over its columns, combined across the
-//   column lanes through LDS in lane order -> dah rows of the band (complete: the block owns the whole rows).
-constexpr int GB_TH = 8;
-template <typename T, int VW>
-__global__ void __launch_bounds__(256) gate_bwd_fused_kernel(const T* x, int xcs, const T* ah, long ahn, const T* aw,
-                                                             long awn, const T* dout, int dcs, T* dx, int ocs,
-                                                             int accumulate, T* dah, long dahn, float* part, int H,
-                                                             int W, int C) {
-  __shared__ float red[256 * VW];
-  const int n = blockIdx.y, band = blockIdx.x, bands = gridDim.x;
-  const int h0 = band * GB_TH, nh = min(GB_TH, H - h0);
-  const int G = C / VW, WL = 256 / G;
-  const int cg = threadIdx.x % G, wl = threadIdx.x / G, c0 = cg * VW;
-  const bool on = wl < WL;
-  float racc[GB_TH][VW];
-#pragma unroll
-  for (int r = 0; r < GB_TH; ++r)
-#pragma unroll
-    for (int e = 0; e < VW; ++e) racc[r][e] = 0.f;
-  if (on)
-    for (int w = wl; w < W; w += WL) {
-      float b[VW], cs[VW];
-      vload<T, VW>(aw + n * awn + (long)w * C + c0, b);
-#pragma unroll
-      for (int e = 0; e < VW; ++e) cs[e] = 0.f;
-#pragma unroll
-      for (int r = 0; r < GB_TH; ++r) {
-        if (r >= nh) break;
-        const long pix = ((long)n * H + h0 + r) * W + w;
-        float a[VW], d[VW], v[VW];
-        vload<T, VW>(ah + n * ahn + (long)(h0 + r) * C + c0, a);
-        vload<T, VW>(dout + pix * dcs + c0, d);
-        vload<T, VW>(x + pix * xcs + c0, v);
-        float o[VW];
-#pragma unroll
-        for (int e = 0; e < VW; ++e) {
-          const float dv = d[e] * v[e];
-          racc[r][e] += dv * b[e];
-          cs[e] += dv * a[e];
-          o[e] = d[e] * a[e] * b[e];
-        }
-        vstore_acc<T, VW>(dx + pix * ocs + c0, o, accumulate);
-      }
-      float* pp = part + (((long)n * bands + band) * W + w) * C + c0;
-#pragma unroll
-      for (int e = 0; e < VW; ++e) pp[e] = cs[e];
-    }
-  for (int r = 0; r < nh; ++r) {
-#pragma unroll
-    for (int e = 0; e < VW; ++e) red[threadIdx.x * VW + e] = racc[r][e];
-    __syncthreads();
-    if (wl == 0) {
-      float t[VW];
-#pragma unroll
-      for (int e = 0; e < VW; ++e) t[e] = 0.f;
-      for (int q = 0; q < WL; ++q)
-#pragma unroll
-        for (int e = 0; e < VW; ++e) t[e] += red[(q * G + cg) * VW + e];
-      vstore<T, VW>(dah + n * dahn + (long)(h0 + r) * C + c0, t);
-    }
-    __syncthreads();
-  }
-}
-
-// daw[n][w][c] = sum over bands (in order) of part[n][band][w][c]; zero_other (coord layout) also writes the rows of
-// the two (H + W)-row gradient planes the gate does not read: dah rows H.., daw rows ..H (daw passed at row H)
-template <typename T, int VW>
-__global__ void __launch_bounds__(256) gate_bwd_cols_kernel(const float* part, int bands, T* dah, long dahn, T* daw,
-                                                            long dawn, int N, int H, int W, int C, int zero_other) {
-  const int G = C / VW;
-  const long items = (long)N * W * G;
-  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < items; i += (long)gridDim.x * 256) {
-    const int cg = (int)(i % G);
-    const long nw = i / G;
-    const int w = (int)(nw % W), n = (int)(nw / W), c0 = cg * VW;
-    float t[VW];
-#pragma unroll
-    for (int e = 0; e < VW; ++e) t[e] = 0.f;
-    for (int b = 0; b < bands; ++b) {
-      const float* pp = part + (((long)n * bands + b) * W + w) * C + c0;
-#pragma unroll
-      for (int e = 0; e < VW; ++e) t[e] += pp[e];
-    }
-    vstore<T, VW>(daw + n * dawn + (long)w * C + c0, t);
-    if (zero_other) {
-#pragma unroll
-      for (int e = 0; e < VW; ++e) t[e] = 0.f;
-      vstore<T, VW>(dah + n * dahn + (long)(H + w) * C + c0, t);
-      for (int h = w; h < H; h += W) vstore<T, VW>(daw + n * dawn + (long)(h - H) * C + c0, t);
-    }
-  }
-}
-
 // ---- adaptive average pool ----
 template <typename T, int VW>
 __global__ void __launch_bounds__(256) adapool_kernel(const T* x, int xcs, int N, int H, int W, int C, T* y, int ycs,
@@ -653,41 +554,6 @@ extern "C" int adr_gate(int dtype, const void* x, int xcs, const void* ah, long 
     else hipLaunchKernelGGL((gate_kernel<float, 1>), g, dim3(256), 0, st, P(const float, x), xcs, P(const float, ah), ahn, P(const float, aw), awn, P(float, o), ocs, N, H, W, C);
   }
   return check_launch("adr_gate");
-}
-
-extern "C" size_t adr_gate_bwd_fused_workspace(int N, int H, int W, int C) {
-  return (size_t)N * cdiv(H, GB_TH) * W * C * sizeof(float);
-}
-
-// adr_gate_bwd (x and dx present, 16-byte vectors) in one pass over dout and x, plus the band fold: see
-// gate_bwd_fused_kernel. ws: adr_gate_bwd_fused_workspace bytes.
-extern "C" int adr_gate_bwd_fused(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw,
-                                  long awn, const void* dout, int dcs, void* dx, int ocs, void* dah, long dahn,
-                                  void* daw, long dawn, int N, int H, int W, int C, int accumulate, int zero_other,
-                                  float* ws, size_t ws_bytes, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
-  const int vw = VW_OF(dtype);
-  ADR_REQUIRE(x && dx && dah && daw && ws && ws_bytes >= adr_gate_bwd_fused_workspace(N, H, W, C),
-              "gate_bwd_fused: operands / workspace");
-  ADR_REQUIRE(vec_ok(C, vw, {xcs, ahn, awn, dcs, ocs, dahn, dawn}, {x, ah, aw, dout, dx, dah, daw}) && C / vw <= 256,
-              "gate_bwd_fused: needs 16-byte channel vectors (C=%d)", C);
-  const dim3 g(cdiv(H, GB_TH), N);
-  const long items = (long)N * W * (C / vw);
-  const dim3 gc((unsigned)std::min<long>(cdiv(items, 256), 4096));
-  if (dtype == ADR_BF16) {
-    hipLaunchKernelGGL((gate_bwd_fused_kernel<__bf16, 8>), g, dim3(256), 0, st, P(const __bf16, x), xcs,
-                       P(const __bf16, ah), ahn, P(const __bf16, aw), awn, P(const __bf16, dout), dcs, P(__bf16, dx), ocs,
-                       accumulate, P(__bf16, dah), dahn, ws, H, W, C);
-    hipLaunchKernelGGL((gate_bwd_cols_kernel<__bf16, 8>), gc, dim3(256), 0, st, ws, (int)g.x, P(__bf16, dah), dahn,
-                       P(__bf16, daw), dawn, N, H, W, C, zero_other);
-  } else {
-    hipLaunchKernelGGL((gate_bwd_fused_kernel<float, 4>), g, dim3(256), 0, st, P(const float, x), xcs,
-                       P(const float, ah), ahn, P(const float, aw), awn, P(const float, dout), dcs, P(float, dx), ocs,
-                       accumulate, P(float, dah), dahn, ws, H, W, C);
-    hipLaunchKernelGGL((gate_bwd_cols_kernel<float, 4>), gc, dim3(256), 0, st, ws, (int)g.x, P(float, dah), dahn,
-                       P(float, daw), dawn, N, H, W, C, zero_other);
-  }
-  return check_launch("adr_gate_bwd_fused");
 }
 
 extern "C" int adr_gate_bwd(int dtype, const void* x, int xcs, const void* ah, long ahn, const void* aw, long awn,
