@@ -1,5 +1,5 @@
 """Per-step GPU time of the REPLAYED training steps only, from a rocprofv3 --kernel-trace CSV of a bench.py run:
-steps are cut at the once-per-step optimizer kernel (sgd_ema), the last `--steps` complete ones are averaged (the
+steps are cut at the once-per-step optimizer kernel (sgd_ema; the loss kernel when the optimizer steps less often), the last `--steps` complete ones are averaged (the
 eager warm-up / capture steps, which launch differently, are left out). Prints the family table (families of
 kernel_breakdown.py), the top kernels and the launch count per step.
 usage: python scripts/replay_breakdown.py <run_kernel_trace.csv> [--steps 8] [--top 40]"""
@@ -19,6 +19,8 @@ ap.add_argument("--top", type=int, default=40)
 a = ap.parse_args()
 rows = sorted(csv.DictReader(open(a.trace)), key=lambda r: int(r["Start_Timestamp"]))
 marks = [i for i, r in enumerate(rows) if "sgd_ema" in r["Kernel_Name"]]
+if len(marks) < 3:  # gradient accumulation (bs < nbs: the optimizer runs every few steps): cut at the loss kernel
+    marks = [i for i, r in enumerate(rows) if "loss_cls_grad_kernel" in r["Kernel_Name"]]
 segs = list(zip(marks[:-1], marks[1:]))[-a.steps:]
 fam = defaultdict(lambda: [0.0, 0])
 ker = defaultdict(lambda: [0.0, 0])

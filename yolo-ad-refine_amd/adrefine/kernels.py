@@ -1966,14 +1966,15 @@ class ActFn(torch.autograd.Function):
         _ew(EW_ACT, (out, out.data_ptr(), out.shape[1]), vx, act=ACT[act])
         ctx.save_for_backward(vx[0])
         ctx.act = act
+        ctx.sink = _sink_of(x)
         return out
 
     @staticmethod
     def backward(ctx, dy):
         (x,) = ctx.saved_tensors
-        dx = _new_like(x)
-        _ew(EW_ACT_BWD, (dx, dx.data_ptr(), dx.shape[1]), _v(x), _v(dy), act=ACT[ctx.act])
-        return dx, None
+        dx, acc = _dx_dst(ctx, tuple(x.shape), x.dtype, x.device)
+        _ew(EW_ACT_BWD, (dx, dx.data_ptr(), dx.stride(3)), _v(x), _v(dy), act=ACT[ctx.act], accumulate=acc)
+        return (None if ctx.sink is not None else dx), None
 
 
 def act(x, name):
@@ -2151,6 +2152,7 @@ class MaxPoolFn(torch.autograd.Function):
                         N, H, W, C, k, stream())
         ctx.save_for_backward(arg)
         ctx.meta = (k, x.shape, x.dtype)
+        ctx.sink = _sink_of(x)
         return y if box is None else y[:, :]
 
     @staticmethod
@@ -2159,10 +2161,10 @@ class MaxPoolFn(torch.autograd.Function):
         k, shape, dtype = ctx.meta
         N, C, H, W = shape
         vd = _v(dy)
-        dx = empty_act(N, C, H, W, dtype, dy.device)
-        lib.adr_maxpool_bwd(dcode(dtype), ctypes.c_void_p(vd[1]), vd[2], fptr(arg), ctypes.c_void_p(dx.data_ptr()), C,
-                            N, H, W, C, k, 0, stream())
-        return dx, None, None
+        dx, acc = _dx_dst(ctx, (N, C, H, W), dtype, dy.device)
+        lib.adr_maxpool_bwd(dcode(dtype), ctypes.c_void_p(vd[1]), vd[2], fptr(arg), ctypes.c_void_p(dx.data_ptr()),
+                            dx.stride(3), N, H, W, C, k, acc, stream())
+        return (None if ctx.sink is not None else dx), None, None
 
 
 def maxpool(x, k, out=None):
@@ -2698,6 +2700,7 @@ class DWConvFn(torch.autograd.Function):
         ctx.save_for_backward(vx[0], wf)
         ctx.meta = (k, w.shape, b is not None)
         ctx.pw, ctx.pb = w, b
+        ctx.sink = _sink_of(x)
         return y
 
     @staticmethod
@@ -2706,15 +2709,16 @@ class DWConvFn(torch.autograd.Function):
         k, wshape, has_b = ctx.meta
         N, C, H, W = x.shape
         vx, vd = _v(x), _v(dy)
-        dx = _new_like(x) if ctx.needs_input_grad[0] else None
+        dx, acc = _dx_dst(ctx, (N, C, H, W), x.dtype, x.device) if ctx.needs_input_grad[0] else (None, 0)
         dw, pdw, dacc = grad_dst(ctx.pw, C * k * k, x.device) if ctx.needs_input_grad[1] else (None, None, 0)
         wsb = lib.adr_dwconv_wgrad_workspace(N, H, W, C, k)
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=x.device)
         lib.adr_dwconv_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]), vd[2], fptr(wf),
-                           ctypes.c_void_p(dx.data_ptr()) if dx is not None else None, C, pdw, N, H, W, C, k, 0,
-                           dacc, fptr(ws), wsb, stream())
+                           ctypes.c_void_p(dx.data_ptr()) if dx is not None else None,
+                           dx.stride(3) if dx is not None else C, pdw, N, H, W, C, k, acc, dacc, fptr(ws), wsb,
+                           stream())
         db = _bias_grad(vd[0], C, N, H * W, vd[2], ctx.pb) if has_b and ctx.needs_input_grad[2] else None
-        return dx, grad_ret(ctx.pw, dw), db, None
+        return (None if ctx.sink is not None else dx), grad_ret(ctx.pw, dw), db, None
 
 
 def dwconv(x, w, b, k):
@@ -2999,16 +3003,17 @@ class AdaPoolFn(torch.autograd.Function):
         lib.adr_adapool(dcode(x.dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(y.data_ptr()), C, oh, ow,
                         stream())
         ctx.meta = (x.shape, x.dtype)
+        ctx.sink = _sink_of(x)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (N, C, H, W), dtype = ctx.meta
         t, p, cs = _v(dy)
-        dx = empty_act(N, C, H, W, dtype, dy.device)
-        lib.adr_adapool_bwd(dcode(dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(dx.data_ptr()), C,
-                            dy.shape[2], dy.shape[3], 0, stream())
-        return dx, None, None
+        dx, acc = _dx_dst(ctx, (N, C, H, W), dtype, dy.device)
+        lib.adr_adapool_bwd(dcode(dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(dx.data_ptr()),
+                            dx.stride(3), dy.shape[2], dy.shape[3], acc, stream())
+        return (None if ctx.sink is not None else dx), None, None
 
 
 def adaptive_avg_pool(x, oh, ow):
@@ -3024,16 +3029,17 @@ class BilinearFn(torch.autograd.Function):
         lib.adr_bilinear(dcode(x.dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(y.data_ptr()), C, oh, ow,
                          stream())
         ctx.meta = (x.shape, x.dtype)
+        ctx.sink = _sink_of(x)
         return y
 
     @staticmethod
     def backward(ctx, dy):
         (N, C, H, W), dtype = ctx.meta
         t, p, cs = _v(dy)
-        dx = empty_act(N, C, H, W, dtype, dy.device)
-        lib.adr_bilinear_bwd(dcode(dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(dx.data_ptr()), C,
-                             dy.shape[2], dy.shape[3], 0, stream())
-        return dx, None, None
+        dx, acc = _dx_dst(ctx, (N, C, H, W), dtype, dy.device)
+        lib.adr_bilinear_bwd(dcode(dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(dx.data_ptr()),
+                             dx.stride(3), dy.shape[2], dy.shape[3], acc, stream())
+        return (None if ctx.sink is not None else dx), None, None
 
 
 def bilinear(x, oh, ow):
@@ -3051,16 +3057,17 @@ class UpsampleNearestFn(torch.autograd.Function):
         lib.adr_upsample_nearest(dcode(x.dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(yp), ycs, s,
                                  stream())
         ctx.meta = (x.shape, x.dtype, s)
+        ctx.sink = _sink_of(x)
         return y if box is None else y[:, :]
 
     @staticmethod
     def backward(ctx, dy):
         (N, C, H, W), dtype, s = ctx.meta
         t, p, cs = _v(dy.to(dtype) if dy.dtype != dtype else dy)
-        dx = empty_act(N, C, H, W, dtype, dy.device)
+        dx, acc = _dx_dst(ctx, (N, C, H, W), dtype, dy.device)
         lib.adr_upsample_nearest_bwd(dcode(dtype), ctypes.c_void_p(p), cs, N, H, W, C, ctypes.c_void_p(dx.data_ptr()),
-                                     C, s, 0, stream())
-        return dx, None, None
+                                     dx.stride(3), s, acc, stream())
+        return (None if ctx.sink is not None else dx), None, None
 
 
 def upsample_nearest(x, s, out=None):

@@ -398,11 +398,14 @@ __device__ __forceinline__ int gsrc_row(int k, int sy, int sx) {  // neighbourho
   return k < GK ? (ky + 1 - sy) * GWIN + kx + 1 - sx : GCELL;
 }
 
+// SB (CO >= 2): ONE phase-1 W_t^T slab instead of two (a second barrier per tap), so the 128- and 256-channel
+// kernels fit two workgroups per CU (LDS 74.8 / 81.5 KB instead of 82.6 / 115.3 KB)
 template <int CO>
 struct GLds {
+  static constexpr bool SB = CO >= 2;
   static constexpr int PW1 = 64 * CO + 8;                                  // phase-1 slab pitch [c][co]
   static constexpr int OMS = GCELL * 32 * 2;                               // om rows of the neighbourhood
-  static constexpr int P1X = GCELL * GXP * 2, P1W = 2 * 64 * PW1 * 2, P1D = 64 * 27 * 4;
+  static constexpr int P1X = GCELL * GXP * 2, P1W = (SB ? 1 : 2) * 64 * PW1 * 2, P1D = 64 * 27 * 4;
   static constexpr int P1 = P1X + P1W + P1D;                               // x window | W_t^T slabs | dom sums
   static constexpr int P2Y = (GCELL + 1) * GDP * 2, P2S = 64 * GSP * 2, P2W = 64 * 72 * 2;
   static constexpr int P2 = P2Y + P2S + P2W;                               // dy window | S_t | W_t slab
@@ -441,7 +444,7 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
   if (!(mode & 1)) {
     __bf16* xwin = reinterpret_cast<__bf16*>(reg);
     __bf16* slab0 = reinterpret_cast<__bf16*>(reg + L::P1X);
-    __bf16* slab1 = slab0 + 64 * L::PW1;
+    __bf16* slab1 = L::SB ? slab0 : slab0 + 64 * L::PW1;
     float* dsum = reinterpret_cast<float*>(reg + L::P1X + L::P1W);  // [pixel][tap][3]: mask, dy, dx sums
     for (int i = tid; i < 64 * 27; i += 256) dsum[i] = 0.f;
     const int pl = 16 * wave + (lane & 15);
@@ -497,7 +500,7 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
                 *reinterpret_cast<const bf16x8*>(&sl[(16 * i + (lane & 15)) * L::PW1 + 32 * k + 8 * g]), fb[k], acc[i], 0,
                 0, 0);
         }
-        if (t + 1 < 9) wstore((t & 1) ? slab0 : slab1);  // last read in tap t-1, before the barrier below
+        if (!L::SB && t + 1 < 9) wstore((t & 1) ? slab0 : slab1);  // last read in tap t-1, before the barrier below
         const float oy = (float)om_p[2 * t], ox = (float)om_p[2 * t + 1];
         const float mk = sigm((float)om_p[18 + t]);
         Corners c0;
@@ -578,6 +581,10 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
           }
         }
         __syncthreads();
+        if (L::SB && t + 1 < 9) {  // one slab: refill it after every wave's tap-t MFMAs (barrier above)
+          wstore(slab0);
+          __syncthreads();
+        }
       }
     }
     // dom rows: offsets d = m * sum(g * d sample / d p), mask logit d = sum(g * sample) * m (1 - m)
@@ -888,8 +895,8 @@ extern "C" int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs
   const int blocks = N * cdiv(H, GT) * cdiv(W, GT);
   static const int mode = getenv("ADR_DCN_BWD_MODE") ? atoi(getenv("ADR_DCN_BWD_MODE")) : 0;  // A/B: 1/2 skip a phase
   if (C == 64) hipLaunchKernelGGL((dcn_bwd_kernel<1, 1, 2>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
-  else if (C == 128) hipLaunchKernelGGL((dcn_bwd_kernel<2, 2, 1>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
-  else hipLaunchKernelGGL((dcn_bwd_kernel<4, 4, 1>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
+  else if (C == 128) hipLaunchKernelGGL((dcn_bwd_kernel<2, 2, 2>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
+  else hipLaunchKernelGGL((dcn_bwd_kernel<4, 4, 2>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
   if (int rc = check_launch("adr_dcn_bwd_bf16")) return rc;
   hipLaunchKernelGGL(dcn_far_apply_kernel, dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags);
   return check_launch("adr_dcn_bwd_bf16 (far corners)");
