@@ -9,8 +9,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+# (2, 64, 40, 40, 7) / (1, 16, 44, 36, 5): the l-scale C2PTSSA maps, whose 16-channel (bf16) / 8-channel (fp32) image
+# slab and 8-channel weight-gradient slab exceed 64 KB of LDS -> the half-width slabs of the whole-image kernels
 @pytest.mark.parametrize("N,C,H,W,k", [(4, 128, 20, 20, 7), (3, 64, 20, 20, 3), (2, 48, 17, 13, 5), (2, 256, 10, 10, 7),
-                                       (2, 32, 40, 40, 3)])
+                                       (2, 32, 40, 40, 3), (2, 64, 40, 40, 7), (1, 16, 44, 36, 5)])
 def test_dwconv_vs_torch(dtype, N, C, H, W, k):
     from adrefine import kernels as K
     torch.manual_seed(0)

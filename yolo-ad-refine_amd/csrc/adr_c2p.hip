@@ -147,10 +147,10 @@ __device__ __forceinline__ void stage_img(const T* src, int cs, int H, int W, in
 }
 
 // the padded image staged as fp32 in LDS (converted once, not per tap read): CB channels per pixel row
-template <typename T>
+template <typename T, int CBT>
 __device__ __forceinline__ void stage_img_f32(const T* src, int cs, int H, int W, int pad, int cb0, int C, int CB,
                                               float* dst) {
-  constexpr int VW = 16 / sizeof(T);
+  constexpr int VW = (int)(16 / sizeof(T)) < CBT ? (int)(16 / sizeof(T)) : CBT;  // a 4-channel slab: 8-byte bf16 reads
   const int Hp = H + 2 * pad, Wp = W + 2 * pad, nv = CB / VW;
   for (int i = threadIdx.x; i < Hp * Wp * nv; i += blockDim.x) {
     const int pp = i / nv, cv = i % nv;
@@ -248,8 +248,8 @@ __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, 
   float* xs = reinterpret_cast<float*>(dwsm);
   float* ds = xs + (long)Hp * Wp * CB;
   float* red = ds + (long)H * W * CB;  // [256][4]
-  stage_img_f32<T>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
-  stage_img_f32<T>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
+  stage_img_f32<T, CB>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
+  stage_img_f32<T, CB>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
   __syncthreads();
   const int pairs = kk * NV;
   int PS = 1;  // pixel splits per (tap, group): a power of two, so split groups never straddle a 256 pass
@@ -304,8 +304,8 @@ __global__ void __launch_bounds__(256) dw_wgrad_row_kernel(const T* x, int xcs, 
   const int Hp = H + 2 * P, Wp = W + 2 * P;
   float* xs = reinterpret_cast<float*>(dwsm);
   float* ds = xs + (long)Hp * Wp * CB;
-  stage_img_f32<T>(x + (long)n * H * W * xcs, xcs, H, W, P, cb0, C, CB, xs);
-  stage_img_f32<T>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
+  stage_img_f32<T, CB>(x + (long)n * H * W * xcs, xcs, H, W, P, cb0, C, CB, xs);
+  stage_img_f32<T, CB>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
   __syncthreads();
   constexpr int pairs = KS * NV;
   int RS = 1;  // row splits per (ky, group): a power of two <= 64 dividing 256, so a group sits in one wave
@@ -909,25 +909,43 @@ static bool dw_row_ok() {
   }
   return v != 0;
 }
-static size_t dw_img_smem(int dtype, int H, int W, int k) {  // weight-gradient kernel (fp32 copies in LDS)
-  (void)dtype;
+constexpr size_t DW_LDS_MAX = 64 * 1024;
+static size_t dw_img_smem_cb(int H, int W, int k, int cb) {  // weight-gradient kernel (fp32 copies in LDS)
   const int p = k / 2;
-  return ((size_t)(H + 2 * p) * (W + 2 * p) + (size_t)H * W) * DW_CB_WG * 4 + 256 * 16;
+  return ((size_t)(H + 2 * p) * (W + 2 * p) + (size_t)H * W) * cb * 4 + 256 * 16;
 }
-static size_t dw_fwd_smem(int dtype, int H, int W, int k) {  // forward / data-gradient kernel
+// the weight-gradient kernels' channel slab: 8, or 4 when an 8-channel image pair does not fit (the l-scale 40x40
+// maps); 0: the map is too large for the whole-image kernels
+static int dw_wg_cb(int H, int W, int k) {
+  return dw_img_smem_cb(H, W, k, DW_CB_WG) <= DW_LDS_MAX ? DW_CB_WG : dw_img_smem_cb(H, W, k, 4) <= DW_LDS_MAX ? 4 : 0;
+}
+static size_t dw_fwd_smem_cb(int dtype, int H, int W, int k, int cb) {  // forward / data-gradient kernel
   const int p = k / 2;
-  const size_t cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, es = dtype == ADR_BF16 ? 2 : 4;
+  const size_t es = dtype == ADR_BF16 ? 2 : 4;
   return (size_t)k * k * cb * 4 + (size_t)(H + 2 * p) * (W + 2 * p) * cb * es;
+}
+// the forward / data-gradient whole-image kernels' channel slab: 16 (bf16) / 8 (fp32), halved when the padded image
+// slab does not fit 64 KB of LDS (one 16-byte vector per pixel is the floor); 0: use the direct kernel
+static int dw_fwd_cb(int dtype, int H, int W, int k) {
+  const int cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, half = cb / 2;
+  return dw_fwd_smem_cb(dtype, H, W, k, cb) <= DW_LDS_MAX ? cb : dw_fwd_smem_cb(dtype, H, W, k, half) <= DW_LDS_MAX ? half : 0;
 }
 template <bool BWD>
 static void dw_img_launch(int dtype, hipStream_t st, const void* x, int xcs, const float* w, const float* b, void* y,
                           int ycs, int N, int H, int W, int C, int k, int acc) {
-  const size_t sm = dw_fwd_smem(dtype, H, W, k);
-  if (dtype == ADR_BF16)
+  const int cb = dw_fwd_cb(dtype, H, W, k);
+  const size_t sm = dw_fwd_smem_cb(dtype, H, W, k, cb);
+  if (dtype == ADR_BF16 && cb == DW_CB_BF16)
     hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
                        (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, H, W, C, k, acc);
-  else
+  else if (dtype == ADR_BF16)
+    hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, DW_CB_BF16 / 2>), dim3(N, cdiv(C, DW_CB_BF16 / 2)), dim3(256), sm,
+                       st, (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, H, W, C, k, acc);
+  else if (cb == DW_CB_F32)
     hipLaunchKernelGGL((dw_img_kernel<float, BWD, DW_CB_F32>), dim3(N, cdiv(C, DW_CB_F32)), dim3(256), sm, st,
+                       (const float*)x, xcs, w, b, (float*)y, ycs, H, W, C, k, acc);
+  else
+    hipLaunchKernelGGL((dw_img_kernel<float, BWD, DW_CB_F32 / 2>), dim3(N, cdiv(C, DW_CB_F32 / 2)), dim3(256), sm, st,
                        (const float*)x, xcs, w, b, (float*)y, ycs, H, W, C, k, acc);
 }
 
@@ -952,7 +970,7 @@ extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w,
   long total = (long)N * H * W * (C / v);
   size_t sm = (size_t)k * k * C * sizeof(float);
   ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
-  if (dw_img_ok() && dw_fwd_smem(dtype, H, W, k) <= 64 * 1024 && xcs % v == 0 && ycs % v == 0) {
+  if (dw_img_ok() && dw_fwd_cb(dtype, H, W, k) && xcs % v == 0 && ycs % v == 0) {
     dw_img_launch<false>(dtype, st, x, xcs, w, b, y, ycs, N, H, W, C, k, 0);
   } else if (dtype == ADR_BF16)
     dw_launch<__bf16, false>(k, dim3(cdiv(total, 256)), sm, st, (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, N, H, W,
@@ -964,7 +982,7 @@ extern "C" int adr_dwconv_fwd(int dtype, const void* x, int xcs, const float* w,
 }
 
 extern "C" int adr_dwconv_fwd_act_supported(int H, int W, int C, int k) {
-  return dw_img_ok() && k % 2 == 1 && C % 8 == 0 && dw_fwd_smem(ADR_BF16, H, W, k) <= 64 * 1024 ? 1 : 0;
+  return dw_img_ok() && k % 2 == 1 && C % 8 == 0 && dw_fwd_smem_cb(ADR_BF16, H, W, k, DW_CB_BF16) <= DW_LDS_MAX ? 1 : 0;
 }
 
 // Eval DWConv-BN-act (reference: Conv.forward_fuse after fuse_conv_and_bn on a depthwise Conv, nn/modules/conv.py:52-54
@@ -975,7 +993,7 @@ extern "C" int adr_dwconv_fwd_act(const void* x, int xcs, const float* w, const 
               "dwconv act: bad arguments");
   ADR_REQUIRE(adr_dwconv_fwd_act_supported(H, W, C, k), "dwconv act: H=%d W=%d C=%d k=%d not on the image kernel", H, W,
               C, k);
-  const size_t sm = dw_fwd_smem(ADR_BF16, H, W, k);
+  const size_t sm = dw_fwd_smem_cb(ADR_BF16, H, W, k, DW_CB_BF16);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL((dw_img_act_kernel<DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
                        (const __bf16*)x, xcs, w, scale, shift, act, (__bf16*)y, ycs, H, W, C, k);
@@ -999,7 +1017,7 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
   if (dx) {
     size_t sm = (size_t)k * k * C * sizeof(float);
     ADR_REQUIRE(total < (1l << 32) && sm <= 64 * 1024, "dwconv_bwd: N*H*W*C=%ld / k=%d C=%d too large", total, k, C);
-    if (dw_img_ok() && dw_fwd_smem(dtype, H, W, k) <= 64 * 1024 && dcs % v == 0 && ocs % v == 0)
+    if (dw_img_ok() && dw_fwd_cb(dtype, H, W, k) && dcs % v == 0 && ocs % v == 0)
       dw_img_launch<true>(dtype, st, dy, dcs, w, nullptr, dx, ocs, N, H, W, C, k, accumulate);
     else if (dtype == ADR_BF16)
       dw_launch<__bf16, true>(k, dim3(cdiv(total, 256)), sm, st, (const __bf16*)dy, dcs, w, nullptr, (__bf16*)dx, ocs, N,
@@ -1013,26 +1031,34 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
     long npix = (long)N * H * W;
     int chunks = cdiv(npix, 1024);
     dim3 g(chunks, k * k);
-    const size_t ism = dw_img_smem(dtype, H, W, k);
-    if (ism <= 64 * 1024 && xcs % v == 0 && dcs % v == 0) {  // small maps (the 20x20 C2PTSSA / EDFFN / Mona path): whole image in LDS
+    const int wcb = dw_wg_cb(H, W, k);
+    const size_t ism = wcb ? dw_img_smem_cb(H, W, k, wcb) : 0;
+    if (wcb && xcs % v == 0 && dcs % v == 0) {  // whole image in LDS (fp32 copies): the 20x20 / 40x40 C2PTSSA, EDFFN, Mona maps
       chunks = N;
-      const dim3 ig(N, cdiv(C, DW_CB_WG));
-      if (dtype == ADR_BF16 && dw_row_ok() && (k == 3 || k == 5 || k == 7)) {
-        if (k == 3)
-          hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, DW_CB_WG, 3>), ig, dim3(256), ism, st, (const __bf16*)x,
-                             xcs, (const __bf16*)dy, dcs, H, W, C, ws);
-        else if (k == 5)
-          hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, DW_CB_WG, 5>), ig, dim3(256), ism, st, (const __bf16*)x,
-                             xcs, (const __bf16*)dy, dcs, H, W, C, ws);
-        else
-          hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, DW_CB_WG, 7>), ig, dim3(256), ism, st, (const __bf16*)x,
-                             xcs, (const __bf16*)dy, dcs, H, W, C, ws);
-      } else if (dtype == ADR_BF16)
-        hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, DW_CB_WG>), ig, dim3(256), ism, st,
-                           (const __bf16*)x, xcs, (const __bf16*)dy, dcs, H, W, C, k, ws);
-      else
-        hipLaunchKernelGGL((dw_wgrad_img_kernel<float, DW_CB_WG>), dim3(N, cdiv(C, DW_CB_WG)), dim3(256), ism, st,
-                           (const float*)x, xcs, (const float*)dy, dcs, H, W, C, k, ws);
+      const dim3 ig(N, cdiv(C, wcb));
+#define ADR_DWWG(CBV)                                                                                                     \
+  if (dtype == ADR_BF16 && dw_row_ok() && (k == 3 || k == 5 || k == 7)) {                                              \
+    if (k == 3)                                                                                                           \
+      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 3>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,          \
+                         (const __bf16*)dy, dcs, H, W, C, ws);                                                            \
+    else if (k == 5)                                                                                                      \
+      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 5>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,          \
+                         (const __bf16*)dy, dcs, H, W, C, ws);                                                            \
+    else                                                                                                                  \
+      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 7>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,          \
+                         (const __bf16*)dy, dcs, H, W, C, ws);                                                            \
+  } else if (dtype == ADR_BF16)                                                                                           \
+    hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, CBV>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,               \
+                       (const __bf16*)dy, dcs, H, W, C, k, ws);                                                           \
+  else                                                                                                                    \
+    hipLaunchKernelGGL((dw_wgrad_img_kernel<float, CBV>), ig, dim3(256), ism, st, (const float*)x, xcs,                 \
+                       (const float*)dy, dcs, H, W, C, k, ws)
+      if (wcb == DW_CB_WG) {
+        ADR_DWWG(DW_CB_WG);
+      } else {
+        ADR_DWWG(4);
+      }
+#undef ADR_DWWG
     } else if (dtype == ADR_BF16)
       hipLaunchKernelGGL(dw_bwd_w_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dy, dcs, N,
                          H, W, C, k, 1024, ws);
