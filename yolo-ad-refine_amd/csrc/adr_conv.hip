@@ -197,8 +197,10 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
   int rows_h = a.rh, rows_w = a.rw, cy = 0, cx = 0;
   int kh0 = 0, kw0 = 0, tstep = 1, nkw = a.s, ktot = a.ktot;
   if constexpr (MODE == CV_DGRAD2) {
-    cy = blockIdx.z >> 1;
-    cx = blockIdx.z & 1;
+    // z = 0 is dispatched first: give it the class with the most taps (odd, odd: 4 of a 3x3 at pad 1), so the
+    // one-tap class's short blocks fill the tail instead of trailing behind it
+    cy = (3 - (int)blockIdx.z) >> 1;
+    cx = (3 - (int)blockIdx.z) & 1;
     rows_h = (a.rh - cy + 1) >> 1;
     rows_w = (a.rw - cx + 1) >> 1;
     kh0 = (cy + a.ph) & 1;
@@ -1171,8 +1173,9 @@ static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
                   d->pad_w == 0 && conv1_enabled();
   // forward XF runs on the streaming kernel with the plain forward's tiling (so its output and statistics rows are
   // bitwise the unfused pair's); the data-gradient XF keeps the per-tile kernel
+  // KT 256 (1 block per CU) measured a gain for DGRAD only (forward at l-scale 1280^2: 126.5 vs 126.4 ms/step)
   if (c1 && (!xf || !dgrad) && red <= (dgrad && p.bn <= 64 ? 256 : 128))
-    p.kt = red <= 64 ? 64 : red <= 128 ? 128 : 256;  // KT 256 (1 block per CU) measured a gain for DGRAD only
+    p.kt = red <= 64 ? 64 : red <= 128 ? 128 : 256;
   return p;
 }
 
