@@ -495,6 +495,10 @@ size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k);
 int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* w, void* dx, int ocs,
                    float* dw, int N, int H, int W, int C, int k, int accumulate, int dw_accumulate, float* ws,
                    size_t ws_bytes, void* stream);
+/* The weight gradient's partial rows only ([*chunks][k*k][C] floats in ws); the trainer reduces them at its
+ * deferred flush through adr_wgrad_reduce_batched (K = 1, RS = k*k, the [C][k*k] parameter layout). */
+int adr_dwconv_wgrad_partials(int dtype, const void* x, int xcs, const void* dy, int dcs, int N, int H, int W, int C,
+                              int k, float* ws, size_t ws_bytes, int* chunks, void* stream);
 /* AdaptiveDynamicTanh (:2493-2577): y = (sum_i tanh(alpha_i x) imp[n,i]) * w[c] + b[c]; imp from adr_gate_mlp. */
 int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alphas, const float* imp, const float* w,
                  const float* b, void* y, int ycs, int N, int HW, int C, void* stream);

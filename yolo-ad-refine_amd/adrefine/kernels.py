@@ -1731,10 +1731,10 @@ class GradSink:
     epilogue (Conv2dFn's dgrad) writes its input gradient here — the first one plainly, later ones accumulating —
     and hands autograd None, so FanOutFn sums one gradient fewer (per conv consumer: a 2-read + 1-write pass and a
     launch become one extra read in the dgrad epilogue). Single stream, so the order is autograd's."""
-    __slots__ = ("buf", "shape", "dtype", "pend")
+    __slots__ = ("buf", "shape", "dtype", "pend", "site")
 
     def __init__(self, shape, dtype):
-        self.buf, self.shape, self.dtype = None, tuple(shape), dtype
+        self.buf, self.shape, self.dtype, self.site = None, tuple(shape), dtype, None
         self.pend = []  # pass-through gradients (AddFn's) waiting to be folded into a conv consumer's dgrad
 
     @staticmethod
@@ -1792,6 +1792,7 @@ def _dx_dst(ctx, shape, dtype, dev):
     return empty_act(*shape, dtype, dev), 0
 
 
+FANOUT_LOG = None  # a list: FanOutFn.backward records (creation site, autograd grads, sink buf, seeded, pending)
 _FANOUT_SINK = bool(int(__import__("os").environ.get("ADR_FANOUT_SINK", "1")))
 _SEED_CAT = bool(int(__import__("os").environ.get("ADR_SEED_CAT", "1")))  # 0: CatFn hands every slice to autograd
 _DEFER_ADD = bool(int(__import__("os").environ.get("ADR_DEFER_ADD", "1")))  # 0: AddFn returns its gradient as is
@@ -1813,6 +1814,11 @@ class FanOutFn(torch.autograd.Function):
     def backward(ctx, *grads):
         gs = [g for g in grads if g is not None]
         sink = ctx.sink
+        if FANOUT_LOG is not None:  # diagnostics (scripts/ew_sites.py): what each fan-out still sums here
+            FANOUT_LOG.append((sink.site if sink is not None else "?", len(gs),
+                               sink is not None and sink.buf is not None,
+                               sink is not None and sink.buf is not None and getattr(sink.buf, "_adr_excl", False),
+                               len(sink.pend) if sink is not None else 0, tuple(gs[0].shape) if gs else None))
         if sink is not None and sink.buf is not None:  # the consumers that accumulated into the shared buffer
             # a seeded concat slice (GradSink.seed) goes first: it is the accumulation target below, so x's
             # gradient stays that slice (SplitFn can then join it with its neighbours without a copy)
@@ -1866,6 +1872,13 @@ def fanout(x, n=2):
     """n views of x whose gradients are summed by libadr (see FanOutFn); conv consumers deliver theirs through a
     shared GradSink."""
     sink = GradSink(x.shape, x.dtype) if _FANOUT_SINK else None
+    if sink is not None and FANOUT_LOG is not None:
+        import sys
+        f = sys._getframe(1)
+        while f is not None and f.f_code.co_filename == __file__:
+            f = f.f_back
+        if f is not None:
+            sink.site = f"{f.f_code.co_filename.rsplit('/', 1)[-1]}:{f.f_lineno}:{f.f_code.co_name}"
     outs = FanOutFn.apply(x, n, sink)
     if sink is not None:
         for o in outs:
@@ -2713,10 +2726,18 @@ class DWConvFn(torch.autograd.Function):
         dw, pdw, dacc = grad_dst(ctx.pw, C * k * k, x.device) if ctx.needs_input_grad[1] else (None, None, 0)
         wsb = lib.adr_dwconv_wgrad_workspace(N, H, W, C, k)
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=x.device)
+        # weight gradient into the arena: the partial rows now, their reduction batched at the deferred flush
+        # (adr_wgrad_reduce_batched with K = 1, RS = k*k: the [C][k*k] parameter layout)
+        defer = pdw is not None and dacc and _dfr() is not None and _TIMING is None and wsb <= DEFER_MAX_BYTES
         lib.adr_dwconv_bwd(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]), vd[2], fptr(wf),
                            ctypes.c_void_p(dx.data_ptr()) if dx is not None else None,
-                           dx.stride(3) if dx is not None else C, pdw, N, H, W, C, k, acc, dacc, fptr(ws), wsb,
-                           stream())
+                           dx.stride(3) if dx is not None else C, None if defer else pdw, N, H, W, C, k, acc, dacc,
+                           fptr(ws), wsb, stream())
+        if defer:
+            chunks = ctypes.c_int(0)
+            lib.adr_dwconv_wgrad_partials(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]),
+                                          vd[2], N, H, W, C, k, fptr(ws), wsb, ctypes.byref(chunks), stream())
+            _dfr().add(ws, k * k * C, chunks.value, pdw, 1, C, C, k * k, 0, dacc)
         db = _bias_grad(vd[0], C, N, H * W, vd[2], ctx.pb) if has_b and ctx.needs_input_grad[2] else None
         return (None if ctx.sink is not None else dx), grad_ret(ctx.pw, dw), db, None
 

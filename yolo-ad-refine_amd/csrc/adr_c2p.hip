@@ -1007,6 +1007,52 @@ extern "C" size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k) 
   return (size_t)chunks * k * k * C * sizeof(float);
 }
 
+// the depthwise weight gradient's partial rows [chunks][k*k][C] into ws; returns chunks (N on the whole-image path)
+static int dw_wgrad_partials(int dtype, const void* x, int xcs, const void* dy, int dcs, int N, int H, int W, int C,
+                             int k, float* ws, hipStream_t st) {
+  const int v = dtype == ADR_BF16 ? 8 : 4;
+  const long npix = (long)N * H * W;
+  const int wcb = dw_wg_cb(H, W, k);
+  if (!(wcb && xcs % v == 0 && dcs % v == 0)) {  // maps too large for LDS: the direct kernel, 1024-pixel chunks
+    const int chunks = cdiv(npix, 1024);
+    const dim3 g(chunks, k * k);
+    if (dtype == ADR_BF16)
+      hipLaunchKernelGGL(dw_bwd_w_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dy, dcs,
+                         N, H, W, C, k, 1024, ws);
+    else
+      hipLaunchKernelGGL(dw_bwd_w_kernel<float>, g, dim3(256), 0, st, (const float*)x, xcs, (const float*)dy, dcs, N,
+                         H, W, C, k, 1024, ws);
+    return chunks;
+  }
+  // whole image in LDS (fp32 copies): the 20x20 / 40x40 C2PTSSA, EDFFN, Mona maps; one partial row per image
+  const size_t ism = dw_img_smem_cb(H, W, k, wcb);
+  const dim3 ig(N, cdiv(C, wcb));
+#define ADR_DWWG(CBV)                                                                                               \
+  if (dtype == ADR_BF16 && dw_row_ok() && (k == 3 || k == 5 || k == 7)) {                                         \
+    if (k == 3)                                                                                                     \
+      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 3>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,    \
+                         (const __bf16*)dy, dcs, H, W, C, ws);                                                      \
+    else if (k == 5)                                                                                                \
+      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 5>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,    \
+                         (const __bf16*)dy, dcs, H, W, C, ws);                                                      \
+    else                                                                                                            \
+      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 7>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,    \
+                         (const __bf16*)dy, dcs, H, W, C, ws);                                                      \
+  } else if (dtype == ADR_BF16)                                                                                     \
+    hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, CBV>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,         \
+                       (const __bf16*)dy, dcs, H, W, C, k, ws);                                                     \
+  else                                                                                                              \
+    hipLaunchKernelGGL((dw_wgrad_img_kernel<float, CBV>), ig, dim3(256), ism, st, (const float*)x, xcs,           \
+                       (const float*)dy, dcs, H, W, C, k, ws)
+  if (wcb == DW_CB_WG) {
+    ADR_DWWG(DW_CB_WG);
+  } else {
+    ADR_DWWG(4);
+  }
+#undef ADR_DWWG
+  return N;
+}
+
 extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, const float* w, void* dx,
                               int ocs, float* dw, int N, int H, int W, int C, int k, int accumulate,
                               int dw_accumulate, float* ws, size_t ws_bytes, void* stream) {
@@ -1028,47 +1074,22 @@ extern "C" int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy,
   }
   if (dw) {
     ADR_REQUIRE(ws_bytes >= adr_dwconv_wgrad_workspace(N, H, W, C, k), "dwconv_bwd: workspace");
-    long npix = (long)N * H * W;
-    int chunks = cdiv(npix, 1024);
-    dim3 g(chunks, k * k);
-    const int wcb = dw_wg_cb(H, W, k);
-    const size_t ism = wcb ? dw_img_smem_cb(H, W, k, wcb) : 0;
-    if (wcb && xcs % v == 0 && dcs % v == 0) {  // whole image in LDS (fp32 copies): the 20x20 / 40x40 C2PTSSA, EDFFN, Mona maps
-      chunks = N;
-      const dim3 ig(N, cdiv(C, wcb));
-#define ADR_DWWG(CBV)                                                                                                     \
-  if (dtype == ADR_BF16 && dw_row_ok() && (k == 3 || k == 5 || k == 7)) {                                              \
-    if (k == 3)                                                                                                           \
-      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 3>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,          \
-                         (const __bf16*)dy, dcs, H, W, C, ws);                                                            \
-    else if (k == 5)                                                                                                      \
-      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 5>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,          \
-                         (const __bf16*)dy, dcs, H, W, C, ws);                                                            \
-    else                                                                                                                  \
-      hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 7>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,          \
-                         (const __bf16*)dy, dcs, H, W, C, ws);                                                            \
-  } else if (dtype == ADR_BF16)                                                                                           \
-    hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, CBV>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,               \
-                       (const __bf16*)dy, dcs, H, W, C, k, ws);                                                           \
-  else                                                                                                                    \
-    hipLaunchKernelGGL((dw_wgrad_img_kernel<float, CBV>), ig, dim3(256), ism, st, (const float*)x, xcs,                 \
-                       (const float*)dy, dcs, H, W, C, k, ws)
-      if (wcb == DW_CB_WG) {
-        ADR_DWWG(DW_CB_WG);
-      } else {
-        ADR_DWWG(4);
-      }
-#undef ADR_DWWG
-    } else if (dtype == ADR_BF16)
-      hipLaunchKernelGGL(dw_bwd_w_kernel<__bf16>, g, dim3(256), 0, st, (const __bf16*)x, xcs, (const __bf16*)dy, dcs, N,
-                         H, W, C, k, 1024, ws);
-    else
-      hipLaunchKernelGGL(dw_bwd_w_kernel<float>, g, dim3(256), 0, st, (const float*)x, xcs, (const float*)dy, dcs, N, H,
-                         W, C, k, 1024, ws);
+    const int chunks = dw_wgrad_partials(dtype, x, xcs, dy, dcs, N, H, W, C, k, ws, st);
     hipLaunchKernelGGL(dw_w_reduce_kernel, dim3(cdiv(C * k * k, 256)), dim3(256), 0, st, ws, chunks, C, k * k, dw,
                        dw_accumulate);
   }
   return check_launch("adr_dwconv_bwd");
+}
+
+// the weight-gradient partial rows only (the trainer reduces them at its deferred flush, batched with the conv
+// weight gradients: adr_wgrad_reduce_batched with K = 1, RS = k*k); returns the row count via *chunks
+extern "C" int adr_dwconv_wgrad_partials(int dtype, const void* x, int xcs, const void* dy, int dcs, int N, int H,
+                                         int W, int C, int k, float* ws, size_t ws_bytes, int* chunks, void* stream) {
+  const int v = dtype == ADR_BF16 ? 8 : 4;
+  ADR_REQUIRE(C % v == 0 && C / v <= 256 && chunks && ws, "dwconv_wgrad_partials: C=%d", C);
+  ADR_REQUIRE(ws_bytes >= adr_dwconv_wgrad_workspace(N, H, W, C, k), "dwconv_wgrad_partials: workspace");
+  *chunks = dw_wgrad_partials(dtype, x, xcs, dy, dcs, N, H, W, C, k, ws, (hipStream_t)stream);
+  return check_launch("adr_dwconv_wgrad_partials");
 }
 
 extern "C" int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alphas, const float* imp, const float* w,
