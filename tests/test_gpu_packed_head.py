@@ -58,10 +58,17 @@ def test_head_packed_matches_levels_autograd(dtype, img, tol):
     assert set(g0) == set(g1)
     # a bias feeding a training-mode BatchNorm (CoordAtt.conv1) has an exactly-zero gradient: both sides are
     # rounding noise, compared on the scale of the conv's weight gradient instead
-    zero = {"coord_attention_reg.conv1.bias": "coord_attention_reg.conv1.weight"}
-    for n, w in zero.items():
+    zero = {"coord_attention_reg.conv1.bias": ("coord_attention_reg.conv1.weight", 1e-3)}
+    # TaskDecomposition's layer-attention gate scales each image's conv output right before a GroupNorm, which is
+    # invariant to that scale: the gate's gradient (and la_conv1 / la_conv2's) is exactly zero in exact arithmetic,
+    # rounding noise in both paths (bf16: noise of the bf16 activations) — bounded against the head's conv grads
+    for d in ("cls_decomp", "reg_decomp"):
+        for q in ("la_conv1.weight", "la_conv1.bias", "la_conv2.weight", "la_conv2.bias"):
+            zero[f"{d}.{q}"] = (f"{d}.reduction_conv.conv.weight", 1e-3 if dtype == torch.float32 else 3e-2)
+    for n, (w, f) in zero.items():
         scale = float(g0[w].norm())
-        assert float(g0.pop(n).norm()) < 1e-3 * scale and float(g1.pop(n).norm()) < 1e-3 * scale
+        r0, r1 = float(g0.pop(n).norm()) / scale, float(g1.pop(n).norm()) / scale
+        assert r0 < f and r1 < f, (n, r0, r1)
     bad = {n: _rel(g1[n], g0[n]) for n in g0 if _rel(g1[n], g0[n]) > tol * 10}
     assert not bad, bad
     for n in b0:  # CoordAtt's BatchNorm: per-level batch statistics, running stats updated level by level

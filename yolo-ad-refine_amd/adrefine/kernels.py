@@ -1780,7 +1780,14 @@ class GradSink:
 def _sink_of(x):
     """The fan-out gradient sink of x when a consumer's backward can write / accumulate x's gradient into it."""
     sk = getattr(x, "_adr_sink", None)
-    return sk if sk is not None and sk.fits(x) else None
+    # the shared buffer must be a vector-aligned NHWC tensor (nhwc() would otherwise hand out a relaid copy)
+    return sk if sk is not None and sk.fits(x) and x.shape[1] % (16 // x.element_size()) == 0 else None
+
+
+def _defer_pass(sk, dy):
+    """A pass-through input gradient (res / base / addend: the op hands dy on unchanged): held in the input's
+    fan-out sink for a conv consumer's dgrad epilogue when possible (GradSink.defer); else dy for autograd."""
+    return None if sk is not None and sk.defer(dy) else dy
 
 
 def _dx_dst(ctx, shape, dtype, dev):
@@ -1795,6 +1802,7 @@ def _dx_dst(ctx, shape, dtype, dev):
 FANOUT_LOG = None  # a list: FanOutFn.backward records (creation site, autograd grads, sink buf, seeded, pending)
 _FANOUT_SINK = bool(int(__import__("os").environ.get("ADR_FANOUT_SINK", "1")))
 _SEED_CAT = bool(int(__import__("os").environ.get("ADR_SEED_CAT", "1")))  # 0: CatFn hands every slice to autograd
+_SHARE_SINK = bool(int(__import__("os").environ.get("ADR_SHARE_SINK", "1")))  # 0: every fan-out owns a sink
 _DEFER_ADD = bool(int(__import__("os").environ.get("ADR_DEFER_ADD", "1")))  # 0: AddFn returns its gradient as is
 
 
@@ -1871,8 +1879,12 @@ class FanOutFn(torch.autograd.Function):
 def fanout(x, n=2):
     """n views of x whose gradients are summed by libadr (see FanOutFn); conv consumers deliver theirs through a
     shared GradSink."""
-    sink = GradSink(x.shape, x.dtype) if _FANOUT_SINK else None
-    if sink is not None and FANOUT_LOG is not None:
+    # a fan-out of a fan-out view (a block that fans out its input, fed from an outer fan-out) shares the outer
+    # sink: consumers on both levels accumulate into one buffer (often the outer's seeded concat slice), so
+    # neither FanOutFn has a sum left to launch; each gradient still reaches the outer sum exactly once
+    outer = _sink_of(x) if _SHARE_SINK else None
+    sink = outer if outer is not None else (GradSink(x.shape, x.dtype) if _FANOUT_SINK else None)
+    if sink is not None and outer is None and FANOUT_LOG is not None:
         import sys
         f = sys._getframe(1)
         while f is not None and f.f_code.co_filename == __file__:
@@ -1954,17 +1966,18 @@ class FmaFn(torch.autograd.Function):
         out = _new_like(va[0])
         _ew(EW_FMA, (out, out.data_ptr(), out.shape[1]), va, vb, vc)
         ctx.save_for_backward(vb[0], vc[0])
+        ctx.sa, ctx.sink = getattr(a, "_adr_sink", None), _sink_of(b)  # fan-out sinks: a's pass-through, b's product
         return out
 
     @staticmethod
     def backward(ctx, dy):
         b, c = ctx.saved_tensors
         vd = _v(dy)
-        db = _new_like(b)
-        _ew(EW_MUL, (db, db.data_ptr(), db.shape[1]), vd, _v(c))
+        db, acc = _dx_dst(ctx, tuple(b.shape), b.dtype, b.device)
+        _ew(EW_MUL, _v(db), vd, _v(c), accumulate=acc)
         dc = _new_like(c)
         _ew(EW_MUL, (dc, dc.data_ptr(), dc.shape[1]), vd, _v(b))
-        return dy, db, dc
+        return _defer_pass(ctx.sa, dy), (None if ctx.sink is not None else db), dc
 
 
 def fma(a, b, c):
@@ -2025,6 +2038,7 @@ class ScaleFn(torch.autograd.Function):
         ctx.save_for_backward(vx[0], gs)
         ctx.meta = (mode, g.shape, res is not None)
         ctx.pg = g
+        ctx.sink, ctx.sres = _sink_of(x), (getattr(res, "_adr_sink", None) if res is not None else None)
         return out if box is None else out[:, :]
 
     @staticmethod
@@ -2035,10 +2049,13 @@ class ScaleFn(torch.autograd.Function):
         vd = _v(dy)
         dx = dg = None
         if ctx.needs_input_grad[0]:
-            dx = _new_like(x)
+            dx, acc = _dx_dst(ctx, (N, C, H, W), x.dtype, x.device)
+            vo = _v(dx)
             gns, gcs = {"scalar": (0, 0), "n": (1, 0), "c": (0, 1), "nc": (C, 1)}[mode]
             lib.adr_bcast_mul(dcode(x.dtype), ctypes.c_void_p(vd[1]), vd[2], fptr(gs), gns, gcs, None, 0,
-                              ctypes.c_void_p(dx.data_ptr()), C, N, H * W, C, 0, stream())
+                              ctypes.c_void_p(vo[1]), vo[2], N, H * W, C, acc, stream())
+            if ctx.sink is not None:
+                dx = None
         if ctx.needs_input_grad[1]:
             sum_n = mode in ("scalar", "c")
             sum_c = mode in ("scalar", "n")
@@ -2048,7 +2065,7 @@ class ScaleFn(torch.autograd.Function):
                 dg = sink(ctx.pg, out.view(gshape))
             else:
                 dg = sink(ctx.pg, _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape))
-        return dx, dg, (dy if has_res else None), None, None
+        return dx, dg, (_defer_pass(ctx.sres, dy) if has_res else None), None, None
 
 
 def scale(x, g, mode, res=None, out=None):
@@ -2075,6 +2092,9 @@ class WeightedSumFn(torch.autograd.Function):
         ctx.save_for_backward(wd, *[_v(x)[0] for x in xs])
         ctx.has_base = base is not None
         ctx.pw = w
+        # fan-out sinks: each x_i's scaled gradient is written (accumulated) into its sink; base's passes through
+        ctx.sinks = [_sink_of(x) for x in xs]
+        ctx.sbase = getattr(base, "_adr_sink", None) if base is not None else None
         return out
 
     @staticmethod
@@ -2082,10 +2102,10 @@ class WeightedSumFn(torch.autograd.Function):
         wd, *xs = ctx.saved_tensors
         vd = _v(dy)
         dxs = []
-        for i, x in enumerate(xs):
-            d = _new_like(x)
-            _ew(EW_AXPBY, (d, d.data_ptr(), d.shape[1]), vd, vd, ca=wd[i:i + 1], cb=_const(0.0, dy.device))
-            dxs.append(d)
+        for i, (x, sk) in enumerate(zip(xs, ctx.sinks)):
+            d, acc = sk.claim(dy.device)[:2] if sk is not None else (_new_like(x), 0)
+            _ew(EW_AXPBY, _v(d), vd, vd, ca=wd[i:i + 1], cb=_const(0.0, dy.device), accumulate=acc)
+            dxs.append(None if sk is not None else d)
         if not ctx.needs_input_grad[0]:
             dw = None
         elif all(_defer_dot(ctx.pw, x, vd[0]) for x in xs):  # the weights' scalar gradients at the flush
@@ -2094,7 +2114,7 @@ class WeightedSumFn(torch.autograd.Function):
                 _dfr().add_dotsum(x, vd[0], dw[i:i + 1])
         else:
             dw = torch.cat([_reduce_dot(x, vd[0], True, True) for x in xs])
-        return (sink(ctx.pw, dw), dy if ctx.has_base else None, *dxs)
+        return (sink(ctx.pw, dw), _defer_pass(ctx.sbase, dy) if ctx.has_base else None, *dxs)
 
 
 def weighted_sum(w, xs, base=None):
@@ -2204,6 +2224,7 @@ class MLCAFn(torch.autograd.Function):
         ctx.save_for_backward(vy[0], wlf, wgf, local, att, sig_l, sig_g)
         ctx.meta = (local_weight, res is not None, wl.shape, wg.shape)
         ctx.pwl, ctx.pwg = wl, wg
+        ctx.sres = getattr(res, "_adr_sink", None) if res is not None else None
         return out
 
     @staticmethod
@@ -2222,7 +2243,8 @@ class MLCAFn(torch.autograd.Function):
                          ctypes.c_void_p(dy.data_ptr()), C, N, H, W, C, fptr(wlf), fptr(wgf), k, float(lw),
                          fptr(local), fptr(att), fptr(sig_l), fptr(sig_g), fptr(dwl), fptr(dwg), fptr(ws), wsb,
                          stream())
-        return dy, (dout if has_res else None), sink(ctx.pwl, dwl.view(wls)), sink(ctx.pwg, dwg.view(wgs)), None
+        return dy, (_defer_pass(ctx.sres, dout) if has_res else None), sink(ctx.pwl, dwl.view(wls)), \
+            sink(ctx.pwg, dwg.view(wgs)), None
 
 
 def mlca(y, res, wl, wg, local_weight=0.5):
