@@ -60,7 +60,7 @@ class FusedPredictor:
             self._run(self.static_in)
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             self.static_out = self._run(self.static_in)
         self.graph = g
 

@@ -43,6 +43,10 @@ from .. import kernels as K
 from ..native import lib
 from .ddp import BucketReducer, cuts_for_bucket, layer_of, stage_of, staged_backward
 
+# Graph capture in thread-local mode: with a process group up (DDP, or bench.py's one-GPU RCCL leg), the RCCL
+# watchdog thread polls its work events while this thread captures; in torch's default global mode that query
+# fails the capture ("operation not permitted when stream is capturing") and takes the process down
+_CAPTURE_MODE = "thread_local"
 _NORM_TYPES = tuple(v for k, v in nn.__dict__.items() if "Norm" in k and isinstance(v, type))
 _ENTRY = np.dtype([("p", "<u8"), ("g", "<u8"), ("b", "<u8"), ("e", "<u8"), ("n", "<i8"), ("grp", "<i4"),
                    ("pad", "<i4")])
@@ -323,14 +327,14 @@ class FusedTrainer:
             t.copy_(v)
         nst = len(self.cuts) + 1
         g_stages = [torch.cuda.CUDAGraph() for _ in range(nst)]
-        cm = [torch.cuda.graph(g_stages[0])]
+        cm = [torch.cuda.graph(g_stages[0], capture_error_mode=_CAPTURE_MODE)]
         cm[0].__enter__()
         nxt = [1]
 
         def after_stage(s):  # close this stage's graph, open the next one on the same memory pool
             cm[0].__exit__(None, None, None)
             if nxt[0] < nst:
-                cm[0] = torch.cuda.graph(g_stages[nxt[0]], pool=g_stages[0].pool())
+                cm[0] = torch.cuda.graph(g_stages[nxt[0]], pool=g_stages[0].pool(), capture_error_mode=_CAPTURE_MODE)
                 nxt[0] += 1
                 cm[0].__enter__()
 
@@ -344,7 +348,7 @@ class FusedTrainer:
                     pass
             raise
         g_opt = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g_opt, pool=g_stages[0].pool()):
+        with torch.cuda.graph(g_opt, pool=g_stages[0].pool(), capture_error_mode=_CAPTURE_MODE):
             self._opt()
         self.graphs = (g_stages, g_opt, items)
         self.grad.copy_(gsaved)
