@@ -242,6 +242,11 @@ int adr_gn_param_grad(const float* partial, int N, int C, int G, const float* me
 /* z = act(x * scale + shift), scale/shift per channel or (per_sample) per (image, channel). */
 int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco, const float* scale,
                    const float* shift, int per_sample, int act, int N, int HW, int C, void* stream);
+/* z = act(x*scale+shift) + res, bitwise the adr_affine_act + adr_ew add pair (BN-act ending a residual branch:
+ * Bottleneck's x + cv2(cv1(x)), nn/modules/block.py:341-354). */
+int adr_affine_act_res(int dtype, const void* x, int xcs, int xco, const void* res, int rcs, void* z, int zcs, int zco,
+                       const float* scale, const float* shift, int per_sample, int act, int N, int HW, int C,
+                       void* stream);
 /* dx (+)= A*g + B*x + C, g = dz * act'(x*scale+shift). */
 int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, const void* dz, int dcs, int dco, void* dx,
                        int ocs, int oco, const float* scale, const float* shift, const float* A, const float* B,

@@ -223,3 +223,43 @@ def test_fwd_bnact_whole_net_step():
     assert not bad, bad[:10]
     bad = [k for k in sa if not torch.equal(sa[k], sb[k])]
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("sliced", [False, True])
+def test_bottleneck_residual_in_bnact_pass(dtype, sliced):
+    """Bottleneck's shortcut added in cv2's BN-act pass (adr_affine_act_res) against the BN-act + add pair:
+    output, input gradient and every parameter gradient bitwise equal, writing into a concat slot or not."""
+    import copy
+
+    from adrefine import kernels as K
+    from adrefine.nn.modules.block import Bottleneck
+    torch.manual_seed(1)
+    m = Bottleneck(64, 64, True, k=(3, 3), e=1.0).cuda().train()
+    with torch.no_grad():
+        for cv in (m.cv1, m.cv2):
+            cv.bn.weight.uniform_(0.5, 1.5)
+            cv.bn.bias.uniform_(-0.3, 0.3)
+    ref = copy.deepcopy(m)
+    x = torch.randn(2, 64, 20, 20, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+    g = torch.randn(2, 64, 20, 20, device="cuda").to(dtype).contiguous(memory_format=torch.channels_last)
+
+    def unfused(mod, xx, out=None):  # the pre-fusion composition: BN-act pass, then the add
+        xa, xb = K.fanout(xx)
+        return K.add(xa, mod.cv2(mod.cv1(xb, lazy=True)), out=out)
+
+    outs = []
+    for mod, fn in ((m, lambda mod, xx, out=None: mod(xx, out=out)), (ref, unfused)):
+        xx = x.detach().clone().requires_grad_(True)
+        if sliced:
+            buf = torch.zeros(2, 128, 20, 20, device="cuda", dtype=dtype).contiguous(memory_format=torch.channels_last)
+            z = fn(mod, xx, out=buf[:, 32:96])
+        else:
+            z = fn(mod, xx)
+        z.backward(g)
+        torch.cuda.synchronize()
+        outs.append((z.detach().clone(), xx.grad.clone(), [p.grad.clone() for p in mod.parameters()]))
+    (z0, dx0, p0), (z1, dx1, p1) = outs
+    assert torch.equal(z0, z1)
+    assert torch.equal(dx0, dx1)
+    assert all(torch.equal(a, b) for a, b in zip(p0, p1))

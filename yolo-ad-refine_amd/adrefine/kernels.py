@@ -1039,7 +1039,8 @@ class BNActFn(torch.autograd.Function):
     """act(BatchNorm2d(y)) — train mode uses batch statistics (from the conv epilogue when given)."""
 
     @staticmethod
-    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None, xfuse=False, lazy=False):
+    def forward(ctx, y, stats, gamma, beta, rm, rv, act, training, momentum, eps, box=None, xfuse=False, lazy=False,
+                res=None):
         dtype = y.dtype
         y, yp, ycs = nhwc(y)
         N, C, H, W = y.shape
@@ -1064,7 +1065,13 @@ class BNActFn(torch.autograd.Function):
                             fptr(beta.detach()), fptr(rm), fptr(rv), float(momentum),
                             float(eps), int(training), fptr(scale), fptr(shift), fptr(mean), fptr(rstd), stream())
         z, zp, zcs = _out_view(box, N, C, H, W, dtype, dev)
-        if lazy and box is None and BN_XF_FWD and training and dtype == torch.bfloat16 and act in ("silu", "none") \
+        ctx.sres = getattr(res, "_adr_sink", None) if res is not None else None
+        if res is not None:  # z = act(bn(y)) + res: the residual add in the same pass
+            vr = _v(res)
+            lib.adr_affine_act_res(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(vr[1]), vr[2],
+                                   ctypes.c_void_p(zp), zcs, 0, fptr(scale), fptr(shift), 0, ACT[act], N, HW, C,
+                                   stream())
+        elif lazy and box is None and BN_XF_FWD and training and dtype == torch.bfloat16 and act in ("silu", "none") \
                 and C % 8 == 0 and C <= 512:
             BnFwd(y, scale, shift, act, z).attach()  # z is written by its consumer conv (or on first other read)
         else:
@@ -1080,6 +1087,8 @@ class BNActFn(torch.autograd.Function):
         y, scale, shift, mean, rstd, gamma = ctx.saved_tensors
         act, training = ctx.meta
         dz, dzp, dzcs = nhwc(dz.to(y.dtype) if dz.dtype != y.dtype else dz)
+        # the residual's gradient is dz itself (held for a conv consumer's dgrad epilogue when its fan-out allows)
+        dres = _defer_pass(ctx.sres, dz) if ctx.needs_input_grad[13] else None
         _, yp, ycs = nhwc(y)
         N, C, H, W = y.shape
         HW = H * W
@@ -1105,7 +1114,7 @@ class BNActFn(torch.autograd.Function):
         else:
             pend.materialize(dy)
         return (dy, None, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None, None, None, None, None,
-                None, None)
+                None, None, dres)
 
 
 # Training Conv-BN-act backward fusion: BNActFn.backward computes the coefficients (nc_reduce + bn_bwd_finalize)
@@ -1570,12 +1579,12 @@ def conv_bn_act_eval(x, w, stride, pad, bn, act: str, cpad=0, out=None):
     return y if out is None else out
 
 
-def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None, xfuse=False, lazy=False):
-    """act(BatchNorm(y)). xfuse: y is a dense conv's output read only here (Conv.forward), so the backward may hand
-    its dy to that conv's data gradient unwritten (BnXf). lazy: the caller's consumer is a conv that can stage y
-    through the BN-act itself (BnFwd)."""
+def bn_act(y, stats, bn: torch.nn.Module, act: str, training: bool, out=None, xfuse=False, lazy=False, res=None):
+    """act(BatchNorm(y)) (+ res). xfuse: y is a dense conv's output read only here (Conv.forward), so the backward may
+    hand its dy to that conv's data gradient unwritten (BnXf). lazy: the caller's consumer is a conv that can stage y
+    through the BN-act itself (BnFwd). res: a residual added in the same pass (adr_affine_act_res)."""
     return BNActFn.apply(y, stats, bn.weight, bn.bias, bn.running_mean, bn.running_var, act, training, bn.momentum,
-                         bn.eps, None if out is None else OutBox(out), xfuse, lazy)
+                         bn.eps, None if out is None else OutBox(out), xfuse, lazy and res is None, res)
 
 
 def gn_act(y, gn: torch.nn.Module, act: str):

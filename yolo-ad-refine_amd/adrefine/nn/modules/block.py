@@ -35,7 +35,7 @@ class Bottleneck(nn.Module):
     def forward(self, x, out=None):
         if self.add:
             xa, xb = K.fanout(x)  # residual + branch: one HIP gradient sum instead of an autograd add
-            return K.add(xa, self.cv2(self.cv1(xb, lazy=True)), out=out)
+            return self.cv2(self.cv1(xb, lazy=True), out=out, res=xa)  # the add in cv2's BN-act pass
         return self.cv2(self.cv1(x, lazy=True), out=out)
 
 

@@ -77,9 +77,12 @@ class Conv(nn.Module):
 
     accepts_out = True  # forward(x, out=view) writes the activation into a caller's concat slice
 
-    def forward(self, x, out=None, lazy=False):
+    def forward(self, x, out=None, lazy=False, res=None):
         """lazy (training): the caller hands the output straight to a conv, which applies this BN-act while staging
-        it (kernels.BnFwd) — the output is written by that conv, not by an elementwise pass here."""
+        it (kernels.BnFwd) — the output is written by that conv, not by an elementwise pass here. res: a residual
+        added to the output (Bottleneck's shortcut) — in the BN-act pass when training, else one add."""
+        if res is not None and not (self.training and self.conv.groups == 1):
+            return K.add(res, self.forward(x, lazy=lazy), out=out)
         cv = self.conv
         if cv.groups != 1:
             k = cv.kernel_size[0]
@@ -99,7 +102,8 @@ class Conv(nn.Module):
         # training: BN partial statistics in the conv epilogue, then finalize + affine + act (or, lazily, the
         # consumer conv applies the affine + act while staging)
         y, st = K.conv2d(x, cv.weight, None, cv.stride[0], cv.padding[0], self.training, _in_pad(x, cv.weight))
-        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out, xfuse=True, lazy=lazy and out is None)
+        return K.bn_act(y, st, self.bn, self.act_name, self.training, out=out, xfuse=True, lazy=lazy and out is None,
+                        res=res)
 
     def stem_ok(self):
         """The adr_stem kernels cover Conv(3, K in {16, 32, 64}, 3, 2) with pad 1 (every yaml's model.0)."""

@@ -840,12 +840,15 @@ static size_t gnf_smem(int vec, int C, int G) {
   return (size_t)GNF_T * vec * 4 + (size_t)2 * C * 8 + (size_t)4 * C * 4 + 8 + (size_t)2 * G * 8;
 }
 
-// z = act(x * scale + shift) ; NHWC; scale/shift per channel or per (n, channel)
+// z = act(x * scale + shift) (+ res) ; NHWC; scale/shift per channel or per (n, channel). With res (a residual
+// branch: Bottleneck's x + cv2(...)) the activation is rounded to T first and the sum rounded again — bitwise the
+// affine_act + adr_ew add pair it replaces
 template <typename T, int ACT>
 __global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x, int xcs, int xco, T* __restrict__ z,
                                                          int zcs, int zco, const float* __restrict__ scale,
                                                          const float* __restrict__ shift, int per_sample, int act,
-                                                         long npix, int HW, int C) {
+                                                         long npix, int HW, int C, const T* __restrict__ res,
+                                                         int rcs) {
   constexpr int VEC = 16 / sizeof(T);
   const PixLanes L(C / VEC);
   if (!L.active) return;
@@ -869,8 +872,17 @@ __global__ void __launch_bounds__(256) affine_act_kernel(const T* __restrict__ x
     const T* e = reinterpret_cast<const T*>(&v);
     u32x4 o;
     T* oe = reinterpret_cast<T*>(&o);
+    if (res) {
+      const u32x4 rv = ld16(res + pix * rcs + c0);
+      const T* re = reinterpret_cast<const T*>(&rv);
 #pragma unroll
-    for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(bn_act_fwd_elem<ACT, sizeof(T) == 2>(to_f(e[k]), sc[k], sh[k]));
+      for (int k = 0; k < VEC; ++k)
+        oe[k] = from_f<T>(to_f(from_f<T>(bn_act_fwd_elem<ACT, sizeof(T) == 2>(to_f(e[k]), sc[k], sh[k]))) +
+                          to_f(re[k]));
+    } else {
+#pragma unroll
+      for (int k = 0; k < VEC; ++k) oe[k] = from_f<T>(bn_act_fwd_elem<ACT, sizeof(T) == 2>(to_f(e[k]), sc[k], sh[k]));
+    }
     st16(z + pix * zcs + zco + c0, o);
   }
 }
@@ -1055,12 +1067,13 @@ extern "C" int adr_gn_bwd_finalize(const float* partial, int N, int chunks, int 
   return check_launch("adr_gn_bwd_finalize");
 }
 
-extern "C" int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco,
-                              const float* scale, const float* shift, int per_sample, int act, int N, int HW, int C,
-                              void* stream) {
+static int affine_act_impl(int dtype, const void* x, int xcs, int xco, const void* res, int rcs, void* z, int zcs,
+                           int zco, const float* scale, const float* shift, int per_sample, int act, int N, int HW,
+                           int C, void* stream) {
   int vec = dtype == ADR_BF16 ? 8 : 4;
   ADR_REQUIRE(C % vec == 0 && xcs % vec == 0 && xco % vec == 0 && zcs % vec == 0 && zco % vec == 0,
               "affine_act: misaligned view (C=%d)", C);
+  ADR_REQUIRE(!res || rcs % vec == 0, "affine_act: misaligned residual view");
   long npix = (long)N * HW;
   ADR_REQUIRE(C / vec <= 256, "affine_act: C=%d too wide", C);
   int grid = grid_for(npix, C / vec);
@@ -1068,13 +1081,26 @@ extern "C" int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* 
 #define ADR_AA(A)                                                                                                   \
   if (dtype == ADR_BF16)                                                                                            \
     hipLaunchKernelGGL((affine_act_kernel<__bf16, A>), dim3(grid), dim3(256), 0, st, (const __bf16*)x, xcs, xco,    \
-                       (__bf16*)z, zcs, zco, scale, shift, per_sample, act, npix, HW, C);                           \
+                       (__bf16*)z, zcs, zco, scale, shift, per_sample, act, npix, HW, C, (const __bf16*)res, rcs);  \
   else                                                                                                              \
     hipLaunchKernelGGL((affine_act_kernel<float, A>), dim3(grid), dim3(256), 0, st, (const float*)x, xcs, xco,      \
-                       (float*)z, zcs, zco, scale, shift, per_sample, act, npix, HW, C)
+                       (float*)z, zcs, zco, scale, shift, per_sample, act, npix, HW, C, (const float*)res, rcs)
   ADR_ACT_DISPATCH(act, ADR_AA);
 #undef ADR_AA
   return check_launch("adr_affine_act");
+}
+
+extern "C" int adr_affine_act(int dtype, const void* x, int xcs, int xco, void* z, int zcs, int zco,
+                              const float* scale, const float* shift, int per_sample, int act, int N, int HW, int C,
+                              void* stream) {
+  return affine_act_impl(dtype, x, xcs, xco, nullptr, 0, z, zcs, zco, scale, shift, per_sample, act, N, HW, C, stream);
+}
+
+extern "C" int adr_affine_act_res(int dtype, const void* x, int xcs, int xco, const void* res, int rcs, void* z,
+                                  int zcs, int zco, const float* scale, const float* shift, int per_sample, int act,
+                                  int N, int HW, int C, void* stream) {
+  ADR_REQUIRE(res, "affine_act_res: residual");
+  return affine_act_impl(dtype, x, xcs, xco, res, rcs, z, zcs, zco, scale, shift, per_sample, act, N, HW, C, stream);
 }
 
 extern "C" int adr_affine_act_bwd(int dtype, const void* x, int xcs, int xco, const void* dz, int dcs, int dco,
