@@ -2217,24 +2217,24 @@ class MLCAFn(torch.autograd.Function):
     """res + MLCA(y) (block.py:1540-1594) — 3 fused kernels forward, 3 (+2 tiny) backward."""
 
     @staticmethod
-    def forward(ctx, y, res, wl, wg, local_weight):
+    def forward(ctx, y, res, wl, wg, local_weight, box=None):
         vy = _v(y)
         N, C, H, W = y.shape
         dev = y.device
         f = lambda *s: torch.empty(s, dtype=torch.float32, device=dev)  # noqa: E731
         local, att, sig_l, sig_g = f(N, 25, C), f(N, 25, C), f(N, 25 * C), f(N, C)
-        out = _new_like(vy[0])
+        out, op, ocs = _out_view(box, N, C, H, W, y.dtype, dev)  # a concat slot when the caller passes one
         vr = _v(res) if res is not None else None
         wlf, wgf = wl.detach().float().contiguous().view(-1), wg.detach().float().contiguous().view(-1)
         k = wlf.numel()
         lib.adr_mlca_fwd(dcode(y.dtype), ctypes.c_void_p(vy[1]), vy[2], ctypes.c_void_p(vr[1]) if vr else None,
-                         vr[2] if vr else 0, ctypes.c_void_p(out.data_ptr()), C, N, H, W, C, fptr(wlf), fptr(wgf), k,
+                         vr[2] if vr else 0, ctypes.c_void_p(op), ocs, N, H, W, C, fptr(wlf), fptr(wgf), k,
                          float(local_weight), fptr(local), fptr(att), fptr(sig_l), fptr(sig_g), stream())
         ctx.save_for_backward(vy[0], wlf, wgf, local, att, sig_l, sig_g)
         ctx.meta = (local_weight, res is not None, wl.shape, wg.shape)
         ctx.pwl, ctx.pwg = wl, wg
         ctx.sres = getattr(res, "_adr_sink", None) if res is not None else None
-        return out
+        return out if box is None else out[:, :]
 
     @staticmethod
     def backward(ctx, dout):
@@ -2253,11 +2253,11 @@ class MLCAFn(torch.autograd.Function):
                          fptr(local), fptr(att), fptr(sig_l), fptr(sig_g), fptr(dwl), fptr(dwg), fptr(ws), wsb,
                          stream())
         return dy, (_defer_pass(ctx.sres, dout) if has_res else None), sink(ctx.pwl, dwl.view(wls)), \
-            sink(ctx.pwg, dwg.view(wgs)), None
+            sink(ctx.pwg, dwg.view(wgs)), None, None
 
 
-def mlca(y, res, wl, wg, local_weight=0.5):
-    return MLCAFn.apply(y, res, wl, wg, local_weight)
+def mlca(y, res, wl, wg, local_weight=0.5, out=None):
+    return MLCAFn.apply(y, res, wl, wg, local_weight, None if out is None else OutBox(out))
 
 
 class AxisMeanFn(torch.autograd.Function):

@@ -77,8 +77,17 @@ class C3(nn.Module):
     accepts_out = True
 
     def forward(self, x, out=None):
+        # the last bottleneck and cv2 write straight into their halves of the concat buffer (no copies)
         xa, xb = K.fanout(x)
-        return self.cv3(K.cat([self.m(self.cv1(xa)), self.cv2(xb)]), out=out)
+        N, _, H, W = x.shape
+        c_ = self.cv1.conv.out_channels
+        buf = K.empty_act(N, 2 * c_, H, W, x.dtype, x.device)
+        *head, last = list(self.m)
+        y = self.cv1(xa)
+        for mm in head:
+            y = mm(y)
+        y = last(y, out=buf[:, :c_]) if getattr(last, "accepts_out", False) else last(y)
+        return self.cv3(K.cat([y, self.cv2(xb, out=buf[:, c_:])], out=buf), out=out)
 
 
 class C3k(C3):
@@ -135,24 +144,24 @@ class MLCA(nn.Module):
         self.conv_local = nn.Conv1d(1, 1, kernel_size=k, padding=(k - 1) // 2, bias=False)
         self.local_weight = local_weight
 
-    def forward(self, x, res=None):
-        return K.mlca(x, res, self.conv_local.weight, self.conv.weight, self.local_weight)
+    def forward(self, x, res=None, out=None):
+        return K.mlca(x, res, self.conv_local.weight, self.conv.weight, self.local_weight, out=out)
 
 
 class Bottleneck_MLCA(Bottleneck):
     """Bottleneck with MLCA on the residual branch (reference block.py:1586-1594); residual add fused."""
 
-    accepts_out = False  # the fused MLCA kernel allocates its own output
+    accepts_out = True  # the fused MLCA kernel writes its output through an `out=` view (a concat slot)
 
     def __init__(self, c1, c2, shortcut=True, g=1, k=(3, 3), e=0.5):
         super().__init__(c1, c2, shortcut, g, k, e)
         self.attention = MLCA(c2)
 
-    def forward(self, x):
+    def forward(self, x, out=None):
         if not self.add:
-            return self.attention(self.cv2(self.cv1(x, lazy=True)), None)
+            return self.attention(self.cv2(self.cv1(x, lazy=True)), None, out=out)
         xa, xb = K.fanout(x)
-        return self.attention(self.cv2(self.cv1(xa, lazy=True)), xb)
+        return self.attention(self.cv2(self.cv1(xa, lazy=True)), xb, out=out)
 
 
 class C3k_MLCA(C3k):
