@@ -340,7 +340,8 @@ int adr_cast(int src_dtype, const void* src, int dst_dtype, void* dst, long n, v
  * Elementwise glue on NHWC views (npix pixels x C channels, per-pixel channel strides).
  * op: 0 copy (torch.cat pieces, block.py:244-247) | 1 o = ca*a + cb*b (Fusion bifpn block.py:1532-1535,
  * residual adds block.py:353, Add :1448-1453) | 2 o = a*b (Multiply :1442-1447) | 3 o = a + b*c
- * (CrossTaskInteraction head.py:744-745) | 4 o = act(a) | 5 o = b*act'(a) | 6 o = a+b+c.
+ * (CrossTaskInteraction head.py:744-745) | 4 o = act(a) | 5 o = b*act'(a) | 6 o = a+b+c | 8 o = T(a*b) + c (the
+ * product rounded to the dtype first: Add(Multiply(a, b), c), bitwise the op-2 + op-1 pair).
  * ca / cb are device scalars (null = 1). accumulate: o += result. */
 int adr_ew(int dtype, int op, int act, const void* a, int acs, const void* b, int bcs, const void* c, int ccs,
            void* o, int ocs, long npix, int C, const float* ca, const float* cb, int accumulate, void* stream);

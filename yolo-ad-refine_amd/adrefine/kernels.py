@@ -1594,7 +1594,7 @@ def gn_act(y, gn: torch.nn.Module, act: str):
 # ---------------------------------------------------------------------------------------------------------
 # elementwise glue
 # ---------------------------------------------------------------------------------------------------------
-EW_COPY, EW_AXPBY, EW_MUL, EW_FMA, EW_ACT, EW_ACT_BWD, EW_ADD3, EW_ACT_BWD_OUT = range(8)
+EW_COPY, EW_AXPBY, EW_MUL, EW_FMA, EW_ACT, EW_ACT_BWD, EW_ADD3, EW_ACT_BWD_OUT, EW_MUL_ADD = range(9)
 
 
 _CONSTS = {}
@@ -1964,6 +1964,37 @@ class MulFn(torch.autograd.Function):
 
 def mul(a, b):
     return MulFn.apply(a, b)
+
+
+class MulAddFn(torch.autograd.Function):
+    """Add(Multiply(p, q), r) (block.py:1442-1453, the HS-FPN gate and its residual) in one pass (EW_MUL_ADD: the
+    product rounded to the compute dtype before the add); forward and backward bitwise MulFn + AddFn."""
+
+    @staticmethod
+    def forward(ctx, p, q, r):
+        vp, vq, vr = _v(p), _v(q), _v(r)
+        out = _new_like(vp[0])
+        _ew(EW_MUL_ADD, (out, out.data_ptr(), out.shape[1]), vp, vq, vr)
+        ctx.save_for_backward(vp[0], vq[0])
+        ctx.sr = getattr(r, "_adr_sink", None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        p, q = ctx.saved_tensors
+        vd = _v(dy)
+        dp = dq = None
+        if ctx.needs_input_grad[0]:
+            dp = _new_like(p)
+            _ew(EW_MUL, (dp, dp.data_ptr(), dp.shape[1]), vd, _v(q))
+        if ctx.needs_input_grad[1]:
+            dq = _new_like(q)
+            _ew(EW_MUL, (dq, dq.data_ptr(), dq.shape[1]), vd, _v(p))
+        return dp, dq, (_defer_pass(ctx.sr, dy) if ctx.needs_input_grad[2] else None)
+
+
+def mul_add(p, q, r):
+    return MulAddFn.apply(p, q, r)
 
 
 class FmaFn(torch.autograd.Function):

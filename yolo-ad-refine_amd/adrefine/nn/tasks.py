@@ -210,9 +210,24 @@ def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
 
     if start > 0:
         fan(start - 1, x)
-    from .modules.block import C2f, SPPF
+    from .modules.block import C2f, SPPF, Add, Multiply
     from .modules.conv import Conv
     nxt = {m.i: layers[k + 1] for k, m in enumerate(layers[:-1])}
+
+    class _MulPend:  # a Multiply whose only reader is the next layer's two-input Add: computed there as one FMA
+        __slots__ = ("a", "b")
+
+        def __init__(self, a, b):
+            self.a, self.b = a, b
+
+    def mul_into_add(m):
+        """Multiply (block.py:1442) feeding only the next layer's Add (block.py:1448) of two inputs — the HS-FPN
+        gate-and-residual pair (yaml layers 17-18, 24-25): Add(Multiply(p, q), r) in one K.mul_add pass (bitwise the
+        pair: the product rounded first)."""
+        n = nxt.get(m.i)
+        return (type(m) is Multiply and isinstance(m.f, list) and len(m.f) == 2 and n is not None and type(n) is Add
+                and isinstance(n.f, list) and len(n.f) == 2 and (-1 in n.f or m.i in n.f) and m.i not in save
+                and m.i not in cuts and (uses or {}).get(m.i, 1) == 1)
 
     def lazy_ok(m):
         """A Conv layer whose output only the next layer reads, first through a Conv on the whole tensor: the
@@ -228,7 +243,13 @@ def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
             x = take(m.f, y[m.f])
         else:
             x = [take(m.i - 1, x) if j == -1 else take(j, y[j]) for j in m.f]
-        x = m(x, lazy=True) if lazy_ok(m) else m(x)
+        if mul_into_add(m):
+            x = _MulPend(x[0], x[1])
+        elif isinstance(x, list) and any(isinstance(t, _MulPend) for t in x):
+            pm = next(t for t in x if isinstance(t, _MulPend))
+            x = K.mul_add(pm.a, pm.b, next(t for t in x if t is not pm))
+        else:
+            x = m(x, lazy=True) if lazy_ok(m) else m(x)
         y.append(x if m.i in save else None)
         if m.i in cuts:
             x = cut_live(x, y, layers, m.i, bounds)  # y[i] and x stay one leaf when they are one tensor

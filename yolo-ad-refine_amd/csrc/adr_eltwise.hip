@@ -19,8 +19,10 @@ namespace adr {
 //  6 add3          : o = a + b + c
 //  7 act_bwd_out   : o = d(=b) * act'(x) written from the OUTPUT a = act(x): relu (a > 0), sigmoid a (1 - a), as
 //                    torch's threshold_backward / sigmoid_backward
+//  8 mul_add       : o = T(a * b) + c, the product rounded to T first and no contraction — bitwise the mul + add
+//                    pair (the HS-FPN gate and residual, Multiply then Add: yaml layers 17-18, 24-25)
 enum EwOp { EW_COPY = 0, EW_AXPBY = 1, EW_MUL = 2, EW_FMA = 3, EW_ACT = 4, EW_ACT_BWD = 5, EW_ADD3 = 6,
-            EW_ACT_BWD_OUT = 7 };
+            EW_ACT_BWD_OUT = 7, EW_MUL_ADD = 8 };
 
 template <typename T>
 __global__ void __launch_bounds__(256) ew_kernel(int op, int act, const T* a, int acs, const T* b, int bcs, const T* c,
@@ -34,9 +36,10 @@ __global__ void __launch_bounds__(256) ew_kernel(int op, int act, const T* a, in
   for (long pix = (long)blockIdx.x * L.rpb + L.r0; pix < npix; pix += (long)gridDim.x * L.rpb) {
     float fa[V], fb[V], fc[V], fo[V];
     VecIO<T>::load(a + pix * acs + c0, fa);
-    if (op == EW_AXPBY || op == EW_MUL || op == EW_FMA || op == EW_ACT_BWD || op == EW_ADD3 || op == EW_ACT_BWD_OUT)
+    if (op == EW_AXPBY || op == EW_MUL || op == EW_FMA || op == EW_ACT_BWD || op == EW_ADD3 || op == EW_ACT_BWD_OUT ||
+        op == EW_MUL_ADD)
       VecIO<T>::load(b + pix * bcs + c0, fb);
-    if (op == EW_FMA || op == EW_ADD3) VecIO<T>::load(c + pix * ccs + c0, fc);
+    if (op == EW_FMA || op == EW_ADD3 || op == EW_MUL_ADD) VecIO<T>::load(c + pix * ccs + c0, fc);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       float r;
@@ -48,6 +51,7 @@ __global__ void __launch_bounds__(256) ew_kernel(int op, int act, const T* a, in
         case EW_ACT: r = act_fwd(act, fa[k]); break;
         case EW_ACT_BWD: r = fb[k] * act_bwd(act, fa[k]); break;
         case EW_ACT_BWD_OUT: r = act == 3 ? (fa[k] > 0.f ? fb[k] : 0.f) : fb[k] * ((1.f - fa[k]) * fa[k]); break;
+        case EW_MUL_ADD: r = __fadd_rn(to_f(from_f<T>(__fmul_rn(fa[k], fb[k]))), fc[k]); break;
         default: r = fa[k] + fb[k] + fc[k]; break;
       }
       fo[k] = r;
@@ -301,7 +305,7 @@ extern "C" int adr_ew(int dtype, int op, int act, const void* a, int acs, const 
   int v = dtype == ADR_BF16 ? 8 : 4;
   ADR_REQUIRE(C % v == 0 && acs % v == 0 && ocs % v == 0 && (!b || bcs % v == 0) && (!c || ccs % v == 0),
               "adr_ew: C=%d / strides must be multiples of %d", C, v);
-  ADR_REQUIRE(op >= 0 && op <= 7 && (op != 7 || act == 3 || act == 4), "adr_ew: op %d act %d", op, act);
+  ADR_REQUIRE(op >= 0 && op <= 8 && (op != 7 || act == 3 || act == 4), "adr_ew: op %d act %d", op, act);
   ADR_REQUIRE(((uintptr_t)a | (uintptr_t)o | (uintptr_t)b | (uintptr_t)c) % 16 == 0, "adr_ew: pointers not 16B aligned");
   ADR_REQUIRE(C / v <= 256, "adr_ew: C=%d too wide", C);
   int g = ew_grid(npix, C / v);
