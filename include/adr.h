@@ -641,6 +641,10 @@ size_t adr_nms_workspace(int B, int nc, int A, int multi, int max_det);
 int adr_nms(const float* y, int B, int nc, int A, float conf, float iou, int multi, int agnostic,
             const unsigned char* class_mask, int max_det, int max_nms, float max_wh, float* out, int* nout, void* ws,
             size_t ws_bytes, void* stream);
+/* Return an adr_nms workspace to its first-use state in place (zero its control words on the stream) after a call
+ * reported a grid-barrier timeout (nout < 0). The buffer is not freed, so a hipGraph that captured adr_nms on it
+ * stays valid. */
+int adr_nms_reset(void* ws, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -2,7 +2,8 @@
 the `nccl` (RCCL) backend with world_size 1 BEFORE any other GPU work, then runs the DDP-staged training step with
 real bucket all-reduces between the captured stage graphs (FusedTrainer(collectives=True)) next to the same staged
 step without collectives, and prints one JSON line: bitwise equality of parameters / EMA / loss items after each
-step, and per-step times. usage: python tests/rccl_step.py <port> <img> <bs> <steps>"""
+step, and per-step times. The collective trainer's graphs are captured while an async all_reduce is still pending
+(pending_at_capture). usage: python tests/rccl_step.py <port> <img> <bs> <steps>"""
 import json
 import os
 import sys
@@ -38,7 +39,24 @@ def main():
     for tr in trainers:
         tr.step(batches[0])
         tr.step(batches[1])
-        tr.capture(batches[2])
+        if tr.collectives:
+            # the r04t abort's condition: the graphs are captured while an async all_reduce is still in flight, so
+            # the RCCL watchdog thread queries its work event DURING the capture (global capture mode aborts there;
+            # the trainer captures in thread_local mode). A queued spin kernel keeps the collective pending.
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            torch.cuda._sleep(1 << 20)
+            e1.record()
+            torch.cuda.synchronize()
+            cycles = int((1 << 20) * 1500.0 / max(e0.elapsed_time(e1), 1e-3))  # ~1.5 s of spinning
+            torch.cuda._sleep(cycles)
+            work = dist.all_reduce(torch.ones(1 << 20, device=dev), async_op=True)
+            res["pending_at_capture"] = not work.is_completed()
+            tr.capture(batches[2])
+            res["pending_after_capture"] = not work.is_completed()
+            work.wait()
+        else:
+            tr.capture(batches[2])
     for b in batches[2:]:
         items = [tr.step(b) for tr in trainers]
         torch.cuda.synchronize()

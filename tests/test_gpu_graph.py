@@ -93,3 +93,55 @@ def test_pack_cache_matches_direct_packing():
         w = sp[0]
         kr, cr = K.pack_weight2(w, torch.bfloat16, cpad, tkc, kpad)  # no active cache here: direct pack
         assert torch.equal(kr, sp[7]) and torch.equal(cr, sp[8]), tuple(w.shape)
+
+
+def _labels_n(bs, n, seed):
+    """Exactly n boxes per image (normalised xywh, classes 0..79): the per-image target count the captured step's
+    static gt must hold."""
+    g = torch.Generator().manual_seed(seed)
+    ctr = 0.1 + 0.8 * torch.rand(bs * n, 2, generator=g)
+    wh = 0.02 + 0.2 * torch.rand(bs * n, 2, generator=g)
+    return {"batch_idx": torch.arange(bs).repeat_interleave(n).float(),
+            "cls": torch.randint(0, 80, (bs * n, 1), generator=g).float(),
+            "bboxes": torch.cat((ctr, wh), 1)}
+
+
+def test_graph_step_grows_target_capacity():
+    """A captured trainer fed batches with 7, then 93, then 7 and 93 targets per image (COCO's Poisson(7.3) counts
+    reach ~93): no error mid-training — the 93-target batch captures a 128-capacity step (capacity_bucket) and later
+    batches switch between the two captures — and every step matches the eager trainer (fp32: loss items 1e-4
+    relative, parameters and EMA within the eager-eager spread bound). Reference: utils/loss.py:392-408 pads the
+    targets per batch; trainer.py:367-398 the step loop."""
+    from adrefine.engine.trainer import FusedTrainer
+    b7 = {"img": synthetic_images(2, 320, seed=0).cuda(), **_labels_n(2, 7, seed=1)}
+    b93 = {"img": synthetic_images(2, 320, seed=5).cuda(), **_labels_n(2, 93, seed=6)}
+    seq = [b7, b7, b93, b7, b93]
+
+    def run(graph):
+        tr = _trainer()
+        out = [tr.step(seq[0]).clone()]
+        if graph:
+            tr.capture(seq[1])  # capacity 7, from the batch
+            assert tr.static_batch["gt"].shape[1] == 7
+        caps = []
+        for b in seq[1:]:
+            out.append(tr.step(b).clone())
+            if graph:
+                caps.append(tr.static_batch["gt"].shape[1])
+        torch.cuda.synchronize()
+        return tr, out, caps
+
+    e1, o1, _ = run(False)
+    e2, o2, _ = run(False)
+    g, og, caps = run(True)
+    assert caps == [7, FusedTrainer.capacity_bucket(93), 7, 128] and FusedTrainer.capacity_bucket(93) == 128
+    assert sorted(g._sets) == [7, 128]
+    for a, b, c in zip(o1, og, o2):
+        spread = float((a - c).abs().max())
+        assert float((a - b).abs().max()) <= 10 * spread + 1e-4 * float(a.abs().max()), (a, b, c)
+    spread = _pdiff(e1, e2)
+    d = _pdiff(e1, g)
+    print(f"eager-eager max |dparam| {spread:.3e}, eager-graph {d:.3e}")
+    assert d <= 10 * spread + 1e-4, (d, spread)
+    ee, eg = e1.ema_state_dict(), g.ema_state_dict()
+    assert max(float((ee[k] - eg[k]).abs().max()) for k in ee) <= 10 * spread + 1e-4

@@ -157,7 +157,6 @@ class FusedTrainer:
         bounds = [[None, None] for _ in range(nst)]
         for name, p, _, _ in self.entries:
             p._adr_grad = self.grad[off:off + p.numel()]
-            p._adr_arena, p._adr_goff = self.grad, off  # (the concurrent head levels' gradient slabs use the offset)
             p._adr_used = False
             self._goff.append(off)
             s = stage_of(layer_of(name), self.cuts)
@@ -198,6 +197,7 @@ class FusedTrainer:
         self.ema_tau = ema_tau
         self.hyper = torch.zeros(16, dtype=torch.float32, device=dev)
         self.graphs = None
+        self._sets = {}  # target capacity -> (graphs, static batch): one captured step per capacity bucket
         self.packs = K.PackCache()
 
     def _build_table(self):
@@ -271,15 +271,15 @@ class FusedTrainer:
         if opt_now:
             self._set_hyper()
         if self.graphs is not None:
-            g_stages, g_opt, items = self.graphs
             if batch is not self.static_batch:
                 b = self._prepare(batch)
+                gt = b["gt"]
+                self._select_capacity(gt.shape[1], b)  # the smallest captured target capacity that holds the batch
                 self.static_batch["img"].copy_(b["img"], non_blocking=True)
-                gt, sgt = b["gt"], self.static_batch["gt"]
-                if gt.shape[1] > sgt.shape[1]:
-                    raise RuntimeError(f"captured step holds {sgt.shape[1]} targets per image, batch has {gt.shape[1]}")
+                sgt = self.static_batch["gt"]
                 sgt.zero_()  # padded rows are masked out by the assigner (mask_gt), as the reference's own padding
                 sgt[:, :gt.shape[1]].copy_(gt, non_blocking=True)
+            g_stages, g_opt, items = self.graphs
             for i, g in enumerate(g_stages):  # stage S-1 (with the forward) first, stage 0 last
                 g.replay()
                 if reduce_now:
@@ -303,10 +303,37 @@ class FusedTrainer:
         self.ni += 1
         return items.detach()
 
+    @staticmethod
+    def capacity_bucket(n):
+        """Target capacity captured for a batch with n targets per image: the next power of two (at least 8), so a
+        real dataloader (Poisson-like label counts, up to ~100 per image on COCO) needs a handful of captures."""
+        return max(8, 1 << max(0, int(n) - 1).bit_length())
+
+    def _select_capacity(self, need, b):
+        """Activate the captured step with the smallest per-image target capacity >= need; capture one for
+        capacity_bucket(need) (from this batch) when none holds it. The reference pads targets per batch
+        (utils/loss.py:392-408); the padded rows are masked by the assigner, so the capacity does not change the
+        step's result — a larger batch never fails mid-training."""
+        if need <= self.static_batch["gt"].shape[1] and need > self._cap_floor():
+            return
+        fits = [c for c in self._sets if c >= need]
+        if fits:
+            self.graphs, self.static_batch = self._sets[min(fits)]
+            return
+        self.capture(b, max_targets=self.capacity_bucket(need))
+
+    def _cap_floor(self):
+        """Largest captured capacity below the active one (a batch above it keeps the active set)."""
+        cur = self.static_batch["gt"].shape[1]
+        lower = [c for c in self._sets if c < cur]
+        return max(lower) if lower else -1
+
     def capture(self, batch, max_targets=None):
         """Capture the step into HIP graphs. Call after at least one eager step (lazy caches, the parameter
         table). The batch becomes the graph's static input (targets padded to max_targets per image); later
-        `step(b)` copies b into it."""
+        `step(b)` copies b into it. Each capture is kept, keyed by its target capacity: step() switches to the
+        smallest one that holds a batch, and captures a larger bucket (capacity_bucket) on the first batch that
+        exceeds them all."""
         assert self.tab_dev is not None, "run one eager step before capture()"
         b = self._prepare(batch)
         gt = b["gt"]
@@ -351,6 +378,7 @@ class FusedTrainer:
         with torch.cuda.graph(g_opt, pool=g_stages[0].pool(), capture_error_mode=_CAPTURE_MODE):
             self._opt()
         self.graphs = (g_stages, g_opt, items)
+        self._sets[cap] = (self.graphs, self.static_batch)
         self.grad.copy_(gsaved)
         torch.cuda.synchronize()
         return self.static_batch

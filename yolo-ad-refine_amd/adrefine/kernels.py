@@ -1204,6 +1204,12 @@ def bnf_clear():
         p.materialize()
 
 
+def bnf_drop():
+    """Forget every pending BN-act output without writing it (a forward that raised part-way: launching their
+    affine_act later could land inside the next forward or graph capture; the entries also pin y and z)."""
+    _BNF_PENDING.clear()
+
+
 def bnxf_clear():
     """Drop pending BN-act backward entries no conv consumed (end of a backward pass)."""
     _BNXF_PENDING.clear()

@@ -318,7 +318,11 @@ class DetectionModel(nn.Module):
             raise RuntimeError("stage cut after the fused stem layer is not supported")
         if getattr(self, "_uses", None) is None:
             self._uses = consumer_counts(self.model)
-        x, bounds = route_layers(layers, self.save, x, y, first, cuts, self._uses)
+        try:
+            x, bounds = route_layers(layers, self.save, x, y, first, cuts, self._uses)
+        except BaseException:
+            K.bnf_drop()  # a failed forward: its pending BN-act outputs must not be written into a later one
+            raise
         K.bnf_clear()  # (every lazy BN-act output has been consumed; nothing may stay unwritten)
         if cuts:
             self.stage_bounds = bounds

@@ -40,7 +40,13 @@ _THR = {}
 def match_predictions(pred_classes, true_classes, iou, iouv=IOUV):
     """engine/validator.py:221-261 (greedy): (P, T) bool of correct detections, computed by adr_match_predictions from
     the (G, P) IoU matrix of one image. Thresholds are applied in float32, as the reference's comparison of a float32
-    IoU array with Python floats is."""
+    IoU array with Python floats is.
+
+    Limits, by design: P <= 2048 detections per image (the kernel keeps each detection's best label in LDS). The
+    detections come from adr_nms, which caps max_det at 300, so this path never approaches it; a larger P raises.
+    Exact IoU ties between labels go to the larger label index — what the reference's reversed ascending argsort
+    gives on small inputs; numpy's sort is not stable on large ones, so tie handling there is parity unpinned (a
+    documented deviation)."""
     dev = iou.device
     G, P = iou.shape
     T = len(iouv)

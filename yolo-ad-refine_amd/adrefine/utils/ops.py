@@ -86,7 +86,13 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
 
 def check_counts(counts, device):
     """A negative per-image count is adr_nms's report of a grid-barrier timeout (the persistent kernel's phases ran
-    out of order). Raise, and drop the workspace so the next call starts from zeroed control words."""
+    out of order). Raise, after returning the workspace to its first-use state IN PLACE (adr_nms_reset zeroes the
+    control words, sticky error flag included): the buffer is not freed, because a FusedPredictor hipGraph may have
+    captured adr_nms on it — freeing would let the allocator hand that memory to another tensor while the graph
+    still writes into it. The next call (eager or replayed) runs from zeroed control words."""
     if any(k < 0 for k in counts):
-        _WS.pop(device, None)
+        ws = _WS.get(device)
+        if ws is not None:
+            lib.adr_nms_reset(ctypes.c_void_p(ws.data_ptr()), ws.numel(), stream())
+            torch.cuda.current_stream(device).synchronize()
         raise RuntimeError("adr_nms: a grid barrier timed out (workgroups not co-resident?); detections are invalid")

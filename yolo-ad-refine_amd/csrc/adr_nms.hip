@@ -1388,6 +1388,19 @@ extern "C" size_t adr_nms_workspace(int B, int nc, int A, int multi, int max_det
   return (c.used > q.used ? c.used : q.used) + 256;
 }
 
+// After a barrier timeout (counts of -1) the control words are in an unknown state: CTL_ERR is sticky and the
+// arrival flags may be a generation apart. Zeroing them in place, on the stream, returns the workspace to its
+// first-use state without freeing it, so a hipGraph that captured adr_nms on this workspace stays valid (the next
+// launch also re-zeroes its cursors: the record word is cleared).
+extern "C" int adr_nms_reset(void* ws, size_t ws_bytes, void* stream) {
+  ADR_REQUIRE(ws && ws_bytes >= NMSP_CTL_BYTES, "nms_reset: workspace of %zu bytes", ws_bytes);
+  if (hipMemsetAsync(ws, 0, NMSP_CTL_BYTES, (hipStream_t)stream) != hipSuccess) {
+    set_error("nms_reset: hipMemsetAsync failed");
+    return ADR_ERR_LAUNCH;
+  }
+  return ADR_OK;
+}
+
 extern "C" int adr_nms(const float* y, int B, int nc, int A, float conf, float iou, int multi, int agnostic,
                        const unsigned char* class_mask, int max_det, int max_nms, float max_wh, float* out, int* nout,
                        void* ws, size_t ws_bytes, void* stream) {
