@@ -121,6 +121,23 @@ int adr_conv2d_fwd_bf16_bnact(const adr_conv_desc* d, const void* y, const void*
 int adr_conv2d_fwd_bf16_bnact_stat_tiles(const adr_conv_desc* d);
 int adr_conv2d_dgrad_bf16_bnact(const adr_conv_desc* d, const void* dz, const void* w_crsk, void* dx, int accumulate,
                                 const void* addend, int addend_cstride, const adr_bnact_xf* xf, void* stream);
+/* BN-backward statistics in the data gradient's epilogue (BSTAT). When the conv's input x was the output
+ * z = act(bn(y)) of a training BatchNorm-act and this conv was its only reader, the stored dx IS that BN's complete
+ * dz: the epilogue reads y at the same pixel / channel and writes per-tile partials (sum g, sum g * y),
+ * g = dz * act'(y * scale + shift) (bf16 arithmetic of adr_nc_reduce's backward mode), as [tiles][2][C] with
+ * tiles = adr_conv2d_dgrad_bf16_stat_tiles(d, xf != NULL); adr_bn_bwd_finalize takes them in place of the
+ * adr_nc_reduce pass. Replaces the statistics half of the BatchNorm2d backward of Conv (nn/modules/conv.py:48-50).
+ * Column c of dx is BN channel c (y, scale, shift point at channel 0); act: ADR_ACT_NONE or ADR_ACT_SILU. */
+typedef struct adr_bn_bstat {
+  const void* y;        /* the BN input, NHWC bf16 over the dx grid, channel stride y_cstride */
+  const float* scale;   /* the BN-act forward affine (adr_bn_finalize) */
+  const float* shift;
+  int y_cstride, act;
+} adr_bn_bstat;
+int adr_conv2d_dgrad_bf16_bstat(const adr_conv_desc* d, const void* dy, const void* w_crsk, void* dx, int accumulate,
+                                const void* addend, int addend_cstride, const adr_bnact_xf* xf,
+                                const adr_bn_bstat* bs, float* stats, void* stream);
+int adr_conv2d_dgrad_bf16_stat_tiles(const adr_conv_desc* d, int xf);
 /* Times x100 the XF kernel for this contraction stages each source element (column tiles x gathers per element):
  * the transform is per-staged-element VALU work, so the fusion pays only near 100. */
 int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad);

@@ -437,14 +437,37 @@ def conv_fwd_fp8(d, xp, w, Cw, Cp, bias, yp, stats):
                            fptr(bias), ctypes.c_void_p(yp), fptr(stats), stream())
 
 
-def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0, addend=None, xf=None, dy=None):
+def conv_dgrad(d, dyp, wpair, bias, dxp, accumulate=0, addend=None, xf=None, dy=None, bst=None, dx=None):
     """dx (+)= conv_transpose(dy, w) (+ addend); wpair = (KRSC, CRSK-or-None) packed weights (pack_weight2).
     `addend` (an NHWC bf16 view shaped like dx) is added in the bf16 engine's epilogue. With `xf` (a BnXf) the
     operand is the BN-act backward of xf.dz, applied while staging and side-written into `dy` (which dyp is not
-    read from)."""
+    read from). With `bst` (a BnStat: dx is the complete dz of that BN) the epilogue also writes the BN's backward
+    statistics partials (BSTAT), handed to the BnStat for its BNActFn.backward."""
     krsc, crsk = wpair
     e2 = crsk is not None and _engine2(d, d.k)
     mode = 2 if d.stride_h == 2 else 1
+    if bst is not None:
+        st = None
+        if xf is not None:
+            _, dzp, dzcs = nhwc(xf.dz)
+            d.y_cstride = dzcs
+            dyp = dzp
+            st = xf.struct(dy)
+        P = lib.adr_conv2d_dgrad_bf16_stat_tiles(ctypes.byref(d), int(xf is not None))
+        part = torch.empty(P * 2 * d.c, dtype=torch.float32, device=dx.device)
+        bs = bst.struct()
+        sym = "" if _TIMING is None else _conv2_symbol(d, 5 | (2 if xf is not None else 0))
+        tok = _t0(sym, *_conv_work(d), _shape(d, "dgrad+bstat" + ("+bnact" if xf is not None else ""))
+                  if _TIMING is not None else "")
+        lib.adr_conv2d_dgrad_bf16_bstat(ctypes.byref(d), ctypes.c_void_p(dyp), ctypes.c_void_p(crsk.data_ptr()),
+                                        ctypes.c_void_p(dxp), int(accumulate),
+                                        None if addend is None else ctypes.c_void_p(addend.data_ptr()),
+                                        0 if addend is None else addend.stride(3),
+                                        None if st is None else ctypes.byref(st), ctypes.byref(bs), fptr(part),
+                                        stream())
+        _t1(tok)
+        bst.set(part, P, dx)
+        return
     if xf is not None:
         _, dzp, dzcs = nhwc(xf.dz)
         d.y_cstride = dzcs  # the operand's view: dz (dy shares its pixel grid, written through the side output)
@@ -903,6 +926,9 @@ class Conv2dFn(torch.autograd.Function):
         ctx.sink = sink if sink is not None and sink.fits(x) else None
         dtype = x.dtype
         pend = _bnf_of(x)  # x = act(bn(y)) not written yet: stage y through the BN-act here
+        # this conv is the only reader of a lazy BN-act output: its data gradient is that BN's complete dz, so the
+        # BN's backward statistics can come from the dgrad epilogue (BnStat / BSTAT)
+        ctx.bstat = pend.bstat if pend is not None and pend.bstat is not None and not pend.bstat.shared else None
         if pend is not None and not (b is None and act is None and cpad == 0 and not CONV_FP8):
             pend.materialize()
             pend = None
@@ -982,7 +1008,9 @@ class Conv2dFn(torch.autograd.Function):
                 conv_dgrad(d2, dyp, (wp, wt), None, buf.data_ptr(), accumulate=acc, addend=add, xf=pend, dy=dy)
             else:
                 dx = empty_act(N, C, H, W, x.dtype, x.device)
-                conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr(), xf=pend, dy=dy)
+                bst = ctx.bstat if (ctx.bstat is not None and BN_BSTAT and wt is not None and _engine2(d2, d2.k)
+                                    and d2.stride_h in (1, 2) and x.dtype == torch.bfloat16) else None
+                conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr(), xf=pend, dy=dy, bst=bst, dx=dx)
         if ctx.needs_input_grad[1]:
             dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
         if has_b and ctx.needs_input_grad[2]:
@@ -1066,6 +1094,7 @@ class BNActFn(torch.autograd.Function):
                             float(eps), int(training), fptr(scale), fptr(shift), fptr(mean), fptr(rstd), stream())
         z, zp, zcs = _out_view(box, N, C, H, W, dtype, dev)
         ctx.sres = getattr(res, "_adr_sink", None) if res is not None else None
+        ctx.bstat = None
         if res is not None:  # z = act(bn(y)) + res: the residual add in the same pass
             vr = _v(res)
             lib.adr_affine_act_res(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(vr[1]), vr[2],
@@ -1073,7 +1102,10 @@ class BNActFn(torch.autograd.Function):
                                    stream())
         elif lazy and box is None and BN_XF_FWD and training and dtype == torch.bfloat16 and act in ("silu", "none") \
                 and C % 8 == 0 and C <= 512:
-            BnFwd(y, scale, shift, act, z).attach()  # z is written by its consumer conv (or on first other read)
+            # z is written by its consumer conv (or on first other read); that conv, z's only reader, also takes the
+            # BN's backward statistics in its data gradient's epilogue (BnStat)
+            ctx.bstat = BnStat(y, scale, shift, act) if BN_BSTAT else None
+            BnFwd(y, scale, shift, act, z, ctx.bstat).attach()
         else:
             lib.adr_affine_act(dcode(dtype), ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(zp), zcs, 0,
                                fptr(scale), fptr(shift), 0, ACT[act], N, HW, C, stream())
@@ -1086,6 +1118,9 @@ class BNActFn(torch.autograd.Function):
     def backward(ctx, dz):
         y, scale, shift, mean, rstd, gamma = ctx.saved_tensors
         act, training = ctx.meta
+        # the statistics partials the consumer conv's data gradient wrote with dz (BSTAT), when dz is that buffer
+        got = ctx.bstat.take(dz) if ctx.bstat is not None else None
+        ctx.bstat = None
         dz, dzp, dzcs = nhwc(dz.to(y.dtype) if dz.dtype != y.dtype else dz)
         # the residual's gradient is dz itself (held for a conv consumer's dgrad epilogue when its fan-out allows)
         dres = _defer_pass(ctx.sres, dz) if ctx.needs_input_grad[13] else None
@@ -1095,16 +1130,20 @@ class BNActFn(torch.autograd.Function):
         dev = y.device
         dt = dcode(y.dtype)
         chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
-        part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
+        part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev) if got is None else None
         f = lambda: torch.empty(C, dtype=torch.float32, device=dev)  # noqa: E731
         A, B, Cc = f(), f(), f()
         dgamma, pg, acc_g = grad_dst(gamma, C, dev)
         dbeta, pb, acc_b = grad_dst(ctx.pbeta, C, dev)
         if acc_g != acc_b:
             raise RuntimeError("BN gamma/beta gradients must share one destination kind")
-        lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
-                          fptr(shift), 0, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
-        lib.adr_bn_bwd_finalize(fptr(part), N * chunks, C, float(N * HW), fptr(mean), fptr(rstd),
+        if got is not None:
+            part, P = got
+        else:
+            P = N * chunks
+            lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
+                              fptr(shift), 0, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
+        lib.adr_bn_bwd_finalize(fptr(part), P, C, float(N * HW), fptr(mean), fptr(rstd),
                                 fptr(gamma.detach()), pg, pb, fptr(A), fptr(B), fptr(Cc), int(training), acc_g,
                                 stream())
         dy = empty_act(N, C, H, W, y.dtype, dev)
@@ -1146,11 +1185,12 @@ _BNF_PENDING = {}  # storage data_ptr -> BnFwd
 
 
 class BnFwd:
-    """A pending BN-act forward: z (allocated, unwritten) = act(y * scale + shift)."""
-    __slots__ = ("y", "scale", "shift", "act", "z", "key")
+    """A pending BN-act forward: z (allocated, unwritten) = act(y * scale + shift); bstat: the BN's BnStat."""
+    __slots__ = ("y", "scale", "shift", "act", "z", "key", "bstat")
 
-    def __init__(self, y, scale, shift, act, z):
+    def __init__(self, y, scale, shift, act, z, bstat=None):
         self.y, self.scale, self.shift, self.act, self.z = y, scale, shift, act, z
+        self.bstat = bstat
         self.key = z.untyped_storage().data_ptr()
 
     def attach(self):
@@ -1181,6 +1221,8 @@ def _bnf_settle(t):
         return
     p = _BNF_PENDING.get(key)
     if p is not None:
+        if p.bstat is not None:  # z has another reader: the consumer conv's dgrad is not its whole gradient
+            p.bstat.shared = True
         p.materialize()
 
 
@@ -1213,6 +1255,50 @@ def bnf_drop():
 def bnxf_clear():
     """Drop pending BN-act backward entries no conv consumed (end of a backward pass)."""
     _BNXF_PENDING.clear()
+
+
+# BN backward statistics in the consumer's data gradient (BSTAT): a lazy BN-act output z (kernels.BnFwd) has exactly
+# one reader, the conv that stages it, so that conv's data gradient IS the BN's complete dz. Its epilogue reads y
+# alongside and writes the (sum g, sum g * y) partials adr_nc_reduce's backward pass would (adr_conv2d_dgrad_bf16_bstat),
+# and BNActFn.backward finalizes from them: the nc_reduce launch and its read of dz and y disappear. The sums are
+# the same per-element terms in another order (fixed per geometry: deterministic). ADR_BN_BSTAT=0 disables.
+BN_BSTAT = bool(int(__import__("os").environ.get("ADR_BN_BSTAT", "1")))
+
+
+class BStatStruct(ctypes.Structure):
+    """adr_bn_bstat (include/adr.h)."""
+    _fields_ = [("y", ctypes.c_void_p), ("scale", ctypes.c_void_p), ("shift", ctypes.c_void_p),
+                ("y_cstride", ctypes.c_int), ("act", ctypes.c_int)]
+
+
+class BnStat:
+    """A training BN-act's backward statistics, taken from its only reader's data gradient: (y, scale, shift, act)
+    from the forward; after that dgrad, the partials and the identity (address, geometry, version) of the dz
+    buffer they were computed from — BNActFn.backward uses them only for exactly that, unmodified, buffer."""
+    __slots__ = ("y", "scale", "shift", "act", "shared", "part", "P", "key")
+
+    def __init__(self, y, scale, shift, act):
+        self.y, self.scale, self.shift, self.act = y, scale, shift, act
+        self.shared = False
+        self.part = self.P = self.key = None
+
+    def struct(self):
+        _, yp, ycs = nhwc(self.y)
+        return BStatStruct(yp, self.scale.data_ptr(), self.shift.data_ptr(), ycs, ACT[self.act])
+
+    @staticmethod
+    def _key(t):
+        return t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype, t._version
+
+    def set(self, part, P, dx):
+        self.part, self.P, self.key = part, P, self._key(dx)
+
+    def take(self, dz):
+        """(partials, rows) when dz is the buffer the dgrad wrote them with (else None); clears the holder."""
+        ok = self.key is not None and self._key(dz) == self.key
+        got = (self.part, self.P) if ok else None
+        self.part = self.P = self.key = None
+        return got
 
 
 class BnXfStruct(ctypes.Structure):

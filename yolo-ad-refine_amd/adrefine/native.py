@@ -106,7 +106,14 @@ def _traced(name, fn, a):
     if rc != 0:
         raise RuntimeError(f"{name}: {lib.lib.adr_last_error().decode()}")
     caller = f"{sys._getframe(2).f_code.co_name}<{sys._getframe(3).f_code.co_name}"
-    ints = tuple(v for v in a if isinstance(v, int) and not isinstance(v, bool) and abs(v) < (1 << 31))
+    ints = []
+    for v in a:  # integer arguments, and a conv descriptor's geometry (passed by reference)
+        if isinstance(v, int) and not isinstance(v, bool) and abs(v) < (1 << 31):
+            ints.append(v)
+        elif isinstance(getattr(v, "_obj", None), ConvDesc):
+            d = v._obj
+            ints += [d.n, d.h, d.w, d.c, d.x_cstride, d.k, d.r, d.s, d.stride_h]
+    ints = tuple(ints)
     OP_TRACE.append((name, caller, ints, e0, e1))
     return rc
 
@@ -115,7 +122,8 @@ _NONSTATUS = {"adr_abi_version", "adr_conv2d_fwd_stat_tiles", "adr_conv2d_fwd_bf
               "adr_opt_chunk_size", "adr_dcn_wgrad_bf16_splits", "adr_gn_fused_supported",
               "adr_fp8_amax_blocks", "adr_conv2d_fp8_supported", "adr_conv2d_fwd_fp8_stat_tiles",
               "adr_dwconv_fwd_act_supported", "adr_conv2d_bf16_xf_reuse", "adr_augment_desc_size",
-              "adr_dcn_bwd_tiles", "adr_conv2d_fwd_bf16_bnact_stat_tiles"}
+              "adr_dcn_bwd_tiles", "adr_conv2d_fwd_bf16_bnact_stat_tiles",
+              "adr_conv2d_dgrad_bf16_stat_tiles"}
 _ = _NONSTATUS
 
 lib = _Lib()

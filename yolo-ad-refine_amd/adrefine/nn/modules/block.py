@@ -49,9 +49,10 @@ class C2f(nn.Module):
         self.cv2 = Conv((2 + n) * self.c, c2, 1)
         self.m = nn.ModuleList(Bottleneck(self.c, self.c, shortcut, g, k=((3, 3), (3, 3)), e=1.0) for _ in range(n))
 
-    def forward(self, x):
+    def forward(self, x, lazy=False):
         # cv1 and every block that can write its output through an `out=` view write straight into their slice
-        # of the concat buffer, so the concat copies only the pieces of blocks that cannot (e.g. MLCA bottlenecks)
+        # of the concat buffer, so the concat copies only the pieces of blocks that cannot (e.g. MLCA bottlenecks).
+        # lazy: the caller hands the output to a conv (its only reader) — cv2's BN-act is applied by that conv
         N, _, H, W = x.shape
         c, n = self.c, len(self.m)
         buf = K.empty_act(N, (2 + n) * c, H, W, x.dtype, x.device)
@@ -60,7 +61,7 @@ class C2f(nn.Module):
             ys[-1], feed = K.fanout(ys[-1])  # used by the concat and by m: one gradient sum, in the concat slice
             slot = buf[:, (2 + i) * c:(3 + i) * c]
             ys.append(m(feed, out=slot) if getattr(m, "accepts_out", False) else m(feed))
-        return self.cv2(K.cat(ys, out=buf))
+        return self.cv2(K.cat(ys, out=buf), lazy=lazy)
 
 
 class C3(nn.Module):
@@ -118,8 +119,8 @@ class SPPF(nn.Module):
         self.cv2 = Conv(c_ * 4, c2, 1, 1)
         self.k = k
 
-    def forward(self, x):
-        # cv1 and the three pools write straight into their slices of the concat buffer (no copies)
+    def forward(self, x, lazy=False):
+        # cv1 and the three pools write straight into their slices of the concat buffer (no copies); lazy: as C2f
         N, _, H, W = x.shape
         c_ = self.cv1.conv.out_channels
         buf = K.empty_act(N, 4 * c_, H, W, x.dtype, x.device)
@@ -127,7 +128,7 @@ class SPPF(nn.Module):
         for i in range(3):
             y[-1], feed = K.fanout(y[-1])
             y.append(K.maxpool(feed, self.k, out=buf[:, (i + 1) * c_:(i + 2) * c_]))
-        return self.cv2(K.cat(y, out=buf))
+        return self.cv2(K.cat(y, out=buf), lazy=lazy)
 
 
 class MLCA(nn.Module):
@@ -463,10 +464,10 @@ class C2PSA(nn.Module):
         self.cv2 = Conv(2 * self.c, c1, 1)
         self.m = nn.Sequential(*(PSABlock(self.c, attn_ratio=0.5, num_heads=self.c // 64) for _ in range(n)))
 
-    def forward(self, x):
+    def forward(self, x, lazy=False):
         a, b = K.split(self.cv1(x), (self.c, self.c))
         b = self.m(b)
-        return self.cv2(K.cat([a, b]))
+        return self.cv2(K.cat([a, b]), lazy=lazy)  # lazy: as C2f
 
 
 class C2ProgressiveTSSA_Fusion(C2PSA):

@@ -111,10 +111,10 @@ class Conv(nn.Module):
         return (cv.in_channels == 3 and cv.out_channels in (16, 32, 64) and cv.kernel_size == (3, 3)
                 and cv.stride == (2, 2) and cv.padding == (1, 1) and cv.groups == 1 and cv.dilation == (1, 1))
 
-    def forward_image(self, img):
-        """The same Conv on the fp32 NCHW image batch, through the stem kernels (bf16 compute)."""
+    def forward_image(self, img, lazy=False):
+        """The same Conv on the fp32 NCHW image batch, through the stem kernels (bf16 compute). lazy: as forward."""
         y, st = K.stem_conv(img, self.conv.weight, self.training)
-        return K.bn_act(y, st if st.numel() else None, self.bn, self.act_name, self.training)
+        return K.bn_act(y, st if st.numel() else None, self.bn, self.act_name, self.training, lazy=lazy)
 
 
 class DWConv(Conv):

@@ -188,6 +188,18 @@ def consumer_counts(layers):
     return uses
 
 
+def lazy_pair(m, n, save, cuts, uses):
+    """Layer m ends in a Conv (a Conv row, or a C2f / C3k2 / SPPF / C2PSA block whose last op is its cv2) and only
+    the next layer n reads its output, first through a Conv on the whole tensor (a Conv row, or the cv1 of C2f /
+    SPPF / C2PSA): m's last BN-act is handed to that conv lazily — it applies the BN-act while staging
+    (kernels.BnFwd) and, being the only reader, its data gradient is the BN's whole dz (kernels.BnStat)."""
+    from .modules.block import C2f, C2PSA, SPPF
+    from .modules.conv import Conv
+    producer = type(m) is Conv or isinstance(m, (C2f, SPPF, C2PSA))
+    return (producer and m.training and n is not None and n.f == -1 and m.i not in save and m.i not in cuts and
+            (uses or {}).get(m.i, 1) == 1 and (type(n) is Conv or isinstance(n, (C2f, SPPF, C2PSA))))
+
+
 def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
     """The layer loop of _predict_once (tasks.py:155-167): each layer reads x (f == -1) or saved outputs y[f],
     and its output is kept in y when a later layer reads it. An output read by several layers is handed to each
@@ -210,8 +222,7 @@ def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
 
     if start > 0:
         fan(start - 1, x)
-    from .modules.block import C2f, SPPF, Add, Multiply
-    from .modules.conv import Conv
+    from .modules.block import Add, Multiply
     nxt = {m.i: layers[k + 1] for k, m in enumerate(layers[:-1])}
 
     class _MulPend:  # a Multiply whose only reader is the next layer's two-input Add: computed there as one FMA
@@ -230,11 +241,7 @@ def route_layers(layers, save, x, y, start=0, cuts=(), uses=None):
                 and m.i not in cuts and (uses or {}).get(m.i, 1) == 1)
 
     def lazy_ok(m):
-        """A Conv layer whose output only the next layer reads, first through a Conv on the whole tensor: the
-        consumer conv applies the BN-act while staging it (kernels.BnFwd)."""
-        n = nxt.get(m.i)
-        return (type(m) is Conv and m.training and n is not None and n.f == -1 and m.i not in save and
-                m.i not in cuts and (uses or {}).get(m.i, 1) == 1 and isinstance(n, (C2f, SPPF, Conv)))
+        return lazy_pair(m, nxt.get(m.i), save, cuts, uses)
 
     for m in layers[start:]:
         if m.f == -1:
@@ -309,7 +316,10 @@ class DetectionModel(nn.Module):
         if x.dim() == 4 and x.shape[1] == 3:
             m0 = self.model[0]
             if self.compute_dtype == torch.bfloat16 and m0.f == -1 and getattr(m0, "stem_ok", lambda: False)():
-                x = m0.forward_image(x)  # stem conv straight from the fp32 image (no NHWC copy of it)
+                if getattr(self, "_uses", None) is None:
+                    self._uses = consumer_counts(self.model)
+                lazy = len(layers) > 1 and lazy_pair(m0, layers[1], self.save, cuts, self._uses)
+                x = m0.forward_image(x, lazy=lazy)  # stem conv straight from the fp32 image (no NHWC copy of it)
                 first = 1
             else:
                 x = K.image_to_nhwc(x, self.compute_dtype, cpad=8)

@@ -63,6 +63,14 @@ struct ConvArgs {
   int xact;
   __bf16* xo;
   int xocs;
+  // BSTAT (DGRAD only, adr_conv2d_dgrad_bf16_bstat): the stored dx is the final gradient dz of a training BatchNorm-act
+  // whose input y (same pixel grid, column c = BN channel c) is read alongside in the epilogue; `stats` then receives
+  // per-tile (sum g, sum g * y), g = dz * act'(y * bs + bt) — the per-element terms of nc_reduce's backward mode —
+  // instead of (sum, sum of squares), so the BN backward needs no statistics pass over dz and y of its own
+  const __bf16* by;
+  int bycs, bact;
+  const float* bs;
+  const float* bt;
 };
 
 constexpr int CBM = 128, CBK = 64, CLD = CBK + 8;
@@ -157,8 +165,64 @@ __device__ __forceinline__ int xcd_block(int b, int nb) {
   return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
 }
 
-template <int BN, int MODE, bool EPI, int XF = XF_NONE>
+// Epilogue statistics of one stored 16-byte chunk (8 columns starting at col): (sum, sum of squares) of the stored
+// values, or with BSTAT the BatchNorm-backward terms (g, g * y) of the stored dz against the BN input y at the same
+// pixel — bn_act_g with the bf16 path's arithmetic, as nc_reduce_kernel<bf16, RED_BWD> evaluates them.
+__device__ __forceinline__ void bstat_chunk(const ConvArgs& a, u32x4 v, u32x4 yv, const float* cs, const float* ct,
+                                            float* s1, float* s2) {
+  const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+  const __bf16* ye = reinterpret_cast<const __bf16*>(&yv);
+  if (a.bact == ACT_SILU) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float yf = (float)ye[e];
+      const float g = bn_act_g<ACT_SILU, true>((float)sv[e], yf, cs[e], ct[e]);
+      s1[e] += g;
+      s2[e] += g * yf;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float yf = (float)ye[e];
+      const float g = bn_act_g<ACT_NONE, true>((float)sv[e], yf, cs[e], ct[e]);
+      s1[e] += g;
+      s2[e] += g * yf;
+    }
+  }
+}
+
+template <bool BST>
+struct EpiStats {
+  float s1[8], s2[8], cs[BST ? 8 : 1], ct[BST ? 8 : 1];
+  __device__ __forceinline__ void init(const ConvArgs& a, bool cok, int col) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
+    if constexpr (BST) {
+      if (cok) {
+        ld_coef<8>(a.bs + col, cs);
+        ld_coef<8>(a.bt + col, ct);
+      }
+    }
+  }
+  // yv: the BN input's chunk at the same pixel / columns (BSTAT; prefetched by the caller before the row loop)
+  __device__ __forceinline__ void add(const ConvArgs& a, u32x4 v, u32x4 yv) {
+    const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+    if constexpr (BST) {
+      bstat_chunk(a, v, yv, cs, ct, s1, s2);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float f = (float)sv[e];
+        s1[e] += f;
+        s2[e] += f * f;
+      }
+    }
+  }
+};
+
+template <int BN, int MODE, bool EPI, int XF = XF_NONE, bool BST = false>
 __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
+  static_assert(!BST || MODE != CV_FWD, "BSTAT: data gradients only");
   constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
   constexpr int WROWS = CBM / WAVES_M, WCOLS = BN / WAVES_N;
   constexpr int TM = WROWS / 16, TN = WCOLS / 16;
@@ -212,7 +276,16 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
   }
   constexpr int ystep = MODE == CV_DGRAD2 ? 2 : 1;
   const long Mrows = (long)a.n * rows_h * rows_w;
-  if ((long)m0 >= Mrows) return;  // block-uniform (a parity class smaller than the grid)
+  // statistics row of this tile: the row tile, and for stride-2 DGRAD the parity class's block of rows
+  const long srow = MODE == CV_DGRAD2 ? (long)blockIdx.z * (gridDim.x / a.ntiles) + mt : mt;
+  if ((long)m0 >= Mrows) {  // block-uniform (a parity class smaller than the grid): its statistics row is zero
+    if (a.stats && tid < BN && n0 + tid < a.N) {
+      float* s = a.stats + srow * 2 * a.N + n0 + tid;
+      s[0] = 0.f;
+      s[a.N] = 0.f;
+    }
+    return;
+  }
   const int hw = rows_h * rows_w;
   auto pixel_of = [&](long m) -> long {
     const long img = m / hw;
@@ -476,17 +549,26 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
         Os[(wr0 + i * 16 + 4 * (lane >> 4) + e) * OPITCH + col] = 
             (__bf16)(EPI ? epi_act(a.eact, fmaf(acc[i][j][e], es, eb)) : acc[i][j][e] + b);
   }
-  __syncthreads();
   constexpr int CPR = BN / 8;          // 16-byte chunks per row
   constexpr int RPP = 256 / CPR;       // rows per pass
+  constexpr int RPT = CBM / RPP;       // rows per thread
   const int oc = tid % CPR, orow = tid / CPR;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
   const bool col_ok = n0 + oc * 8 < a.N;
-  for (int r = orow; r < CBM; r += RPP) {
+  // BSTAT: the BN input rows of this thread's output chunks, in flight across the barrier and the LDS read-back
+  u32x4 ypre[BST ? RPT : 1];
+  if constexpr (BST) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const long m = (long)m0 + orow + k * RPP;
+      ypre[k] = (m < Mrows && col_ok) ? ld16(a.by + pixel_of(m) * a.bycs + n0 + oc * 8) : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __syncthreads();
+  EpiStats<BST> es;
+  es.init(a, col_ok, n0 + oc * 8);
+  auto out_row = [&](int r, const u32x4& yv) {
     const long m = (long)m0 + r;
-    if (m >= Mrows || !col_ok) continue;
+    if (m >= Mrows || !col_ok) return;
     u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
     const long pix = pixel_of(m);
     __bf16* dst = a.out + pix * a.ocs + a.oco + n0 + oc * 8;
@@ -505,22 +587,20 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
       for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e]);
     }
     st16(dst, v);
-    if (a.stats) {
-      const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+    if (a.stats) es.add(a, v, yv);
+  };
+  if constexpr (BST) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = (float)sv[e];
-        s1[e] += f;
-        s2[e] += f * f;
-      }
-    }
+    for (int k = 0; k < RPT; ++k) out_row(orow + k * RPP, ypre[k]);
+  } else {
+    for (int r = orow; r < CBM; r += RPP) out_row(r, ypre[0]);
   }
   if (a.stats) {  // fixed-order reduction over the row groups of each column
     __syncthreads();  // every thread is done reading the output image that `red` aliases
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[0][orow][oc * 8 + e] = s1[e];
-      red[1][orow][oc * 8 + e] = s2[e];
+      red[0][orow][oc * 8 + e] = es.s1[e];
+      red[1][orow][oc * 8 + e] = es.s2[e];
     }
     __syncthreads();
     if (tid < BN && n0 + tid < a.N) {
@@ -529,7 +609,7 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
         x1 += red[0][g][tid];
         x2 += red[1][g][tid];
       }
-      float* s = a.stats + (long)mt * 2 * a.N + n0 + tid;
+      float* s = a.stats + srow * 2 * a.N + n0 + tid;
       s[0] = x1;
       s[a.N] = x2;
     }
@@ -550,8 +630,9 @@ typedef __attribute__((ext_vector_type(2))) unsigned int u32x2c;
 // XF_FWD (adr_conv2d_fwd_bf16_bnact): the A rows are the producer BatchNorm's input y; each staged chunk becomes
 // z = act(y * s + t) (the thread's 8 reduction channels are fixed, so their coefficients live in registers) and
 // column tile 0 side-writes it once (every z element exactly once: rows are pixels).
-template <int BN, int MODE, int KT, bool EPI = false, int XF = XF_NONE>
+template <int BN, int MODE, int KT, bool EPI = false, int XF = XF_NONE, bool BST = false>
 __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
+  static_assert(!BST || MODE == CV_DGRAD, "BSTAT: data gradients only");
   static_assert(MODE == CV_FWD || MODE == CV_DGRAD, "conv1: FWD or stride-1 DGRAD");
   static_assert(XF == XF_NONE || (XF == XF_FWD && MODE == CV_FWD && !EPI), "conv1: forward XF only");
   constexpr int WAVES_N = BN >= 128 ? 2 : 1, WAVES_M = 4 / WAVES_N;
@@ -617,6 +698,13 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
   for (int e = 0; e < 8; ++e) s1[e] = s2[e] = 0.f;
   const int oc = tid % CPR, orow = tid / CPR;
   const bool col_ok = n0 + oc * 8 < a.N;
+  float bcs[BST ? 8 : 1], bct[BST ? 8 : 1];
+  if constexpr (BST) {
+    if (col_ok) {
+      ld_coef<8>(a.bs + n0 + oc * 8, bcs);
+      ld_coef<8>(a.bt + n0 + oc * 8, bct);
+    }
+  }
   const int wr0 = wm * WROWS, wc0 = wn * WCOLS;
   float bias4[TN][4], es4[EPI ? TN : 1][4];  // bias, or (EPI: eval Conv-BN-act) the affine shift + bias and scale
 #pragma unroll
@@ -682,10 +770,51 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
         *reinterpret_cast<u32x2c*>(&Os[(wr0 + 16 * i + (lane & 15)) * OPITCH + wc0 + 16 * j + 4 * (lane >> 4)]) =
             *reinterpret_cast<u32x2c*>(v);
       }
+    constexpr int RPT = CBM / RPP;
+    u32x4 ypre[BST ? RPT : 1];  // BSTAT: this thread's BN input rows, in flight across the barrier
+    if constexpr (BST) {
+#pragma unroll
+      for (int k = 0; k < RPT; ++k) {
+        const long m = (long)mt * CBM + orow + k * RPP;
+        ypre[k] = (m < Mrows && col_ok) ? ld16(a.by + m * a.bycs + n0 + oc * 8) : u32x4{0u, 0u, 0u, 0u};
+      }
+    }
     __syncthreads();  // output image complete; every wave is done with the A tile
-    for (int r = orow; r < CBM; r += RPP) {
+    if constexpr (!BST) {
+      for (int r = orow; r < CBM; r += RPP) {
+        const long m = (long)mt * CBM + r;
+        if (m >= Mrows || !col_ok) continue;
+        u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
+        __bf16* dst = a.out + m * a.ocs + a.oco + n0 + oc * 8;
+        if (MODE == CV_DGRAD && a.addend) {
+          const u32x4 q = ld16(a.addend + m * a.adcs + n0 + oc * 8);
+          const u32x4 o = a.accumulate ? ld16(dst) : u32x4{0u, 0u, 0u, 0u};
+          const __bf16 *qv = reinterpret_cast<const __bf16*>(&q), *ov = reinterpret_cast<const __bf16*>(&o);
+          __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e] + (float)qv[e]);
+        } else if (a.accumulate) {
+          const u32x4 o = ld16(dst);
+          const __bf16* ov = reinterpret_cast<const __bf16*>(&o);
+          __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e]);
+        }
+        st16(dst, v);
+        if (a.stats) {
+          const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float f = (float)sv[e];
+            s1[e] += f;
+            s2[e] += f * f;
+          }
+        }
+      }
+    } else {
+    auto out_row = [&](int r, const u32x4& yv) {
       const long m = (long)mt * CBM + r;
-      if (m >= Mrows || !col_ok) continue;
+      if (m >= Mrows || !col_ok) return;
       u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
       __bf16* dst = a.out + m * a.ocs + a.oco + n0 + oc * 8;
       if (MODE == CV_DGRAD && a.addend) {
@@ -704,13 +833,22 @@ __device__ __forceinline__ void conv1_body(const ConvArgs& a, int groups) {
       }
       st16(dst, v);
       if (a.stats) {
-        const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+        if constexpr (BST) {
+          bstat_chunk(a, v, yv, bcs, bct, s1, s2);
+        } else {
+          const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float f = (float)sv[e];
-          s1[e] += f;
-          s2[e] += f * f;
+          for (int e = 0; e < 8; ++e) {
+            const float f = (float)sv[e];
+            s1[e] += f;
+            s2[e] += f * f;
+          }
         }
+      }
+    };
+      if constexpr (BST) {
+#pragma unroll
+        for (int k = 0; k < RPT; ++k) out_row(orow + k * RPP, ypre[k]);
       }
     }
   }
@@ -751,8 +889,9 @@ __device__ __forceinline__ int c3_swz(int row, int kq) { return row * C3_LD + ((
 // WN = 2 (the wide tile, `conv3w_kernel`): 512 threads own a 256-pixel x 128-channel tile — waves 4 along M (64 rows
 // each) x 2 along N — so each staged byte of the halo and of the weight slab feeds twice the MFMA work of the
 // 128 x 64 tile: the big-channel 3x3 convs (l-scale C, K >= 128) were L2-bound at ~0.37 of the bf16 MFMA peak.
-template <int TW, bool DG, int BN, bool EPI, int XF = XF_NONE, int WN = 1>
+template <int TW, bool DG, int BN, bool EPI, int XF = XF_NONE, int WN = 1, bool BST = false>
 __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
+  static_assert(!BST || DG, "BSTAT: data gradients only");
   constexpr int NT = 256 * WN, PIX = 128 * WN;         // threads, tile pixels
   constexpr int TH = PIX / TW, HWW = TW + 2, NPIX = (TH + 2) * HWW;
   constexpr int A_TOT = NPIX * (C3_CK / 8), A_CH = (A_TOT + NT - 1) / NT;
@@ -900,15 +1039,24 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
         Os[(wr0 + i * 16 + 4 * (lane >> 4) + e) * OPITCH + col] = 
             (__bf16)(EPI ? epi_act(a.eact, fmaf(acc[i][j][e], es, eb)) : acc[i][j][e] + b);
   }
-  __syncthreads();
   const int oc = tid % CPR, orow = tid / CPR;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
   const bool col_ok = n0 + oc * 8 < a.N;
-  for (int r = orow; r < PIX; r += RPP) {
+  constexpr int RPT = PIX / RPP;
+  u32x4 ypre[BST ? RPT : 1];  // BSTAT: this thread's BN input rows, in flight across the barrier
+  if constexpr (BST) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = orow + k * RPP, y = y0 + r / TW;
+      ypre[k] = (y < H && col_ok) ? ld16(a.by + ((long)(img * H + y) * W + x0 + r % TW) * a.bycs + n0 + oc * 8)
+                                  : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __syncthreads();
+  EpiStats<BST> es;
+  es.init(a, col_ok, n0 + oc * 8);
+  auto out_row = [&](int r, const u32x4& yv) {
     const int y = y0 + r / TW;
-    if (y >= H || !col_ok) continue;
+    if (y >= H || !col_ok) return;
     u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
     const long pix = (long)(img * H + y) * W + x0 + r % TW;
     __bf16* dst = a.out + pix * a.ocs + a.oco + n0 + oc * 8;
@@ -927,22 +1075,20 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
       for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e]);
     }
     st16(dst, v);
-    if (a.stats) {
-      const __bf16* sv = reinterpret_cast<const __bf16*>(&v);
+    if (a.stats) es.add(a, v, yv);
+  };
+  if constexpr (BST) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const float f = (float)sv[e];
-        s1[e] += f;
-        s2[e] += f * f;
-      }
-    }
+    for (int k = 0; k < RPT; ++k) out_row(orow + k * RPP, ypre[k]);
+  } else {
+    for (int r = orow; r < PIX; r += RPP) out_row(r, ypre[0]);
   }
   if (a.stats) {
     __syncthreads();
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      red[0][orow][oc * 8 + e] = s1[e];
-      red[1][orow][oc * 8 + e] = s2[e];
+      red[0][orow][oc * 8 + e] = es.s1[e];
+      red[1][orow][oc * 8 + e] = es.s2[e];
     }
     __syncthreads();
     if (tid < BN && n0 + tid < a.N) {
@@ -991,6 +1137,22 @@ __global__ void __launch_bounds__(256, (XF == XF_BWD && BN == 64) ? 2 : 3) conv_
 }
 template <int TW, bool DG, int BN, int XF>
 __global__ void __launch_bounds__(256, 2) conv3_xf_kernel(ConvArgs a) { conv3_body<TW, DG, BN, false, XF>(a); }
+// BSTAT data gradients (adr_conv2d_dgrad_bf16_bstat): the same bodies with the BN-backward statistics epilogue, as
+// separate symbols so the plain kernels keep their code and register allocation
+template <int BN, int MODE, int XF>
+__global__ void __launch_bounds__(256, XF == XF_BWD ? ((BN == 64) ? 2 : 3) : (BN <= 64 ? 4 : 2))
+    conv_bf16_bst_kernel(ConvArgs a) {
+  conv_bf16_body<BN, MODE, false, XF, true>(a);
+}
+template <int BN, int KT>
+__global__ void __launch_bounds__(256, KT == 256 ? 1 : (KT == 64 && BN <= 64) ? 3 : 2) conv1_bst_kernel(ConvArgs a, int groups) {
+  conv1_body<BN, CV_DGRAD, KT, false, XF_NONE, true>(a, groups);
+}
+template <int TW, int BN, int XF>
+__global__ void __launch_bounds__(256, XF == XF_NONE ? 3 : 2) conv3_bst_kernel(ConvArgs a) {
+  conv3_body<TW, true, BN, false, XF, 1, true>(a);
+}
+__global__ void __launch_bounds__(512, 1) conv3w_bst_kernel(ConvArgs a) { conv3_body<16, true, 128, false, XF_NONE, 2, true>(a); }
 
 // tile width of the 3x3 path for this geometry, or 0 when it does not apply
 static int conv3_tw(const adr_conv_desc* d, int red_ch, int out_ch) {
@@ -1012,6 +1174,30 @@ static bool conv3_wide(const adr_conv_desc* d, int tw, int red_ch, int out_ch) {
 }
 template <bool DG>
 static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hipStream_t st, bool wide = false) {
+  if (DG && g.by) {  // BSTAT data gradient
+    if constexpr (!DG) return;
+    if (wide) {
+      g.ntiles = g.N / 128;
+      hipLaunchKernelGGL(conv3w_bst_kernel, dim3(conv3_tiles(d, 16, 256) * g.ntiles), dim3(512), 0, st, g);
+      return;
+    }
+    g.ntiles = g.N / bn;
+    dim3 grid(conv3_tiles(d, tw) * g.ntiles);
+#define ADR_C3B(TW_, BN_)                                                                                   \
+  do {                                                                                                      \
+    if (g.xs) hipLaunchKernelGGL((conv3_bst_kernel<TW_, BN_, XF_BWD>), grid, dim3(256), 0, st, g);          \
+    else hipLaunchKernelGGL((conv3_bst_kernel<TW_, BN_, XF_NONE>), grid, dim3(256), 0, st, g);              \
+  } while (0)
+    if (bn == 64) {
+      if (tw == 16) ADR_C3B(16, 64);
+      else ADR_C3B(8, 64);
+    } else {
+      if (tw == 16) ADR_C3B(16, 32);
+      else ADR_C3B(8, 32);
+    }
+#undef ADR_C3B
+    return;
+  }
   if (wide) {
     g.ntiles = g.N / 128;
     dim3 grid(conv3_tiles(d, 16, 256) * g.ntiles);
@@ -1053,6 +1239,23 @@ static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hi
 
 template <int MODE>
 static void launch_conv(int bn, dim3 grid, const ConvArgs& g, hipStream_t st) {
+  if constexpr (MODE != CV_FWD) {
+    if (g.by) {  // BSTAT data gradient (XF: bn <= 64)
+#define ADR_CB(BN_)                                                                                         \
+  do {                                                                                                      \
+    if (g.xs) hipLaunchKernelGGL((conv_bf16_bst_kernel<BN_, MODE, XF_BWD>), grid, dim3(256), 0, st, g);     \
+    else hipLaunchKernelGGL((conv_bf16_bst_kernel<BN_, MODE, XF_NONE>), grid, dim3(256), 0, st, g);         \
+  } while (0)
+      switch (bn) {
+        case 16: ADR_CB(16); break;
+        case 32: ADR_CB(32); break;
+        case 64: ADR_CB(64); break;
+        default: hipLaunchKernelGGL((conv_bf16_bst_kernel<128, MODE, XF_NONE>), grid, dim3(256), 0, st, g); break;
+      }
+#undef ADR_CB
+      return;
+    }
+  }
   if (g.xs) {  // XF (bn <= 64)
     constexpr int XF = MODE == CV_FWD ? XF_FWD : XF_BWD;
     switch (bn) {
@@ -1100,7 +1303,9 @@ static void launch_conv1(int bn, int kt, long rows, ConvArgs& g, hipStream_t st)
   const dim3 grid(groups * g.ntiles);
 #define ADR_C1(BN, KT)                                                                                     \
   do {                                                                                                     \
-    if (MODE == CV_FWD && g.escale)                                                                        \
+    if (MODE == CV_DGRAD && g.by)                                                                          \
+      hipLaunchKernelGGL((conv1_bst_kernel<BN, KT>), grid, dim3(256), 0, st, g, groups);                   \
+    else if (MODE == CV_FWD && g.escale)                                                                   \
       hipLaunchKernelGGL((conv1_act_kernel<BN, KT>), grid, dim3(256), 0, st, g, groups);                   \
     else if (MODE == CV_FWD && g.xs)                                                                       \
       hipLaunchKernelGGL((conv1_xf_kernel<BN, KT>), grid, dim3(256), 0, st, g, groups);                    \
@@ -1254,7 +1459,8 @@ extern "C" int adr_conv2d_fwd_bf16_act(const adr_conv_desc* d, const void* x, co
 
 static int conv_dgrad_impl(const adr_conv_desc* d, const void* dy, const void* w_crsk, const float* bias, void* dx,
                            int accumulate, const void* addend, int adcs, void* stream,
-                           const adr_bnact_xf* xf = nullptr) {
+                           const adr_bnact_xf* xf = nullptr, const adr_bn_bstat* bst = nullptr,
+                           float* stats = nullptr) {
   int rc = conv_check(d);
   if (rc) return rc;
   ConvArgs g{};
@@ -1262,7 +1468,17 @@ static int conv_dgrad_impl(const adr_conv_desc* d, const void* dy, const void* w
     rc = xf_args(xf, true, d->k, d->n, d->ho, d->wo, g);
     if (rc) return rc;
   }
-  g.src = (const __bf16*)dy; g.wt = (const __bf16*)w_crsk; g.out = (__bf16*)dx; g.bias = bias; g.stats = nullptr;
+  if (bst) {
+    ADR_REQUIRE(stats && bst->y && bst->scale && bst->shift && (bst->act == ACT_NONE || bst->act == ACT_SILU),
+                "conv dgrad bstat: stats / y / scale / shift / act (none or silu)");
+    ADR_REQUIRE(bst->y_cstride >= d->c && bst->y_cstride % 8 == 0 && ((uintptr_t)bst->y & 15) == 0 &&
+                    ((uintptr_t)bst->scale & 15) == 0 && ((uintptr_t)bst->shift & 15) == 0,
+                "conv dgrad bstat: 16-byte aligned y view / coefficients");
+    ADR_REQUIRE((long)d->n * d->h * d->w * bst->y_cstride < (1l << 30), "conv dgrad bstat: y exceeds 2^30 elements");
+    g.by = (const __bf16*)bst->y; g.bycs = bst->y_cstride; g.bact = bst->act; g.bs = bst->scale; g.bt = bst->shift;
+  }
+  g.src = (const __bf16*)dy; g.wt = (const __bf16*)w_crsk; g.out = (__bf16*)dx; g.bias = bias;
+  g.stats = bst ? stats : nullptr;
   g.addend = (const __bf16*)addend; g.adcs = adcs;
   g.n = d->n; g.sh_ = d->ho; g.sw_ = d->wo; g.scs = d->y_cstride; g.sco = d->y_coff; g.sc = d->k;
   g.rh = d->h; g.rw = d->w; g.ocs = d->x_cstride; g.oco = d->x_coff;
@@ -1317,6 +1533,21 @@ extern "C" int adr_conv2d_dgrad_bf16_bnact(const adr_conv_desc* d, const void* d
   return conv_dgrad_impl(d, dz, w_crsk, nullptr, dx, accumulate, addend, addend_cstride, stream, xf);
 }
 
+// Any of the data gradients above (plain / + addend / XF), whose stored dx is the final gradient dz of a training
+// BatchNorm-act (the conv's input was that BN's output, with no other reader): the epilogue also reads the BN input y
+// and writes per-tile (sum g, sum g * y) partials — adr_nc_reduce's backward statistics — to stats
+// ([adr_conv2d_dgrad_bf16_stat_tiles][2][C]), so adr_bn_bwd_finalize runs on them without a pass over dz and y.
+extern "C" int adr_conv2d_dgrad_bf16_bstat(const adr_conv_desc* d, const void* dy, const void* w_crsk, void* dx,
+                                           int accumulate, const void* addend, int addend_cstride,
+                                           const adr_bnact_xf* xf, const adr_bn_bstat* bs, float* stats,
+                                           void* stream) {
+  ADR_REQUIRE(bs, "conv dgrad bstat: bs");
+  if (addend)
+    ADR_REQUIRE(addend_cstride >= d->c && addend_cstride % 8 == 0 && ((uintptr_t)addend & 15) == 0,
+                "conv dgrad bstat: addend view");
+  return conv_dgrad_impl(d, dy, w_crsk, nullptr, dx, accumulate, addend, addend_cstride, stream, xf, bs, stats);
+}
+
 // The forward counterpart: the conv's input is a training BatchNorm's input y; z = act(y * scale + shift) is
 // applied while staging (0 in the zero padding) and side-written once to xf->out. Replaces adr_affine_act +
 // adr_conv2d_fwd_bf16 (stats as adr_conv2d_fwd_bf16).
@@ -1349,13 +1580,35 @@ static int fwd_stat_tiles(const adr_conv_desc* d, bool xf) {
 
 extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) { return fwd_stat_tiles(d, false); }
 
+// statistics rows of adr_conv2d_dgrad_bf16_bstat (xf: with the XF operand transform)
+extern "C" int adr_conv2d_dgrad_bf16_stat_tiles(const adr_conv_desc* d, int xf) {
+  const ConvPlan pl = conv_plan(d, true, xf != 0);
+  if (pl.mode == CV_DGRAD2) return 4 * cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM);
+  if (pl.tw) return pl.wide ? conv3_tiles(d, 16, 256) : conv3_tiles(d, pl.tw);
+  if (pl.kt) return conv1_groups((long)d->n * d->h * d->w, cdiv(d->c, pl.bn), pl.kt, pl.bn);
+  return cdiv((long)d->n * d->h * d->w, CBM);
+}
+
 // statistics rows of adr_conv2d_fwd_bf16_bnact (its kernel choice can differ from the plain forward's)
 extern "C" int adr_conv2d_fwd_bf16_bnact_stat_tiles(const adr_conv_desc* d) { return fwd_stat_tiles(d, true); }
 
 extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, char* buf, int len) {
   ADR_REQUIRE(d && buf && len >= 64, "conv kernel symbol: bad arguments");
   const bool dg = (dgrad & 1) != 0, xf = (dgrad & 2) != 0;  // bit 1: the BN-act (XF) variant
+  const bool bst = dg && (dgrad & 4) != 0;                     // bit 2: the BSTAT data gradient
   const ConvPlan pl = conv_plan(d, dg, xf);
+  if (bst) {
+    if (pl.tw && pl.wide && !xf)
+      snprintf(buf, len, "_ZN3adr17conv3w_bst_kernelENS_8ConvArgsE");
+    else if (pl.tw)
+      snprintf(buf, len, "_ZN3adr16conv3_bst_kernelILi%dELi%dELi%dEEEvNS_8ConvArgsE", pl.tw, pl.bn, xf ? XF_BWD : XF_NONE);
+    else if (pl.kt && !xf)
+      snprintf(buf, len, "_ZN3adr16conv1_bst_kernelILi%dELi%dEEEvNS_8ConvArgsEi", pl.bn, pl.kt);
+    else
+      snprintf(buf, len, "_ZN3adr20conv_bf16_bst_kernelILi%dELi%dELi%dEEEvNS_8ConvArgsE", pl.bn, pl.mode,
+               xf ? XF_BWD : XF_NONE);
+    return ADR_OK;
+  }
   if (xf && pl.tw)
     snprintf(buf, len, "_ZN3adr15conv3_xf_kernelILi%dELb%dELi%dELi%dEEEvNS_8ConvArgsE", pl.tw, dg ? 1 : 0, pl.bn,
              dg ? XF_BWD : XF_FWD);
