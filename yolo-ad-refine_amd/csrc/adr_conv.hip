@@ -1104,6 +1104,237 @@ __device__ __forceinline__ void conv3_body(const ConvArgs& a) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// 3x3 / stride-2 / pad-1 DATA GRADIENT on super-pixel halo tiles (DG2H; also nn.ConvTranspose2d(k3, s2, p1) forward).
+// dx pixel (2i + py, 2j + px) of output class (py, px) reads dy only at (i + di, j + dj), di, dj in {0, 1}: class
+// (0,0) one tap (kh, kw) = (1,1); (0,1) taps (1,0) / (1,2) at dj = 1 / 0; (1,0) taps (0,1) / (2,1) at di = 1 / 0;
+// (1,1) the four corners. A block owns an 8 x TJ tile of super-pixels (i, j) — the 16 x 2TJ dx pixels of all four
+// classes — and BN output channels. Per 32-channel chunk of dy it stages the 9 x (TJ+1) dy halo and the 9-tap weight
+// slab in LDS ONCE and runs every (class, tap) out of LDS: each dy element is staged ~(9 (TJ+1)) / (8 TJ) times per
+// column tile, against once per (class, tap) gather in the per-class implicit GEMM (conv_bf16_kernel<BN,
+// CV_DGRAD2>), and the four classes share one launch and one weight slab. Wave w owns super-pixels 16 w .. 16 w + 15
+// in all four classes: 4 + 2 + 2 + 1 = 9 (fragment, tap) MFMA units per 32-channel chunk for every wave, four
+// accumulator sets, no cross-wave sums.
+constexpr int G2_TI = 8, G2_TJ = 8;  // super-pixel tile rows; columns of the launched tile
+template <int TJ>
+struct G2Geo {
+  static constexpr int NT = 32 * TJ, W = NT / 64;             // threads, waves (= fragments per class)
+  static constexpr int HW = TJ + 1, NPIX = (G2_TI + 1) * HW;  // halo
+  static constexpr int PIX = 4 * G2_TI * TJ;                  // dx pixels per tile (16 x 2TJ)
+};
+// tap q of class c: weight tap index kh * 3 + kw and the dy offsets (di, dj)
+__device__ __forceinline__ void g2_tap(int c, int q, int& t, int& di, int& dj) {
+  const int py = c >> 1, px = c & 1;
+  const int kh = py ? ((c == 3 ? (q >> 1) : q) ? 2 : 0) : 1;
+  const int kw = px ? ((c == 3 ? (q & 1) : q) ? 2 : 0) : 1;
+  t = kh * 3 + kw;
+  di = py && kh == 0;
+  dj = px && kw == 0;
+}
+
+template <int TJ, int BN, int XF, bool BST>
+__device__ __forceinline__ void dg2_body(const ConvArgs& a) {
+  using G = G2Geo<TJ>;
+  constexpr int NT = G::NT, W = G::W, HW = G::HW, NPIX = G::NPIX, PIX = G::PIX, DXW = 2 * TJ;
+  constexpr int A_TOT = NPIX * (C3_CK / 8), A_CH = (A_TOT + NT - 1) / NT;
+  constexpr int B_TOT = 9 * BN * (C3_CK / 8), B_CH = (B_TOT + NT - 1) / NT;
+  constexpr int TN = BN / 16, NS = 4;  // column fragments; accumulator sets (one per output class)
+  constexpr int OPITCH = BN + 8, CPR = BN / 8, RPP = NT / CPR, RPT = PIX / RPP;
+  constexpr int SMEM_A = NPIX * C3_LD, SMEM_B = 9 * BN * C3_LD;
+  constexpr int SMEM_AB = 2 * (SMEM_A + SMEM_B), SMEM_O = 2 * PIX * OPITCH, SMEM_R = 2 * RPP * BN * 4;
+  constexpr int SMEM_BYTES = SMEM_AB > SMEM_O ? (SMEM_AB > SMEM_R ? SMEM_AB : SMEM_R) : (SMEM_O > SMEM_R ? SMEM_O : SMEM_R);
+  __shared__ __attribute__((aligned(16))) unsigned char lds_raw[SMEM_BYTES];
+  __bf16* As = reinterpret_cast<__bf16*>(lds_raw);
+  __bf16* Bs = As + SMEM_A;
+  float (*red)[RPP][BN] = reinterpret_cast<float (*)[RPP][BN]>(lds_raw);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int Ho = a.sh_, Wo = a.sw_, H = a.rh, Wd = a.rw;  // dy grid, dx image
+  const int tx = (Wo + TJ - 1) / TJ, ty = (Ho + G2_TI - 1) / G2_TI;
+  const int bid = xcd_block(blockIdx.x, gridDim.x);
+  const int mt = bid / a.ntiles, nt = bid - mt * a.ntiles;
+  const int n0 = nt * BN;
+  const int img = mt / (tx * ty), trem = mt - img * (tx * ty);
+  const int i0 = (trem / tx) * G2_TI, j0 = (trem - (trem / tx) * tx) * TJ;
+
+  // halo chunks of this thread: e = tid + NT i -> halo cell e / 4 (dy pixel (i0 + cell / HW, j0 + cell % HW)),
+  // channel quad e % 4
+  constexpr unsigned OOR = 0x7FFFFFF0u;
+  const __amdgpu_buffer_rsrc_t src_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.src, (short)0, a.src_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wt_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.wt, (short)0, a.wt_bytes, 0x00020000);
+  int a_off[A_CH], a_pix[A_CH];
+  unsigned a_in = 0;  // XF: halo cells inside the tile (their dy pixel's unique writer)
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int e = tid + NT * i, q = e >> 2, hy = q / HW, hx = q - (q / HW) * HW;
+    const int gy = i0 + hy, gx = j0 + hx;
+    const bool ok = e < A_TOT && gy < Ho && gx < Wo;
+    a_pix[i] = ok ? (img * Ho + gy) * Wo + gx : -1;
+    a_off[i] = ok ? a_pix[i] * a.scs + a.sco + (e & 3) * 8 : -1;
+    a_in |= (unsigned)(ok && hy < G2_TI && hx < TJ) << i;
+  }
+  constexpr int XTAB = XF == XF_BWD ? 5 * XMAXC : 4;
+  __shared__ __attribute__((aligned(16))) float xtab[XTAB];
+  if constexpr (XF != XF_NONE) xf_table<XF>(a, xtab);
+  const __amdgpu_buffer_rsrc_t xy_rs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.xy, (short)0, XF == XF_BWD ? a.xy_bytes : 0, 0x00020000);
+  constexpr int XA = XF == XF_BWD ? A_CH : 1;
+  u32x4 ry[XA];
+  const int xq = (tid & 3) * 8;  // this thread's channels within a chunk step
+  // weight slab rows: q = tid + NT i -> row q / 4 = tap * BN + col, channel quad q % 4 (CRSK: [c][tap][k])
+  int b_off[B_CH];
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) {
+    const int q = tid + NT * i, row = q >> 2, tap = row / BN, col = row - tap * BN;
+    b_off[i] = (q < B_TOT && n0 + col < a.N) ? (n0 + col) * 9 * a.sc + tap * a.sc + (q & 3) * 8 : -1;
+  }
+
+  u32x4 ra[A_CH], rb[B_CH];
+  auto load = [&](int c0) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(src_rs, a_off[i] >= 0 ? (unsigned)(a_off[i] + c0) * 2u : OOR, 0, 0);
+      if constexpr (XF == XF_BWD)
+        ry[i] = __builtin_amdgcn_raw_buffer_load_b128(
+            xy_rs, a_pix[i] >= 0 ? (unsigned)(a_pix[i] * a.xycs + c0 + xq) * 2u : OOR, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i)
+      rb[i] = __builtin_amdgcn_raw_buffer_load_b128(wt_rs, b_off[i] >= 0 ? (unsigned)(b_off[i] + c0) * 2u : OOR, 0, 0);
+  };
+  auto store = [&](int c0) {
+    XfCoef<XF == XF_NONE ? XF_FWD : XF> xk;
+    if constexpr (XF != XF_NONE) xk.load(xtab, c0 + xq);
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int e = tid + NT * i;
+      if constexpr (XF == XF_NONE) {
+        if (e < A_TOT) st16(&As[c3_swz(e >> 2, e & 3)], ra[i]);
+      } else {
+        u32x4 v = {0u, 0u, 0u, 0u};
+        if (a_pix[i] >= 0) v = xf_chunk<XF>(ra[i], ry[XF == XF_BWD ? i : 0], xk, a.xact);
+        if (nt == 0 && ((a_in >> i) & 1)) st16(a.xo + (long)a_pix[i] * a.xocs + c0 + xq, v);
+        if (e < A_TOT) st16(&As[c3_swz(e >> 2, e & 3)], v);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int q = tid + NT * i;
+      if (q < B_TOT) st16(&Bs[c3_swz(q >> 2, q & 3)], rb[i]);
+    }
+  };
+
+  // accumulator set c = output class (2 py + px) of this wave's 16 super-pixels; the lane's fragment row's halo cell
+  const int sp_row = 16 * wave + (lane & 15);  // super-pixel index in the tile (row-major, TJ per row)
+  const int cell0 = (sp_row / TJ) * HW + (sp_row % TJ);
+  const int kq = lane >> 4;
+  f32x4 acc[NS][TN];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[s][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int nch = a.sc / C3_CK;
+  load(0);
+  for (int ch = 0; ch < nch; ++ch) {
+    store(ch * C3_CK);
+    __syncthreads();
+    if (ch + 1 < nch) load((ch + 1) * C3_CK);
+#pragma unroll
+    for (int c = 0; c < NS; ++c) {
+#pragma unroll
+      for (int q = 0; q < (c == 3 ? 4 : c == 0 ? 1 : 2); ++q) {
+        int t, di, dj;
+        g2_tap(c, q, t, di, dj);
+        const int s = c;
+        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(&As[c3_swz(cell0 + di * HW + dj, kq)]);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const bf16x8 fb = *reinterpret_cast<const bf16x8*>(&Bs[c3_swz(t * BN + 16 * j + (lane & 15), kq)]);
+          acc[s][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb, acc[s][j], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- epilogue: bf16 image of the 16 x 2TJ dx tile in LDS, 16-byte row stores, optional statistics ----
+  __bf16* Os = reinterpret_cast<__bf16*>(lds_raw);
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    const int c = s, py = c >> 1, px = c & 1, f = wave;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = 16 * j + (lane & 15);
+      const float b = (a.bias && n0 + col < a.N) ? a.bias[n0 + col] : 0.f;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int sp = 16 * f + 4 * (lane >> 4) + e;
+        const int ly = 2 * (sp / TJ) + py, lx = 2 * (sp % TJ) + px;
+        Os[(ly * DXW + lx) * OPITCH + col] = (__bf16)(acc[s][j][e] + b);
+      }
+    }
+  }
+  const int oc = tid % CPR, orow = tid / CPR;
+  const bool col_ok = n0 + oc * 8 < a.N;
+  const int y0 = 2 * i0, x0 = 2 * j0;
+  u32x4 ypre[BST ? RPT : 1];  // BSTAT: this thread's BN input rows, in flight across the barrier
+  if constexpr (BST) {
+#pragma unroll
+    for (int k = 0; k < RPT; ++k) {
+      const int r = orow + k * RPP, y = y0 + r / DXW, x = x0 + r % DXW;
+      ypre[k] = (y < H && x < Wd && col_ok) ? ld16(a.by + ((long)(img * H + y) * Wd + x) * a.bycs + n0 + oc * 8)
+                                           : u32x4{0u, 0u, 0u, 0u};
+    }
+  }
+  __syncthreads();
+  EpiStats<BST> es;
+  es.init(a, col_ok, n0 + oc * 8);
+#pragma unroll
+  for (int k = 0; k < RPT; ++k) {
+    const int r = orow + k * RPP, y = y0 + r / DXW, x = x0 + r % DXW;
+    if (y >= H || x >= Wd || !col_ok) continue;
+    u32x4 v = *reinterpret_cast<const u32x4*>(&Os[r * OPITCH + oc * 8]);
+    const long pix = (long)(img * H + y) * Wd + x;
+    __bf16* dst = a.out + pix * a.ocs + a.oco + n0 + oc * 8;
+    if (a.addend) {
+      const u32x4 qv4 = ld16(a.addend + pix * a.adcs + n0 + oc * 8);
+      const u32x4 o = a.accumulate ? ld16(dst) : u32x4{0u, 0u, 0u, 0u};
+      const __bf16 *qv = reinterpret_cast<const __bf16*>(&qv4), *ov = reinterpret_cast<const __bf16*>(&o);
+      __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e] + (float)qv[e]);
+    } else if (a.accumulate) {
+      const u32x4 o = ld16(dst);
+      const __bf16* ov = reinterpret_cast<const __bf16*>(&o);
+      __bf16* nv = reinterpret_cast<__bf16*>(&v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) nv[e] = (__bf16)((float)nv[e] + (float)ov[e]);
+    }
+    st16(dst, v);
+    if (a.stats) es.add(a, v, ypre[BST ? k : 0]);
+  }
+  if (a.stats) {
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[0][orow][oc * 8 + e] = es.s1[e];
+      red[1][orow][oc * 8 + e] = es.s2[e];
+    }
+    __syncthreads();
+    if (tid < BN && n0 + tid < a.N) {
+      float x1 = 0.f, x2 = 0.f;
+      for (int g = 0; g < RPP; ++g) {
+        x1 += red[0][g][tid];
+        x2 += red[1][g][tid];
+      }
+      float* sp = a.stats + (long)mt * 2 * a.N + n0 + tid;
+      sp[0] = x1;
+      sp[a.N] = x2;
+    }
+  }
+}
+
 // entry points (the bodies are shared; the eval Conv-BN-act variants are separate symbols so the training
 // kernels keep their code and register allocation)
 template <int BN, int MODE>
@@ -1137,6 +1368,11 @@ __global__ void __launch_bounds__(256, (XF == XF_BWD && BN == 64) ? 2 : 3) conv_
 }
 template <int TW, bool DG, int BN, int XF>
 __global__ void __launch_bounds__(256, 2) conv3_xf_kernel(ConvArgs a) { conv3_body<TW, DG, BN, false, XF>(a); }
+// stride-2 3x3 data gradient on super-pixel halo tiles (plain / XF backward operand / BSTAT epilogue)
+template <int TJ, int BN, int XF, bool BST>
+__global__ void __launch_bounds__(32 * TJ, (XF == XF_BWD && BN == 64) ? 2 : 3) dg2_kernel(ConvArgs a) {
+  dg2_body<TJ, BN, XF, BST>(a);
+}
 // BSTAT data gradients (adr_conv2d_dgrad_bf16_bstat): the same bodies with the BN-backward statistics epilogue, as
 // separate symbols so the plain kernels keep their code and register allocation
 template <int BN, int MODE, int XF>
@@ -1235,6 +1471,25 @@ static void launch_conv3(int tw, int bn, const adr_conv_desc* d, ConvArgs& g, hi
     if (tw == 16) hipLaunchKernelGGL((conv3_kernel<16, DG, 32>), grid, dim3(256), 0, st, g);
     else hipLaunchKernelGGL((conv3_kernel<8, DG, 32>), grid, dim3(256), 0, st, g);
   }
+}
+
+static int dg2_tiles(const adr_conv_desc* d) {
+  return d->n * ((d->ho + G2_TI - 1) / G2_TI) * ((d->wo + G2_TJ - 1) / G2_TJ);
+}
+static void launch_dg2(int bn, const adr_conv_desc* d, ConvArgs& g, hipStream_t st) {
+  g.ntiles = g.N / bn;
+  const dim3 grid(dg2_tiles(d) * g.ntiles), blk(32 * G2_TJ);
+#define ADR_G2(BN_)                                                                                            \
+  do {                                                                                                         \
+    if (g.xs && g.by) hipLaunchKernelGGL((dg2_kernel<G2_TJ, BN_, XF_BWD, true>), grid, blk, 0, st, g);         \
+    else if (g.xs) hipLaunchKernelGGL((dg2_kernel<G2_TJ, BN_, XF_BWD, false>), grid, blk, 0, st, g);           \
+    else if (g.by) hipLaunchKernelGGL((dg2_kernel<G2_TJ, BN_, XF_NONE, true>), grid, blk, 0, st, g);           \
+    else hipLaunchKernelGGL((dg2_kernel<G2_TJ, BN_, XF_NONE, false>), grid, blk, 0, st, g);                    \
+  } while (0)
+  if (bn == 64) ADR_G2(64);
+  else if (bn == 32) ADR_G2(32);
+  else ADR_G2(16);
+#undef ADR_G2
 }
 
 template <int MODE>
@@ -1363,10 +1618,25 @@ struct ConvPlan {
   int bn;    // else conv_bf16_kernel<bn, mode>
   int mode;  // CV_FWD / CV_DGRAD / CV_DGRAD2
   int kt;    // > 0: conv1_kernel<bn, mode, kt> (streaming 1x1, reduction <= kt)
+  int dg2;   // > 0 (stride-2 DGRAD): dg2_kernel<dg2 = TJ, bn> (super-pixel halo tiles, all parity classes at once)
 };
+static int dg2_enabled() {
+  static const int on = getenv("ADR_DG2H") ? atoi(getenv("ADR_DG2H")) : 1;  // A/B: 0 = per-class implicit GEMM
+  return on;
+}
 static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   ConvPlan p{0, 0, 0, dgrad ? (d->stride_h == 2 ? CV_DGRAD2 : CV_DGRAD) : CV_FWD};
   const int red = dgrad ? d->k : d->c, out = dgrad ? d->c : d->k;
+  // DG2H where its 8 x 8 super-pixel tiles cover the dy grid with <= 15 % padding (the 20 x 20 grids of the P5
+  // layers would run 44 % empty rows: the per-class implicit GEMM is faster there, 27 vs 32 us)
+  const long g2_area = (long)((d->ho + G2_TI - 1) / G2_TI * G2_TI) * ((d->wo + G2_TJ - 1) / G2_TJ * G2_TJ);
+  if (p.mode == CV_DGRAD2 && d->r == 3 && d->s == 3 && d->pad_h == 1 && d->pad_w == 1 && red % C3_CK == 0 &&
+      out % 16 == 0 && (out <= 64 || out % 64 == 0) && g2_area * 100 <= 115l * d->ho * d->wo && dg2_enabled()) {
+    p.dg2 = G2_TJ;
+    p.bn = out % 64 == 0 ? 64 : out % 32 == 0 ? 32 : 16;
+    p.kt = 0;
+    return p;
+  }
   if (p.mode != CV_DGRAD2) p.tw = conv3_tw(d, red, out);
   p.wide = p.tw && !xf && conv3_wide(d, p.tw, red, out);
   // 1x1 contractions are two or three K-steps long: 64-wide column tiles (4 waves/SIMD) hide their load latency
@@ -1491,7 +1761,9 @@ static int conv_dgrad_impl(const adr_conv_desc* d, const void* dy, const void* w
   const int bn = pl.bn;
   g.ntiles = cdiv(g.N, bn);
   hipStream_t st = (hipStream_t)stream;
-  if (pl.mode == CV_DGRAD2) {  // parity classes; the largest (even, even) class sizes the grid
+  if (pl.dg2) {  // stride-2 3x3: all parity classes on super-pixel halo tiles
+    launch_dg2(bn, d, g, st);
+  } else if (pl.mode == CV_DGRAD2) {  // parity classes; the largest (even, even) class sizes the grid
     dim3 grid(cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM) * g.ntiles, 1, 4);
     launch_conv<CV_DGRAD2>(bn, grid, g, st);
   } else if (pl.tw) {
@@ -1565,6 +1837,7 @@ extern "C" int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad) {
   const ConvPlan pl = conv_plan(d, dgrad != 0, true);
   const int out = dgrad ? d->c : d->k;
   const int nt = pl.tw ? out / pl.bn : cdiv(out, pl.bn);
+  if (pl.dg2) return nt * 100 * (G2_TI + 1) * (pl.dg2 + 1) / (G2_TI * pl.dg2);
   if (pl.tw) return nt * 100 * (128 / pl.tw + 2) * (pl.tw + 2) / 128;
   const int taps = d->r * d->s;
   if (!dgrad) return nt * 100 * taps / (d->stride_h * d->stride_w);
@@ -1583,6 +1856,7 @@ extern "C" int adr_conv2d_fwd_bf16_stat_tiles(const adr_conv_desc* d) { return f
 // statistics rows of adr_conv2d_dgrad_bf16_bstat (xf: with the XF operand transform)
 extern "C" int adr_conv2d_dgrad_bf16_stat_tiles(const adr_conv_desc* d, int xf) {
   const ConvPlan pl = conv_plan(d, true, xf != 0);
+  if (pl.dg2) return dg2_tiles(d);
   if (pl.mode == CV_DGRAD2) return 4 * cdiv((long)d->n * ((d->h + 1) / 2) * ((d->w + 1) / 2), CBM);
   if (pl.tw) return pl.wide ? conv3_tiles(d, 16, 256) : conv3_tiles(d, pl.tw);
   if (pl.kt) return conv1_groups((long)d->n * d->h * d->w, cdiv(d->c, pl.bn), pl.kt, pl.bn);
@@ -1597,6 +1871,11 @@ extern "C" int adr_conv2d_bf16_kernel_symbol(const adr_conv_desc* d, int dgrad, 
   const bool dg = (dgrad & 1) != 0, xf = (dgrad & 2) != 0;  // bit 1: the BN-act (XF) variant
   const bool bst = dg && (dgrad & 4) != 0;                     // bit 2: the BSTAT data gradient
   const ConvPlan pl = conv_plan(d, dg, xf);
+  if (pl.dg2) {
+    snprintf(buf, len, "_ZN3adr10dg2_kernelILi%dELi%dELi%dELb%dEEEvNS_8ConvArgsE", pl.dg2, pl.bn, xf ? XF_BWD : XF_NONE,
+             bst ? 1 : 0);
+    return ADR_OK;
+  }
   if (bst) {
     if (pl.tw && pl.wide && !xf)
       snprintf(buf, len, "_ZN3adr17conv3w_bst_kernelENS_8ConvArgsE");
