@@ -157,6 +157,18 @@ int adr_conv2d_wgrad(const adr_conv_desc* d, const void* x, const void* dy, floa
  * split `out` may be dw itself, accumulate allowed for bf16), adr_wgrad_reduce sums the slabs in a fixed
  * order into dw (+= if accumulate). */
 int adr_conv2d_wgrad_splits(const adr_conv_desc* d);
+/* Many WGRAD partial launches in one call (bf16 engine): each job writes exactly what adr_conv2d_wgrad_partials(
+ * &job->d, x, dy, out, accumulate) writes (same splits and tiles, bitwise), but the jobs on the generic tile kernel
+ * are grouped by tile shape into one launch per shape. The trainer defers the weight gradients of a backward stage
+ * and issues them here at the stage's end (reference: the per-conv weight gradients of nn.Conv2d's backward). */
+typedef struct adr_wgrad_job {
+  adr_conv_desc d;
+  const void* x;
+  const void* dy;
+  float* out;
+  int accumulate, pad_;
+} adr_wgrad_job;
+int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int count, void* stream);
 int adr_conv2d_wgrad_partials(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
                               void* stream);
 int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accumulate, void* stream);

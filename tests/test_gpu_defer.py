@@ -2,7 +2,8 @@
 adr_nc_reduce_batched, adr_gn_param_grad_batched) against the immediate per-call path: one bf16 training
 forward/backward of the 701 graph at 320^2 bs 2 with each ADR_DEFER_* switch off, the gradient arena compared
 bitwise with the default (all deferred). Covers the AYHead's per-level shared GroupNorm modules (a repeated
-destination starts a new batched launch) and flushes with more entries than one launch holds."""
+destination starts a new batched launch) and flushes with more entries than one launch holds; and the grouped
+WGRAD partial launches (adr_conv2d_wgrad_partials_batched) against one launch per conv."""
 import pytest
 import torch
 
@@ -28,10 +29,12 @@ def _arena():
     return tr.grad.clone()
 
 
-@pytest.mark.parametrize("knob", ["_DEFER_DOT", "_DEFER_COLSUM", "_DEFER_GN", "all"])
+@pytest.mark.parametrize("knob", ["_DEFER_DOT", "_DEFER_COLSUM", "_DEFER_GN", "_DEFER_WGRAD", "all"])
 def test_deferred_reductions_bitwise(knob):
+    """_DEFER_WGRAD: the WGRAD partials of the stage's convs grouped into one launch per tile shape at the flush
+    (adr_conv2d_wgrad_partials_batched) — the same tiles / splits per conv, so bitwise the per-conv launches."""
     import adrefine.kernels as K
-    names = ["_DEFER_DOT", "_DEFER_COLSUM", "_DEFER_GN"] if knob == "all" else [knob]
+    names = ["_DEFER_DOT", "_DEFER_COLSUM", "_DEFER_GN", "_DEFER_WGRAD"] if knob == "all" else [knob]
     ref = _arena()
     saved = {n: getattr(K, n) for n in names}
     try:

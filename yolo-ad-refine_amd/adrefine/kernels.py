@@ -620,6 +620,12 @@ class WgradEntry(ctypes.Structure):
         (n, ctypes.c_int) for n in ("splits", "K", "C", "Cp", "RS", "transpose_kc", "accumulate", "pad_")]
 
 
+class WgradJob(ctypes.Structure):
+    """adr_wgrad_job (include/adr.h)."""
+    _fields_ = [("d", ConvDesc), ("x", ctypes.c_void_p), ("dy", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("accumulate", ctypes.c_int), ("pad_", ctypes.c_int)]
+
+
 class PsumEntry(ctypes.Structure):
     """adr_psum_entry (include/adr.h)."""
     _fields_ = [("partial", ctypes.c_void_p), ("out", ctypes.c_void_p)] + [
@@ -662,6 +668,7 @@ class WgradDeferral:
     destination's contributions still accumulate in program order."""
 
     def __init__(self):
+        self.jobs, self.jkeep = [], []  # deferred WGRAD partial launches (grouped by tile shape at the flush)
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
         self.axpys, self.akeep, self.adsts = [], [], set()
@@ -719,6 +726,17 @@ class WgradDeferral:
         self.pkeep.append(part)
         self.pdsts.add(dst)
 
+    def add_job(self, d, xp, dyp, ws, keep):
+        """A conv's WGRAD partials into `ws`, launched at the flush together with the stage's other weight gradients
+        (adr_conv2d_wgrad_partials_batched: one launch per tile shape, bitwise the per-conv launches). x and dy stay
+        alive (keep) and dy is pinned so no fan-out accumulates into it in place before the flush reads it."""
+        for t in keep:
+            if torch.is_tensor(t):
+                t._adr_pinned = True
+                _v(t)[0]._adr_pinned = True
+        self.jobs.append(WgradJob(ConvDesc.from_buffer_copy(d), xp, dyp, ws.data_ptr(), 0, 0))
+        self.jkeep += [ws, *keep]
+
     def add(self, ws, stride, splits, dst, K_, C_, Cp, RS_, transpose_kc, acc):
         dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
         if dst in self.dsts:
@@ -731,6 +749,10 @@ class WgradDeferral:
         self._flush()
 
     def _flush(self):
+        if self.jobs:  # the deferred weight-gradient partials, before their reductions
+            arr = (WgradJob * len(self.jobs))(*self.jobs)
+            lib.adr_conv2d_wgrad_partials_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.jobs), stream())
+            self.jobs, self.jkeep = [], []
         if self.dots:  # before the axpys that add their outputs into the arena
             arr = (DotsumEntry * len(self.dots))(*self.dots)
             lib.adr_dotsum_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.dots), stream())
@@ -804,6 +826,11 @@ def _grad_buf(tgt):
     return tgt._adr_grad
 
 
+# WGRAD partials of arena-bound bf16 weight gradients deferred to the stage's flush and grouped into one launch per
+# tile shape (WgradDeferral.add_job; ADR_DEFER_WGRAD=0: one launch per conv, at its backward)
+_DEFER_WGRAD = bool(int(__import__("os").environ.get("ADR_DEFER_WGRAD", "1")))
+
+
 def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device, keep=()):
     """Weight gradient of a conv contraction straight into its parameter's gradient destination: the split-K
     WGRAD GEMM writes [split][K][RS][C] fp32 slabs, and one fused reduce+unpack kernel sums the splits in a
@@ -814,10 +841,10 @@ def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device, keep=()):
     RS_ = 1
     for v in wshape[2:]:
         RS_ *= v
-    return _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device)
+    return _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep)
 
 
-def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device):
+def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep=()):
     splits = lib.adr_conv2d_wgrad_splits(ctypes.byref(d))
     stride = K * RS * C
     es = 2 if d.dtype == BF16 else 4
@@ -826,14 +853,19 @@ def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device):
     work = (es * (d.n * d.h * d.w * d.c + d.n * d.ho * d.wo * d.k) + 4 * stride, 2 * d.n * d.ho * d.wo * d.k * RS * d.c)
     shp = _shape(d, f"wgrad/{splits}") if _TIMING is not None else ""
     ws = torch.empty(splits * stride, dtype=torch.float32, device=device)
+    Cp = max(C_, cpad)
+    out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
+    if (_DEFER_WGRAD and keep and _dfr() is not None and acc and _TIMING is None and d.dtype == BF16 and
+            splits * stride * 4 <= DEFER_MAX_BYTES):
+        _dfr().add_job(d, xp, dyp, ws, keep)  # partials at the flush, grouped with the stage's other convs'
+        _dfr().add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
+        return grad_ret(param, out)
     rep = _reps()
     tok = _t0(name, *work, shp, rep)
     for _ in range(rep):
         lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(ws), 0,
                                       stream())
     _t1(tok)
-    Cp = max(C_, cpad)
-    out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
     if _dfr() is not None and acc and _TIMING is None and splits * stride * 4 <= DEFER_MAX_BYTES:
         _dfr().add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
         return grad_ret(param, out)

@@ -51,8 +51,8 @@ __device__ __forceinline__ void wg_xcd_block(int& bx, int& by) {
   bx = b - by * gx;
 }
 
-template <int BM, int BN, int KU>  // KU: 32*WK-row sub-steps per k-step
-__device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a) {
+template <int BM, int BN, int KU>  // KU: 32*WK-row sub-steps per k-step; (bid, split): tile and split of the block
+__device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int split) {
   constexpr int WM = BM / 16 < 2 ? BM / 16 : 2;
   constexpr int WN = BN / 16 < 2 ? BN / 16 : 2;
   constexpr int WK = 4 / (WM * WN);
@@ -72,9 +72,7 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wk = wave / (WM * WN), wmn = wave % (WM * WN), wm = wmn / WN, wn = wmn % WN;
   const int RS = a.r * a.s;
-  // block x -> (co tile, tap, ci tile); block y = split
-  int bid, split;
-  wg_xcd_block(bid, split);
+  // bid -> (co tile, tap, ci tile)
   const int ct = bid % a.ctiles;
   bid /= a.ctiles;
   const int tap = bid % RS;
@@ -245,7 +243,31 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a) {
 
 template <int BM, int BN>
 __global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
-  wgrad_bf16_body<BM, BN, wg_ku(BM, BN)>(a);
+  int bid, split;  // block x -> tile, block y = split (XCD-aware order)
+  wg_xcd_block(bid, split);
+  wgrad_bf16_body<BM, BN, wg_ku(BM, BN)>(a, bid, split);
+}
+
+// Grouped WGRAD: the weight gradients of many convs (the deferred ones of a backward stage, one BM x BN tile shape)
+// in ONE launch. Block b belongs to entry j (start[j] <= b < start[j+1]); inside it, consecutive blocks walk the
+// tiles of one split (as the single launch's XCD order groups them), so each block computes exactly what the
+// entry's own launch would — same tiles, splits and fixed-order partial sums: the grouped result is bitwise the
+// per-conv one. Small weight gradients (a 1x1 128 -> 128 at 20 x 20 is 100 workgroups for the whole chip) stop
+// costing a launch and a half-empty machine each.
+constexpr int WGB_MAX = 24;
+struct WgBatch {
+  WgArgs e[WGB_MAX];
+  int start[WGB_MAX + 1];
+  int tiles[WGB_MAX];
+  int count;
+};
+template <int BM, int BN>
+__global__ void __launch_bounds__(256) wgrad_bf16_batched_kernel(WgBatch b) {
+  int j = 0;
+  while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  const int local = (int)blockIdx.x - b.start[j];
+  const int split = local / b.tiles[j];
+  wgrad_bf16_body<BM, BN, wg_ku(BM, BN)>(b.e[j], local - split * b.tiles[j], split);
 }
 
 
@@ -625,11 +647,8 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   return p;
 }
 
-int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
-                      const WgPlan& p, hipStream_t st) {
-  ADR_REQUIRE(2l * d->n * d->h * d->w * d->x_cstride < (1l << 31) && 2l * d->n * d->ho * d->wo * d->y_cstride < (1l << 31),
-              "conv wgrad (bf16): operand exceeds 2 GB (32-bit buffer offsets)");
-  WgArgs g;
+static void wgrad_args(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
+                       const WgPlan& p, WgArgs& g) {
   g.x = (const __bf16*)x;
   g.dy = (const __bf16*)dy;
   g.out = out;
@@ -643,6 +662,14 @@ int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, flo
   g.accumulate = accumulate;
   g.x_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
   g.dy_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
+}
+
+int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
+                      const WgPlan& p, hipStream_t st) {
+  ADR_REQUIRE(2l * d->n * d->h * d->w * d->x_cstride < (1l << 31) && 2l * d->n * d->ho * d->wo * d->y_cstride < (1l << 31),
+              "conv wgrad (bf16): operand exceeds 2 GB (32-bit buffer offsets)");
+  WgArgs g;
+  wgrad_args(d, x, dy, out, accumulate, p, g);
   dim3 grid(p.tiles, p.splits);
   if (p.thin) {
     if (p.thin == 1) {
@@ -673,4 +700,75 @@ int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, flo
   return check_launch("adr_conv2d_wgrad(bf16)");
 }
 
+template <int BM>
+static void launch_batch_bm(int bn, int blocks, const WgBatch& b, hipStream_t st) {
+  switch (bn) {
+    case 16: hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 16>), dim3(blocks), dim3(256), 0, st, b); break;
+    case 32: hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 32>), dim3(blocks), dim3(256), 0, st, b); break;
+    case 64: hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 64>), dim3(blocks), dim3(256), 0, st, b); break;
+    default: hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 128>), dim3(blocks), dim3(256), 0, st, b); break;
+  }
+}
+
 }  // namespace adr
+
+using namespace adr;
+
+// The WGRAD partials of `count` convs (bf16 engine), each exactly as adr_conv2d_wgrad_partials(job) would write them:
+// the jobs on the generic tile kernel are grouped by tile shape into launches of up to WGB_MAX (one launch per shape
+// instead of one per conv); the 3x3 halo-tile / thin-channel ones run their own launches.
+extern "C" int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int count, void* stream) {
+  ADR_REQUIRE(count >= 0 && (count == 0 || jobs), "wgrad partials batched: count=%d", count);
+  hipStream_t st = (hipStream_t)stream;
+  struct Pending {
+    WgBatch b;
+    int blocks;
+  };
+  // one open batch per (bm, bn) in {16, 32, 64, 128}^2
+  static thread_local Pending open[4][4];
+  int used[4][4] = {};
+  auto idx = [](int v) { return v <= 16 ? 0 : v <= 32 ? 1 : v <= 64 ? 2 : 3; };
+  auto fire = [&](int i, int j) {
+    Pending& pd = open[i][j];
+    const int bm = 16 << i, bn = 16 << j;
+    pd.b.start[pd.b.count] = pd.blocks;
+    switch (bm) {
+      case 16: launch_batch_bm<16>(bn, pd.blocks, pd.b, st); break;
+      case 32: launch_batch_bm<32>(bn, pd.blocks, pd.b, st); break;
+      case 64: launch_batch_bm<64>(bn, pd.blocks, pd.b, st); break;
+      default: launch_batch_bm<128>(bn, pd.blocks, pd.b, st); break;
+    }
+    used[i][j] = 0;
+  };
+  for (int q = 0; q < count; ++q) {
+    const adr_wgrad_job& jb = jobs[q];
+    const adr_conv_desc* d = &jb.d;
+    ADR_REQUIRE(d->dtype == ADR_BF16, "wgrad partials batched: bf16 jobs only (job %d)", q);
+    ADR_REQUIRE(2l * d->n * d->h * d->w * d->x_cstride < (1l << 31) && 2l * d->n * d->ho * d->wo * d->y_cstride < (1l << 31),
+                "wgrad partials batched: operand exceeds 2 GB (job %d)", q);
+    const WgPlan p = wgrad_bf16_plan(d);
+    ADR_REQUIRE(!jb.accumulate || p.splits == 1, "wgrad partials batched: accumulate needs a single split (job %d)", q);
+    if (p.thin || p.tw3) {
+      if (int rc = wgrad_bf16_launch(d, jb.x, jb.dy, jb.out, jb.accumulate, p, st)) return rc;
+      continue;
+    }
+    const int i = idx(p.bm), j = idx(p.bn);
+    Pending& pd = open[i][j];
+    if (!used[i][j]) {
+      pd.b.count = 0;
+      pd.blocks = 0;
+      used[i][j] = 1;
+    }
+    const int k = pd.b.count;
+    wgrad_args(d, jb.x, jb.dy, jb.out, jb.accumulate, p, pd.b.e[k]);
+    pd.b.start[k] = pd.blocks;
+    pd.b.tiles[k] = p.tiles;
+    pd.blocks += p.tiles * p.splits;
+    pd.b.count = k + 1;
+    if (pd.b.count == WGB_MAX) fire(i, j);
+  }
+  for (int i = 0; i < 4; ++i)
+    for (int j = 0; j < 4; ++j)
+      if (used[i][j]) fire(i, j);
+  return check_launch("adr_conv2d_wgrad_partials_batched");
+}
