@@ -8,8 +8,10 @@ from collections import defaultdict
 FAMILIES = [  # (family, substrings) — first match wins
     ("conv fwd/dgrad (adr_conv, MFMA)", ["conv_bf16_kernel", "conv3_kernel", "conv1_kernel", "conv_bf16_xf", "conv3_xf",
                                          "conv3w_kernel", "conv_bf16_act", "conv1_xf", "conv1_act", "conv3_act",
-                                         "conv_fp8", "gemm_kernel", "stem_fwd"]),
-    ("conv wgrad (MFMA) + split-K reduce", ["wgrad_bf16_kernel", "wgrad3_kernel", "wgrad3t_kernel", "wgrad_reduce", "stem_wgrad"]),
+                                         "conv_fp8", "gemm_kernel", "stem_fwd", "conv_bf16_bst", "conv1_bst",
+                                         "conv3_bst", "conv3w_bst", "dg2_kernel"]),
+    ("conv wgrad (MFMA) + split-K reduce", ["wgrad_bf16_kernel", "wgrad_bf16_batched", "wgrad3_kernel", "wgrad3t_kernel",
+                                            "wgrad_reduce", "stem_wgrad"]),
     ("BN/GN stats, finalize, affine+act", ["nc_reduce", "affine_act", "bn_finalize", "bn_bwd_finalize", "gn_",
                                            "partial_sum", "nc_collapse", "dot_reduce"]),
     ("elementwise / broadcast", ["ew_kernel", "bcast_", "axpy", "cast_kernel", "scale_"]),

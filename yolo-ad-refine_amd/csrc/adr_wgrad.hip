@@ -630,7 +630,8 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   const long outsz = (long)d->k * d->r * d->s * d->c;
   p.tiles = cdiv(d->k, p.bm) * d->r * d->s * cdiv(d->c, p.bn);
   long s = (1024 + p.tiles - 1) / p.tiles;                  // ~4 workgroups per CU
-  const long by_work = red / ((long)p.R * 8);               // >= 8 k-steps per split
+  static const long min_ks = getenv("ADR_WG_MIN_KSTEPS") ? atol(getenv("ADR_WG_MIN_KSTEPS")) : 16;  // A/B (8 before grouping)
+  const long by_work = red / ((long)p.R * min_ks);          // >= 16 k-steps per split (grouped launches fill the chip)
   // <= 24 MB of partials (stays in L2/MALL); weights above 1 MB (l-scale: 3x3 256->256, 1x1 512->512) get 96 MB so
   // their splits still fill the chip (configs[4]: 145.2 -> 142.2 ms/step; the n-scale step is unchanged)
   static const long bg = part_budget("ADR_WG_PART_MB", 24);
