@@ -478,6 +478,29 @@ int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs, const voi
                      void* dx, int dxcs, void* dom, int domcs, float* dxf, int* tile_flags, int N, int H, int W, int C,
                      int Cout, void* stream);
 int adr_dcn_bwd_tiles(int N, int H, int W);
+/* The AYHead's pyramid levels of one DyDCNv2 call per launch (LevelDCNFn; reference head.py:751-782 runs the module
+ * per level): each writes, for every level, exactly what adr_dcn_{fwd,wgrad,bwd}_bf16 write for that level alone
+ * (same blocks and arithmetic: bitwise), one launch for all levels (bwd: plus one far-corner launch). Per level:
+ * pointers into the level-packed activations, its H x W, the wgrad partial slab and split count, the bwd far-corner
+ * scratch (dxf: N*H*W*C fp32, flags: adr_dcn_bwd_tiles ints; zero on first use, left zero). Up to 3 levels. */
+typedef struct adr_dcn_level {
+  const void* x;
+  const void* om;
+  const void* dy;
+  void* y;
+  void* dx;
+  void* dom;
+  float* dxf;
+  int* flags;
+  float* part;
+  int H, W, splits, pad_;
+} adr_dcn_level;
+int adr_dcn_fwd_bf16_levels(const adr_dcn_level* lv, int levels, int xcs, int omcs, const void* w_krsc, int ycs,
+                            int N, int C, int Cout, void* stream);
+int adr_dcn_wgrad_bf16_levels(const adr_dcn_level* lv, int levels, int xcs, int omcs, int dycs, int N, int C,
+                              int Cout, void* stream);
+int adr_dcn_bwd_bf16_levels(const adr_dcn_level* lv, int levels, int xcs, int omcs, int dycs, const void* w_t,
+                            int dxcs, int domcs, int N, int C, int Cout, void* stream);
 /* ---------------------------------------------------------------------------------------------------------
  * Training augmentation pixels (data/augment.py v8_transforms :2273-2335, through Format :2072-2100 and
  * YOLODataset.collate_fn, data/dataset.py:230-246): Mosaic canvas -> warpAffine (RandomPerspective) -> RandomHSV

@@ -114,3 +114,42 @@ def test_dcn_bf16_backward_repeatable_near(C):
     _, dx, dom, dw = _run(x, om, w, gy, torch.bfloat16)
     _, dx2, dom2, dw2 = _run(x, om, w, gy, torch.bfloat16)
     assert torch.equal(dx, dx2) and torch.equal(dom, dom2) and torch.equal(dw, dw2)
+
+
+@pytest.mark.parametrize("C", [64, 128])
+def test_dcn_levels_one_launch_bitwise(C):
+    """The AYHead's three pyramid levels in one launch per direction (adr_dcn_{fwd,bwd,wgrad}_bf16_levels, the
+    level-packed head's LevelDCNFn) against one launch per level: output, input / offset / weight gradients
+    bitwise equal (|offsets| < 2 px, so the backward has no far-corner atomics)."""
+    from adrefine import kernels as K
+    N, dims = 2, [(24, 24), (12, 12), (6, 6)]
+    pack = K.LevelPack(N, dims)
+    g = torch.Generator().manual_seed(9)
+    xs = [torch.randn(N, C, H, W, generator=g) for H, W in dims]
+    oms = []
+    for H, W in dims:
+        om = torch.zeros(N, 32, H, W)
+        om[:, :18] = (torch.rand(N, 18, H, W, generator=g) * 2 - 1) * 1.8
+        om[:, 18:27] = torch.randn(N, 9, H, W, generator=g) * 2
+        oms.append(om)
+    w = torch.randn(C, C, 3, 3, generator=g) * (9 * C) ** -0.5
+    gys = [torch.randn(N, C, H, W, generator=g) for H, W in dims]
+    runs = []
+    for levels in (True, False):
+        old = K.DCN_LEVELS
+        K.DCN_LEVELS = levels
+        try:
+            xd = [t.cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True) for t in xs]
+            od = [t.cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True) for t in oms]
+            wd = w.cuda().requires_grad_(True)
+            y = K.dcn_levels(K.level_join(xd, pack), K.level_join(od, pack), wd, pack)
+            ys = K.level_split(y, pack)
+            torch.autograd.backward(list(ys), [t.cuda().to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+                                               for t in gys])
+            torch.cuda.synchronize()
+            runs.append([y.detach().clone()] + [t.grad.clone() for t in xd] + [t.grad.clone() for t in od] +
+                        [wd.grad.clone()])
+        finally:
+            K.DCN_LEVELS = old
+    for i, (a, b) in enumerate(zip(*runs)):
+        assert torch.equal(a, b), i

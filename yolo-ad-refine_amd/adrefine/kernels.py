@@ -2721,6 +2721,36 @@ def _dcn_far_scratch(dev, N, H, W, C):
     return cur[0][:N * H * W * C], cur[1][:int(lib.adr_dcn_bwd_tiles(N, H, W))]
 
 
+def _dcn_far_scratch_levels(dev, N, dims, C):
+    """Per-level disjoint views of the persistent far-corner scratch, for the levels-in-one-launch backward."""
+    n = sum(N * H * W * C for H, W in dims)
+    nt = sum(int(lib.adr_dcn_bwd_tiles(N, H, W)) for H, W in dims)
+    f, g = _dcn_far_scratch(dev, 1, 1, 1, 1)  # the current pair (grown below when too small)
+    if f.numel() < n or g.numel() < nt:
+        key = str(dev)
+        cur = _DCN_FAR.get(key)
+        _DCN_FAR_RETIRED.append(cur)
+        _DCN_FAR[key] = (torch.zeros(max(n, cur[0].numel()), dtype=torch.float32, device=dev),
+                         torch.zeros(max(nt, cur[1].numel()), dtype=torch.int32, device=dev))
+    f, g = _DCN_FAR[str(dev)]
+    out, o, ot = [], 0, 0
+    for H, W in dims:
+        k, kt = N * H * W * C, int(lib.adr_dcn_bwd_tiles(N, H, W))
+        out.append((f[o:o + k], g[ot:ot + kt]))
+        o, ot = o + k, ot + kt
+    return out
+
+
+class DcnLevelStruct(ctypes.Structure):
+    """adr_dcn_level (include/adr.h)."""
+    _fields_ = [(n, ctypes.c_void_p) for n in ("x", "om", "dy", "y", "dx", "dom", "dxf", "flags", "part")] + [
+        (n, ctypes.c_int) for n in ("H", "W", "splits", "pad_")]
+
+
+# the AYHead's DCN levels in one launch per direction (adr_dcn_*_bf16_levels; ADR_DCN_LEVELS=0: one per level)
+DCN_LEVELS = bool(int(__import__("os").environ.get("ADR_DCN_LEVELS", "1")))
+
+
 def _dcn_work(N, H, W, C, Cout, es=2):
     """Algorithmic (bytes, flops) of one DCN pass: x, the 27 offset/mask channels, the weight and y (or dy) once."""
     pix = N * H * W
@@ -3918,7 +3948,22 @@ class LevelDCNFn(torch.autograd.Function):
         y = pack.empty(Cout, dtype, dev)
         ctx.fused = _dcn_fused(dtype, C, Cout, omcs)
         ctx.fused_bwd = ctx.fused and C == Cout and C in (64, 128, 256)
-        if ctx.fused:
+        if ctx.fused and DCN_LEVELS and len(pack.dims) <= 3:
+            wp = pack_weight2(w, dtype)[0]
+            lv = (DcnLevelStruct * len(pack.dims))()
+            for l, (H, W) in enumerate(pack.dims):
+                lv[l].x, lv[l].om = pack.at(xp, xcs, es, l), pack.at(omp, omcs, es, l)
+                lv[l].y = pack.at(y.data_ptr(), Cout, es, l)
+                lv[l].H, lv[l].W = H, W
+            work = [sum(v) for v in zip(*[_dcn_work(N, H, W, C, Cout) for H, W in pack.dims])]
+            tok = _t0("adr::dcn_fwd_levels_kernel(adr::DcnLevels)", *work,
+                      f"dcn fwd levels n{N} {pack.dims} c{C}->{Cout}" if _TIMING is not None else "", _reps())
+            for _ in range(_reps()):
+                lib.adr_dcn_fwd_bf16_levels(ctypes.cast(lv, ctypes.c_void_p), len(pack.dims), xcs, omcs, fptr(wp),
+                                            Cout, N, C, Cout, stream())
+            _t1(tok)
+            ctx.save_for_backward(x, om, w)
+        elif ctx.fused:
             wp = pack_weight2(w, dtype)[0]
             for l, (H, W) in enumerate(pack.dims):
                 tok = _t0("adr::dcn_fwd_kernel(adr::DcnArgs)", *_dcn_work(N, H, W, C, Cout),
@@ -3965,7 +4010,45 @@ class LevelDCNFn(torch.autograd.Function):
             for l, (H, W) in enumerate(pack.dims):
                 lib.adr_dcn_im2col(dcode(dtype), pack.at(xp, xcs, es, l), xcs, pack.at(omp, omcs, es, l), omcs,
                                    pack.at(cols.data_ptr(), 9 * C, es, l), N, H, W, C, stream())
-        if ctx.fused_bwd:
+        if ctx.fused_bwd and DCN_LEVELS and len(pack.dims) <= 3:
+            dx = pack.empty(C, dtype, dev)
+            dom = pack.empty(omc, dtype, dev)
+            lv = (DcnLevelStruct * len(pack.dims))()
+            far = _dcn_far_scratch_levels(dev, N, pack.dims, C)
+            for l, (H, W) in enumerate(pack.dims):
+                lv[l].x, lv[l].om = pack.at(xp, xcs, es, l), pack.at(omp, omcs, es, l)
+                lv[l].dy = pack.at(dyp, dycs, es, l)
+                lv[l].dx, lv[l].dom = pack.at(dx.data_ptr(), C, es, l), pack.at(dom.data_ptr(), omc, es, l)
+                lv[l].dxf, lv[l].flags = far[l][0].data_ptr(), far[l][1].data_ptr()
+                lv[l].H, lv[l].W = H, W
+            works = [_dcn_work(N, H, W, C, Cout) for H, W in pack.dims]
+            nb = sum(w_[0] + 2 * N * H * W * C for w_, (H, W) in zip(works, pack.dims))
+            tok = _t0("adr::dcn_bwd_levels_kernel(adr::DcnLevels)", nb, 2 * sum(w_[1] for w_ in works),
+                      f"dcn bwd levels n{N} {pack.dims} c{C}->{Cout}" if _TIMING is not None else "")
+            lib.adr_dcn_bwd_bf16_levels(ctypes.cast(lv, ctypes.c_void_p), len(pack.dims), xcs, omcs, dycs, fptr(wt),
+                                        C, omc, N, C, Cout, stream())
+            _t1(tok)
+            if ctx.needs_input_grad[2]:
+                stride = Cout * 9 * C
+                splits = [lib.adr_dcn_wgrad_bf16_splits(N, H, W, C, Cout) for H, W in pack.dims]
+                ws = torch.empty(sum(splits) * stride, dtype=torch.float32, device=dev)
+                s0 = 0
+                for l in range(len(pack.dims)):
+                    lv[l].part, lv[l].splits = ws.data_ptr() + 4 * s0 * stride, splits[l]
+                    s0 += splits[l]
+                tok = _t0("adr::dcn_wgrad_levels_kernel(adr::DcnLevels)",
+                          sum(w_[0] for w_ in works) + 4 * s0 * stride, sum(w_[1] for w_ in works),
+                          f"dcn wgrad levels/{s0} n{N} {pack.dims} c{C}->{Cout}" if _TIMING is not None else "")
+                lib.adr_dcn_wgrad_bf16_levels(ctypes.cast(lv, ctypes.c_void_p), len(pack.dims), xcs, omcs, dycs, N, C,
+                                              Cout, stream())
+                _t1(tok)
+                out, ptr, acc = grad_dst(ctx.pw, stride, dev)
+                if _dfr() is not None and acc and _TIMING is None:
+                    _dfr().add(ws, stride, s0, ptr, Cout, C, C, 9, 0, acc)
+                else:
+                    lib.adr_wgrad_reduce_unpack(fptr(ws), stride, s0, ptr, Cout, C, C, 9, 0, acc, stream())
+                dw = grad_ret(ctx.pw, out)
+        elif ctx.fused_bwd:
             dx = pack.empty(C, dtype, dev)
             dom = pack.empty(omc, dtype, dev)
             for l, (H, W) in enumerate(pack.dims):

@@ -96,14 +96,13 @@ struct DcnArgs {
 // ------------------------------------------------------------------------------------------------------------
 constexpr int FBM = 128, FLD = 72;
 
-__global__ void __launch_bounds__(256, 2) dcn_fwd_kernel(DcnArgs a) {
+__device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
   __shared__ __attribute__((aligned(16))) __bf16 As[2][FBM * FLD];
   __shared__ __attribute__((aligned(16))) __bf16 Bs[2][64 * FLD];
   __shared__ __attribute__((aligned(16))) __bf16 Oms[FBM * 32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long M = (long)a.N * a.H * a.W;
   const int mtiles = (int)((M + FBM - 1) / FBM), ntiles = a.Cout / 64;
-  const int bid = xcd_order(blockIdx.x, gridDim.x);
   const int mt = bid / ntiles, nt = bid % ntiles;
   const long m0 = (long)mt * FBM;
   const int co0 = nt * 64;
@@ -228,20 +227,43 @@ __global__ void __launch_bounds__(256, 2) dcn_fwd_kernel(DcnArgs a) {
   }
 }
 
+__global__ void __launch_bounds__(256, 2) dcn_fwd_kernel(DcnArgs a) { dcn_fwd_body(a, xcd_order(blockIdx.x, gridDim.x)); }
+
+// The AYHead's three pyramid levels in ONE launch (LevelDCNFn): block b of the grid (XCD-ordered) belongs to level l
+// with start[l] <= b < start[l + 1] and runs exactly the block b - start[l] of that level's own launch, so the
+// results are bitwise the per-level launches'; the P4 / P5 levels (1 / 4 and 1 / 16 of P3's tiles, latency-bound
+// on their own) fill the P3 launch's tail instead of running as launches of a few hundred workgroups.
+struct DcnLevels {
+  DcnArgs a[3];
+  float* dxf[3];
+  int* flags[3];
+  int start[4];
+  int tiles[3];  // wgrad: tile blocks per split
+  int nl;
+};
+__device__ __forceinline__ int dcn_level(const DcnLevels& L, int b) {
+  int l = 0;
+  while (l + 1 < L.nl && b >= L.start[l + 1]) ++l;
+  return l;
+}
+__global__ void __launch_bounds__(256, 2) dcn_fwd_levels_kernel(DcnLevels L) {
+  const int b = xcd_order(blockIdx.x, gridDim.x), l = dcn_level(L, b);
+  dcn_fwd_body(L.a[l], b - L.start[l]);
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // weight gradient: block = (co tile 64, tap, c tile 64) x split over pixels; 64 pixel rows per k-step
 // ------------------------------------------------------------------------------------------------------------
 constexpr int WR = 64, WP = 80;  // rows per k-step; LDS row pitch (odd multiple of 16 elements: conflict-free tr reads)
 
-__global__ void __launch_bounds__(256, 2) dcn_wgrad_kernel(DcnArgs a) {
+// (b: XCD-ordered block of the level's launch, tiles: tile blocks per split)
+__device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tiles) {
   __shared__ __attribute__((aligned(16))) __bf16 As[WR * WP];  // dy rows [p][co]
   __shared__ __attribute__((aligned(16))) __bf16 Bs[WR * WP];  // sampled rows [p][c]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ctiles = a.C / 64, cotiles = a.Cout / 64;
-  const int nbx = gridDim.x * gridDim.y;
-  int b = xcd_order(blockIdx.x + blockIdx.y * gridDim.x, nbx);
-  const int split = b / gridDim.x;
-  b -= split * gridDim.x;
+  const int split = b / tiles;
+  b -= split * tiles;
   const int ct = b % ctiles;
   b /= ctiles;
   const int t = b % 9, cot = b / 9;
@@ -358,6 +380,14 @@ __global__ void __launch_bounds__(256, 2) dcn_wgrad_kernel(DcnArgs a) {
     }
 }
 
+__global__ void __launch_bounds__(256, 2) dcn_wgrad_kernel(DcnArgs a) {
+  dcn_wgrad_body(a, xcd_order(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y), gridDim.x);
+}
+__global__ void __launch_bounds__(256, 2) dcn_wgrad_levels_kernel(DcnLevels L) {
+  const int b = xcd_order(blockIdx.x, gridDim.x), l = dcn_level(L, b);
+  dcn_wgrad_body(L.a[l], b - L.start[l], L.tiles[l]);
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // data / offset / mask gradients, gathered by destination tile (C == Cout in {64, 128, 256})
 //
@@ -412,8 +442,8 @@ struct GLds {
   static constexpr int TOTAL = OMS + (P1 > P2 ? P1 : P2) + 64;             // + K-step masks
 };
 
-template <int CC, int CO, int OCC>
-__global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf, int* flags, int mode) {
+template <int CC, int CO>
+__device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* flags, int mode, int bid) {
   using L = GLds<CO>;
   __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
   __bf16* oms = reinterpret_cast<__bf16*>(smem);
@@ -422,7 +452,6 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
   constexpr int C = 64 * CC, Cout = 64 * CO;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int tw = (a.W + GT - 1) / GT, th = (a.H + GT - 1) / GT;
-  const int bid = xcd_order(blockIdx.x, gridDim.x);
   const int n = bid / (tw * th);
   const int rem = bid - n * tw * th;
   const int h0 = (rem / tw) * GT, w0 = (rem % tw) * GT;
@@ -764,10 +793,19 @@ __global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf
   }
 }
 
+template <int CC, int CO, int OCC>
+__global__ void __launch_bounds__(256, OCC) dcn_bwd_kernel(DcnArgs a, float* dxf, int* flags, int mode) {
+  dcn_bwd_body<CC, CO>(a, dxf, flags, mode, xcd_order(blockIdx.x, gridDim.x));
+}
+template <int CC, int CO, int OCC>
+__global__ void __launch_bounds__(256, OCC) dcn_bwd_levels_kernel(DcnLevels L, int mode) {
+  const int b = xcd_order(blockIdx.x, gridDim.x), l = dcn_level(L, b);
+  dcn_bwd_body<CC, CO>(L.a[l], L.dxf[l], L.flags[l], mode, b - L.start[l]);
+}
+
 // flagged tiles: dx += dxf (far corners), then dxf and the flag back to zero
-__global__ void __launch_bounds__(256) dcn_far_apply_kernel(DcnArgs a, float* dxf, int* flags) {
+__device__ __forceinline__ void dcn_far_apply_body(const DcnArgs& a, float* dxf, int* flags, int b) {
   const int tw = (a.W + GT - 1) / GT, th = (a.H + GT - 1) / GT;
-  const int b = blockIdx.x;
   if (flags[b] == 0) return;
   const int n = b / (tw * th), rem = b - n * tw * th;
   const int h0 = (rem / tw) * GT, w0 = (rem % tw) * GT;
@@ -788,6 +826,13 @@ __global__ void __launch_bounds__(256) dcn_far_apply_kernel(DcnArgs a, float* dx
   }
   __syncthreads();
   if (threadIdx.x == 0) flags[b] = 0;
+}
+__global__ void __launch_bounds__(256) dcn_far_apply_kernel(DcnArgs a, float* dxf, int* flags) {
+  dcn_far_apply_body(a, dxf, flags, blockIdx.x);
+}
+__global__ void __launch_bounds__(256) dcn_far_apply_levels_kernel(DcnLevels L) {
+  const int b = blockIdx.x, l = dcn_level(L, b);
+  dcn_far_apply_body(L.a[l], L.dxf[l], L.flags[l], b - L.start[l]);
 }
 
 }  // namespace adr
@@ -904,3 +949,109 @@ extern "C" int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs
 
 /* Number of 8x8 tiles (the tile_flags length adr_dcn_bwd_bf16 needs). */
 extern "C" int adr_dcn_bwd_tiles(int N, int H, int W) { return N * cdiv(H, GT) * cdiv(W, GT); }
+
+// ---- the three AYHead pyramid levels per launch (LevelDCNFn): each entry point writes exactly what its per-level
+// counterpart above writes for every level (same blocks, same arithmetic), in one launch (bwd: + one far-corner
+// launch) instead of one per level ----
+static int dcn_levels_fill(const adr_dcn_level* lv, int levels, int xcs, int omcs, int N, int C, int Cout,
+                           DcnLevels& L) {
+  ADR_REQUIRE(lv && levels >= 1 && levels <= 3, "dcn levels: %d levels (1..3)", levels);
+  L = DcnLevels{};
+  L.nl = levels;
+  for (int l = 0; l < levels; ++l) {
+    if (int rc = dcn_check(N, lv[l].H, lv[l].W, C, Cout, xcs, omcs)) return rc;
+    DcnArgs& a = L.a[l];
+    a.x = (const __bf16*)lv[l].x;
+    a.om = (const __bf16*)lv[l].om;
+    a.xcs = xcs;
+    a.omcs = omcs;
+    a.N = N;
+    a.H = lv[l].H;
+    a.W = lv[l].W;
+    a.C = C;
+    a.Cout = Cout;
+    a.x_bytes = (int)((long)N * a.H * a.W * xcs * 2);
+  }
+  return 0;
+}
+
+extern "C" int adr_dcn_fwd_bf16_levels(const adr_dcn_level* lv, int levels, int xcs, int omcs, const void* w_krsc,
+                                       int ycs, int N, int C, int Cout, void* stream) {
+  DcnLevels L;
+  if (int rc = dcn_levels_fill(lv, levels, xcs, omcs, N, C, Cout, L)) return rc;
+  int total = 0;
+  for (int l = 0; l < levels; ++l) {
+    DcnArgs& a = L.a[l];
+    a.w = (const __bf16*)w_krsc;
+    a.y = (__bf16*)lv[l].y;
+    a.ycs = ycs;
+    a.w_bytes = Cout * 9 * C * 2;
+    L.start[l] = total;
+    total += cdiv((long)N * a.H * a.W, FBM) * (Cout / 64);
+  }
+  L.start[levels] = total;
+  hipLaunchKernelGGL(dcn_fwd_levels_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, L);
+  return check_launch("adr_dcn_fwd_bf16_levels");
+}
+
+extern "C" int adr_dcn_wgrad_bf16_levels(const adr_dcn_level* lv, int levels, int xcs, int omcs, int dycs, int N,
+                                         int C, int Cout, void* stream) {
+  DcnLevels L;
+  if (int rc = dcn_levels_fill(lv, levels, xcs, omcs, N, C, Cout, L)) return rc;
+  int total = 0;
+  const int tiles = 9 * (C / 64) * (Cout / 64);
+  for (int l = 0; l < levels; ++l) {
+    DcnArgs& a = L.a[l];
+    ADR_REQUIRE(lv[l].part && lv[l].splits >= 1, "dcn_wgrad levels: partials / splits of level %d", l);
+    a.dy = (const __bf16*)lv[l].dy;
+    a.dycs = dycs;
+    a.part = lv[l].part;
+    a.dy_bytes = (int)((long)N * a.H * a.W * dycs * 2);
+    const long M = (long)N * a.H * a.W;
+    const long steps = (M + WR - 1) / WR;
+    a.rows_per_split = ((steps + lv[l].splits - 1) / lv[l].splits) * WR;
+    a.splits = lv[l].splits;
+    L.tiles[l] = tiles;
+    L.start[l] = total;
+    total += tiles * lv[l].splits;
+  }
+  L.start[levels] = total;
+  hipLaunchKernelGGL(dcn_wgrad_levels_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, L);
+  return check_launch("adr_dcn_wgrad_bf16_levels");
+}
+
+extern "C" int adr_dcn_bwd_bf16_levels(const adr_dcn_level* lv, int levels, int xcs, int omcs, int dycs,
+                                       const void* w_t, int dxcs, int domcs, int N, int C, int Cout, void* stream) {
+  DcnLevels L;
+  if (int rc = dcn_levels_fill(lv, levels, xcs, omcs, N, C, Cout, L)) return rc;
+  ADR_REQUIRE(C == Cout && (C == 64 || C == 128 || C == 256),
+              "dcn_bwd levels (bf16 fused): C == Cout in {64, 128, 256} (C=%d Cout=%d)", C, Cout);
+  ADR_REQUIRE(domcs >= 32 && domcs % 8 == 0 && dycs % 8 == 0 && dxcs % 8 == 0 && dxcs >= C,
+              "dcn_bwd levels: domcs=%d dycs=%d dxcs=%d", domcs, dycs, dxcs);
+  int total = 0;
+  for (int l = 0; l < levels; ++l) {
+    DcnArgs& a = L.a[l];
+    ADR_REQUIRE(lv[l].dxf && lv[l].flags && lv[l].dx && lv[l].dom, "dcn_bwd levels: buffers of level %d", l);
+    a.dy = (const __bf16*)lv[l].dy;
+    a.w = (const __bf16*)w_t;
+    a.dx = (__bf16*)lv[l].dx;
+    a.dom = (__bf16*)lv[l].dom;
+    a.dycs = dycs;
+    a.dxcs = dxcs;
+    a.domcs = domcs;
+    a.w_bytes = 9 * C * Cout * 2;
+    L.dxf[l] = lv[l].dxf;
+    L.flags[l] = lv[l].flags;
+    L.start[l] = total;
+    total += N * cdiv(a.H, GT) * cdiv(a.W, GT);
+  }
+  L.start[levels] = total;
+  hipStream_t s = (hipStream_t)stream;
+  static const int mode = getenv("ADR_DCN_BWD_MODE") ? atoi(getenv("ADR_DCN_BWD_MODE")) : 0;
+  if (C == 64) hipLaunchKernelGGL((dcn_bwd_levels_kernel<1, 1, 2>), dim3(total), dim3(256), 0, s, L, mode);
+  else if (C == 128) hipLaunchKernelGGL((dcn_bwd_levels_kernel<2, 2, 2>), dim3(total), dim3(256), 0, s, L, mode);
+  else hipLaunchKernelGGL((dcn_bwd_levels_kernel<4, 4, 2>), dim3(total), dim3(256), 0, s, L, mode);
+  if (int rc = check_launch("adr_dcn_bwd_bf16_levels")) return rc;
+  hipLaunchKernelGGL(dcn_far_apply_levels_kernel, dim3(total), dim3(256), 0, s, L);
+  return check_launch("adr_dcn_bwd_bf16_levels (far corners)");
+}
