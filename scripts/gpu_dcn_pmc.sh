@@ -1,22 +1,23 @@
-# dcn_bwd phase A/B timings and SQ counters at the n-scale P3 shape (scripts/dcn_bwd_micro.py)
-set -o pipefail
-OUT=gpurun_out/dcnpmc; mkdir -p $OUT
-for m in 0 1 2 3; do ADR_DCN_BWD_MODE=$m timeout -k 10 60 python scripts/dcn_bwd_micro.py 2>&1 | grep dcn_bwd || exit 1; done
-SPREAD=2.5 timeout -k 10 60 python scripts/dcn_bwd_micro.py 2>&1 | grep dcn_bwd || exit 1
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+#!/bin/bash
+# DCN backward stall breakdown (one --pmc pass per mode). usage (GPU box): bash scripts/gpu_dcn_pmc.sh OUTDIR
+set -e
+out=${1:-gpurun_out/dcn_pmc}
+mkdir -p "$out"
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
 for m in 0 1 2; do
-export ADR_DCN_BWD_MODE=$m
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_LDS SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_WAIT_ANY SQ_INSTS_VMEM_RD --output-format csv -d $OUT/p1_$m -o run -- python3 scripts/dcn_bwd_micro.py > $OUT/p1_$m.log 2>&1 || exit 1
-timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_ANY SQ_INSTS_SALU SQ_WAVES SQ_INST_CYCLES_VMEM --output-format csv -d $OUT/p2_$m -o run -- python3 scripts/dcn_bwd_micro.py > $OUT/p2_$m.log 2>&1 || exit 1
+  ADR_DCN_BWD_MODE=$m R=5 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+    SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU -d "$out/m$m" -o pmc --output-format csv \
+    -- python3 scripts/dcn_bwd_micro.py
 done
-python3 - <<'PY'
-import csv, glob, collections
-for d in sorted(glob.glob("gpurun_out/dcnpmc/p*_*")):
-    f = glob.glob(d + "/**/*counter_collection.csv", recursive=True)
-    if not f: print(d, "no csv"); continue
-    acc = collections.defaultdict(float); n = collections.Counter()
-    for r in csv.DictReader(open(f[0])):
-        if "dcn_bwd_kernel" not in r["Kernel_Name"]: continue
-        acc[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
-    print(d, {k: round(v / max(1, n[k]) / 1e6, 3) for k, v in acc.items()}, "(M per launch)")
+python3 - "$out" <<'PY'
+import csv, glob, sys, collections
+for m in (0, 1, 2):
+    tot = collections.defaultdict(float); n = collections.Counter()
+    for f in glob.glob(f"{sys.argv[1]}/m{m}/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            if "dcn_bwd" not in r["Kernel_Name"]:
+                continue
+            tot[r["Counter_Name"]] += float(r["Counter_Value"]); n[r["Counter_Name"]] += 1
+    print(f"mode {m}: " + "  ".join(f"{k}={tot[k]/max(n[k],1):.3g}" for k in sorted(tot)))
 PY

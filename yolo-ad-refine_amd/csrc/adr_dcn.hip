@@ -534,50 +534,42 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
         const float mk = sigm((float)om_p[18 + t]);
         Corners c0;
         sample((float)(ph - 1 + t / 3) + oy, (float)(pw - 1 + t % 3) + ox, a.H, a.W, c0);
-        // the four corners' channels 16 i + 4 g .. +3: from the staged neighbourhood, or (corner outside it) global
-        u32x2 xv[4][4];
+        // the four corners' channels 16 i + 4 g .. +3: from the staged neighbourhood, or (corner outside it) global.
+        // The bilinear value and its two slopes are linear in the corners, so the channel sums are taken per corner
+        // first (D_q = sum_c dcols_c x_qc: one FMA per channel and corner) and interpolated once per lane.
+        float D[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int yy = c0.y0 + (q >> 1), xx = c0.x0 + (q & 1);
           const int cy = yy - wy0, cx = xx - wx0;
           const bool ok = pok && c0.ok[q];
+          u32x2 xv[4];
           if (cy >= 0 && cy < GWIN && cx >= 0 && cx < GWIN) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-              const u32x2 v = *reinterpret_cast<const u32x2*>(&xwin[(cy * GWIN + cx) * GXP + 16 * i + 4 * g]);
-              xv[q][i] = ok ? v : (u32x2){0u, 0u};
-            }
+            for (int i = 0; i < 4; ++i)
+              xv[i] = *reinterpret_cast<const u32x2*>(&xwin[(cy * GWIN + cx) * GXP + 16 * i + 4 * g]);
           } else {
             const int pix = ibase + yy * a.W + xx;
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              xv[q][i] = __builtin_amdgcn_raw_buffer_load_b64(
+              xv[i] = __builtin_amdgcn_raw_buffer_load_b64(
                   xr, ok ? (unsigned)(pix * a.xcs + cc * 64 + 16 * i + 4 * g) * 2u : OOR, 0, 0);
           }
-        }
-        float smk = 0.f, spy = 0.f, spx = 0.f;
+          float d = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          float xf[4][4];
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            const __bf16* e = reinterpret_cast<const __bf16*>(&xv[q][i]);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) xf[q][k] = (float)e[k];
+          for (int i = 0; i < 4; ++i) {
+            d += acc[i][0] * __uint_as_float(xv[i].x << 16);
+            d += acc[i][1] * __uint_as_float(xv[i].x & 0xFFFF0000u);
+            d += acc[i][2] * __uint_as_float(xv[i].y << 16);
+            d += acc[i][3] * __uint_as_float(xv[i].y & 0xFFFF0000u);
           }
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const float top = xf[0][e] + c0.lx * (xf[1][e] - xf[0][e]);
-            const float bot = xf[2][e] + c0.lx * (xf[3][e] - xf[2][e]);
-            const float d01 = xf[1][e] - xf[0][e], d23 = xf[3][e] - xf[2][e];
-            const float val = top + c0.ly * (bot - top);
-            const float sy = bot - top, sx = d01 + c0.ly * (d23 - d01);
-            const float gv = acc[i][e];
-            smk += gv * val;
-            spy += gv * sy;
-            spx += gv * sx;
-          }
+          D[q] = ok ? d : 0.f;
         }
+        const float top = D[0] + c0.lx * (D[1] - D[0]);
+        const float bot = D[2] + c0.lx * (D[3] - D[2]);
+        const float d01 = D[1] - D[0], d23 = D[3] - D[2];
+        float smk = top + c0.ly * (bot - top);
+        float spy = bot - top, spx = d01 + c0.ly * (d23 - d01);
         smk += __shfl_xor(smk, 16, 64);
         smk += __shfl_xor(smk, 32, 64);
         spy += __shfl_xor(spy, 16, 64);
@@ -704,7 +696,7 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
       else if (t + 1 < 9) wissue(t + 1, 0, coc);
       else if (coc + 1 < CO) wissue(0, 0, coc + 1);
       if (tid < 4) kmask[4 * ((tt + 1) & 1) + tid] = 0u;  // next tap's masks (read after two more barriers)
-      unsigned bits[4] = {0u, 0u, 0u, 0u};  // K steps (bit) with entries in each wave's destination rows
+      bool hit[4] = {false, false, false, false};  // this source has entries in each wave's destination rows
       if (tid < GK) {  // source k = tid of the tap's sub-window: its corners that land in this tile
 #pragma unroll
         for (int q = 0; q < 4; ++q)
@@ -724,17 +716,16 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
           if (sok && c0.ok[q] && qy >= 0 && qy < GT && qx >= 0 && qx < GT) {
             prevq[q] = qy * GT + qx;
             S[prevq[q] * GSP + tid] = (__bf16)(mk * c0.w[q]);
-            bits[qy >> 1] |= 1u << (tid >> 5);
+            hit[qy >> 1] = true;
           }
         }
       }
-      // OR over the wave first (xor butterfly), then one LDS atomic per wave and destination wave: same-address
-      // LDS atomics from every lane serialise
+      // K step of source k = k >> 5: each half wave is one K step, so a ballot gives the wave's two bits; then one
+      // LDS atomic per wave and destination wave (same-address LDS atomics from every lane serialise)
 #pragma unroll
       for (int w4 = 0; w4 < 4; ++w4) {
-        unsigned b = bits[w4];
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) b |= (unsigned)__shfl_xor((int)b, o, 64);
+        const unsigned long long m = __ballot(hit[w4]);
+        const unsigned b = ((unsigned)m ? 1u << (2 * wave) : 0u) | ((unsigned)(m >> 32) ? 2u << (2 * wave) : 0u);
         if (lane == 0 && b) atomicOr(&kmask[4 * (tt & 1) + w4], b);
       }
       __syncthreads();  // S_t, masks and the W slab complete
