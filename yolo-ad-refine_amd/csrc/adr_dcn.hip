@@ -429,26 +429,39 @@ __device__ __forceinline__ int gsrc_row(int k, int sy, int sx) {  // neighbourho
 }
 
 // SB (CO >= 2): ONE phase-1 W_t^T slab instead of two (a second barrier per tap), so the 128- and 256-channel
-// kernels fit two workgroups per CU (LDS 74.8 / 81.5 KB instead of 82.6 / 115.3 KB)
-template <int CO>
+// kernels fit two workgroups per CU (LDS 74.8 / 81.5 KB instead of 82.6 / 115.3 KB).
+// LEAN (C = Cout = 64): no om rows in LDS (each lane loads the offset pair / mask logit it needs from global, one
+// tap ahead), the dy window at a 64-element pitch with its 16-byte chunks XOR-swizzled by row pair (transposing
+// reads stay conflict-free), S_t at a 152-element pitch (K columns 144..159 are multiplied by the dy window's
+// zero row, so they may read the next row / the K-step masks placed right after S_t) and the phase-2 W_t slab at a
+// 68-element pitch: 53.6 KB, three workgroups per CU instead of two (at 53.9 KB the dispatcher placed only two).
+template <int CC, int CO>
 struct GLds {
   static constexpr bool SB = CO >= 2;
+  static constexpr bool LEAN = CC == 1 && CO == 1;
   static constexpr int PW1 = 64 * CO + 8;                                  // phase-1 slab pitch [c][co]
-  static constexpr int OMS = GCELL * 32 * 2;                               // om rows of the neighbourhood
+  static constexpr int OMS = LEAN ? 0 : GCELL * 32 * 2;                    // om rows of the neighbourhood
   static constexpr int P1X = GCELL * GXP * 2, P1W = (SB ? 1 : 2) * 64 * PW1 * 2, P1D = 64 * 27 * 4;
   static constexpr int P1 = P1X + P1W + P1D;                               // x window | W_t^T slabs | dom sums
-  static constexpr int P2Y = (GCELL + 1) * GDP * 2, P2S = 64 * GSP * 2, P2W = 64 * 72 * 2;
-  static constexpr int P2 = P2Y + P2S + P2W;                               // dy window | S_t | W_t slab
-  static constexpr int TOTAL = OMS + (P1 > P2 ? P1 : P2) + 64;             // + K-step masks
+  static constexpr int DP = LEAN ? 64 : GDP, SP = LEAN ? 152 : GSP;        // dy-window / S_t row pitches
+  static constexpr int WP = LEAN ? 68 : 72;                                // phase-2 W_t slab pitch (8-B rows)
+  static constexpr int P2Y = (GCELL + 1) * DP * 2, P2S = 64 * SP * 2, P2W = 64 * WP * 2;
+  static constexpr int KM = LEAN ? P2Y + P2S : -1;                         // K-step masks inside phase 2 (LEAN)
+  static constexpr int P2 = P2Y + P2S + (LEAN ? 64 : 0) + P2W;             // dy window | S_t | (masks) | W_t slab
+  static constexpr int TOTAL = OMS + (P1 > P2 ? P1 : P2) + (LEAN ? 0 : 64);  // + K-step masks
 };
+// element offset e (multiple of 4) of dy-window row `row` (LEAN: chunk pair swizzled by (row >> 1) & 3)
+template <bool LEAN>
+__device__ __forceinline__ int dsw(int row, int e) { return LEAN ? e ^ (((row >> 1) & 3) << 4) : e; }
 
 template <int CC, int CO>
 __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* flags, int mode, int bid) {
-  using L = GLds<CO>;
+  using L = GLds<CC, CO>;
+  constexpr bool LEAN = L::LEAN;
   __shared__ __attribute__((aligned(16))) char smem[L::TOTAL];
   __bf16* oms = reinterpret_cast<__bf16*>(smem);
   char* reg = smem + L::OMS;
-  unsigned* kmask = reinterpret_cast<unsigned*>(smem + L::TOTAL - 64);  // [2 taps][4 waves]
+  unsigned* kmask = reinterpret_cast<unsigned*>(L::LEAN ? smem + L::KM : smem + L::TOTAL - 64);  // [2 taps][4 waves]
   constexpr int C = 64 * CC, Cout = 64 * CO;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4;
   const int tw = (a.W + GT - 1) / GT, th = (a.H + GT - 1) / GT;
@@ -460,9 +473,20 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
   const u32x4 z4 = {0u, 0u, 0u, 0u};
+  const __amdgpu_buffer_rsrc_t omr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.om, (short)0, (a.N * a.H * a.W) * a.omcs * 2, 0x00020000);
+  // LEAN: offset pair (2t, 2t+1) and mask logit (18+t) of pixel `pix` for tap t, zeros when !ok
+  auto omload = [&](bool ok, int pix, int t, unsigned& off2, unsigned& mlog) {
+    const unsigned base = (unsigned)(pix * a.omcs) * 2u;
+    off2 = __builtin_amdgcn_raw_buffer_load_b32(omr, ok ? base + 4u * t : OOR, 0, 0);
+    mlog = __builtin_amdgcn_raw_buffer_load_b16(omr, ok ? base + 2u * (18 + t) : OOR, 0, 0);
+  };
+  auto bf_lo = [](unsigned v) { return __uint_as_float(v << 16); };
+  auto bf_hi = [](unsigned v) { return __uint_as_float(v & 0xFFFF0000u); };
   auto inimg = [&](int yy, int xx) { return yy >= 0 && yy < a.H && xx >= 0 && xx < a.W; };
 
   // offset / mask rows of the 14x14 neighbourhood (zero outside the image)
+  if constexpr (!LEAN)
   for (int q = tid; q < GCELL * 4; q += 256) {
     const int cell = q >> 2, ch = (q & 3) * 8;
     const int yy = wy0 + cell / GWIN, xx = wx0 + cell % GWIN;
@@ -481,6 +505,8 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
     const bool pok = ph < a.H && pw < a.W;
     const long ppix = ibase + (long)ph * a.W + pw;
     const __bf16* om_p = oms + ((ph - wy0) * GWIN + pw - wx0) * 32;
+    unsigned po2 = 0u, pml = 0u;  // LEAN: this tap's offset pair / mask logit of the lane's pixel (one tap ahead)
+    if constexpr (LEAN) omload(pok, (int)ppix, 0, po2, pml);
     bf16x8 fb[2 * CO];  // dy fragments of this lane's pixel (B operand, k = output channel)
 #pragma unroll
     for (int k = 0; k < 2 * CO; ++k) {
@@ -530,8 +556,14 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
                 0, 0);
         }
         if (!L::SB && t + 1 < 9) wstore((t & 1) ? slab0 : slab1);  // last read in tap t-1, before the barrier below
-        const float oy = (float)om_p[2 * t], ox = (float)om_p[2 * t + 1];
-        const float mk = sigm((float)om_p[18 + t]);
+        float oy, ox, ml;
+        if constexpr (LEAN) {
+          oy = bf_lo(po2), ox = bf_hi(po2), ml = bf_lo(pml);
+          if (t + 1 < 9) omload(pok, (int)ppix, t + 1, po2, pml);
+        } else {
+          oy = (float)om_p[2 * t], ox = (float)om_p[2 * t + 1], ml = (float)om_p[18 + t];
+        }
+        const float mk = sigm(ml);
         Corners c0;
         sample((float)(ph - 1 + t / 3) + oy, (float)(pw - 1 + t % 3) + ox, a.H, a.W, c0);
         // the four corners' channels 16 i + 4 g .. +3: from the staged neighbourhood, or (corner outside it) global.
@@ -578,9 +610,15 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
         spx += __shfl_xor(spx, 32, 64);
         if (g == 0) {
           float* d = dsum + (pl * 9 + t) * 3;
-          d[0] += smk;
-          d[1] += spy;
-          d[2] += spx;
+          if constexpr (LEAN) {  // one channel chunk: the finished dom values
+            d[0] = smk * mk * (1.f - mk);
+            d[1] = mk * spy;
+            d[2] = mk * spx;
+          } else {
+            d[0] += smk;
+            d[1] += spy;
+            d[2] += spx;
+          }
         }
         // corners whose destination tile cannot see this source: scatter this chunk of dcols into dxf
         if (pok) {
@@ -618,11 +656,17 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
         for (int k = 27; k < 32; ++k) row[k] = (__bf16)0.f;
 #pragma unroll
         for (int t = 0; t < 9; ++t) {
-          const float mk = sigm((float)o[18 + t]);
           const float* d = dsum + (tid * 9 + t) * 3;
-          row[2 * t] = (__bf16)(mk * d[1]);
-          row[2 * t + 1] = (__bf16)(mk * d[2]);
-          row[18 + t] = (__bf16)(d[0] * mk * (1.f - mk));
+          if constexpr (LEAN) {
+            row[2 * t] = (__bf16)d[1];
+            row[2 * t + 1] = (__bf16)d[2];
+            row[18 + t] = (__bf16)d[0];
+          } else {
+            const float mk = sigm((float)o[18 + t]);
+            row[2 * t] = (__bf16)(mk * d[1]);
+            row[2 * t + 1] = (__bf16)(mk * d[2]);
+            row[18 + t] = (__bf16)(d[0] * mk * (1.f - mk));
+          }
         }
         __bf16* dst = a.dom + (long)(ibase + hh * a.W + ww) * a.domcs;
 #pragma unroll
@@ -636,14 +680,14 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
   __syncthreads();  // the dom rows are read out of the phase-1 sums that S_t is about to overwrite
   __bf16* dyw = reinterpret_cast<__bf16*>(reg);
   __bf16* S = reinterpret_cast<__bf16*>(reg + L::P2Y);
-  __bf16* Wsl = reinterpret_cast<__bf16*>(reg + L::P2Y + L::P2S);
+  __bf16* Wsl = reinterpret_cast<__bf16*>(reg + L::P2Y + L::P2S + (LEAN ? 64 : 0));
   f32x4 dxa[CC][4];  // dx^T: [c chunk][c tile] rows c = 16 i + 4 g + e, column q = 16 wave + (lane & 15)
 #pragma unroll
   for (int cc = 0; cc < CC; ++cc)
 #pragma unroll
     for (int i = 0; i < 4; ++i) dxa[cc][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int q4 = (lane >> 2) & 3, p4 = lane & 3;
-  const __bf16* Sq = S + (16 * wave + (lane & 15)) * GSP;  // this lane's destination row of S_t
+  const __bf16* Sq = S + (16 * wave + (lane & 15)) * L::SP;  // this lane's destination row of S_t
   u32x4 wreg[2];
   auto wissue = [&](int t, int cc, int coc) {
 #pragma unroll
@@ -657,7 +701,13 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = tid + 256 * i;
-      st16(&Wsl[(q >> 3) * 72 + (q & 7) * 8], wreg[i]);
+      __bf16* d = &Wsl[(q >> 3) * L::WP + (q & 7) * 8];
+      if constexpr (LEAN) {  // 136-byte rows: two 8-byte stores
+        *reinterpret_cast<u32x2*>(d) = (u32x2){wreg[i].x, wreg[i].y};
+        *reinterpret_cast<u32x2*>(d + 4) = (u32x2){wreg[i].z, wreg[i].w};
+      } else {
+        st16(d, wreg[i]);
+      }
     }
   };
   bf16x8 gb[2];  // G_t^T as the B operand of dx^T += W_t^T G_t^T (k = co, slots {16 (2kk+h) + 4 g + e})
@@ -666,13 +716,21 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
     for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const __bf16* wrow = Wsl + (16 * i + (lane & 15)) * 72 + 32 * kk + 4 * g;
+        const __bf16* wrow = Wsl + (16 * i + (lane & 15)) * L::WP + 32 * kk + 4 * g;
         u32x2 aa[2] = {*reinterpret_cast<const u32x2*>(wrow), *reinterpret_cast<const u32x2*>(wrow + 16)};
         dxa[cc][i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(aa), gb[kk], dxa[cc][i], 0, 0, 0);
       }
   };
+  // LEAN: source k = tid's offset pair / mask logit for the coming tap (one tap ahead)
+  unsigned so2 = 0u, sml = 0u;
+  auto somload = [&](int t) {
+    const int ky = tid / GSUB, kx = tid - ky * GSUB;
+    const int py = wy0 + ky + 2 - t / 3, px = wx0 + kx + 2 - t % 3;
+    omload(tid < GK && inimg(py, px), ibase + py * a.W + px, t, so2, sml);
+  };
+  if constexpr (LEAN) somload(0);
   // S_t starts all-zero; thread k (< 144) writes and later clears only its own column
-  for (int q = tid; q < 64 * GSP / 8; q += 256) st16(&S[8 * q], z4);
+  for (int q = tid; q < 64 * L::SP / 8; q += 256) st16(&S[8 * q], z4);
   if (tid < 8) kmask[tid] = 0u;
   int prevq[4] = {-1, -1, -1, -1};
 #pragma unroll 1
@@ -682,7 +740,7 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
     for (int q = tid; q < (GCELL + 1) * 8; q += 256) {
       const int row = q >> 3, ch = (q & 7) * 8;
       const int yy = wy0 + row / GWIN, xx = wx0 + row % GWIN;
-      st16(&dyw[row * GDP + ch], row < GCELL && inimg(yy, xx)
+      st16(&dyw[row * L::DP + dsw<LEAN>(row, ch)], row < GCELL && inimg(yy, xx)
                                      ? ld16(a.dy + (long)(ibase + yy * a.W + xx) * a.dycs + coc * 64 + ch)
                                      : z4);
     }
@@ -700,22 +758,29 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
       if (tid < GK) {  // source k = tid of the tap's sub-window: its corners that land in this tile
 #pragma unroll
         for (int q = 0; q < 4; ++q)
-          if (prevq[q] >= 0) S[prevq[q] * GSP + tid] = (__bf16)0.f;
+          if (prevq[q] >= 0) S[prevq[q] * L::SP + tid] = (__bf16)0.f;
         const int ky = tid / GSUB, kx = tid - ky * GSUB;
         const int cy = ky + 1 - sy, cx = kx + 1 - sx;
         const int py = wy0 + cy, px = wx0 + cx;
         const bool sok = inimg(py, px);
-        const __bf16* o = oms + (cy * GWIN + cx) * 32;
-        const float mk = sigm((float)o[18 + t]);
+        float oy, ox, ml;
+        if constexpr (LEAN) {
+          oy = bf_lo(so2), ox = bf_hi(so2), ml = bf_lo(sml);
+          if (t + 1 < 9) somload(t + 1);
+        } else {
+          const __bf16* o = oms + (cy * GWIN + cx) * 32;
+          oy = (float)o[2 * t], ox = (float)o[2 * t + 1], ml = (float)o[18 + t];
+        }
+        const float mk = sigm(ml);
         Corners c0;
-        sample((float)(py - 1 + t / 3) + (float)o[2 * t], (float)(px - 1 + t % 3) + (float)o[2 * t + 1], a.H, a.W, c0);
+        sample((float)(py - 1 + t / 3) + oy, (float)(px - 1 + t % 3) + ox, a.H, a.W, c0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           const int qy = c0.y0 + (q >> 1) - h0, qx = c0.x0 + (q & 1) - w0;
           prevq[q] = -1;
           if (sok && c0.ok[q] && qy >= 0 && qy < GT && qx >= 0 && qx < GT) {
             prevq[q] = qy * GT + qx;
-            S[prevq[q] * GSP + tid] = (__bf16)(mk * c0.w[q]);
+            S[prevq[q] * L::SP + tid] = (__bf16)(mk * c0.w[q]);
             hit[qy >> 1] = true;
           }
         }
@@ -743,7 +808,8 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
         const int rlo = gsrc_row(32 * kk + 4 * g + q4, sy, sx), rhi = gsrc_row(32 * kk + 16 + 4 * g + q4, sy, sx);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          v4s aa[2] = {tr16(dyw + rlo * GDP + 16 * j + 4 * p4), tr16(dyw + rhi * GDP + 16 * j + 4 * p4)};
+          v4s aa[2] = {tr16(dyw + rlo * L::DP + dsw<LEAN>(rlo, 16 * j + 4 * p4)),
+                       tr16(dyw + rhi * L::DP + dsw<LEAN>(rhi, 16 * j + 4 * p4))};
           ga[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(aa), fbs, ga[j], 0, 0, 0);
         }
       }
@@ -930,7 +996,7 @@ extern "C" int adr_dcn_bwd_bf16(const void* x, int xcs, const void* om, int omcs
   hipStream_t s = (hipStream_t)stream;
   const int blocks = N * cdiv(H, GT) * cdiv(W, GT);
   static const int mode = getenv("ADR_DCN_BWD_MODE") ? atoi(getenv("ADR_DCN_BWD_MODE")) : 0;  // A/B: 1/2 skip a phase
-  if (C == 64) hipLaunchKernelGGL((dcn_bwd_kernel<1, 1, 2>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
+  if (C == 64) hipLaunchKernelGGL((dcn_bwd_kernel<1, 1, 3>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
   else if (C == 128) hipLaunchKernelGGL((dcn_bwd_kernel<2, 2, 2>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
   else hipLaunchKernelGGL((dcn_bwd_kernel<4, 4, 2>), dim3(blocks), dim3(256), 0, s, a, dxf, tile_flags, mode);
   if (int rc = check_launch("adr_dcn_bwd_bf16")) return rc;
@@ -1039,7 +1105,7 @@ extern "C" int adr_dcn_bwd_bf16_levels(const adr_dcn_level* lv, int levels, int 
   L.start[levels] = total;
   hipStream_t s = (hipStream_t)stream;
   static const int mode = getenv("ADR_DCN_BWD_MODE") ? atoi(getenv("ADR_DCN_BWD_MODE")) : 0;
-  if (C == 64) hipLaunchKernelGGL((dcn_bwd_levels_kernel<1, 1, 2>), dim3(total), dim3(256), 0, s, L, mode);
+  if (C == 64) hipLaunchKernelGGL((dcn_bwd_levels_kernel<1, 1, 3>), dim3(total), dim3(256), 0, s, L, mode);
   else if (C == 128) hipLaunchKernelGGL((dcn_bwd_levels_kernel<2, 2, 2>), dim3(total), dim3(256), 0, s, L, mode);
   else hipLaunchKernelGGL((dcn_bwd_levels_kernel<4, 4, 2>), dim3(total), dim3(256), 0, s, L, mode);
   if (int rc = check_launch("adr_dcn_bwd_bf16_levels")) return rc;
