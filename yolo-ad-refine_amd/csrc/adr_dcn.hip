@@ -441,7 +441,8 @@ struct GLds {
   static constexpr bool LEAN = CC == 1 && CO == 1;
   static constexpr int PW1 = 64 * CO + 8;                                  // phase-1 slab pitch [c][co]
   static constexpr int OMS = LEAN ? 0 : GCELL * 32 * 2;                    // om rows of the neighbourhood
-  static constexpr int P1X = GCELL * GXP * 2, P1W = (SB ? 1 : 2) * 64 * PW1 * 2, P1D = 64 * 27 * 4;
+  static constexpr int XP = LEAN ? 68 : GXP;  // x-window pitch: 68 (34 dwords) spreads the corner reads over 32 slots
+  static constexpr int P1X = GCELL * XP * 2, P1W = (SB ? 1 : 2) * 64 * PW1 * 2, P1D = 64 * 27 * 4;
   static constexpr int P1 = P1X + P1W + P1D;                               // x window | W_t^T slabs | dom sums
   static constexpr int DP = LEAN ? 64 : GDP, SP = LEAN ? 152 : GSP;        // dy-window / S_t row pitches
   static constexpr int WP = LEAN ? 68 : 72;                                // phase-2 W_t slab pitch (8-B rows)
@@ -536,8 +537,14 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
       for (int q = tid; q < GCELL * 8; q += 256) {
         const int cell = q >> 3, ch = (q & 7) * 8;
         const int yy = wy0 + cell / GWIN, xx = wx0 + cell % GWIN;
-        st16(&xwin[cell * GXP + ch],
-             inimg(yy, xx) ? ld16(a.x + (long)(ibase + yy * a.W + xx) * a.xcs + cc * 64 + ch) : z4);
+        const u32x4 v = inimg(yy, xx) ? ld16(a.x + (long)(ibase + yy * a.W + xx) * a.xcs + cc * 64 + ch) : z4;
+        __bf16* d = &xwin[cell * L::XP + ch];
+        if constexpr (LEAN) {  // 136-byte rows: two 8-byte stores
+          *reinterpret_cast<u32x2*>(d) = (u32x2){v.x, v.y};
+          *reinterpret_cast<u32x2*>(d + 4) = (u32x2){v.z, v.w};
+        } else {
+          st16(d, v);
+        }
       }
       wstore(slab0);
       __syncthreads();
@@ -579,7 +586,7 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
           if (cy >= 0 && cy < GWIN && cx >= 0 && cx < GWIN) {
 #pragma unroll
             for (int i = 0; i < 4; ++i)
-              xv[i] = *reinterpret_cast<const u32x2*>(&xwin[(cy * GWIN + cx) * GXP + 16 * i + 4 * g]);
+              xv[i] = *reinterpret_cast<const u32x2*>(&xwin[(cy * GWIN + cx) * L::XP + 16 * i + 4 * g]);
           } else {
             const int pix = ibase + yy * a.W + xx;
 #pragma unroll
