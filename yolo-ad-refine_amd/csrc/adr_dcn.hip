@@ -32,6 +32,8 @@ namespace {
 typedef short v4s __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 typedef __attribute__((ext_vector_type(2))) unsigned int u32x2;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ v4s tr16(const __bf16* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p)); }
 
@@ -547,11 +549,17 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
         }
       }
       wstore(slab0);
+      if (!L::SB) wload(1, cc);
       __syncthreads();
 #pragma unroll 1
       for (int t = 0; t < 9; ++t) {
         const __bf16* sl = (t & 1) ? slab1 : slab0;
-        if (t + 1 < 9) wload(t + 1, cc);
+        if (L::SB) {
+          if (t + 1 < 9) wload(t + 1, cc);
+        } else {  // two slabs: W_{t+1} (loaded during tap t-1) into the slab tap t-1 read, then fetch W_{t+2}
+          if (t + 1 < 9) wstore((t & 1) ? slab0 : slab1);
+          if (t + 2 < 9) wload(t + 2, cc);
+        }
         f32x4 acc[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -562,7 +570,6 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
                 *reinterpret_cast<const bf16x8*>(&sl[(16 * i + (lane & 15)) * L::PW1 + 32 * k + 8 * g]), fb[k], acc[i], 0,
                 0, 0);
         }
-        if (!L::SB && t + 1 < 9) wstore((t & 1) ? slab0 : slab1);  // last read in tap t-1, before the barrier below
         float oy, ox, ml;
         if constexpr (LEAN) {
           oy = bf_lo(po2), ox = bf_hi(po2), ml = bf_lo(pml);
@@ -576,33 +583,53 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
         // the four corners' channels 16 i + 4 g .. +3: from the staged neighbourhood, or (corner outside it) global.
         // The bilinear value and its two slopes are linear in the corners, so the channel sums are taken per corner
         // first (D_q = sum_c dcols_c x_qc: one FMA per channel and corner) and interpolated once per lane.
+        // Corners inside the 14x14 neighbourhood (|offset| < ~3 px) read the staged window; the rest are fetched
+        // from global in a separate, wave-uniform branch, so the common path never waits on the memory counter
+        // (the next tap's W_t^T slab loads stay in flight under the LDS reads and the FMAs).
+        u32x2 xv[4][4];
+        bool farq[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int cy = c0.y0 + (q >> 1) - wy0, cx = c0.x0 + (q & 1) - wx0;
+          const bool inwin = (unsigned)cy < (unsigned)GWIN && (unsigned)cx < (unsigned)GWIN;
+          farq[q] = !inwin && pok && c0.ok[q];
+          const __bf16* xr0 = &xwin[(inwin ? cy * GWIN + cx : 0) * L::XP + 4 * g];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) xv[q][i] = *reinterpret_cast<const u32x2*>(xr0 + 16 * i);
+        }
+        if (__ballot(farq[0] || farq[1] || farq[2] || farq[3])) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int pix = ibase + (c0.y0 + (q >> 1)) * a.W + c0.x0 + (q & 1);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(
+                  xr, farq[q] ? (unsigned)(pix * a.xcs + cc * 64 + 16 * i + 4 * g) * 2u : OOR, 0, 0);
+              if (farq[q]) xv[q][i] = v;
+            }
+          }
+          __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) here, so the common path below carries no wait
+        }
+        // D_q on the packed bf16 dot unit: dcols rounded to bf16 pairs once per tap (the products are exact in
+        // fp32, the sums fp32), 8 v_dot2 per corner instead of 16 conversions + 16 FMAs
+        bf16x2 dp[4][2];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          dp[i][0] = (bf16x2){(__bf16)acc[i][0], (__bf16)acc[i][1]};
+          dp[i][1] = (bf16x2){(__bf16)acc[i][2], (__bf16)acc[i][3]};
+        }
         float D[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int yy = c0.y0 + (q >> 1), xx = c0.x0 + (q & 1);
-          const int cy = yy - wy0, cx = xx - wx0;
-          const bool ok = pok && c0.ok[q];
-          u32x2 xv[4];
-          if (cy >= 0 && cy < GWIN && cx >= 0 && cx < GWIN) {
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              xv[i] = *reinterpret_cast<const u32x2*>(&xwin[(cy * GWIN + cx) * L::XP + 16 * i + 4 * g]);
-          } else {
-            const int pix = ibase + yy * a.W + xx;
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-              xv[i] = __builtin_amdgcn_raw_buffer_load_b64(
-                  xr, ok ? (unsigned)(pix * a.xcs + cc * 64 + 16 * i + 4 * g) * 2u : OOR, 0, 0);
-          }
           float d = 0.f;
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            d += acc[i][0] * __uint_as_float(xv[i].x << 16);
-            d += acc[i][1] * __uint_as_float(xv[i].x & 0xFFFF0000u);
-            d += acc[i][2] * __uint_as_float(xv[i].y << 16);
-            d += acc[i][3] * __uint_as_float(xv[i].y & 0xFFFF0000u);
+            // whole-vector bit cast + swizzles: hipcc (ROCm 7.2) folds bit_cast(bf16x2, v.y) to v.x
+            const bf16x4 v = __builtin_bit_cast(bf16x4, xv[q][i]);
+            d = __builtin_amdgcn_fdot2_f32_bf16(dp[i][0], v.xy, d, false);
+            d = __builtin_amdgcn_fdot2_f32_bf16(dp[i][1], v.zw, d, false);
           }
-          D[q] = ok ? d : 0.f;
+          D[q] = pok && c0.ok[q] ? d : 0.f;
         }
         const float top = D[0] + c0.lx * (D[1] - D[0]);
         const float bot = D[2] + c0.lx * (D[3] - D[2]);
