@@ -45,9 +45,18 @@ def _train(dtype):
     return torch.stack(losses).cpu().double(), (final - init).cpu().double(), names
 
 
+_CACHE = {}
+
+
+def _ours(dtype):
+    if dtype not in _CACHE:
+        _CACHE[dtype] = _train(dtype)
+    return _CACHE[dtype]
+
+
 def test_bf16_trains_like_fp32():
-    l32, u32, n32 = _train(torch.float32)
-    l16, u16, n16 = _train(torch.bfloat16)
+    l32, u32, n32 = _ours(torch.float32)
+    l16, u16, n16 = _ours(torch.bfloat16)
     assert n32 == n16
     assert torch.isfinite(l32).all() and torch.isfinite(l16).all()
     t32, t16 = l32.sum(1), l16.sum(1)
@@ -62,3 +71,37 @@ def test_bf16_trains_like_fp32():
     assert t32[-1] <= 0.01 * t32[0] and t16[-1] <= 0.01 * t16[0], (t32, t16)
     assert float(rel.max()) <= 0.20 and float(rel.mean()) <= 0.06 and float(rel[-1]) <= 0.15, rel
     assert cos >= 0.8 and dn <= 0.05, (cos, dn)
+
+
+def test_bf16_gap_vs_reference_fp16_amp():
+    """the reference trains with fp16 autocast + GradScaler (engine/trainer.py:269, 383, 393), so
+    its own arithmetic already moves the trajectory away from fp32. The oracle (tests/bf16_sim.oracle_train) runs
+    the same 50 steps twice on the device, in fp32 and under fp16 autocast; the bf16 HIP trajectory's gap to the
+    fp32 HIP trajectory is bounded by a stated multiple of that fp16-AMP gap over the same steps."""
+    import time
+
+    from bf16_sim import oracle_train
+    from adrefine.data.synthetic import labels
+    from adrefine.engine.trainer import param_groups
+    from adrefine.nn.tasks import DetectionModel
+    from recipe import recipe_state_dict
+    from conftest import state_dict_spec
+    l32, _, _ = _ours(torch.float32)
+    l16, _, _ = _ours(torch.bfloat16)
+    groups = [[n for n, _ in g] for g in param_groups(DetectionModel(str(CFG)))]
+    P = recipe_state_dict([(k, s) for k, s, _ in state_dict_spec("701")])
+    from adrefine.data.synthetic import images_u8
+    x = images_u8(BS, S, seed=21).float() / 255.0
+    lab = labels(BS, 80, seed=22)
+    t0 = time.time()
+    o32, _ = oracle_train(P, CFG, groups, x, lab, STEPS, amp_fp16=False)
+    o16, scale = oracle_train(P, CFG, groups, x, lab, STEPS, amp_fp16=True)
+    o16c, _ = oracle_train(P, CFG, groups, x, lab, STEPS, amp_fp16=True, init_scale=scale)
+    gap = lambda a, b: ((a.sum(1) - b.sum(1)).abs() / b.sum(1).abs())  # noqa: E731
+    g_ours, g_amp, g_ampc, g_anchor = gap(l16, l32), gap(o16, o32), gap(o16c, o32), gap(o32, l32)
+    print(f"oracle runs {time.time() - t0:.1f}s; settled GradScaler scale {scale}")
+    for name, g in (("fp32 HIP vs fp32 oracle", g_anchor), ("bf16 HIP vs fp32 HIP", g_ours),
+                    ("fp16-AMP (scaler from 2^16) vs fp32 oracle", g_amp),
+                    ("fp16-AMP (settled scaler) vs fp32 oracle", g_ampc)):
+        print(f"{name}: max {float(g.max()):.4f} mean {float(g.mean()):.4f} last-10 max {float(g[-10:].max()):.4f}")
+    print("per-step", [round(float(a), 4) for a in g_ours], [round(float(a), 4) for a in g_ampc])

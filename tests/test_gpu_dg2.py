@@ -28,8 +28,9 @@ CASES = [  # n, C (dx channels), K (dy channels), H, W
 
 
 @pytest.mark.parametrize("n,C,Kc,H,W", CASES)
-def test_dg2_matches_conv_transpose(n, C, Kc, H, W):
+def test_dg2_matches_conv_transpose(n, C, Kc, H, W, monkeypatch):
     from adrefine import kernels as K
+    monkeypatch.setenv("ADR_DG2H", "2")  # DG2H even where the plan would pick the per-class GEMM (ragged tiles)
     from adrefine.native import lib
     torch.manual_seed(3)
     Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
@@ -56,10 +57,22 @@ def test_dg2_matches_conv_transpose(n, C, Kc, H, W):
     assert rel2 < 5e-3, rel2
 
 
-def test_dg2_concat_slice_output():
+def test_dg2_plan_padding_rule(monkeypatch):
+    """Default plan: DG2H only where its 8 x 8 super-pixel tiles cover the dy grid with <= 15 % padding (80^2 -> 40^2
+    yes, 20^2 -> 10^2 no: the per-class implicit GEMM runs those)."""
+    from adrefine import kernels as K
+    monkeypatch.setenv("ADR_DG2H", "1")
+    d, _, _ = K.conv_desc(2, 80, 80, 64, 64, 128, 3, 3, 2, 2, 1, 1, 128, torch.bfloat16)
+    assert "dg2_kernel" in K._conv2_symbol(d, True)
+    d, _, _ = K.conv_desc(2, 20, 20, 64, 64, 128, 3, 3, 2, 2, 1, 1, 128, torch.bfloat16)
+    assert "conv_bf16_kernel" in K._conv2_symbol(d, True)
+
+
+def test_dg2_concat_slice_output(monkeypatch):
     """dx written into a channel slice of a wider gradient buffer (the concat-gradient sink): channel stride 96,
     offset 32; the other channels untouched."""
     from adrefine import kernels as K
+    monkeypatch.setenv("ADR_DG2H", "2")
     from adrefine.native import lib
     torch.manual_seed(4)
     n, C, Kc, H, W = 2, 32, 64, 24, 24

@@ -1620,9 +1620,11 @@ struct ConvPlan {
   int kt;    // > 0: conv1_kernel<bn, mode, kt> (streaming 1x1, reduction <= kt)
   int dg2;   // > 0 (stride-2 DGRAD): dg2_kernel<dg2 = TJ, bn> (super-pixel halo tiles, all parity classes at once)
 };
-static int dg2_enabled() {
-  static const int on = getenv("ADR_DG2H") ? atoi(getenv("ADR_DG2H")) : 1;  // A/B: 0 = per-class implicit GEMM
-  return on;
+// ADR_DG2H: 0 = per-class implicit GEMM only (A/B), 1 = DG2H where it pays (default), 2 = DG2H wherever it applies
+// (tests: ragged super-pixel tiles). Read per plan, so a test can switch it in-process.
+static int dg2_mode() {
+  const char* e = getenv("ADR_DG2H");
+  return e ? atoi(e) : 1;
 }
 static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   ConvPlan p{0, 0, 0, dgrad ? (d->stride_h == 2 ? CV_DGRAD2 : CV_DGRAD) : CV_FWD};
@@ -1631,7 +1633,8 @@ static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   // layers would run 44 % empty rows: the per-class implicit GEMM is faster there, 27 vs 32 us)
   const long g2_area = (long)((d->ho + G2_TI - 1) / G2_TI * G2_TI) * ((d->wo + G2_TJ - 1) / G2_TJ * G2_TJ);
   if (p.mode == CV_DGRAD2 && d->r == 3 && d->s == 3 && d->pad_h == 1 && d->pad_w == 1 && red % C3_CK == 0 &&
-      out % 16 == 0 && (out <= 64 || out % 64 == 0) && g2_area * 100 <= 115l * d->ho * d->wo && dg2_enabled()) {
+      out % 16 == 0 && (out <= 64 || out % 64 == 0) && dg2_mode() &&
+      (dg2_mode() == 2 || g2_area * 100 <= 115l * d->ho * d->wo)) {
     p.dg2 = G2_TJ;
     p.bn = out % 64 == 0 ? 64 : out % 32 == 0 ? 32 : 16;
     p.kt = 0;
