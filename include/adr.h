@@ -169,6 +169,9 @@ typedef struct adr_wgrad_job {
   int accumulate, pad_;
 } adr_wgrad_job;
 int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int count, void* stream);
+/* The tile kernel a job of adr_conv2d_wgrad_partials_batched goes to: bm * 256 + bn of the grouped
+ * wgrad_bf16_batched_kernel<bm, bn>, or 0 when the job runs its own thin / 3x3-halo kernel (bench timing labels). */
+int adr_conv2d_wgrad_batched_tile(const adr_conv_desc* d);
 int adr_conv2d_wgrad_partials(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
                               void* stream);
 int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accumulate, void* stream);

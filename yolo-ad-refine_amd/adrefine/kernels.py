@@ -668,7 +668,7 @@ class WgradDeferral:
     destination's contributions still accumulate in program order."""
 
     def __init__(self):
-        self.jobs, self.jkeep = [], []  # deferred WGRAD partial launches (grouped by tile shape at the flush)
+        self.jobs, self.jkeep, self.jwork = [], [], []  # deferred WGRAD partial launches
         self.entries, self.keep, self.dsts = [], [], set()
         self.psums, self.pkeep, self.pdsts = [], [], set()
         self.axpys, self.akeep, self.adsts = [], [], set()
@@ -726,7 +726,7 @@ class WgradDeferral:
         self.pkeep.append(part)
         self.pdsts.add(dst)
 
-    def add_job(self, d, xp, dyp, ws, keep):
+    def add_job(self, d, xp, dyp, ws, keep, work=(0, 0), shp=""):
         """A conv's WGRAD partials into `ws`, launched at the flush together with the stage's other weight gradients
         (adr_conv2d_wgrad_partials_batched: one launch per tile shape, bitwise the per-conv launches). x and dy stay
         alive (keep) and dy is pinned so no fan-out accumulates into it in place before the flush reads it."""
@@ -735,6 +735,7 @@ class WgradDeferral:
                 t._adr_pinned = True
                 _v(t)[0]._adr_pinned = True
         self.jobs.append(WgradJob(ConvDesc.from_buffer_copy(d), xp, dyp, ws.data_ptr(), 0, 0))
+        self.jwork.append((work, shp))
         self.jkeep += [ws, *keep]
 
     def add(self, ws, stride, splits, dst, K_, C_, Cp, RS_, transpose_kc, acc):
@@ -748,11 +749,38 @@ class WgradDeferral:
     def flush(self):
         self._flush()
 
+    def _timed_jobs(self):
+        """bench.py's roofline timing: the same grouped launches the step makes (one per tile shape, at most
+        WGB_MAX = 24 jobs each), each bracketed by HIP events and labelled with the grouped kernel and the summed
+        algorithmic bytes / flops of its jobs; thin / halo jobs (their own kernels) one call each. The partial
+        writes are idempotent, so each call repeats TIMING_REPEAT times inside its event pair."""
+        groups = {}
+        for job, (work, shp) in zip(self.jobs, self.jwork):
+            tile = lib.adr_conv2d_wgrad_batched_tile(ctypes.byref(job.d))
+            groups.setdefault(tile, []).append((job, work, shp))
+        for tile, items in groups.items():
+            step = 24 if tile else 1
+            for i in range(0, len(items), step):
+                part = items[i:i + step]
+                name = (f"void adr::wgrad_bf16_batched_kernel<{tile // 256}, {tile % 256}>(adr::WgBatch)" if tile
+                        else "adr_conv2d_wgrad (thin / 3x3 halo kernel)")
+                nb = sum(w[0] for _, w, _ in part)
+                fl = sum(w[1] for _, w, _ in part)
+                arr = (WgradJob * len(part))(*[j for j, _, _ in part])
+                rep = TIMING_REPEAT
+                tok = _t0(name, nb, fl, " + ".join(sh for _, _, sh in part), rep)
+                for _ in range(rep):
+                    lib.adr_conv2d_wgrad_partials_batched(ctypes.cast(arr, ctypes.c_void_p), len(part), stream())
+                _t1(tok)
+
     def _flush(self):
         if self.jobs:  # the deferred weight-gradient partials, before their reductions
-            arr = (WgradJob * len(self.jobs))(*self.jobs)
-            lib.adr_conv2d_wgrad_partials_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.jobs), stream())
-            self.jobs, self.jkeep = [], []
+            if _TIMING is None:
+                arr = (WgradJob * len(self.jobs))(*self.jobs)
+                lib.adr_conv2d_wgrad_partials_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.jobs), stream())
+            else:
+                self._timed_jobs()
+            self.jobs, self.jkeep, self.jwork = [], [], []
         if self.dots:  # before the axpys that add their outputs into the arena
             arr = (DotsumEntry * len(self.dots))(*self.dots)
             lib.adr_dotsum_batched(ctypes.cast(arr, ctypes.c_void_p), len(self.dots), stream())
@@ -855,9 +883,10 @@ def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep=()
     ws = torch.empty(splits * stride, dtype=torch.float32, device=device)
     Cp = max(C_, cpad)
     out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
-    if (_DEFER_WGRAD and keep and _dfr() is not None and acc and _TIMING is None and d.dtype == BF16 and
+    if (_DEFER_WGRAD and keep and _dfr() is not None and acc and d.dtype == BF16 and
             splits * stride * 4 <= DEFER_MAX_BYTES):
-        _dfr().add_job(d, xp, dyp, ws, keep)  # partials at the flush, grouped with the stage's other convs'
+        # partials at the flush, grouped with the stage's other convs' (timed there per grouped launch)
+        _dfr().add_job(d, xp, dyp, ws, keep, work, shp)
         _dfr().add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
         return grad_ret(param, out)
     rep = _reps()

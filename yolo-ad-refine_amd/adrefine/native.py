@@ -123,7 +123,7 @@ _NONSTATUS = {"adr_abi_version", "adr_conv2d_fwd_stat_tiles", "adr_conv2d_fwd_bf
               "adr_fp8_amax_blocks", "adr_conv2d_fp8_supported", "adr_conv2d_fwd_fp8_stat_tiles",
               "adr_dwconv_fwd_act_supported", "adr_conv2d_bf16_xf_reuse", "adr_augment_desc_size",
               "adr_dcn_bwd_tiles", "adr_conv2d_fwd_bf16_bnact_stat_tiles",
-              "adr_conv2d_dgrad_bf16_stat_tiles"}
+              "adr_conv2d_dgrad_bf16_stat_tiles", "adr_conv2d_wgrad_batched_tile"}
 _ = _NONSTATUS
 
 lib = _Lib()

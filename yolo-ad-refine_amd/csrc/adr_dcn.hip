@@ -722,6 +722,16 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
 #pragma unroll
     for (int i = 0; i < 4; ++i) dxa[cc][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int q4 = (lane >> 2) & 3, p4 = lane & 3;
+  // neighbourhood row of this lane's sub-window sources at tap (0, 0) shift, per K step and half (-1: k >= GK, the
+  // window's zero row); a tap subtracts its uniform shift sy * GWIN + sx
+  int gbase[GKS][2];
+#pragma unroll
+  for (int kk = 0; kk < GKS; ++kk)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int k = 32 * kk + 16 * h + 4 * g + q4;
+      gbase[kk][h] = k < GK ? gsrc_row(k, 0, 0) : -1;
+    }
   const __bf16* Sq = S + (16 * wave + (lane & 15)) * L::SP;  // this lane's destination row of S_t
   u32x4 wreg[2];
   auto wissue = [&](int t, int cc, int coc) {
@@ -840,7 +850,8 @@ __device__ __forceinline__ void dcn_bwd_body(const DcnArgs& a, float* dxf, int* 
         const __bf16* sr = Sq + 32 * kk + 4 * g;
         u32x2 bs[2] = {*reinterpret_cast<const u32x2*>(sr), *reinterpret_cast<const u32x2*>(sr + 16)};
         const bf16x8 fbs = *reinterpret_cast<bf16x8*>(bs);
-        const int rlo = gsrc_row(32 * kk + 4 * g + q4, sy, sx), rhi = gsrc_row(32 * kk + 16 + 4 * g + q4, sy, sx);
+        const int tsh = sy * GWIN + sx;
+        const int rlo = gbase[kk][0] < 0 ? GCELL : gbase[kk][0] - tsh, rhi = gbase[kk][1] < 0 ? GCELL : gbase[kk][1] - tsh;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           v4s aa[2] = {tr16(dyw + rlo * L::DP + dsw<LEAN>(rlo, 16 * j + 4 * p4)),

@@ -718,6 +718,12 @@ using namespace adr;
 // The WGRAD partials of `count` convs (bf16 engine), each exactly as adr_conv2d_wgrad_partials(job) would write them:
 // the jobs on the generic tile kernel are grouped by tile shape into launches of up to WGB_MAX (one launch per shape
 // instead of one per conv); the 3x3 halo-tile / thin-channel ones run their own launches.
+extern "C" int adr_conv2d_wgrad_batched_tile(const adr_conv_desc* d) {
+  if (!d || d->dtype != ADR_BF16) return 0;
+  const WgPlan p = wgrad_bf16_plan(d);
+  return (p.thin || p.tw3) ? 0 : p.bm * 256 + p.bn;
+}
+
 extern "C" int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int count, void* stream) {
   ADR_REQUIRE(count >= 0 && (count == 0 || jobs), "wgrad partials batched: count=%d", count);
   hipStream_t st = (hipStream_t)stream;
