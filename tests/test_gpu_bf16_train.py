@@ -76,8 +76,16 @@ def test_bf16_trains_like_fp32():
 def test_bf16_gap_vs_reference_fp16_amp():
     """the reference trains with fp16 autocast + GradScaler (engine/trainer.py:269, 383, 393), so
     its own arithmetic already moves the trajectory away from fp32. The oracle (tests/bf16_sim.oracle_train) runs
-    the same 50 steps twice on the device, in fp32 and under fp16 autocast; the bf16 HIP trajectory's gap to the
-    fp32 HIP trajectory is bounded by a stated multiple of that fp16-AMP gap over the same steps."""
+    the same 50 steps on the device in fp32 and under fp16 autocast; the bf16 HIP trajectory's gap to the fp32 HIP
+    trajectory (per-step relative gap of the total loss) is bounded by 1.5x the fp16-AMP gap over the same steps,
+    in mean and in max.
+
+    The AMP run is taken with the GradScaler already settled (init_scale = the scale the reference's default 2^16
+    start reaches after the same 50 steps, here 16): from 2^16 the loss (x batch size) overflows fp16 in the
+    backward, so the first ~13 steps are skipped, and that trajectory lags fp32 by up to 434x at step 14 before it
+    catches up (printed below, not bounded). Measured (round 5): bf16 HIP vs fp32 HIP mean 0.031, max 0.107;
+    fp16-AMP (settled) vs fp32 oracle mean 0.060, max 0.175 — ratios 0.52 / 0.61; fp32 HIP vs fp32 oracle itself
+    drifts to mean 0.023, max 0.095 over the 50 steps (the trajectory amplifies last-bit differences)."""
     import time
 
     from bf16_sim import oracle_train
@@ -105,3 +113,5 @@ def test_bf16_gap_vs_reference_fp16_amp():
                     ("fp16-AMP (settled scaler) vs fp32 oracle", g_ampc)):
         print(f"{name}: max {float(g.max()):.4f} mean {float(g.mean()):.4f} last-10 max {float(g[-10:].max()):.4f}")
     print("per-step", [round(float(a), 4) for a in g_ours], [round(float(a), 4) for a in g_ampc])
+    assert float(g_ours.mean()) <= 1.5 * float(g_ampc.mean()), (float(g_ours.mean()), float(g_ampc.mean()))
+    assert float(g_ours.max()) <= 1.5 * float(g_ampc.max()), (float(g_ours.max()), float(g_ampc.max()))

@@ -2218,7 +2218,7 @@ class ScaleFn(torch.autograd.Function):
     """x * g (+ res) with g a device tensor broadcast as: 'scalar' (shape ()), 'n' (N,), 'c' (C,), 'nc' (N, C)."""
 
     @staticmethod
-    def forward(ctx, x, g, res, mode, box=None):
+    def forward(ctx, x, g, res, mode, box=None, from_out=False):
         vx = _v(x)
         N, C, H, W = x.shape
         gs = g.detach().float().contiguous()
@@ -2228,7 +2228,10 @@ class ScaleFn(torch.autograd.Function):
         lib.adr_bcast_mul(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], fptr(gs), gns, gcs,
                           ctypes.c_void_p(vr[1]) if vr else None, vr[2] if vr else 0, ctypes.c_void_p(op),
                           ocs, N, H * W, C, 0, stream())
-        ctx.save_for_backward(vx[0], gs)
+        # from_out (bf16, per-image gates feeding a normalisation): dg = sum(dy * out) / g from the very tensor the
+        # next op consumed, instead of sum(dy * x) from the separately rounded x
+        ctx.from_out = from_out and mode == "n" and res is None and x.dtype == torch.bfloat16
+        ctx.save_for_backward(out if ctx.from_out else vx[0], gs)
         ctx.meta = (mode, g.shape, res is not None)
         ctx.pg = g
         ctx.sink, ctx.sres = _sink_of(x), (getattr(res, "_adr_sink", None) if res is not None else None)
@@ -2256,13 +2259,18 @@ class ScaleFn(torch.autograd.Function):
                 out = torch.empty(1, dtype=torch.float32, device=x.device)
                 _dfr().add_dotsum(x, vd[0], out)
                 dg = sink(ctx.pg, out.view(gshape))
+            elif ctx.from_out:
+                dg = sink(ctx.pg, (_reduce_dot(x, vd[0], sum_n, sum_c) / gs.clamp_min(1e-30)).view(gshape))
             else:
                 dg = sink(ctx.pg, _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape))
-        return dx, dg, (_defer_pass(ctx.sres, dy) if has_res else None), None, None
+        return dx, dg, (_defer_pass(ctx.sres, dy) if has_res else None), None, None, None
 
 
-def scale(x, g, mode, res=None, out=None):
-    return ScaleFn.apply(x, g, res, mode, None if out is None else OutBox(out))
+def scale(x, g, mode, res=None, out=None, grad_from_out=False):
+    """x * g broadcast by `mode`. grad_from_out: the gate gradient of a per-image gate ('n') is taken from the
+    output (sum(dy * out) / g) — used where a normalisation follows, whose input gradient is orthogonal to the
+    output it normalised, so the near-zero true gate gradient is not buried under the rounding of x (bf16)."""
+    return ScaleFn.apply(x, g, res, mode, None if out is None else OutBox(out), grad_from_out)
 
 
 class WeightedSumFn(torch.autograd.Function):

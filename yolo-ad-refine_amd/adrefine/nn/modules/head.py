@@ -121,7 +121,7 @@ class TaskDecomposition(nn.Module):
                        "relu", "sigmoid")  # (N, 1)
         y, _ = K.conv2d(feat, self.reduction_conv.conv.weight, None, 1, 0)
         s = s.view(-1) if pack is None else K.seg_expand(s.view(-1), pack)  # packed: the image's gate per sub-image
-        y = K.scale(y, s, "n")
+        y = K.scale(y, s, "n", grad_from_out=True)  # GroupNorm follows: d/ds from the GN input itself
         if pack is not None:
             return K.gn_act_packed(y, pack, [self.reduction_conv.gn], "silu")
         return K.gn_act(y, self.reduction_conv.gn, "silu")
