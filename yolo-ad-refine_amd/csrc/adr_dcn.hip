@@ -386,9 +386,13 @@ __device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tile
 __global__ void __launch_bounds__(256, 2) dcn_wgrad_kernel(DcnArgs a) {
   dcn_wgrad_body(a, xcd_order(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y), gridDim.x);
 }
+// Levels dispatch in order (P3's long split blocks first, the short P5 blocks fill the tail) and the XCD grouping is
+// applied within a level: interleaving the three levels over the whole grid started long P3 blocks last (l-scale:
+// 7.6 ms for the three levels in one launch against 4.1 ms as three launches)
 __global__ void __launch_bounds__(256, 2) dcn_wgrad_levels_kernel(DcnLevels L) {
-  const int b = xcd_order(blockIdx.x, gridDim.x), l = dcn_level(L, b);
-  dcn_wgrad_body(L.a[l], b - L.start[l], L.tiles[l]);
+  const int l = dcn_level(L, blockIdx.x), s0 = L.start[l];
+  const int b = xcd_order(blockIdx.x - s0, L.start[l + 1] - s0);
+  dcn_wgrad_body(L.a[l], b, L.tiles[l]);
 }
 
 // ------------------------------------------------------------------------------------------------------------
