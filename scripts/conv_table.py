@@ -11,6 +11,7 @@ sys.path.insert(0, str(ROOT / "yolo-ad-refine_amd"))
 ap = argparse.ArgumentParser()
 ap.add_argument("--bs", type=int, default=64)
 ap.add_argument("--steps", type=int, default=2)
+ap.add_argument("--by-gap", action="store_true", help="sort by time above the attainable roofline (8 TB/s, 2.5 PF)")
 args = ap.parse_args()
 
 import torch
@@ -36,6 +37,13 @@ for tag, shape, nb, fl, t in K.timing_detail():  # every timed libadr launch, ke
     a[0] += 1; a[1] += nb or 0; a[2] += fl or 0; a[3] += t
 tot = sum(v[3] for v in agg.values()) / args.steps
 print(f"timed total per step: {1e3 * tot:.2f} ms")
-for shape, (n, nb, fl, t) in sorted(agg.items(), key=lambda kv: -kv[1][3])[:200]:
+def att(v):  # attainable time of the entry's launches: max(bytes / HBM peak, flops / bf16 MFMA peak) per launch
+    n, nb, fl, t = v
+    return n * max(nb / n / 8e12, fl / n / 2.5e15)
+
+
+key = (lambda kv: -(kv[1][3] - att(kv[1]))) if args.by_gap else (lambda kv: -kv[1][3])
+for shape, (n, nb, fl, t) in sorted(agg.items(), key=key)[:200]:
+    a = att((n, nb, fl, t))
     print(f"{1e3 * t / args.steps:7.3f} ms {n // args.steps:3d}x {1e6 * t / n:8.1f}us {nb / t / 1e9:7.0f} GB/s "
-          f"{fl / t / 1e12:6.1f} TF/s  {shape}")
+          f"{fl / t / 1e12:6.1f} TF/s  att {a / t:5.2f} gap {1e3 * (t - a) / args.steps:6.3f} ms  {shape}")

@@ -14,6 +14,14 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture(autouse=True)
+def _xf_everywhere(monkeypatch):
+    """The engine declines the XF data gradient where it measured slower (the per-tile engine instead of the
+    streaming 1x1 kernel, DG2H; adr_conv2d_bf16_xf_reuse). Those fused kernels stay correct and tested: take them."""
+    monkeypatch.setenv("ADR_XF_STREAM", "1")
+    monkeypatch.setenv("ADR_XF_DG2", "1")
+
+
+@pytest.fixture(autouse=True)
 def _no_bstat():
     """These tests pin the XF fusions bitwise against the unfused pairs. The BN backward statistics taken in the
     consumer's data gradient (BSTAT) sum the same terms in another order — tested on its own in test_gpu_bstat.py —

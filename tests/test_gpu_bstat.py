@@ -21,6 +21,14 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _xf_everywhere(monkeypatch):
+    """BSTAT with the XF operand transform on every kernel family, including the ones whose XF path the engine
+    declines by default (adr_conv2d_bf16_xf_reuse)."""
+    monkeypatch.setenv("ADR_XF_STREAM", "1")
+    monkeypatch.setenv("ADR_XF_DG2", "1")
+
+
 def _nhwc(t):
     return t.contiguous(memory_format=torch.channels_last)
 

@@ -1838,6 +1838,19 @@ extern "C" int adr_conv2d_fwd_bf16_bnact(const adr_conv_desc* d, const void* y, 
 // replaces only when each element is staged about once (adr_conv2d_{fwd,dgrad}_bf16_bnact callers test this).
 extern "C" int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad) {
   const ConvPlan pl = conv_plan(d, dgrad != 0, true);
+  if (dgrad) {
+    // an XF data gradient that would leave the streaming 1x1 kernel for the per-tile engine is latency-bound on the
+    // large thin maps (e.g. 160^2 x 32 -> 48: 187 us fused against ~70 us for the BN-act pass + streaming dgrad)
+    // and so is the stride-2 halo-tile one on the stem-side maps (320^2 x 16 <- 160^2 x 32: 291 us fused, the BN-act
+    // pass + plain DG2H are faster; same-box step A/B 20.93 -> 20.83 ms). ADR_XF_STREAM / ADR_XF_DG2 / ADR_XF_CONV3
+    // = 1 keep the fusion there (A/B only).
+    const char* es = getenv("ADR_XF_STREAM");
+    const char* eg = getenv("ADR_XF_DG2");
+    const char* e3 = getenv("ADR_XF_CONV3");
+    if (!(es && atoi(es)) && conv_plan(d, true, false).kt > 0 && pl.kt == 0) return 1 << 20;
+    if (!(eg && atoi(eg)) && pl.dg2) return 1 << 20;
+    if (e3 && !atoi(e3) && pl.tw) return 1 << 20;
+  }
   const int out = dgrad ? d->c : d->k;
   const int nt = pl.tw ? out / pl.bn : cdiv(out, pl.bn);
   if (pl.dg2) return nt * 100 * (G2_TI + 1) * (pl.dg2 + 1) / (G2_TI * pl.dg2);
