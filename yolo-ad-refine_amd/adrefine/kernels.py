@@ -1241,7 +1241,7 @@ _BNXF_PENDING = {}
 BN_XF_FWD = bool(int(__import__("os").environ.get("ADR_BN_XF_FWD", "1")))
 # the forward transform is one affine + activation per staged element (the backward's needs a second operand and
 # the BN-backward linear term): two column tiles of the streaming 1x1 kernel still qualify
-BN_XF_FWD_MAX_REUSE = 200
+BN_XF_FWD_MAX_REUSE = int(__import__("os").environ.get("ADR_BN_XF_FWD_MAX_REUSE", "200"))
 _BNF_PENDING = {}  # storage data_ptr -> BnFwd
 
 
