@@ -86,3 +86,35 @@ def test_network_train_step_loss_and_grads(tag):
         if abs(mine - v) > 2e-3 * v + floor:
             bad.append((k, mine, v))
     assert not bad, bad[:10]
+
+
+@pytest.mark.parametrize("kind", ["random", "zeros", "tiny"])
+def test_tal_topk_fast_path_equals_serial(kind, monkeypatch):
+    """TAL top-10 (utils/tal.py select_topk_candidates): the parallel fast path (unique top-10 set) and the serial
+    heap-select (ADR_TAL_TOPK_SERIAL=1, the path rows with ties at the cut take) give bitwise the same loss and
+    gradients. 'random' features: COCO-shape labels at bs 8 / 640 (long positive runs -> fast path; small boxes with
+    fewer than 10 positive anchors -> T = 0 ties -> serial). 'zeros': every anchor predicts the same box and score,
+    so mirror-symmetric anchors tie exactly at T > 0 (the fallback on tied cuts). 'tiny': boxes shrunk 8x, so most
+    rows have fewer than 10 positive align values (T = 0: the short heap simulation)."""
+    from adrefine.data.synthetic import labels
+    from adrefine.utils.loss import v8DetectionLoss
+    S, bs = 640, 8
+    _, fd = _feats(S, bs, 11, torch.float32)
+    if kind == "zeros":
+        fd = [torch.zeros_like(f).requires_grad_(True) for f in fd]
+    batch = labels(bs, 80, seed=5)
+    if kind == "tiny":
+        batch["bboxes"][:, 2:] /= 8
+    crit = v8DetectionLoss(_M())
+    out = {}
+    for ser in ("1", "0"):
+        monkeypatch.setenv("ADR_TAL_TOPK_SERIAL", ser)
+        for f in fd:
+            f.grad = None
+        loss, items = crit(fd, batch)
+        loss.backward()
+        out[ser] = (loss.detach().clone(), items.clone(), [f.grad.clone() for f in fd])
+    assert torch.equal(out["0"][0], out["1"][0]) and torch.equal(out["0"][1], out["1"][1])
+    for a, b in zip(out["0"][2], out["1"][2]):
+        assert torch.equal(a, b)
+    assert float(out["0"][1].abs().sum()) > 0

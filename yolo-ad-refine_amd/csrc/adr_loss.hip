@@ -280,10 +280,29 @@ __device__ void adjust_heap(KV* f, int hole, int len, KV value) {
   f[hole] = value;
 }
 
-// One wave per (image, gt) row, same sequence of heap operations as the scalar heap-select: candidates are
-// screened 64 at a time against the current heap top (a ballot), and only those that beat it are inserted,
-// in index order, by lane 0 on an LDS heap — so the selected set, ties included, is exactly libstdc++'s.
-__global__ void __launch_bounds__(256) tal_topk_kernel(const float* align, uint8_t* flags, int rows, int A) {
+__device__ __forceinline__ float wave_max_f(float v) {
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// One wave per (image, gt) row (reference utils/tal.py select_topk_candidates: torch.topk(metrics, 10), whose CPU
+// kernel is libstdc++'s partial_sort / heap-select with comp(x, y) = x > y).
+// Fast path — exact whenever the top-10 SET is unique: each lane keeps the 10 largest of its strided slice of the
+// row in registers (sorted, statically unrolled insertion; an element enters only when it beats the lane's 10th);
+// the row's 10th largest T (with multiplicity) is merged from the 64 lists by wave max/sum rounds. When exactly 10
+// elements are >= T (no tie spills over the cut) every correct top-k selects the same set, and the lanes flag
+// their entries >= T. Otherwise — ties at T beyond the cut (typically T = 0: fewer than 10 positive align values),
+// a lane list truncated at a value equal to T, or a NaN — the heap-select itself decides which tied elements stay,
+// so the row runs the serial path below. Round 5: 177 -> see DESIGN §9 (the serial heap on long positive runs was
+// one dependent LDS chain per insert).
+// Serial path: the same sequence of heap operations as the scalar heap-select: candidates are screened 64 at a
+// time against the current heap top (a ballot), and only those that beat it are inserted, in index order, by
+// lane 0 on an LDS heap — so the selected set, ties included, is exactly libstdc++'s.
+__global__ void __launch_bounds__(256) tal_topk_kernel(const float* align, uint8_t* flags, int rows, int A, int serial) {
   __shared__ KV heap[4][TOPK];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int r = blockIdx.x * 4 + wave;
@@ -295,6 +314,110 @@ __global__ void __launch_bounds__(256) tal_topk_kernel(const float* align, uint8
   if (A <= TOPK) {
     for (int a = lane; a < A; a += 64) fl[a] |= 2;
     return;
+  }
+  if (!serial) {
+    float lv[TOPK];
+    int li[TOPK];
+#pragma unroll
+    for (int k = 0; k < TOPK; ++k) {
+      lv[k] = -INFINITY;
+      li[k] = -1;
+    }
+    bool nan = false, neg = false;
+    auto insert = [&](float v, int a) {
+      nan |= v != v;
+      neg |= v < 0.f;
+      if (v > lv[TOPK - 1]) {
+        float cv = v;
+        int ci = a;
+#pragma unroll
+        for (int k = 0; k < TOPK; ++k) {  // strict >: an equal value stays behind the earlier index
+          const bool sw = cv > lv[k];
+          const float tv = lv[k];
+          const int ti = li[k];
+          lv[k] = sw ? cv : tv;
+          li[k] = sw ? ci : ti;
+          cv = sw ? tv : cv;
+          ci = sw ? ti : ci;
+        }
+      }
+    };
+    int a = lane;
+    for (; a + 192 < A; a += 256) {
+      const float v0 = m[a], v1 = m[a + 64], v2 = m[a + 128], v3 = m[a + 192];
+      insert(v0, a);
+      insert(v1, a + 64);
+      insert(v2, a + 128);
+      insert(v3, a + 192);
+    }
+    for (; a < A; a += 64) insert(m[a], a);
+    // merge: T = the row's TOPK-th largest; h = own entries strictly above the current candidate
+    int need = TOPK, h = 0, tot = 0;
+    float T = -INFINITY;
+    for (int round = 0; round < TOPK; ++round) {
+      float hv = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < TOPK; ++k) hv = (k == h) ? lv[k] : hv;
+      const float mx = wave_max_f(hv);
+      int c = 0;
+#pragma unroll
+      for (int k = 0; k < TOPK; ++k) c += (k >= h && lv[k] == mx) ? 1 : 0;
+      tot = wave_sum_i(c);
+      if (tot >= need || mx == -INFINITY) {
+        T = mx;
+        break;
+      }
+      need -= tot;
+      h += c;
+    }
+    // a full list ending at T may have dropped further elements equal to T
+    const bool trunc = li[TOPK - 1] >= 0 && lv[TOPK - 1] == T;
+    const bool ambiguous = __ballot(nan || trunc) != 0ull || tot != need || T == -INFINITY;
+    if (!ambiguous) {
+#pragma unroll
+      for (int k = 0; k < TOPK; ++k)
+        if (li[k] >= 0 && lv[k] >= T) fl[li[k]] |= 2;
+      return;
+    }
+    // T == 0 with no negative / NaN element: fewer than TOPK positives, so the heap always holds a zero and its
+    // top stays 0 — every positive at index >= TOPK is inserted (in index order) and no zero ever is. The heap-select
+    // is then make_heap(first TOPK) + one adjust_heap per such positive; all positives sit in the lane lists.
+    if (T == 0.f && __ballot(nan || neg) == 0ull) {
+      KV* hp = heap[wave];
+      __shared__ KV posq[4][TOPK];
+      int base = 0;
+#pragma unroll
+      for (int k = 0; k < TOPK; ++k) {
+        const bool p = li[k] >= TOPK && lv[k] > 0.f;
+        const unsigned long long msk = __ballot(p);
+        if (p) posq[wave][base + __popcll(msk & ((1ull << lane) - 1ull))] = KV{lv[k], li[k]};
+        base += __popcll(msk);
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        for (int k = 0; k < TOPK; ++k) hp[k] = KV{m[k], k};
+        for (int parent = (TOPK - 2) / 2;; --parent) {  // make_heap
+          adjust_heap(hp, parent, TOPK, hp[parent]);
+          if (parent == 0) break;
+        }
+        for (int q = 1; q < base; ++q) {  // scan order = index order (insertion sort of <= TOPK - 1 entries)
+          const KV e = posq[wave][q];
+          int j = q - 1;
+          while (j >= 0 && posq[wave][j].i > e.i) {
+            posq[wave][j + 1] = posq[wave][j];
+            --j;
+          }
+          posq[wave][j + 1] = e;
+        }
+        for (int q = 0; q < base; ++q) {
+          const KV e = posq[wave][q];
+          if (e.v > hp[0].v) adjust_heap(hp, 0, TOPK, e);
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      if (lane < TOPK) fl[hp[lane].i] |= 2;
+      return;
+    }
   }
   KV* h = heap[wave];
   if (lane == 0) {
@@ -722,7 +845,10 @@ extern "C" int adr_det_loss(int dtype, const void* f0, const void* f1, const voi
   if (nmax > 0) {
     long tot = (long)rows * A;
     LDISPATCH(tal_metrics_kernel, dim3(cdiv(tot, 256)), dim3(256), L, B, nmax, nc, gt, pbox, align, ovl, flags);
-    hipLaunchKernelGGL(tal_topk_kernel, dim3(cdiv((long)rows, 4)), dim3(256), 0, st, align, flags, (int)rows, A);
+    // ADR_TAL_TOPK_SERIAL=1: every row on the serial heap-select (the tie path; tests compare the two bitwise)
+    const char* ser = getenv("ADR_TAL_TOPK_SERIAL");
+    hipLaunchKernelGGL(tal_topk_kernel, dim3(cdiv((long)rows, 4)), dim3(256), 0, st, align, flags, (int)rows, A,
+                       ser && atoi(ser) != 0 ? 1 : 0);
     hipLaunchKernelGGL(tal_assign_kernel, dim3(cdiv((long)n, 256)), dim3(256), 0, st, flags, ovl, B, nmax, A, tgi, fg);
     hipLaunchKernelGGL(tal_norm_kernel, dim3((unsigned)rows), dim3(256), 0, st, align, ovl, tgi, fg, B, nmax, A, pos);
   } else {

@@ -204,6 +204,143 @@ __global__ void __launch_bounds__(256) stem_wgrad_kernel(const TI* __restrict__ 
   }
 }
 
+// weight gradient, persistent form (rows of the image fit one LDS plan: W <= STEM_LOOP_W, W % 4 == 0): a block walks
+// a contiguous range of (image, output-row-pair) tiles, accumulating in registers, and the next tile's image words
+// and dy chunks are loaded into registers while the current one runs its MFMA steps — the per-tile kernel above
+// exposed a full load latency per tile at 3 blocks per CU and wrote one partial slab per tile (10 240 at bs 64,
+// 640^2), which the reduce then gathered. Same MFMA steps per tile as above; partials [block][KT*16][32].
+constexpr int STEM_LOOP_W = 640;
+template <typename TI> struct StemWord { typedef unsigned T; };            // 4 uint8 pixels
+template <> struct StemWord<float> { typedef f32x4 T; };                   // 4 fp32 pixels
+__device__ __forceinline__ void stem_put4(__bf16* d, unsigned v) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) d[e] = (__bf16)img_val((uint8_t)(v >> (8 * e)));
+}
+__device__ __forceinline__ void stem_put4(__bf16* d, f32x4 v) {
+#pragma unroll
+  for (int e = 0; e < 4; ++e) d[e] = (__bf16)v[e];
+}
+
+template <int KT, typename TI>
+__global__ void __launch_bounds__(256) stem_wgrad_loop_kernel(const TI* __restrict__ img, int H, int W,
+                                                              const __bf16* __restrict__ dy, int dcs, int Ho, int Wo,
+                                                              int ntiles, int per, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+  constexpr int IR = 2 * STEM_ROWS + 1, NR = 3 * IR;
+  constexpr int DCH = STEM_ROWS * (STEM_LOOP_W / 2) * KT * 2 / 256;  // 16-byte dy chunks per thread
+  typedef typename StemWord<TI>::T Word;
+  const int Wp = W + 2;
+  __bf16* xs = reinterpret_cast<__bf16*>(smraw);                 // [3][IR][Wp]
+  __bf16* ds = xs + ((3 * IR * Wp + 7) & ~7);                    // [STEM_ROWS * Wo][KT * 16]
+  float* red = reinterpret_cast<float*>(smraw);                  // [4][KT*16][32], after the last tile
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nrb = (Ho + STEM_ROWS - 1) / STEM_ROWS;
+  const int t0 = blockIdx.x * per, t1 = min(ntiles, t0 + per);
+  const int W4 = W / 4;
+  if (tid < NR) {  // zero columns -1 and W (never written by the row stores)
+    xs[tid * Wp] = (__bf16)0.f;
+    xs[tid * Wp + W + 1] = (__bf16)0.f;
+  }
+  Word iv[NR];
+  u32x4 dv[DCH];
+  auto load = [&](int tile) {
+    const int rb = tile % nrb, n = tile / nrb;
+    const int oy0 = rb * STEM_ROWS, iy0 = 2 * oy0 - 1, npx = min(STEM_ROWS, Ho - oy0) * Wo;
+#pragma unroll
+    for (int row = 0; row < NR; ++row) {
+      const int c = row / IR, iy = iy0 + row % IR;
+      const bool ok = tid < W4 && iy >= 0 && iy < H;
+      if constexpr (sizeof(Word) == 4) iv[row] = ok ? *reinterpret_cast<const unsigned*>(img + (((long)n * 3 + c) * H + iy) * W + 4 * tid) : 0u;
+      else iv[row] = ok ? *reinterpret_cast<const f32x4*>(img + (((long)n * 3 + c) * H + iy) * W + 4 * tid) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    const __bf16* dyb = dy + ((long)n * Ho + oy0) * Wo * (long)dcs;
+    const int nch = npx * KT * 2;
+#pragma unroll
+    for (int u = 0; u < DCH; ++u) {
+      const int i = tid + 256 * u;
+      if (i < nch) dv[u] = ld16(dyb + (long)(i / (KT * 2)) * dcs + (i % (KT * 2)) * 8);
+    }
+  };
+  auto store = [&](int tile) {
+    const int rb = tile % nrb;
+    const int npx = min(STEM_ROWS, Ho - rb * STEM_ROWS) * Wo, nch = npx * KT * 2;
+    if (tid < W4) {
+#pragma unroll
+      for (int row = 0; row < NR; ++row) stem_put4(xs + row * Wp + 1 + 4 * tid, iv[row]);
+    }
+#pragma unroll
+    for (int u = 0; u < DCH; ++u) {
+      const int i = tid + 256 * u;
+      if (i < nch) *reinterpret_cast<u32x4*>(ds + (long)(i / (KT * 2)) * KT * 16 + (i % (KT * 2)) * 8) = dv[u];
+    }
+  };
+  const int g = lane >> 4, i = lane & 15;
+  int cj[2], kyj[2], kxj[2];
+  bool jok[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const int j = jt * 16 + i;
+    jok[jt] = j < 27;
+    const int jj = jok[jt] ? j : 0;
+    cj[jt] = jj / 9;
+    kyj[jt] = (jj % 9) / 3;
+    kxj[jt] = jj % 3;
+  }
+  f32x4 acc[KT][2];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) acc[t][0] = acc[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (t0 < t1) load(t0);
+  for (int tile = t0; tile < t1; ++tile) {
+    store(tile);
+    __syncthreads();
+    if (tile + 1 < t1) load(tile + 1);
+    const int npx = min(STEM_ROWS, Ho - (tile % nrb) * STEM_ROWS) * Wo;
+    const int nsteps = (npx + 31) / 32;
+    for (int s = wave; s < nsteps; s += 4) {
+      const int pbase = s * 32 + 8 * g;
+      int r = pbase / Wo, ox = pbase - r * Wo;
+      s16x8 a[KT], b[2];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const bool pok = pbase + e < npx;
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          const __bf16 v = pok ? ds[(long)(pbase + e) * KT * 16 + t * 16 + i] : (__bf16)0.f;
+          a[t][e] = *reinterpret_cast<const short*>(&v);
+        }
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+          const __bf16 v = (pok && jok[jt]) ? xs[(cj[jt] * IR + 2 * r + kyj[jt]) * Wp + 2 * ox + kxj[jt]]
+                                            : (__bf16)0.f;
+          b[jt][e] = *reinterpret_cast<const short*>(&v);
+        }
+        if (++ox == Wo) {
+          ox = 0;
+          ++r;
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < KT; ++t)
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+          acc[t][jt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&a[t]),
+                                                               *reinterpret_cast<bf16x8*>(&b[jt]), acc[t][jt], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) red[(wave * KT * 16 + t * 16 + 4 * g + rr) * 32 + jt * 16 + i] = acc[t][jt][rr];
+  __syncthreads();
+  for (int idx = tid; idx < KT * 16 * 32; idx += 256) {
+    const int M = KT * 16 * 32;
+    part[(long)blockIdx.x * M + idx] = (red[idx] + red[M + idx]) + (red[2 * M + idx] + red[3 * M + idx]);
+  }
+}
+
 static size_t stem_wgrad_smem(int Wp, int wseg, int KT) {
   const int IR = 2 * STEM_ROWS + 1;
   return (((size_t)3 * IR * Wp + 7) & ~(size_t)7) * 2 + (size_t)STEM_ROWS * wseg * KT * 16 * 2 +
@@ -260,13 +397,19 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const TI* __restrict__ im
     }
   }
   __syncthreads();
-  float s1[KT], s2[KT];
+  // D^T[k][pixel] = W (16 k x 32 j) * im2col^T (32 j x 16 pixels): the same two register operands as
+  // im2col * W^T with the roles swapped, so lane (g, i) holds output channels t*16 + 4g .. +3 of pixel i — one
+  // 8-byte store per lane, 512 contiguous bytes per wave when ycs == 16 (the D[pixel][k] orientation stored
+  // 2-byte values, four partial 32-byte pieces per cache line per instruction)
+  float s1[KT][4], s2[KT][4];
 #pragma unroll
-  for (int t = 0; t < KT; ++t) s1[t] = s2[t] = 0.f;
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s1[t][rr] = s2[t][rr] = 0.f;
   const int npx = nrow * Wo;
   __bf16* yb = y + ((long)n * Ho + oy0) * Wo * (long)ycs;
   for (int st = wave; st * 16 < npx; st += 4) {
-    // A = im2col: lane supplies A[pixel i][j = 8g + e]
+    // B = im2col^T: lane supplies B[j = 8g + e][pixel i]
     const int p = st * 16 + i;
     const bool pok = p < npx;
     const int r = pok ? p / Wo : 0, ox = pok ? p - r * Wo : 0;
@@ -279,34 +422,37 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const TI* __restrict__ im
 #pragma unroll
     for (int t = 0; t < KT; ++t) {
       f32x4 d = {0.f, 0.f, 0.f, 0.f};
-      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&a), *reinterpret_cast<bf16x8*>(&bw[t]),
+      d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&bw[t]), *reinterpret_cast<bf16x8*>(&a),
                                                   d, 0, 0, 0);
-      // D[pixel 4g + rr][k = t*16 + i]
+      // D[k = t*16 + 4g + rr][pixel i]
+      if (pok) {
+        __bf16 v[4];
 #pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        const int q = st * 16 + 4 * g + rr;
-        if (q < npx) {
-          const __bf16 v = (__bf16)d[rr];
-          yb[(long)q * ycs + t * 16 + i] = v;
-          const float f = (float)v;
-          s1[t] += f;
-          s2[t] += f * f;
+        for (int rr = 0; rr < 4; ++rr) {
+          v[rr] = (__bf16)d[rr];
+          const float f = (float)v[rr];
+          s1[t][rr] += f;
+          s2[t][rr] += f * f;
         }
+        *reinterpret_cast<uint2*>(yb + (long)p * ycs + t * 16 + 4 * g) = *reinterpret_cast<const uint2*>(v);
       }
     }
   }
   if (!stats) return;
 #pragma unroll
-  for (int t = 0; t < KT; ++t) {  // combine the four lane groups (same k), then the waves
-    s1[t] += __shfl_xor(s1[t], 16, 64);
-    s1[t] += __shfl_xor(s1[t], 32, 64);
-    s2[t] += __shfl_xor(s2[t], 16, 64);
-    s2[t] += __shfl_xor(s2[t], 32, 64);
-    if (g == 0) {
-      red[wave][0][t * 16 + i] = s1[t];
-      red[wave][1][t * 16 + i] = s2[t];
+  for (int t = 0; t < KT; ++t)  // combine the 16 pixel lanes of each channel group, then the waves
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[t][rr] += __shfl_xor(s1[t][rr], o, 64);
+        s2[t][rr] += __shfl_xor(s2[t][rr], o, 64);
+      }
+      if (i == 0) {
+        red[wave][0][t * 16 + 4 * g + rr] = s1[t][rr];
+        red[wave][1][t * 16 + 4 * g + rr] = s2[t][rr];
+      }
     }
-  }
   __syncthreads();
   if (threadIdx.x < 2 * KT * 16) {
     const int q = threadIdx.x / (KT * 16), k = threadIdx.x % (KT * 16);
@@ -341,8 +487,9 @@ extern "C" int adr_stem_fwd_tiles(int N, int Ho) { return N * ((Ho + STEM_ROWS -
 template <typename TI>
 static int stem_fwd(const TI* img, int N, int H, int W, const float* w, int K, void* y, int ycs, float* stats,
                     void* stream) {
-  ADR_REQUIRE(N > 0 && H > 1 && W > 1 && (K == 16 || K == 32 || K == 64) && ycs >= K,
-              "stem_conv_fwd: N=%d H=%d W=%d K=%d ycs=%d", N, H, W, K, ycs);
+  ADR_REQUIRE(N > 0 && H > 1 && W > 1 && (K == 16 || K == 32 || K == 64) && ycs >= K && ycs % 4 == 0 &&
+                  ((uintptr_t)y & 7) == 0,
+              "stem_conv_fwd: N=%d H=%d W=%d K=%d ycs=%d (8-byte aligned rows)", N, H, W, K, ycs);
   const int Ho = (H - 1) / 2 + 1, Wo = (W - 1) / 2 + 1;
   ADR_REQUIRE((long)N * Ho * Wo < (1l << 31), "stem_conv_fwd: too many pixels");
   const size_t sm = (((size_t)3 * (2 * STEM_ROWS + 1) * (W + 2) + 7) & ~(size_t)7) * 2;
@@ -390,7 +537,30 @@ static int stem_wgrad(const TI* img, int N, int H, int W, const void* dy, int dc
   const size_t sm = stem_wgrad_smem(segs == 1 ? W + 2 : 2 * wseg + 2, wseg, KT);
   ADR_REQUIRE(sm <= 64 * 1024 && dcs % 8 == 0, "stem_conv_wgrad: W=%d too wide for the LDS plan", W);
   hipStream_t st = (hipStream_t)stream;
-  if (K == 16)
+  int nblk = blocks;
+  if (segs == 1 && W % 4 == 0 && W <= STEM_LOOP_W) {  // persistent form: ~4 blocks per CU, contiguous tile ranges
+    const size_t lsm = (((size_t)3 * (2 * STEM_ROWS + 1) * (W + 2) + 7) & ~(size_t)7) * 2 +
+                       (size_t)STEM_ROWS * Wo * KT * 16 * 2;
+    const size_t lsm_red = (size_t)4 * KT * 16 * 32 * 4;
+    const size_t lsmem = lsm > lsm_red ? lsm : lsm_red;
+    auto kern = K == 16 ? (const void*)stem_wgrad_loop_kernel<1, TI>
+                        : K == 32 ? (const void*)stem_wgrad_loop_kernel<2, TI> : (const void*)stem_wgrad_loop_kernel<4, TI>;
+    int occ = 1, dev = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, lsmem) != hipSuccess || occ < 1) occ = 1;
+    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int want = cus * (occ < 4 ? occ : 4);  // one resident round of blocks
+    const int per = (blocks + want - 1) / want;
+    nblk = (blocks + per - 1) / per;
+    if (K == 16)
+      hipLaunchKernelGGL((stem_wgrad_loop_kernel<1, TI>), dim3(nblk), dim3(256), lsmem, st, img, H, W, (const __bf16*)dy,
+                         dcs, Ho, Wo, blocks, per, ws);
+    else if (K == 32)
+      hipLaunchKernelGGL((stem_wgrad_loop_kernel<2, TI>), dim3(nblk), dim3(256), lsmem, st, img, H, W, (const __bf16*)dy,
+                         dcs, Ho, Wo, blocks, per, ws);
+    else
+      hipLaunchKernelGGL((stem_wgrad_loop_kernel<4, TI>), dim3(nblk), dim3(256), lsmem, st, img, H, W, (const __bf16*)dy,
+                         dcs, Ho, Wo, blocks, per, ws);
+  } else if (K == 16)
     hipLaunchKernelGGL((stem_wgrad_kernel<1, TI>), dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs,
                        Ho, Wo, segs, wseg, ws);
   else if (K == 32)
@@ -399,7 +569,7 @@ static int stem_wgrad(const TI* img, int N, int H, int W, const void* dy, int dc
   else
     hipLaunchKernelGGL((stem_wgrad_kernel<4, TI>), dim3(blocks), dim3(256), sm, st, img, H, W, (const __bf16*)dy, dcs,
                        Ho, Wo, segs, wseg, ws);
-  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(K * 27), dim3(256), 0, st, ws, blocks, K, dw, accumulate);
+  hipLaunchKernelGGL(stem_wgrad_reduce_kernel, dim3(K * 27), dim3(256), 0, st, ws, nblk, K, dw, accumulate);
   return check_launch("adr_stem_conv_wgrad");
 }
 
