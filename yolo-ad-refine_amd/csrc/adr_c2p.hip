@@ -11,6 +11,7 @@
 //     returns dfft[c,uv] = <B_uv, sum_patches dy x^T>.
 #include "adr_common.h"
 #include <cstdlib>
+#include <type_traits>
 
 namespace adr {
 
@@ -134,15 +135,24 @@ __global__ void __launch_bounds__(256) dw_bwd_w_kernel(const T* x, int xcs, cons
 // channels, every LDS access is one 16-byte vector of VW channels.
 template <typename T>
 __device__ __forceinline__ void stage_img(const T* src, int cs, int H, int W, int pad, int cb0, int C, int CB, T* dst) {
-  constexpr int VW = 16 / sizeof(T);
-  const int Hp = H + 2 * pad, Wp = W + 2 * pad, nv = CB / VW;
-  for (int i = threadIdx.x; i < Hp * Wp * nv; i += blockDim.x) {
-    const int pp = i / nv, cv = i % nv;
-    const int yy = pp / Wp - pad, xx = pp % Wp - pad;
-    const int c = cb0 + cv * VW;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W && c < C) v = ld16(src + ((long)yy * W + xx) * cs + c);
-    *reinterpret_cast<u32x4*>(dst + (long)pp * CB + cv * VW) = v;
+  constexpr int VW = 16 / sizeof(T), U = 8;  // U loads in flight per thread (a load-store loop serialises latencies)
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad, nv = CB / VW, tot = Hp * Wp * nv;
+  for (int i0 = threadIdx.x; i0 < tot; i0 += U * blockDim.x) {
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * blockDim.x;
+      const int pp = i / nv, cv = i % nv;
+      const int yy = pp / Wp - pad, xx = pp % Wp - pad;
+      const int c = cb0 + cv * VW;
+      v[u] = (u32x4){0u, 0u, 0u, 0u};
+      if (i < tot && yy >= 0 && yy < H && xx >= 0 && xx < W && c < C) v[u] = ld16(src + ((long)yy * W + xx) * cs + c);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * blockDim.x;
+      if (i < tot) *reinterpret_cast<u32x4*>(dst + (long)(i / nv) * CB + (i % nv) * VW) = v[u];
+    }
   }
 }
 
@@ -151,89 +161,155 @@ template <typename T, int CBT>
 __device__ __forceinline__ void stage_img_f32(const T* src, int cs, int H, int W, int pad, int cb0, int C, int CB,
                                               float* dst) {
   constexpr int VW = (int)(16 / sizeof(T)) < CBT ? (int)(16 / sizeof(T)) : CBT;  // a 4-channel slab: 8-byte bf16 reads
-  const int Hp = H + 2 * pad, Wp = W + 2 * pad, nv = CB / VW;
-  for (int i = threadIdx.x; i < Hp * Wp * nv; i += blockDim.x) {
-    const int pp = i / nv, cv = i % nv;
-    const int yy = pp / Wp - pad, xx = pp % Wp - pad;
-    const int c = cb0 + cv * VW;
-    float f[VW];
+  constexpr int U = 8;  // loads in flight per thread
+  const int Hp = H + 2 * pad, Wp = W + 2 * pad, nv = CB / VW, tot = Hp * Wp * nv;
+  for (int i0 = threadIdx.x; i0 < tot; i0 += U * blockDim.x) {
+    float f[U][VW];
 #pragma unroll
-    for (int e = 0; e < VW; ++e) f[e] = 0.f;
-    if (yy >= 0 && yy < H && xx >= 0 && xx < W && c < C) vload<T, VW>(src + ((long)yy * W + xx) * cs + c, f);
-    float* d = dst + (long)pp * CB + cv * VW;
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * blockDim.x;
+      const int pp = i / nv, cv = i % nv;
+      const int yy = pp / Wp - pad, xx = pp % Wp - pad;
+      const int c = cb0 + cv * VW;
 #pragma unroll
-    for (int e = 0; e < VW; e += 4) *reinterpret_cast<f32x4*>(d + e) = (f32x4){f[e], f[e + 1], f[e + 2], f[e + 3]};
+      for (int e = 0; e < VW; ++e) f[u][e] = 0.f;
+      if (i < tot && yy >= 0 && yy < H && xx >= 0 && xx < W && c < C) vload<T, VW>(src + ((long)yy * W + xx) * cs + c, f[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int i = i0 + u * blockDim.x;
+      if (i >= tot) continue;
+      float* d = dst + (long)(i / nv) * CB + (i % nv) * VW;
+#pragma unroll
+      for (int e = 0; e < VW; e += 4)
+        *reinterpret_cast<f32x4*>(d + e) = (f32x4){f[u][e], f[u][e + 1], f[u][e + 2], f[u][e + 3]};
+    }
   }
 }
 
 // y = dwconv(x, w) (+b) or dx (+)= dwconv^T(dy, w): items (pixel, VW-channel vector), taps from the LDS image
 // EPI (eval DWConv-BN-act, adr_dwconv_fwd_act): the BatchNorm scale folds into the staged fp32 taps, the shift is
-// the bias, and the activation is applied before the store — the reference's fuse_conv_and_bn on a depthwise conv
-template <typename T, bool BWD, int CB, bool EPI>
+// the bias, and the activation is applied before the store — the reference's fuse_conv_and_bn on a depthwise conv.
+// F32S (bf16 tensors whose fp32 padded slab fits the LDS plan): the image is converted to fp32 once at staging, so a
+// tap is two 16-byte LDS reads + four v_pk_fma_f32 per 8 channels instead of eight conversions + eight FMAs — the
+// kernel is VALU-bound (a 7x7 at 20x20: 27 us at ~12 TF/s). Per output the sum is bias + taps in (ky, kx) order,
+// each an fp32 fma: bitwise the same for every variant.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+template <typename T, bool BWD, int CB, bool EPI, bool F32S = false>
 __device__ __forceinline__ void dw_img_body(const T* x, int xcs, const float* w, const float* b, T* y, int ycs, int H,
                                             int W, int C, int k, int accumulate, const float* escale, int eact) {
   constexpr int VW = 16 / sizeof(T), NV = CB / VW;
+  typedef typename std::conditional<F32S, float, T>::type S;  // LDS image element
   extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
   const int n = blockIdx.x, cb0 = blockIdx.y * CB, p = k / 2, kk = k * k;
   const int Wp = W + 2 * p;
   float* wl = reinterpret_cast<float*>(dwsm);                        // [kk][CB]
-  T* xs = reinterpret_cast<T*>(dwsm + (size_t)kk * CB * sizeof(float));
+  S* xs = reinterpret_cast<S*>(dwsm + (size_t)kk * CB * sizeof(float));
   for (int i = threadIdx.x; i < kk * CB; i += 256) {
     const int t = i / CB, c = cb0 + i % CB;
     wl[i] = c < C ? w[(long)c * kk + t] * (EPI ? escale[c] : 1.f) : 0.f;
   }
-  stage_img<T>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
+  if constexpr (F32S) stage_img_f32<T, CB>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
+  else stage_img<T>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
   __syncthreads();
-  for (int it = threadIdx.x; it < H * W * NV; it += 256) {
-    const int pix = it / NV, cv = it % NV, c = cb0 + cv * VW;
-    if (c >= C) continue;
-    const int oy = pix / W, ox = pix % W;
-    float acc[VW];
+  // items (pixel, VW-channel vector): 256 % NV == 0, so a thread's vector cv is fixed and it walks pixels
+  // threadIdx / NV + j * (256 / NV), four at a time with the tap loop outside (a tap's weights read once per four)
+  static_assert(256 % NV == 0, "dw_img_body: NV must divide the block");
+  constexpr int PQ = 4, PSTEP = 256 / NV;
+  const int cv = threadIdx.x % NV, c = cb0 + cv * VW;
+  if (c < C) {
+    for (int p0 = threadIdx.x / NV; p0 < H * W; p0 += PQ * PSTEP) {
+      f32x2 acc[PQ][VW / 2];
+      int base[PQ];
+      bool ok[PQ];
 #pragma unroll
-    for (int e = 0; e < VW; ++e) acc[e] = (!BWD && b) ? b[c + e] : 0.f;
-    for (int ky = 0; ky < k; ++ky)
-      for (int kx = 0; kx < k; ++kx) {
-        // forward: x[oy + ky - p][ox + kx - p] = padded row oy + ky; data gradient: taps mirrored
-        const int py = BWD ? oy + 2 * p - ky : oy + ky, px = BWD ? ox + 2 * p - kx : ox + kx;
-        const u32x4 v = *reinterpret_cast<const u32x4*>(xs + ((long)py * Wp + px) * CB + cv * VW);
-        const T* e8 = reinterpret_cast<const T*>(&v);
-        const float* wt = wl + (ky * k + kx) * CB + cv * VW;
+      for (int q = 0; q < PQ; ++q) {
+        const int pix = p0 + q * PSTEP;
+        ok[q] = pix < H * W;
+        const int pp = ok[q] ? pix : 0, oy = pp / W, ox = pp % W;
+        // forward: x[oy + ky - p][ox + kx - p] = padded row oy + ky; data gradient: taps mirrored (from 2p)
+        base[q] = BWD ? (oy + 2 * p) * Wp + ox + 2 * p : oy * Wp + ox;
 #pragma unroll
-        for (int e = 0; e < VW; ++e) acc[e] += to_f(e8[e]) * wt[e];
+        for (int e = 0; e < VW / 2; ++e)
+          acc[q][e] = (!BWD && b) ? (f32x2){b[c + 2 * e], b[c + 2 * e + 1]} : (f32x2){0.f, 0.f};
       }
-    T* dst = y + ((long)n * H * W + pix) * ycs + c;
-    if (BWD && accumulate) {
-      const u32x4 pv = ld16(dst);
-      const T* pe = reinterpret_cast<const T*>(&pv);
+      for (int ky = 0; ky < k; ++ky)
+        for (int kx = 0; kx < k; ++kx) {
+          f32x2 wv[VW / 2];
+          const float* wt = wl + (ky * k + kx) * CB + cv * VW;
 #pragma unroll
-      for (int e = 0; e < VW; ++e) acc[e] += to_f(pe[e]);
-    }
-    if constexpr (EPI) {
+          for (int e = 0; e < VW; e += 4) {
+            const f32x4 w4 = *reinterpret_cast<const f32x4*>(wt + e);
+            wv[e / 2] = (f32x2){w4[0], w4[1]};
+            wv[e / 2 + 1] = (f32x2){w4[2], w4[3]};
+          }
+          const int toff = BWD ? -(ky * Wp + kx) : ky * Wp + kx;
 #pragma unroll
-      for (int e = 0; e < VW; ++e) {
-        const float v = acc[e];
-        acc[e] = eact == ACT_SILU ? act_fwd_c<ACT_SILU, true>(v) : eact == ACT_SIGMOID ? act_fwd_c<ACT_SIGMOID, true>(v)
+          for (int q = 0; q < PQ; ++q) {
+            if (!ok[q]) continue;
+            const S* src = xs + ((long)(base[q] + toff)) * CB + cv * VW;
+            f32x2 xv[VW / 2];
+            if constexpr (sizeof(S) == 4) {
+#pragma unroll
+              for (int e = 0; e < VW; e += 4) {
+                const f32x4 x4 = *reinterpret_cast<const f32x4*>(src + e);
+                xv[e / 2] = (f32x2){x4[0], x4[1]};
+                xv[e / 2 + 1] = (f32x2){x4[2], x4[3]};
+              }
+            } else {
+              const u32x4 v = *reinterpret_cast<const u32x4*>(src);
+              const T* e8 = reinterpret_cast<const T*>(&v);
+#pragma unroll
+              for (int e = 0; e < VW / 2; ++e) xv[e] = (f32x2){to_f(e8[2 * e]), to_f(e8[2 * e + 1])};
+            }
+#pragma unroll
+            for (int e = 0; e < VW / 2; ++e) acc[q][e] = __builtin_elementwise_fma(xv[e], wv[e], acc[q][e]);
+          }
+        }
+#pragma unroll
+      for (int q = 0; q < PQ; ++q) {
+        if (!ok[q]) continue;
+        float a[VW];
+#pragma unroll
+        for (int e = 0; e < VW / 2; ++e) {
+          a[2 * e] = acc[q][e][0];
+          a[2 * e + 1] = acc[q][e][1];
+        }
+        T* dst = y + ((long)n * H * W + p0 + q * PSTEP) * ycs + c;
+        if (BWD && accumulate) {
+          const u32x4 pv = ld16(dst);
+          const T* pe = reinterpret_cast<const T*>(&pv);
+#pragma unroll
+          for (int e = 0; e < VW; ++e) a[e] += to_f(pe[e]);
+        }
+        if constexpr (EPI) {
+#pragma unroll
+          for (int e = 0; e < VW; ++e) {
+            const float v = a[e];
+            a[e] = eact == ACT_SILU ? act_fwd_c<ACT_SILU, true>(v) : eact == ACT_SIGMOID ? act_fwd_c<ACT_SIGMOID, true>(v)
                                                                     : act_fwd(eact, v);
+          }
+        }
+        u32x4 o;
+        T* oe = reinterpret_cast<T*>(&o);
+#pragma unroll
+        for (int e = 0; e < VW; ++e) oe[e] = from_f<T>(a[e]);
+        st16(dst, o);
       }
     }
-    u32x4 o;
-    T* oe = reinterpret_cast<T*>(&o);
-#pragma unroll
-    for (int e = 0; e < VW; ++e) oe[e] = from_f<T>(acc[e]);
-    st16(dst, o);
   }
 }
 
-template <typename T, bool BWD, int CB>
+template <typename T, bool BWD, int CB, bool F32S = false>
 __global__ void __launch_bounds__(256) dw_img_kernel(const T* x, int xcs, const float* w, const float* b, T* y,
                                                      int ycs, int H, int W, int C, int k, int accumulate) {
-  dw_img_body<T, BWD, CB, false>(x, xcs, w, b, y, ycs, H, W, C, k, accumulate, nullptr, 0);
+  dw_img_body<T, BWD, CB, false, F32S>(x, xcs, w, b, y, ycs, H, W, C, k, accumulate, nullptr, 0);
 }
-template <int CB>
+template <int CB, bool F32S = false>
 __global__ void __launch_bounds__(256) dw_img_act_kernel(const __bf16* x, int xcs, const float* w, const float* scale,
                                                          const float* shift, int act, __bf16* y, int ycs, int H, int W,
                                                          int C, int k) {
-  dw_img_body<__bf16, false, CB, true>(x, xcs, w, shift, y, ycs, H, W, C, k, 0, scale, act);
+  dw_img_body<__bf16, false, CB, true, F32S>(x, xcs, w, shift, y, ycs, H, W, C, k, 0, scale, act);
 }
 
 // weight gradient: items (tap, 4-channel group, pixel split PS) over fp32 copies of the padded image and of dy
@@ -727,6 +803,24 @@ __global__ void edffn_build_kernel(const float* w, const float* Bm, int C, int n
   M[i] = s;
 }
 
+// the same, 8 channels per thread (the basis element read once for 8 channels, loads of the u loop in flight):
+// per output the same fp32 sum over u in order
+__global__ void __launch_bounds__(256) edffn_build8_kernel(const float* w, const float* Bm, int C, int nuv, float* M) {
+  const int e = blockIdx.x * 256 + threadIdx.x, c0 = blockIdx.y * 8;
+  if (e >= 4096) return;
+  float s[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) s[q] = 0.f;
+#pragma unroll 4
+  for (int u = 0; u < nuv; ++u) {
+    const float b = Bm[(long)u * 4096 + e];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] += w[(c0 + q) * nuv + u] * b;
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) M[(long)(c0 + q) * 4096 + e] = s[q];
+}
+
 // y_patch = M_c x_patch for every 8x8 patch of channel c (transpose: M_c^T, the backward).
 // Block = one channel x EDFFN_PPB patches; lane = patch position: the lane keeps its row (column for the
 // transpose) of M_c in 64 registers, the wave stages each patch's 64 inputs in LDS and every lane reads them
@@ -771,6 +865,110 @@ __global__ void __launch_bounds__(256) edffn_apply_kernel(const T* x, int xcs, c
     } else {
       float* scratch = reinterpret_cast<float*>(y);
       scratch[(((long)n * ph_n * 8 + yy) * (pw_n * 8) + xx) * C + c] = s;
+    }
+  }
+}
+
+// The same apply on the fp32 matrix cores (bf16 tensors): block = 8 channels x 16 patches. The per-channel kernel above
+// reads one 2-byte element of a 256-byte pixel row per lane (every channel block re-fetches every line): 63 us per
+// call at bs 64, 20x20, C = 128. Here a 16-byte load brings a pixel's 8 channels into LDS as fp32 [ch][pos][patch]
+// (pitch 17: the four k-slot row groups of an MFMA B read fall on disjoint banks), each wave runs two channels as
+// D (64 positions x 16 patches) = M_c (64 x 64) * X_c (64 x 16) on v_mfma_f32_16x16x4_f32 — exact fp32 products,
+// fp32 sums — with the reduction index of step js, slot g being j = 16g + js so a lane's A values are 16 consecutive
+// floats of one M row (four 16-byte loads; the transpose reads M columns, lanes along i, coalesced), and the result
+// goes through LDS [patch][pos][ch] so the stores are 16-byte (bf16) / 32-byte (fp32 scratch) pixel rows.
+constexpr int EA_CG = 8, EA_PG = 16, EA_XP = EA_PG + 1, EA_YP = 64 * EA_CG + 4;
+template <bool TR>
+__global__ void __launch_bounds__(256) edffn_apply_mfma_kernel(const __bf16* x, int xcs, const float* M, void* yv,
+                                                               int ycs, int N, int H, int W, int C) {
+  __shared__ __attribute__((aligned(16))) float Xs[EA_CG * 64 * EA_XP];
+  __shared__ __attribute__((aligned(16))) float Ys[EA_PG * EA_YP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int ncg = C / EA_CG, cg = blockIdx.x % ncg, pg = blockIdx.x / ncg;
+  const int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8, ppi = ph_n * pw_n, npatch = N * ppi;
+  const int c0 = cg * EA_CG;
+  // stage: item (patch p, position pos), p fastest
+  {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = tid + 256 * u, pl = it % EA_PG, pos = it / EA_PG, pp = pg * EA_PG + pl;
+      v[u] = (u32x4){0u, 0u, 0u, 0u};
+      if (pp < npatch) {
+        const int n = pp / ppi, q = pp % ppi;
+        const int yy = (q / pw_n) * 8 + pos / 8, xx = (q % pw_n) * 8 + pos % 8;
+        if (!TR) v[u] = ld16(x + (((long)n * H + reflect_idx(yy, H)) * W + reflect_idx(xx, W)) * xcs + c0);
+        else if (yy < H && xx < W) v[u] = ld16(x + (((long)n * H + yy) * W + xx) * xcs + c0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = tid + 256 * u, pl = it % EA_PG, pos = it / EA_PG;
+      const __bf16* e = reinterpret_cast<const __bf16*>(&v[u]);
+#pragma unroll
+      for (int ch = 0; ch < EA_CG; ++ch) Xs[(ch * 64 + pos) * EA_XP + pl] = to_f(e[ch]);
+    }
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int cc = 0; cc < 2; ++cc) {
+    const int ch = wave * 2 + cc;
+    const float* Mc = M + (long)(c0 + ch) * 4096;
+    f32x4 acc[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) acc[it] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    float a[4][16];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int i = it * 16 + cl;
+      if (!TR) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const f32x4 m4 = *reinterpret_cast<const f32x4*>(Mc + i * 64 + 16 * g + 4 * q);
+          a[it][4 * q] = m4[0]; a[it][4 * q + 1] = m4[1]; a[it][4 * q + 2] = m4[2]; a[it][4 * q + 3] = m4[3];
+        }
+      } else {
+#pragma unroll
+        for (int js = 0; js < 16; ++js) a[it][js] = Mc[(16 * g + js) * 64 + i];
+      }
+    }
+    const float* xb = Xs + (ch * 64 + 16 * g) * EA_XP + cl;
+#pragma unroll
+    for (int js = 0; js < 16; ++js) {
+      const float bv = xb[js * EA_XP];
+#pragma unroll
+      for (int it = 0; it < 4; ++it) acc[it] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[it][js], bv, acc[it], 0, 0, 0);
+    }
+    // D[i = it*16 + 4g + r][patch cl]
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) Ys[cl * EA_YP + (it * 16 + 4 * g + r) * EA_CG + ch] = acc[it][r];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int it = tid + 256 * u, pl = it % EA_PG, pos = it / EA_PG, pp = pg * EA_PG + pl;
+    if (pp >= npatch) continue;
+    const int n = pp / ppi, q = pp % ppi;
+    const int yy = (q / pw_n) * 8 + pos / 8, xx = (q % pw_n) * 8 + pos % 8;
+    const float* ys = Ys + pl * EA_YP + pos * EA_CG;
+    const f32x4 lo = *reinterpret_cast<const f32x4*>(ys), hi = *reinterpret_cast<const f32x4*>(ys + 4);
+    if (!TR) {
+      if (yy < H && xx < W) {
+        u32x4 o;
+        __bf16* oe = reinterpret_cast<__bf16*>(&o);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          oe[e] = from_f<__bf16>(lo[e]);
+          oe[4 + e] = from_f<__bf16>(hi[e]);
+        }
+        st16(reinterpret_cast<__bf16*>(yv) + (((long)n * H + yy) * W + xx) * ycs + c0, o);
+      }
+    } else {
+      float* d = reinterpret_cast<float*>(yv) + (((long)n * ph_n * 8 + yy) * (pw_n * 8) + xx) * C + c0;
+      *reinterpret_cast<f32x4*>(d) = lo;
+      *reinterpret_cast<f32x4*>(d + 4) = hi;
     }
   }
 }
@@ -854,6 +1052,122 @@ __global__ void __launch_bounds__(256) edffn_dw_kernel(const T* x, int xcs, cons
   for (int e = tid; e < 4096; e += 256) out[e] = (dM[0][e] + dM[1][e]) + (dM[2][e] + dM[3][e]);
 }
 
+// The dM partials on the fp32 matrix cores (bf16 tensors): block = 8 channels x one of EDFFN_DWS patch splits;
+// chunks of 16 patches of dY (real pixels, zero padding) and X (reflect-padded) are staged as fp32 [ch][pos][patch]
+// (16-byte pixel loads), and each wave accumulates two channels' 64 x 64 dM = dY (64 x P) * X^T (P x 64) over its
+// split on v_mfma_f32_16x16x4_f32 (16 f32x4 tiles per channel). The per-channel kernel above gathered one 2-byte
+// element of a 256-byte pixel row per lane (48 us per call at bs 64, 20x20, C = 128). Same partial layout.
+template <bool UNUSED = false>
+__global__ void __launch_bounds__(256) edffn_dw_mfma_kernel(const __bf16* x, int xcs, const __bf16* dy, int dcs,
+                                                            int N, int H, int W, int C, float* part) {
+  __shared__ __attribute__((aligned(16))) float Ds[EA_CG * 64 * EA_XP];
+  __shared__ __attribute__((aligned(16))) float Xs[EA_CG * 64 * EA_XP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, cl = lane & 15;
+  const int ncg = C / EA_CG, cg = blockIdx.x % ncg, sp = blockIdx.x / ncg;
+  const int pw_n = (W + 7) / 8, ph_n = (H + 7) / 8, ppi = ph_n * pw_n, npatch = N * ppi;
+  const int nchunk = (npatch + EA_PG - 1) / EA_PG, per = (nchunk + EDFFN_DWS - 1) / EDFFN_DWS;
+  const int k0 = sp * per, k1 = min(nchunk, k0 + per);
+  const int c0 = cg * EA_CG;
+  f32x4 acc[2][16];
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc)
+#pragma unroll
+    for (int t = 0; t < 16; ++t) acc[cc][t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int kc = k0; kc < k1; ++kc) {
+    u32x4 vx[4], vd[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = tid + 256 * u, pl = it % EA_PG, pos = it / EA_PG, pp = kc * EA_PG + pl;
+      vx[u] = vd[u] = (u32x4){0u, 0u, 0u, 0u};
+      if (pp < npatch) {
+        const int n = pp / ppi, q = pp % ppi;
+        const int yy = (q / pw_n) * 8 + pos / 8, xx = (q % pw_n) * 8 + pos % 8;
+        vx[u] = ld16(x + (((long)n * H + reflect_idx(yy, H)) * W + reflect_idx(xx, W)) * xcs + c0);
+        if (yy < H && xx < W) vd[u] = ld16(dy + (((long)n * H + yy) * W + xx) * dcs + c0);
+      }
+    }
+    __syncthreads();  // the previous chunk's MFMA reads are done
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int it = tid + 256 * u, pl = it % EA_PG, pos = it / EA_PG;
+      const __bf16* ex = reinterpret_cast<const __bf16*>(&vx[u]);
+      const __bf16* ed = reinterpret_cast<const __bf16*>(&vd[u]);
+#pragma unroll
+      for (int ch = 0; ch < EA_CG; ++ch) {
+        Xs[(ch * 64 + pos) * EA_XP + pl] = to_f(ex[ch]);
+        Ds[(ch * 64 + pos) * EA_XP + pl] = to_f(ed[ch]);
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int cc = 0; cc < 2; ++cc) {
+      const int ch = wave * 2 + cc;
+      const float* db = Ds + (ch * 64 + cl) * EA_XP + g;
+      const float* xb = Xs + (ch * 64 + cl) * EA_XP + g;
+#pragma unroll
+      for (int ks = 0; ks < EA_PG / 4; ++ks) {
+        float av[4], bv[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          av[t] = db[t * 16 * EA_XP + 4 * ks];  // A[i = t*16 + cl][patch 4ks + g]
+          bv[t] = xb[t * 16 * EA_XP + 4 * ks];  // B[patch 4ks + g][j = t*16 + cl]
+        }
+#pragma unroll
+        for (int it = 0; it < 4; ++it)
+#pragma unroll
+          for (int jt = 0; jt < 4; ++jt)
+            acc[cc][it * 4 + jt] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[it], bv[jt], acc[cc][it * 4 + jt], 0, 0, 0);
+      }
+    }
+  }
+  // D[i = it*16 + 4g + r][j = jt*16 + cl] -> part[(sp * C + c) * 4096 + i * 64 + j]
+#pragma unroll
+  for (int cc = 0; cc < 2; ++cc) {
+    float* out = part + ((long)sp * C + c0 + wave * 2 + cc) * 4096;
+#pragma unroll
+    for (int it = 0; it < 4; ++it)
+#pragma unroll
+      for (int jt = 0; jt < 4; ++jt)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[(it * 16 + 4 * g + r) * 64 + jt * 16 + cl] = acc[cc][it * 4 + jt][r];
+  }
+}
+
+// dw[c][uv] (+)= sum_e B[uv][e] * sum_split part[split][c][e]; block = (channel, half of the uv rows): the split
+// sum of dM_c goes to LDS (16-byte loads), then a wave per uv row reads B[uv] as 16 float4 per lane (all in flight)
+// against it and reduces in a fixed order. The per-channel kernel below kept 8 scalar basis loads in flight per wave
+// (43 us per call: latency on the 640 KB basis read by every block).
+__global__ void __launch_bounds__(256) edffn_dw_fin2_kernel(const float* part, int C, const float* Bm, int nuv,
+                                                            float* dw, int accumulate) {
+  __shared__ __attribute__((aligned(16))) float dM[4096];
+  const int c = blockIdx.x, half = blockIdx.y, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int e4 = threadIdx.x; e4 < 1024; e4 += 256) {
+    f32x4 v[EDFFN_DWS];
+#pragma unroll
+    for (int sp = 0; sp < EDFFN_DWS; ++sp) v[sp] = *reinterpret_cast<const f32x4*>(part + ((long)sp * C + c) * 4096 + 4 * e4);
+    f32x4 sacc = v[0];
+#pragma unroll
+    for (int sp = 1; sp < EDFFN_DWS; ++sp) sacc += v[sp];
+    *reinterpret_cast<f32x4*>(dM + 4 * e4) = sacc;
+  }
+  __syncthreads();
+  const int u0 = half * ((nuv + 1) / 2), u1 = min(nuv, u0 + (nuv + 1) / 2);
+  for (int u = u0 + wave; u < u1; u += 4) {
+    const f32x4* b = reinterpret_cast<const f32x4*>(Bm + (long)u * 4096);
+    f32x4 bv[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) bv[k] = b[lane + 64 * k];
+    float sacc = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const f32x4 m4 = *reinterpret_cast<const f32x4*>(dM + 4 * (lane + 64 * k));
+      sacc += bv[k][0] * m4[0] + bv[k][1] * m4[1] + bv[k][2] * m4[2] + bv[k][3] * m4[3];
+    }
+    sacc = wave_sum(sacc);
+    if (lane == 0) dw[c * nuv + u] = accumulate ? dw[c * nuv + u] + sacc : sacc;
+  }
+}
+
 // dw[c][uv] (+)= sum_e B[uv][e] * sum_split part[split][c][e]: block per channel, fixed order
 __global__ void __launch_bounds__(256) edffn_dw_fin_kernel(const float* part, int C, const float* Bm, int nuv,
                                                            float* dw, int accumulate) {
@@ -930,12 +1244,20 @@ static int dw_fwd_cb(int dtype, int H, int W, int k) {
   const int cb = dtype == ADR_BF16 ? DW_CB_BF16 : DW_CB_F32, half = cb / 2;
   return dw_fwd_smem_cb(dtype, H, W, k, cb) <= DW_LDS_MAX ? cb : dw_fwd_smem_cb(dtype, H, W, k, half) <= DW_LDS_MAX ? half : 0;
 }
+// bf16 with a 16-channel slab whose fp32 padded image fits 64 KB (the 20x20 maps): the F32S variant
+static bool dw_f32s(int dtype, int H, int W, int k, int cb) {
+  return dtype == ADR_BF16 && cb == DW_CB_BF16 && dw_fwd_smem_cb(ADR_F32, H, W, k, DW_CB_BF16) <= DW_LDS_MAX;
+}
 template <bool BWD>
 static void dw_img_launch(int dtype, hipStream_t st, const void* x, int xcs, const float* w, const float* b, void* y,
                           int ycs, int N, int H, int W, int C, int k, int acc) {
   const int cb = dw_fwd_cb(dtype, H, W, k);
   const size_t sm = dw_fwd_smem_cb(dtype, H, W, k, cb);
-  if (dtype == ADR_BF16 && cb == DW_CB_BF16)
+  if (dw_f32s(dtype, H, W, k, cb))  // 8-channel slabs: twice the blocks of the 16-channel plan (latency-bound at 2 waves/SIMD)
+    hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, DW_CB_BF16 / 2, true>), dim3(N, cdiv(C, DW_CB_BF16 / 2)), dim3(256),
+                       dw_fwd_smem_cb(ADR_F32, H, W, k, DW_CB_BF16 / 2), st, (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs,
+                       H, W, C, k, acc);
+  else if (dtype == ADR_BF16 && cb == DW_CB_BF16)
     hipLaunchKernelGGL((dw_img_kernel<__bf16, BWD, DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
                        (const __bf16*)x, xcs, w, b, (__bf16*)y, ycs, H, W, C, k, acc);
   else if (dtype == ADR_BF16)
@@ -993,10 +1315,15 @@ extern "C" int adr_dwconv_fwd_act(const void* x, int xcs, const float* w, const 
               "dwconv act: bad arguments");
   ADR_REQUIRE(adr_dwconv_fwd_act_supported(H, W, C, k), "dwconv act: H=%d W=%d C=%d k=%d not on the image kernel", H, W,
               C, k);
-  const size_t sm = dw_fwd_smem_cb(ADR_BF16, H, W, k, DW_CB_BF16);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL((dw_img_act_kernel<DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256), sm, st,
-                       (const __bf16*)x, xcs, w, scale, shift, act, (__bf16*)y, ycs, H, W, C, k);
+  if (dw_f32s(ADR_BF16, H, W, k, DW_CB_BF16))
+    hipLaunchKernelGGL((dw_img_act_kernel<DW_CB_BF16, true>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256),
+                       dw_fwd_smem_cb(ADR_F32, H, W, k, DW_CB_BF16), st, (const __bf16*)x, xcs, w, scale, shift, act,
+                       (__bf16*)y, ycs, H, W, C, k);
+  else
+    hipLaunchKernelGGL((dw_img_act_kernel<DW_CB_BF16>), dim3(N, cdiv(C, DW_CB_BF16)), dim3(256),
+                       dw_fwd_smem_cb(ADR_BF16, H, W, k, DW_CB_BF16), st, (const __bf16*)x, xcs, w, scale, shift, act,
+                       (__bf16*)y, ycs, H, W, C, k);
   return check_launch("adr_dwconv_fwd_act");
 }
 
@@ -1191,9 +1518,20 @@ extern "C" int adr_group_mean(int dtype, const void* x, int xcs, int S, int HW, 
 }
 
 extern "C" int adr_edffn_build(const float* w, const float* basis, int C, int nuv, float* M, void* stream) {
-  hipLaunchKernelGGL(edffn_build_kernel, dim3(cdiv((long)C * 4096, 256)), dim3(256), 0, (hipStream_t)stream, w, basis,
-                     C, nuv, M);
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(edffn_build8_kernel, dim3(16, C / 8), dim3(256), 0, (hipStream_t)stream, w, basis, C, nuv, M);
+  else
+    hipLaunchKernelGGL(edffn_build_kernel, dim3(cdiv((long)C * 4096, 256)), dim3(256), 0, (hipStream_t)stream, w, basis,
+                       C, nuv, M);
   return check_launch("adr_edffn_build");
+}
+
+// the matrix-core apply: bf16 tensors, 8-channel groups, 16-byte aligned channel rows (ADR_EDFFN_MFMA=0: the
+// per-channel kernel, A/B)
+static bool edffn_mfma_ok(int dtype, int C, int xcs, int ycs) {
+  const char* e = getenv("ADR_EDFFN_MFMA");  // read per call: tests compare the two paths in one process
+  const bool v = e ? atoi(e) != 0 : true;
+  return v && dtype == ADR_BF16 && C % EA_CG == 0 && xcs % 8 == 0 && ycs % 8 == 0;
 }
 
 extern "C" int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, void* y, int ycs, int N, int H, int W,
@@ -1202,7 +1540,10 @@ extern "C" int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, 
   ADR_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && H >= 4 && W >= 4, "edffn: N=%d H=%d W=%d C=%d", N, H, W, C);
   const long np = (long)N * ((H + 7) / 8) * ((W + 7) / 8);
   dim3 grid((unsigned)(cdiv(np, EDFFN_PPB) * C));
-  if (dtype == ADR_BF16)
+  if (edffn_mfma_ok(dtype, C, xcs, ycs))
+    hipLaunchKernelGGL(edffn_apply_mfma_kernel<false>, dim3((unsigned)(C / EA_CG * cdiv(np, EA_PG))), dim3(256), 0, st,
+                       (const __bf16*)x, xcs, M, y, ycs, N, H, W, C);
+  else if (dtype == ADR_BF16)
     hipLaunchKernelGGL(edffn_apply_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)x, xcs, M, (__bf16*)y, ycs,
                        N, H, W, C, 0);
   else
@@ -1230,7 +1571,10 @@ extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, 
   const long np = (long)N * ((H + 7) / 8) * ((W + 7) / 8);
   dim3 grid((unsigned)(cdiv(np, EDFFN_PPB) * C));
   float* dpad = ws;
-  if (dtype == ADR_BF16)
+  if (edffn_mfma_ok(dtype, C, dcs, 8))
+    hipLaunchKernelGGL(edffn_apply_mfma_kernel<true>, dim3((unsigned)(C / EA_CG * cdiv(np, EA_PG))), dim3(256), 0, st,
+                       (const __bf16*)dy, dcs, M, (void*)dpad, 0, N, H, W, C);
+  else if (dtype == ADR_BF16)
     hipLaunchKernelGGL(edffn_apply_kernel<__bf16>, grid, dim3(256), 0, st, (const __bf16*)dy, dcs, M, (__bf16*)dpad, 0,
                        N, H, W, C, 1);
   else
@@ -1245,13 +1589,19 @@ extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, 
                        (float*)dx, ocs);
   if (dw) {
     float* part = ws + edffn_pad_floats(N, H, W, C);
-    if (dtype == ADR_BF16)
+    if (edffn_mfma_ok(dtype, C, xcs, dcs))
+      hipLaunchKernelGGL(edffn_dw_mfma_kernel<>, dim3((unsigned)(C / EA_CG * EDFFN_DWS)), dim3(256), 0, st,
+                         (const __bf16*)x, xcs, (const __bf16*)dy, dcs, N, H, W, C, part);
+    else if (dtype == ADR_BF16)
       hipLaunchKernelGGL(edffn_dw_kernel<__bf16>, dim3(C, EDFFN_DWS), dim3(256), 0, st, (const __bf16*)x, xcs,
                          (const __bf16*)dy, dcs, N, H, W, C, part);
     else
       hipLaunchKernelGGL(edffn_dw_kernel<float>, dim3(C, EDFFN_DWS), dim3(256), 0, st, (const float*)x, xcs,
                          (const float*)dy, dcs, N, H, W, C, part);
-    hipLaunchKernelGGL(edffn_dw_fin_kernel, dim3(C), dim3(256), 0, st, part, C, basis, nuv, dw, dw_accumulate);
+    if (edffn_mfma_ok(dtype, C, xcs, dcs))
+      hipLaunchKernelGGL(edffn_dw_fin2_kernel, dim3(C, 2), dim3(256), 0, st, part, C, basis, nuv, dw, dw_accumulate);
+    else
+      hipLaunchKernelGGL(edffn_dw_fin_kernel, dim3(C), dim3(256), 0, st, part, C, basis, nuv, dw, dw_accumulate);
   }
   return check_launch("adr_edffn_bwd");
 }

@@ -342,15 +342,23 @@ __global__ void __launch_bounds__(256) tal_topk_kernel(const float* align, uint8
         }
       }
     };
-    int a = lane;
-    for (; a + 192 < A; a += 256) {
-      const float v0 = m[a], v1 = m[a + 64], v2 = m[a + 128], v3 = m[a + 192];
-      insert(v0, a);
-      insert(v1, a + 64);
-      insert(v2, a + 128);
-      insert(v3, a + 192);
+    // 16 loads per lane in flight: the next block of the row is loaded while the current one is inserted
+    constexpr int U = 16;
+    float cur[U], nxt[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) cur[u] = lane + 64 * u < A ? m[lane + 64 * u] : -INFINITY;
+    for (int a0 = 0; a0 < A; a0 += 64 * U) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int an = a0 + 64 * U + lane + 64 * u;
+        nxt[u] = an < A ? m[an] : -INFINITY;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (a0 + lane + 64 * u < A) insert(cur[u], a0 + lane + 64 * u);
+#pragma unroll
+      for (int u = 0; u < U; ++u) cur[u] = nxt[u];
     }
-    for (; a < A; a += 64) insert(m[a], a);
     // merge: T = the row's TOPK-th largest; h = own entries strictly above the current candidate
     int need = TOPK, h = 0, tot = 0;
     float T = -INFINITY;
