@@ -1004,7 +1004,7 @@ __global__ void __launch_bounds__(256) edffn_fold_kernel(const float* dpad, int 
 // basis in place (no dM round trip through memory).
 // dM partial per (channel, patch split): grid (C, EDFFN_DWS); 4 waves x patch stride, two patches' loads in
 // flight per iteration; part[(split * C + c) * 4096 + e]
-constexpr int EDFFN_DWS = 8;
+constexpr int EDFFN_DWS = 16;  // patch splits of the dM partials (16: 256 blocks of the MFMA kernel at C = 128)
 template <typename T>
 __global__ void __launch_bounds__(256) edffn_dw_kernel(const T* x, int xcs, const T* dy, int dcs, int N, int H, int W,
                                                        int C, float* part) {
