@@ -420,6 +420,27 @@ __global__ void __launch_bounds__(256) bcast_fill_kernel(const float* g, int gns
   *q = from_f<T>(accumulate ? to_f(*q) + v : v);
 }
 
+// bf16, 8 channels per thread (one 16-byte load / store; 32-bit index math): the same per-element v = g * s and
+// optional accumulate as bcast_fill_kernel (was 80 us, 0.9 TB/s, on the head's 1344 x 400 x 64 gradient fill)
+__global__ void __launch_bounds__(256) bcast_fill8_kernel(const float* g, int gns, int gcs, float s, __bf16* o, int ocs,
+                                                          unsigned npix, unsigned HW, unsigned C8, int accumulate) {
+  const unsigned i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= npix * C8) return;
+  const unsigned pix = i / C8, c = (i - pix * C8) * 8u, n = pix / HW;
+  __bf16* q = o + (size_t)pix * ocs + c;
+  u32x4 prev = {0u, 0u, 0u, 0u};
+  if (accumulate) prev = ld16(q);
+  const __bf16* pe = reinterpret_cast<const __bf16*>(&prev);
+  u32x4 out;
+  __bf16* oe = reinterpret_cast<__bf16*>(&out);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float v = g[(long)n * gns + (long)(c + e) * gcs] * s;
+    oe[e] = from_f<__bf16>(accumulate ? to_f(pe[e]) + v : v);
+  }
+  st16(q, out);
+}
+
 // o = x * p[pix] (p: channel 0 of a view) ; bwd: dx = dout*p ; dp[pix] = sum_c dout*x
 template <typename T>
 __global__ void __launch_bounds__(256) mul_pixel_kernel(const T* x, int xcs, const T* p, int pcs, T* o, int ocs,
@@ -660,6 +681,11 @@ extern "C" int adr_bcast_fill(int dtype, const float* g, int gns, int gcs, float
                               int C, int accumulate, void* stream) {
   long npix = (long)N * HW;
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == ADR_BF16 && C % 8 == 0 && ocs % 8 == 0 && ((uintptr_t)o & 15) == 0 && npix * (C / 8) < (1l << 31)) {
+    hipLaunchKernelGGL(bcast_fill8_kernel, dim3(cdiv(npix * (C / 8), 256)), dim3(256), 0, st, g, gns, gcs, s,
+                       (__bf16*)o, ocs, (unsigned)npix, (unsigned)HW, (unsigned)(C / 8), accumulate);
+    return check_launch("adr_bcast_fill");
+  }
   if (dtype == ADR_BF16)
     hipLaunchKernelGGL(bcast_fill_kernel<__bf16>, dim3(cdiv(npix * C, 256)), dim3(256), 0, st, g, gns, gcs, s,
                        (__bf16*)o, ocs, npix, HW, C, accumulate);

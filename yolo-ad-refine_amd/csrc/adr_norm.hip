@@ -9,6 +9,8 @@
 // Reference semantics: nn.BatchNorm2d with eps 1e-3 / momentum 0.03 (utils/torch_utils.py:426-436),
 // unbiased running_var update; GroupNorm(16, C) eps 1e-5 (nn/modules/head.py:613).
 #include "adr_common.h"
+#include <cstdio>
+#include <cstdlib>
 
 namespace adr {
 
@@ -1147,6 +1149,10 @@ extern "C" int adr_nc_reduce_batched(const adr_colsum_entry* entries, int count,
     }
     ADR_REQUIRE(blocks < (1l << 31), "nc_reduce_batched: grid");
     nb.start[nb.count] = (int)blocks;
+    if (getenv("ADR_DEBUG_NCB"))  // entry table for profiling (one line per entry)
+      for (int j = 0; j < nb.count; ++j)
+        fprintf(stderr, "ncb %d: N=%d HW=%d C=%d xcs=%d rows=%d chunks=%d blocks=%d\n", b0 + j, nb.e[j].N, nb.e[j].HW,
+                nb.e[j].C, nb.e[j].xcs, nb.e[j].rows_per_chunk, nb.e[j].chunks, nb.e[j].N * nb.e[j].chunks);
     hipLaunchKernelGGL(nc_reduce_batched_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, nb);
   }
   return check_launch("adr_nc_reduce_batched");
