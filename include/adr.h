@@ -167,6 +167,8 @@ typedef struct adr_wgrad_job {
   const void* dy;
   float* out;
   int accumulate, pad_;
+  float* bias;  /* NULL, or [splits][2][K] rows whose half 0 receives sum_p dy[p][k] per split (fused bias gradient:
+                   the column sums nn.Conv2d's bias backward takes, reference nn/modules/conv.py:36-54 / head.py) */
 } adr_wgrad_job;
 int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int count, void* stream);
 /* The tile kernel a job of adr_conv2d_wgrad_partials_batched goes to: bm * 256 + bn of the grouped
@@ -174,6 +176,13 @@ int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int count, void
 int adr_conv2d_wgrad_batched_tile(const adr_conv_desc* d);
 int adr_conv2d_wgrad_partials(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
                               void* stream);
+/* The bias gradient's column sums of dy computed by the weight-gradient GEMM that already holds dy in registers
+ * (one extra MFMA per row tile against ones) instead of a separate pass over dy (adr_nc_reduce / the batched column
+ * sums): fusable when the plan is the generic bf16 tile kernel with bm, bn >= 32 (adr_conv2d_wgrad_bias_fusable).
+ * bias_part: [splits][2][K] floats, half 0 of each row written (reduce with adr_partial_sum, which = 0). */
+int adr_conv2d_wgrad_bias_fusable(const adr_conv_desc* d);
+int adr_conv2d_wgrad_partials_bias(const adr_conv_desc* d, const void* x, const void* dy, float* out, float* bias_part,
+                                   void* stream);
 int adr_wgrad_reduce(const float* part, float* dw, long n, int splits, int accumulate, void* stream);
 /* The split sum fused with the KRSC -> (K, C, R, S) parameter layout (adr_unpack_weight_grad): part holds
  * `splits` slabs of split_stride floats whose first K*RS*Cp entries are [k][rs][c]; dst (+)= their sum at

@@ -623,7 +623,7 @@ class WgradEntry(ctypes.Structure):
 class WgradJob(ctypes.Structure):
     """adr_wgrad_job (include/adr.h)."""
     _fields_ = [("d", ConvDesc), ("x", ctypes.c_void_p), ("dy", ctypes.c_void_p), ("out", ctypes.c_void_p),
-                ("accumulate", ctypes.c_int), ("pad_", ctypes.c_int)]
+                ("accumulate", ctypes.c_int), ("pad_", ctypes.c_int), ("bias", ctypes.c_void_p)]
 
 
 class PsumEntry(ctypes.Structure):
@@ -726,7 +726,7 @@ class WgradDeferral:
         self.pkeep.append(part)
         self.pdsts.add(dst)
 
-    def add_job(self, d, xp, dyp, ws, keep, work=(0, 0), shp=""):
+    def add_job(self, d, xp, dyp, ws, keep, work=(0, 0), shp="", bias=None):
         """A conv's WGRAD partials into `ws`, launched at the flush together with the stage's other weight gradients
         (adr_conv2d_wgrad_partials_batched: one launch per tile shape, bitwise the per-conv launches). x and dy stay
         alive (keep) and dy is pinned so no fan-out accumulates into it in place before the flush reads it."""
@@ -734,9 +734,10 @@ class WgradDeferral:
             if torch.is_tensor(t):
                 t._adr_pinned = True
                 _v(t)[0]._adr_pinned = True
-        self.jobs.append(WgradJob(ConvDesc.from_buffer_copy(d), xp, dyp, ws.data_ptr(), 0, 0))
+        self.jobs.append(WgradJob(ConvDesc.from_buffer_copy(d), xp, dyp, ws.data_ptr(), 0, 0,
+                                  bias.data_ptr() if bias is not None else None))
         self.jwork.append((work, shp))
-        self.jkeep += [ws, *keep]
+        self.jkeep += [ws, *keep] + ([bias] if bias is not None else [])
 
     def add(self, ws, stride, splits, dst, K_, C_, Cp, RS_, transpose_kc, acc):
         dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
@@ -859,20 +860,38 @@ def _grad_buf(tgt):
 _DEFER_WGRAD = bool(int(__import__("os").environ.get("ADR_DEFER_WGRAD", "1")))
 
 
-def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device, keep=()):
+def _fuse_wg_bias():
+    """ADR_FUSE_WG_BIAS=0: bias gradients by their own column-sum pass (read per call: tests compare the two)."""
+    return __import__("os").environ.get("ADR_FUSE_WG_BIAS", "1") != "0"
+
+
+def _bias_rows(bias_param, K, P, part, device):
+    """The fused bias gradient's [P][2][K] split rows into the parameter's gradient destination (batched at the
+    flush when deferring; adr_partial_sum otherwise). Returns the autograd value (grad_ret)."""
+    db, pb, acc = grad_dst(bias_param, K, device)
+    if _dfr() is not None and acc:
+        _dfr().add_psum(part, P, K, 0, pb, acc)
+    else:
+        lib.adr_partial_sum(fptr(part), P, K, 0, pb, acc, stream())
+    return grad_ret(bias_param, db)
+
+
+def wgrad_param(param, d, xp, dyp, K, C, RS, wshape, cpad, device, keep=(), bias=None):
     """Weight gradient of a conv contraction straight into its parameter's gradient destination: the split-K
     WGRAD GEMM writes [split][K][RS][C] fp32 slabs, and one fused reduce+unpack kernel sums the splits in a
     fixed order and scatters them into the (K, C, R, S) layout of `param` (the trainer's arena slice when
     present, accumulating; otherwise a fresh tensor returned for autograd). wshape may cover only the first
-    rows / unpadded channels of the GEMM (padded convs, DCN's [Cout][9C] columns)."""
+    rows / unpadded channels of the GEMM (padded convs, DCN's [Cout][9C] columns).
+    bias: the conv's bias parameter — when given, returns (dw, fused, db): with fused True the bias gradient's column
+    sums came out of the same deferred WGRAD launch (adr_wgrad_job.bias) and db is its autograd value."""
     K_, C_ = wshape[0], wshape[1]
     RS_ = 1
     for v in wshape[2:]:
         RS_ *= v
-    return _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep)
+    return _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep, bias)
 
 
-def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep=()):
+def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep=(), bias=None):
     splits = lib.adr_conv2d_wgrad_splits(ctypes.byref(d))
     stride = K * RS * C
     es = 2 if d.dtype == BF16 else 4
@@ -886,9 +905,17 @@ def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep=()
     if (_DEFER_WGRAD and keep and _dfr() is not None and acc and d.dtype == BF16 and
             splits * stride * 4 <= DEFER_MAX_BYTES):
         # partials at the flush, grouped with the stage's other convs' (timed there per grouped launch)
-        _dfr().add_job(d, xp, dyp, ws, keep, work, shp)
+        bpart = None
+        if bias is not None and K == K_ and _fuse_wg_bias() and lib.adr_conv2d_wgrad_bias_fusable(ctypes.byref(d)):
+            bpart = torch.empty(splits * 2 * K, dtype=torch.float32, device=device)
+        _dfr().add_job(d, xp, dyp, ws, keep, work, shp, bias=bpart)
         _dfr().add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
+        if bias is not None:
+            return (grad_ret(param, out), bpart is not None,
+                    _bias_rows(bias, K, splits, bpart, device) if bpart is not None else None)
         return grad_ret(param, out)
+    if bias is not None:  # not fused: the caller takes the bias gradient its own way
+        return (_wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep), False, None)
     rep = _reps()
     tok = _t0(name, *work, shp, rep)
     for _ in range(rep):
@@ -1072,9 +1099,14 @@ class Conv2dFn(torch.autograd.Function):
                 bst = ctx.bstat if (ctx.bstat is not None and BN_BSTAT and wt is not None and _engine2(d2, d2.k)
                                     and d2.stride_h in (1, 2) and x.dtype == torch.bfloat16) else None
                 conv_dgrad(d2, dyp, (wp, wt), None, dx.data_ptr(), xf=pend, dy=dy, bst=bst, dx=dx)
+        fused = False
         if ctx.needs_input_grad[1]:
-            dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
-        if has_b and ctx.needs_input_grad[2]:
+            if has_b and ctx.needs_input_grad[2]:  # the bias column sums from the same WGRAD launch when it can
+                dw, fused, db = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy),
+                                            bias=ctx.pb)
+            else:
+                dw = wgrad_param(ctx.pw, d, xp, dyp, K, C, R * S, wshape, cpad, x.device, keep=(x, dy))
+        if has_b and ctx.needs_input_grad[2] and not fused:
             db = _bias_grad(dy, K, N, Ho * Wo, dycs, ctx.pb)
         return dx, dw, db, None, None, None, None, None, None
 
@@ -3857,9 +3889,11 @@ def seg_expand(v, pack):
     return SegExpandFn.apply(v, pack)
 
 
-def wgrad_param_multi(param, pieces, K, C, RS, wshape, cpad, device):
+def wgrad_param_multi(param, pieces, K, C, RS, wshape, cpad, device, bias=None):
     """wgrad_param over several contractions of one weight (the head's per-level convs): every piece's split-K slabs
-    go to one buffer and ONE reduction sums them all (one deferral entry, no flush for a repeated destination)."""
+    go to one buffer and ONE reduction sums them all (one deferral entry, no flush for a repeated destination).
+    bias: as in wgrad_param — returns (dw, fused, db), the pieces' bias column sums written by the same launches
+    (adr_conv2d_wgrad_partials_bias) into one [sum of splits][2][K] row set."""
     K_, C_ = wshape[0], wshape[1]
     RS_ = 1
     for v in wshape[2:]:
@@ -3867,6 +3901,10 @@ def wgrad_param_multi(param, pieces, K, C, RS, wshape, cpad, device):
     stride = K * RS * C
     splits = [lib.adr_conv2d_wgrad_splits(ctypes.byref(d)) for d, _, _ in pieces]
     ws = torch.empty(sum(splits) * stride, dtype=torch.float32, device=device)
+    bpart = None
+    if (bias is not None and K == K_ and _fuse_wg_bias() and
+            all(lib.adr_conv2d_wgrad_bias_fusable(ctypes.byref(d)) for d, _, _ in pieces)):
+        bpart = torch.empty(sum(splits) * 2 * K, dtype=torch.float32, device=device)
     s0 = 0
     for (d, xp, dyp), sp in zip(pieces, splits):
         es = 2 if d.dtype == BF16 else 4
@@ -3875,17 +3913,25 @@ def wgrad_param_multi(param, pieces, K, C, RS, wshape, cpad, device):
         work = (es * (d.n * d.h * d.w * d.c + d.n * d.ho * d.wo * d.k) + 4 * sp * stride,
                 2 * d.n * d.ho * d.wo * d.k * RS * d.c)
         tok = _t0(name, *work, _shape(d, f"wgrad/{sp}") if _TIMING is not None else "")
-        lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp),
-                                      ctypes.c_void_p(ws.data_ptr() + 4 * s0 * stride), 0, stream())
+        if bpart is not None:
+            lib.adr_conv2d_wgrad_partials_bias(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp),
+                                               ctypes.c_void_p(ws.data_ptr() + 4 * s0 * stride),
+                                               ctypes.c_void_p(bpart.data_ptr() + 4 * s0 * 2 * K), stream())
+        else:
+            lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp),
+                                          ctypes.c_void_p(ws.data_ptr() + 4 * s0 * stride), 0, stream())
         _t1(tok)
         s0 += sp
     Cp = max(C_, cpad)
     out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
     if _dfr() is not None and acc and _TIMING is None and s0 * stride * 4 <= DEFER_MAX_BYTES:
         _dfr().add(ws, stride, s0, ptr, K_, C_, Cp, RS_, 0, acc)
+    else:
+        lib.adr_wgrad_reduce_unpack(fptr(ws), stride, s0, ptr, K_, C_, Cp, RS_, 0, acc, stream())
+    if bias is None:
         return grad_ret(param, out)
-    lib.adr_wgrad_reduce_unpack(fptr(ws), stride, s0, ptr, K_, C_, Cp, RS_, 0, acc, stream())
-    return grad_ret(param, out)
+    db = _bias_rows(bias, K, s0, bpart, device) if bpart is not None else None
+    return grad_ret(param, out), bpart is not None, db
 
 
 class LevelConvFn(torch.autograd.Function):
@@ -3955,8 +4001,13 @@ class LevelConvFn(torch.autograd.Function):
             for l, (H, W) in enumerate(pack.dims):
                 d, _, _ = conv_desc(pack.N, H, W, C, xcs, Kp, R, Sk, 1, 1, pad, pad, dycs, x.dtype)
                 pieces.append((d, pack.at(xp, xcs, es, l).value, pack.at(dyp, dycs, es, l).value))
-            dw = wgrad_param_multi(ctx.pw, pieces, Kp, C, R * Sk, wshape, 0, dev)
-        if has_b and ctx.needs_input_grad[2]:
+            if has_b and ctx.needs_input_grad[2] and not kpad:
+                dw, fused, db = wgrad_param_multi(ctx.pw, pieces, Kp, C, R * Sk, wshape, 0, dev, bias=ctx.pb)
+            else:
+                dw, fused = wgrad_param_multi(ctx.pw, pieces, Kp, C, R * Sk, wshape, 0, dev), False
+        else:
+            fused = False
+        if has_b and ctx.needs_input_grad[2] and not fused:
             if kpad:
                 db = sink(ctx.pb, _bias_grad(dy, Kp, Np, S, dycs)[:K])
             else:

@@ -21,5 +21,5 @@ struct WgPlan {
 };
 WgPlan wgrad_bf16_plan(const adr_conv_desc* d);
 int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
-                      const WgPlan& p, hipStream_t st);
+                      const WgPlan& p, hipStream_t st, float* bias = nullptr);
 }  // namespace adr

@@ -21,6 +21,7 @@
 namespace adr {
 
 typedef short v4s __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) v4s lds_v4s;
 
 struct WgArgs {
@@ -35,6 +36,7 @@ struct WgArgs {
   int ctiles;  // input-channel tiles per tap
   int x_bytes, dy_bytes;  // buffer-descriptor extents (< 2^31): out-of-range offsets read as zero
   int accumulate;
+  float* bias;  // optional: [split][2][K] rows, row half 0 = sum_p dy[p][k] over the split (the conv's bias gradient)
 };
 
 __device__ __forceinline__ v4s tr_read(const __bf16* p) {
@@ -151,6 +153,15 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
   for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // bias column sums ride on the dy fragments already in registers (lane: output channel i*16 + (lane & 15), 8 of
+  // the k-step's pixels): four v_dot2 against ones per fragment into one fp32 per row tile, in the blocks of the
+  // first (tap, input-channel) tile column, by the waves of column 0 (wave-uniform); the four lane groups' sums are
+  // combined at the end. (A ones-MFMA variant cost 16 accumulator registers: 3 -> 2 waves per SIMD.)
+  const bool do_bias = WK == 1 && a.bias != nullptr && tap == 0 && ct == 0 && wn == 0;
+  float bsum[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) bsum[i] = 0.f;
+  const bf16x2 ones2 = (bf16x2){(__bf16)1.f, (__bf16)1.f};
 
   // transposed-read addressing: lane (g, q4, p4) -> row rb + 4g + q4 (+16), column base + 4*p4
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
@@ -190,6 +201,15 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      if (do_bias) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const bf16x8 f = fa[i];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            bsum[i] = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){f[2 * q], f[2 * q + 1]}, ones2, bsum[i], false);
+        }
+      }
     }
     __syncthreads();
     if (t + 1 < ksteps) {
@@ -223,6 +243,15 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
 #pragma unroll
           for (int s2 = 0; s2 < WK - 1; ++s2) acc[i][j][e] += red[s2 * BM * BN + rr * BN + cc];
         }
+  }
+  if (do_bias) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float t = bsum[i] + __shfl_xor(bsum[i], 16, 64);
+      t += __shfl_xor(t, 32, 64);
+      const int co = m0 + wm * WROWS + i * 16 + (lane & 15);
+      if (lane < 16 && co < a.k) a.bias[(long)split * 2 * a.k + co] = t;
+    }
   }
   float* part = a.out + (long)split * a.k * ((long)RS * a.c);
 #pragma unroll
@@ -648,6 +677,9 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
   return p;
 }
 
+// the fused bias column sums need the generic tile kernel with one reduction slice per wave (WK == 1: bm, bn >= 32)
+static bool wgrad_bias_ok(const WgPlan& p) { return !p.thin && !p.tw3 && p.bm >= 32 && p.bn >= 32; }
+
 static void wgrad_args(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
                        const WgPlan& p, WgArgs& g) {
   g.x = (const __bf16*)x;
@@ -663,14 +695,17 @@ static void wgrad_args(const adr_conv_desc* d, const void* x, const void* dy, fl
   g.accumulate = accumulate;
   g.x_bytes = (int)(2l * d->n * d->h * d->w * d->x_cstride);
   g.dy_bytes = (int)(2l * d->n * d->ho * d->wo * d->y_cstride);
+  g.bias = nullptr;
 }
 
 int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
-                      const WgPlan& p, hipStream_t st) {
+                      const WgPlan& p, hipStream_t st, float* bias) {
   ADR_REQUIRE(2l * d->n * d->h * d->w * d->x_cstride < (1l << 31) && 2l * d->n * d->ho * d->wo * d->y_cstride < (1l << 31),
               "conv wgrad (bf16): operand exceeds 2 GB (32-bit buffer offsets)");
+  ADR_REQUIRE(!bias || wgrad_bias_ok(p), "conv wgrad (bf16): fused bias sums need the generic tile with bm, bn >= 32");
   WgArgs g;
   wgrad_args(d, x, dy, out, accumulate, p, g);
+  g.bias = bias;
   dim3 grid(p.tiles, p.splits);
   if (p.thin) {
     if (p.thin == 1) {
@@ -724,6 +759,17 @@ extern "C" int adr_conv2d_wgrad_batched_tile(const adr_conv_desc* d) {
   return (p.thin || p.tw3) ? 0 : p.bm * 256 + p.bn;
 }
 
+extern "C" int adr_conv2d_wgrad_bias_fusable(const adr_conv_desc* d) {
+  return d && d->dtype == ADR_BF16 && wgrad_bias_ok(wgrad_bf16_plan(d)) ? 1 : 0;
+}
+
+extern "C" int adr_conv2d_wgrad_partials_bias(const adr_conv_desc* d, const void* x, const void* dy, float* out,
+                                              float* bias_part, void* stream) {
+  ADR_REQUIRE(d && d->dtype == ADR_BF16 && bias_part, "conv wgrad partials + bias: bf16 descriptor and bias rows");
+  const WgPlan p = wgrad_bf16_plan(d);
+  return wgrad_bf16_launch(d, x, dy, out, 0, p, (hipStream_t)stream, bias_part);
+}
+
 extern "C" int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int count, void* stream) {
   ADR_REQUIRE(count >= 0 && (count == 0 || jobs), "wgrad partials batched: count=%d", count);
   hipStream_t st = (hipStream_t)stream;
@@ -755,8 +801,9 @@ extern "C" int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int 
                 "wgrad partials batched: operand exceeds 2 GB (job %d)", q);
     const WgPlan p = wgrad_bf16_plan(d);
     ADR_REQUIRE(!jb.accumulate || p.splits == 1, "wgrad partials batched: accumulate needs a single split (job %d)", q);
+    ADR_REQUIRE(!jb.bias || wgrad_bias_ok(p), "wgrad partials batched: job %d has fused bias sums on a tile without them", q);
     if (p.thin || p.tw3) {
-      if (int rc = wgrad_bf16_launch(d, jb.x, jb.dy, jb.out, jb.accumulate, p, st)) return rc;
+      if (int rc = wgrad_bf16_launch(d, jb.x, jb.dy, jb.out, jb.accumulate, p, st, nullptr)) return rc;
       continue;
     }
     const int i = idx(p.bm), j = idx(p.bn);
@@ -768,6 +815,7 @@ extern "C" int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int 
     }
     const int k = pd.b.count;
     wgrad_args(d, jb.x, jb.dy, jb.out, jb.accumulate, p, pd.b.e[k]);
+    pd.b.e[k].bias = jb.bias;
     pd.b.start[k] = pd.blocks;
     pd.b.tiles[k] = p.tiles;
     pd.blocks += p.tiles * p.splits;
