@@ -2,7 +2,8 @@
 column sums sum_p dy[p][k] of nn.Conv2d's bias backward (reference nn/modules/conv.py:36-54; the AYHead's biased
 convs, head.py) come out of the WGRAD launch that already holds dy in registers. The weight partials must be
 bitwise the plain launch's; the split rows summed must match an fp64 column sum of the same bf16 dy (the products
-are dy * 1, exact; only the fp32 summation order differs)."""
+are dy * 1, exact; only the fp32 summation order differs). Shapes cover the generic tile kernel (1x1, 3x3 s2) and
+the 3x3 s1 halo-tile kernel (wgrad3, both KF variants)."""
 import ctypes
 
 import pytest
@@ -16,7 +17,8 @@ def _nhwc(t):
 
 
 @pytest.mark.parametrize("N,H,W,C,K,R,S", [(4, 40, 40, 64, 80, 1, 1), (2, 80, 80, 128, 128, 1, 1),
-                                           (4, 40, 40, 64, 128, 3, 2), (1344 // 64, 20, 20, 64, 64, 1, 1)])
+                                           (4, 40, 40, 64, 128, 3, 2), (1344 // 64, 20, 20, 64, 64, 1, 1),
+                                           (4, 80, 80, 128, 128, 3, 1), (3, 20, 20, 64, 32, 3, 1)])
 def test_wgrad_bias_partials(N, H, W, C, K, R, S):
     from adrefine import kernels as Kn
     from adrefine.native import lib

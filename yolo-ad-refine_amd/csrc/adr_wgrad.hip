@@ -372,6 +372,11 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
 
   // transposed-read lane roles (see the header comment of this file): row 4g + q4 (+16), column 4 p4
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
+  // fused bias column sums (see wgrad_bf16_body): the dy fragment of each 32-pixel step, in the blocks of the first
+  // input-channel tile, by the waves of input-channel half 0
+  const bool do_bias = a.bias != nullptr && ct == 0 && wcf == 0;
+  const bf16x2 ones2 = (bf16x2){(__bf16)1.f, (__bf16)1.f};
+  float bsum = 0.f;
   f32x4 acc[9][NCF];
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -390,6 +395,10 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
       v4s lo = tr_read(da + plo * PD), hi = tr_read(da + phi * PD);
       v4s both[2] = {lo, hi};
       const bf16x8 fa = *reinterpret_cast<bf16x8*>(both);
+      if (do_bias) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) bsum = __builtin_amdgcn_fdot2_f32_bf16((bf16x2){fa[2 * q], fa[2 * q + 1]}, ones2, bsum, false);
+      }
       const int qlo = (plo / TW) * HWW + plo % TW, qhi = (phi / TW) * HWW + phi % TW;
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
@@ -406,6 +415,11 @@ __global__ void __launch_bounds__(256, 2) wgrad3_kernel(WgArgs a) {
     __syncthreads();
   }
 
+  if (do_bias) {  // lane (lane & 15) holds channel k0 + wkf*16 + (lane & 15) over its 8-pixel slots: combine the groups
+    float t = bsum + __shfl_xor(bsum, 16, 64);
+    t += __shfl_xor(t, 32, 64);
+    if (lane < 16) a.bias[(long)split * 2 * a.k + k0 + wkf * 16 + lane] = t;
+  }
   float* part = a.out + (long)split * a.k * (9L * a.c);
 #pragma unroll
   for (int t = 0; t < 9; ++t)
@@ -678,7 +692,7 @@ WgPlan wgrad_bf16_plan(const adr_conv_desc* d) {
 }
 
 // the fused bias column sums need the generic tile kernel with one reduction slice per wave (WK == 1: bm, bn >= 32)
-static bool wgrad_bias_ok(const WgPlan& p) { return !p.thin && !p.tw3 && p.bm >= 32 && p.bn >= 32; }
+static bool wgrad_bias_ok(const WgPlan& p) { return !p.thin && (p.tw3 || (p.bm >= 32 && p.bn >= 32)); }
 
 static void wgrad_args(const adr_conv_desc* d, const void* x, const void* dy, float* out, int accumulate,
                        const WgPlan& p, WgArgs& g) {
@@ -718,6 +732,7 @@ int wgrad_bf16_launch(const adr_conv_desc* d, const void* x, const void* dy, flo
     return check_launch("adr_conv2d_wgrad(bf16, thin 3x3 halo)");
   }
   if (p.tw3) {
+    g.bias = bias;  // the 3x3 halo kernel takes the fused bias sums too
     if (p.bm == 64) {
       if (p.tw3 == 16) hipLaunchKernelGGL((wgrad3_kernel<16, 4>), grid, dim3(256), 0, st, g);
       else hipLaunchKernelGGL((wgrad3_kernel<8, 4>), grid, dim3(256), 0, st, g);
@@ -803,7 +818,7 @@ extern "C" int adr_conv2d_wgrad_partials_batched(const adr_wgrad_job* jobs, int 
     ADR_REQUIRE(!jb.accumulate || p.splits == 1, "wgrad partials batched: accumulate needs a single split (job %d)", q);
     ADR_REQUIRE(!jb.bias || wgrad_bias_ok(p), "wgrad partials batched: job %d has fused bias sums on a tile without them", q);
     if (p.thin || p.tw3) {
-      if (int rc = wgrad_bf16_launch(d, jb.x, jb.dy, jb.out, jb.accumulate, p, st, nullptr)) return rc;
+      if (int rc = wgrad_bf16_launch(d, jb.x, jb.dy, jb.out, jb.accumulate, p, st, jb.bias)) return rc;
       continue;
     }
     const int i = idx(p.bm), j = idx(p.bn);
