@@ -902,34 +902,42 @@ def _wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep=()
     ws = torch.empty(splits * stride, dtype=torch.float32, device=device)
     Cp = max(C_, cpad)
     out, ptr, acc = grad_dst(param, K_ * C_ * RS_, device)
+    # the bias gradient's column sums from this same launch (deferred or not: the two paths stay bitwise equal)
+    bpart = None
+    if (bias is not None and d.dtype == BF16 and K == K_ and _fuse_wg_bias() and
+            lib.adr_conv2d_wgrad_bias_fusable(ctypes.byref(d))):
+        bpart = torch.empty(splits * 2 * K, dtype=torch.float32, device=device)
+
+    def ret():
+        if bias is None:
+            return grad_ret(param, out)
+        return (grad_ret(param, out), bpart is not None,
+                _bias_rows(bias, K, splits, bpart, device) if bpart is not None else None)
+
     if (_DEFER_WGRAD and keep and _dfr() is not None and acc and d.dtype == BF16 and
             splits * stride * 4 <= DEFER_MAX_BYTES):
         # partials at the flush, grouped with the stage's other convs' (timed there per grouped launch)
-        bpart = None
-        if bias is not None and K == K_ and _fuse_wg_bias() and lib.adr_conv2d_wgrad_bias_fusable(ctypes.byref(d)):
-            bpart = torch.empty(splits * 2 * K, dtype=torch.float32, device=device)
         _dfr().add_job(d, xp, dyp, ws, keep, work, shp, bias=bpart)
         _dfr().add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
-        if bias is not None:
-            return (grad_ret(param, out), bpart is not None,
-                    _bias_rows(bias, K, splits, bpart, device) if bpart is not None else None)
-        return grad_ret(param, out)
-    if bias is not None:  # not fused: the caller takes the bias gradient its own way
-        return (_wgrad_param(param, d, xp, dyp, K, C, RS, K_, C_, RS_, cpad, device, keep), False, None)
+        return ret()
     rep = _reps()
     tok = _t0(name, *work, shp, rep)
     for _ in range(rep):
-        lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(ws), 0,
-                                      stream())
+        if bpart is not None:
+            lib.adr_conv2d_wgrad_partials_bias(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(ws),
+                                               fptr(bpart), stream())
+        else:
+            lib.adr_conv2d_wgrad_partials(ctypes.byref(d), ctypes.c_void_p(xp), ctypes.c_void_p(dyp), fptr(ws), 0,
+                                          stream())
     _t1(tok)
     if _dfr() is not None and acc and _TIMING is None and splits * stride * 4 <= DEFER_MAX_BYTES:
         _dfr().add(ws, stride, splits, ptr, K_, C_, Cp, RS_, 0, acc)
-        return grad_ret(param, out)
+        return ret()
     tok = _t0("adr::wgrad_reduce_kernel<true, OUT, SL> (split reduce + unpack)",
               4 * stride * (splits + 1), stride * splits, shp)
     lib.adr_wgrad_reduce_unpack(fptr(ws), stride, splits, ptr, K_, C_, Cp, RS_, 0, acc, stream())
     _t1(tok)
-    return grad_ret(param, out)
+    return ret()
 
 
 def _bias_grad(dy, K, N, HW, cs, param=None):
