@@ -405,6 +405,15 @@ typedef struct {
   long n;
 } adr_axpy_entry;
 int adr_axpy_batched(const adr_axpy_entry* entries, int count, void* stream);
+/* The pieces of one torch.cat(dim=1) that their producers did not write in place, copied in ONE launch (bf16 NHWC,
+ * 16-byte channel rows): dst[p][c] = src[p][c] for p < npix, c < C of each piece (reference torch.cat in Concat,
+ * nn/modules/conv.py:322-335, and the neck / head concats); bitwise the per-piece adr_ew copies. */
+typedef struct adr_copy_piece {
+  const void* src;
+  void* dst;
+  int scs, dcs, C, pad_;
+} adr_copy_piece;
+int adr_copy_pieces(const adr_copy_piece* pieces, int count, long npix, void* stream);
 /* BiFPN weights w = relu(fw)/(sum relu(fw)+eps) and backward (block.py:1532-1535). */
 int adr_fusion_weights(const float* fw, int n, float eps, float* w, void* stream);
 int adr_fusion_weights_bwd(const float* fw, int n, float eps, const float* dw, float* dfw, void* stream);

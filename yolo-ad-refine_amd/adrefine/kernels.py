@@ -650,6 +650,12 @@ class DotsumEntry(ctypes.Structure):
         (n, ctypes.c_int) for n in ("xcs", "dcs", "N", "HW", "C", "rows_per_chunk", "chunks", "pad_")]
 
 
+class CopyPiece(ctypes.Structure):
+    """adr_copy_piece (include/adr.h)."""
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p)] + [
+        (n, ctypes.c_int) for n in ("scs", "dcs", "C", "pad_")]
+
+
 class AxpyEntry(ctypes.Structure):
     """adr_axpy_entry (include/adr.h)."""
     _fields_ = [("x", ctypes.c_void_p), ("y", ctypes.c_void_p), ("n", ctypes.c_long)]
@@ -1832,14 +1838,22 @@ class CatFn(torch.autograd.Function):
         if tuple(out.shape) != (N, Ctot, H, W) or out.stride(1) != 1 or out.stride(3) != Ctot:
             raise RuntimeError("cat: out buffer must be a whole NHWC activation of the concat shape")
         off = 0
-        sizes = []
+        sizes, todo = [], []
         for x in xs:
             v = _v(x)
             o = out[:, off:off + x.shape[1]]
             if not (v[1] == o.data_ptr() and v[2] == Ctot):  # producers that wrote in place need no copy
-                _ew(EW_COPY, (o, o.data_ptr(), Ctot), v)
+                todo.append((o, v, x.shape[1]))
             sizes.append(x.shape[1])
             off += x.shape[1]
+        if len(todo) > 1 and _TIMING is None and t0.dtype == torch.bfloat16 and all(
+                c % 8 == 0 and v[2] % 8 == 0 and v[1] % 16 == 0 and o.data_ptr() % 16 == 0 for o, v, c in todo):
+            # every piece that needs a copy in one launch (adr_copy_pieces; bitwise the per-piece copies)
+            arr = (CopyPiece * len(todo))(*[CopyPiece(v[1], o.data_ptr(), v[2], Ctot, c, 0) for o, v, c in todo])
+            lib.adr_copy_pieces(ctypes.cast(arr, ctypes.c_void_p), len(todo), N * H * W, stream())
+        else:
+            for o, v, _ in todo:
+                _ew(EW_COPY, (o, o.data_ptr(), Ctot), v)
         ctx.sizes = sizes
         # pieces that are fan-out views with a gradient sink: backward can make their slice the sink's buffer
         ctx.sinks = [getattr(x, "_adr_sink", None) for x in xs]

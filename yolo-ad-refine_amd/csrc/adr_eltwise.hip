@@ -422,6 +422,50 @@ extern "C" int adr_axpy_batched(const adr_axpy_entry* entries, int count, void* 
 }
 
 
+constexpr int CPB_MAX = 8;
+struct CopyBatch {
+  adr_copy_piece e[CPB_MAX];
+  int start[CPB_MAX + 1];
+  int count;
+  unsigned npix;
+};
+// block b belongs to piece j (start[j] <= b < start[j+1]); a thread moves one 16-byte chunk (8 bf16 channels)
+__global__ void __launch_bounds__(256) copy_pieces_kernel(CopyBatch b) {
+  int j = 0;
+  while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
+  const adr_copy_piece& en = b.e[j];
+  const unsigned c8 = (unsigned)en.C / 8u;
+  const unsigned i = (unsigned)(blockIdx.x - b.start[j]) * 256u + threadIdx.x;
+  if (i >= b.npix * c8) return;
+  const unsigned pix = i / c8, c = (i - pix * c8) * 8u;
+  st16(reinterpret_cast<__bf16*>(en.dst) + (size_t)pix * en.dcs + c,
+       ld16(reinterpret_cast<const __bf16*>(en.src) + (size_t)pix * en.scs + c));
+}
+
+extern "C" int adr_copy_pieces(const adr_copy_piece* pieces, int count, long npix, void* stream) {
+  ADR_REQUIRE(count >= 0 && (count == 0 || pieces) && npix >= 0 && npix < (1l << 31), "copy_pieces: count=%d npix=%ld",
+              count, npix);
+  for (int b0 = 0; b0 < count; b0 += CPB_MAX) {
+    CopyBatch cb{};
+    cb.count = count - b0 < CPB_MAX ? count - b0 : CPB_MAX;
+    cb.npix = (unsigned)npix;
+    long blocks = 0;
+    for (int j = 0; j < cb.count; ++j) {
+      const adr_copy_piece& en = pieces[b0 + j];
+      ADR_REQUIRE(en.src && en.dst && en.C > 0 && en.C % 8 == 0 && en.scs % 8 == 0 && en.dcs % 8 == 0 &&
+                      ((uintptr_t)en.src & 15) == 0 && ((uintptr_t)en.dst & 15) == 0 && npix * (en.C / 8) < (1l << 31),
+                  "copy_pieces: piece %d (C=%d scs=%d dcs=%d)", b0 + j, en.C, en.scs, en.dcs);
+      cb.e[j] = en;
+      cb.start[j] = (int)blocks;
+      blocks += cdiv(npix * (en.C / 8), 256);
+    }
+    ADR_REQUIRE(blocks < (1l << 31), "copy_pieces: grid");
+    cb.start[cb.count] = (int)blocks;
+    if (blocks) hipLaunchKernelGGL(copy_pieces_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, cb);
+  }
+  return check_launch("adr_copy_pieces");
+}
+
 extern "C" int adr_axpy(long n, float a, const float* x, float* y, void* stream) {
   if (n <= 0) return ADR_OK;
   hipLaunchKernelGGL(axpy_kernel, dim3(cdiv(n, 256)), dim3(256), 0, (hipStream_t)stream, n, a, x, y);
