@@ -578,6 +578,14 @@ int adr_dwconv_bwd(int dtype, const void* x, int xcs, const void* dy, int dcs, c
  * deferred flush through adr_wgrad_reduce_batched (K = 1, RS = k*k, the [C][k*k] parameter layout). */
 int adr_dwconv_wgrad_partials(int dtype, const void* x, int xcs, const void* dy, int dcs, int N, int H, int W, int C,
                               int k, float* ws, size_t ws_bytes, int* chunks, void* stream);
+/* The same partial rows plus the depthwise conv's bias gradient (column sums of dy per image, from the staged dy
+ * slab the weight gradient already holds): bias_part [N][2][C], half 0 written (adr_partial_sum, which = 0).
+ * Only on the whole-image kernels (adr_dwconv_wgrad_bias_fusable). Reference: nn.Conv2d(groups=C, bias=True)'s bias
+ * backward in the C2PTSSA / EDFFN / Mona depthwise convs (block.py:2376-2710). */
+int adr_dwconv_wgrad_bias_fusable(int dtype, int H, int W, int C, int k, int xcs, int dcs);
+int adr_dwconv_wgrad_partials_bias(int dtype, const void* x, int xcs, const void* dy, int dcs, int N, int H, int W,
+                                   int C, int k, float* ws, size_t ws_bytes, float* bias_part, int* chunks,
+                                   void* stream);
 /* AdaptiveDynamicTanh (:2493-2577): y = (sum_i tanh(alpha_i x) imp[n,i]) * w[c] + b[c]; imp from adr_gate_mlp. */
 int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alphas, const float* imp, const float* w,
                  const float* b, void* y, int ycs, int N, int HW, int C, void* stream);

@@ -3040,12 +3040,23 @@ class DWConvFn(torch.autograd.Function):
                            ctypes.c_void_p(dx.data_ptr()) if dx is not None else None,
                            dx.stride(3) if dx is not None else C, None if defer else pdw, N, H, W, C, k, acc, dacc,
                            fptr(ws), wsb, stream())
+        db, fused = None, False
         if defer:
             chunks = ctypes.c_int(0)
-            lib.adr_dwconv_wgrad_partials(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]),
-                                          vd[2], N, H, W, C, k, fptr(ws), wsb, ctypes.byref(chunks), stream())
+            if (has_b and ctx.needs_input_grad[2] and _fuse_wg_bias() and
+                    lib.adr_dwconv_wgrad_bias_fusable(dcode(x.dtype), H, W, C, k, vx[2], vd[2])):
+                # the bias gradient's column sums from the staged dy slab of the same launch
+                bpart = torch.empty(N * 2 * C, dtype=torch.float32, device=x.device)
+                lib.adr_dwconv_wgrad_partials_bias(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2],
+                                                   ctypes.c_void_p(vd[1]), vd[2], N, H, W, C, k, fptr(ws), wsb,
+                                                   fptr(bpart), ctypes.byref(chunks), stream())
+                db, fused = _bias_rows(ctx.pb, C, N, bpart, x.device), True
+            else:
+                lib.adr_dwconv_wgrad_partials(dcode(x.dtype), ctypes.c_void_p(vx[1]), vx[2], ctypes.c_void_p(vd[1]),
+                                              vd[2], N, H, W, C, k, fptr(ws), wsb, ctypes.byref(chunks), stream())
             _dfr().add(ws, k * k * C, chunks.value, pdw, 1, C, C, k * k, 0, dacc)
-        db = _bias_grad(vd[0], C, N, H * W, vd[2], ctx.pb) if has_b and ctx.needs_input_grad[2] else None
+        if has_b and ctx.needs_input_grad[2] and not fused:
+            db = _bias_grad(vd[0], C, N, H * W, vd[2], ctx.pb)
         return (None if ctx.sink is not None else dx), grad_ret(ctx.pw, dw), db, None
 
 

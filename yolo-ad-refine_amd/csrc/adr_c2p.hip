@@ -312,11 +312,29 @@ __global__ void __launch_bounds__(256) dw_img_act_kernel(const __bf16* x, int xc
   dw_img_body<__bf16, false, CB, true, F32S>(x, xcs, w, shift, y, ycs, H, W, C, k, 0, scale, act);
 }
 
+// the depthwise conv's bias gradient for this (image, channel slab): column sums of the staged fp32 dy image,
+// CB channels x (256 / CB) pixel splits combined in a fixed order; bias_part[n][2][C], half 0
+template <int CB>
+__device__ __forceinline__ void dw_bias_rows(const float* ds, int HW, int n, int cb0, int C, float* bias_part) {
+  __shared__ float bred[256];
+  constexpr int PSPL = 256 / CB;
+  const int c = threadIdx.x % CB, ps = threadIdx.x / CB;
+  float sacc = 0.f;
+  for (int pix = ps; pix < HW; pix += PSPL) sacc += ds[(long)pix * CB + c];
+  bred[threadIdx.x] = sacc;
+  __syncthreads();
+  if (threadIdx.x < CB) {
+    float t = 0.f;
+    for (int q = 0; q < PSPL; ++q) t += bred[q * CB + threadIdx.x];
+    if (cb0 + (int)threadIdx.x < C) bias_part[(long)n * 2 * C + cb0 + threadIdx.x] = t;
+  }
+}
+
 // weight gradient: items (tap, 4-channel group, pixel split PS) over fp32 copies of the padded image and of dy
 // in LDS (converted once at staging), partial sums combined in LDS in fixed order; partial[n][t][c]
 template <typename T, int CB>
 __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, const T* dy, int dcs, int H, int W,
-                                                           int C, int k, float* partial) {
+                                                           int C, int k, float* partial, float* bias_part) {
   constexpr int NV = CB / 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
   const int n = blockIdx.x, cb0 = blockIdx.y * CB, p = k / 2, kk = k * k;
@@ -327,6 +345,7 @@ __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, 
   stage_img_f32<T, CB>(x + (long)n * H * W * xcs, xcs, H, W, p, cb0, C, CB, xs);
   stage_img_f32<T, CB>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
   __syncthreads();
+  if (bias_part) dw_bias_rows<CB>(ds, H * W, n, cb0, C, bias_part);
   const int pairs = kk * NV;
   int PS = 1;  // pixel splits per (tap, group): a power of two, so split groups never straddle a 256 pass
   while (PS * 2 * pairs <= 256) PS *= 2;
@@ -373,7 +392,7 @@ __global__ void __launch_bounds__(256) dw_wgrad_img_kernel(const T* x, int xcs, 
 // lanes of one wave, combined by an xor butterfly (fixed order: deterministic).
 template <typename T, int CB, int KS>
 __global__ void __launch_bounds__(256) dw_wgrad_row_kernel(const T* x, int xcs, const T* dy, int dcs, int H, int W,
-                                                           int C, float* partial) {
+                                                           int C, float* partial, float* bias_part) {
   constexpr int NV = CB / 4, P = KS / 2, KK = KS * KS;
   extern __shared__ __attribute__((aligned(16))) unsigned char dwsm[];
   const int n = blockIdx.x, cb0 = blockIdx.y * CB;
@@ -383,6 +402,7 @@ __global__ void __launch_bounds__(256) dw_wgrad_row_kernel(const T* x, int xcs, 
   stage_img_f32<T, CB>(x + (long)n * H * W * xcs, xcs, H, W, P, cb0, C, CB, xs);
   stage_img_f32<T, CB>(dy + (long)n * H * W * dcs, dcs, H, W, 0, cb0, C, CB, ds);
   __syncthreads();
+  if (bias_part) dw_bias_rows<CB>(ds, H * W, n, cb0, C, bias_part);
   constexpr int pairs = KS * NV;
   int RS = 1;  // row splits per (ky, group): a power of two <= 64 dividing 256, so a group sits in one wave
   while (RS * 2 * pairs <= 256 && RS < 64 && RS < H) RS *= 2;
@@ -1336,7 +1356,7 @@ extern "C" size_t adr_dwconv_wgrad_workspace(int N, int H, int W, int C, int k) 
 
 // the depthwise weight gradient's partial rows [chunks][k*k][C] into ws; returns chunks (N on the whole-image path)
 static int dw_wgrad_partials(int dtype, const void* x, int xcs, const void* dy, int dcs, int N, int H, int W, int C,
-                             int k, float* ws, hipStream_t st) {
+                             int k, float* ws, hipStream_t st, float* bias_part = nullptr) {
   const int v = dtype == ADR_BF16 ? 8 : 4;
   const long npix = (long)N * H * W;
   const int wcb = dw_wg_cb(H, W, k);
@@ -1358,19 +1378,19 @@ static int dw_wgrad_partials(int dtype, const void* x, int xcs, const void* dy, 
   if (dtype == ADR_BF16 && dw_row_ok() && (k == 3 || k == 5 || k == 7)) {                                         \
     if (k == 3)                                                                                                     \
       hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 3>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,    \
-                         (const __bf16*)dy, dcs, H, W, C, ws);                                                      \
+                         (const __bf16*)dy, dcs, H, W, C, ws, bias_part);                                           \
     else if (k == 5)                                                                                                \
       hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 5>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,    \
-                         (const __bf16*)dy, dcs, H, W, C, ws);                                                      \
+                         (const __bf16*)dy, dcs, H, W, C, ws, bias_part);                                           \
     else                                                                                                            \
       hipLaunchKernelGGL((dw_wgrad_row_kernel<__bf16, CBV, 7>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,    \
-                         (const __bf16*)dy, dcs, H, W, C, ws);                                                      \
+                         (const __bf16*)dy, dcs, H, W, C, ws, bias_part);                                           \
   } else if (dtype == ADR_BF16)                                                                                     \
     hipLaunchKernelGGL((dw_wgrad_img_kernel<__bf16, CBV>), ig, dim3(256), ism, st, (const __bf16*)x, xcs,         \
-                       (const __bf16*)dy, dcs, H, W, C, k, ws);                                                     \
+                       (const __bf16*)dy, dcs, H, W, C, k, ws, bias_part);                                          \
   else                                                                                                              \
     hipLaunchKernelGGL((dw_wgrad_img_kernel<float, CBV>), ig, dim3(256), ism, st, (const float*)x, xcs,           \
-                       (const float*)dy, dcs, H, W, C, k, ws)
+                       (const float*)dy, dcs, H, W, C, k, ws, bias_part)
   if (wcb == DW_CB_WG) {
     ADR_DWWG(DW_CB_WG);
   } else {
@@ -1417,6 +1437,21 @@ extern "C" int adr_dwconv_wgrad_partials(int dtype, const void* x, int xcs, cons
   ADR_REQUIRE(ws_bytes >= adr_dwconv_wgrad_workspace(N, H, W, C, k), "dwconv_wgrad_partials: workspace");
   *chunks = dw_wgrad_partials(dtype, x, xcs, dy, dcs, N, H, W, C, k, ws, (hipStream_t)stream);
   return check_launch("adr_dwconv_wgrad_partials");
+}
+
+extern "C" int adr_dwconv_wgrad_bias_fusable(int dtype, int H, int W, int C, int k, int xcs, int dcs) {
+  const int v = dtype == ADR_BF16 ? 8 : 4;
+  return C % v == 0 && xcs % v == 0 && dcs % v == 0 && dw_wg_cb(H, W, k) ? 1 : 0;
+}
+
+extern "C" int adr_dwconv_wgrad_partials_bias(int dtype, const void* x, int xcs, const void* dy, int dcs, int N, int H,
+                                              int W, int C, int k, float* ws, size_t ws_bytes, float* bias_part,
+                                              int* chunks, void* stream) {
+  ADR_REQUIRE(chunks && ws && bias_part && adr_dwconv_wgrad_bias_fusable(dtype, H, W, C, k, xcs, dcs),
+              "dwconv_wgrad_partials_bias: H=%d W=%d C=%d k=%d not on the whole-image kernels", H, W, C, k);
+  ADR_REQUIRE(ws_bytes >= adr_dwconv_wgrad_workspace(N, H, W, C, k), "dwconv_wgrad_partials_bias: workspace");
+  *chunks = dw_wgrad_partials(dtype, x, xcs, dy, dcs, N, H, W, C, k, ws, (hipStream_t)stream, bias_part);
+  return check_launch("adr_dwconv_wgrad_partials_bias");
 }
 
 extern "C" int adr_adyt_fwd(int dtype, const void* x, int xcs, const float* alphas, const float* imp, const float* w,
