@@ -1077,7 +1077,6 @@ __global__ void __launch_bounds__(256) edffn_dw_kernel(const T* x, int xcs, cons
 // (16-byte pixel loads), and each wave accumulates two channels' 64 x 64 dM = dY (64 x P) * X^T (P x 64) over its
 // split on v_mfma_f32_16x16x4_f32 (16 f32x4 tiles per channel). The per-channel kernel above gathered one 2-byte
 // element of a 256-byte pixel row per lane (48 us per call at bs 64, 20x20, C = 128). Same partial layout.
-template <bool UNUSED = false>
 __global__ void __launch_bounds__(256) edffn_dw_mfma_kernel(const __bf16* x, int xcs, const __bf16* dy, int dcs,
                                                             int N, int H, int W, int C, float* part) {
   __shared__ __attribute__((aligned(16))) float Ds[EA_CG * 64 * EA_XP];
@@ -1625,7 +1624,7 @@ extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, 
   if (dw) {
     float* part = ws + edffn_pad_floats(N, H, W, C);
     if (edffn_mfma_ok(dtype, C, xcs, dcs))
-      hipLaunchKernelGGL(edffn_dw_mfma_kernel<>, dim3((unsigned)(C / EA_CG * EDFFN_DWS)), dim3(256), 0, st,
+      hipLaunchKernelGGL(edffn_dw_mfma_kernel, dim3((unsigned)(C / EA_CG * EDFFN_DWS)), dim3(256), 0, st,
                          (const __bf16*)x, xcs, (const __bf16*)dy, dcs, N, H, W, C, part);
     else if (dtype == ADR_BF16)
       hipLaunchKernelGGL(edffn_dw_kernel<__bf16>, dim3(C, EDFFN_DWS), dim3(256), 0, st, (const __bf16*)x, xcs,

@@ -297,7 +297,7 @@ __device__ __forceinline__ int wave_sum_i(int v) {
 // elements are >= T (no tie spills over the cut) every correct top-k selects the same set, and the lanes flag
 // their entries >= T. Otherwise — ties at T beyond the cut (typically T = 0: fewer than 10 positive align values),
 // a lane list truncated at a value equal to T, or a NaN — the heap-select itself decides which tied elements stay,
-// so the row runs the serial path below. Round 5: 177 -> see DESIGN §9 (the serial heap on long positive runs was
+// so the row runs the serial path below. Round 5: 177 -> 33 us per step (the serial heap on long positive runs was
 // one dependent LDS chain per insert).
 // Serial path: the same sequence of heap operations as the scalar heap-select: candidates are screened 64 at a
 // time against the current heap top (a ballot), and only those that beat it are inserted, in index order, by
