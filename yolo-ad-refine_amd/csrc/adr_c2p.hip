@@ -1562,10 +1562,11 @@ extern "C" int adr_edffn_build(const float* w, const float* basis, int C, int nu
 
 // the matrix-core apply: bf16 tensors, 8-channel groups, 16-byte aligned channel rows (ADR_EDFFN_MFMA=0: the
 // per-channel kernel, A/B)
-static bool edffn_mfma_ok(int dtype, int C, int xcs, int ycs) {
+static bool edffn_mfma_ok(int dtype, int C, int xcs, int ycs, const void* p0 = nullptr, const void* p1 = nullptr) {
   const char* e = getenv("ADR_EDFFN_MFMA");  // read per call: tests compare the two paths in one process
   const bool v = e ? atoi(e) != 0 : true;
-  return v && dtype == ADR_BF16 && C % EA_CG == 0 && xcs % 8 == 0 && ycs % 8 == 0;
+  return v && dtype == ADR_BF16 && C % EA_CG == 0 && xcs % 8 == 0 && ycs % 8 == 0 &&
+         ((uintptr_t)p0 & 15) == 0 && ((uintptr_t)p1 & 15) == 0;  // 16-byte pixel-row loads / stores
 }
 
 extern "C" int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, void* y, int ycs, int N, int H, int W,
@@ -1574,7 +1575,7 @@ extern "C" int adr_edffn_fwd(int dtype, const void* x, int xcs, const float* M, 
   ADR_REQUIRE(N > 0 && H > 0 && W > 0 && C > 0 && H >= 4 && W >= 4, "edffn: N=%d H=%d W=%d C=%d", N, H, W, C);
   const long np = (long)N * ((H + 7) / 8) * ((W + 7) / 8);
   dim3 grid((unsigned)(cdiv(np, EDFFN_PPB) * C));
-  if (edffn_mfma_ok(dtype, C, xcs, ycs))
+  if (edffn_mfma_ok(dtype, C, xcs, ycs, x, y))
     hipLaunchKernelGGL(edffn_apply_mfma_kernel<false>, dim3((unsigned)(C / EA_CG * cdiv(np, EA_PG))), dim3(256), 0, st,
                        (const __bf16*)x, xcs, M, y, ycs, N, H, W, C);
   else if (dtype == ADR_BF16)
@@ -1605,7 +1606,7 @@ extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, 
   const long np = (long)N * ((H + 7) / 8) * ((W + 7) / 8);
   dim3 grid((unsigned)(cdiv(np, EDFFN_PPB) * C));
   float* dpad = ws;
-  if (edffn_mfma_ok(dtype, C, dcs, 8))
+  if (edffn_mfma_ok(dtype, C, dcs, 8, dy))
     hipLaunchKernelGGL(edffn_apply_mfma_kernel<true>, dim3((unsigned)(C / EA_CG * cdiv(np, EA_PG))), dim3(256), 0, st,
                        (const __bf16*)dy, dcs, M, (void*)dpad, 0, N, H, W, C);
   else if (dtype == ADR_BF16)
@@ -1623,7 +1624,7 @@ extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, 
                        (float*)dx, ocs);
   if (dw) {
     float* part = ws + edffn_pad_floats(N, H, W, C);
-    if (edffn_mfma_ok(dtype, C, xcs, dcs))
+    if (edffn_mfma_ok(dtype, C, xcs, dcs, x, dy))
       hipLaunchKernelGGL(edffn_dw_mfma_kernel, dim3((unsigned)(C / EA_CG * EDFFN_DWS)), dim3(256), 0, st,
                          (const __bf16*)x, xcs, (const __bf16*)dy, dcs, N, H, W, C, part);
     else if (dtype == ADR_BF16)
@@ -1632,7 +1633,7 @@ extern "C" int adr_edffn_bwd(int dtype, const void* x, int xcs, const void* dy, 
     else
       hipLaunchKernelGGL(edffn_dw_kernel<float>, dim3(C, EDFFN_DWS), dim3(256), 0, st, (const float*)x, xcs,
                          (const float*)dy, dcs, N, H, W, C, part);
-    if (edffn_mfma_ok(dtype, C, xcs, dcs))
+    if (edffn_mfma_ok(dtype, C, xcs, dcs, x, dy))
       hipLaunchKernelGGL(edffn_dw_fin2_kernel, dim3(C, 2), dim3(256), 0, st, part, C, basis, nuv, dw, dw_accumulate);
     else
       hipLaunchKernelGGL(edffn_dw_fin_kernel, dim3(C), dim3(256), 0, st, part, C, basis, nuv, dw, dw_accumulate);
