@@ -2,7 +2,9 @@
 640x640 batches, bs 64 per GPU (BASELINE.json configs[2] per GPU; configs[3] = 8 GPUs x 64 via DDP/RCCL).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--bs 64] [--img 640] [--dtype bf16|fp32]
-  N>1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+  N>1: python bench.py --gpus N starts the N ranks itself (python -m torch.distributed.run ... as a child process);
+       under an outside launcher (torch.distributed.run --nproc-per-node N ... bench.py --gpus N) it runs as a rank.
+       WORLD_SIZE != N, or fewer than N visible GPUs: exit code 2 with the reason on stderr.
   python bench.py --infer [--infer-bs 32]   BASELINE.json configs[1]: batched inference (uint8 -> eval forward
                                             -> decode -> NMS) as its own JSON line
 
@@ -352,20 +354,33 @@ def main():
     ap.add_argument("--augment-bench", type=int, default=1, help="time the GPU training augmentation chain")
     ap.add_argument("--conv-fp8", action="store_true",
                     help="forward convs on the fp8 (e4m3) MFMA engine (configs[4]'s fp8 conv path; backward bf16)")
+    ap.add_argument("--ddp-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend of the N-rank run (nccl = RCCL over xGMI; gloo for tests)")
+    ap.add_argument("--share-gpu", action="store_true",
+                    help="tests only (with --ddp-backend gloo): every rank on GPU rank %% visible, so the N-rank "
+                         "launch path runs on a one-GPU box")
     args = ap.parse_args()
+    if args.share_gpu and args.ddp_backend != "gloo":
+        print("bench.py: --share-gpu needs --ddp-backend gloo (RCCL refuses two ranks on one GPU)", file=sys.stderr)
+        sys.exit(2)
+    # --gpus N: validate against the environment and start the N ranks ourselves when no launcher did, all before
+    # any GPU call (a child process, never exec; trainer.py:184-204 / utils/dist.py:56-66)
+    from adrefine.engine.ddp import LaunchError, check_world, launch_ranks
+    try:
+        mode = check_world(args.gpus, share_gpu=args.share_gpu)
+    except LaunchError as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if mode == "launch":
+        sys.exit(launch_ranks(args.gpus, Path(__file__).resolve(), sys.argv[1:]))
     if args.scale != "n":  # configs[4]: its own line; the n/640 baselines (CPU, inference) do not apply
         args.no_cpu_baseline, args.infer_steps = True, 0
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    from adrefine.engine.ddp import setup_ddp
+    rank, local, world, dev = setup_ddp(backend=args.ddp_backend, share_gpu=args.share_gpu)
     import adrefine.kernels as K
     K.CONV_FP8 = K.CONV_FP8 or args.conv_fp8
     from adrefine.engine.trainer import FusedTrainer
@@ -500,6 +515,9 @@ def main():
                                    f"{args.img}x{args.img}, synthetic COCO-shape labels, TAL+DFL+CIoU/NWD loss, "
                                    f"SGD+EMA", "global_batch": world * args.bs, "img": args.img,
                        "parallelism": f"dp{world}",
+                       "ddp": None if world == 1 else {"backend": args.ddp_backend, "launched_by": (
+                           "bench.py --gpus (child torch.distributed.run)" if os.environ.get("ADR_SELF_LAUNCHED")
+                           else "outside launcher"), "shared_gpu": args.share_gpu},
                        "nms": "not in the train step (measured in the inference leg at validator settings)"},
             "roofline": roof, "cpu_baseline": cpu, "loss_finite": finite,
             "ms_per_step_events": step_stats, "ddp_staging": staging,

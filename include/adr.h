@@ -253,6 +253,14 @@ int adr_gn_finalize_packed(const float* partial, int levels, const int* k, int N
                            float* shift, float* mean, float* rstd, void* stream);
 /* Backward coefficients of the level-packed GroupNorm (partial from adr_nc_reduce RED_BWD over the sub-images):
  * dx = A*g + B*x + C with A, B, C [N'][C] replicated per sub-image (adr_gn_bwd_finalize's gn_bwd_coef per image). */
+/* Gradient of per-image gates s feeding a GroupNorm (TaskDecomposition, nn/modules/head.py:651-667 — replaces the
+ * autograd of `weight * conv_weight` -> bmm -> gn for its gate): dL/ds = sum(dZ * Z) / s, computed as the exact
+ * eps-residue eps * rstd^2 * sum(dY' * Zhat) per group from the backward's fp32 partial rows (sum g, sum g*x) and the
+ * forward's mean / rstd (level-packed layout as adr_gn_bwd_coef_packed; an unpacked GN is levels 1, k {1}). gate /
+ * dgate per sub-image [N']: the segment's value goes to its first sub-image, 0 to the others. */
+int adr_gn_gate_grad(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows, int C, int G,
+                     const void* const* gamma, const float* mean, const float* rstd, float eps, const float* gate,
+                     float* dgate, void* stream);
 int adr_gn_bwd_coef_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows, int C,
                            int G, const void* const* gamma, const float* mean, const float* rstd, float* A, float* B,
                            float* Cc, void* stream);

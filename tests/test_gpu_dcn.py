@@ -153,3 +153,32 @@ def test_dcn_levels_one_launch_bitwise(C):
             K.DCN_LEVELS = old
     for i, (a, b) in enumerate(zip(*runs)):
         assert torch.equal(a, b), i
+
+
+def test_dcn_levels_far_scratch_reused():
+    """Two eager LevelDCNFn backwards of the same shape reuse ONE persistent far-corner scratch pair: no new
+    allocation, nothing retired (the prefix-view size check reallocated it on every call)."""
+    from adrefine import kernels as K
+    N, C, dims = 2, 64, [(24, 24), (12, 12), (6, 6)]
+    pack = K.LevelPack(N, dims)
+    g = torch.Generator().manual_seed(3)
+    old = K.DCN_LEVELS
+    K.DCN_LEVELS = True
+    try:
+        ptrs = []
+        for rep in range(3):
+            xd = [torch.randn(N, C, H, W, generator=g).cuda().to(torch.bfloat16)
+                  .contiguous(memory_format=torch.channels_last).requires_grad_(True) for H, W in dims]
+            od = [(torch.randn(N, 32, H, W, generator=g) * 3).cuda().to(torch.bfloat16)
+                  .contiguous(memory_format=torch.channels_last).requires_grad_(True) for H, W in dims]
+            wd = (torch.randn(C, C, 3, 3, generator=g) * (9 * C) ** -0.5).cuda().requires_grad_(True)
+            y = K.dcn_levels(K.level_join(xd, pack), K.level_join(od, pack), wd, pack)
+            y.float().square().sum().backward()
+            torch.cuda.synchronize()
+            f, fl = K._DCN_FAR[str(xd[0].device)]
+            ptrs.append((f.data_ptr(), fl.data_ptr(), len(K._DCN_FAR_RETIRED)))
+        assert ptrs[1] == ptrs[2], ptrs
+        # the kernels leave the scratch zero again
+        assert float(K._DCN_FAR[str(xd[0].device)][0].abs().max()) == 0.0
+    finally:
+        K.DCN_LEVELS = old

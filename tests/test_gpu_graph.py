@@ -109,7 +109,7 @@ def _labels_n(bs, n, seed):
 def test_graph_step_grows_target_capacity():
     """A captured trainer fed batches with 7, then 93, then 7 and 93 targets per image (COCO's Poisson(7.3) counts
     reach ~93): no error mid-training — the 93-target batch captures a 128-capacity step (capacity_bucket) and later
-    batches switch between the two captures — and every step matches the eager trainer (fp32: loss items 1e-4
+    the smaller capture is dropped (graph memory stays one captured step) — and every step matches the eager trainer (fp32: loss items 1e-4
     relative, parameters and EMA within the eager-eager spread bound). Reference: utils/loss.py:392-408 pads the
     targets per batch; trainer.py:367-398 the step loop."""
     from adrefine.engine.trainer import FusedTrainer
@@ -134,8 +134,8 @@ def test_graph_step_grows_target_capacity():
     e1, o1, _ = run(False)
     e2, o2, _ = run(False)
     g, og, caps = run(True)
-    assert caps == [7, FusedTrainer.capacity_bucket(93), 7, 128] and FusedTrainer.capacity_bucket(93) == 128
-    assert sorted(g._sets) == [7, 128]
+    assert caps == [7, 128, 128, 128] and FusedTrainer.capacity_bucket(93) == 128
+    assert sorted(g._sets) == [128]
     for a, b, c in zip(o1, og, o2):
         spread = float((a - c).abs().max())
         assert float((a - b).abs().max()) <= 10 * spread + 1e-4 * float(a.abs().max()), (a, b, c)
@@ -145,3 +145,25 @@ def test_graph_step_grows_target_capacity():
     assert d <= 10 * spread + 1e-4, (d, spread)
     ee, eg = e1.ema_state_dict(), g.ema_state_dict()
     assert max(float((ee[k] - eg[k]).abs().max()) for k in ee) <= 10 * spread + 1e-4
+
+
+def test_graph_capacity_buckets_bounded_memory():
+    """Walking through target-capacity buckets 8 -> 16 -> 32 -> 64 -> 128 keeps ONE captured step alive (ADVICE r05:
+    each set owns a private pool holding a whole step's activations): the reserved memory after the last capture
+    stays within 1.5x of what the first capture reserved."""
+    tr = _trainer()
+    bs = [{"img": synthetic_images(2, 320, seed=0).cuda(), **_labels_n(2, n, seed=1)} for n in (5, 12, 30, 60, 120)]
+    tr.step(bs[0])
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    base = torch.cuda.memory_reserved()
+    tr.capture(bs[0])
+    torch.cuda.synchronize()
+    one = torch.cuda.memory_reserved() - base
+    for b in bs[1:]:
+        tr.step(b)
+    torch.cuda.synchronize()
+    assert sorted(tr._sets) == [128]
+    grown = torch.cuda.memory_reserved() - base
+    print(f"one captured set {one / 2**20:.1f} MiB, after 4 bucket captures {grown / 2**20:.1f} MiB")
+    assert grown <= 1.5 * one + (64 << 20), (one, grown)

@@ -38,7 +38,11 @@ def test_train_forward_head_outputs():
     x = synthetic_images(2, 320, seed=int(g["img_seed"])).cuda()
     preds = m(x)
     for i, p in enumerate(preds):
-        assert_close(p.float(), g[f"pred{i}"], rtol=2e-4, atol=2e-4, what=f"pred{i}")
+        r = torch.as_tensor(g[f"pred{i}"]).double()
+        err, sc = float((p.detach().double().cpu() - r).abs().max()), float(r.abs().max())
+        print(f"pred{i}: max|d| {err:.3e} scale {sc:.3e} -> {err / (1 + sc):.2e} of (1 + max|ref|)")
+        # north_star: fp32 logits within 1e-4
+        assert_close(p.float(), g[f"pred{i}"], rtol=1e-4, atol=1e-4, what=f"pred{i}")
     # BN running statistics updated with momentum 0.03 / unbiased variance, as the reference
     sd = m.state_dict()
     assert_close(sd["model.0.bn.running_mean"], g["post_model.0.bn.running_mean"], rtol=1e-4, atol=1e-5)

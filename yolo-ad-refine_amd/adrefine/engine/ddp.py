@@ -25,7 +25,12 @@ saved or validated (trainer.py:436-444) — so skipping that broadcast changes n
 """
 from __future__ import annotations
 
+import os
 import re
+import socket
+import subprocess
+import sys
+from datetime import timedelta
 
 import torch
 
@@ -157,3 +162,93 @@ class BucketReducer:
         self.works = []
         done, self.launched = self.launched, []
         return done
+
+
+# ---- process launch and group setup (one process per GPU) -------------------------------------------------------
+
+def find_free_network_port() -> int:
+    """A free TCP port on 127.0.0.1 for the rendezvous (utils/dist.py:13-22)."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def generate_ddp_command(world_size, script, argv, port=None):
+    """The command that re-runs `script argv` as `world_size` ranks on this node (utils/dist.py:56-66: the reference
+    writes a temp trainer file and runs `python -m torch.distributed.run --nproc_per_node N --master_port P file`;
+    here the script itself is re-run with its own arguments, so no temp file). Rendezvous on 127.0.0.1."""
+    port = find_free_network_port() if port is None else int(port)
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={int(world_size)}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port), str(script), *[str(a) for a in argv]]
+
+
+class LaunchError(RuntimeError):
+    """A multi-GPU request this node or environment cannot satisfy (wrong GPU count / WORLD_SIZE mismatch)."""
+
+
+def check_world(gpus, env=None, visible=None, share_gpu=False):
+    """Validate a `--gpus N` request against the environment BEFORE any GPU call. Returns "launch" when N > 1 and
+    this process is not a rank yet (the caller re-launches itself via generate_ddp_command), "rank" when it runs as
+    one of N ranks (WORLD_SIZE == N), "single" for N == 1 outside a launcher. Raises LaunchError when WORLD_SIZE is
+    set and differs from N, or when fewer than N GPUs are visible (`visible`: device count, default
+    torch.cuda.device_count(), which does not initialise the GPU). share_gpu (tests only: gloo ranks placed on
+    GPU rank % visible) needs one visible GPU."""
+    env = os.environ if env is None else env
+    gpus = int(gpus)
+    if gpus < 1:
+        raise LaunchError(f"--gpus must be >= 1 (got {gpus})")
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise LaunchError(f"WORLD_SIZE={ws} from the launcher but --gpus {gpus}: they must agree "
+                              f"(run torch.distributed.run --nproc-per-node {gpus} ... --gpus {gpus}, or drop the "
+                              f"launcher and let --gpus {gpus} start the ranks)")
+        return "rank" if gpus > 1 else "single"
+    if gpus == 1:
+        return "single"
+    n = torch.cuda.device_count() if visible is None else int(visible)
+    if share_gpu and n >= 1:
+        return "launch"
+    if n < gpus:
+        raise LaunchError(f"--gpus {gpus} asks for {gpus} ranks (one per GPU) but {n} GPU(s) are visible")
+    return "launch"
+
+
+def launch_ranks(world_size, script, argv):
+    """Run `script argv` as world_size ranks in a CHILD process (never exec: trainer.py:184-204 runs the DDP command
+    with subprocess.run as well) and return its exit code."""
+    cmd = generate_ddp_command(world_size, script, argv)
+    print(f"DDP: launching {' '.join(cmd)}", file=sys.stderr, flush=True)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this host driver (RCCL)
+    env["ADR_SELF_LAUNCHED"] = "1"
+    return subprocess.run(cmd, env=env).returncode
+
+
+def setup_ddp(backend=None, timeout_s=10800, share_gpu=False):
+    """Per-rank process-group setup (trainer.py:217-228): device = LOCAL_RANK, backend nccl (= RCCL on ROCm) when a
+    GPU is there else gloo, with the reference's 3 h timeout. Returns (rank, local_rank, world_size, device).
+    The reference also exports TORCH_NCCL_BLOCKING_WAIT=1; that makes every `work.wait()` block the host until the
+    all-reduce finishes, which would stop the host from enqueueing the next stage-graph replay behind the bucket
+    collectives (engine/ddp.py BucketReducer), so the timeout is left to the process group's watchdog instead.
+    share_gpu (gloo only; tests on a one-GPU box): rank r uses GPU LOCAL_RANK % device_count."""
+    import torch.distributed as dist
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if backend is None:
+        backend = "nccl" if torch.cuda.is_available() and dist.is_nccl_available() else "gloo"
+    if share_gpu and backend == "nccl":
+        raise LaunchError("share_gpu needs the gloo backend (RCCL refuses two ranks on one GPU)")
+    if torch.cuda.is_available():
+        gi = local % torch.cuda.device_count() if share_gpu else local
+        torch.cuda.set_device(gi)
+        dev = torch.device("cuda", gi)
+    elif backend == "nccl":
+        raise LaunchError("backend nccl (RCCL) needs a GPU")
+    else:
+        dev = torch.device("cpu")
+    if world > 1 and not dist.is_initialized():
+        kw = {"device_id": dev} if backend == "nccl" else {}
+        dist.init_process_group(backend, timeout=timedelta(seconds=timeout_s), rank=rank, world_size=world, **kw)
+    return rank, local, world, dev

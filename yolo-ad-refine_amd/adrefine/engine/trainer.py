@@ -311,9 +311,9 @@ class FusedTrainer:
 
     def _select_capacity(self, need, b):
         """Activate the captured step with the smallest per-image target capacity >= need; capture one for
-        capacity_bucket(need) (from this batch) when none holds it. The reference pads targets per batch
-        (utils/loss.py:392-408); the padded rows are masked by the assigner, so the capacity does not change the
-        step's result — a larger batch never fails mid-training."""
+        capacity_bucket(need) (from this batch) when none holds it (capture() then drops the smaller sets). The
+        reference pads targets per batch (utils/loss.py:392-408); the padded rows are masked by the assigner, so
+        the capacity does not change the step's result — a larger batch never fails mid-training."""
         if need <= self.static_batch["gt"].shape[1] and need > self._cap_floor():
             return
         fits = [c for c in self._sets if c >= need]
@@ -331,9 +331,8 @@ class FusedTrainer:
     def capture(self, batch, max_targets=None):
         """Capture the step into HIP graphs. Call after at least one eager step (lazy caches, the parameter
         table). The batch becomes the graph's static input (targets padded to max_targets per image); later
-        `step(b)` copies b into it. Each capture is kept, keyed by its target capacity: step() switches to the
-        smallest one that holds a batch, and captures a larger bucket (capacity_bucket) on the first batch that
-        exceeds them all."""
+        `step(b)` copies b into it. The capture is kept keyed by its target capacity; the first batch that exceeds
+        it captures a larger bucket (capacity_bucket), which replaces every smaller one."""
         assert self.tab_dev is not None, "run one eager step before capture()"
         b = self._prepare(batch)
         gt = b["gt"]
@@ -378,9 +377,17 @@ class FusedTrainer:
         with torch.cuda.graph(g_opt, pool=g_stages[0].pool(), capture_error_mode=_CAPTURE_MODE):
             self._opt()
         self.graphs = (g_stages, g_opt, items)
+        # a larger capacity holds every batch a smaller one held: drop the smaller sets, so graph memory stays at
+        # ONE captured step (each set owns a private pool with a whole step's activations) however many buckets a
+        # real dataloader walks through
+        dropped = [c for c in self._sets if c < cap]
+        for c in dropped:
+            del self._sets[c]
         self._sets[cap] = (self.graphs, self.static_batch)
         self.grad.copy_(gsaved)
         torch.cuda.synchronize()
+        if dropped:
+            torch.cuda.empty_cache()  # return the dropped sets' private pools
         return self.static_batch
 
     def param_grad(self, name):

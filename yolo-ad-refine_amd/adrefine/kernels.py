@@ -11,6 +11,7 @@ Every op here launches HIP kernels from libadr_hip.so; nothing falls back to PyT
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 
@@ -1382,12 +1383,12 @@ class BnStat:
     """A training BN-act's backward statistics, taken from its only reader's data gradient: (y, scale, shift, act)
     from the forward; after that dgrad, the partials and the identity (address, geometry, version) of the dz
     buffer they were computed from — BNActFn.backward uses them only for exactly that, unmodified, buffer."""
-    __slots__ = ("y", "scale", "shift", "act", "shared", "part", "P", "key")
+    __slots__ = ("y", "scale", "shift", "act", "shared", "part", "P", "key", "ref")
 
     def __init__(self, y, scale, shift, act):
         self.y, self.scale, self.shift, self.act = y, scale, shift, act
         self.shared = False
-        self.part = self.P = self.key = None
+        self.part = self.P = self.key = self.ref = None
 
     def struct(self):
         _, yp, ycs = nhwc(self.y)
@@ -1398,13 +1399,17 @@ class BnStat:
         return t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype, t._version
 
     def set(self, part, P, dx):
-        self.part, self.P, self.key = part, P, self._key(dx)
+        # a weak reference to dx itself: a buffer freed and re-allocated at the same address is not dx
+        self.part, self.P, self.key, self.ref = part, P, self._key(dx), weakref.ref(dx)
 
     def take(self, dz):
-        """(partials, rows) when dz is the buffer the dgrad wrote them with (else None); clears the holder."""
-        ok = self.key is not None and self._key(dz) == self.key
+        """(partials, rows) when dz is the buffer the dgrad wrote them with (else None): dx still alive, dz the
+        same storage at the same geometry and version; clears the holder."""
+        dx = self.ref() if self.ref is not None else None
+        ok = (dx is not None and self._key(dz) == self.key and
+              (dz is dx or dz.untyped_storage().data_ptr() == dx.untyped_storage().data_ptr()))
         got = (self.part, self.P) if ok else None
-        self.part = self.P = self.key = None
+        self.part = self.P = self.key = self.ref = None
         return got
 
 
@@ -1475,12 +1480,30 @@ def _defer_gn(acc):
     return bool(acc) and _DEFER_GN and _dfr() is not None and _TIMING is None
 
 
+_GATE_GRAD = {}  # dy.data_ptr() -> (weakref to dy, dgate): per-image gate gradients computed by a GN backward
+
+
+def _gn_gate_grad(gate, eps, part, ks, N, chunks, sub_rows, C, groups, gammas, mean, rstd, dy):
+    """dL/ds of the per-image gate s whose output s*y this GroupNorm normalised (ScaleFn grad_from_out), from the
+    GN backward's own fp32 partial rows (adr_gn_gate_grad: the exact eps residue of the scale-invariant sum), left
+    for ScaleFn.backward under dy's address."""
+    dgate = torch.empty_like(gate)
+    kk = (ctypes.c_int * len(ks))(*ks)
+    gp, _keep = _ptrs(gammas)
+    lib.adr_gn_gate_grad(fptr(part), len(ks), ctypes.cast(kk, ctypes.c_void_p), N, chunks, sub_rows, C, groups, gp,
+                         fptr(mean), fptr(rstd), float(eps), fptr(gate), fptr(dgate), stream())
+    for key in [key for key, (r, _) in _GATE_GRAD.items() if r() is None]:
+        del _GATE_GRAD[key]
+    _GATE_GRAD[dy.data_ptr()] = (weakref.ref(dy), dgate)
+
+
 class GNActFn(torch.autograd.Function):
     """act(GroupNorm(G)(y)) with per-(image, group) statistics."""
 
     @staticmethod
     def forward(ctx, y, gamma, beta, groups, act, eps):
         dtype = y.dtype
+        ctx.gate, ctx.eps = getattr(y, "_adr_gate", None), eps  # y = s * conv(...) from ScaleFn(grad_from_out)
         y, yp, ycs = nhwc(y)
         N, C, H, W = y.shape
         HW = H * W
@@ -1543,6 +1566,8 @@ class GNActFn(torch.autograd.Function):
                 _dfr().add_gnparam(part, mean, rstd, pg, pb, N, 1, C, groups, acc_g)
             else:
                 lib.adr_gn_param_grad(fptr(part), N, C, groups, fptr(mean), fptr(rstd), pg, pb, acc_g, stream())
+            if ctx.gate is not None:
+                _gn_gate_grad(ctx.gate, ctx.eps, part, [1], N, 1, HW, C, groups, [gamma.detach()], mean, rstd, dy)
             return dy, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None
         chunks = lib.adr_nc_reduce_chunks(HW, _stats_rows(N, HW))
         part = torch.empty(N * chunks * 2 * C, dtype=torch.float32, device=dev)
@@ -1565,6 +1590,8 @@ class GNActFn(torch.autograd.Function):
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
                                fptr(Cc), 1, 1, ACT[act], N, HW, C, 0, stream())
+        if ctx.gate is not None:
+            _gn_gate_grad(ctx.gate, ctx.eps, part, [1], N, chunks, HW, C, groups, [gamma.detach()], mean, rstd, dy)
         return dy, grad_ret(gamma, dgamma), grad_ret(ctx.pbeta, dbeta), None, None, None
 
 
@@ -2286,6 +2313,8 @@ class ScaleFn(torch.autograd.Function):
         # next op consumed, instead of sum(dy * x) from the separately rounded x
         ctx.from_out = from_out and mode == "n" and res is None and x.dtype == torch.bfloat16
         ctx.save_for_backward(out if ctx.from_out else vx[0], gs)
+        if ctx.from_out and box is None:
+            out._adr_gate = gs  # the GroupNorm that reads out computes dL/dgs from its fp32 statistics
         ctx.meta = (mode, g.shape, res is not None)
         ctx.pg = g
         ctx.sink, ctx.sres = _sink_of(x), (getattr(res, "_adr_sink", None) if res is not None else None)
@@ -2314,7 +2343,13 @@ class ScaleFn(torch.autograd.Function):
                 _dfr().add_dotsum(x, vd[0], out)
                 dg = sink(ctx.pg, out.view(gshape))
             elif ctx.from_out:
-                dg = sink(ctx.pg, (_reduce_dot(x, vd[0], sum_n, sum_c) / gs.clamp_min(1e-30)).view(gshape))
+                ent = _GATE_GRAD.pop(dy.data_ptr(), None)
+                src = ent[0]() if ent is not None else None
+                if src is not None and src.shape == dy.shape and \
+                        src.untyped_storage().data_ptr() == dy.untyped_storage().data_ptr():
+                    dg = sink(ctx.pg, ent[1].view(gshape))  # the GN backward's exact residue (adr_gn_gate_grad)
+                else:
+                    dg = sink(ctx.pg, (_reduce_dot(x, vd[0], sum_n, sum_c) / gs.clamp_min(1e-30)).view(gshape))
             else:
                 dg = sink(ctx.pg, _reduce_dot(x, vd[0], sum_n, sum_c).view(gshape))
         return dx, dg, (_defer_pass(ctx.sres, dy) if has_res else None), None, None, None
@@ -2816,14 +2851,16 @@ def _dcn_far_scratch_levels(dev, N, dims, C):
     """Per-level disjoint views of the persistent far-corner scratch, for the levels-in-one-launch backward."""
     n = sum(N * H * W * C for H, W in dims)
     nt = sum(int(lib.adr_dcn_bwd_tiles(N, H, W)) for H, W in dims)
-    f, g = _dcn_far_scratch(dev, 1, 1, 1, 1)  # the current pair (grown below when too small)
-    if f.numel() < n or g.numel() < nt:
-        key = str(dev)
-        cur = _DCN_FAR.get(key)
-        _DCN_FAR_RETIRED.append(cur)
-        _DCN_FAR[key] = (torch.zeros(max(n, cur[0].numel()), dtype=torch.float32, device=dev),
-                         torch.zeros(max(nt, cur[1].numel()), dtype=torch.int32, device=dev))
-    f, g = _DCN_FAR[str(dev)]
+    key = str(dev)
+    cur = _DCN_FAR.get(key)
+    # compare against the FULL persistent pair (not a prefix view), so it grows only when really too small
+    if cur is None or cur[0].numel() < n or cur[1].numel() < nt:
+        if cur is not None:
+            _DCN_FAR_RETIRED.append(cur)
+            n, nt = max(n, cur[0].numel()), max(nt, cur[1].numel())
+        _DCN_FAR[key] = (torch.zeros(n, dtype=torch.float32, device=dev),
+                         torch.zeros(nt, dtype=torch.int32, device=dev))
+    f, g = _DCN_FAR[key]
     out, o, ot = [], 0, 0
     for H, W in dims:
         k, kt = N * H * W * C, int(lib.adr_dcn_bwd_tiles(N, H, W))
@@ -3783,6 +3820,7 @@ class GNPackFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, pack, groups, act, eps, per_level, *params):
         dtype = y.dtype
+        ctx.gate, ctx.eps = getattr(y, "_adr_gate", None), eps  # y = s * conv(...) from ScaleFn(grad_from_out)
         y, yp, ycs = nhwc(y)
         Np, C, _, S = y.shape
         dev = y.device
@@ -3834,6 +3872,9 @@ class GNPackFn(torch.autograd.Function):
         lib.adr_affine_act_bwd(dt, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0,
                                ctypes.c_void_p(dy.data_ptr()), C, 0, fptr(scale), fptr(shift), fptr(A), fptr(B),
                                fptr(Cc), 1, 1, ACT[act], Np, S, C, 0, stream())
+        if ctx.gate is not None:
+            _gn_gate_grad(ctx.gate, ctx.eps, part, list(pack.k), pack.N, chunks, S, C, groups,
+                          [params[l if per_level else 0].detach() for l in range(pack.L)], mean, rstd, dy)
         grads = [None] * len(params)
         for j in range(nl):  # dgamma / dbeta over the sub-images of level j (or of every level: shared)
             s0, n = (pack.sub0[j], pack.N * pack.k[j]) if per_level else (0, Np)

@@ -1301,6 +1301,57 @@ extern "C" int adr_gn_finalize_packed(const float* partial, int levels, const in
   return check_launch("adr_gn_finalize_packed");
 }
 
+// Gradient of a per-image gate s feeding a GroupNorm (TaskDecomposition: GN(s_b * conv(feat)), head.py:651-667).
+// GN is invariant to s up to eps, so dL/ds = sum(dZ * Z) / s is the eps-sized residue of a cancelling sum; from the
+// backward's fp32 group statistics it is exact algebra: with Z = mu + Zhat/rstd and sum(Zhat) = 0,
+//   sum_{i in g} dZ_i Z_i = sum_{i in g} dY'_i Zhat_i * (1 - var * rstd^2) = eps * rstd^2 * sum_{i in g} dY'_i Zhat_i,
+// dY' = gamma * g, sum_{i in g} dY' Zhat = sum_{c in g} gamma_c * rstd * (sum g*x - mu * sum g)   (partial rows).
+// Block per (level, image) segment; writes dL/ds / into the segment's first sub-image, 0 into the others (the
+// gate's per-sub-image expansion sums them back).
+__global__ void __launch_bounds__(256) gn_gate_grad_packed_kernel(const float* __restrict__ partial, LevelPackArgs a,
+                                                                  const float* __restrict__ mean,
+                                                                  const float* __restrict__ rstd, float eps,
+                                                                  const float* __restrict__ gate, float* dgate) {
+  int l, first, k;
+  lp_segment(a, l, first, k);
+  const int C = a.C, G = a.G, cpg = C / G;
+  __shared__ double sa[1024], sg[1024], xa[256], xb[256];
+  __shared__ double red[256];
+  gn_chan_sums(partial + (long)first * a.chunks * 2 * C, 0, k * a.chunks, C, sa, sg, xa, xb);
+  const float* gamma = a.gamma[l];
+  double t = 0.0;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    const int g = c / cpg;
+    const double mu = mean[(long)first * G + g], rs = rstd[(long)first * G + g];
+    const double gmm = gamma ? gamma[c] : 1.0;
+    t += (double)eps * rs * rs * gmm * (sg[c] - mu * sa[c]) * rs;
+  }
+  red[threadIdx.x] = t;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  for (int j = threadIdx.x; j < k; j += 256) {
+    float v = 0.0f;
+    if (j == 0) {
+      const double s = (double)gate[first];
+      v = (float)(red[0] / (fabs(s) > 1e-30 ? s : 1e-30));
+    }
+    dgate[first + j] = v;
+  }
+}
+
+extern "C" int adr_gn_gate_grad(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows,
+                                int C, int G, const void* const* gamma, const float* mean, const float* rstd,
+                                float eps, const float* gate, float* dgate, void* stream) {
+  LevelPackArgs a;
+  if (int rc = level_pack_args(a, levels, k, N, chunks, sub_rows, C, G, gamma, nullptr, "gn_gate_grad")) return rc;
+  hipLaunchKernelGGL(gn_gate_grad_packed_kernel, dim3(levels * N), dim3(256), 0, (hipStream_t)stream, partial, a,
+                     mean, rstd, eps, gate, dgate);
+  return check_launch("adr_gn_gate_grad");
+}
+
 extern "C" int adr_gn_bwd_coef_packed(const float* partial, int levels, const int* k, int N, int chunks, int sub_rows,
                                       int C, int G, const void* const* gamma, const float* mean, const float* rstd,
                                       float* A, float* B, float* Cc, void* stream) {
