@@ -284,6 +284,62 @@ def stage_overhead(model, tr, batch, bs, steps=30):
             else rccl_err}
 
 
+def lscale_bench(dev, dtype, steps=10, warmup=3, bs=16, img=1280):
+    """BASELINE.json configs[4] per GPU, as an object of the default line: the 701 yaml at l scale (depth/width
+    1.0/1.0, nn/tasks.py:1050-1051), 1280^2, bs 16, the same captured train step (fwd + loss + bwd + SGD + EMA),
+    `steps` timed replays after `warmup` eager steps + capture. MFMA fraction from BASELINE.md's 765.6 GFLOP
+    forward per image (backward = 2x forward)."""
+    import torch
+    import yaml
+
+    from adrefine.data.synthetic import train_batch
+    from adrefine.engine.trainer import FusedTrainer
+    from adrefine.nn.tasks import DetectionModel
+    torch.cuda.synchronize()
+    torch.cuda.reset_peak_memory_stats(dev)
+    cfg = yaml.safe_load(CFG.read_text())
+    cfg["scale"] = "l"
+    torch.manual_seed(0)
+    model = DetectionModel(cfg, compute_dtype=dtype).to(dev)
+    tr = FusedTrainer(model, batch_size=bs, world_size=1)
+    batch, _ = train_batch(bs, img, seed=11, device=dev, u8=True)
+    for _ in range(warmup):
+        tr.step(batch)
+    tr.capture(batch)
+    tr.step(batch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        items = tr.step(batch)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    ips = bs * steps / dt
+    peak = torch.cuda.max_memory_allocated(dev) / 2 ** 30
+    finite = bool(torch.isfinite(items).all())
+    tr.graphs, tr._sets = None, {}
+    del tr, model
+    torch.cuda.empty_cache()
+    mfma_peak = BF16_MFMA_PEAK_TF if dtype == torch.bfloat16 else F32_MFMA_PEAK_TF
+    return {"config": f"BASELINE configs[4] per GPU: yolo11-701-YOLO-AD-Refine.yaml (l) train step bs={bs} "
+                      f"{img}x{img}, hipGraph, {steps} timed steps after {warmup} warm-up + capture",
+            "value": round(ips, 2), "unit": "images/s", "ms_per_step": round(1000 * dt / steps, 3),
+            "flops_per_img": 3 * 765.6e9, "mfma_frac": round(ips * 3 * 765.6e9 / (mfma_peak * 1e12), 4),
+            "peak_hbm_gib": round(peak, 2), "loss_finite": finite, "dtype": str(dtype).split(".")[-1],
+            "fp8": "not used: the e4m3 forward-conv engine (--conv-fp8) is not faster than bf16 at this config "
+                   "(DESIGN.md §9)"}
+
+
+def step_traffic():
+    """Whole-step HBM traffic per image from profiles/step_traffic.json (scripts/step_traffic.py: PMC bytes per
+    launch x launches per replayed step, per kernel); None when absent."""
+    f = ROOT / "profiles" / "step_traffic.json"
+    if not f.exists():
+        return None
+    d = json.loads(f.read_text())
+    return {"traffic_bytes_per_img": d["traffic_bytes_per_img"], "traffic_over_alg": d["traffic_over_alg"],
+            "coverage_of_kernel_time": d["coverage"], "source": "profiles/step_traffic.json (" + d["source"] + ")"}
+
+
 def augment_bench(bs, img, dev, reps=5):
     """The training augmentation chain (data/augment.py v8_transforms, default hyp) on a synthetic dataset: host side
     (draws, labels, plans) per batch and the fused GPU render (adr_augment_u8) per batch, HIP events on its stream."""
@@ -352,6 +408,8 @@ def main():
     ap.add_argument("--scale", default="n", choices=["n", "s", "m", "l", "x"],
                     help="model scale of the 701 yaml (configs[4] = l at 1280^2, bs 16/GPU)")
     ap.add_argument("--augment-bench", type=int, default=1, help="time the GPU training augmentation chain")
+    ap.add_argument("--lscale-steps", type=int, default=10,
+                    help="timed steps of the configs[4] l/1280/bs16 object in the default line (0: skip)")
     ap.add_argument("--conv-fp8", action="store_true",
                     help="forward convs on the fp8 (e4m3) MFMA engine (configs[4]'s fp8 conv path; backward bf16)")
     ap.add_argument("--ddp-backend", default="nccl", choices=["nccl", "gloo"],
@@ -474,6 +532,11 @@ def main():
                 roof["network"] = {"bytes_per_img": NET_BYTES_PER_IMG, "flops_per_img": NET_FLOPS_PER_IMG,
                                    "hbm_frac": round(ips * NET_BYTES_PER_IMG / (HBM_PEAK_GBS * 1e9), 4),
                                    "mfma_frac": round(ips * NET_FLOPS_PER_IMG / (mfma_peak * 1e12), 4)}
+                st = step_traffic()
+                if st is not None and args.bs == 64:
+                    roof["network"].update(st)
+                    roof["network"]["traffic_gbs_at_this_step_rate"] = round(
+                        ips * st["traffic_bytes_per_img"] / 1e9, 1)
             elif args.scale == "l" and args.img == 1280:  # 765.6 GFLOP fwd per image, bwd = 2x fwd
                 roof["network"] = {"flops_per_img": 3 * 765.6e9,
                                    "mfma_frac": round(ips * 3 * 765.6e9 / (mfma_peak * 1e12), 4)}
@@ -526,6 +589,11 @@ def main():
             "augment": (augment_bench(args.bs, args.img, dev) if world == 1 and args.augment_bench and
                         args.scale == "n" else None),
         }
+        if world == 1 and args.scale == "n" and args.lscale_steps > 0 and not args.no_graph:
+            graphs, tr.graphs, tr._sets = tr.graphs, None, {}  # free the n step's graph pool first
+            del graphs
+            torch.cuda.empty_cache()
+            out["lscale"] = lscale_bench(dev, dtype, steps=args.lscale_steps)
         print(json.dumps(out), flush=True)
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -37,8 +37,8 @@ def main():
         res[k] = {"launches": len(fv), "read_bytes_per_launch": round(rd), "write_bytes_per_launch": round(wr),
                   "hbm_bytes_per_launch": round(rd + wr)}
     doc = {"source": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE (separate passes) over "
-                     "`python bench.py --no-graph --steps 2 --warmup 1 --roofline-steps 1 --no-cpu-baseline --infer-steps 0 "
-                     "--stage-check 0`; "
+                     "`python bench.py --no-graph --steps 2 --warmup 1 --roofline-steps 0 --no-cpu-baseline --infer-steps 0 "
+                     "--stage-check 0 --augment-bench 0 --lscale-steps 0` (eager steps only: the replayed step's launch mix); "
                      "read = 2 x FETCH_SIZE x 1 KiB (gfx950 half-count correction), write = WRITE_SIZE x 1 KiB",
            "kernels": dict(sorted(res.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"] * kv[1]["launches"]))}
     json.dump(doc, open(out, "w"), indent=1)

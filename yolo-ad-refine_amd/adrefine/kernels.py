@@ -128,6 +128,63 @@ def _ptr(v):
     return v.value if isinstance(v, ctypes.c_void_p) else v
 
 
+def _entries(args, struct):
+    """The ctypes entry array a batched entry point was handed (args[0] = pointer, args[1] = count)."""
+    n = int(args[1])
+    return ctypes.cast(args[0], ctypes.POINTER(struct))[:n] if n > 0 and _ptr(args[0]) else []
+
+
+# batched entry points: algorithmic bytes summed over their entries (each entry's tensors touched once)
+_BATCHED_BYTES = {
+    "adr_wgrad_reduce_batched": lambda a: sum(
+        4 * (e.splits * e.K * e.RS * e.Cp + e.K * e.C * e.RS * (2 if e.accumulate else 1))
+        for e in _entries(a, WgradEntry)),
+    "adr_nc_reduce_batched": lambda a: sum(2 * e.N * e.HW * e.C + 4 * e.N * e.chunks * 2 * e.C
+                                           for e in _entries(a, ColsumEntry)),
+    "adr_partial_sum_batched": lambda a: sum(4 * (e.P * e.C + e.C * (2 if e.accumulate else 1))
+                                             for e in _entries(a, PsumEntry)),
+    "adr_axpy_batched": lambda a: sum(12 * e.n for e in _entries(a, AxpyEntry)),
+    "adr_gn_param_grad_batched": lambda a: sum(
+        4 * (e.N * e.chunks * 2 * e.C + 2 * e.N * e.G + 2 * e.C * (2 if e.accumulate else 1))
+        for e in _entries(a, GnParamEntry)),
+    "adr_dotsum_batched": lambda a: sum(4 * e.N * e.HW * e.C + 4 * e.N * e.chunks * 2 * e.C
+                                        for e in _entries(a, DotsumEntry)),
+    "adr_copy_pieces": lambda a: sum(4 * int(a[2]) * e.C for e in _entries(a, CopyPiece)),
+}
+
+
+def _scan_tensors(v, want, found, depth=0):
+    if torch.is_tensor(v):
+        if v.is_cuda:
+            p = v.data_ptr()
+            if p in want:
+                found[p] = max(found.get(p, 0), v.numel() * v.element_size())
+        return
+    if depth < 1 and isinstance(v, (tuple, list)) and len(v) <= 64:
+        for u in v:
+            _scan_tensors(u, want, found, depth + 1)
+
+
+def _generic_bytes(name, args):
+    """Algorithmic bytes of an entry point without its own estimator: the logical size of every device tensor it is
+    handed (each read or written once), found by matching its pointer arguments against the tensors live in the
+    calling frames (the autograd Function that issued it). None when no pointer matched."""
+    import sys
+    types_ = lib.protos.get(name, (None, []))[1]
+    want = {_ptr(a) for a, t in zip(args, types_) if t is ctypes.c_void_p and _ptr(a)}
+    if not want:
+        return None
+    found = {}
+    f = sys._getframe(3)
+    for _ in range(4):
+        if f is None or len(found) == len(want):
+            break
+        for v in list(f.f_locals.values()):
+            _scan_tensors(v, want, found)
+        f = f.f_back
+    return sum(found.values()) if found else None
+
+
 _UNTIMED = ("_symbol", "_workspace", "_splits", "_tiles", "_chunks", "_size", "_floats", "_supported", "adr_set_f32")
 
 
@@ -161,6 +218,10 @@ def _hook_call(name, fn, args):
                 label = label.replace("__bf16", "float")
             nbytes = int(spec[1](args))
             rep = TIMING_REPEAT if spec[2](args) else 1
+        elif name in _BATCHED_BYTES:
+            nbytes = int(_BATCHED_BYTES[name](args))
+        else:
+            nbytes = _generic_bytes(name, args)
         shape = _call_site() if name in _SITE_LABELS else ""
         if name == "adr_ew":
             shape = f"op{args[1]}{'+acc' if args[15] else ''} {args[11]}px x{args[12]}ch @{shape}"
@@ -196,6 +257,24 @@ def roofline_report(recs, dtype, hbm_gbs, mfma_tf):
         a[3] += t
         a[4] = a[4] and nb is not None
     total_t = sum(v[3] for v in agg.values())
+    # whole-step accounting: per label, ideal = max(bytes / HBM peak, flops / MFMA peak) summed over its launches;
+    # lost = measured - ideal; worst = the label losing the most time (labels without bytes count as all lost)
+    ideal = {}
+    for tag_, nb_, fl_, t_ in recs:
+        ideal[tag_] = ideal.get(tag_, 0.0) + max((nb_ or 0) / (hbm_gbs * 1e9), (fl_ or 0) / (mfma_tf * 1e12))
+    known_t = sum(v[3] for v in agg.values() if v[4])
+    known_ideal = sum(ideal[k] for k, v in agg.items() if v[4])
+    lost = {k: v[3] - ideal[k] for k, v in agg.items()}
+    wk = max(lost, key=lost.get)
+    worst = {"kernel": wk, "launches": agg[wk][0], "ms_total": round(1e3 * agg[wk][3], 3),
+             "lost_ms": round(1e3 * lost[wk], 3), "attainable_frac": round(ideal[wk] / agg[wk][3], 4)
+             if agg[wk][4] else None, "has_bytes": agg[wk][4]}
+    step = {"timed_ms": round(1e3 * total_t, 3), "launches": sum(v[0] for v in agg.values()),
+            "ms_with_alg_bytes": round(1e3 * known_t, 3), "ms_without_alg_bytes": round(1e3 * (total_t - known_t), 3),
+            "labels_without_alg_bytes": sorted(k for k, v in agg.items() if not v[4]),
+            "ideal_ms": round(1e3 * known_ideal, 3),
+            "attainable_frac": round(known_ideal / known_t, 4) if known_t else None,
+            "alg_bytes": int(sum(v[1] for v in agg.values())), "alg_flops": int(sum(v[2] for v in agg.values()))}
     tag, (cnt, nb, fl, t, known) = max(agg.items(), key=lambda kv: kv[1][3])
     gbs = nb / t / 1e9 if known else None
     tfs = fl / t / 1e12
@@ -208,9 +287,12 @@ def roofline_report(recs, dtype, hbm_gbs, mfma_tf):
             "launches": cnt, "avg_us": round(1e6 * t / cnt, 2), "alg_bytes_per_launch": int(nb / cnt),
             "alg_flops_per_launch": int(fl / cnt), "achieved_gbs": None if gbs is None else round(gbs, 1),
             "achieved_tfs": round(tfs, 2), "share_of_timed_time": round(t / total_t, 3),
+            "worst": worst, "step": step,
             "kernels": {k: {"launches": v[0], "ms_total": round(1e3 * v[3], 3), "avg_us": round(1e6 * v[3] / v[0], 2),
-                            "gbs": round(v[1] / v[3] / 1e9, 1) if v[4] and v[1] else None}
-                        for k, v in sorted(agg.items(), key=lambda kv: -kv[1][3])[:25]}}
+                            "gbs": round(v[1] / v[3] / 1e9, 1) if v[4] and v[1] else None,
+                            "tfs": round(v[2] / v[3] / 1e12, 2) if v[2] else None,
+                            "frac": round(ideal[k] / v[3], 4) if v[4] else None}
+                        for k, v in sorted(agg.items(), key=lambda kv: -kv[1][3])[:40]}}
 
 
 def dcode(dtype) -> int:
@@ -1481,6 +1563,7 @@ def _defer_gn(acc):
 
 
 _GATE_GRAD = {}  # dy.data_ptr() -> (weakref to dy, dgate): per-image gate gradients computed by a GN backward
+_GN_GATE = bool(int(__import__("os").environ.get("ADR_GN_GATE", "1")))  # 0: gate gradient from sum(dy * out) (A/B)
 
 
 def _gn_gate_grad(gate, eps, part, ks, N, chunks, sub_rows, C, groups, gammas, mean, rstd, dy):
@@ -1503,7 +1586,7 @@ class GNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, gamma, beta, groups, act, eps):
         dtype = y.dtype
-        ctx.gate, ctx.eps = getattr(y, "_adr_gate", None), eps  # y = s * conv(...) from ScaleFn(grad_from_out)
+        ctx.gate, ctx.eps = getattr(y, "_adr_gate", None) if _GN_GATE else None, eps  # y = s*conv() (ScaleFn)
         y, yp, ycs = nhwc(y)
         N, C, H, W = y.shape
         HW = H * W
@@ -3820,7 +3903,7 @@ class GNPackFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, y, pack, groups, act, eps, per_level, *params):
         dtype = y.dtype
-        ctx.gate, ctx.eps = getattr(y, "_adr_gate", None), eps  # y = s * conv(...) from ScaleFn(grad_from_out)
+        ctx.gate, ctx.eps = getattr(y, "_adr_gate", None) if _GN_GATE else None, eps  # y = s*conv() (ScaleFn)
         y, yp, ycs = nhwc(y)
         Np, C, _, S = y.shape
         dev = y.device
