@@ -749,6 +749,13 @@ def _nullctx():
     return contextlib.nullcontext()
 
 
+def _dbg_flush(kind, what):
+    if _DEBUG_BNSTAT:
+        import traceback
+        print(f"deferral flush on repeated {kind} destination {what}:", "".join(traceback.format_stack(limit=5)[:-2]),
+              flush=True)
+
+
 class WgradDeferral:
     """Collects the split-K reductions of every conv weight gradient that lands in the trainer's gradient arena
     and runs them as a few batched launches (adr_wgrad_reduce_batched) when the backward pass ends, instead of
@@ -801,6 +808,7 @@ class WgradDeferral:
         """A parameter gradient computed into a temporary, to be added into the arena (sink)."""
         dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
         if dst in self.adsts:
+            _dbg_flush("axpy", n)
             self.flush()
         self.axpys.append(AxpyEntry(src.data_ptr(), dst, n))
         self.akeep.append(src)
@@ -810,6 +818,7 @@ class WgradDeferral:
         """A bias gradient (adr_partial_sum into the arena), batched the same way."""
         dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
         if dst in self.pdsts:
+            _dbg_flush("psum", C)
             self.flush()
         self.psums.append(PsumEntry(part.data_ptr(), dst, P, C, which, acc))
         self.pkeep.append(part)
@@ -831,6 +840,7 @@ class WgradDeferral:
     def add(self, ws, stride, splits, dst, K_, C_, Cp, RS_, transpose_kc, acc):
         dst = dst.value if isinstance(dst, ctypes.c_void_p) else int(dst)
         if dst in self.dsts:
+            _dbg_flush("wgrad", (K_, C_, RS_))
             self.flush()
         self.entries.append(WgradEntry(ws.data_ptr(), dst, stride, splits, K_, C_, Cp, RS_, transpose_kc, acc, 0))
         self.keep.append(ws)
@@ -1461,6 +1471,9 @@ class BStatStruct(ctypes.Structure):
                 ("y_cstride", ctypes.c_int), ("act", ctypes.c_int)]
 
 
+_DEBUG_BNSTAT = bool(int(__import__("os").environ.get("ADR_DEBUG_BNSTAT", "0")))
+
+
 class BnStat:
     """A training BN-act's backward statistics, taken from its only reader's data gradient: (y, scale, shift, act)
     from the forward; after that dgrad, the partials and the identity (address, geometry, version) of the dz
@@ -1490,6 +1503,9 @@ class BnStat:
         dx = self.ref() if self.ref is not None else None
         ok = (dx is not None and self._key(dz) == self.key and
               (dz is dx or dz.untyped_storage().data_ptr() == dx.untyped_storage().data_ptr()))
+        if _DEBUG_BNSTAT and self.key is not None and not ok:
+            print(f"BnStat.take miss: key {'same' if self._key(dz) == self.key else 'differs'}, dx "
+                  f"{'dead' if dx is None else 'alive'} {tuple(dz.shape)}", flush=True)
         got = (self.part, self.P) if ok else None
         self.part = self.P = self.key = self.ref = None
         return got
@@ -2914,10 +2930,18 @@ _DCN_FAR = {}  # device -> (fp32 far-corner buffer, tile flags), grown to the la
 _DCN_FAR_RETIRED = []  # outgrown buffers: a captured graph may still address them
 
 
+# 1: a freshly zeroed far-corner pair per backward call (its memset also leaves the buffer in the Infinity Cache
+# right before the kernel's far-corner atomics); 0: one persistent pair per device (the kernels leave it zero)
+_DCN_FAR_FRESH = bool(int(__import__("os").environ.get("ADR_DCN_FAR_FRESH", "0")))
+
+
 def _dcn_far_scratch(dev, N, H, W, C):
     """Persistent zeroed scratch of adr_dcn_bwd_bf16: the fp32 far-corner buffer and the tile flags. The kernels
     leave both zero again, so ONE pair per device serves every level, shape, step and graph replay (calls are
     stream-ordered); a call uses a prefix view of it."""
+    if _DCN_FAR_FRESH:
+        return (torch.zeros(N * H * W * C, dtype=torch.float32, device=dev),
+                torch.zeros(int(lib.adr_dcn_bwd_tiles(N, H, W)), dtype=torch.int32, device=dev))
     key = str(dev)
     n, nt = N * H * W * C, int(lib.adr_dcn_bwd_tiles(N, H, W))
     cur = _DCN_FAR.get(key)
@@ -2936,14 +2960,16 @@ def _dcn_far_scratch_levels(dev, N, dims, C):
     nt = sum(int(lib.adr_dcn_bwd_tiles(N, H, W)) for H, W in dims)
     key = str(dev)
     cur = _DCN_FAR.get(key)
+    if _DCN_FAR_FRESH:
+        cur = (torch.zeros(n, dtype=torch.float32, device=dev), torch.zeros(nt, dtype=torch.int32, device=dev))
     # compare against the FULL persistent pair (not a prefix view), so it grows only when really too small
-    if cur is None or cur[0].numel() < n or cur[1].numel() < nt:
+    elif cur is None or cur[0].numel() < n or cur[1].numel() < nt:
         if cur is not None:
             _DCN_FAR_RETIRED.append(cur)
             n, nt = max(n, cur[0].numel()), max(nt, cur[1].numel())
-        _DCN_FAR[key] = (torch.zeros(n, dtype=torch.float32, device=dev),
-                         torch.zeros(nt, dtype=torch.int32, device=dev))
-    f, g = _DCN_FAR[key]
+        _DCN_FAR[key] = cur = (torch.zeros(n, dtype=torch.float32, device=dev),
+                               torch.zeros(nt, dtype=torch.int32, device=dev))
+    f, g = cur
     out, o, ot = [], 0, 0
     for H, W in dims:
         k, kt = N * H * W * C, int(lib.adr_dcn_bwd_tiles(N, H, W))
