@@ -14,7 +14,7 @@ bash scripts/pmc_bench_traffic.sh || exit 1
 cp gpurun_out/pmc_bench/pmc_traffic.json profiles/pmc_traffic.json && cp gpurun_out/pmc_bench/pmc_traffic.json $OUT/ || exit 1
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 bench.py --steps 25 --warmup 2 --no-cpu-baseline --infer-steps 0 --augment-bench 0 --lscale-steps 0 --stage-check 0 --roofline-steps 0 > $OUT/prof.log 2>&1 || { tail -20 $OUT/prof.log; exit 1; }
 TRACE=$(find $OUT/prof -name "*kernel_trace.csv" | head -1)
-python3 scripts/replay_breakdown.py $TRACE --steps 8 --top 40 > $OUT/replay.md 2>&1 || exit 1
+python3 scripts/replay_breakdown.py $TRACE --steps 8 --top 40 --pmc profiles/pmc_traffic.json > $OUT/replay.md 2>&1 || exit 1
 python3 scripts/step_traffic.py $TRACE profiles/pmc_traffic.json $OUT/step_traffic.json --bs 64 > $OUT/step_traffic.log 2>&1 || { cat $OUT/step_traffic.log; exit 1; }
 cp $OUT/step_traffic.json profiles/step_traffic.json || exit 1
 timeout -k 10 600 python3 bench.py > $OUT/bench.log 2>&1 || { tail -20 $OUT/bench.log; exit 1; }
