@@ -31,7 +31,7 @@ def main():
     for coll in (True, False):
         torch.manual_seed(0)
         m = DetectionModel(str(cfg), compute_dtype=torch.bfloat16).to(dev)
-        cuts = cuts_for_bucket(m, DDP_BUCKET_MB)
+        cuts = cuts_for_bucket(m, min(DDP_BUCKET_MB, 4.0))  # four stages: every inter-stage path exercised
         trainers.append(FusedTrainer(m, batch_size=bs, world_size=1, stages=cuts, collectives=coll))
     batches = [train_batch(bs, img, seed=s, device=dev, u8=True)[0] for s in (11, 12, 13, 14)]
     res = {"cuts": list(trainers[0].cuts), "backend": dist.get_backend(), "world_size": dist.get_world_size(),

@@ -42,11 +42,13 @@ def _worker(rank, port, out_dir, q):
         m = DetectionModel(str(CFG))
         load_recipe_into(m)
         m = m.cuda()
-        tr = FusedTrainer(m, nbs=WORLD * BS, batch_size=WORLD * BS, world_size=WORLD)
         from adrefine.engine.ddp import cuts_for_bucket
         from adrefine.engine.trainer import DDP_BUCKET_MB
+        assert FusedTrainer(m, nbs=WORLD * BS, batch_size=WORLD * BS, world_size=WORLD).cuts == \
+            cuts_for_bucket(m, DDP_BUCKET_MB)  # the default stage split (8 MB buckets: one cut)
         # ~4 MB gradient buckets: four stages, cuts inside the neck included (after L7, L10, L20)
-        assert tr.cuts == cuts_for_bucket(m, DDP_BUCKET_MB) and len(tr.cuts) >= 3 and tr.accumulate == 1
+        tr = FusedTrainer(m, nbs=WORLD * BS, batch_size=WORLD * BS, world_size=WORLD, stages=cuts_for_bucket(m, 4.0))
+        assert len(tr.cuts) >= 3 and tr.accumulate == 1
         x, lab = _shard(0, rank)
         tr.step({"img": x.cuda(), **lab})  # eager: bucket all-reduces launched between backward stages
         x, lab = _shard(1, rank)

@@ -6,8 +6,8 @@ layers' gradients overlaps the backward of the early layers. This build keeps ev
 flat fp32 arena written by the kernels themselves (no per-parameter hooks), so it gets the same overlap a
 different way:
 
-* the layer list is cut into stages (`cuts` = layer indices after which a stage ends; default after L6 and L10,
-  SURVEY.md §8e) and the tensors that cross a cut are detached into fresh leaves during the forward
+* the layer list is cut into stages (`cuts` = layer indices after which a stage ends; by default where the
+  gradient filled from the last layer reaches ~8 MB: after L10, two stages — trainer.DDP_BUCKET_MB) and the tensors that cross a cut are detached into fresh leaves during the forward
   (`cut_live`), so the backward runs stage by stage, last stage first (`staged_backward`);
 * the arena is laid out stage-major, last stage first (`stage_of`, FusedTrainer), so when a stage's backward
   (and its batched WGRAD reductions) is done, its parameters' gradients form one contiguous bucket;

@@ -51,9 +51,13 @@ _NORM_TYPES = tuple(v for k, v in nn.__dict__.items() if "Norm" in k and isinsta
 _ENTRY = np.dtype([("p", "<u8"), ("g", "<u8"), ("b", "<u8"), ("e", "<u8"), ("n", "<i8"), ("grp", "<i4"),
                    ("pad", "<i4")])
 _CHUNK = np.dtype([("e", "<i4"), ("p", "<i4"), ("s", "<i8"), ("l", "<i8")])
-# stage ends for the bucketed all-reduce: buckets of ~ADR_DDP_BUCKET_MB MB of gradients, filled
-# from the last layer down (ddp.cuts_for_bucket); DDP_CUTS overrides with fixed layer cuts (e.g. "6,10")
-DDP_BUCKET_MB = float(os.environ.get("ADR_DDP_BUCKET_MB", "4"))
+# stage ends for the bucketed all-reduce: buckets of ~ADR_DDP_BUCKET_MB MB of gradients, filled from the last layer
+# down (ddp.cuts_for_bucket); DDP_CUTS overrides with fixed layer cuts (e.g. "6,10"). 8 MB: one cut after L10, two
+# stages — the first bucket (L11-L33, 8.5 MiB of 15.6) all-reduces under the backbone's backward. Measured on one GPU with
+# the one-rank RCCL group (scripts/_r06l.sh, same box): 4 MB buckets (cuts 7, 10, 20) cost 2.0 % over the unstaged
+# step, 8 MB 0.9 %, 16 MB (no cut, no overlap) 0.3 %; SURVEY §8e puts the 16.4 MB all-reduce at 30-60 us over xGMI,
+# so the exposed second bucket costs about what the extra cuts would
+DDP_BUCKET_MB = float(os.environ.get("ADR_DDP_BUCKET_MB", "8"))
 DDP_CUTS = tuple(int(v) for v in os.environ["ADR_DDP_CUTS"].split(",")) if os.environ.get("ADR_DDP_CUTS") else None
 
 

@@ -1341,6 +1341,9 @@ class BNActFn(torch.autograd.Function):
             part, P = got
         else:
             P = N * chunks
+            if _DEBUG_BNSTAT:
+                print(f"BN bwd stats pass: dz from {getattr(dz, '_adr_src', '?')} {tuple(dz.shape)} act {act} "
+                      f"xfuse {ctx.xfuse} sres {ctx.sres is not None}", flush=True)
             lib.adr_nc_reduce(dt, 1, ctypes.c_void_p(yp), ycs, 0, ctypes.c_void_p(dzp), dzcs, 0, fptr(scale),
                               fptr(shift), 0, ACT[act], N, HW, C, _stats_rows(N, HW), fptr(part), stream())
         lib.adr_bn_bwd_finalize(fptr(part), P, C, float(N * HW), fptr(mean), fptr(rstd),
@@ -2183,6 +2186,8 @@ class FanOutFn(torch.autograd.Function):
         if not gs:
             return None, None, None
         if len(gs) == 1:
+            if _DEBUG_BNSTAT:
+                gs[0]._adr_src = "fanout(1)"
             return gs[0], None, None
         dt = gs[0].dtype
         gs = [g if g.dtype == dt else g.to(dt) for g in gs]
@@ -2199,6 +2204,8 @@ class FanOutFn(torch.autograd.Function):
                 else:
                     _ew(EW_COPY, va, _v(rest[0]), accumulate=1)
                     rest = rest[1:]
+            if _DEBUG_BNSTAT:
+                acc._adr_src = f"fanout-excl({len(gs)})"
             return acc, None, None
         out = _new_like(_v(gs[0])[0])
         vo = (out, out.data_ptr(), out.shape[1])
@@ -2215,6 +2222,8 @@ class FanOutFn(torch.autograd.Function):
             else:
                 _ew(EW_COPY, vo, _v(rest[0]), accumulate=1)
                 rest = rest[1:]
+        if _DEBUG_BNSTAT:
+            out._adr_src = f"fanout({len(gs)})"
         return out, None, None
 
 
