@@ -468,6 +468,9 @@ int adr_upsample_nearest_bwd(int dtype, const void* dy, int dcs, int N, int H, i
 int adr_mlca_fwd(int dtype, const void* y, int ycs, const void* res, int rcs, void* out, int ocs, int N, int H, int W,
                  int C, const float* wl, const float* wg, int k, float local_weight, float* local, float* att,
                  float* sig_l, float* sig_g, void* stream);
+/* adr_mlca_bwd: dwl / dwg (k floats each) receive the two Conv1d weight gradients; with both NULL they are left as
+ * per-image rows [N][2][k] (local conv in half 0, global in half 1) at float offset 2 * N * 25 * C of ws, for the
+ * caller to reduce (adr_partial_sum(_batched) with P = N, C = k, which = 0 / 1: the trainer's deferred flush). */
 size_t adr_mlca_bwd_workspace(int N, int C, int k);
 int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout, int dcs, void* dy, int ocs, int N, int H, int W,
                  int C, const float* wl, const float* wg, int k, float local_weight, const float* local,

@@ -922,6 +922,8 @@ def _defer_dot(param, x, dy):
 _DEFER_DOT = bool(int(__import__("os").environ.get("ADR_DEFER_DOT", "1")))  # scalar dot gradients at the flush
 _DEFER_COLSUM = bool(int(__import__("os").environ.get("ADR_DEFER_COLSUM", "1")))
 _DEFER = None  # the active WgradDeferral (set by the trainer around its backward pass)
+# MLCA's two Conv1d weight gradients as partial sums at the flush (ADR_DEFER_MLCA=0: summed at the MLCA backward)
+_DEFER_MLCA = bool(int(__import__("os").environ.get("ADR_DEFER_MLCA", "1")))
 # Partial sets above this size are reduced right away (while still in L2) instead of deferred. Measured
 # (scripts/ab_env.sh): deferring all of them is fastest — 32.39 ms vs 32.49 / 32.64 / 32.70 ms for 16 / 4 / 1 MB.
 DEFER_MAX_BYTES = int(__import__("os").environ.get("ADR_DEFER_MAX_BYTES", 1 << 62))
@@ -2633,16 +2635,29 @@ class MLCAFn(torch.autograd.Function):
         vd, vy = _v(dout), _v(y)
         dy = _new_like(y)
         k = wlf.numel()
-        dwl = torch.empty(k, dtype=torch.float32, device=y.device)
-        dwg = torch.empty(k, dtype=torch.float32, device=y.device)
         wsb = lib.adr_mlca_bwd_workspace(N, C, k)
         ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=y.device)
+        tl, tg = _target(ctx.pwl), _target(ctx.pwg)
+        # both Conv1d weight gradients land in the arena: leave the per-image rows and reduce them at the deferred
+        # flush with the other partial sums (no sum launch, no temporaries, no axpy entries)
+        defer = (_DEFER_MLCA and _dfr() is not None and _TIMING is None and tl is not None and tg is not None
+                 and tl is not tg)
+        dwl = dwg = None
+        if not defer:
+            dwl = torch.empty(k, dtype=torch.float32, device=y.device)
+            dwg = torch.empty(k, dtype=torch.float32, device=y.device)
         lib.adr_mlca_bwd(dcode(y.dtype), ctypes.c_void_p(vy[1]), vy[2], ctypes.c_void_p(vd[1]), vd[2],
                          ctypes.c_void_p(dy.data_ptr()), C, N, H, W, C, fptr(wlf), fptr(wgf), k, float(lw),
                          fptr(local), fptr(att), fptr(sig_l), fptr(sig_g), fptr(dwl), fptr(dwg), fptr(ws), wsb,
                          stream())
-        return dy, (_defer_pass(ctx.sres, dout) if has_res else None), sink(ctx.pwl, dwl.view(wls)), \
-            sink(ctx.pwg, dwg.view(wgs)), None, None
+        dres = _defer_pass(ctx.sres, dout) if has_res else None
+        if defer:
+            rows = ws[2 * N * 25 * C:2 * N * 25 * C + 2 * N * k]
+            for which, t in ((0, tl), (1, tg)):
+                _dfr().add_psum(rows, N, k, which, fptr(_grad_buf(t)), 1)
+                t._adr_used = True
+            return dy, dres, None, None, None, None
+        return dy, dres, sink(ctx.pwl, dwl.view(wls)), sink(ctx.pwg, dwg.view(wgs)), None, None
 
 
 def mlca(y, res, wl, wg, local_weight=0.5, out=None):

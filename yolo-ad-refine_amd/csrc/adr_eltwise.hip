@@ -149,6 +149,20 @@ __device__ __forceinline__ void nc_collapse_body(const float* partial, int N, in
   if (threadIdx.x == 0) out[idx] = accumulate ? out[idx] + (float)sh[0] : (float)sh[0];
 }
 
+// no collapse (per (n, c) outputs, e.g. the head's per-sub-image pooled sums): one thread per output, its chunks
+// summed in order in double — one 256-thread workgroup per output (the kernel below) spent ~27 us on the packed
+// head's 1344 x 128 outputs of one or two chunks each
+__global__ void __launch_bounds__(256) nc_sum_chunks_kernel(const float* __restrict__ partial, int N, int chunks,
+                                                            int C, int which, float* out, int accumulate) {
+  const long idx = (long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long)N * C) return;
+  const int n = (int)(idx / C), c = (int)(idx - (long)n * C);
+  const float* p = partial + ((long)n * chunks * 2 + which) * C + c;
+  double s = 0.0;
+  for (int ch = 0; ch < chunks; ++ch) s += (double)p[(long)ch * 2 * C];
+  out[idx] = accumulate ? out[idx] + (float)s : (float)s;
+}
+
 template <int NT>
 __global__ void __launch_bounds__(NT) nc_collapse_kernel(const float* partial, int N, int chunks, int C, int which,
                                                          float* out, int sum_n, int sum_c, int accumulate) {
@@ -380,7 +394,10 @@ extern "C" int adr_dotsum_batched(const adr_dotsum_entry* entries, int count, vo
 extern "C" int adr_nc_collapse(const float* partial, int N, int chunks, int C, int which, float* out, int sum_n,
                                int sum_c, int accumulate, void* stream) {
   int outn = (sum_n ? 1 : N) * (sum_c ? 1 : C);
-  if (outn == 1)
+  if (!sum_n && !sum_c && outn > 1)
+    hipLaunchKernelGGL(nc_sum_chunks_kernel, dim3(cdiv((long)outn, 256)), dim3(256), 0, (hipStream_t)stream, partial,
+                       N, chunks, C, which, out, accumulate);
+  else if (outn == 1)
     hipLaunchKernelGGL(nc_collapse_kernel<1024>, dim3(1), dim3(1024), 0, (hipStream_t)stream, partial, N, chunks, C,
                        which, out, sum_n, sum_c, accumulate);
   else

@@ -282,9 +282,9 @@ __global__ void __launch_bounds__(256) mlca_att_bwd_kernel(const float* local, c
       }
       __syncthreads();
     }
-    if (threadIdx.x == 0) {
-      dwl_part[(long)n * k + t] = red[0];
-      dwg_part[(long)n * k + t] = red[256];
+    if (threadIdx.x == 0) {  // rows [n][2][k]: the local conv's in half 0, the global conv's in half 1
+      dwl_part[((long)n * 2 + 0) * k + t] = red[0];
+      dwl_part[((long)n * 2 + 1) * k + t] = red[256];
     }
     __syncthreads();
   }
@@ -344,14 +344,14 @@ __global__ void __launch_bounds__(256) mlca_bwd_y_kernel(const T* dout, int dcs,
   }
 }
 
-// the local and global 1-D conv weight gradients: block 0 sums part[0..rows) into out0, block 1 the next rows
-// (part + rows * cols) into out1 — one launch for both (cols <= blockDim)
+// the local and global 1-D conv weight gradients from the per-image rows [rows][2][cols]: block 0 sums half 0 into
+// out0, block 1 half 1 into out1 — one launch for both (cols <= blockDim)
 __global__ void sum_rows_kernel(const float* part, int rows, int cols, float* out0, float* out1) {
   const int c = threadIdx.x;
   if (c >= cols) return;
-  const float* p = part + (long)blockIdx.x * rows * cols;
+  const float* p = part + (long)blockIdx.x * cols;
   float s = 0.f;
-  for (int r = 0; r < rows; ++r) s += p[(long)r * cols + c];
+  for (int r = 0; r < rows; ++r) s += p[(long)r * 2 * cols + c];
   (blockIdx.x ? out1 : out0)[c] = s;
 }
 
@@ -405,6 +405,7 @@ extern "C" int adr_mlca_fwd(int dtype, const void* y, int ycs, const void* res, 
   return check_launch("adr_mlca_fwd");
 }
 
+// ws layout: datt [N][25][C] | dlocal [N][25][C] | weight-gradient rows [N][2][k] | S [5][C] (floats)
 extern "C" size_t adr_mlca_bwd_workspace(int N, int C, int k) {
   return ((size_t)N * LS * LS * C * 2 + (size_t)N * k * 2 + (size_t)LS * C) * sizeof(float);
 }
@@ -417,8 +418,8 @@ extern "C" int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout,
   hipStream_t st = (hipStream_t)stream;
   float* datt = ws;
   float* dlocal = ws + (size_t)N * LS * LS * C;
-  float* dwl_part = dlocal + (size_t)N * LS * LS * C;
-  float* dwg_part = dwl_part + (size_t)N * k;
+  float* dwl_part = dlocal + (size_t)N * LS * LS * C;  // [N][2][k] per-image weight-gradient rows
+  float* dwg_part = dwl_part + (size_t)N * k;           // (unused by the kernels: both halves live in dwl_part)
   float* S = dwg_part + (size_t)N * k;
   const bool v = mlca_vec(dtype, C, {ycs, dcs, ocs}, {y, dout, dy});
   MLCA_DISPATCH(dtype, v, mlca_bwd_bins_kernel, dim3(LS * LS, N), (const TT*)y, ycs, (const TT*)dout, dcs, H, W, C,
@@ -431,6 +432,7 @@ extern "C" int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout,
   MLCA_DISPATCH(dtype, v, mlca_bwd_y_kernel, mlca_grid((long)N * H * W, dtype, v, C), (const TT*)dout, dcs, att,
                 dlocal, (TT*)dy, ocs, N, H, W, C);
   ADR_REQUIRE(k <= 64, "mlca_bwd: kernel size %d", k);
-  hipLaunchKernelGGL(sum_rows_kernel, dim3(2), dim3(64), 0, st, dwl_part, N, k, dwl, dwg);  // dwg_part follows dwl_part
+  ADR_REQUIRE((dwl == nullptr) == (dwg == nullptr), "mlca_bwd: dwl and dwg both given or both NULL");
+  if (dwl) hipLaunchKernelGGL(sum_rows_kernel, dim3(2), dim3(64), 0, st, dwl_part, N, k, dwl, dwg);
   return check_launch("adr_mlca_bwd");
 }
