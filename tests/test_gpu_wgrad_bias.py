@@ -78,3 +78,40 @@ def test_wgrad_bias_train_step_matches_unfused(monkeypatch):
         else:
             assert torch.equal(a, b), k
     assert nb > 0
+
+
+@pytest.mark.parametrize("N,H,W,C,K,R,S", [(2, 80, 80, 128, 128, 1, 1), (4, 40, 40, 256, 136, 3, 2),
+                                           (3, 17, 13, 192, 160, 1, 1), (2, 9, 7, 136, 200, 3, 2)])
+def test_wgrad_double_buffered_tile_bitwise(monkeypatch, N, H, W, C, K, R, S):
+    """The 128 x 128 WGRAD tile runs double-buffered (two LDS stages, loads two k-steps ahead, adr_wgrad.hip
+    wgrad_bf16_body<.., DB>): same k-steps, same order, so its weight partials and fused bias rows must be bitwise
+    the single-stage kernel's (ADR_WG_DB=0) — including ragged k-steps (split ends inside a step), channel tails and
+    the 3x3 stride-2 gathers."""
+    from adrefine import kernels as Kn
+    from adrefine.native import lib
+    torch.manual_seed(1)
+    pad = R // 2
+    x = _nhwc(torch.randn(N, C, H, W, device="cuda").to(torch.bfloat16))
+    d, Ho, Wo = Kn.conv_desc(N, H, W, C, C, K, R, R, S, S, pad, pad, K, torch.bfloat16)
+    dy = _nhwc(torch.randn(N, K, Ho, Wo, device="cuda").to(torch.bfloat16))
+    assert lib.adr_conv2d_wgrad_batched_tile(ctypes.byref(d)) == 128 * 256 + 128
+    splits = lib.adr_conv2d_wgrad_splits(ctypes.byref(d))
+    n = splits * K * R * R * C
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("ADR_WG_DB", mode)
+        w = torch.full((n,), float("nan"), device="cuda")
+        bp = torch.full((splits * 2 * K,), float("nan"), device="cuda")
+        assert lib.adr_conv2d_wgrad_partials_bias(ctypes.byref(d), ctypes.c_void_p(x.data_ptr()),
+                                                  ctypes.c_void_p(dy.data_ptr()), ctypes.c_void_p(w.data_ptr()),
+                                                  ctypes.c_void_p(bp.data_ptr()), st) == 0
+        torch.cuda.synchronize()
+        out[mode] = (w, bp.view(splits, 2, K)[:, 0].clone())
+    assert torch.isfinite(out["1"][0]).all()
+    assert torch.equal(out["0"][0], out["1"][0])
+    assert torch.equal(out["0"][1], out["1"][1])
+    ref = torch.einsum("nkhw,nchw->kc", dy.float(), x.float()) if R == 1 else None
+    if ref is not None:
+        got = out["1"][0].view(splits, K, C).sum(0)
+        assert float((got - ref).abs().max()) <= 1e-4 * float(ref.abs().max())

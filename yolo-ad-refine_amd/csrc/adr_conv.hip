@@ -463,7 +463,7 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int q = tid + 256 * i;
-      if (q < B_TOT) st16(&Bs[(q >> 3) * CLD + (q & 7) * 8], rb[i]);
+      if (B_TOT % 256 == 0 || q < B_TOT) st16(&Bs[(q >> 3) * CLD + (q & 7) * 8], rb[i]);
     }
   };
 
@@ -493,23 +493,23 @@ __device__ __forceinline__ void conv_bf16_body(const ConvArgs& a) {
     }
   };
   if constexpr (DB) {
-    // stage s (LDS) and register set s alternate; step t computes stage t&1 while set t&1 receives step t+2
-    if (ksteps > 0) {
-      load(S0{});
-      store(S0{});
-      if (ksteps > 1) load(S1{});
-      __syncthreads();
-    }
+    // stage s (LDS) and register set s alternate; step t computes stage t&1 while set t&1 receives step t+2.
+    // Loads and stores are unconditional: past the last step the decoder's tap is >= ntaps, every chunk reads
+    // out of range (zeros, no memory access) and the stores land in a stage nobody reads again — straight-line
+    // VMEM lets the compiler count the older set's loads (vmcnt(N) > 0) instead of draining the just-issued
+    // prefetch with vmcnt(0) at the store
+    load(S0{});
+    store(S0{});
+    load(S1{});
+    __syncthreads();
     auto step = [&](int t, auto S) {
       constexpr int cur = decltype(S)::value;
       using SO = std::integral_constant<int, 1 - cur>;
       set_stage(cur);
-      if (t + 2 < ksteps) load(S);  // set cur was stored into its stage one step ago
+      load(S);  // set cur was stored into its stage one step ago
       compute();
-      if (t + 1 < ksteps) {
-        set_stage(1 - cur);
-        store(SO{});  // step t+1 (loaded two steps ago) into the other stage, last read in step t-1
-      }
+      set_stage(1 - cur);
+      store(SO{});  // step t+1 (loaded two steps ago) into the other stage, last read in step t-1
       __syncthreads();
     };
     for (int t = 0; t < ksteps; t += 2) {

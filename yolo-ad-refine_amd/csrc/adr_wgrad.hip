@@ -53,7 +53,10 @@ __device__ __forceinline__ void wg_xcd_block(int& bx, int& by) {
   bx = b - by * gx;
 }
 
-template <int BM, int BN, int KU>  // KU: 32*WK-row sub-steps per k-step; (bid, split): tile and split of the block
+// KU: 32*WK-row sub-steps per k-step; (bid, split): tile and split of the block. DB: two LDS stages and two register
+// sets — the loads of step t+2 are issued while step t computes (two steps of MFMA work to land behind instead of one)
+// and one barrier per step; the k-steps, their order and every sum are those of the single-stage loop (bitwise equal)
+template <int BM, int BN, int KU, bool DB = false>
 __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int split) {
   constexpr int WM = BM / 16 < 2 ? BM / 16 : 2;
   constexpr int WN = BN / 16 < 2 ? BN / 16 : 2;
@@ -67,8 +70,9 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
   constexpr int A_CHT = R * BM / 8, B_CHT = R * BN / 8;  // 16-byte chunks per k-step
   constexpr int A_CH = (A_CHT + 255) / 256, B_CH = (B_CHT + 255) / 256;
 
-  __shared__ __attribute__((aligned(16))) __bf16 As[R * PA];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[R * PB];
+  constexpr int NS = DB ? 2 : 1;  // LDS stages = register sets
+  __shared__ __attribute__((aligned(16))) __bf16 As[NS * R * PA];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[NS * R * PB];
   __shared__ float red[WK > 1 ? (WK - 1) * BM * BN : 1];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -85,7 +89,7 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
   const long pend = min(a.red_total, pbeg + a.red_per_split);
   const int hw = a.ho * a.wo;
 
-  u32x4 ra[A_CH], rb[B_CH];
+  u32x4 ra_s[NS][A_CH], rb_s[NS][B_CH];
   constexpr unsigned OOR = 0x7FFFFFF0u;
   const __amdgpu_buffer_rsrc_t x_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t dy_rs = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
@@ -103,7 +107,9 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
     b_ox[i] = rem - b_oy[i] * a.wo;
   }
 
-  auto load = [&](int t) {
+  auto load = [&](int t, auto S) {
+    u32x4(&ra)[A_CH] = ra_s[decltype(S)::value];
+    u32x4(&rb)[B_CH] = rb_s[decltype(S)::value];
     const long p0 = pbeg + (long)t * R;
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
@@ -135,16 +141,18 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
       }
     }
   };
-  auto store = [&]() {
+  auto store = [&](auto S, int stage) {
+    const u32x4(&ra)[A_CH] = ra_s[decltype(S)::value];
+    const u32x4(&rb)[B_CH] = rb_s[decltype(S)::value];
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int q = tid + 256 * i;
-      if (q < A_CHT) st16(&As[(q / (BM / 8)) * PA + (q % (BM / 8)) * 8], ra[i]);
+      if (A_CHT % 256 == 0 || q < A_CHT) st16(&As[stage * R * PA + (q / (BM / 8)) * PA + (q % (BM / 8)) * 8], ra[i]);
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int q = tid + 256 * i;
-      if (q < B_CHT) st16(&Bs[(q / (BN / 8)) * PB + (q % (BN / 8)) * 8], rb[i]);
+      if (B_CHT % 256 == 0 || q < B_CHT) st16(&Bs[stage * R * PB + (q / (BN / 8)) * PB + (q % (BN / 8)) * 8], rb[i]);
     }
   };
 
@@ -170,17 +178,13 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
   const __bf16* b_base = Bs + row0 * PB + wn * WCOLS + 4 * p4;
 
   const int ksteps = a.ksteps;
-  if (ksteps > 0) {
-    load(0);
-    store();
-    __syncthreads();
-  }
-  for (int t = 0; t < ksteps; ++t) {
-    if (t + 1 < ksteps) load(t + 1);
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, NS - 1>;
+  auto compute = [&](int stage) {
 #pragma unroll
     for (int u = 0; u < KU; ++u) {
-      const __bf16* ab = a_base + u * 32 * WK * PA;
-      const __bf16* bb = b_base + u * 32 * WK * PB;
+      const __bf16* ab = a_base + stage * R * PA + u * 32 * WK * PA;
+      const __bf16* bb = b_base + stage * R * PB + u * 32 * WK * PB;
       bf16x8 fa[TM], fb[TN];
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
@@ -211,10 +215,43 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
         }
       }
     }
+  };
+  if constexpr (DB) {
+    // step t computes stage t&1 while register set t&1 receives step t+2; step t+1 (set 1-(t&1), loaded one step
+    // ago) goes into the other stage, last read in step t-1 (before the previous barrier)
+    load(0, S0{});
+    store(S0{}, 0);
+    load(1, S1{});
     __syncthreads();
-    if (t + 1 < ksteps) {
-      store();
+    // the loads and stores are unconditional: past the last step every chunk is out of range (p >= pend: the
+    // descriptor returns zeros, no memory access), and straight-line VMEM lets the compiler count the older set's
+    // loads with vmcnt(4) instead of draining the just-issued prefetch with vmcnt(0) at the store
+    auto step = [&](int t, auto S) {
+      constexpr int cur = decltype(S)::value;
+      using SO = std::integral_constant<int, 1 - cur>;
+      load(t + 2, S);
+      compute(cur);
+      store(SO{}, 1 - cur);
       __syncthreads();
+    };
+    for (int t = 0; t < ksteps; t += 2) {
+      step(t, S0{});
+      if (t + 1 < ksteps) step(t + 1, S1{});
+    }
+  } else {
+    if (ksteps > 0) {
+      load(0, S0{});
+      store(S0{}, 0);
+      __syncthreads();
+    }
+    for (int t = 0; t < ksteps; ++t) {
+      if (t + 1 < ksteps) load(t + 1, S0{});
+      compute(0);
+      __syncthreads();
+      if (t + 1 < ksteps) {
+        store(S0{}, 0);
+        __syncthreads();
+      }
     }
   }
 
@@ -270,11 +307,11 @@ __device__ __forceinline__ void wgrad_bf16_body(const WgArgs& a, int bid, int sp
     }
 }
 
-template <int BM, int BN>
-__global__ void __launch_bounds__(256) wgrad_bf16_kernel(WgArgs a) {
+template <int BM, int BN, bool DB = false>
+__global__ void __launch_bounds__(256, DB ? 3 : 1) wgrad_bf16_kernel(WgArgs a) {
   int bid, split;  // block x -> tile, block y = split (XCD-aware order)
   wg_xcd_block(bid, split);
-  wgrad_bf16_body<BM, BN, wg_ku(BM, BN)>(a, bid, split);
+  wgrad_bf16_body<BM, BN, wg_ku(BM, BN), DB>(a, bid, split);
 }
 
 // Grouped WGRAD: the weight gradients of many convs (the deferred ones of a backward stage, one BM x BN tile shape)
@@ -290,13 +327,13 @@ struct WgBatch {
   int tiles[WGB_MAX];
   int count;
 };
-template <int BM, int BN>
-__global__ void __launch_bounds__(256) wgrad_bf16_batched_kernel(WgBatch b) {
+template <int BM, int BN, bool DB = false>
+__global__ void __launch_bounds__(256, DB ? 3 : 1) wgrad_bf16_batched_kernel(WgBatch b) {
   int j = 0;
   while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
   const int local = (int)blockIdx.x - b.start[j];
   const int split = local / b.tiles[j];
-  wgrad_bf16_body<BM, BN, wg_ku(BM, BN)>(b.e[j], local - split * b.tiles[j], split);
+  wgrad_bf16_body<BM, BN, wg_ku(BM, BN), DB>(b.e[j], local - split * b.tiles[j], split);
 }
 
 
@@ -604,6 +641,13 @@ static bool thin_enabled() {
   return v != 0;
 }
 
+// the 128 x 128 tile runs double-buffered (wgrad_bf16_body<.., DB = true>, bitwise the single-stage loop);
+// ADR_WG_DB=0 selects the single-stage kernel (A/B; read per launch, so a test can switch it in-process)
+static bool wg_db() {
+  const char* e = getenv("ADR_WG_DB");
+  return e ? atoi(e) != 0 : true;
+}
+
 static int wg_pick16(int n) { return n <= 16 ? 16 : n <= 32 ? 32 : n <= 64 ? 64 : 128; }
 
 template <int BM>
@@ -613,7 +657,10 @@ static void launch_bm(int bn, dim3 grid, const WgArgs& g, hipStream_t st) {
     case 32: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 32>), grid, dim3(256), 0, st, g); break;
     case 64: hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 64>), grid, dim3(256), 0, st, g); break;
     default:
-      hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 128>), grid, dim3(256), 0, st, g);
+      if (BM == 128 && wg_db())
+        hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 128, true>), grid, dim3(256), 0, st, g);
+      else
+        hipLaunchKernelGGL((wgrad_bf16_kernel<BM, 128>), grid, dim3(256), 0, st, g);
       break;
   }
 }
@@ -757,7 +804,12 @@ static void launch_batch_bm(int bn, int blocks, const WgBatch& b, hipStream_t st
     case 16: hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 16>), dim3(blocks), dim3(256), 0, st, b); break;
     case 32: hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 32>), dim3(blocks), dim3(256), 0, st, b); break;
     case 64: hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 64>), dim3(blocks), dim3(256), 0, st, b); break;
-    default: hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 128>), dim3(blocks), dim3(256), 0, st, b); break;
+    default:
+      if (BM == 128 && wg_db())
+        hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 128, true>), dim3(blocks), dim3(256), 0, st, b);
+      else
+        hipLaunchKernelGGL((wgrad_bf16_batched_kernel<BM, 128>), dim3(blocks), dim3(256), 0, st, b);
+      break;
   }
 }
 
