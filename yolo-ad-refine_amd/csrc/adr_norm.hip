@@ -173,13 +173,18 @@ __device__ __forceinline__ void col_sums2(const float* __restrict__ partial, int
   b = (b + b1) + (b2 + b3);
 }
 
+// pre-summed partial rows of a long finalize (fin_presum_kernel, below)
+constexpr int FIN_PMAX = 2048, FIN_S = 256, FIN_SCRATCH = 1 << 20;  // floats
+__device__ float g_fin_scratch[FIN_SCRATCH];
+
 __global__ void __launch_bounds__(256) bn_finalize_kernel(const float* __restrict__ partial, int P, int C, double count,
                                                           const float* __restrict__ gamma,
                                                           const float* __restrict__ beta, float* running_mean,
                                                           float* running_var, float momentum, float eps,
                                                           int training, float* scale, float* shift, float* mean_out,
-                                                          float* rstd_out) {
+                                                          float* rstd_out, int presummed) {
   int c = blockIdx.x;
+  if (presummed) partial = g_fin_scratch;
   double mean, var;
   if (training) {
     double a = 0.0, b = 0.0;
@@ -213,8 +218,9 @@ __global__ void __launch_bounds__(256) bn_bwd_finalize_kernel(const float* __res
                                                               const float* __restrict__ rstd,
                                                               const float* __restrict__ gamma, float* dgamma,
                                                               float* dbeta, float* A, float* B, float* Cc,
-                                                              int training, int accumulate) {
+                                                              int training, int accumulate, int presummed) {
   int c = blockIdx.x;
+  if (presummed) partial = g_fin_scratch;
   double a = 0.0, b = 0.0;
   col_sums2(partial, P, C, c, a, b);
   block_sum2(a, b);
@@ -1030,20 +1036,71 @@ extern "C" int adr_nc_reduce(int dtype, int mode, const void* x, int xcs, int xc
   return check_launch("adr_nc_reduce");
 }
 
+// ADR_FIN_PRESUM=0: the single-launch finalize at every P (A/B; read per call, so a test can switch it in-process)
+static bool fin_presum_off() {
+  const char* e = getenv("ADR_FIN_PRESUM");
+  return e && atoi(e) == 0;
+}
+
+// Long finalizes (P > 4096 partial rows, > 2048 at C >= 256: the 160^2 / 320^2 layers, P = 6 400 - 25 600 at bs 64) are two
+// launches: the per-channel kernels above read one 4-byte column per block, so a block's P row reads are P separate
+// cache lines and every channel block walks the same lines (14 us at P = 12 800, C = 32; 45 us at C = 256, against
+// 3 us for P = 50). fin_presum_kernel first sums blocks of `rb` consecutive rows of all 2C columns with coalesced
+// reads over the whole chip (double accumulation, fixed order) into the device-global scratch, and the finalize
+// reduces those <= FIN_S rows. Deterministic (the split depends on P only); the finalizes of a process are issued
+// on one stream (the scratch is not per-stream).
+
+__global__ void __launch_bounds__(256) fin_presum_kernel(const float* __restrict__ partial, int P, int C2, int rb) {
+  float* out = g_fin_scratch;
+  __shared__ double red[256];
+  const int p0 = blockIdx.x * rb, p1 = min(P, p0 + rb);
+  for (int c0 = 0; c0 < C2; c0 += 256) {
+    const int cw = min(256, C2 - c0), parts = 256 / cw;  // threads = (column, row part)
+    const int c = c0 + (int)threadIdx.x % cw, part = (int)threadIdx.x / cw;
+    double a = 0.0;
+    if (part < parts)
+      for (int p = p0 + part; p < p1; p += parts) a += partial[(long)p * C2 + c];
+    red[threadIdx.x] = a;
+    __syncthreads();
+    if ((int)threadIdx.x < cw) {
+      double t = 0.0;
+      for (int q = 0; q < parts; ++q) t += red[q * cw + threadIdx.x];
+      out[(long)blockIdx.x * C2 + c] = (float)t;
+    }
+    __syncthreads();
+  }
+}
+
+// long finalize: pre-sum the caller's [P][2][C] rows into the scratch (returns 1, P becomes the scratch rows)
+static int fin_rows(const float* partial, int& P, int C, hipStream_t st) {
+  // measured (scripts/finalize_micro.py): the extra launch pays from P = 6 400 at every C and from P = 3 200 at C >= 256
+  if (!partial || P <= FIN_PMAX || (P <= 2 * FIN_PMAX && C < 256) || (long)FIN_S * 2 * C > FIN_SCRATCH ||
+      fin_presum_off())
+    return 0;
+  const int rb = (P + FIN_S - 1) / FIN_S, S = (P + rb - 1) / rb;
+  hipLaunchKernelGGL(fin_presum_kernel, dim3(S), dim3(256), 0, st, partial, P, 2 * C, rb);
+  P = S;
+  return 1;
+}
+
 extern "C" int adr_bn_finalize(const float* partial, int P, int C, double count, const float* gamma, const float* beta,
                                float* running_mean, float* running_var, float momentum, float eps, int training,
                                float* scale, float* shift, float* mean, float* rstd, void* stream) {
   ADR_REQUIRE(C > 0, "bn_finalize: C");
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, P, C, count, gamma, beta,
-                     running_mean, running_var, momentum, eps, training, scale, shift, mean, rstd);
+  hipStream_t st = (hipStream_t)stream;
+  const int pre = training ? fin_rows(partial, P, C, st) : 0;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count, gamma, beta,
+                     running_mean, running_var, momentum, eps, training, scale, shift, mean, rstd, pre);
   return check_launch("adr_bn_finalize");
 }
 
 extern "C" int adr_bn_bwd_finalize(const float* partial, int P, int C, double count, const float* mean,
                                    const float* rstd, const float* gamma, float* dgamma, float* dbeta, float* A,
                                    float* B, float* Cc, int training, int accumulate, void* stream) {
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, (hipStream_t)stream, partial, P, C, count, mean,
-                     rstd, gamma, dgamma, dbeta, A, B, Cc, training, accumulate);
+  hipStream_t st = (hipStream_t)stream;
+  const int pre = fin_rows(partial, P, C, st);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(C), dim3(256), 0, st, partial, P, C, count, mean,
+                     rstd, gamma, dgamma, dbeta, A, B, Cc, training, accumulate, pre);
   return check_launch("adr_bn_bwd_finalize");
 }
 
