@@ -205,6 +205,15 @@ def _call_site():
     return f"{owner}.{f.f_code.co_name}:{f.f_lineno}" if owner else f"{f.f_code.co_name}:{f.f_lineno}"
 
 
+# algorithmic flops of the generic entry points that run matrix work (the rest are byte-bound: 0)
+# flash attention: forward S = Q K^T and O = P V; backward the standard five products (S recomputed, dV = P^T dO,
+# dP = dO V^T, dQ = dS K, dK = dS^T Q) — 2 B h L^2 per unit of width (q/k width dqk, v width dv)
+_ALG_FLOPS = {
+    "adr_attn_fwd": lambda a: 2.0 * a[11] * a[13] * a[12] ** 2 * (a[14] + a[15]),
+    "adr_attn_bwd": lambda a: 2.0 * a[21] * a[23] * a[22] ** 2 * (3 * a[24] + 2 * a[25]),
+}
+
+
 def _hook_call(name, fn, args):
     """Generic timing of one libadr call (outside annotated regions; host-side queries are not timed)."""
     if _TIMING is None or _ANNOT[0] > 0 or name.endswith(_UNTIMED):
@@ -222,6 +231,7 @@ def _hook_call(name, fn, args):
             nbytes = int(_BATCHED_BYTES[name](args))
         else:
             nbytes = _generic_bytes(name, args)
+        flops = int(_ALG_FLOPS[name](args)) if name in _ALG_FLOPS else 0
         shape = _call_site() if name in _SITE_LABELS else ""
         if name == "adr_ew":
             shape = f"op{args[1]}{'+acc' if args[15] else ''} {args[11]}px x{args[12]}ch @{shape}"
@@ -233,7 +243,7 @@ def _hook_call(name, fn, args):
             if rc != 0:
                 break
         e1.record()
-        _TIMING.append((label, nbytes, 0, e0, e1, shape, rep))
+        _TIMING.append((label, nbytes, flops, e0, e1, shape, rep))
     if rc != 0:
         raise RuntimeError(f"{name}: {lib.lib.adr_last_error().decode()}")
     return rc

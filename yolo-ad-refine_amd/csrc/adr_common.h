@@ -34,6 +34,16 @@ template <> __device__ __forceinline__ __bf16 from_f<__bf16>(float v) { return (
 // 16-byte vector of T (8 bf16 or 4 f32)
 template <typename T> struct Vec16 { static constexpr int N = 16 / sizeof(T); };
 
+// XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin over the 8 XCDs (id % 8), each
+// with its own L2. Logical id = rank of the block among its XCD's blocks, offset by the blocks of the XCDs before it,
+// so consecutive logical ids (blocks reading the same rows) share one L2. Bijective for every nb: the XCDs below
+// r = nb % 8 get one block more (a grid that is not a multiple of 8 used to keep the identity order, which spread
+// e.g. the nine tap blocks of one DCN weight-gradient split over eight L2s). The results never depend on the order.
+__device__ __forceinline__ int xcd_remap(int b, int nb) {
+  const int q = nb >> 3, r = nb & 7, x = b & 7;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
 __device__ __forceinline__ u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
 __device__ __forceinline__ void st16(void* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
 // VEC consecutive fp32 coefficients (16-byte aligned: VEC-multiple channel offsets into torch allocations)

@@ -160,10 +160,8 @@ __device__ __forceinline__ float epi_act(int act, float v) {
 // XCD-aware block order: the dispatcher deals consecutive workgroup ids round-robin over the 8 XCDs (each with
 // its own L2), so the column tiles of one row tile — which read the same A rows — would land on different XCDs
 // and each fetch those rows from HBM. Renumbering so that consecutive logical ids share an XCD keeps them in one
-// L2 (grids that are not a multiple of 8 keep the identity order).
-__device__ __forceinline__ int xcd_block(int b, int nb) {
-  return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3);
-}
+// L2 (xcd_remap, adr_common.h: bijective for every grid size).
+__device__ __forceinline__ int xcd_block(int b, int nb) { return xcd_remap(b, nb); }
 
 // Epilogue statistics of one stored 16-byte chunk (8 columns starting at col): (sum, sum of squares) of the stored
 // values, or with BSTAT the BatchNorm-backward terms (g, g * y) of the stored dz against the BN input y at the same

@@ -45,7 +45,7 @@ struct Fp8Args {
 constexpr int F8BM = 128, F8BK = 128, F8P = 144;  // LDS row pitch in bytes
 constexpr int AMAX_BLOCKS = 256;
 
-__device__ __forceinline__ int xcd_block8(int b, int nb) { return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3); }
+__device__ __forceinline__ int xcd_block8(int b, int nb) { return xcd_remap(b, nb); }
 
 // per-block max |x| over an NHWC channel view (C channels at offset co of stride cs), 8 channels per lane
 __global__ void __launch_bounds__(256) amax_bf16_kernel(const __bf16* x, int cs, int co, long npix, int C, float* part) {

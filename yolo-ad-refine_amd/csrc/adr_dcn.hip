@@ -37,7 +37,7 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ v4s tr16(const __bf16* p) { return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)(p)); }
 
-__device__ __forceinline__ int xcd_order(int b, int nb) { return (nb & 7) ? b : (b & 7) * (nb >> 3) + (b >> 3); }
+__device__ __forceinline__ int xcd_order(int b, int nb) { return xcd_remap(b, nb); }
 
 constexpr unsigned OOR = 0x7FFFFFF0u;  // out-of-range buffer offset: the load returns zeros
 

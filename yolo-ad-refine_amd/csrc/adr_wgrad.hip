@@ -48,7 +48,7 @@ __device__ __forceinline__ v4s tr_read(const __bf16* p) {
 __device__ __forceinline__ void wg_xcd_block(int& bx, int& by) {
   const int gx = gridDim.x, nb = gx * gridDim.y;
   int b = blockIdx.x + blockIdx.y * gx;
-  if ((nb & 7) == 0) b = (b & 7) * (nb >> 3) + (b >> 3);
+  b = xcd_remap(b, nb);
   by = b / gx;
   bx = b - by * gx;
 }
@@ -331,7 +331,9 @@ template <int BM, int BN, bool DB = false>
 __global__ void __launch_bounds__(256, DB ? 3 : 1) wgrad_bf16_batched_kernel(WgBatch b) {
   int j = 0;
   while (j + 1 < b.count && (int)blockIdx.x >= b.start[j + 1]) ++j;
-  const int local = (int)blockIdx.x - b.start[j];
+  // XCD-aware order within the entry (every XCD gets an eighth of each entry, so the mix of long and short entries
+  // stays balanced; the blocks of one entry with the same id % 8 share an XCD whatever start[j] is)
+  const int local = xcd_remap((int)blockIdx.x - b.start[j], b.start[j + 1] - b.start[j]);
   const int split = local / b.tiles[j];
   wgrad_bf16_body<BM, BN, wg_ku(BM, BN), DB>(b.e[j], local - split * b.tiles[j], split);
 }
