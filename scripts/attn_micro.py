@@ -1,5 +1,6 @@
 """Time the flash attention (adr_attn_fwd / adr_attn_bwd) at the C2PTSSA MHA shape: bs 64, 2 heads of 64,
-1200 tokens (3 stacked 20x20 scales), bf16; HIP events; prints achieved TFLOP/s (4*B*H*L^2*d fwd, 2.5x bwd)."""
+1200 tokens (3 stacked 20x20 scales), bf16 (env B, H, L, D, R: l-scale 1280^2 is B 16, H 4, L 4800); HIP events; prints achieved TFLOP/s (4*B*H*L^2*d fwd, 2.5x bwd)."""
+import os
 import sys
 from pathlib import Path
 
@@ -9,7 +10,7 @@ ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT / "yolo-ad-refine_amd"))
 from adrefine import kernels as K  # noqa: E402
 
-B, H, L, D, R = 64, 2, 1200, 64, 20
+B, H, L, D, R = (int(os.environ.get(k, v)) for k, v in (("B", 64), ("H", 2), ("L", 1200), ("D", 64), ("R", 20)))
 E = H * D
 qkv = (torch.randn(B, 3 * E, L, 1, device="cuda") * 0.5).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
 qkv.requires_grad_(True)

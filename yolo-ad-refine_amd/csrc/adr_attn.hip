@@ -151,8 +151,9 @@ __global__ void __launch_bounds__(256) attn_fwd_kernel(const T* q, const T* k, c
   __shared__ __attribute__((aligned(16))) T Ks[BLK * LDT];
   __shared__ __attribute__((aligned(16))) T Vs[BLK * LDT];
   const int nqb = (L + BLK - 1) / BLK;
-  const int qb = blockIdx.x % nqb;
-  const int bh = blockIdx.x / nqb;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // the blocks of one (image, head) share an XCD's L2 (K / V)
+  const int qb = bid % nqb;
+  const int bh = bid / nqb;
   const int b = bh / heads, h = bh % heads;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const long rowb = (long)b * L;
@@ -261,8 +262,9 @@ __global__ void __launch_bounds__(256) attn_bwd_kv_kernel(const T* q, const T* k
   __shared__ __attribute__((aligned(16))) T Ds[BLK * LDT];
   __shared__ float ls[BLK], dd[BLK];
   const int nkb = (L + BLK - 1) / BLK;
-  const int kb = blockIdx.x % nkb;
-  const int bh = blockIdx.x / nkb;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // the blocks of one (image, head) share an XCD's L2 (Q / dO)
+  const int kb = bid % nkb;
+  const int bh = bid / nkb;
   const int b = bh / heads, h = bh % heads;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const long rowb = (long)b * L;
@@ -345,8 +347,9 @@ __global__ void __launch_bounds__(256) attn_bwd_q_kernel(const T* q, const T* k,
   __shared__ __attribute__((aligned(16))) T Ks[BLK * LDT];
   __shared__ __attribute__((aligned(16))) T Vs[BLK * LDT];
   const int nqb = (L + BLK - 1) / BLK;
-  const int qb = blockIdx.x % nqb;
-  const int bh = blockIdx.x / nqb;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // the blocks of one (image, head) share an XCD's L2 (K / V)
+  const int qb = bid % nqb;
+  const int bh = bid / nqb;
   const int b = bh / heads, h = bh % heads;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4, c = lane & 15;
   const long rowb = (long)b * L;
