@@ -95,35 +95,43 @@ struct DcnArgs {
 };
 
 // ------------------------------------------------------------------------------------------------------------
-// forward: 128 pixels x 64 output channels per block, K = 9 taps x C in 64-channel slabs
+// forward: 128 pixels x FCO output channels per block (FCO = 64, or 128 for Cout % 128 == 0: the sampled A slab
+// then feeds twice the columns — the l-scale head's 256 channels sampled every slab four times), K = 9 taps x C in
+// 64-channel slabs; 4 x FCO / 64 waves: 4 along the pixels x FCO / 64 along the columns. Each output element sums the
+// same K steps in the same order for either FCO (bitwise equal).
 // ------------------------------------------------------------------------------------------------------------
 constexpr int FBM = 128, FLD = 72;
+__host__ __device__ constexpr int dcn_fwd_fco(int Cout) { return Cout % 128 == 0 ? 128 : 64; }
 
+template <int FCO>
 __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
+  constexpr int NT = 4 * FCO;          // threads
+  constexpr int SPR = NT / FBM;        // sampling threads per pixel row (2 / 4)
+  constexpr int SCH = 64 / SPR / 8;    // 16-byte chunks each of them samples per corner (4 / 2)
+  constexpr int OP = FCO + 8;          // epilogue image pitch
+  static_assert(FBM * OP <= 2 * FBM * FLD, "epilogue image fits the A buffers");
   __shared__ __attribute__((aligned(16))) __bf16 As[2][FBM * FLD];
-  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][64 * FLD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][FCO * FLD];
   __shared__ __attribute__((aligned(16))) __bf16 Oms[FBM * 32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long M = (long)a.N * a.H * a.W;
-  const int mtiles = (int)((M + FBM - 1) / FBM), ntiles = a.Cout / 64;
+  const int ntiles = a.Cout / FCO;
   const int mt = bid / ntiles, nt = bid % ntiles;
   const long m0 = (long)mt * FBM;
-  const int co0 = nt * 64;
-  (void)mtiles;
+  const int co0 = nt * FCO;
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.x_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.w_bytes, 0x00020000);
 
   // offset / mask rows of the tile (first 32 channels) into LDS
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int q = tid + 256 * i, r = q >> 2, ch = (q & 3) * 8;
+  for (int q = tid; q < FBM * 4; q += NT) {
+    const int r = q >> 2, ch = (q & 3) * 8;
     const long m = m0 + r;
     u32x4 v = {0u, 0u, 0u, 0u};
     if (m < M) v = ld16(a.om + m * a.omcs + ch);
     st16(&Oms[r * 32 + ch], v);
   }
-  // this thread's sampling row and channel half
-  const int r = tid >> 1, hf = tid & 1;
+  // this thread's sampling row and channel part
+  const int r = tid / SPR, hf = tid % SPR;
   const long m = m0 + r;
   const bool rok = m < M;
   int n, h, w;
@@ -132,7 +140,7 @@ __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
   const int cchunks = a.C / 64, steps = 9 * cchunks;
   __syncthreads();
 
-  u32x4 raw[4][4];  // [corner][chunk]
+  u32x4 raw[4][SCH];  // [corner][chunk]
   float cw[4];
   u32x4 rb[2];
   auto load = [&](int s) {
@@ -141,7 +149,7 @@ __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
     const float mk = sigm((float)Oms[r * 32 + 18 + t]);
     Corners cs;
     sample((float)(h - 1 + t / 3) + oy, (float)(w - 1 + t % 3) + ox, a.H, a.W, cs);
-    const int c = cc * 64 + hf * 32;
+    const int c = cc * 64 + hf * (64 / SPR);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const bool ok = rok && cs.ok[q];
@@ -149,11 +157,11 @@ __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
       const int pix = ibase + (cs.y0 + (q >> 1)) * a.W + cs.x0 + (q & 1);
       const unsigned base = ok ? (unsigned)(pix * a.xcs + c) * 2u : OOR;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) raw[q][j] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? base + 16u * j : OOR, 0, 0);
+      for (int j = 0; j < SCH; ++j) raw[q][j] = __builtin_amdgcn_raw_buffer_load_b128(xr, ok ? base + 16u * j : OOR, 0, 0);
     }
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int q = tid + 256 * i;
+    for (int i = 0; i < 2; ++i) {  // B: FCO rows x 64 channels = 2 chunks per thread
+      const int q = tid + NT * i;
       const int row = q >> 3, ch = (q & 7) * 8;
       rb[i] = __builtin_amdgcn_raw_buffer_load_b128(
           wr, (unsigned)(((co0 + row) * 9 * a.C) + t * a.C + cc * 64 + ch) * 2u, 0, 0);
@@ -161,7 +169,7 @@ __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < SCH; ++j) {
       float acc8[8], f[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc8[e] = 0.f;
@@ -175,11 +183,11 @@ __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
       __bf16* oe = reinterpret_cast<__bf16*>(&o);
 #pragma unroll
       for (int e = 0; e < 8; ++e) oe[e] = (__bf16)acc8[e];
-      st16(&As[buf][r * FLD + hf * 32 + 8 * j], o);
+      st16(&As[buf][r * FLD + hf * (64 / SPR) + 8 * j], o);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int q = tid + 256 * i;
+      const int q = tid + NT * i;
       st16(&Bs[buf][(q >> 3) * FLD + (q & 7) * 8], rb[i]);
     }
   };
@@ -189,7 +197,7 @@ __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  const int wr0 = wave * 32;
+  const int wr0 = (wave & 3) * 32, wc0 = (wave >> 2) * 64;  // 32 pixel rows x 64 columns per wave
   load(0);
   store(0);
   __syncthreads();
@@ -204,7 +212,8 @@ __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
         fa[i] = *reinterpret_cast<const bf16x8*>(&As[cur][(wr0 + 16 * i + (lane & 15)) * FLD + 32 * kk + 8 * (lane >> 4)]);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        fb[j] = *reinterpret_cast<const bf16x8*>(&Bs[cur][(16 * j + (lane & 15)) * FLD + 32 * kk + 8 * (lane >> 4)]);
+        fb[j] = *reinterpret_cast<const bf16x8*>(
+            &Bs[cur][(wc0 + 16 * j + (lane & 15)) * FLD + 32 * kk + 8 * (lane >> 4)]);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -213,24 +222,27 @@ __device__ __forceinline__ void dcn_fwd_body(const DcnArgs& a, int bid) {
     if (s + 1 < steps) store(cur ^ 1);  // the other buffer was last read in step s-1 (before the barrier)
     __syncthreads();
   }
-  // epilogue: bf16 image of the tile (in A buffer 0), then 16-byte row stores
+  // epilogue: bf16 image of the tile (in the A buffers), then 16-byte row stores
   __bf16* Os = As[0];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) Os[(wr0 + 16 * i + 4 * (lane >> 4) + e) * FLD + 16 * j + (lane & 15)] = (__bf16)acc[i][j][e];
+      for (int e = 0; e < 4; ++e)
+        Os[(wr0 + 16 * i + 4 * (lane >> 4) + e) * OP + wc0 + 16 * j + (lane & 15)] = (__bf16)acc[i][j][e];
   __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int q = tid + 256 * i, row = q >> 3, ch = (q & 7) * 8;
+  for (int q = tid; q < FBM * (FCO / 8); q += NT) {
+    const int row = q / (FCO / 8), ch = (q % (FCO / 8)) * 8;
     const long mm = m0 + row;
-    if (mm < M) st16(a.y + mm * a.ycs + co0 + ch, *reinterpret_cast<const u32x4*>(&Os[row * FLD + ch]));
+    if (mm < M) st16(a.y + mm * a.ycs + co0 + ch, *reinterpret_cast<const u32x4*>(&Os[row * OP + ch]));
   }
 }
 
-__global__ void __launch_bounds__(256, 2) dcn_fwd_kernel(DcnArgs a) { dcn_fwd_body(a, xcd_order(blockIdx.x, gridDim.x)); }
+template <int FCO>
+__global__ void __launch_bounds__(4 * FCO, FCO == 64 ? 2 : 1) dcn_fwd_kernel(DcnArgs a) {
+  dcn_fwd_body<FCO>(a, xcd_order(blockIdx.x, gridDim.x));
+}
 
 // The AYHead's three pyramid levels in ONE launch (LevelDCNFn): block b of the grid (XCD-ordered) belongs to level l
 // with start[l] <= b < start[l + 1] and runs exactly the block b - start[l] of that level's own launch, so the
@@ -249,29 +261,37 @@ __device__ __forceinline__ int dcn_level(const DcnLevels& L, int b) {
   while (l + 1 < L.nl && b >= L.start[l + 1]) ++l;
   return l;
 }
-__global__ void __launch_bounds__(256, 2) dcn_fwd_levels_kernel(DcnLevels L) {
+template <int FCO>
+__global__ void __launch_bounds__(4 * FCO, FCO == 64 ? 2 : 1) dcn_fwd_levels_kernel(DcnLevels L) {
   const int b = xcd_order(blockIdx.x, gridDim.x), l = dcn_level(L, b);
-  dcn_fwd_body(L.a[l], b - L.start[l]);
+  dcn_fwd_body<FCO>(L.a[l], b - L.start[l]);
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// weight gradient: block = (co tile 64, tap, c tile 64) x split over pixels; 64 pixel rows per k-step
+// weight gradient: block = (tap, c tile 64) x split over pixels, ALL output channels (COT = Cout for 64 / 128 / 256):
+// the sampled B slab of a (tap, c tile) is built once and multiplies every co row of dy — with 64-wide co tiles the
+// l-scale head (Cout 256) sampled each slab four times. 64 pixel rows per k-step; each output element accumulates the
+// same k-steps in the same order whatever COT is (bitwise the 64-wide tiles).
 // ------------------------------------------------------------------------------------------------------------
 constexpr int WR = 64, WP = 80;  // rows per k-step; LDS row pitch (odd multiple of 16 elements: conflict-free tr reads)
+__host__ __device__ constexpr int dcn_wg_cot(int Cout) { return Cout == 128 || Cout == 256 ? Cout : 64; }
 
 // (b: XCD-ordered block of the level's launch, tiles: tile blocks per split)
+template <int COT>
 __device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tiles) {
-  __shared__ __attribute__((aligned(16))) __bf16 As[WR * WP];  // dy rows [p][co]
+  constexpr int AP = COT + 16;               // dy row pitch: odd multiple of 16 elements
+  constexpr int ACH = WR * (COT / 8) / 256;  // 16-byte dy chunks per thread and k-step
+  constexpr int WCO = COT / 2, TM = WCO / 16;
+  __shared__ __attribute__((aligned(16))) __bf16 As[WR * AP];  // dy rows [p][co]
   __shared__ __attribute__((aligned(16))) __bf16 Bs[WR * WP];  // sampled rows [p][c]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int ctiles = a.C / 64, cotiles = a.Cout / 64;
+  const int ctiles = a.C / 64;
   const int split = b / tiles;
   b -= split * tiles;
   const int ct = b % ctiles;
   b /= ctiles;
   const int t = b % 9, cot = b / 9;
-  (void)cotiles;
-  const int c0 = ct * 64, co0 = cot * 64;
+  const int c0 = ct * 64, co0 = cot * COT;
   const long M = (long)a.N * a.H * a.W;
   const long pbeg = (long)split * a.rows_per_split;
   const long pend = min(M, pbeg + a.rows_per_split);
@@ -279,15 +299,21 @@ __device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tile
   const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dy_bytes, 0x00020000);
   const int ti = t / 3, tj = t % 3;
 
-  u32x4 ra[2], rq[2][4];
+  u32x4 ra[ACH], rq[2][4];
   float cw[2][4];
   auto load = [&](long p0) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int q = tid + 256 * i, row = q / (COT / 8), ch = (q % (COT / 8)) * 8;
+      const long p = p0 + row;
+      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(dyr, p < pend ? (unsigned)((int)p * a.dycs + co0 + ch) * 2u : OOR,
+                                                    0, 0);
+    }
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = tid + 256 * i, row = q >> 3, ch = (q & 7) * 8;
       const long p = p0 + row;
       const bool ok = p < pend;
-      ra[i] = __builtin_amdgcn_raw_buffer_load_b128(dyr, ok ? (unsigned)((int)p * a.dycs + co0 + ch) * 2u : OOR, 0, 0);
       int n = 0, h = 0, w = 0;
       pix_nhw(ok ? p : 0, a.H, a.W, n, h, w);
       const __bf16* o = a.om + (ok ? p : 0) * a.omcs;
@@ -307,9 +333,13 @@ __device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tile
   };
   auto store = [&]() {
 #pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int q = tid + 256 * i, row = q / (COT / 8), ch = (q % (COT / 8)) * 8;
+      st16(&As[row * AP + ch], ra[i]);
+    }
+#pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int q = tid + 256 * i, row = q >> 3, ch = (q & 7) * 8;
-      st16(&As[row * WP + ch], ra[i]);
       float s8[8], f[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) s8[e] = 0.f;
@@ -326,16 +356,16 @@ __device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tile
       st16(&Bs[row * WP + ch], o);
     }
   };
-  // waves 2 x 2 over (co, c): 32 x 32 each
+  // waves 2 x 2 over (co, c): COT/2 x 32 each
   const int wm = wave >> 1, wn = wave & 1;
-  f32x4 acc[2][2];
+  f32x4 acc[TM][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
   const int g = lane >> 4, q4 = (lane >> 2) & 3, p4 = lane & 3;
   const int row0 = 4 * g + q4;
-  const __bf16* a_base = As + row0 * WP + wm * 32 + 4 * p4;
+  const __bf16* a_base = As + row0 * AP + wm * WCO + 4 * p4;
   const __bf16* b_base = Bs + row0 * WP + wn * 32 + 4 * p4;
   const int ksteps = (int)((pend - pbeg + WR - 1) / WR);
   if (ksteps > 0) {
@@ -347,10 +377,10 @@ __device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tile
     if (s + 1 < ksteps) load(pbeg + (long)(s + 1) * WR);
 #pragma unroll
     for (int u = 0; u < WR / 32; ++u) {
-      bf16x8 fa[2], fb[2];
+      bf16x8 fa[TM], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        v4s both[2] = {tr16(a_base + u * 32 * WP + i * 16), tr16(a_base + (u * 32 + 16) * WP + i * 16)};
+      for (int i = 0; i < TM; ++i) {
+        v4s both[2] = {tr16(a_base + u * 32 * AP + i * 16), tr16(a_base + (u * 32 + 16) * AP + i * 16)};
         fa[i] = *reinterpret_cast<bf16x8*>(both);
       }
 #pragma unroll
@@ -359,7 +389,7 @@ __device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tile
         fb[j] = *reinterpret_cast<bf16x8*>(both);
       }
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
@@ -371,28 +401,30 @@ __device__ __forceinline__ void dcn_wgrad_body(const DcnArgs& a, int b, int tile
   }
   float* part = a.part + (long)split * a.Cout * 9 * a.C;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < TM; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int c = c0 + wn * 32 + 16 * j + (lane & 15);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int co = co0 + wm * 32 + 16 * i + 4 * (lane >> 4) + e;
+        const int co = co0 + wm * WCO + 16 * i + 4 * (lane >> 4) + e;
         part[((long)co * 9 + t) * a.C + c] = acc[i][j][e];
       }
     }
 }
 
+template <int COT>
 __global__ void __launch_bounds__(256, 2) dcn_wgrad_kernel(DcnArgs a) {
-  dcn_wgrad_body(a, xcd_order(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y), gridDim.x);
+  dcn_wgrad_body<COT>(a, xcd_order(blockIdx.x + blockIdx.y * gridDim.x, gridDim.x * gridDim.y), gridDim.x);
 }
 // Levels dispatch in order (P3's long split blocks first, the short P5 blocks fill the tail) and the XCD grouping is
 // applied within a level: interleaving the three levels over the whole grid started long P3 blocks last (l-scale:
 // 7.6 ms for the three levels in one launch against 4.1 ms as three launches)
+template <int COT>
 __global__ void __launch_bounds__(256, 2) dcn_wgrad_levels_kernel(DcnLevels L) {
   const int l = dcn_level(L, blockIdx.x), s0 = L.start[l];
   const int b = xcd_order(blockIdx.x - s0, L.start[l + 1] - s0);
-  dcn_wgrad_body(L.a[l], b, L.tiles[l]);
+  dcn_wgrad_body<COT>(L.a[l], b, L.tiles[l]);
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -973,15 +1005,17 @@ extern "C" int adr_dcn_fwd_bf16(const void* x, int xcs, const void* om, int omcs
   a.x_bytes = (int)((long)N * H * W * xcs * 2);
   a.w_bytes = Cout * 9 * C * 2;
   const long M = (long)N * H * W;
-  const int blocks = cdiv(M, FBM) * (Cout / 64);
-  hipLaunchKernelGGL(dcn_fwd_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
+  const int fco = dcn_fwd_fco(Cout);
+  const int blocks = cdiv(M, FBM) * (Cout / fco);
+  if (fco == 128) hipLaunchKernelGGL(dcn_fwd_kernel<128>, dim3(blocks), dim3(512), 0, (hipStream_t)stream, a);
+  else hipLaunchKernelGGL(dcn_fwd_kernel<64>, dim3(blocks), dim3(256), 0, (hipStream_t)stream, a);
   return check_launch("adr_dcn_fwd_bf16");
 }
 
 extern "C" int adr_dcn_wgrad_bf16_splits(int N, int H, int W, int C, int Cout) {
   const long M = (long)N * H * W;
   const long steps = (M + WR - 1) / WR;
-  const int tiles = 9 * (C / 64) * (Cout / 64);
+  const int tiles = 9 * (C / 64) * (Cout / dcn_wg_cot(Cout));
   long s = 1024 / tiles + 1;  // >= ~1k blocks
   if (s > steps) s = steps;
   if (s < 1) s = 1;
@@ -1011,8 +1045,12 @@ extern "C" int adr_dcn_wgrad_bf16(const void* x, int xcs, const void* om, int om
   const long steps = (M + WR - 1) / WR;
   a.rows_per_split = ((steps + splits - 1) / splits) * WR;
   a.splits = splits;
-  dim3 grid(9 * (C / 64) * (Cout / 64), splits);
-  hipLaunchKernelGGL(dcn_wgrad_kernel, grid, dim3(256), 0, (hipStream_t)stream, a);
+  dim3 grid(9 * (C / 64) * (Cout / dcn_wg_cot(Cout)), splits);
+  switch (dcn_wg_cot(Cout)) {
+    case 256: hipLaunchKernelGGL(dcn_wgrad_kernel<256>, grid, dim3(256), 0, (hipStream_t)stream, a); break;
+    case 128: hipLaunchKernelGGL(dcn_wgrad_kernel<128>, grid, dim3(256), 0, (hipStream_t)stream, a); break;
+    default: hipLaunchKernelGGL(dcn_wgrad_kernel<64>, grid, dim3(256), 0, (hipStream_t)stream, a); break;
+  }
   return check_launch("adr_dcn_wgrad_bf16");
 }
 
@@ -1094,10 +1132,13 @@ extern "C" int adr_dcn_fwd_bf16_levels(const adr_dcn_level* lv, int levels, int 
     a.ycs = ycs;
     a.w_bytes = Cout * 9 * C * 2;
     L.start[l] = total;
-    total += cdiv((long)N * a.H * a.W, FBM) * (Cout / 64);
+    total += cdiv((long)N * a.H * a.W, FBM) * (Cout / dcn_fwd_fco(Cout));
   }
   L.start[levels] = total;
-  hipLaunchKernelGGL(dcn_fwd_levels_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, L);
+  if (dcn_fwd_fco(Cout) == 128)
+    hipLaunchKernelGGL(dcn_fwd_levels_kernel<128>, dim3(total), dim3(512), 0, (hipStream_t)stream, L);
+  else
+    hipLaunchKernelGGL(dcn_fwd_levels_kernel<64>, dim3(total), dim3(256), 0, (hipStream_t)stream, L);
   return check_launch("adr_dcn_fwd_bf16_levels");
 }
 
@@ -1106,7 +1147,7 @@ extern "C" int adr_dcn_wgrad_bf16_levels(const adr_dcn_level* lv, int levels, in
   DcnLevels L;
   if (int rc = dcn_levels_fill(lv, levels, xcs, omcs, N, C, Cout, L)) return rc;
   int total = 0;
-  const int tiles = 9 * (C / 64) * (Cout / 64);
+  const int tiles = 9 * (C / 64) * (Cout / dcn_wg_cot(Cout));
   for (int l = 0; l < levels; ++l) {
     DcnArgs& a = L.a[l];
     ADR_REQUIRE(lv[l].part && lv[l].splits >= 1, "dcn_wgrad levels: partials / splits of level %d", l);
@@ -1123,7 +1164,11 @@ extern "C" int adr_dcn_wgrad_bf16_levels(const adr_dcn_level* lv, int levels, in
     total += tiles * lv[l].splits;
   }
   L.start[levels] = total;
-  hipLaunchKernelGGL(dcn_wgrad_levels_kernel, dim3(total), dim3(256), 0, (hipStream_t)stream, L);
+  switch (dcn_wg_cot(Cout)) {
+    case 256: hipLaunchKernelGGL(dcn_wgrad_levels_kernel<256>, dim3(total), dim3(256), 0, (hipStream_t)stream, L); break;
+    case 128: hipLaunchKernelGGL(dcn_wgrad_levels_kernel<128>, dim3(total), dim3(256), 0, (hipStream_t)stream, L); break;
+    default: hipLaunchKernelGGL(dcn_wgrad_levels_kernel<64>, dim3(total), dim3(256), 0, (hipStream_t)stream, L); break;
+  }
   return check_launch("adr_dcn_wgrad_bf16_levels");
 }
 
