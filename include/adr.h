@@ -361,6 +361,12 @@ int adr_pack_weight2(int dtype, const float* src, void* krsc, void* crsk, int K,
  * packing elements [start, start+len) of one weight (the trainer packs every conv weight once per step). */
 int adr_pack_chunk_size(void);
 int adr_pack_weight2_batched(int dtype, const void* table, int nchunks, void* stream);
+/* The same packing by 64 x 64 tiles (what the trainer launches once per step): table = ntiles device rows
+ * {const float* src; void* krsc; void* crsk; int K, Kp, C, Cp, RS, transpose_kc; int t, k0, c0, pad;}
+ * (adr_pack_tile_size() bytes each), each row packing tap t, rows [k0, k0+64) x columns [c0, c0+64) of one weight
+ * (clipped to Kp x Cp; zeros beyond K / C) into both layouts with coalesced stores. */
+int adr_pack_tile_size(void);
+int adr_pack_weight2_tiled(int dtype, const void* table, int ntiles, void* stream);
 int adr_unpack_weight_grad(const float* src, float* dst, int K, int C, int Cp, int RS, int transpose_kc,
                            int accumulate, void* stream);
 /* Stem: model.0 Conv(3, K, 3, 2) (nn/modules/conv.py:36-54, the first yaml row) straight from the fp32 NCHW

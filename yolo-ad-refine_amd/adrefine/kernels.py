@@ -150,7 +150,10 @@ _BATCHED_BYTES = {
     "adr_dotsum_batched": lambda a: sum(4 * e.N * e.HW * e.C + 4 * e.N * e.chunks * 2 * e.C
                                         for e in _entries(a, DotsumEntry)),
     "adr_copy_pieces": lambda a: sum(4 * int(a[2]) * e.C for e in _entries(a, CopyPiece)),
+    # fp32 weights read once, both bf16 layouts written (PackCache._build records the sum per table)
+    "adr_pack_weight2_tiled": lambda a: _PACK_BYTES.get(int(a[1]), 0),
 }
+_PACK_BYTES = {}  # device table pointer -> algorithmic bytes of one adr_pack_weight2_tiled launch
 
 
 def _scan_tensors(v, want, found, depth=0):
@@ -602,8 +605,6 @@ class PackCache:
     all of them in ONE batched launch at the start of the step (inside the captured graph), and pack_weight2
     returns the cached buffers until the optimizer invalidates them."""
 
-    CHUNK = 1 << 13
-
     def __init__(self, cache_bn_coefs=False):
         self.specs = {}
         self.valid = False
@@ -620,20 +621,25 @@ class PackCache:
             _bn_eval_coefs_into(bn, scale, shift)
 
     def _build(self):
+        """One row per (weight, tap, 64 x 64 tile) for adr_pack_weight2_tiled (coalesced stores in both layouts)."""
         import numpy as np
         dt = np.dtype([("src", "<u8"), ("krsc", "<u8"), ("crsk", "<u8"), ("K", "<i4"), ("Kp", "<i4"), ("C", "<i4"),
-                       ("Cp", "<i4"), ("RS", "<i4"), ("tkc", "<i4"), ("start", "<i8"), ("len", "<i8")])
-        assert dt.itemsize == lib.adr_pack_chunk_size()
+                       ("Cp", "<i4"), ("RS", "<i4"), ("tkc", "<i4"), ("t", "<i4"), ("k0", "<i4"), ("c0", "<i4"),
+                       ("pad", "<i4")])
+        assert dt.itemsize == lib.adr_pack_tile_size()
         rows = []
         for sp in self.specs.values():
             w, K, Kp, C, Cp, RS, tkc, krsc, crsk = sp
-            n = Kp * RS * Cp
-            for st in range(0, n, self.CHUNK):
-                rows.append((w.data_ptr(), krsc.data_ptr(), crsk.data_ptr(), K, Kp, C, Cp, RS, tkc, st,
-                             min(self.CHUNK, n - st)))
+            for t in range(RS):
+                for k0 in range(0, Kp, 64):
+                    for c0 in range(0, Cp, 64):
+                        rows.append((w.data_ptr(), krsc.data_ptr(), crsk.data_ptr(), K, Kp, C, Cp, RS, tkc, t, k0,
+                                     c0, 0))
         tab = np.array(rows, dtype=dt)
         dev = next(iter(self.specs.values()))[0].device
         self.tab_dev = torch.from_numpy(tab.view(np.uint8).copy()).to(dev)
+        _PACK_BYTES[self.tab_dev.data_ptr()] = sum(4 * K * C * RS + 2 * 2 * Kp * Cp * RS
+                                                   for _, K, Kp, C, Cp, RS, _, _, _ in self.specs.values())
         self.nchunks = len(rows)
         self.table = len(self.specs)
 
@@ -642,7 +648,7 @@ class PackCache:
             return
         if self.table != len(self.specs):
             self._build()
-        lib.adr_pack_weight2_batched(BF16, fptr(self.tab_dev), self.nchunks, stream())
+        lib.adr_pack_weight2_tiled(BF16, fptr(self.tab_dev), self.nchunks, stream())
         self.valid = True
 
 

@@ -118,7 +118,7 @@ def _traced(name, fn, a):
     return rc
 
 
-_NONSTATUS = {"adr_abi_version", "adr_conv2d_wgrad_bias_fusable", "adr_dwconv_wgrad_bias_fusable", "adr_conv2d_fwd_stat_tiles", "adr_conv2d_fwd_bf16_stat_tiles", "adr_conv2d_wgrad_splits", "adr_nc_reduce_chunks", "adr_opt_entry_size", "adr_pack_chunk_size", "adr_stem_fwd_tiles",
+_NONSTATUS = {"adr_abi_version", "adr_conv2d_wgrad_bias_fusable", "adr_dwconv_wgrad_bias_fusable", "adr_conv2d_fwd_stat_tiles", "adr_conv2d_fwd_bf16_stat_tiles", "adr_conv2d_wgrad_splits", "adr_nc_reduce_chunks", "adr_opt_entry_size", "adr_pack_chunk_size", "adr_pack_tile_size", "adr_stem_fwd_tiles",
               "adr_opt_chunk_size", "adr_dcn_wgrad_bf16_splits", "adr_gn_fused_supported",
               "adr_fp8_amax_blocks", "adr_conv2d_fp8_supported", "adr_conv2d_fwd_fp8_stat_tiles",
               "adr_dwconv_fwd_act_supported", "adr_conv2d_bf16_xf_reuse", "adr_augment_desc_size",
