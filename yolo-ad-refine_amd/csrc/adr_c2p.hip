@@ -603,15 +603,17 @@ __global__ void adyt_alpha_kernel(const float* dan, const float* imp, int N, flo
 // Per-(image, head) block; threads = TPP tokens x LD lanes, a lane holding VW consecutive channels of the head
 // (D = LD * VW): every q/k/v/dout access is a 16-byte vector, per-token sums over d are LD-lane xor shuffles,
 // per-channel sums over tokens go through one LDS pass (chan_sum).
-template <typename T, int VW, int LD>
-__global__ void __launch_bounds__(256) tssa_fwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok,
+// NTH = 1024 threads: one block per (image, head) walks all the tokens, and with 256 threads the passes were
+// load-latency bound (~7 GB/s per block: 64 - 128 blocks per launch); four times the loads in flight per block
+template <typename T, int VW, int LD, int NTH = 1024>
+__global__ void __launch_bounds__(NTH) tssa_fwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok,
                                                        const float* temp, T* out, int ocs, int oimg, int heads,
                                                        float* Pi_out, float* ss_out, float* attn_out) {
-  constexpr int TPP = 256 / LD, D = LD * VW;
+  constexpr int TPP = NTH / LD, D = LD * VW;
   extern __shared__ float Pi[];  // Ntok
-  __shared__ float red[256 * VW];
+  __shared__ float red[NTH * VW];
   __shared__ float at[D];
-  __shared__ float sh[256];
+  __shared__ float sh[NTH];
   const int b = blockIdx.x / heads, h = blockIdx.x % heads;
   const int lane = threadIdx.x % LD, r0 = threadIdx.x / LD, c0 = h * D + lane * VW;
   const long base = (long)b * Ntok, bh = (long)b * heads + h;
@@ -640,20 +642,20 @@ __global__ void __launch_bounds__(256) tssa_fwd_kernel(const T* q, const T* k, c
   }
   sh[threadIdx.x] = mx;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = NTH / 2; o > 0; o >>= 1) {
     if (threadIdx.x < o) sh[threadIdx.x] = fmaxf(sh[threadIdx.x], sh[threadIdx.x + o]);
     __syncthreads();
   }
   mx = sh[0];
   __syncthreads();
   float z = 0.f;
-  for (int n = threadIdx.x; n < Ntok; n += 256) {
+  for (int n = threadIdx.x; n < Ntok; n += NTH) {
     const float e = __expf(Pi[n] - mx);
     Pi[n] = e;
     z += e;
   }
-  z = block_sum256(z, sh);
-  for (int n = threadIdx.x; n < Ntok; n += 256) {
+  z = block_sum<NTH>(z, sh);
+  for (int n = threadIdx.x; n < Ntok; n += NTH) {
     Pi[n] /= z;
     Pi_out[bh * Ntok + n] = Pi[n];
   }
@@ -668,7 +670,7 @@ __global__ void __launch_bounds__(256) tssa_fwd_kernel(const T* q, const T* k, c
 #pragma unroll
     for (int e = 0; e < VW; ++e) p[e] += Pi[n] * kv[e] * kv[e];
   }
-  chan_sum<VW, LD>(p, red, at);
+  chan_sum<VW, LD, NTH>(p, red, at);
   if (threadIdx.x < D) {
     const float a = 1.f / (1.f + at[threadIdx.x]);
     at[threadIdx.x] = a;
@@ -685,16 +687,16 @@ __global__ void __launch_bounds__(256) tssa_fwd_kernel(const T* q, const T* k, c
   }
 }
 
-template <typename T, int VW, int LD>
-__global__ void __launch_bounds__(256) tssa_bwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok,
+template <typename T, int VW, int LD, int NTH = 1024>
+__global__ void __launch_bounds__(NTH) tssa_bwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok,
                                                        const float* temp, const T* dout, int dcs, int dimg, int heads,
                                                        const float* Pi_in, const float* ss_in, const float* attn_in,
                                                        T* dq, T* dk, T* dv, int gcs, float* dtemp_part) {
-  constexpr int TPP = 256 / LD, D = LD * VW;
+  constexpr int TPP = NTH / LD, D = LD * VW;
   extern __shared__ float dPi[];  // Ntok
-  __shared__ float red[256 * VW];
+  __shared__ float red[NTH * VW];
   __shared__ float dd[D];
-  __shared__ float sh[256];
+  __shared__ float sh[NTH];
   const int b = blockIdx.x / heads, h = blockIdx.x % heads;
   const int lane = threadIdx.x % LD, r0 = threadIdx.x / LD, c0 = h * D + lane * VW;
   const long base = (long)b * Ntok, bh = (long)b * heads + h;
@@ -721,7 +723,7 @@ __global__ void __launch_bounds__(256) tssa_bwd_kernel(const T* q, const T* k, c
     }
     vstore<T, VW>(dv + (base + n) * gcs + c0, o);
   }
-  chan_sum<VW, LD>(p, red, dd);
+  chan_sum<VW, LD, NTH>(p, red, dd);
   if (threadIdx.x < D) dd[threadIdx.x] = -dd[threadIdx.x] * attn[threadIdx.x] * attn[threadIdx.x];  // ddots
   __syncthreads();
   // dPi[n] = sum_d (-dout v attn + ddots k^2) ; dk = ddots * Pi * 2k
@@ -746,7 +748,7 @@ __global__ void __launch_bounds__(256) tssa_bwd_kernel(const T* q, const T* k, c
       part += pn * s;
     }
   }
-  const float dot = block_sum256(part, sh);
+  const float dot = block_sum<NTH>(part, sh);
   // softmax backward -> dl ; dtemp partial ; dss -> dq
   float tpart = 0.f;
   for (int n = r0; n < Ntok; n += TPP) {
@@ -773,7 +775,7 @@ __global__ void __launch_bounds__(256) tssa_bwd_kernel(const T* q, const T* k, c
     }
     vstore<T, VW>(dq + (base + n) * gcs + c0, o);
   }
-  tpart = block_sum256(tpart, sh);
+  tpart = block_sum<NTH>(tpart, sh);
   if (threadIdx.x == 0) dtemp_part[bh] = tpart;
 }
 
@@ -1507,11 +1509,11 @@ extern "C" int adr_tssa_fwd(int dtype, const void* q, const void* k, const void*
   const size_t sm = Ntok * sizeof(float);
   ADR_REQUIRE(sm <= 64 * 1024, "tssa: Ntok=%d too large", Ntok);
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL((tssa_fwd_kernel<__bf16, 8, 8>), dim3(B * heads), dim3(256), sm, st, (const __bf16*)q,
+    hipLaunchKernelGGL((tssa_fwd_kernel<__bf16, 8, 8>), dim3(B * heads), dim3(1024), sm, st, (const __bf16*)q,
                        (const __bf16*)k, (const __bf16*)v, cs, Ntok, temp, (__bf16*)out, ocs, oimg, heads, Pi, ss,
                        attn);
   else
-    hipLaunchKernelGGL((tssa_fwd_kernel<float, 4, 16>), dim3(B * heads), dim3(256), sm, st, (const float*)q,
+    hipLaunchKernelGGL((tssa_fwd_kernel<float, 4, 16>), dim3(B * heads), dim3(1024), sm, st, (const float*)q,
                        (const float*)k, (const float*)v, cs, Ntok, temp, (float*)out, ocs, oimg, heads, Pi, ss, attn);
   return check_launch("adr_tssa_fwd");
 }
@@ -1527,11 +1529,11 @@ extern "C" int adr_tssa_bwd(int dtype, const void* q, const void* k, const void*
   const size_t sm = Ntok * sizeof(float);
   ADR_REQUIRE(sm <= 64 * 1024, "tssa_bwd: Ntok=%d too large", Ntok);
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL((tssa_bwd_kernel<__bf16, 8, 8>), dim3(B * heads), dim3(256), sm, st, (const __bf16*)q,
+    hipLaunchKernelGGL((tssa_bwd_kernel<__bf16, 8, 8>), dim3(B * heads), dim3(1024), sm, st, (const __bf16*)q,
                        (const __bf16*)k, (const __bf16*)v, cs, Ntok, temp, (const __bf16*)dout, dcs, dimg, heads, Pi,
                        ss, attn, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, gcs, ws);
   else
-    hipLaunchKernelGGL((tssa_bwd_kernel<float, 4, 16>), dim3(B * heads), dim3(256), sm, st, (const float*)q,
+    hipLaunchKernelGGL((tssa_bwd_kernel<float, 4, 16>), dim3(B * heads), dim3(1024), sm, st, (const float*)q,
                        (const float*)k, (const float*)v, cs, Ntok, temp, (const float*)dout, dcs, dimg, heads, Pi, ss,
                        attn, (float*)dq, (float*)dk, (float*)dv, gcs, ws);
   hipLaunchKernelGGL(tssa_temp_reduce_kernel, dim3(1), dim3(64), 0, st, ws, B, heads, dtemp);

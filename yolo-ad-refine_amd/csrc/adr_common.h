@@ -267,7 +267,20 @@ __device__ __forceinline__ float tok_sum(float v) {
   return v;
 }
 
-// block-wide sum of one float per thread (256 threads), result broadcast
+// block-wide sum of one float per thread (NTH threads, sh[NTH]), result broadcast
+template <int NTH>
+__device__ __forceinline__ float block_sum(float v, float* sh) {
+  sh[threadIdx.x] = v;
+  __syncthreads();
+  for (int o = NTH / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  const float r = sh[0];
+  __syncthreads();
+  return r;
+}
+// the same for 256 threads
 __device__ __forceinline__ float block_sum256(float v, float* sh) {
   sh[threadIdx.x] = v;
   __syncthreads();
@@ -280,15 +293,15 @@ __device__ __forceinline__ float block_sum256(float v, float* sh) {
   return r;
 }
 
-// per-channel (d) sum over the block's token rows: red has 256 * VW floats; result in dsum[D]
-template <int VW, int LD>
+// per-channel (d) sum over the block's token rows: red has NTH * VW floats; result in dsum[D]
+template <int VW, int LD, int NTH = 256>
 __device__ __forceinline__ void chan_sum(const float* part, float* red, float* dsum) {
-  constexpr int TPP = 256 / LD;
+  constexpr int TPP = NTH / LD;
   const int lane = threadIdx.x % LD;
 #pragma unroll
   for (int e = 0; e < VW; ++e) red[threadIdx.x * VW + e] = part[e];
   __syncthreads();
-  for (int d = threadIdx.x; d < LD * VW; d += 256) {
+  for (int d = threadIdx.x; d < LD * VW; d += NTH) {
     const int ln = d / VW, e = d % VW;
     float t = 0.f;
     for (int r = 0; r < TPP; ++r) t += red[(r * LD + ln) * VW + e];
