@@ -40,3 +40,24 @@ def test_one_hip_runtime_loaded():
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300).stdout.strip()
     libs = eval(out)  # noqa: S307 - our own printed list
     assert len(libs) == 1 and "torch" in libs[0], libs
+
+
+def test_roofline_byte_estimators_take_ctypes_pointers():
+    """bench.py's roofline timing hands every entry point's arguments, ctypes pointers included, to the per-entry
+    byte / flop estimators (kernels._BATCHED_BYTES, _ALG_FLOPS); they must read c_void_p arguments (CPU check)."""
+    import ctypes
+    from adrefine import kernels as K
+    tab = ctypes.c_void_p(0x1234000)
+    f = K._BATCHED_BYTES["adr_pack_weight2_tiled"]
+    assert f((1, tab, 7, None)) == 0
+    K._PACK_BYTES[0x1234000] = 4096
+    try:
+        assert f((1, tab, 7, None)) == 4096
+    finally:
+        del K._PACK_BYTES[0x1234000]
+    p = ctypes.c_void_p(1)
+    fwd = (1, p, p, p, 384, 0, 128, 256, 64, p, 128, 2, 100, 2, 64, 64, 0.125, p, None)
+    assert K._ALG_FLOPS["adr_attn_fwd"](fwd) == 2.0 * 2 * 2 * 100 ** 2 * 128
+    bwd = (1, p, p, p, 384, 0, 128, 256, 64, p, 128, p, 128, p, p, p, p, 384, 0, 128, 256, 2, 100, 2, 64, 64, 0.125,
+           p, None)
+    assert K._ALG_FLOPS["adr_attn_bwd"](bwd) == 2.0 * 2 * 2 * 100 ** 2 * (3 * 64 + 2 * 64)

@@ -151,7 +151,7 @@ _BATCHED_BYTES = {
                                         for e in _entries(a, DotsumEntry)),
     "adr_copy_pieces": lambda a: sum(4 * int(a[2]) * e.C for e in _entries(a, CopyPiece)),
     # fp32 weights read once, both bf16 layouts written (PackCache._build records the sum per table)
-    "adr_pack_weight2_tiled": lambda a: _PACK_BYTES.get(int(a[1]), 0),
+    "adr_pack_weight2_tiled": lambda a: _PACK_BYTES.get(_ptr(a[1]), 0),
 }
 _PACK_BYTES = {}  # device table pointer -> algorithmic bytes of one adr_pack_weight2_tiled launch
 
