@@ -23,6 +23,18 @@ constexpr int STEM_ROWS = 2;
 // a multiplication by the fp32 reciprocal (BinaryDivTrueKernel), so this does too — bitwise the reference's input
 __device__ __forceinline__ float img_val(float v) { return v; }
 __device__ __forceinline__ float img_val(uint8_t v) { return (float)v * (1.f / 255.f); }
+// word of 4 image pixels, pixel e of it, two values as a packed bf16 pair
+template <typename TI> struct StemQWord { typedef unsigned T; };  // 4 uint8 pixels
+template <> struct StemQWord<float> { typedef f32x4 T; };
+__device__ __forceinline__ float stem_w(unsigned v, int e) { return img_val((uint8_t)(v >> (8 * e))); }
+__device__ __forceinline__ float stem_w(f32x4 v, int e) { return v[e]; }
+typedef __attribute__((ext_vector_type(2))) unsigned u32x2s;
+typedef __attribute__((ext_vector_type(2))) float stem_f2;
+typedef __attribute__((ext_vector_type(2))) __bf16 stem_bf2;
+__device__ __forceinline__ unsigned pack_bf2(float a, float b) {  // one v_cvt_pk_bf16_f32
+  const stem_bf2 r = __builtin_convertvector((stem_f2){a, b}, stem_bf2);
+  return *reinterpret_cast<const unsigned*>(&r);
+}
 
 // stage image rows iy0 .. iy0+IR-1 of the 3 channels of image n into LDS as bf16 [3][IR][W+2] with zero
 // columns at -1 and W (and zero rows outside the image); 16-byte (fp32) / 4-byte (uint8) loads when W % 4 == 0
@@ -341,6 +353,138 @@ __global__ void __launch_bounds__(256) stem_wgrad_loop_kernel(const TI* __restri
   }
 }
 
+// weight gradient, persistent, on deinterleaved rows (W % 32 == 0, W <= STEM_LOOP_W, K <= 32). The kernel above feeds
+// each 16x16x32 step with 24 two-byte LDS reads per lane (eight dy values of one channel, sixteen im2col taps of
+// eight pixels); here both operands come from 8-byte reads:
+//   * dy^T (A: output channel x 32 pixels) by ds_read_b64_tr_b16 from the natural [pixel][K] dy image: lane group g
+//     takes pixels 4g .. 4g+3 and 16 + 4g .. 16 + 4g + 3 of the step (two transposed 4 x 16 blocks; the two groups of
+//     a 32-lane half read 256 contiguous bytes, no bank conflict);
+//   * im2col (B: 32 pixels x tap) from the staged input rows split by column parity — E[m] = x[2m], O[m] = x[2m+1],
+//     O'[m] = x[2m-1] — where tap kx of output columns ox .. ox+3 is the aligned 8-byte run E / O / O' [ox .. ox+3]
+//     (kx = 1 / 2 / 0), the same pixels as the dy block.
+// The reduction slots of a step are permuted against the kernel above (the MFMA sums the same 32 products), so the
+// partials agree to fp32 rounding. Next-tile prefetch into registers and partials [block][KT*16][32] as above.
+constexpr int STEM_PP_PAD = 8;  // plane pitch Wo + 8: the 16 taps of a lane group spread over the banks
+template <int KT, typename TI>
+__global__ void __launch_bounds__(256) stem_wgrad_q_kernel(const TI* __restrict__ img, int H, int W,
+                                                           const __bf16* __restrict__ dy, int dcs, int Ho, int Wo,
+                                                           int ntiles, int per, float* __restrict__ part) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+  constexpr int IR = 2 * STEM_ROWS + 1, NR = 3 * IR, KC = KT * 16;
+  constexpr int DCH = STEM_ROWS * (STEM_LOOP_W / 2) * KT * 2 / 256;  // 16-byte dy chunks per thread
+  typedef typename StemWord<TI>::T Word;
+  const int PP = Wo + STEM_PP_PAD;
+  __bf16* pl = reinterpret_cast<__bf16*>(smraw);                          // [NR][3: E, O, O'][PP]
+  __bf16* ds = pl + ((NR * 3 * PP + 7) & ~7);                             // [STEM_ROWS * Wo][KC]
+  float* red = reinterpret_cast<float*>(smraw);                           // [4][KC][32], after the last tile
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nrb = (Ho + STEM_ROWS - 1) / STEM_ROWS;
+  const int t0 = blockIdx.x * per, t1 = min(ntiles, t0 + per);
+  const int W4 = W / 4;
+  if (tid < NR) pl[(tid * 3 + 2) * PP] = (__bf16)0.f;  // O'[0] = x[-1] (never written by the row stores)
+  Word iv[NR];
+  u32x4 dv[DCH];
+  int tile_npx = 0;
+  auto load = [&](int tile) {
+    const int rb = tile % nrb, n = tile / nrb;
+    const int oy0 = rb * STEM_ROWS, iy0 = 2 * oy0 - 1, npx = min(STEM_ROWS, Ho - oy0) * Wo;
+#pragma unroll
+    for (int row = 0; row < NR; ++row) {
+      const int c = row / IR, iy = iy0 + row % IR;
+      const bool ok = tid < W4 && iy >= 0 && iy < H;
+      if constexpr (sizeof(Word) == 4) iv[row] = ok ? *reinterpret_cast<const unsigned*>(img + (((long)n * 3 + c) * H + iy) * W + 4 * tid) : 0u;
+      else iv[row] = ok ? *reinterpret_cast<const f32x4*>(img + (((long)n * 3 + c) * H + iy) * W + 4 * tid) : (f32x4){0.f, 0.f, 0.f, 0.f};
+    }
+    const __bf16* dyb = dy + ((long)n * Ho + oy0) * Wo * (long)dcs;
+    const int nch = npx * KT * 2;
+#pragma unroll
+    for (int u = 0; u < DCH; ++u) {
+      const int i = tid + 256 * u;
+      dv[u] = i < nch ? ld16(dyb + (long)(i / (KT * 2)) * dcs + (i % (KT * 2)) * 8) : u32x4{0u, 0u, 0u, 0u};
+    }
+  };
+  auto store = [&]() {
+    if (tid < W4) {
+#pragma unroll
+      for (int row = 0; row < NR; ++row) {
+        const float x0 = stem_w(iv[row], 0), x1 = stem_w(iv[row], 1), x2 = stem_w(iv[row], 2), x3 = stem_w(iv[row], 3);
+        __bf16* b = pl + row * 3 * PP;
+        *reinterpret_cast<unsigned*>(b + 2 * tid) = pack_bf2(x0, x2);           // E[2q], E[2q+1]
+        *reinterpret_cast<unsigned*>(b + PP + 2 * tid) = pack_bf2(x1, x3);      // O[2q], O[2q+1]
+        b[2 * PP + 2 * tid + 1] = (__bf16)x1;                                   // O'[2q+1]
+        if (2 * tid + 2 < PP) b[2 * PP + 2 * tid + 2] = (__bf16)x3;             // O'[2q+2]
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < DCH; ++u) {
+      const int i = tid + 256 * u;
+      if (i < STEM_ROWS * Wo * KT * 2) *reinterpret_cast<u32x4*>(ds + (long)(i / (KT * 2)) * KC + (i % (KT * 2)) * 8) = dv[u];
+    }
+  };
+  const int g = lane >> 4, i = lane & 15, q4 = (lane & 15) >> 2, p4 = lane & 3;
+  // this lane's taps (B columns jt*16 + i): staged plane (row c*IR + ky, parity array) and validity
+  int jpl[2];
+  bool jok[2];
+#pragma unroll
+  for (int jt = 0; jt < 2; ++jt) {
+    const int j = jt * 16 + i;
+    jok[jt] = j < 27;
+    const int jj = jok[jt] ? j : 0, c = jj / 9, ky = (jj % 9) / 3, kx = jj % 3;
+    jpl[jt] = (c * IR + ky) * 3 + (kx == 1 ? 0 : kx == 2 ? 1 : 2);
+  }
+  f32x4 acc[KT][2];
+#pragma unroll
+  for (int t = 0; t < KT; ++t) acc[t][0] = acc[t][1] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  typedef __attribute__((ext_vector_type(4))) short s16x4;
+  if (t0 < t1) load(t0);
+  for (int tile = t0; tile < t1; ++tile) {
+    store();
+    __syncthreads();
+    if (tile + 1 < t1) load(tile + 1);
+    const int nsteps = STEM_ROWS * Wo / 32;  // a short last row pair reads zero dy rows
+    for (int s = wave; s < nsteps; s += 4) {
+      s16x4 a[KT][2];
+      uint2 b[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int p = s * 32 + 16 * h + 4 * g;  // first pixel of this lane group's block
+        // dy^T block: lane 4q + p4 addresses pixel p + q4, channels t*16 + 4 p4 .. +3
+#pragma unroll
+        for (int t = 0; t < KT; ++t)
+          a[t][h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (__attribute__((address_space(3))) s16x4*)(ds + (long)(p + q4) * KC + t * 16 + 4 * p4));
+        const int r = p / Wo, ox = p - r * Wo;
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt)
+          b[jt][h] = jok[jt] ? *reinterpret_cast<const uint2*>(pl + (jpl[jt] + 6 * r) * PP + ox) : uint2{0u, 0u};
+      }
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const s16x4 a0 = a[t][0], a1 = a[t][1];
+        const s16x8 av = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+#pragma unroll
+        for (int jt = 0; jt < 2; ++jt) {
+          const uint4 bv = {b[jt][0].x, b[jt][0].y, b[jt][1].x, b[jt][1].y};
+          acc[t][jt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<const bf16x8*>(&av),
+                                                               *reinterpret_cast<const bf16x8*>(&bv), acc[t][jt], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int jt = 0; jt < 2; ++jt)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) red[(wave * KC + t * 16 + 4 * g + rr) * 32 + jt * 16 + i] = acc[t][jt][rr];
+  __syncthreads();
+  for (int idx = tid; idx < KC * 32; idx += 256) {
+    const int M = KC * 32;
+    part[(long)blockIdx.x * M + idx] = (red[idx] + red[M + idx]) + (red[2 * M + idx] + red[3 * M + idx]);
+  }
+}
+
 static size_t stem_wgrad_smem(int Wp, int wseg, int KT) {
   const int IR = 2 * STEM_ROWS + 1;
   return (((size_t)3 * IR * Wp + 7) & ~(size_t)7) * 2 + (size_t)STEM_ROWS * wseg * KT * 16 * 2 +
@@ -460,6 +604,194 @@ __global__ void __launch_bounds__(256) stem_fwd_kernel(const TI* __restrict__ im
   }
 }
 
+// Forward on quad images (W % 4 == 0). The kernel above gathers the im2col operand from the staged bf16 rows with
+// eight 2-byte LDS reads per lane per 16 pixels and stages the rows with 2-byte writes: on the bs 64, 640^2 stem a
+// third of its wave cycles were LDS issue stalls (SQ_WAIT_INST_LDS, scripts/stem_micro.py). Here each staged input
+// row (c, iy) is stored as quads Q[row][ox] = (x = 2ox-1, 2ox, 2ox+1, 0): the three taps of output column ox in one
+// aligned 8-byte word, so the 27 (-> 32) reduction slots of a pixel are 9 quads (c, ky). A 16x16x32 step takes
+// quads (g, g+4) in lane group g (two 8-byte reads) and a second step quad 8 (lane group 0), so a lane reads 2-3
+// LDS words per 16 pixels; the staging writes 16 bytes per (row, output column pair). Rows of the quad image are
+// QP = 16 (mod 32) quads apart, so the two lane groups of each 32-lane half (rows an odd number apart) hit disjoint
+// banks. Wide images are walked in column segments of STEM_QSEG output columns. Output contract as above; the
+// statistics rows (adr_stem_fwd_tiles) hold per-block sums (see the end of the kernel), whose total is the same.
+constexpr int STEM_QSEG = 320;  // <= 512: one column pair per thread in the staging
+__host__ __device__ constexpr int stem_qp(int nox) { return (nox + 15) / 32 * 32 + 16; }
+
+// persistent: a block walks a contiguous range of units (tile = (image, output-row pair), column segment) — the
+// W^T fragments are built once per block, the next unit's image words are in flight (registers) while the current
+// one runs its MFMA steps, and consecutive tiles share their boundary input row in L2. The kernel is bound by
+// instruction issue (SQ_ACTIVE_INST_ANY ~ the wave lifetime: bs 64, 640^2, 91.6 M wave instructions for the row
+// kernel above, 61 M here at per-tile statistics), hence buffer loads / stores with out-of-range zeros instead of
+// branches, scalar step geometry, packed conversions, and one statistics reduction per block.
+template <int KT, typename TI>
+__global__ void __launch_bounds__(256) stem_fwd_q_kernel(const TI* __restrict__ img, int H, int W,
+                                                         const float* __restrict__ w, __bf16* __restrict__ y, int ycs,
+                                                         int Ho, int Wo, float* __restrict__ stats, int nunits, int per,
+                                                         int probe, int N) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
+  constexpr int IR = 2 * STEM_ROWS + 1, NR = 3 * IR;
+  typedef typename StemQWord<TI>::T Word;
+  const int segs = (Wo + STEM_QSEG - 1) / STEM_QSEG;
+  const int QP = stem_qp(Wo < STEM_QSEG ? Wo : STEM_QSEG);
+  uint2* Q = reinterpret_cast<uint2*>(smraw);  // [NR][QP]
+  __shared__ float red[4][2][KT * 16];
+  const int nrb = (Ho + STEM_ROWS - 1) / STEM_ROWS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, i = lane & 15;
+  const int u0 = blockIdx.x * per, u1 = min(nunits, u0 + per);
+  // A = W (16 k x 32 slots): lane (g, i) supplies output channel t*16 + i at slots 8g + e: quad g (e < 4) or g + 4
+  // (e >= 4), tap kx = e & 3 (kx 3 is the zero pad); the second step holds quad 8 in lane group 0
+  s16x8 bw[2][KT];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int q = h == 0 ? (e < 4 ? g : g + 4) : (g == 0 && e < 4 ? 8 : -1), kx = e & 3;
+      const bool ok = q >= 0 && kx < 3;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        const __bf16 v = (__bf16)(ok ? w[(t * 16 + i) * 27 + (q / 3) * 9 + (q % 3) * 3 + kx] : 0.f);
+        bw[h][t][e] = *reinterpret_cast<const short*>(&v);
+      }
+    }
+  // quad q = (c, ky) -> staged row c * IR + ky (+ 2 r for output row r of the pair)
+  auto qrow = [](int q) { return (q / 3) * IR + q % 3; };
+  const int rA = qrow(g) * QP, rB = qrow(g + 4) * QP, rC = qrow(8) * QP;
+  const __amdgpu_buffer_rsrc_t yrs =
+      __builtin_amdgcn_make_buffer_rsrc((void*)y, (short)0, N * Ho * Wo * ycs * 2, 0x00020000);
+  Word v[NR];
+  float lv[NR];  // the pixel at x - 1 of each row
+  // unit -> (image, first output row, column segment)
+  auto unit_geo = [&](int u, int& n, int& oy0, int& ox0) {
+    const int tile = u / segs;
+    ox0 = (u - tile * segs) * STEM_QSEG;
+    n = tile / nrb;
+    oy0 = (tile - n * nrb) * STEM_ROWS;
+  };
+  auto load = [&](int u) {
+    int n, oy0, ox0;
+    unit_geo(u, n, oy0, ox0);
+    const int x = 2 * (ox0 + 2 * tid), iy0 = 2 * oy0 - 1;
+    const bool tok = 2 * tid < min(STEM_QSEG, Wo - ox0) && !(probe & 2);
+    // buffer loads over image n: rows above / below the image, columns past the segment and x - 1 = -1 read
+    // out of range, which the hardware returns as zeros (no branch, no select)
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(img + (long)n * 3 * H * W), (short)0, 3 * H * W * (int)sizeof(TI),
+                                          0x00020000);
+    constexpr unsigned OOR = 0x7FFFFFF0u;
+#pragma unroll
+    for (int row = 0; row < NR; ++row) {
+      const int iy = iy0 + row % IR;
+      const bool rok = tok && (unsigned)iy < (unsigned)H;
+      const unsigned off = ((row / IR) * H + iy) * W + x;
+      const unsigned ob = rok ? off * (unsigned)sizeof(TI) : OOR;
+      const unsigned lb = rok && x > 0 ? (off - 1) * (unsigned)sizeof(TI) : OOR;
+      if constexpr (sizeof(Word) == 4) {
+        v[row] = __builtin_amdgcn_raw_buffer_load_b32(rs, ob, 0, 0);
+        lv[row] = img_val((uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rs, lb, 0, 0));
+      } else {
+        const u32x4 b = __builtin_amdgcn_raw_buffer_load_b128(rs, ob, 0, 0);
+        v[row] = *reinterpret_cast<const f32x4*>(&b);
+        lv[row] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, lb, 0, 0));
+      }
+    }
+  };
+  auto store = [&](int u) {
+    int n, oy0, ox0;
+    unit_geo(u, n, oy0, ox0);
+    if (2 * tid < min(STEM_QSEG, Wo - ox0)) {
+#pragma unroll
+      for (int row = 0; row < NR; ++row) {
+        const float x1 = stem_w(v[row], 1);
+        uint4 q;
+        q.x = pack_bf2(lv[row], stem_w(v[row], 0));
+        q.y = pack_bf2(x1, 0.f);
+        q.z = pack_bf2(x1, stem_w(v[row], 2));
+        q.w = pack_bf2(stem_w(v[row], 3), 0.f);
+        *reinterpret_cast<uint4*>(Q + row * QP + 2 * tid) = q;
+      }
+    }
+  };
+  float s1[KT][4], s2[KT][4];
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) s1[t][rr] = s2[t][rr] = 0.f;
+  if (u0 < u1) load(u0);
+  for (int u = u0; u < u1; ++u) {
+    int n, oy0, ox0;
+    unit_geo(u, n, oy0, ox0);
+    store(u);
+    __syncthreads();
+    if (u + 1 < u1) load(u + 1);
+    const int nrow = min(STEM_ROWS, Ho - oy0), nox = min(STEM_QSEG, Wo - ox0), npx = nrow * nox;
+    const int ybase = (((n * Ho + oy0) * Wo + ox0) * ycs + 4 * g) * 2;  // bytes, < 2^31 (checked by the launcher)
+    for (int st = wave; st * 16 < npx; st += 4) {
+      // the step's first pixel, row and column in scalar registers; a step crosses into the next row only when
+      // nox is not a multiple of 16
+      const int pb = st * 16, rs = pb / nox, os = pb - rs * nox;
+      int r = rs, ox = os + i;
+      if (nox & 15) {
+        if (ox >= nox) {
+          ox -= nox;
+          ++r;
+        }
+      }
+      const bool pok = pb + i < npx;
+      if (!pok) r = ox = 0;
+      const uint2* qb = Q + 2 * r * QP + ox;
+      const uint2 a0 = qb[rA], a1 = qb[rB];
+      uint2 a2 = {0u, 0u};
+      if (g == 0) a2 = qb[rC];
+      const uint4 b01 = {a0.x, a0.y, a1.x, a1.y}, b2 = {a2.x, a2.y, 0u, 0u};
+      const unsigned yo = pok && !(probe & 1) ? ybase + (r * Wo + ox) * ycs * 2 : 0x7FFFFFF0u;
+#pragma unroll
+      for (int t = 0; t < KT; ++t) {
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&bw[0][t]),
+                                                    *reinterpret_cast<const bf16x8*>(&b01), d, 0, 0, 0);
+        d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&bw[1][t]),
+                                                    *reinterpret_cast<const bf16x8*>(&b2), d, 0, 0, 0);
+        const unsigned lo = pack_bf2(d[0], d[1]), hi = pack_bf2(d[2], d[3]);
+        const float m = pok ? 1.f : 0.f;  // statistics of the stored pixels only
+        const float f0 = __uint_as_float(lo << 16) * m, f1 = __uint_as_float(lo & 0xFFFF0000u) * m;
+        const float f2 = __uint_as_float(hi << 16) * m, f3 = __uint_as_float(hi & 0xFFFF0000u) * m;
+        s1[t][0] += f0; s1[t][1] += f1; s1[t][2] += f2; s1[t][3] += f3;
+        s2[t][0] += f0 * f0; s2[t][1] += f1 * f1; s2[t][2] += f2 * f2; s2[t][3] += f3 * f3;
+        __builtin_amdgcn_raw_buffer_store_b64((u32x2s){lo, hi}, yrs, yo + t * 32, 0, 0);
+      }
+    }
+    __syncthreads();  // the quads are read before the next unit's store
+  }
+  // statistics: the block's sums (over all its tiles) in the row of its first tile, zeros in its other tiles' rows
+  // (the BatchNorm finalize sums every row of adr_stem_fwd_tiles)
+  if (!stats || u0 >= u1) return;
+#pragma unroll
+  for (int t = 0; t < KT; ++t)
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[t][rr] += __shfl_xor(s1[t][rr], o, 64);
+        s2[t][rr] += __shfl_xor(s2[t][rr], o, 64);
+      }
+      if (i == 0) {
+        red[wave][0][t * 16 + 4 * g + rr] = s1[t][rr];
+        red[wave][1][t * 16 + 4 * g + rr] = s2[t][rr];
+      }
+    }
+  __syncthreads();
+  const int tile0 = u0 / segs, tile1 = (u1 + segs - 1) / segs;
+  for (int idx = tid; idx < (tile1 - tile0) * 2 * KT * 16; idx += 256) {
+    float v = 0.f;
+    if (idx < 2 * KT * 16) {
+      const int q = idx / (KT * 16), k = idx % (KT * 16);
+      v = (red[0][q][k] + red[1][q][k]) + (red[2][q][k] + red[3][q][k]);
+    }
+    stats[(long)tile0 * 2 * KT * 16 + idx] = v;
+  }
+}
+
 // dw[k][j] (+)= sum_blocks part[b][k][j], j < 27 (the (K, 3, 3, 3) parameter layout)
 __global__ void __launch_bounds__(256) stem_wgrad_reduce_kernel(const float* __restrict__ part, int nblk, int K,
                                                                 float* dw, int accumulate) {
@@ -496,6 +828,31 @@ static int stem_fwd(const TI* img, int N, int H, int W, const float* w, int K, v
   ADR_REQUIRE(sm <= 64 * 1024, "stem_conv_fwd: W=%d too wide for the LDS plan", W);
   hipStream_t st = (hipStream_t)stream;
   const dim3 grid(adr_stem_fwd_tiles(N, Ho));
+  const char* qe = getenv("ADR_STEM_FWD_Q");  // A/B, read per call: 0 = the row-gather kernel
+  const char* pe = getenv("ADR_STEM_PROBE");  // diagnostics: 1 = no y stores, 2 = no image loads
+  const int probe = pe ? atoi(pe) : 0;
+  if (W % 4 == 0 && (!qe || atoi(qe))) {
+    const size_t qsm = (size_t)3 * (2 * STEM_ROWS + 1) * stem_qp(Wo < STEM_QSEG ? Wo : STEM_QSEG) * 8;
+    ADR_REQUIRE(qsm <= 64 * 1024 && 3l * H * W * (long)sizeof(TI) < (1l << 31) && 2l * N * Ho * Wo * ycs < (1l << 31),
+                "stem_conv_fwd: quad image %zu bytes / 32-bit buffer offsets", qsm);
+    const int nunits = (int)grid.x * ((Wo + STEM_QSEG - 1) / STEM_QSEG);
+    auto kern = K == 16 ? (const void*)stem_fwd_q_kernel<1, TI>
+                        : K == 32 ? (const void*)stem_fwd_q_kernel<2, TI> : (const void*)stem_fwd_q_kernel<4, TI>;
+    int occ = 1, dev = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, qsm) != hipSuccess || occ < 1) occ = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    // one resident round of blocks; whole tiles per block (a tile's statistics row sums all its column segments)
+    const int segs = (Wo + STEM_QSEG - 1) / STEM_QSEG;
+    const int per = ((int)grid.x + cus * occ - 1) / (cus * occ) * segs;
+    const dim3 qgrid((nunits + per - 1) / per);
+    if (K == 16)
+      hipLaunchKernelGGL((stem_fwd_q_kernel<1, TI>), qgrid, dim3(256), qsm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats, nunits, per, probe, N);
+    else if (K == 32)
+      hipLaunchKernelGGL((stem_fwd_q_kernel<2, TI>), qgrid, dim3(256), qsm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats, nunits, per, probe, N);
+    else
+      hipLaunchKernelGGL((stem_fwd_q_kernel<4, TI>), qgrid, dim3(256), qsm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats, nunits, per, probe, N);
+    return check_launch("adr_stem_conv_fwd");
+  }
   if (K == 16)
     hipLaunchKernelGGL((stem_fwd_kernel<1, TI>), grid, dim3(256), sm, st, img, H, W, w, (__bf16*)y, ycs, Ho, Wo, stats);
   else if (K == 32)
@@ -538,7 +895,26 @@ static int stem_wgrad(const TI* img, int N, int H, int W, const void* dy, int dc
   ADR_REQUIRE(sm <= 64 * 1024 && dcs % 8 == 0, "stem_conv_wgrad: W=%d too wide for the LDS plan", W);
   hipStream_t st = (hipStream_t)stream;
   int nblk = blocks;
-  if (segs == 1 && W % 4 == 0 && W <= STEM_LOOP_W) {  // persistent form: ~4 blocks per CU, contiguous tile ranges
+  const char* qe = getenv("ADR_STEM_WG_Q");  // A/B, read per call: 0 = the row-gather kernels
+  const size_t qsm_rows = (((size_t)3 * 3 * (2 * STEM_ROWS + 1) * (Wo + STEM_PP_PAD) + 7) & ~(size_t)7) * 2 +
+                          (size_t)STEM_ROWS * Wo * KT * 16 * 2;
+  const size_t qsm_red = (size_t)4 * KT * 16 * 32 * 4;
+  const size_t qsm = qsm_rows > qsm_red ? qsm_rows : qsm_red;
+  if (W % 32 == 0 && W <= STEM_LOOP_W && KT <= 2 && qsm <= 64 * 1024 && (!qe || atoi(qe))) {
+    auto kern = K == 16 ? (const void*)stem_wgrad_q_kernel<1, TI> : (const void*)stem_wgrad_q_kernel<2, TI>;
+    int occ = 1, dev = 0, cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, qsm) != hipSuccess || occ < 1) occ = 1;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int want = cus * (occ < 4 ? occ : 4);
+    const int per = (blocks + want - 1) / want;
+    nblk = (blocks + per - 1) / per;
+    if (K == 16)
+      hipLaunchKernelGGL((stem_wgrad_q_kernel<1, TI>), dim3(nblk), dim3(256), qsm, st, img, H, W, (const __bf16*)dy,
+                         dcs, Ho, Wo, blocks, per, ws);
+    else
+      hipLaunchKernelGGL((stem_wgrad_q_kernel<2, TI>), dim3(nblk), dim3(256), qsm, st, img, H, W, (const __bf16*)dy,
+                         dcs, Ho, Wo, blocks, per, ws);
+  } else if (segs == 1 && W % 4 == 0 && W <= STEM_LOOP_W) {  // persistent form: ~4 blocks per CU, contiguous tile ranges
     const size_t lsm = (((size_t)3 * (2 * STEM_ROWS + 1) * (W + 2) + 7) & ~(size_t)7) * 2 +
                        (size_t)STEM_ROWS * Wo * KT * 16 * 2;
     const size_t lsm_red = (size_t)4 * KT * 16 * 32 * 4;
