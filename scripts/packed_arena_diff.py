@@ -38,3 +38,7 @@ rows.sort(reverse=True)
 print(f"arena rel diff {sum(r[0] ** 2 for r in rows) ** 0.5:.3e}")
 for share, rel, n in rows[:25]:
     print(f"{share:.3e} of arena  rel {rel:.3e}  {n}")
+if "--all" in sys.argv:
+    for n in g0:
+        d = float((g1[n] - g0[n]).norm())
+        print(f"rel {d / max(float(g0[n].norm()), 1e-30):.2e}  |g| {float(g0[n].norm()):.3e}  {n}")

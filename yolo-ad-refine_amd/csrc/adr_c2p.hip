@@ -603,8 +603,14 @@ __global__ void adyt_alpha_kernel(const float* dan, const float* imp, int N, flo
 // Per-(image, head) block; threads = TPP tokens x LD lanes, a lane holding VW consecutive channels of the head
 // (D = LD * VW): every q/k/v/dout access is a 16-byte vector, per-token sums over d are LD-lane xor shuffles,
 // per-channel sums over tokens go through one LDS pass (chan_sum).
-// NTH = 1024 threads: one block per (image, head) walks all the tokens, and with 256 threads the passes were
-// load-latency bound (~7 GB/s per block: 64 - 128 blocks per launch); four times the loads in flight per block
+// NTH threads per block. 1024 (four times the loads in flight per image-head block) measured n-scale -0.13 ms,
+// l-scale -1.1 ms, and each kernel's outputs agree with the 256-thread kernels to fp32 rounding
+// (scripts/tssa_ab.py), but with them the fp32 gradient arena of the packed-head trainer test
+// (test_gpu_packed_head.py) drifted 200x further from the per-level loop (2.4e-4 vs 1.2e-6 relative, uniformly
+// over the backbone and neck, scripts/packed_arena_diff.py). Not explained; the launches stay at 256.
+#ifndef TSSA_NTH
+#define TSSA_NTH 256
+#endif
 template <typename T, int VW, int LD, int NTH = 1024>
 __global__ void __launch_bounds__(NTH) tssa_fwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok,
                                                        const float* temp, T* out, int ocs, int oimg, int heads,
@@ -1509,11 +1515,11 @@ extern "C" int adr_tssa_fwd(int dtype, const void* q, const void* k, const void*
   const size_t sm = Ntok * sizeof(float);
   ADR_REQUIRE(sm <= 64 * 1024, "tssa: Ntok=%d too large", Ntok);
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL((tssa_fwd_kernel<__bf16, 8, 8>), dim3(B * heads), dim3(1024), sm, st, (const __bf16*)q,
+    hipLaunchKernelGGL((tssa_fwd_kernel<__bf16, 8, 8, TSSA_NTH>), dim3(B * heads), dim3(TSSA_NTH), sm, st, (const __bf16*)q,
                        (const __bf16*)k, (const __bf16*)v, cs, Ntok, temp, (__bf16*)out, ocs, oimg, heads, Pi, ss,
                        attn);
   else
-    hipLaunchKernelGGL((tssa_fwd_kernel<float, 4, 16>), dim3(B * heads), dim3(1024), sm, st, (const float*)q,
+    hipLaunchKernelGGL((tssa_fwd_kernel<float, 4, 16, TSSA_NTH>), dim3(B * heads), dim3(TSSA_NTH), sm, st, (const float*)q,
                        (const float*)k, (const float*)v, cs, Ntok, temp, (float*)out, ocs, oimg, heads, Pi, ss, attn);
   return check_launch("adr_tssa_fwd");
 }
@@ -1529,11 +1535,11 @@ extern "C" int adr_tssa_bwd(int dtype, const void* q, const void* k, const void*
   const size_t sm = Ntok * sizeof(float);
   ADR_REQUIRE(sm <= 64 * 1024, "tssa_bwd: Ntok=%d too large", Ntok);
   if (dtype == ADR_BF16)
-    hipLaunchKernelGGL((tssa_bwd_kernel<__bf16, 8, 8>), dim3(B * heads), dim3(1024), sm, st, (const __bf16*)q,
+    hipLaunchKernelGGL((tssa_bwd_kernel<__bf16, 8, 8, TSSA_NTH>), dim3(B * heads), dim3(TSSA_NTH), sm, st, (const __bf16*)q,
                        (const __bf16*)k, (const __bf16*)v, cs, Ntok, temp, (const __bf16*)dout, dcs, dimg, heads, Pi,
                        ss, attn, (__bf16*)dq, (__bf16*)dk, (__bf16*)dv, gcs, ws);
   else
-    hipLaunchKernelGGL((tssa_bwd_kernel<float, 4, 16>), dim3(B * heads), dim3(1024), sm, st, (const float*)q,
+    hipLaunchKernelGGL((tssa_bwd_kernel<float, 4, 16, TSSA_NTH>), dim3(B * heads), dim3(TSSA_NTH), sm, st, (const float*)q,
                        (const float*)k, (const float*)v, cs, Ntok, temp, (const float*)dout, dcs, dimg, heads, Pi, ss,
                        attn, (float*)dq, (float*)dk, (float*)dv, gcs, ws);
   hipLaunchKernelGGL(tssa_temp_reduce_kernel, dim3(1), dim3(64), 0, st, ws, B, heads, dtemp);
