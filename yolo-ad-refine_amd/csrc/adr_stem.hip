@@ -353,7 +353,8 @@ __global__ void __launch_bounds__(256) stem_wgrad_loop_kernel(const TI* __restri
   }
 }
 
-// weight gradient, persistent, on deinterleaved rows (W % 32 == 0, W <= STEM_LOOP_W, K <= 32). The kernel above feeds
+// weight gradient, persistent, on deinterleaved rows (W % 4 == 0, tiles of two output rows x stem_wq_seg columns
+// dividing the row into multiples of 16). The kernel above feeds
 // each 16x16x32 step with 24 two-byte LDS reads per lane (eight dy values of one channel, sixteen im2col taps of
 // eight pixels); here both operands come from 8-byte reads:
 //   * dy^T (A: output channel x 32 pixels) by ds_read_b64_tr_b16 from the natural [pixel][K] dy image: lane group g
@@ -364,43 +365,60 @@ __global__ void __launch_bounds__(256) stem_wgrad_loop_kernel(const TI* __restri
 //     (kx = 1 / 2 / 0), the same pixels as the dy block.
 // The reduction slots of a step are permuted against the kernel above (the MFMA sums the same 32 products), so the
 // partials agree to fp32 rounding. Next-tile prefetch into registers and partials [block][KT*16][32] as above.
-constexpr int STEM_PP_PAD = 8;  // plane pitch Wo + 8: the 16 taps of a lane group spread over the banks
+constexpr int STEM_PP_PAD = 8;  // plane pitch wseg + 8: the 16 taps of a lane group spread over the banks
+// output columns per tile: the whole row at K 16 (n-scale 640^2: 320), 160-column segments at K 32 / 64 (the dy
+// slab of two rows x 160 columns x 64 channels is 40 KB)
+__host__ __device__ constexpr int stem_wq_seg(int KT) { return KT == 1 ? 320 : 160; }
 template <int KT, typename TI>
 __global__ void __launch_bounds__(256) stem_wgrad_q_kernel(const TI* __restrict__ img, int H, int W,
                                                            const __bf16* __restrict__ dy, int dcs, int Ho, int Wo,
                                                            int ntiles, int per, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smraw[];
-  constexpr int IR = 2 * STEM_ROWS + 1, NR = 3 * IR, KC = KT * 16;
-  constexpr int DCH = STEM_ROWS * (STEM_LOOP_W / 2) * KT * 2 / 256;  // 16-byte dy chunks per thread
+  constexpr int IR = 2 * STEM_ROWS + 1, NR = 3 * IR, KC = KT * 16, WSEG = stem_wq_seg(KT);
+  constexpr int DCH = STEM_ROWS * WSEG * KT * 2 / 256;  // 16-byte dy chunks per thread
   typedef typename StemWord<TI>::T Word;
-  const int PP = Wo + STEM_PP_PAD;
+  const int wseg = Wo < WSEG ? Wo : WSEG, segs = (Wo + wseg - 1) / wseg;  // the host checks Wo % wseg == 0
+  const int PP = wseg + STEM_PP_PAD;
   __bf16* pl = reinterpret_cast<__bf16*>(smraw);                          // [NR][3: E, O, O'][PP]
-  __bf16* ds = pl + ((NR * 3 * PP + 7) & ~7);                             // [STEM_ROWS * Wo][KC]
+  __bf16* ds = pl + ((NR * 3 * PP + 7) & ~7);                             // [STEM_ROWS * wseg][KC]
   float* red = reinterpret_cast<float*>(smraw);                           // [4][KC][32], after the last tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nrb = (Ho + STEM_ROWS - 1) / STEM_ROWS;
   const int t0 = blockIdx.x * per, t1 = min(ntiles, t0 + per);
-  const int W4 = W / 4;
-  if (tid < NR) pl[(tid * 3 + 2) * PP] = (__bf16)0.f;  // O'[0] = x[-1] (never written by the row stores)
+  const int W4 = wseg / 2;  // image words (4 pixels) per staged row of a segment
   Word iv[NR];
+  float lpx = 0.f;  // thread row < NR: the pixel left of the segment, x = 2 ox0 - 1 (O'[0])
   u32x4 dv[DCH];
-  int tile_npx = 0;
+  // tile -> (image, row pair, column segment)
+  auto geo = [&](int tile, int& n, int& oy0, int& ox0) {
+    const int seg = tile % segs, rt = tile / segs;
+    n = rt / nrb;
+    oy0 = (rt - n * nrb) * STEM_ROWS;
+    ox0 = seg * wseg;
+  };
   auto load = [&](int tile) {
-    const int rb = tile % nrb, n = tile / nrb;
-    const int oy0 = rb * STEM_ROWS, iy0 = 2 * oy0 - 1, npx = min(STEM_ROWS, Ho - oy0) * Wo;
+    int n, oy0, ox0;
+    geo(tile, n, oy0, ox0);
+    const int iy0 = 2 * oy0 - 1, nrow = min(STEM_ROWS, Ho - oy0);
+    const TI* imn = img + (long)n * 3 * H * W + 2 * ox0;
 #pragma unroll
     for (int row = 0; row < NR; ++row) {
       const int c = row / IR, iy = iy0 + row % IR;
       const bool ok = tid < W4 && iy >= 0 && iy < H;
-      if constexpr (sizeof(Word) == 4) iv[row] = ok ? *reinterpret_cast<const unsigned*>(img + (((long)n * 3 + c) * H + iy) * W + 4 * tid) : 0u;
-      else iv[row] = ok ? *reinterpret_cast<const f32x4*>(img + (((long)n * 3 + c) * H + iy) * W + 4 * tid) : (f32x4){0.f, 0.f, 0.f, 0.f};
+      if constexpr (sizeof(Word) == 4) iv[row] = ok ? *reinterpret_cast<const unsigned*>(imn + ((long)c * H + iy) * W + 4 * tid) : 0u;
+      else iv[row] = ok ? *reinterpret_cast<const f32x4*>(imn + ((long)c * H + iy) * W + 4 * tid) : (f32x4){0.f, 0.f, 0.f, 0.f};
     }
-    const __bf16* dyb = dy + ((long)n * Ho + oy0) * Wo * (long)dcs;
-    const int nch = npx * KT * 2;
+    if (tid < NR) {
+      const int c = tid / IR, iy = iy0 + tid % IR;
+      lpx = (ox0 > 0 && iy >= 0 && iy < H) ? img_val(imn[((long)c * H + iy) * W - 1]) : 0.f;
+    }
+    const __bf16* dyb = dy + (((long)n * Ho + oy0) * Wo + ox0) * (long)dcs;
+    const int nch = nrow * wseg * KT * 2;
 #pragma unroll
     for (int u = 0; u < DCH; ++u) {
-      const int i = tid + 256 * u;
-      dv[u] = i < nch ? ld16(dyb + (long)(i / (KT * 2)) * dcs + (i % (KT * 2)) * 8) : u32x4{0u, 0u, 0u, 0u};
+      const int i = tid + 256 * u, px = i / (KT * 2), pr = px / wseg;  // segment pixel -> (row, column)
+      dv[u] = i < nch ? ld16(dyb + ((long)pr * Wo + (px - pr * wseg)) * dcs + (i % (KT * 2)) * 8)
+                      : u32x4{0u, 0u, 0u, 0u};
     }
   };
   auto store = [&]() {
@@ -415,10 +433,11 @@ __global__ void __launch_bounds__(256) stem_wgrad_q_kernel(const TI* __restrict_
         if (2 * tid + 2 < PP) b[2 * PP + 2 * tid + 2] = (__bf16)x3;             // O'[2q+2]
       }
     }
+    if (tid < NR) pl[(tid * 3 + 2) * PP] = (__bf16)lpx;  // O'[0]
 #pragma unroll
     for (int u = 0; u < DCH; ++u) {
       const int i = tid + 256 * u;
-      if (i < STEM_ROWS * Wo * KT * 2) *reinterpret_cast<u32x4*>(ds + (long)(i / (KT * 2)) * KC + (i % (KT * 2)) * 8) = dv[u];
+      if (i < STEM_ROWS * wseg * KT * 2) *reinterpret_cast<u32x4*>(ds + (long)(i / (KT * 2)) * KC + (i % (KT * 2)) * 8) = dv[u];
     }
   };
   const int g = lane >> 4, i = lane & 15, q4 = (lane & 15) >> 2, p4 = lane & 3;
@@ -441,7 +460,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_q_kernel(const TI* __restrict_
     store();
     __syncthreads();
     if (tile + 1 < t1) load(tile + 1);
-    const int nsteps = STEM_ROWS * Wo / 32;  // a short last row pair reads zero dy rows
+    const int nsteps = STEM_ROWS * wseg / 32;  // a short last row pair reads zero dy rows
     for (int s = wave; s < nsteps; s += 4) {
       s16x4 a[KT][2];
       uint2 b[2][2];
@@ -453,7 +472,7 @@ __global__ void __launch_bounds__(256) stem_wgrad_q_kernel(const TI* __restrict_
         for (int t = 0; t < KT; ++t)
           a[t][h] = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
               (__attribute__((address_space(3))) s16x4*)(ds + (long)(p + q4) * KC + t * 16 + 4 * p4));
-        const int r = p / Wo, ox = p - r * Wo;
+        const int r = p / wseg, ox = p - r * wseg;
 #pragma unroll
         for (int jt = 0; jt < 2; ++jt)
           b[jt][h] = jok[jt] ? *reinterpret_cast<const uint2*>(pl + (jpl[jt] + 6 * r) * PP + ox) : uint2{0u, 0u};
@@ -896,24 +915,32 @@ static int stem_wgrad(const TI* img, int N, int H, int W, const void* dy, int dc
   hipStream_t st = (hipStream_t)stream;
   int nblk = blocks;
   const char* qe = getenv("ADR_STEM_WG_Q");  // A/B, read per call: 0 = the row-gather kernels
-  const size_t qsm_rows = (((size_t)3 * 3 * (2 * STEM_ROWS + 1) * (Wo + STEM_PP_PAD) + 7) & ~(size_t)7) * 2 +
-                          (size_t)STEM_ROWS * Wo * KT * 16 * 2;
+  const int qseg = Wo < stem_wq_seg(KT) ? Wo : stem_wq_seg(KT);
+  const size_t qsm_rows = (((size_t)3 * 3 * (2 * STEM_ROWS + 1) * (qseg + STEM_PP_PAD) + 7) & ~(size_t)7) * 2 +
+                          (size_t)STEM_ROWS * qseg * KT * 16 * 2;
   const size_t qsm_red = (size_t)4 * KT * 16 * 32 * 4;
   const size_t qsm = qsm_rows > qsm_red ? qsm_rows : qsm_red;
-  if (W % 32 == 0 && W <= STEM_LOOP_W && KT <= 2 && qsm <= 64 * 1024 && (!qe || atoi(qe))) {
-    auto kern = K == 16 ? (const void*)stem_wgrad_q_kernel<1, TI> : (const void*)stem_wgrad_q_kernel<2, TI>;
+  // whole 32-pixel steps per tile, 4-pixel runs within a row, 16-byte image words per thread pair
+  if (W % 4 == 0 && Wo % qseg == 0 && qseg % 16 == 0 && qsm <= 64 * 1024 && (!qe || atoi(qe))) {
+    const int qtiles = N * ((Ho + STEM_ROWS - 1) / STEM_ROWS) * (Wo / qseg);
+    auto kern = K == 16 ? (const void*)stem_wgrad_q_kernel<1, TI>
+                        : K == 32 ? (const void*)stem_wgrad_q_kernel<2, TI> : (const void*)stem_wgrad_q_kernel<4, TI>;
     int occ = 1, dev = 0, cus = 256;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, kern, 256, qsm) != hipSuccess || occ < 1) occ = 1;
     if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int want = cus * (occ < 4 ? occ : 4);
-    const int per = (blocks + want - 1) / want;
-    nblk = (blocks + per - 1) / per;
+    const int per = (qtiles + want - 1) / want;
+    nblk = (qtiles + per - 1) / per;
+    ADR_REQUIRE((size_t)nblk * K * 32 * sizeof(float) <= ws_bytes, "stem_conv_wgrad: workspace");
     if (K == 16)
       hipLaunchKernelGGL((stem_wgrad_q_kernel<1, TI>), dim3(nblk), dim3(256), qsm, st, img, H, W, (const __bf16*)dy,
-                         dcs, Ho, Wo, blocks, per, ws);
-    else
+                         dcs, Ho, Wo, qtiles, per, ws);
+    else if (K == 32)
       hipLaunchKernelGGL((stem_wgrad_q_kernel<2, TI>), dim3(nblk), dim3(256), qsm, st, img, H, W, (const __bf16*)dy,
-                         dcs, Ho, Wo, blocks, per, ws);
+                         dcs, Ho, Wo, qtiles, per, ws);
+    else
+      hipLaunchKernelGGL((stem_wgrad_q_kernel<4, TI>), dim3(nblk), dim3(256), qsm, st, img, H, W, (const __bf16*)dy,
+                         dcs, Ho, Wo, qtiles, per, ws);
   } else if (segs == 1 && W % 4 == 0 && W <= STEM_LOOP_W) {  // persistent form: ~4 blocks per CU, contiguous tile ranges
     const size_t lsm = (((size_t)3 * (2 * STEM_ROWS + 1) * (W + 2) + 7) & ~(size_t)7) * 2 +
                        (size_t)STEM_ROWS * Wo * KT * 16 * 2;
