@@ -611,6 +611,16 @@ __global__ void adyt_alpha_kernel(const float* dan, const float* imp, int N, flo
 #ifndef TSSA_NTH
 #define TSSA_NTH 256
 #endif
+// Instead, each thread issues the 16-byte loads of TSSA_U of its tokens before using any (the same tokens, the same
+// per-thread order of the sums: bitwise the one-token loop), for the same loads-in-flight at 256 threads.
+constexpr int TSSA_U = 4;
+template <typename T, int VW>
+__device__ __forceinline__ void vdecode(const u32x4& v, float* f) {
+  static_assert(VW * sizeof(T) == 16, "16-byte token rows");
+  const T* e = reinterpret_cast<const T*>(&v);
+#pragma unroll
+  for (int i = 0; i < VW; ++i) f[i] = to_f(e[i]);
+}
 template <typename T, int VW, int LD, int NTH = 1024>
 __global__ void __launch_bounds__(NTH) tssa_fwd_kernel(const T* q, const T* k, const T* v, int cs, int Ntok,
                                                        const float* temp, T* out, int ocs, int oimg, int heads,
@@ -626,9 +636,17 @@ __global__ void __launch_bounds__(NTH) tssa_fwd_kernel(const T* q, const T* k, c
   const float tp = temp[h];
   // pass 1: ss = sum_d (q / max(|q|, eps))^2 and the logits
   float mx = -INFINITY;
-  for (int n = r0; n < Ntok; n += TPP) {
+  for (int n0 = r0; n0 < Ntok; n0 += TSSA_U * TPP) {
+  u32x4 qr[TSSA_U];
+#pragma unroll
+  for (int u = 0; u < TSSA_U; ++u)
+    if (n0 + u * TPP < Ntok) qr[u] = ld16(q + (base + n0 + u * TPP) * cs + c0);
+#pragma unroll
+  for (int u = 0; u < TSSA_U; ++u) {
+    const int n = n0 + u * TPP;
+    if (n >= Ntok) continue;
     float qv[VW];
-    vload<T, VW>(q + (base + n) * cs + c0, qv);
+    vdecode<T, VW>(qr[u], qv);
     float s2 = 0.f;
 #pragma unroll
     for (int e = 0; e < VW; ++e) s2 += qv[e] * qv[e];
@@ -645,6 +663,7 @@ __global__ void __launch_bounds__(NTH) tssa_fwd_kernel(const T* q, const T* k, c
       Pi[n] = ss * tp;
     }
     mx = fmaxf(mx, ss * tp);
+  }
   }
   sh[threadIdx.x] = mx;
   __syncthreads();
@@ -670,11 +689,20 @@ __global__ void __launch_bounds__(NTH) tssa_fwd_kernel(const T* q, const T* k, c
   float p[VW];
 #pragma unroll
   for (int e = 0; e < VW; ++e) p[e] = 0.f;
-  for (int n = r0; n < Ntok; n += TPP) {
-    float kv[VW];
-    vload<T, VW>(k + (base + n) * cs + c0, kv);
+  for (int n0 = r0; n0 < Ntok; n0 += TSSA_U * TPP) {
+    u32x4 kr[TSSA_U];
 #pragma unroll
-    for (int e = 0; e < VW; ++e) p[e] += Pi[n] * kv[e] * kv[e];
+    for (int u = 0; u < TSSA_U; ++u)
+      if (n0 + u * TPP < Ntok) kr[u] = ld16(k + (base + n0 + u * TPP) * cs + c0);
+#pragma unroll
+    for (int u = 0; u < TSSA_U; ++u) {
+      const int n = n0 + u * TPP;
+      if (n >= Ntok) continue;
+      float kv[VW];
+      vdecode<T, VW>(kr[u], kv);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) p[e] += Pi[n] * kv[e] * kv[e];
+    }
   }
   chan_sum<VW, LD, NTH>(p, red, at);
   if (threadIdx.x < D) {
@@ -684,12 +712,21 @@ __global__ void __launch_bounds__(NTH) tssa_fwd_kernel(const T* q, const T* k, c
   }
   __syncthreads();
   // pass 3: out = -v * Pi * attn
-  for (int n = r0; n < Ntok; n += TPP) {
-    float vv[VW];
-    vload<T, VW>(v + (base + n) * cs + c0, vv);
+  for (int n0 = r0; n0 < Ntok; n0 += TSSA_U * TPP) {
+    u32x4 vr[TSSA_U];
 #pragma unroll
-    for (int e = 0; e < VW; ++e) vv[e] = -vv[e] * Pi[n] * at[lane * VW + e];
-    vstore<T, VW>(out + ((long)b * oimg + n) * ocs + c0, vv);
+    for (int u = 0; u < TSSA_U; ++u)
+      if (n0 + u * TPP < Ntok) vr[u] = ld16(v + (base + n0 + u * TPP) * cs + c0);
+#pragma unroll
+    for (int u = 0; u < TSSA_U; ++u) {
+      const int n = n0 + u * TPP;
+      if (n >= Ntok) continue;
+      float vv[VW];
+      vdecode<T, VW>(vr[u], vv);
+#pragma unroll
+      for (int e = 0; e < VW; ++e) vv[e] = -vv[e] * Pi[n] * at[lane * VW + e];
+      vstore<T, VW>(out + ((long)b * oimg + n) * ocs + c0, vv);
+    }
   }
 }
 
@@ -717,10 +754,21 @@ __global__ void __launch_bounds__(NTH) tssa_bwd_kernel(const T* q, const T* k, c
   float p[VW];
 #pragma unroll
   for (int e = 0; e < VW; ++e) p[e] = 0.f;
-  for (int n = r0; n < Ntok; n += TPP) {
+  for (int n0 = r0; n0 < Ntok; n0 += TSSA_U * TPP) {
+  u32x4 gr[TSSA_U], vr[TSSA_U];
+#pragma unroll
+  for (int u = 0; u < TSSA_U; ++u)
+    if (n0 + u * TPP < Ntok) {
+      gr[u] = ld16(dout + ((long)b * dimg + n0 + u * TPP) * dcs + c0);
+      vr[u] = ld16(v + (base + n0 + u * TPP) * cs + c0);
+    }
+#pragma unroll
+  for (int u = 0; u < TSSA_U; ++u) {
+    const int n = n0 + u * TPP;
+    if (n >= Ntok) continue;
     float g[VW], vv[VW], o[VW];
-    vload<T, VW>(dout + ((long)b * dimg + n) * dcs + c0, g);
-    vload<T, VW>(v + (base + n) * cs + c0, vv);
+    vdecode<T, VW>(gr[u], g);
+    vdecode<T, VW>(vr[u], vv);
     const float pn = Pi[n];
 #pragma unroll
     for (int e = 0; e < VW; ++e) {
@@ -729,16 +777,29 @@ __global__ void __launch_bounds__(NTH) tssa_bwd_kernel(const T* q, const T* k, c
     }
     vstore<T, VW>(dv + (base + n) * gcs + c0, o);
   }
+  }
   chan_sum<VW, LD, NTH>(p, red, dd);
   if (threadIdx.x < D) dd[threadIdx.x] = -dd[threadIdx.x] * attn[threadIdx.x] * attn[threadIdx.x];  // ddots
   __syncthreads();
   // dPi[n] = sum_d (-dout v attn + ddots k^2) ; dk = ddots * Pi * 2k
   float part = 0.f;
-  for (int n = r0; n < Ntok; n += TPP) {
+  for (int n0 = r0; n0 < Ntok; n0 += TSSA_U * TPP) {
+  u32x4 gr[TSSA_U], vr[TSSA_U], kr[TSSA_U];
+#pragma unroll
+  for (int u = 0; u < TSSA_U; ++u)
+    if (n0 + u * TPP < Ntok) {
+      gr[u] = ld16(dout + ((long)b * dimg + n0 + u * TPP) * dcs + c0);
+      vr[u] = ld16(v + (base + n0 + u * TPP) * cs + c0);
+      kr[u] = ld16(k + (base + n0 + u * TPP) * cs + c0);
+    }
+#pragma unroll
+  for (int u = 0; u < TSSA_U; ++u) {
+    const int n = n0 + u * TPP;
+    if (n >= Ntok) continue;
     float g[VW], vv[VW], kv[VW], o[VW];
-    vload<T, VW>(dout + ((long)b * dimg + n) * dcs + c0, g);
-    vload<T, VW>(v + (base + n) * cs + c0, vv);
-    vload<T, VW>(k + (base + n) * cs + c0, kv);
+    vdecode<T, VW>(gr[u], g);
+    vdecode<T, VW>(vr[u], vv);
+    vdecode<T, VW>(kr[u], kv);
     const float pn = Pi[n];
     float sp = 0.f;
 #pragma unroll
@@ -754,15 +815,24 @@ __global__ void __launch_bounds__(NTH) tssa_bwd_kernel(const T* q, const T* k, c
       part += pn * s;
     }
   }
+  }
   const float dot = block_sum<NTH>(part, sh);
   // softmax backward -> dl ; dtemp partial ; dss -> dq
   float tpart = 0.f;
-  for (int n = r0; n < Ntok; n += TPP) {
+  for (int n0 = r0; n0 < Ntok; n0 += TSSA_U * TPP) {
+  u32x4 qr[TSSA_U];
+#pragma unroll
+  for (int u = 0; u < TSSA_U; ++u)
+    if (n0 + u * TPP < Ntok) qr[u] = ld16(q + (base + n0 + u * TPP) * cs + c0);
+#pragma unroll
+  for (int u = 0; u < TSSA_U; ++u) {
+    const int n = n0 + u * TPP;
+    if (n >= Ntok) continue;
     const float dl = Pi[n] * (dPi[n] - dot);
     if (lane == 0) tpart += dl * ss[n];
     const float dss = dl * tp;
     float qv[VW];
-    vload<T, VW>(q + (base + n) * cs + c0, qv);
+    vdecode<T, VW>(qr[u], qv);
     float s2 = 0.f;
 #pragma unroll
     for (int e = 0; e < VW; ++e) s2 += qv[e] * qv[e];
@@ -780,6 +850,7 @@ __global__ void __launch_bounds__(NTH) tssa_bwd_kernel(const T* q, const T* k, c
       o[e] = dqn / r - (nrm > 1e-12f ? qv[e] * qdq / (r * r * r) : 0.f);
     }
     vstore<T, VW>(dq + (base + n) * gcs + c0, o);
+  }
   }
   tpart = block_sum<NTH>(tpart, sh);
   if (threadIdx.x == 0) dtemp_part[bh] = tpart;
