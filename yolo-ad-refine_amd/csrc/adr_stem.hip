@@ -745,7 +745,36 @@ __global__ void __launch_bounds__(256) stem_fwd_q_kernel(const TI* __restrict__ 
     if (u + 1 < u1) load(u + 1);
     const int nrow = min(STEM_ROWS, Ho - oy0), nox = min(STEM_QSEG, Wo - ox0), npx = nrow * nox;
     const int ybase = (((n * Ho + oy0) * Wo + ox0) * ycs + 4 * g) * 2;  // bytes, < 2^31 (checked by the launcher)
-    for (int st = wave; st * 16 < npx; st += 4) {
+    // fast path (every row a multiple of 64 columns, all pixels valid): blocks of 64 pixels of one row per wave,
+    // four 16-pixel steps whose LDS and store addresses differ by immediates, no validity masks
+    const int nb64 = (nox & 63) || (probe & 1) ? 0 : npx / 64;
+    for (int blk = wave; blk < nb64; blk += 4) {
+      const int pb = blk * 64, r = pb / nox, oxb = pb - r * nox;  // scalar
+      const uint2* qb = Q + 2 * r * QP + oxb + i;
+      const unsigned yo = ybase + ((r * Wo + oxb + i) * ycs) * 2;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint2 a0 = qb[rA + 16 * j], a1 = qb[rB + 16 * j];
+        uint2 a2 = {0u, 0u};
+        if (g == 0) a2 = qb[rC + 16 * j];
+        const uint4 b01 = {a0.x, a0.y, a1.x, a1.y}, b2 = {a2.x, a2.y, 0u, 0u};
+#pragma unroll
+        for (int t = 0; t < KT; ++t) {
+          f32x4 d = {0.f, 0.f, 0.f, 0.f};
+          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&bw[0][t]),
+                                                      *reinterpret_cast<const bf16x8*>(&b01), d, 0, 0, 0);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*reinterpret_cast<bf16x8*>(&bw[1][t]),
+                                                      *reinterpret_cast<const bf16x8*>(&b2), d, 0, 0, 0);
+          const unsigned lo = pack_bf2(d[0], d[1]), hi = pack_bf2(d[2], d[3]);
+          const float f0 = __uint_as_float(lo << 16), f1 = __uint_as_float(lo & 0xFFFF0000u);
+          const float f2 = __uint_as_float(hi << 16), f3 = __uint_as_float(hi & 0xFFFF0000u);
+          s1[t][0] += f0; s1[t][1] += f1; s1[t][2] += f2; s1[t][3] += f3;
+          s2[t][0] += f0 * f0; s2[t][1] += f1 * f1; s2[t][2] += f2 * f2; s2[t][3] += f3 * f3;
+          __builtin_amdgcn_raw_buffer_store_b64((u32x2s){lo, hi}, yrs, yo, 16 * j * ycs * 2 + t * 32, 0);
+        }
+      }
+    }
+    for (int st = nb64 ? npx / 16 : wave; st * 16 < npx; st += 4) {
       // the step's first pixel, row and column in scalar registers; a step crosses into the next row only when
       // nox is not a multiple of 16
       const int pb = st * 16, rs = pb / nox, os = pb - rs * nox;
