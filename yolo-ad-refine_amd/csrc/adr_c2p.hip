@@ -607,12 +607,13 @@ __global__ void adyt_alpha_kernel(const float* dan, const float* imp, int N, flo
 // l-scale -1.1 ms, and each kernel's outputs agree with the 256-thread kernels to fp32 rounding
 // (scripts/tssa_ab.py), but with them the fp32 gradient arena of the packed-head trainer test
 // (test_gpu_packed_head.py) drifted 200x further from the per-level loop (2.4e-4 vs 1.2e-6 relative, uniformly
-// over the backbone and neck, scripts/packed_arena_diff.py). Not explained; the launches stay at 256.
+// over the backbone and neck, scripts/packed_arena_diff.py); at 512 it is 1.1e-6. Not explained; the launches run
+// 512 threads.
 #ifndef TSSA_NTH
-#define TSSA_NTH 256
+#define TSSA_NTH 512
 #endif
-// Instead, each thread issues the 16-byte loads of TSSA_U of its tokens before using any (the same tokens, the same
-// per-thread order of the sums: bitwise the one-token loop), for the same loads-in-flight at 256 threads.
+// Each thread also issues the 16-byte loads of TSSA_U of its tokens before using any (the same tokens, the same
+// per-thread order of the sums: bitwise the one-token loop).
 constexpr int TSSA_U = 4;
 template <typename T, int VW>
 __device__ __forceinline__ void vdecode(const u32x4& v, float* f) {
