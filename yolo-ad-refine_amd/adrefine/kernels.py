@@ -20,11 +20,13 @@ from .native import ConvDesc, lib
 F32, BF16 = 0, 1
 ACT = {"none": 0, "silu": 1, "gelu": 2, "relu": 3, "sigmoid": 4, "hswish": 5}
 _NC_MIN_BLOCKS = int(__import__("os").environ.get("ADR_NC_MIN_BLOCKS", 512))
-_NC_ROWS = int(__import__("os").environ.get("ADR_NC_ROWS", 256))
+# 1024 rows per chunk (was 256): fewer partial rows for the finalize kernels to walk; same-box sweep (4 runs each,
+# scripts/ab_sweep.sh r06cb): 256 -> 19.54, 512 -> 19.50, 1024 -> 19.48 ms/step
+_NC_ROWS = int(__import__("os").environ.get("ADR_NC_ROWS", 1024))
 
 
 def _stats_rows(N, HW):
-    """Rows per adr_nc_reduce chunk: 256 (ADR_NC_ROWS), shrunk (in multiples of 32) on small maps until the
+    """Rows per adr_nc_reduce chunk: 1024 (ADR_NC_ROWS), shrunk (in multiples of 32) on small maps until the
     reduction grid has ~_NC_MIN_BLOCKS workgroups — at 20x20 a 256-row chunk leaves 128 workgroups for the
     whole chip."""
     rows = _NC_ROWS
