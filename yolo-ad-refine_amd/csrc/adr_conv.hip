@@ -1644,6 +1644,16 @@ static ConvPlan conv_plan(const adr_conv_desc* d, bool dgrad, bool xf = false) {
   // better than 128-wide ones (2 waves/SIMD), at the cost of reading the A rows once per column tile (L2 hits).
   // XF kernels are single-buffered: at most 64 columns.
   p.bn = p.tw ? conv3_bn(out) : ((d->r * d->s == 1 || xf) && out > 64) ? 64 : conv_pick_bn(out);
+  {
+    // the 128-wide double-buffered tile runs two workgroups per CU; when its grid is under two such rounds of the
+    // chip (the n-scale 80^2 -> 40^2 / 40^2 -> 20^2 stride-2 convs: 800 / 200 workgroups), the 64-wide tile's
+    // four per CU fill it better. ADR_CONV_BN_MAX: A/B override (128 = never narrow, 64 = always)
+    const char* e = getenv("ADR_CONV_BN_MAX");
+    const int cap = e ? atoi(e) : 0;
+    const long rows = dgrad ? (long)d->n * d->h * d->w : (long)d->n * d->ho * d->wo;
+    const long grid128 = (rows + CBM - 1) / CBM * ((out + 127) / 128);
+    if (!p.tw && p.bn == 128 && (cap ? cap < 128 : grid128 < 1024)) p.bn = cap ? (cap >= 16 ? cap : 64) : 64;
+  }
   p.kt = 0;
   const bool c1 = !p.tw && p.mode != CV_DGRAD2 && d->r == 1 && d->s == 1 && d->stride_h == 1 && d->pad_h == 0 &&
                   d->pad_w == 0 && conv1_enabled();
