@@ -16,9 +16,10 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(autouse=True)
 def _xf_everywhere(monkeypatch):
     """The engine declines the XF data gradient where it measured slower (the per-tile engine instead of the
-    streaming 1x1 kernel, DG2H; adr_conv2d_bf16_xf_reuse). Those fused kernels stay correct and tested: take them."""
+    streaming 1x1 kernel, DG2H, the 3x3 halo tiles; adr_conv2d_bf16_xf_reuse). Those fused kernels stay correct and tested: take them."""
     monkeypatch.setenv("ADR_XF_STREAM", "1")
     monkeypatch.setenv("ADR_XF_DG2", "1")
+    monkeypatch.setenv("ADR_XF_CONV3", "1")
 
 
 @pytest.fixture(autouse=True)

@@ -27,6 +27,7 @@ def _xf_everywhere(monkeypatch):
     declines by default (adr_conv2d_bf16_xf_reuse)."""
     monkeypatch.setenv("ADR_XF_STREAM", "1")
     monkeypatch.setenv("ADR_XF_DG2", "1")
+    monkeypatch.setenv("ADR_XF_CONV3", "1")
 
 
 def _nhwc(t):

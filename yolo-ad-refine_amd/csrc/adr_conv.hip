@@ -1850,14 +1850,15 @@ extern "C" int adr_conv2d_bf16_xf_reuse(const adr_conv_desc* d, int dgrad) {
     // an XF data gradient that would leave the streaming 1x1 kernel for the per-tile engine is latency-bound on the
     // large thin maps (e.g. 160^2 x 32 -> 48: 187 us fused against ~70 us for the BN-act pass + streaming dgrad)
     // and so is the stride-2 halo-tile one on the stem-side maps (320^2 x 16 <- 160^2 x 32: 291 us fused, the BN-act
-    // pass + plain DG2H are faster; same-box step A/B 20.93 -> 20.83 ms). ADR_XF_STREAM / ADR_XF_DG2 / ADR_XF_CONV3
-    // = 1 keep the fusion there (A/B only).
+    // pass + plain DG2H are faster; same-box step A/B 20.93 -> 20.83 ms), and since round 6 the 3x3 halo-tile one too
+    // (l-scale 111.2 -> 110.6 ms same box, n-scale neutral). ADR_XF_STREAM / ADR_XF_DG2 / ADR_XF_CONV3 = 1 keep the
+    // fusion there (A/B, tests).
     const char* es = getenv("ADR_XF_STREAM");
     const char* eg = getenv("ADR_XF_DG2");
     const char* e3 = getenv("ADR_XF_CONV3");
     if (!(es && atoi(es)) && conv_plan(d, true, false).kt > 0 && pl.kt == 0) return 1 << 20;
     if (!(eg && atoi(eg)) && pl.dg2) return 1 << 20;
-    if (e3 && !atoi(e3) && pl.tw) return 1 << 20;
+    if (!(e3 && atoi(e3)) && pl.tw) return 1 << 20;
   }
   const int out = dgrad ? d->c : d->k;
   const int nt = pl.tw ? out / pl.bn : cdiv(out, pl.bn);
