@@ -614,7 +614,10 @@ __global__ void adyt_alpha_kernel(const float* dan, const float* imp, int N, flo
 #endif
 // Each thread also issues the 16-byte loads of TSSA_U of its tokens before using any (the same tokens, the same
 // per-thread order of the sums: bitwise the one-token loop).
-constexpr int TSSA_U = 4;
+#ifndef TSSA_LOADS
+#define TSSA_LOADS 4
+#endif
+constexpr int TSSA_U = TSSA_LOADS;
 template <typename T, int VW>
 __device__ __forceinline__ void vdecode(const u32x4& v, float* f) {
   static_assert(VW * sizeof(T) == 16, "16-byte token rows");
