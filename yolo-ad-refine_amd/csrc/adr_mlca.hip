@@ -228,7 +228,12 @@ __global__ void __launch_bounds__(256) mlca_bwd_bins_kernel(const T* y, int ycs,
 }
 
 // bwd2: one block per image -> dlocal [N][25][C]; per-image weight grads dwl_part/dwg_part [N][k]
-__global__ void __launch_bounds__(256) mlca_att_bwd_kernel(const float* local, const float* datt, const float* sig_l,
+// MLCA_NT threads: one block per image walks all 25 x C bins (16 blocks at l-scale), so wider blocks put more
+// loads in flight
+#ifndef MLCA_NT
+#define MLCA_NT 512
+#endif
+__global__ void __launch_bounds__(MLCA_NT) mlca_att_bwd_kernel(const float* local, const float* datt, const float* sig_l,
                                                            const float* sig_g, const float* S, int N, int C,
                                                            const float* wl, const float* wg, int k, float lw,
                                                            float* dlocal, float* dwl_part, float* dwg_part) {
@@ -242,8 +247,8 @@ __global__ void __launch_bounds__(256) mlca_att_bwd_kernel(const float* local, c
   float* dyg = sm;                 // C   : d(pre-sigmoid global)
   float* g = sm + C;               // C   : global means
   float* dyl = sm + 2 * C;         // L_len : d(pre-sigmoid local seq)
-  float* red = sm + 2 * C + L_len; // 256*2*k scratch
-  for (int c = threadIdx.x; c < C; c += 256) {
+  float* red = sm + 2 * C + L_len; // 2 * MLCA_NT scratch
+  for (int c = threadIdx.x; c < C; c += MLCA_NT) {
     float m = 0.f;
     for (int p = 0; p < LS * LS; ++p) m += L[p * C + c];
     // d sig_g[n][c] = (1-lw) * sum over bins i whose batch-row window holds n of S[i][c] / |rows(i)|
@@ -256,7 +261,7 @@ __global__ void __launch_bounds__(256) mlca_att_bwd_kernel(const float* local, c
     dyg[c] = (1.f - lw) * s * sgv * (1.f - sgv);
     g[c] = m / (float)(LS * LS);
   }
-  for (int idx = threadIdx.x; idx < L_len; idx += 256) {
+  for (int idx = threadIdx.x; idx < L_len; idx += MLCA_NT) {
     float s = SL[idx];
     dyl[idx] = lw * D[idx] * s * (1.f - s);
   }
@@ -264,32 +269,32 @@ __global__ void __launch_bounds__(256) mlca_att_bwd_kernel(const float* local, c
   // weight grads: dwl[t] = sum_i dyl[i] * L[i + t - pad] ; dwg[t] = sum_c dyg[c] * g[c + t - pad]
   for (int t = 0; t < k; ++t) {
     float a = 0.f, b = 0.f;
-    for (int i = threadIdx.x; i < L_len; i += 256) {
+    for (int i = threadIdx.x; i < L_len; i += MLCA_NT) {
       int q = i + t - pad;
       if (q >= 0 && q < L_len) a += dyl[i] * L[q];
     }
-    for (int c = threadIdx.x; c < C; c += 256) {
+    for (int c = threadIdx.x; c < C; c += MLCA_NT) {
       int q = c + t - pad;
       if (q >= 0 && q < C) b += dyg[c] * g[q];
     }
     red[threadIdx.x] = a;
-    red[256 + threadIdx.x] = b;
+    red[MLCA_NT + threadIdx.x] = b;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
+    for (int o = MLCA_NT / 2; o > 0; o >>= 1) {
       if (threadIdx.x < o) {
         red[threadIdx.x] += red[threadIdx.x + o];
-        red[256 + threadIdx.x] += red[256 + threadIdx.x + o];
+        red[MLCA_NT + threadIdx.x] += red[MLCA_NT + threadIdx.x + o];
       }
       __syncthreads();
     }
     if (threadIdx.x == 0) {  // rows [n][2][k]: the local conv's in half 0, the global conv's in half 1
       dwl_part[((long)n * 2 + 0) * k + t] = red[0];
-      dwl_part[((long)n * 2 + 1) * k + t] = red[256];
+      dwl_part[((long)n * 2 + 1) * k + t] = red[MLCA_NT];
     }
     __syncthreads();
   }
   // dlocal[q] = sum_t wl[t] * dyl[q - t + pad] + dg[c]/25 with dg[c] = sum_t wg[t] * dyg[c - t + pad]
-  for (int q = threadIdx.x; q < L_len; q += 256) {
+  for (int q = threadIdx.x; q < L_len; q += MLCA_NT) {
     float s = 0.f;
     for (int t = 0; t < k; ++t) {
       int i = q - t + pad;
@@ -424,10 +429,10 @@ extern "C" int adr_mlca_bwd(int dtype, const void* y, int ycs, const void* dout,
   const bool v = mlca_vec(dtype, C, {ycs, dcs, ocs}, {y, dout, dy});
   MLCA_DISPATCH(dtype, v, mlca_bwd_bins_kernel, dim3(LS * LS, N), (const TT*)y, ycs, (const TT*)dout, dcs, H, W, C,
                 datt);
-  size_t sm = (2 * C + LS * LS * C + 512) * sizeof(float);
+  size_t sm = (2 * C + LS * LS * C + 2 * MLCA_NT) * sizeof(float);
   ADR_REQUIRE(sm <= 160 * 1024, "mlca_bwd: C=%d too large for the per-image LDS plan", C);
   hipLaunchKernelGGL(mlca_gsum_kernel, dim3(LS), dim3(256), 0, st, datt, N, C, S);
-  hipLaunchKernelGGL(mlca_att_bwd_kernel, dim3(N), dim3(256), sm, st, local, datt, sig_l, sig_g, S, N, C, wl, wg, k,
+  hipLaunchKernelGGL(mlca_att_bwd_kernel, dim3(N), dim3(MLCA_NT), sm, st, local, datt, sig_l, sig_g, S, N, C, wl, wg, k,
                      local_weight, dlocal, dwl_part, dwg_part);
   MLCA_DISPATCH(dtype, v, mlca_bwd_y_kernel, mlca_grid((long)N * H * W, dtype, v, C), (const TT*)dout, dcs, att,
                 dlocal, (TT*)dy, ocs, N, H, W, C);
